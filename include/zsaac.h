@@ -1,0 +1,198 @@
+/*
+ * zsaac.h — C-ABI of libzsaac_hip.so, the MI355X (gfx950) kernels behind the zero-shot audio
+ * captioning hot path of XinMing0411/zero-shot-AAC.
+ *
+ * Conventions:
+ *   - every pointer is a DEVICE pointer owned by the caller (PyTorch caching allocator); the
+ *     library never allocates or frees caller memory;
+ *   - shapes/strides are explicit ints, element strides (not bytes);
+ *   - `dtype` selects the storage/compute type of weights and GEMM operands:
+ *       ZS_F32  = parity mode (f32 operands, exact-f32 MFMA 32x32x2f32, f32 accumulate)
+ *       ZS_BF16 = perf mode   (bf16 operands, MFMA 32x32x16 bf16, f32 accumulate)
+ *     residual streams, softmax, LayerNorm statistics and all reductions are f32 in both modes;
+ *   - `stream` is a hipStream_t (pass torch.cuda.current_stream().cuda_stream); every launch is
+ *     stream-ordered, allocation-free and sync-free, so a caller may capture it into a hipGraph;
+ *   - return 0 on success or a negative zs_status; zs_last_error() gives a thread-local message.
+ *
+ * Each entry point names the reference code it replaces (paths under the reference repo root).
+ */
+#ifndef ZSAAC_H
+#define ZSAAC_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum zs_status { ZS_OK = 0, ZS_ERR_ARG = -1, ZS_ERR_DTYPE = -2, ZS_ERR_HIP = -3, ZS_ERR_UNSUPPORTED = -4 };
+enum zs_dtype { ZS_F32 = 0, ZS_BF16 = 1 };
+enum zs_act { ZS_ACT_NONE = 0, ZS_ACT_GELU_ERF = 1, ZS_ACT_GELU_TANH = 2, ZS_ACT_RELU = 3, ZS_ACT_TANH = 4 };
+
+/* ------------------------------------------------------------------ runtime */
+int zs_version(void);                         /* ABI version, bumped on signature change */
+int zs_last_error(char* buf, size_t len);     /* copies the thread-local last error message */
+int zs_device_arch(char* buf, size_t len);    /* gcnArchName of the current device (e.g. gfx950) */
+
+/* ------------------------------------------------------------------ audio front end
+ * zs_logmel: retrieval/models/feature_extractor.py:34-38 (torchlibrosa Spectrogram +
+ * LogmelFilterBank, n_fft 1024, hop 320, hann, center/reflect, power 2, 64 Slaney mels,
+ * 10*log10(max(x,1e-10))) fused with bn0 (htsat.py:949-951 / cnns.py:176-178):
+ *   wav [B][T] f32 -> out [B][n_frames][64] f32, n_frames = T/hop + 1.
+ * window[1024], twiddle[1024] = (cos, sin)(-2*pi*k/1024) interleaved for k < 512 (the DFT is a
+ * radix-2 FFT in LDS: 1 block per frame), melW[64][513] (librosa.filters.mel, row m nonzero on
+ * [mel_lo[m], mel_hi[m])), bn_{mean,var,weight,bias}[64] (eval BatchNorm, eps 1e-5; pass NULL
+ * bn_mean to skip bn0). */
+int zs_logmel(const float* wav, int B, int T, const float* window, const float* twiddle,
+              const float* melW,
+              const int* mel_lo, const int* mel_hi, const float* bn_mean, const float* bn_var,
+              const float* bn_weight, const float* bn_bias, float* out, void* stream);
+
+/* zs_wav2img: htsat.py:908-923 reshape_wav2img — bicubic (A=-0.75, align_corners=True) resize of
+ * the time axis T_in -> 1024 and fold (B,1,1024,64) -> (B,256,256).  in [B][T_in][64] f32. */
+int zs_wav2img(const float* in, int B, int T_in, float* img, void* stream);
+
+/* zs_patch_embed: htsat.py:115-125 PatchEmbed (Conv2d 1->96, k4 s4) + LayerNorm(96):
+ * img [B][256][256] f32 -> x [B*4096][96] f32 (token = row*64 + col of the 64x64 patch grid). */
+int zs_patch_embed(const float* img, int B, const float* w /*[96][16]*/, const float* b,
+                   const float* ln_w, const float* ln_b, float* x, void* stream);
+
+/* ------------------------------------------------------------------ generic building blocks
+ * zs_layernorm: y[m] = LN(x[rows ? rows[m] : m]) * w + b over C (eps), x f32, y in `ydtype`
+ * (ZS_F32/ZS_BF16).  `rows` (int32, may be NULL) gathers rows, e.g. GPT-2 ln_f on the last
+ * prompt position of every ragged row. */
+int zs_layernorm(const float* x, int M, int C, int ldx, const int* rows, const float* w,
+                 const float* b, float eps, void* y, int ldy, int ydtype, void* stream);
+
+/* zs_gemm: out[m][n] = act(sum_k A[m][k] * W[n][k] + bias[n]) + residual[m][n]
+ *   A [M][lda], W [N][ldw] in `dtype`; bias f32 or NULL; residual f32 [M][ldr] or NULL (may alias
+ *   out); out in `out_dtype`.  K % 32 == 0.  split_k > 1 needs a f32 workspace of
+ *   split_k*M*N floats (deterministic slab reduction, no atomics).
+ *   Replaces every nn.Linear / HF Conv1D on the path (Conv1D weights are repacked to [N][K]). */
+int zs_gemm(int M, int N, int K, int dtype, const void* A, int lda, const void* W, int ldw,
+            const float* bias, const float* residual, int ldr, void* out, int ldo, int out_dtype,
+            int act, int split_k, float* workspace, void* stream);
+
+/* zs_l2norm_rows: y = x / max(||x||_2, eps) per row (F.normalize, ase_model.py:54). in-place ok */
+int zs_l2norm_rows(const float* x, int M, int C, float eps, float* y, void* stream);
+
+/* ------------------------------------------------------------------ HTSAT
+ * zs_window_attention: htsat.py:312-347 W-MSA/SW-MSA for one SwinTransformerBlock, with the
+ * cyclic roll (htsat.py:443-463), window partition/reverse and the -100 shift mask (406-425)
+ * folded into the indexing.  qkv [B*H*W][3C] (dtype) in natural token order; out [B*H*W][C]
+ * (dtype) in natural token order.  head_dim = C/heads (24 in HTSAT), ws*ws == 64.
+ * rel_table [(2ws-1)^2][heads] f32. */
+int zs_window_attention(const void* qkv, int B, int H, int W, int C, int heads, int ws, int shift,
+                        const float* rel_table, void* out, int dtype, void* stream);
+
+/* zs_patch_merge_ln: htsat.py:492-511 gather x0..x3 of each 2x2 patch + LayerNorm(4C):
+ * x [B][H][W][C] f32 -> y [B*(H/2)*(W/2)][4C] (dtype); the reduction Linear is a zs_gemm. */
+int zs_patch_merge_ln(const float* x, int B, int H, int W, int C, const float* ln_w,
+                      const float* ln_b, void* y, int dtype, void* stream);
+
+/* zs_ln_meanpool: htsat.py:830,838-847 final LayerNorm + mean over the N tokens -> [B][C] f32. */
+int zs_ln_meanpool(const float* x, int B, int N, int C, const float* ln_w, const float* ln_b,
+                   float* out, void* stream);
+
+/* ------------------------------------------------------------------ CNN14 (cnns.py:36-78,171-201)
+ * zs_conv3x3_bn_relu: NHWC implicit-GEMM conv3x3 pad 1 (no bias) + eval BN + ReLU.
+ *   x [B][H][W][Cin] (dtype), w [Cout][3][3][Cin] (dtype), bn folded as scale/shift f32 [Cout]
+ *   (y = relu(conv*scale + shift)), out [B][H][W][Cout] (dtype). */
+int zs_conv3x3_bn_relu(const void* x, int B, int H, int W, int Cin, const void* w, int Cout,
+                       const float* scale, const float* shift, void* out, int dtype, void* stream);
+/* zs_avgpool2: 2x2 average pool (floor) NHWC, dtype in/out. */
+int zs_avgpool2(const void* x, int B, int H, int W, int C, void* out, int dtype, void* stream);
+/* zs_cnn_head: mean over freq (W) then max + mean over time (H): x [B][H][W][C] -> [B][C] f32. */
+int zs_cnn_head(const void* x, int B, int H, int W, int C, float* out, int dtype, void* stream);
+/* zs_cast: f32 -> dtype element copy (e.g. the bn0'd log-mel as the NHWC C=1 CNN14 input). */
+int zs_cast(const float* x, long n, void* y, int dtype, void* stream);
+
+/* ------------------------------------------------------------------ prompt
+ * zs_prompt_assemble: dataset/dataset.py:441-453 + utils.py:131-188 on device —
+ * sim = emb[b] . labels^T (softmax is monotonic: top-k on sim, ties -> lower index), then
+ * ids = head + (label ids + ',')* + tail ("There are l1, l2 in this audio.").
+ * label_tok [L][max_tok] int32 with label_len[L]; out hard_ids [B][h_cap] int32 (0-padded,
+ * padding_captions utils.py:190-208), hard_len [B], chosen [B][k] int32 (may be NULL). */
+int zs_prompt_assemble(const float* emb, int B, int D, const float* labels, int L, int k,
+                       const int* label_tok, const int* label_len, int max_tok, int* hard_ids,
+                       int h_cap, int* hard_len, int* chosen, void* stream);
+
+/* ------------------------------------------------------------------ mapper / small attention
+ * zs_row_attention: per row b, per head h: softmax(scale * q_i . k_j) v_j over j < len[b]
+ * (causal: j <= i).  q element (b, i, h, d) at q[(b*L + i)*ldq + h*hd + d], k/v likewise with
+ * ldkv, out with ldo (all dtype).  Serves models/mapper.py:49-66 (non-causal, hd 96) and the GPT-2
+ * prompt prefill (causal, hd 64).  L <= 128, hd <= 128. */
+int zs_row_attention(const void* q, int ldq, const void* k, const void* v, int ldkv, int B, int L,
+                     const int* len, int heads, int hd, int causal, float scale, void* out, int ldo,
+                     int dtype, void* stream);
+
+/* ------------------------------------------------------------------ GPT-2 decode
+ * zs_gpt2_prefill_embed: clap_to_gpt (caption_model.py:315-329) + the caller's wte lookup
+ * (predict_prompt.py:133) + GPT-2 input embedding:  row b, position p < P_b = hard_len[b]+n_soft:
+ *   e = p < H_b ? wte[hard_ids[b][p]] : soft[b][p-H_b]   (prefix_embed, written to `embed`)
+ *   x = e + wpe[p]                                         (transformer input, written to `x`)
+ * rows padded to Pmax with zeros.  plen[b] = P_b, last_row[b] = b*Pmax + P_b - 1.  wte/wpe in
+ * dtype, soft f32 with clip b's n_soft*D prefix at soft + b*soft_ld. */
+int zs_gpt2_prefill_embed(const int* hard_ids, const int* hard_len, int h_cap, const float* soft,
+                          int soft_ld, int n_soft, const void* wte, const void* wpe, int B,
+                          int Pmax, int D, float* embed, float* x, int* plen, int* last_row,
+                          int dtype, void* stream);
+
+/* zs_kv_write: copy k,v of `n` tokens per row from qkv [R*n][3D] into the cache
+ * kc/vc [rows][heads][Lmax][hd] at cache row r*row_stride, positions pos0[r] + i (pos0 NULL -> 0).
+ * row_stride = beam puts a clip's beam-search prompt in its first beam row. */
+int zs_kv_write(const void* qkv, int R, int n, int D, int heads, const int* pos0, int row_stride,
+                void* kc, void* vc, int Lmax, int dtype, void* stream);
+
+/* zs_decode_attention: one new token per row r at position pos[r]: append its k,v (from
+ * qkv[r]) to the cache, attend over positions 0..pos[r] (kv row for position j of row r is
+ * kvrow[r*Lmax + j] when kvrow != NULL, else r — the beam-search history indirection),
+ * scale 1/sqrt(hd), f32 softmax.  out [R][D] (dtype).  HF GPT2Attention eager semantics. */
+int zs_decode_attention(const void* qkv, int R, int D, int heads, void* kc, void* vc, int Lmax,
+                        const int* pos, const int* kvrow, void* out, int dtype, void* stream);
+
+/* zs_embed_tokens: x[r] = wte[tok[r]] + wpe[pos[r]] (f32 out), optional row gather. */
+int zs_embed_tokens(const int* tok, const int* pos, const void* wte, const void* wpe, int R, int D,
+                    float* x, int dtype, void* stream);
+
+/* zs_lmhead_topk: per row m of A [M][K] (dtype) against W [V][K] (dtype; tied wte):
+ *   logits = A W^T, split in column blocks of 128; per (row, block) writes the block's max,
+ *   sum(exp(logit - max)) and its top-`topk` (value, index) (ties -> lower index).
+ *   part_stat [M][nblk][2] f32, part_val [M][nblk][topk] f32, part_idx [M][nblk][topk] int32,
+ *   nblk = ceil(V/128).  topk <= 8.  With row_norm != 0 each A row is L2-normalised first
+ *   (get_prefix_tokens, gpt2_prefix_eval.py:271-278: W must then be normalize(wte)). */
+int zs_lmhead_topk(int M, int K, int V, int dtype, const void* A, int lda, const void* W,
+                   int topk, int row_norm, float* part_stat, float* part_val, int* part_idx,
+                   void* stream);
+int zs_lmhead_nblk(int V);
+
+/* zs_argmax_finalize: merge zs_lmhead_topk partials (topk 1) into idx[M] (lower index on ties). */
+int zs_argmax_finalize(const float* part_val, const int* part_idx, int M, int nblk, int* idx,
+                       void* stream);
+
+/* zs_greedy_step: generate2's per-step bookkeeping (gpt2_prefix_eval.py:208-215) for R rows:
+ * tok = argmax(partials); rows already done keep emitting nothing; out_ids[r][step] = tok,
+ * out_len[r] = step+1 while not done; done |= tok in {stop0, stop1}; pos[r] += 1 (next position);
+ * next_tok[r] = tok.  `step` is read from *step_ctr (device) and *step_ctr += 1 by the last
+ * block, so a captured graph replays without host arguments.  all_done[0] = AND(done). */
+int zs_greedy_step(const float* part_val, const int* part_idx, int R, int nblk, int* step_ctr,
+                   int max_steps, int stop0, int stop1, int* out_ids, int* out_len, int* done,
+                   int* pos, int* next_tok, int* all_done, void* stream);
+
+/* zs_beam_step: generate_beam's per-step update (gpt2_prefix_eval.py:119-151) for C clips x
+ * `beam` rows, from zs_lmhead_topk partials (topk >= beam) with log(softmax) semantics.
+ * first != 0: step 0 (row c*beam of each clip is the only live source).  Updates scores,
+ * seq_len, stopped, the token history tokens [R][max_steps], the kv-row indirection table
+ * kvrow [R][Lmax] (history of the chosen source row + this step's own slot), pos[R],
+ * next_tok[R]; all_done[0] = every row stopped. */
+int zs_beam_step(const float* part_stat, const float* part_val, const int* part_idx, int C,
+                 int beam, int nblk, int topk, int first, int stop, int* step_ctr, int max_steps,
+                 float* scores, float* seq_len, int* stopped, int* tokens, int* tokens_tmp,
+                 int* kvrow, int* kvrow_tmp, int Lmax, int* pos, int* next_tok, int* all_done,
+                 void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ZSAAC_H */

@@ -1,0 +1,109 @@
+"""Import shims that let THIS container import the read-only reference for golden generation only.
+
+Used solely by tests/golden/make_goldens.py (never by tests at run time, never on the GPU box:
+/root/reference does not exist there).  What is shimmed and why:
+
+* ``transformers.AdamW`` was removed in transformers 5.x; gpt2_prefix_eval.py:2 and
+  dataset/dataset.py:11 import it -> wrapped module adds ``AdamW = torch.optim.AdamW``.
+* ``train`` (gpt2_prefix_eval.py:7) names a module absent from the reference -> stub.
+* ``GPT2LMHeadModel.from_pretrained('gpt2')`` (models/caption_model.py:52) is a name fetch that is
+  unavailable offline -> returns a locally built ``GPT2LMHeadModel(GPT2Config())`` with eager
+  attention, into which the caller loads the seeded synthetic state dict.
+* torchlibrosa (front end), ruamel.yaml, wandb, loguru, sentence_transformers, librosa are absent
+  -> stubs.  The torchlibrosa stub is an IDENTITY module, so the reference HTSAT/CNN14 forward is
+  driven from a log-mel input; the front end itself is third-party arithmetic that stays
+  "parity unpinned" (DESIGN.md §Oracle).
+"""
+from __future__ import annotations
+
+import sys
+import types
+
+import torch
+import torch.nn as nn
+
+REF = "/root/reference"
+
+
+class _Any:
+    def __init__(self, *a, **k):
+        pass
+
+    def __call__(self, *a, **k):
+        return self
+
+    def __getattr__(self, name):
+        return _Any()
+
+
+def _stub(name, **attrs):
+    m = types.ModuleType(name)
+
+    def __getattr__(attr):  # noqa: N807
+        return _Any
+    m.__getattr__ = __getattr__
+    for k, v in attrs.items():
+        setattr(m, k, v)
+    sys.modules[name] = m
+    return m
+
+
+class _Identity(nn.Module):
+    def __init__(self, *a, **k):
+        super().__init__()
+
+    def forward(self, x):
+        return x
+
+
+_installed = False
+
+
+def install():
+    global _installed
+    if _installed:
+        return
+    import transformers  # import the real package BEFORE stubbing librosa
+    from transformers import GPT2Config, GPT2LMHeadModel
+
+    def _from_pretrained(*a, **k):
+        cfg = GPT2Config()
+        cfg._attn_implementation = "eager"
+        m = GPT2LMHeadModel(cfg)
+        return m
+    GPT2LMHeadModel.from_pretrained = staticmethod(_from_pretrained)
+
+    _stub("train", ClipCocoDataset=type("ClipCocoDataset", (), {}),
+          ClipCaptionModel=type("ClipCaptionModel", (nn.Module,), {}))
+    tl = _stub("torchlibrosa", Spectrogram=_Identity, LogmelFilterBank=_Identity)
+    _stub("torchlibrosa.augmentation", SpecAugmentation=_Identity)
+    tl.augmentation = sys.modules["torchlibrosa.augmentation"]
+    import yaml as _yaml
+    ry = _stub("ruamel")
+    ry.yaml = _yaml
+    sys.modules["ruamel.yaml"] = _yaml
+    for name in ("wandb", "loguru", "sentence_transformers", "librosa", "stanza", "peft",
+                 "bitsandbytes", "deepl", "openai"):
+        if name not in sys.modules:
+            _stub(name)
+    sys.modules["loguru"].logger = _Any()
+    sys.modules["sentence_transformers"].util = _Any()
+    if REF not in sys.path:
+        sys.path.insert(0, REF)
+    # lazy module: set the missing names directly on it (``from transformers import AdamW``);
+    # done last because resolving other lazy attributes can rebuild the module's namespace
+    transformers = sys.modules["transformers"]
+    transformers.__dict__["AdamW"] = torch.optim.AdamW
+    transformers.__dict__.setdefault("get_linear_schedule_with_warmup", lambda *a, **k: None)
+    _installed = True
+
+
+def gpt2_from_state_dict(sd_gpt):
+    """A reference-config GPT2LMHeadModel (eager attention) holding ``sd_gpt`` (no 'gpt.' prefix)."""
+    install()
+    from transformers import GPT2LMHeadModel  # noqa
+    m = GPT2LMHeadModel.from_pretrained("gpt2")
+    missing, unexpected = m.load_state_dict(sd_gpt, strict=False)
+    assert not unexpected, unexpected
+    assert all("attn.bias" in k or "masked_bias" in k for k in missing), missing
+    return m.eval()

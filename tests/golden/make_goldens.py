@@ -1,0 +1,261 @@
+"""Generate the golden fixtures of tests/golden/*.npz by RUNNING THE REFERENCE (read-only, imported
+from /root/reference through tests/golden/_refshim.py) on seeded synthetic weights and inputs.
+
+The reference has no tests, fixtures or golden vectors of its own, so these
+fixtures are the pin for oracle/ and for the HIP path.  Only arrays are written; no reference
+source travels.  Weights come from zsaac.synthetic (seeded, regenerated identically by the tests),
+so the fixtures hold inputs + outputs only.
+
+    python tests/golden/make_goldens.py            # all fixtures (several minutes on 8 cores)
+    python tests/golden/make_goldens.py htsat cnn14  # a subset
+
+Fixture list (reference call sites in brackets):
+  c1_greedy.npz   C1 harness: 50 CLAP embeddings -> ClapTestDataset_withHardPrompt.__getitem__ +
+                  collate (dataset/dataset.py:441-453,632-647) -> clap_to_gpt
+                  (models/caption_model.py:315-329) -> get_prefix_tokens + generate2
+                  (gpt2_prefix_eval.py:161-222,271-278), as predict_prompt.py:129-148 drives them.
+  beam.npz        generate_beam beam 5 and beam 3 (gpt2_prefix_eval.py:99-158).
+  mappers.npz     MLP and TransformerMapper forward + clap_to_gpt (models/mapper.py, caption_model.py).
+  htsat.npz       HTSAT forward from log-mel (retrieval/models/htsat.py:941-958) + ASE
+                  audio_proj/normalize (ase_model.py:52-55).
+  cnn14.npz       CNN14 forward from log-mel (cnns.py:171-201) + audio_proj/normalize.
+  prompt.npz      compose_discrete_prompts strings + padding_captions (utils.py:158-208).
+"""
+from __future__ import annotations
+
+import os
+import pickle
+import sys
+import tempfile
+import time
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, HERE)
+sys.path.insert(0, os.path.join(REPO, "zero-shot-aac_amd"))
+
+import _refshim  # noqa: E402
+
+_refshim.install()  # puts /root/reference first on sys.path
+
+from zsaac import synthetic as S  # noqa: E402
+from zsaac.tokenizer import IdTokenizer, TableTokenizer, synthetic_label_names  # noqa: E402
+
+# the golden decoder weights (scaled-up init for non-degenerate argmax margins;
+# stop_boost makes '.'/' .' fire within 67 steps for part of the clips)
+GPT2_KW = dict(seed=0, std=0.1, emb_std=0.1, stop_boost=2.0)
+SOUND_EFFECT_NUM = 3
+
+
+def _save(name, **arrays):
+    path = os.path.join(HERE, name)
+    np.savez_compressed(path, **arrays)
+    print(f"wrote {path} ({os.path.getsize(path) / 1e3:.1f} kB)", flush=True)
+
+
+def _pad(rows, fill=-1):
+    n = max([len(r) for r in rows] + [1])
+    out = np.full((len(rows), n), fill, dtype=np.int64)
+    for i, r in enumerate(rows):
+        out[i, :len(r)] = r
+    return out, np.array([len(r) for r in rows], dtype=np.int64)
+
+
+def _caption_model(mapping_type="mlp"):
+    from models.caption_model import ClapCaption_prompt
+    sd = S.gpt2_state_dict(**GPT2_KW)
+    if mapping_type == "mlp":
+        sd.update(S.mlp_mapper_state_dict(1))
+    else:
+        sd.update(S.transformer_mapper_state_dict(2))
+    m = ClapCaption_prompt(10, clip_length=10, prefix_size=1024, num_layers=8,
+                           mapping_type=mapping_type, only_prefix=False, only_soft_prompt=False)
+    missing, unexpected = m.load_state_dict(sd, strict=False)
+    assert not unexpected, unexpected
+    assert all("attn.bias" in k or "masked_bias" in k for k in missing), missing
+    return m.eval()
+
+
+class _PrefixTok(IdTokenizer):
+    """decode(token) -> 'id|' so get_prefix_tokens' "".join stays parseable."""
+
+    def decode(self, ids):
+        return super().decode(ids) + "|"
+
+
+def gen_c1(n_clips=50, entry_length=67):
+    import transformers
+    import gpt2_prefix_eval as G
+    names = synthetic_label_names()
+    label_ids = S.label_token_table()
+    tok = TableTokenizer.for_labels(names, label_ids)
+    transformers.GPT2Tokenizer.from_pretrained = staticmethod(lambda *a, **k: tok)
+    from dataset.dataset import ClapTestDataset_withHardPrompt, collate
+    table = S.label_table()
+    emb = S.synthetic_clap_embeddings(n_clips)
+    tmp = tempfile.mkdtemp()
+    data_p, lab_p = os.path.join(tmp, "data.pkl"), os.path.join(tmp, "labels.pkl")
+    with open(data_p, "wb") as f:
+        pickle.dump([{"audio_embedding": emb[i:i + 1].clone(), "audio_id": f"clip{i:04d}",
+                      "caption": ["x"]} for i in range(n_clips)], f)
+    with open(lab_p, "wb") as f:
+        pickle.dump([{"label_id": i, "label": names[i], "label_embedding": table[i:i + 1].clone()}
+                     for i in range(len(names))], f)
+    ds = ClapTestDataset_withHardPrompt(data_p, normalize_prefix=True, sound_effect_path=lab_p,
+                                        sound_effect_num=SOUND_EFFECT_NUM)
+    model = _caption_model("mlp")
+    embeddings = torch.nn.functional.normalize(model.gpt.get_input_embeddings().weight.data, 2, 1)
+    hard_rows, greedy_rows, pref_rows, pe_keep = [], [], [], []
+    t0 = time.time()
+    for i in range(n_clips):
+        audio_id, prefix, hard, mask = collate([ds[i]])
+        prefix = prefix.to(dtype=torch.float32)
+        with torch.no_grad():
+            emb_h = model.gpt.transformer.wte(hard)
+            pe, _ = model.clap_to_gpt(prefix, emb_h)
+            ps = G.get_prefix_tokens(pe, embeddings, _PrefixTok())
+            out = G.generate2(model, IdTokenizer(), embed=pe, entry_length=entry_length)
+        hard_rows.append(hard[0].tolist())
+        pref_rows.append([int(t) for t in ps[0].split("|") if t])
+        greedy_rows.append([int(t) for t in out.split()])
+        if i < 4:
+            pe_keep.append(pe[0].numpy())
+        if i % 10 == 0:
+            print(f"  c1 clip {i}: H={hard.shape[1]} gen={len(greedy_rows[-1])} "
+                  f"({time.time() - t0:.0f}s)", flush=True)
+    hard, hard_len = _pad(hard_rows)
+    greedy, greedy_len = _pad(greedy_rows)
+    pref, _ = _pad(pref_rows)
+    pe_pad = np.zeros((len(pe_keep), max(p.shape[0] for p in pe_keep), 768), np.float32)
+    for i, p in enumerate(pe_keep):
+        pe_pad[i, :p.shape[0]] = p
+    _save("c1_greedy.npz", clap_emb=emb.numpy(), hard_ids=hard, hard_len=hard_len,
+          greedy_ids=greedy, greedy_len=greedy_len, prefix_tokens=pref,
+          prefix_embed=pe_pad, entry_length=np.int64(entry_length),
+          sound_effect_num=np.int64(SOUND_EFFECT_NUM), normalize_prefix=np.int64(1))
+
+
+def gen_beam(n_clips=4, entry_length=67):
+    import gpt2_prefix_eval as G
+    model = _caption_model("mlp")
+    emb = S.synthetic_clap_embeddings(n_clips, seed=99)
+    label_ids = S.label_token_table()
+    out = {}
+    hard_rows = []
+    for i in range(n_clips):
+        # fixed hard prompt: "There are <label i>, <label 2i+1> in this audio."
+        hard_rows.append([1858, 389] + label_ids[i] + [11] + label_ids[2 * i + 1] + [287, 428, 6597, 13])
+    hard, hard_len = _pad(hard_rows)
+    for beam in (5, 3):
+        rows = []
+        for i in range(n_clips):
+            h = torch.tensor([hard_rows[i]])
+            with torch.no_grad():
+                pe, _ = model.clap_to_gpt(emb[i:i + 1].unsqueeze(0), model.gpt.transformer.wte(h))
+                texts = G.generate_beam(model, IdTokenizer(), beam_size=beam, embed=pe,
+                                        entry_length=entry_length)
+            rows.append([[int(t) for t in s.split()] for s in texts])
+            print(f"  beam{beam} clip {i}: lens {[len(r) for r in rows[-1]]}", flush=True)
+        flat = [r for clip in rows for r in clip]
+        ids, lens = _pad(flat)
+        out[f"beam{beam}_ids"] = ids.reshape(n_clips, beam, -1)
+        out[f"beam{beam}_len"] = lens.reshape(n_clips, beam)
+    _save("beam.npz", clap_emb=emb.numpy(), hard_ids=hard, hard_len=hard_len,
+          entry_length=np.int64(entry_length), **out)
+
+
+def gen_mappers():
+    from models.mapper import MLP, TransformerMapper
+    x = S.synthetic_clap_embeddings(3, seed=11).unsqueeze(1)  # [3,1,1024] as in make_preds
+    mlp = MLP((1024, 3840, 7680))
+    mlp.load_state_dict({k.replace("clap_project.", ""): v for k, v in S.mlp_mapper_state_dict(1).items()})
+    tm = TransformerMapper(1024, 768, 10, 10, 8)
+    tm.load_state_dict({k.replace("clap_project.", ""): v
+                        for k, v in S.transformer_mapper_state_dict(2).items()})
+    with torch.no_grad():
+        y_mlp = mlp.eval()(x)
+        y_tm = tm.eval()(x)
+        model = _caption_model("transformer")
+        h = torch.tensor([[1858, 389, 1223, 287, 428, 6597, 13]])
+        pe_tm, _ = model.clap_to_gpt(x[:1], model.gpt.transformer.wte(h))
+    _save("mappers.npz", x=x.numpy(), mlp_out=y_mlp.numpy(), tmapper_out=y_tm.numpy(),
+          tm_hard_ids=h.numpy(), tm_prefix_embed=pe_tm[0].numpy())
+
+
+def _audio_config(kind):
+    return {"audio_args": {"sr": 32000, "n_fft": 1024, "hop_length": 320, "f_min": 50,
+                           "f_max": 14000, "n_mels": 64, "max_length": 10, "mono": True},
+            "audio_encoder_args": {"type": kind, "model": "Cnn14", "pretrained": False,
+                                   "freeze": False},
+            "training": {"spec_augmentation": True, "dropout": 0.2}}
+
+
+def _logmel_input(n, seed):
+    g = torch.Generator().manual_seed(seed)
+    # log-mel-like magnitudes (dB), [B,1,T=1001,F=64]: what AudioFeature hands to bn0
+    return torch.randn(n, 1, 1001, 64, generator=g) * 8.0 - 20.0
+
+
+def _encode(kind, audio_sd, width):
+    from retrieval.models.audio_encoder import AudioEncoder
+    enc = AudioEncoder(_audio_config(kind))
+    missing, unexpected = enc.load_state_dict(
+        {k.replace("audio_encoder.", ""): v for k, v in audio_sd.items()}, strict=False)
+    assert not unexpected, unexpected
+    proj = torch.nn.Sequential(torch.nn.Linear(width, 1024), torch.nn.ReLU(), torch.nn.Linear(1024, 1024))
+    proj.load_state_dict({k.replace("audio_proj.", ""): v
+                          for k, v in S.audio_proj_state_dict(5, audio_width=width).items()})
+    return enc.eval(), proj.eval(), missing
+
+
+def gen_htsat():
+    enc, proj, missing = _encode("transformer", S.htsat_state_dict(3), 768)
+    assert all(("relative_position_index" in k) or ("attn_mask" in k) for k in missing), missing
+    x = _logmel_input(2, 21)
+    with torch.no_grad():
+        feat = enc(x)
+        emb = torch.nn.functional.normalize(proj(feat), dim=-1)  # ASE.encode_audio, ase_model.py:52-55
+    _save("htsat.npz", logmel=x.numpy(), embedding768=feat.numpy(), clap_emb=emb.numpy())
+
+
+def gen_cnn14():
+    enc, proj, missing = _encode("cnn", S.cnn14_state_dict(4), 2048)
+    assert not missing, missing
+    x = _logmel_input(2, 22)
+    with torch.no_grad():
+        feat = enc(x)
+        emb = torch.nn.functional.normalize(proj(feat), dim=-1)
+    _save("cnn14.npz", logmel=x.numpy(), embedding2048=feat.numpy(), clap_emb=emb.numpy())
+
+
+def gen_prompt():
+    import utils as U
+
+    class CharTok:
+        def encode(self, s):
+            return [ord(c) for c in s]
+    names = synthetic_label_names()
+    sets = [[], [names[0]], [names[5], names[77]], [names[1], names[2], names[3], names[526]]]
+    strings = ["".join(chr(c) for c in U.parse_entities(CharTok(), s, 0).tolist()) for s in sets]
+    hp = [torch.tensor([5, 6, 7]), torch.tensor([1]), torch.tensor([9, 8, 7, 6, 5])]
+    padded, mask = U.padding_captions(hp, [3, 1, 5])
+    enc = np.array([s.encode() for s in strings], dtype=object)
+    _save("prompt.npz", strings=np.array(strings), n_labels=np.array([len(s) for s in sets]),
+          pad_ids=padded.numpy(), pad_mask=mask.numpy())
+    del enc
+
+
+ALL = {"prompt": gen_prompt, "mappers": gen_mappers, "htsat": gen_htsat, "cnn14": gen_cnn14,
+       "beam": gen_beam, "c1": gen_c1}
+
+if __name__ == "__main__":
+    torch.set_num_threads(os.cpu_count() or 8)
+    torch.manual_seed(0)
+    for name in (sys.argv[1:] or list(ALL)):
+        t = time.time()
+        print(f"[{name}]", flush=True)
+        ALL[name]()
+        print(f"[{name}] done in {time.time() - t:.1f}s", flush=True)

@@ -1,0 +1,172 @@
+"""End-to-end parity of the HIP path against the reference goldens (tests/golden/*.npz, produced
+by running the reference) and the oracle.
+
+Tolerances (stated per north_star):
+  * greedy token ids: BIT-EXACT in f32 parity mode (C1 fixture: 50 clips, 67 steps, with stops);
+  * beam token lists and order: exact in f32 mode;
+  * encoder embeddings: f32 mode max |err| <= 2e-4 * max|ref| (HTSAT) / 5e-4 (CNN14 deep convs);
+    bf16 mode cosine(ref, got) >= 0.995;
+  * mapper outputs: f32 1e-4 relative.
+bf16 greedy ids are reported (agreement fraction), not asserted bit-exact: bf16 moves logits by
+~1e-2, which exceeds the oracle's top-2 margin on some steps.
+"""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+GPT2_KW = dict(seed=0, std=0.1, emb_std=0.1, stop_boost=2.0)
+
+
+@pytest.fixture(scope="module")
+def caption_sd():
+    from zsaac import synthetic as S
+    sd = S.gpt2_state_dict(**GPT2_KW)
+    sd.update(S.mlp_mapper_state_dict(1))
+    sd.update(S.transformer_mapper_state_dict(2))
+    return sd
+
+
+def _pipeline(caption_sd, dtype, batch, beam=0, mapping="mlp", audio_sd=None, encoder="htsat",
+              entry_length=67):
+    from zsaac import synthetic as S
+    from zsaac.pipeline import CaptionConfig, CaptionPipeline
+    cfg = CaptionConfig(encoder=encoder, mapping_type=mapping, dtype=dtype, batch=batch, beam=beam,
+                        entry_length=entry_length)
+    return CaptionPipeline(caption_sd, audio_sd, S.label_table(), S.label_token_table(), cfg)
+
+
+def _rel(a, b):
+    a, b = np.asarray(a, np.float64), np.asarray(b, np.float64)
+    return float(np.abs(a - b).max() / (np.abs(b).max() + 1e-12))
+
+
+def test_c1_greedy_f32_bit_exact(cuda, golden, caption_sd):
+    g = golden("c1_greedy.npz")
+    pipe = _pipeline(caption_sd, torch.float32, 50)
+    out = pipe.caption_emb(torch.from_numpy(g["clap_emb"]).to(cuda))
+    # hard prompt assembled on device == the reference dataset's __getitem__ + collate
+    hl = out.hard_len.cpu().numpy()
+    assert hl.tolist() == g["hard_len"].tolist()
+    hi = out.hard_ids.cpu().numpy()
+    for b in range(50):
+        assert hi[b, :hl[b]].tolist() == g["hard_ids"][b, :hl[b]].tolist()
+    # prefix embeddings (clap_to_gpt) for the stored clips
+    pe = pipe.embed.view(50, pipe.Pmax, 768).cpu().numpy()
+    for b in range(g["prefix_embed"].shape[0]):
+        n = hl[b] + 10
+        assert _rel(pe[b, :n], g["prefix_embed"][b, :n]) < 1e-5
+    # get_prefix_tokens ids
+    pt = out.prefix_token_lists()
+    for b in range(50):
+        assert pt[b] == g["prefix_tokens"][b, :len(pt[b])].tolist(), b
+    # generate2 ids, bit-exact
+    caps = out.captions()
+    mism = [b for b in range(50) if caps[b] != g["greedy_ids"][b, :g["greedy_len"][b]].tolist()]
+    assert not mism, f"greedy mismatch on clips {mism}"
+
+
+def test_c1_greedy_bf16_agreement(cuda, golden, caption_sd):
+    g = golden("c1_greedy.npz")
+    pipe = _pipeline(caption_sd, torch.bfloat16, 50)
+    caps = pipe.caption_emb(torch.from_numpy(g["clap_emb"]).to(cuda)).captions()
+    agree, total = 0, 0
+    for b in range(50):
+        ref = g["greedy_ids"][b, :g["greedy_len"][b]].tolist()
+        n = 0
+        while n < min(len(ref), len(caps[b])) and ref[n] == caps[b][n]:
+            n += 1
+        agree += n
+        total += len(ref)
+    print(f"bf16 greedy: {agree}/{total} leading tokens agree ({agree / total:.3f})")
+    assert agree / total > 0.2   # sanity: bf16 decode tracks f32 for a good part of each caption
+
+
+@pytest.mark.parametrize("beam", [5, 3])
+def test_beam_f32(cuda, golden, caption_sd, beam):
+    g = golden("beam.npz")
+    C = g["clap_emb"].shape[0]
+    pipe = _pipeline(caption_sd, torch.float32, C, beam=beam)
+    # feed the fixture's fixed hard prompts: bypass prompt assembly
+    from zsaac import ops
+    dec = pipe.decoder
+    B, Pmax = C, pipe.Pmax
+    hard = torch.zeros(C, pipe.h_cap, dtype=torch.int32)
+    hard[:, :g["hard_ids"].shape[1]] = torch.from_numpy(np.maximum(g["hard_ids"], 0))
+    hard_len = torch.from_numpy(g["hard_len"]).int()
+    emb = torch.from_numpy(g["clap_emb"]).to(cuda)
+    soft = pipe.mapper(emb)
+    ops.prefill_embed(hard.to(cuda), hard_len.to(cuda), soft, pipe.mapper.soft_ld, 10,
+                      pipe.gpt.wte, pipe.gpt.wpe, B, Pmax, pipe.embed[:B * Pmax], dec.x, dec.plen,
+                      dec.last_row)
+    dec.prefill(B, Pmax, row_stride=beam)
+    ids, ln, sc = dec.beam(C, beam, Pmax)
+    from zsaac.pipeline import CaptionBatch
+    cb = CaptionBatch(ids, ln, sc, hard, hard_len, dec.plen[:B], None, emb)
+    got = cb.beams()
+    for c in range(C):
+        ref = [g[f"beam{beam}_ids"][c, i, :g[f"beam{beam}_len"][c, i]].tolist() for i in range(beam)]
+        assert got[c] == ref, c
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_mappers(cuda, golden, caption_sd, dtype):
+    from zsaac.decoder import MlpMapper, TransformerMapperEngine
+    g = golden("mappers.npz")
+    x = torch.from_numpy(g["x"][:, 0]).to(cuda)
+    m = MlpMapper(caption_sd, cuda, dtype, 3)
+    t = TransformerMapperEngine(caption_sd, cuda, dtype, 3)
+    ym = m(x).cpu().numpy().reshape(3, 1, -1)
+    yt = t(x).cpu().numpy().reshape(3, 10, 768)
+    tol = 1e-4 if dtype == torch.float32 else 3e-2
+    assert _rel(ym, g["mlp_out"]) < tol
+    assert _rel(yt, g["tmapper_out"]) < tol
+
+
+@pytest.mark.parametrize("kind,fixture,width", [("htsat", "htsat.npz", 768), ("cnn14", "cnn14.npz", 2048)])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_encoder_from_logmel(cuda, golden, kind, fixture, width, dtype):
+    from zsaac import synthetic as S
+    from zsaac.encoder import AudioEncoder
+    from oracle import audio as A
+    g = golden(fixture)
+    sd = S.htsat_state_dict(3) if kind == "htsat" else S.cnn14_state_dict(4)
+    sd.update(S.audio_proj_state_dict(5, audio_width=width))
+    enc = AudioEncoder(sd, kind, dtype, max_batch=2, device=cuda)
+    lm = torch.from_numpy(g["logmel"])               # [2,1,1001,64] (pre-bn0)
+    bn = A.bn0(lm, {k: v for k, v in sd.items()})[:, 0]   # bn0 is fused into zs_logmel normally
+    emb = enc.encode_logmel(bn.to(cuda)).cpu().numpy()
+    feat = enc.feat[:2].cpu().numpy()
+    key = "embedding768" if kind == "htsat" else "embedding2048"
+    if dtype == torch.float32:
+        assert _rel(feat, g[key]) < (2e-4 if kind == "htsat" else 5e-4)
+        assert _rel(emb, g["clap_emb"]) < 5e-4
+    else:
+        cos = (emb * g["clap_emb"]).sum(-1) / np.linalg.norm(emb, axis=-1) / np.linalg.norm(g["clap_emb"], axis=-1)
+        assert cos.min() > 0.995, cos
+
+
+def test_pipeline_from_wav_f32_vs_oracle(cuda, caption_sd):
+    """wav -> log-mel -> HTSAT -> proj -> prompt -> mapper -> greedy (f32) vs the oracle chain."""
+    from oracle import audio as A, caption as OC, frontend as OF
+    from zsaac import synthetic as S
+    asd = S.htsat_state_dict(3)
+    asd.update(S.audio_proj_state_dict(5))
+    pipe = _pipeline(caption_sd, torch.float32, 2, audio_sd=asd, entry_length=20)
+    wav = S.synthetic_waveforms(2)
+    out = pipe.caption_wav(wav.to(cuda))
+    with torch.no_grad():
+        lm = OF.logmel(wav)
+        emb = A.audio_project(A.htsat_embedding(lm, asd), asd)
+    assert _rel(out.clap_emb.cpu().numpy(), emb.numpy()) < 2e-3
+    table, lt = S.label_table(), S.label_token_table()
+    caps = out.captions()
+    for b in range(2):
+        idx = OC.sound_effect_choice(out.clap_emb[b:b + 1].cpu(), table, 3)[0].tolist()
+        hard = torch.tensor([OC.prompt_ids(idx, lt)])
+        assert out.hard_ids[b, :hard.shape[1]].cpu().tolist() == hard[0].tolist()
+        pe = OC.clap_to_gpt(torch.nn.functional.normalize(out.clap_emb[b:b + 1].cpu(), dim=-1)[None],
+                            hard, caption_sd)
+        ref = OC.generate2(pe, caption_sd, entry_length=20, use_cache=True)
+        assert caps[b] == ref

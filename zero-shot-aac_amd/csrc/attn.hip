@@ -1,0 +1,293 @@
+// Attention kernels:
+//  * window_attention  — HTSAT W-MSA / SW-MSA (htsat.py:312-347), roll + partition folded in;
+//  * row_attention     — dense per-row attention (TransformerMapper MHA, GPT-2 prompt prefill);
+//  * decode_attention  — one new token per row against the KV cache (GPT-2 decode), with an
+//                        optional per-position row indirection for beam search;
+//  * kv_write          — prefill K/V into the cache.
+// Softmax statistics are f32; one wave per query block.
+#include "common.h"
+
+namespace zs {
+
+// ------------------------------------------------------------------ HTSAT window attention
+// grid (B * nWh * nWw, heads), block 64: thread i = token i of the 8x8 window.
+template <typename T, int HD>
+__global__ __launch_bounds__(64) void window_attn_kernel(const T* __restrict__ qkv, int H, int W,
+                                                         int C, int heads, int shift,
+                                                         const float* __restrict__ table,
+                                                         T* __restrict__ out) {
+  constexpr int WS = 8, N = 64;
+  __shared__ float Ks[N][HD + 1];
+  __shared__ float Vs[N][HD + 1];
+  const int nWw = W / WS, nWh = H / WS;
+  const int win = blockIdx.x, head = blockIdx.y;
+  const int b = win / (nWh * nWw), wyx = win % (nWh * nWw), wy = wyx / nWw, wx = wyx % nWw;
+  const int i = threadIdx.x, iy = i / WS, ix = i % WS;
+  const int sy = wy * WS + iy, sx = wx * WS + ix;           // coords in the rolled image
+  const int hh = (sy + shift) % H, ww = (sx + shift) % W;   // natural coords (roll(-shift))
+  const long tok = ((long)b * H + hh) * W + ww;
+  const T* row = qkv + tok * 3 * C + head * HD;
+  const float scale = rsqrtf((float)HD);
+  float q[HD];
+#pragma unroll
+  for (int d = 0; d < HD; ++d) {
+    q[d] = ldf(row + d) * scale;
+    Ks[i][d] = ldf(row + C + d);
+    Vs[i][d] = ldf(row + 2 * C + d);
+  }
+  // shift-mask region label of this token (htsat.py:406-425 slices on rolled coords)
+  auto region = [&](int y, int x) {
+    const int ry = y < H - WS ? 0 : (y < H - shift ? 1 : 2);
+    const int rx = x < W - WS ? 0 : (x < W - shift ? 1 : 2);
+    return ry * 3 + rx;
+  };
+  const int my_reg = shift > 0 ? region(sy, sx) : 0;
+  __syncthreads();
+  float s[N];
+  float mx = -INFINITY;
+#pragma unroll
+  for (int j = 0; j < N; ++j) {
+    float acc = 0.f;
+#pragma unroll
+    for (int d = 0; d < HD; ++d) acc += q[d] * Ks[j][d];
+    const int jy = j / WS, jx = j % WS;
+    acc += table[((iy - jy + WS - 1) * (2 * WS - 1) + (ix - jx + WS - 1)) * heads + head];
+    if (shift > 0 && region(wy * WS + jy, wx * WS + jx) != my_reg) acc += -100.0f;
+    s[j] = acc;
+    mx = fmaxf(mx, acc);
+  }
+  float sum = 0.f;
+#pragma unroll
+  for (int j = 0; j < N; ++j) {
+    s[j] = expf(s[j] - mx);
+    sum += s[j];
+  }
+  const float inv = 1.0f / sum;
+  float o[HD];
+#pragma unroll
+  for (int d = 0; d < HD; ++d) o[d] = 0.f;
+#pragma unroll
+  for (int j = 0; j < N; ++j) {
+    const float p = s[j] * inv;
+#pragma unroll
+    for (int d = 0; d < HD; ++d) o[d] += p * Vs[j][d];
+  }
+  T* orow = out + tok * C + head * HD;
+#pragma unroll
+  for (int d = 0; d < HD; ++d) stf(orow + d, o[d]);
+}
+
+// ------------------------------------------------------------------ dense row attention
+// grid (B, heads, ceil(L/64)), block 64: thread = query i; K/V of the row staged in LDS.
+template <typename T, int HD>
+__global__ __launch_bounds__(64) void row_attn_kernel(const T* __restrict__ q, int ldq,
+                                                      const T* __restrict__ k,
+                                                      const T* __restrict__ v, int ldkv, int L,
+                                                      const int* __restrict__ lens, int causal,
+                                                      float scale, T* __restrict__ out, int ldo) {
+  extern __shared__ float sm[];  // K [L][HD] then V [L][HD]
+  float* Ks = sm;
+  float* Vs = sm + L * HD;
+  const int b = blockIdx.x, h = blockIdx.y;
+  const int len = lens ? lens[b] : L;
+  for (int e = threadIdx.x; e < len * HD; e += 64) {
+    const int j = e / HD, d = e % HD;
+    const long off = ((long)b * L + j) * ldkv + h * HD + d;
+    Ks[e] = ldf(k + off);
+    Vs[e] = ldf(v + off);
+  }
+  __syncthreads();
+  const int i = blockIdx.z * 64 + threadIdx.x;
+  if (i >= L) return;
+  float qr[HD], o[HD];
+  const T* qrow = q + ((long)b * L + i) * ldq + h * HD;
+#pragma unroll
+  for (int d = 0; d < HD; ++d) { qr[d] = ldf(qrow + d); o[d] = 0.f; }
+  const int jend = causal ? min(i + 1, len) : len;
+  float m = -INFINITY, l = 0.f;
+  for (int j = 0; j < jend; ++j) {
+    float s = 0.f;
+#pragma unroll
+    for (int d = 0; d < HD; ++d) s += qr[d] * Ks[j * HD + d];
+    s *= scale;
+    const float mn = fmaxf(m, s);
+    const float corr = expf(m - mn), p = expf(s - mn);
+    l = l * corr + p;
+#pragma unroll
+    for (int d = 0; d < HD; ++d) o[d] = o[d] * corr + p * Vs[j * HD + d];
+    m = mn;
+  }
+  const float inv = l > 0.f ? 1.0f / l : 0.f;
+  T* orow = out + ((long)b * L + i) * ldo + h * HD;
+#pragma unroll
+  for (int d = 0; d < HD; ++d) stf(orow + d, o[d] * inv);
+}
+
+// ------------------------------------------------------------------ GPT-2 decode attention
+// grid (R, heads), block 64 (hd == 64): append k/v of the new token at pos[r], attend 0..pos[r].
+template <typename T>
+__global__ __launch_bounds__(64) void decode_attn_kernel(const T* __restrict__ qkv, int D,
+                                                         int heads, T* __restrict__ kc,
+                                                         T* __restrict__ vc, int Lmax,
+                                                         const int* __restrict__ pos,
+                                                         const int* __restrict__ kvrow,
+                                                         T* __restrict__ out) {
+  constexpr int HD = 64;
+  extern __shared__ float sm[];
+  float* qs = sm;            // [64]
+  float* kn = sm + 64;       // [64]  new key (also written to the cache)
+  float* sc = sm + 128;      // [Lmax] scores
+  const int r = blockIdx.x, h = blockIdx.y, d = threadIdx.x;
+  const int p = min(pos[r], Lmax - 1);   // defensive: callers keep pos < Lmax
+  const T* row = qkv + (long)r * 3 * D + h * HD;
+  const float qd = ldf(row + d), kd = ldf(row + D + d);
+  const T vd = row[2 * D + d];
+  const long slot = (((long)r * heads + h) * Lmax + p) * HD + d;
+  kc[slot] = row[D + d];
+  vc[slot] = vd;
+  qs[d] = qd;
+  kn[d] = kd;
+  __syncthreads();
+  const float scale = 0.125f;  // 1/sqrt(64)
+  float mx = -INFINITY;
+  for (int j = d; j <= p; j += 64) {
+    float s = 0.f;
+    if (j == p) {
+#pragma unroll 8
+      for (int e = 0; e < HD; ++e) s += qs[e] * kn[e];
+    } else {
+      const int pr = kvrow ? kvrow[(long)r * Lmax + j] : r;
+      const T* kr = kc + (((long)pr * heads + h) * Lmax + j) * HD;
+#pragma unroll 8
+      for (int e = 0; e < HD; ++e) s += qs[e] * ldf(kr + e);
+    }
+    s *= scale;
+    sc[j] = s;
+    mx = fmaxf(mx, s);
+  }
+  mx = wave_max(mx);
+  float sum = 0.f;
+  for (int j = d; j <= p; j += 64) {
+    const float e = expf(sc[j] - mx);
+    sc[j] = e;
+    sum += e;
+  }
+  sum = wave_sum(sum);
+  __syncthreads();
+  const float inv = 1.0f / sum;
+  float o = 0.f;
+  for (int j = 0; j <= p; ++j) {
+    float vv;
+    if (j == p) vv = Cvt<T>::to_f(vd);
+    else {
+      const int pr = kvrow ? kvrow[(long)r * Lmax + j] : r;
+      vv = ldf(vc + (((long)pr * heads + h) * Lmax + j) * HD + d);
+    }
+    o += sc[j] * inv * vv;
+  }
+  stf(out + (long)r * D + h * HD + d, o);
+}
+
+template <typename T>
+__global__ void kv_write_kernel(const T* __restrict__ qkv, int R, int n, int D, int heads,
+                                const int* __restrict__ pos0, int row_stride, T* __restrict__ kc,
+                                T* __restrict__ vc, int Lmax) {
+  const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long total = (long)R * n * D;
+  if (e >= total) return;
+  const int hd = D / heads;
+  const int c = e % D;
+  const long t = e / D;
+  const int i = t % n, r = t / n;
+  const int h = c / hd, d = c % hd;
+  const int p = (pos0 ? pos0[r] : 0) + i;
+  const long slot = (((long)r * row_stride * heads + h) * Lmax + p) * hd + d;
+  kc[slot] = qkv[t * 3 * D + D + c];
+  vc[slot] = qkv[t * 3 * D + 2 * D + c];
+}
+
+}  // namespace zs
+
+using namespace zs;
+
+extern "C" int zs_window_attention(const void* qkv, int B, int H, int W, int C, int heads, int ws,
+                                   int shift, const float* rel_table, void* out, int dtype,
+                                   void* stream) {
+  ZS_REQUIRE(ws == 8 && H % ws == 0 && W % ws == 0, "zs_window_attention: ws must be 8 and divide H, W");
+  ZS_REQUIRE(heads > 0 && C % heads == 0, "zs_window_attention: C %% heads");
+  ZS_REQUIRE(shift >= 0 && shift < ws, "zs_window_attention: shift");
+  const int hd = C / heads;
+  dim3 grid(B * (H / ws) * (W / ws), heads);
+  hipStream_t st = S(stream);
+#define WA(T, HD_)                                                                             \
+  hipLaunchKernelGGL((window_attn_kernel<T, HD_>), grid, dim3(64), 0, st, (const T*)qkv, H, W, C, \
+                     heads, shift, rel_table, (T*)out)
+  if (hd == 24) {
+    if (dtype == ZS_BF16) WA(bf16_t, 24); else WA(float, 24);
+  } else if (hd == 32) {
+    if (dtype == ZS_BF16) WA(bf16_t, 32); else WA(float, 32);
+  } else {
+    return fail(ZS_ERR_UNSUPPORTED, "zs_window_attention: head_dim %d unsupported (24, 32)", hd);
+  }
+#undef WA
+  ZS_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int zs_row_attention(const void* q, int ldq, const void* k, const void* v, int ldkv,
+                                int B, int L, const int* len, int heads, int hd, int causal,
+                                float scale, void* out, int ldo, int dtype, void* stream) {
+  ZS_REQUIRE(B > 0 && L > 0 && L <= 256 && heads > 0, "zs_row_attention: bad shape");
+  const size_t smem = (size_t)2 * L * hd * sizeof(float);
+  ZS_REQUIRE(smem <= 160 * 1024, "zs_row_attention: L*hd too large for LDS");
+  dim3 grid(B, heads, cdiv(L, 64));
+  hipStream_t st = S(stream);
+#define RA(T, HD_)                                                                              \
+  hipLaunchKernelGGL((row_attn_kernel<T, HD_>), grid, dim3(64), smem, st, (const T*)q, ldq,       \
+                     (const T*)k, (const T*)v, ldkv, L, len, causal, scale, (T*)out, ldo)
+  if (hd == 64) {
+    if (dtype == ZS_BF16) RA(bf16_t, 64); else RA(float, 64);
+  } else if (hd == 96) {
+    if (dtype == ZS_BF16) RA(bf16_t, 96); else RA(float, 96);
+  } else {
+    return fail(ZS_ERR_UNSUPPORTED, "zs_row_attention: head_dim %d unsupported (64, 96)", hd);
+  }
+#undef RA
+  ZS_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int zs_decode_attention(const void* qkv, int R, int D, int heads, void* kc, void* vc,
+                                   int Lmax, const int* pos, const int* kvrow, void* out,
+                                   int dtype, void* stream) {
+  ZS_REQUIRE(R > 0 && heads > 0 && D / heads == 64 && D % heads == 0,
+             "zs_decode_attention: head_dim must be 64");
+  ZS_REQUIRE(Lmax > 0 && Lmax <= 4096, "zs_decode_attention: Lmax");
+  dim3 grid(R, heads);
+  const size_t smem = (128 + (size_t)Lmax) * sizeof(float);
+  if (dtype == ZS_BF16)
+    hipLaunchKernelGGL(decode_attn_kernel<bf16_t>, grid, dim3(64), smem, S(stream),
+                       (const bf16_t*)qkv, D, heads, (bf16_t*)kc, (bf16_t*)vc, Lmax, pos, kvrow,
+                       (bf16_t*)out);
+  else
+    hipLaunchKernelGGL(decode_attn_kernel<float>, grid, dim3(64), smem, S(stream),
+                       (const float*)qkv, D, heads, (float*)kc, (float*)vc, Lmax, pos, kvrow,
+                       (float*)out);
+  ZS_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int zs_kv_write(const void* qkv, int R, int n, int D, int heads, const int* pos0,
+                           int row_stride, void* kc, void* vc, int Lmax, int dtype,
+                           void* stream) {
+  ZS_REQUIRE(R > 0 && n > 0 && heads > 0 && D % heads == 0 && n <= Lmax, "zs_kv_write: bad shape");
+  const long total = (long)R * n * D;
+  if (dtype == ZS_BF16)
+    hipLaunchKernelGGL(kv_write_kernel<bf16_t>, dim3(cdiv(total, 256)), dim3(256), 0, S(stream),
+                       (const bf16_t*)qkv, R, n, D, heads, pos0, row_stride, (bf16_t*)kc, (bf16_t*)vc, Lmax);
+  else
+    hipLaunchKernelGGL(kv_write_kernel<float>, dim3(cdiv(total, 256)), dim3(256), 0, S(stream),
+                       (const float*)qkv, R, n, D, heads, pos0, row_stride, (float*)kc, (float*)vc, Lmax);
+  ZS_LAUNCH_CHECK();
+  return 0;
+}

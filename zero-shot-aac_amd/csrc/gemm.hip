@@ -1,0 +1,274 @@
+// MFMA GEMM for every Linear/Conv1D on the hot path, plus the LM-head GEMM with a fused
+// per-row max / sum-exp / top-k epilogue (greedy argmax, beam log-softmax top-k,
+// get_prefix_tokens cosine argmax).
+//
+//   out[m][n] = act(sum_k A[m][k] * W[n][k] + bias[n]) + residual[m][n]
+//
+// Tiles: BM x BN x 32, 256 threads = 4 waves in a 2x2 grid, each wave owning (BM/2) x (BN/2) as
+// 32x32 MFMA tiles.  bf16: v_mfma_f32_32x32x16_bf16 (2 per 32-deep k-tile); f32 (parity mode):
+// v_mfma_f32_32x32x2f32 with lane-half h owning k in [16h,16h+16) so both dtypes share one LDS
+// image ([row][32 + 16B pad], read 16 B per lane).  Global->LDS is register staged and double
+// buffered (next tile's loads issued before the current tile's MFMAs).
+#include "gemm_core.h"
+
+namespace zs {
+
+__device__ __forceinline__ void store_out(void* out, int out_dtype, long idx, float v) {
+  if (out_dtype == ZS_BF16) reinterpret_cast<bf16_t*>(out)[idx] = f2bf(v);
+  else reinterpret_cast<float*>(out)[idx] = v;
+}
+
+template <typename T, int BM, int BN>
+__global__ __launch_bounds__(256) void gemm_kernel(GemmArgs g) {
+  constexpr int LDW = BK + GemmTraits<T>::PAD;
+  __shared__ __attribute__((aligned(16))) T smem[2 * (BM + BN) * LDW];
+  constexpr int TM = BM / 64, TN = BN / 64;
+  const int n0 = blockIdx.x * BN, m0 = blockIdx.y * BM, z = blockIdx.z;
+  const int kbeg = z * g.k_per_split, kend = min(g.K, kbeg + g.k_per_split);
+  f32x16_t acc[TM][TN];
+  DenseA<T, BM> la{(const T*)g.A, g.lda, g.M, m0};
+  gemm_mainloop<T, BM, BN>(la, (const T*)g.W, g.ldw, g.N, n0, kbeg, kend, smem, acc);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int wr0 = (wid >> 1) * (BM / 2), wc0 = (wid & 1) * (BN / 2);
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int n = n0 + wc0 + j * 32 + (lane & 31);
+      if (n >= g.N) continue;
+      const float bias = (g.split_k == 1 && g.bias) ? g.bias[n] : 0.f;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int m = m0 + wr0 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5);
+        if (m >= g.M) continue;
+        float v = acc[i][j][e];
+        if (g.split_k > 1) {
+          g.ws[((long)z * g.M + m) * g.N + n] = v;
+        } else {
+          v = act_apply(v + bias, g.act);
+          if (g.residual) v += g.residual[(long)m * g.ldr + n];
+          store_out(g.out, g.out_dtype, (long)m * g.ldo + n, v);
+        }
+      }
+    }
+}
+
+// deterministic split-K reduction: sum slabs in order, then the same epilogue
+__global__ void splitk_reduce_kernel(GemmArgs g) {
+  long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  long total = (long)g.M * g.N;
+  if (idx >= total) return;
+  int m = idx / g.N, n = idx % g.N;
+  float v = 0.f;
+  for (int z = 0; z < g.split_k; ++z) v += g.ws[(long)z * total + idx];
+  if (g.bias) v += g.bias[n];
+  v = act_apply(v, g.act);
+  if (g.residual) v += g.residual[(long)m * g.ldr + n];
+  store_out(g.out, g.out_dtype, (long)m * g.ldo + n, v);
+}
+
+template <typename T, int BM, int BN>
+static int launch_gemm(GemmArgs& g, hipStream_t st) {
+  dim3 grid(cdiv(g.N, BN), cdiv(g.M, BM), g.split_k);
+  hipLaunchKernelGGL((gemm_kernel<T, BM, BN>), grid, dim3(256), 0, st, g);
+  ZS_LAUNCH_CHECK();
+  return 0;
+}
+
+template <typename T>
+static int dispatch_gemm(GemmArgs& g, hipStream_t st) {
+  const bool small_m = g.M <= 64;
+  const bool wide_n = g.N >= 2048 && !small_m;
+  if (small_m) return wide_n ? launch_gemm<T, 64, 128>(g, st) : launch_gemm<T, 64, 64>(g, st);
+  if (wide_n) return launch_gemm<T, 128, 128>(g, st);
+  return launch_gemm<T, 128, 64>(g, st);
+}
+
+// ------------------------------------------------------------------ LM head (+ row reductions)
+constexpr int LM_BN = 128;
+constexpr int MAXK = 8;
+
+template <typename T, int BM, int KMAX>
+__global__ __launch_bounds__(256) void lmhead_kernel(int M, int K, int V, const T* A, int lda,
+                                                     const T* W, int topk, int row_norm,
+                                                     float* part_stat, float* part_val,
+                                                     int* part_idx) {
+  constexpr int LDW = BK + GemmTraits<T>::PAD;
+  constexpr int TM = BM / 64, TN = LM_BN / 64;
+  constexpr int SM_MAIN = 2 * (BM + LM_BN) * LDW * (int)sizeof(T);
+  constexpr int SM_EPI = BM * (LM_BN + 1) * 4;
+  constexpr int SM = SM_MAIN > SM_EPI ? SM_MAIN : SM_EPI;
+  __shared__ __attribute__((aligned(16))) char smem_raw[SM];
+  __shared__ float inv_norm[BM];
+  const int n0 = blockIdx.x * LM_BN, m0 = blockIdx.y * BM;
+  const int nblk = gridDim.x;
+  f32x16_t acc[TM][TN];
+  DenseA<T, BM> la{A, lda, M, m0};
+  gemm_mainloop<T, BM, LM_BN>(la, W, K, V, n0, 0, K, (T*)smem_raw, acc);
+  // row norms for get_prefix_tokens (normalize(a) . w == (a . w) / max(||a||, 1e-12))
+  if (row_norm) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    for (int r = wid; r < BM; r += 4) {
+      float s = 0.f;
+      if (m0 + r < M)
+        for (int k = lane; k < K; k += 64) {
+          float a = ldf(A + (long)(m0 + r) * lda + k);
+          s += a * a;
+        }
+      s = wave_sum(s);
+      if (lane == 0) inv_norm[r] = 1.0f / fmaxf(sqrtf(s), 1e-12f);
+    }
+  }
+  __syncthreads();
+  float* tile = reinterpret_cast<float*>(smem_raw);   // [BM][LM_BN+1]
+  {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int wr0 = (wid >> 1) * (BM / 2), wc0 = (wid & 1) * (LM_BN / 2);
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int r = wr0 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5);
+          const int c = wc0 + j * 32 + (lane & 31);
+          tile[r * (LM_BN + 1) + c] = acc[i][j][e];
+        }
+  }
+  __syncthreads();
+  // each row is reduced by TPR threads, each scanning LM_BN/TPR consecutive columns
+  constexpr int TPR = 256 / BM;
+  constexpr int CPT = LM_BN / TPR;
+  const int r = threadIdx.x / TPR, sub = threadIdx.x % TPR;
+  const int m = m0 + r;
+  const float scale = row_norm ? inv_norm[r] : 1.0f;
+  float mx = -INFINITY;
+  float tv[KMAX];
+  int ti[KMAX];
+#pragma unroll
+  for (int q = 0; q < KMAX; ++q) { tv[q] = -INFINITY; ti[q] = 0x7fffffff; }
+  for (int c = sub * CPT; c < sub * CPT + CPT; ++c) {
+    const int n = n0 + c;
+    if (n >= V) break;
+    const float v = tile[r * (LM_BN + 1) + c] * scale;
+    mx = fmaxf(mx, v);
+    // insertion into the descending top-k list (strict > keeps the lower index on ties)
+    if (KMAX == 1) {
+      if (v > tv[0]) { tv[0] = v; ti[0] = n; }
+    } else if (v > tv[KMAX - 1]) {
+      // bubble the new value up the (static-indexed) list
+      float cv = v;
+      int ci = n;
+#pragma unroll
+      for (int q = 0; q < KMAX; ++q) {
+        if (cv > tv[q]) {
+          const float t = tv[q];
+          const int u = ti[q];
+          tv[q] = cv; ti[q] = ci;
+          cv = t; ci = u;
+        }
+      }
+    }
+  }
+  // combine max across the TPR threads of this row (consecutive lanes)
+  float gmx = mx;
+#pragma unroll
+  for (int o = 1; o < TPR; o <<= 1) gmx = fmaxf(gmx, __shfl_xor(gmx, o, 64));
+  float se = 0.f;
+  for (int c = sub * CPT; c < sub * CPT + CPT; ++c) {
+    const int n = n0 + c;
+    if (n >= V) break;
+    se += expf(tile[r * (LM_BN + 1) + c] * scale - gmx);
+  }
+#pragma unroll
+  for (int o = 1; o < TPR; o <<= 1) se += __shfl_xor(se, o, 64);
+  __syncthreads();
+  // merge the TPR sorted lists through LDS (reuse the tile area after the barrier)
+  float* mv = reinterpret_cast<float*>(smem_raw);
+  int* mi = reinterpret_cast<int*>(smem_raw + 256 * MAXK * 4);
+#pragma unroll
+  for (int q = 0; q < KMAX; ++q) { mv[threadIdx.x * MAXK + q] = tv[q]; mi[threadIdx.x * MAXK + q] = ti[q]; }
+  __syncthreads();
+  if (sub == 0 && m < M) {
+    const long o = ((long)m * nblk + blockIdx.x);
+    part_stat[o * 2 + 0] = gmx;
+    part_stat[o * 2 + 1] = se;
+    int ptr[TPR];
+#pragma unroll
+    for (int t = 0; t < TPR; ++t) ptr[t] = 0;
+    for (int q = 0; q < topk; ++q) {
+      int best = -1;
+      float bv = -INFINITY;
+      int bi = 0x7fffffff;
+#pragma unroll
+      for (int t = 0; t < TPR; ++t) {
+        if (ptr[t] >= topk) continue;
+        const float v = mv[(threadIdx.x + t) * MAXK + ptr[t]];
+        const int ix = mi[(threadIdx.x + t) * MAXK + ptr[t]];
+        if (best < 0 || v > bv || (v == bv && ix < bi)) { best = t; bv = v; bi = ix; }
+      }
+      ptr[best]++;
+      part_val[o * topk + q] = bv;
+      part_idx[o * topk + q] = bi;
+    }
+  }
+}
+
+}  // namespace zs
+
+using namespace zs;
+
+extern "C" int zs_gemm(int M, int N, int K, int dtype, const void* A, int lda, const void* W,
+                       int ldw, const float* bias, const float* residual, int ldr, void* out,
+                       int ldo, int out_dtype, int act, int split_k, float* workspace,
+                       void* stream) {
+  ZS_REQUIRE(M >= 0 && N > 0 && K > 0, "zs_gemm: bad shape M=%d N=%d K=%d", M, N, K);
+  ZS_REQUIRE(K % BK == 0, "zs_gemm: K=%d must be a multiple of 32", K);
+  ZS_REQUIRE(lda % 8 == 0 && ldw % 8 == 0, "zs_gemm: lda/ldw must be multiples of 8");
+  ZS_REQUIRE(split_k >= 1, "zs_gemm: split_k >= 1");
+  ZS_REQUIRE(dtype == ZS_F32 || dtype == ZS_BF16, "zs_gemm: dtype");
+  if (M == 0) return 0;
+  GemmArgs g{M, N, K, lda, ldw, ldr, ldo, A, W, bias, residual, out, out_dtype, act, 1, K, workspace};
+  if (split_k > 1) {
+    int kps = cdiv(cdiv(K, split_k), BK) * BK;
+    int s = cdiv(K, kps);
+    ZS_REQUIRE(workspace != nullptr, "zs_gemm: split_k needs a workspace");
+    g.split_k = s;
+    g.k_per_split = kps;
+  }
+  hipStream_t st = S(stream);
+  int rc = dtype == ZS_BF16 ? dispatch_gemm<bf16_t>(g, st) : dispatch_gemm<float>(g, st);
+  if (rc) return rc;
+  if (g.split_k > 1) {
+    long total = (long)M * N;
+    hipLaunchKernelGGL(splitk_reduce_kernel, dim3(cdiv(total, 256)), dim3(256), 0, st, g);
+    ZS_LAUNCH_CHECK();
+  }
+  return 0;
+}
+
+extern "C" int zs_lmhead_nblk(int V) { return cdiv(V, LM_BN); }
+
+extern "C" int zs_lmhead_topk(int M, int K, int V, int dtype, const void* A, int lda,
+                              const void* W, int topk, int row_norm, float* part_stat,
+                              float* part_val, int* part_idx, void* stream) {
+  ZS_REQUIRE(M > 0 && K > 0 && V > 0, "zs_lmhead_topk: bad shape");
+  ZS_REQUIRE(K % BK == 0 && lda % 8 == 0, "zs_lmhead_topk: K %% 32, lda %% 8");
+  ZS_REQUIRE(topk >= 1 && topk <= MAXK, "zs_lmhead_topk: 1 <= topk <= 8");
+  hipStream_t st = S(stream);
+  const int nblk = cdiv(V, LM_BN);
+#define LMH(T, BM_, KM_)                                                                     \
+  hipLaunchKernelGGL((lmhead_kernel<T, BM_, KM_>), dim3(nblk, cdiv(M, BM_)), dim3(256), 0, st, \
+                     M, K, V, (const T*)A, lda, (const T*)W, topk, row_norm, part_stat,       \
+                     part_val, part_idx)
+#define LMH_K(T, BM_) do { if (topk == 1) LMH(T, BM_, 1); else LMH(T, BM_, 8); } while (0)
+  if (M <= 64) {
+    if (dtype == ZS_BF16) LMH_K(bf16_t, 64); else LMH_K(float, 64);
+  } else {
+    if (dtype == ZS_BF16) LMH_K(bf16_t, 128); else LMH_K(float, 128);
+  }
+#undef LMH_K
+#undef LMH
+  ZS_LAUNCH_CHECK();
+  return 0;
+}

@@ -1,0 +1,442 @@
+// GPT-2 decode glue + prompt assembly:
+//  * prompt_assemble  — sound_effect_choice + compose_discrete_prompts + padding_captions on
+//                       device (utils.py:131-208, dataset/dataset.py:441-453);
+//  * prefill_embed    — clap_to_gpt concat (caption_model.py:315-329) + wte/wpe lookup;
+//  * embed_tokens     — decode-step input embedding;
+//  * argmax_finalize / greedy_step / beam_step — generate2 / generate_beam bookkeeping on device
+//    (gpt2_prefix_eval.py:99-158, 161-222) so a captured decode step needs no host round trip.
+#include "common.h"
+
+namespace zs {
+
+// ------------------------------------------------------------------ prompt
+__global__ __launch_bounds__(256) void prompt_kernel(const float* __restrict__ emb, int D,
+                                                     const float* __restrict__ labels, int L,
+                                                     int k, const int* __restrict__ ltok,
+                                                     const int* __restrict__ llen, int max_tok,
+                                                     int* __restrict__ hard_ids, int h_cap,
+                                                     int* __restrict__ hard_len,
+                                                     int* __restrict__ chosen) {
+  extern __shared__ float sm[];
+  float* e = sm;          // [D]
+  float* sim = sm + D;    // [L]
+  __shared__ int sel[16];
+  __shared__ float rv[4];
+  __shared__ int ri[4];
+  const int b = blockIdx.x;
+  for (int d = threadIdx.x; d < D; d += 256) e[d] = emb[(long)b * D + d];
+  __syncthreads();
+  for (int l = threadIdx.x; l < L; l += 256) {
+    const float* lr = labels + (long)l * D;
+    float s = 0.f;
+    for (int d = 0; d < D; ++d) s += e[d] * lr[d];
+    sim[l] = s;
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  for (int q = 0; q < k; ++q) {
+    float bv = -INFINITY;
+    int bi = 0x7fffffff;
+    for (int l = threadIdx.x; l < L; l += 256) {
+      bool taken = false;
+      for (int p = 0; p < q; ++p) taken |= (sel[p] == l);
+      if (!taken && (sim[l] > bv || (sim[l] == bv && l < bi))) { bv = sim[l]; bi = l; }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const float ov = __shfl_xor(bv, o, 64);
+      const int oi = __shfl_xor(bi, o, 64);
+      if (ov > bv || (ov == bv && oi < bi)) { bv = ov; bi = oi; }
+    }
+    if (lane == 0) { rv[wid] = bv; ri[wid] = bi; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      float v = rv[0];
+      int i = ri[0];
+      for (int w = 1; w < 4; ++w)
+        if (rv[w] > v || (rv[w] == v && ri[w] < i)) { v = rv[w]; i = ri[w]; }
+      sel[q] = i;
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    int* out = hard_ids + (long)b * h_cap;
+    int n = 0;
+    auto put = [&](int id) { if (n < h_cap) out[n] = id; ++n; };
+    put(1858); put(389);                    // "There", " are"
+    if (k == 0) {
+      put(1223);                            // " something"
+    } else {
+      for (int q = 0; q < k; ++q) {
+        const int l = sel[q];
+        for (int t = 0; t < llen[l] && t < max_tok; ++t) put(ltok[(long)l * max_tok + t]);
+        if (q + 1 < k) put(11);             // ","
+        if (chosen) chosen[(long)b * k + q] = l;
+      }
+    }
+    put(287); put(428); put(6597); put(13); // " in", " this", " audio", "."
+    hard_len[b] = n < h_cap ? n : h_cap;
+    for (int t = n; t < h_cap; ++t) out[t] = 0;
+  }
+}
+
+// ------------------------------------------------------------------ embeddings
+template <typename T>
+__global__ void prefill_embed_kernel(const int* __restrict__ hard_ids,
+                                     const int* __restrict__ hard_len, int h_cap,
+                                     const float* __restrict__ soft, int soft_ld, int n_soft,
+                                     const T* __restrict__ wte, const T* __restrict__ wpe, int Pmax,
+                                     int D, float* __restrict__ embed, float* __restrict__ x,
+                                     int* __restrict__ plen, int* __restrict__ last_row) {
+  const int b = blockIdx.y, p = blockIdx.x;
+  const int H = hard_len[b], P = H + n_soft;
+  if (p == 0 && threadIdx.x == 0) {
+    plen[b] = P;
+    if (last_row) last_row[b] = b * Pmax + P - 1;
+  }
+  const long o = ((long)b * Pmax + p) * D;
+  for (int d = threadIdx.x; d < D; d += blockDim.x) {
+    float e = 0.f, xv = 0.f;
+    if (p < H) e = ldf(wte + (long)hard_ids[(long)b * h_cap + p] * D + d);
+    else if (p < P) e = soft[(long)b * soft_ld + (long)(p - H) * D + d];
+    if (p < P) xv = e + ldf(wpe + (long)p * D + d);
+    if (embed) embed[o + d] = e;
+    x[o + d] = xv;
+  }
+}
+
+template <typename T>
+__global__ void embed_tokens_kernel(const int* __restrict__ tok, const int* __restrict__ pos,
+                                    const T* __restrict__ wte, const T* __restrict__ wpe, int D,
+                                    float* __restrict__ x) {
+  const int r = blockIdx.x;
+  const int t = tok[r], p = pos[r];
+  for (int d = threadIdx.x; d < D; d += blockDim.x)
+    x[(long)r * D + d] = ldf(wte + (long)t * D + d) + ldf(wpe + (long)p * D + d);
+}
+
+// ------------------------------------------------------------------ argmax over LM-head partials
+__device__ __forceinline__ void wave_argmax(float& v, int& i) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float ov = __shfl_xor(v, o, 64);
+    const int oi = __shfl_xor(i, o, 64);
+    if (ov > v || (ov == v && oi < i)) { v = ov; i = oi; }
+  }
+}
+
+__device__ __forceinline__ int row_argmax(const float* pv, const int* pi, int r, int nblk,
+                                          int lane) {
+  float v = -INFINITY;
+  int i = 0x7fffffff;
+  for (int k = lane; k < nblk; k += 64) {
+    const float cv = pv[(long)r * nblk + k];
+    const int ci = pi[(long)r * nblk + k];
+    if (cv > v || (cv == v && ci < i)) { v = cv; i = ci; }
+  }
+  wave_argmax(v, i);
+  return i;
+}
+
+__global__ void argmax_finalize_kernel(const float* __restrict__ pv, const int* __restrict__ pi,
+                                       int M, int nblk, int* __restrict__ idx) {
+  const int lane = threadIdx.x & 63;
+  const int r = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (r >= M) return;
+  const int t = row_argmax(pv, pi, r, nblk, lane);
+  if (lane == 0) idx[r] = t;
+}
+
+// one block (1024 threads = 16 waves) for all R rows
+__global__ __launch_bounds__(1024) void greedy_step_kernel(
+    const float* __restrict__ pv, const int* __restrict__ pi, int R, int nblk, int* step_ctr,
+    int max_steps, int stop0, int stop1, int* __restrict__ out_ids, int* __restrict__ out_len,
+    int* __restrict__ done, int* __restrict__ pos, int* __restrict__ next_tok,
+    int* __restrict__ all_done) {
+  __shared__ int s_step;
+  __shared__ int s_alive;
+  if (threadIdx.x == 0) { s_step = *step_ctr; s_alive = 0; }
+  __syncthreads();
+  const int step = s_step;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  for (int r = wid; r < R; r += nw) {
+    const int t = row_argmax(pv, pi, r, nblk, lane);
+    if (lane == 0) {
+      int d = done[r];
+      if (!d && step < max_steps) {
+        out_ids[(long)r * max_steps + step] = t;
+        out_len[r] = step + 1;
+        if (t == stop0 || t == stop1) d = 1;
+        done[r] = d;
+      }
+      if (!d) atomicAdd(&s_alive, 1);
+      next_tok[r] = t;
+      if (step < max_steps) pos[r] += 1;   // past entry_length the graph tail re-runs in place
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    *step_ctr = step + 1;
+    all_done[0] = (s_alive == 0 || step + 1 >= max_steps) ? 1 : 0;
+  }
+}
+
+// ------------------------------------------------------------------ beam search step
+// one block per clip; beam <= 8, topk (partials per block) >= beam
+__global__ __launch_bounds__(256) void beam_step_kernel(
+    const float* __restrict__ pstat, const float* __restrict__ pv, const int* __restrict__ pi,
+    int beam, int nblk, int topk, int first, int stop, const int* __restrict__ step_ctr,
+    int max_steps, float* __restrict__ scores, float* __restrict__ seq_len,
+    int* __restrict__ stopped, int* __restrict__ tokens, int* __restrict__ tokens_tmp,
+    int* __restrict__ kvrow, int* __restrict__ kvrow_tmp, int Lmax, int* __restrict__ pos,
+    int* __restrict__ next_tok) {
+  constexpr int MB = 8;
+  __shared__ float c_val[MB * MB];      // candidate values per (source row, rank)
+  __shared__ int c_tok[MB * MB];
+  __shared__ float c_logp[MB * MB];
+  __shared__ int sel_src[MB], sel_tok[MB];
+  __shared__ float sel_avg[MB];
+  __shared__ int s_skip;
+  const int c = blockIdx.x, lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int step = *step_ctr;
+  const int r0 = c * beam;
+  if (threadIdx.x == 0) {
+    int all = 1;
+    for (int i = 0; i < beam; ++i) all &= stopped[r0 + i];
+    s_skip = (!first && all) || step >= max_steps;
+  }
+  __syncthreads();
+  if (s_skip) return;   // finished clip: the reference has left its loop; state is frozen
+  const int nsrc = first ? 1 : beam;
+  // per source row: lse pieces and its top-`beam` logits (merging the per-block sorted lists)
+  for (int i = wid; i < nsrc; i += 4) {
+    const int prow = first ? c : r0 + i;   // partial row (prefill rows are per clip)
+    float M = -INFINITY;
+    for (int k = lane; k < nblk; k += 64) M = fmaxf(M, pstat[((long)prow * nblk + k) * 2]);
+    M = wave_max(M);
+    float Ssum = 0.f;
+    for (int k = lane; k < nblk; k += 64) {
+      const float bm = pstat[((long)prow * nblk + k) * 2];
+      Ssum += pstat[((long)prow * nblk + k) * 2 + 1] * expf(bm - M);
+    }
+    Ssum = wave_sum(Ssum);
+    // top-beam over all blocks' lists: `beam` rounds of wave argmax over list heads
+    float lastv = INFINITY;
+    int lasti = -1;
+    for (int q = 0; q < beam; ++q) {
+      float bv = -INFINITY;
+      int bi = 0x7fffffff;
+      for (int k = lane; k < nblk; k += 64)
+        for (int t = 0; t < topk; ++t) {
+          const float v = pv[((long)prow * nblk + k) * topk + t];
+          const int ix = pi[((long)prow * nblk + k) * topk + t];
+          // strictly after the previous pick in (value desc, index asc) order
+          const bool after = v < lastv || (v == lastv && ix > lasti);
+          if (after && (v > bv || (v == bv && ix < bi))) { bv = v; bi = ix; }
+        }
+      wave_argmax(bv, bi);
+      lastv = bv;
+      lasti = bi;
+      if (lane == 0) {
+        // generate_beam: logits.softmax(-1).log() (gpt2_prefix_eval.py:122)
+        const float lp = logf(expf(bv - M) / Ssum);
+        c_tok[i * MB + q] = bi;
+        c_logp[i * MB + q] = lp;
+      }
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float newlen[MB];
+    if (first) {
+      for (int q = 0; q < beam; ++q) {
+        sel_src[q] = 0; sel_tok[q] = c_tok[q]; sel_avg[q] = c_logp[q];
+      }
+    } else {
+      // candidates: non-stopped rows -> (score + logp) / (len + 1); stopped rows -> token 0
+      // with logp 0 at their unchanged length (gpt2_prefix_eval.py:132-137)
+      for (int i = 0; i < beam; ++i) {
+        const int r = r0 + i;
+        const bool st = stopped[r];
+        newlen[i] = st ? seq_len[r] : seq_len[r] + 1.0f;
+        if (st) {
+          c_val[i * MB] = (scores[r] + 0.0f) / newlen[i];
+          c_tok[i * MB] = 0;
+          for (int q = 1; q < beam; ++q) c_val[i * MB + q] = -INFINITY;
+        } else {
+          for (int q = 0; q < beam; ++q) c_val[i * MB + q] = (scores[r] + c_logp[i * MB + q]) / newlen[i];
+        }
+      }
+      // top-beam over beam x beam candidates; ties -> lower flattened index src*V + tok
+      unsigned used[MB] = {0};
+      for (int q = 0; q < beam; ++q) {
+        int bs = -1, bq = -1;
+        float bv = -INFINITY;
+        long bflat = 0x7fffffffffffffffL;
+        for (int i = 0; i < beam; ++i)
+          for (int t = 0; t < beam; ++t) {
+            if (used[i] & (1u << t)) continue;
+            const float v = c_val[i * MB + t];
+            const long flat = (long)i * 50257 + c_tok[i * MB + t];
+            if (bs < 0 || v > bv || (v == bv && flat < bflat)) { bs = i; bq = t; bv = v; bflat = flat; }
+          }
+        used[bs] |= 1u << bq;
+        sel_src[q] = bs; sel_tok[q] = c_tok[bs * MB + bq]; sel_avg[q] = bv;
+      }
+      for (int q = 0; q < beam; ++q) c_val[q] = newlen[sel_src[q]];   // reuse: chosen lengths
+    }
+  }
+  __syncthreads();
+  // gather histories of the chosen sources into tmp, then write back
+  const int P = pos[r0];   // all rows of a clip share the position of this step's token
+  for (int q = 0; q < beam; ++q) {
+    const int src = first ? r0 : r0 + sel_src[q];
+    const int dst = r0 + q;
+    for (int s = threadIdx.x; s < step; s += 256)
+      tokens_tmp[(long)dst * max_steps + s] = tokens[(long)src * max_steps + s];
+    for (int s = threadIdx.x; s < Lmax; s += 256) {
+      int v;
+      if (first) v = s < P ? r0 : -1;                       // prompt lives in clip row r0
+      else v = s < P ? kvrow[(long)src * Lmax + s] : (s == P ? src : -1);
+      kvrow_tmp[(long)dst * Lmax + s] = v;
+    }
+  }
+  __syncthreads();
+  for (int q = 0; q < beam; ++q) {
+    const int dst = r0 + q;
+    for (int s = threadIdx.x; s < step; s += 256)
+      tokens[(long)dst * max_steps + s] = tokens_tmp[(long)dst * max_steps + s];
+    for (int s = threadIdx.x; s < Lmax; s += 256)
+      kvrow[(long)dst * Lmax + s] = kvrow_tmp[(long)dst * Lmax + s];
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int st_new[MB];
+    float len_new[MB], sc_new[MB];
+    for (int q = 0; q < beam; ++q) {
+      const int src = r0 + sel_src[q];
+      if (first) {
+        len_new[q] = 1.0f;
+        sc_new[q] = sel_avg[q];
+        st_new[q] = 0;
+      } else {
+        len_new[q] = c_val[q];
+        sc_new[q] = sel_avg[q] * len_new[q];   // scores = scores_sum_average * seq_lengths
+        st_new[q] = stopped[src];
+      }
+    }
+    for (int q = 0; q < beam; ++q) {
+      const int dst = r0 + q;
+      const int tok = sel_tok[q];
+      tokens[(long)dst * max_steps + step] = tok;
+      seq_len[dst] = len_new[q];
+      scores[dst] = sc_new[q];
+      stopped[dst] = st_new[q] | (tok == stop);
+      next_tok[dst] = tok;
+      pos[dst] = (first ? P : P + 1);
+    }
+  }
+}
+
+__global__ void beam_advance_kernel(const int* __restrict__ stopped, int R, int* step_ctr,
+                                    int max_steps, int* all_done) {
+  __shared__ int alive;
+  if (threadIdx.x == 0) alive = 0;
+  __syncthreads();
+  int a = 0;
+  for (int r = threadIdx.x; r < R; r += blockDim.x) a |= !stopped[r];
+  if (a) atomicOr(&alive, 1);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int s = *step_ctr + 1;
+    *step_ctr = s;
+    all_done[0] = (!alive || s >= max_steps) ? 1 : 0;
+  }
+}
+
+}  // namespace zs
+
+using namespace zs;
+
+extern "C" int zs_prompt_assemble(const float* emb, int B, int D, const float* labels, int L,
+                                  int k, const int* label_tok, const int* label_len, int max_tok,
+                                  int* hard_ids, int h_cap, int* hard_len, int* chosen,
+                                  void* stream) {
+  ZS_REQUIRE(B > 0 && D > 0 && L > 0 && k >= 0 && k <= 16 && k <= L, "zs_prompt_assemble: bad shape");
+  const size_t smem = (size_t)(D + L) * sizeof(float);
+  ZS_REQUIRE(smem <= 64 * 1024, "zs_prompt_assemble: D+L too large");
+  hipLaunchKernelGGL(prompt_kernel, dim3(B), dim3(256), smem, S(stream), emb, D, labels, L, k,
+                     label_tok, label_len, max_tok, hard_ids, h_cap, hard_len, chosen);
+  ZS_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int zs_gpt2_prefill_embed(const int* hard_ids, const int* hard_len, int h_cap,
+                                     const float* soft, int soft_ld, int n_soft, const void* wte,
+                                     const void* wpe, int B, int Pmax, int D, float* embed,
+                                     float* x, int* plen, int* last_row, int dtype, void* stream) {
+  ZS_REQUIRE(B > 0 && Pmax > 0 && D > 0, "zs_gpt2_prefill_embed: bad shape");
+  dim3 grid(Pmax, B);
+  if (dtype == ZS_BF16)
+    hipLaunchKernelGGL(prefill_embed_kernel<bf16_t>, grid, dim3(256), 0, S(stream), hard_ids,
+                       hard_len, h_cap, soft, soft_ld, n_soft, (const bf16_t*)wte, (const bf16_t*)wpe,
+                       Pmax, D, embed, x, plen, last_row);
+  else
+    hipLaunchKernelGGL(prefill_embed_kernel<float>, grid, dim3(256), 0, S(stream), hard_ids,
+                       hard_len, h_cap, soft, soft_ld, n_soft, (const float*)wte, (const float*)wpe,
+                       Pmax, D, embed, x, plen, last_row);
+  ZS_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int zs_embed_tokens(const int* tok, const int* pos, const void* wte, const void* wpe,
+                               int R, int D, float* x, int dtype, void* stream) {
+  ZS_REQUIRE(R > 0 && D > 0, "zs_embed_tokens: bad shape");
+  if (dtype == ZS_BF16)
+    hipLaunchKernelGGL(embed_tokens_kernel<bf16_t>, dim3(R), dim3(256), 0, S(stream), tok, pos,
+                       (const bf16_t*)wte, (const bf16_t*)wpe, D, x);
+  else
+    hipLaunchKernelGGL(embed_tokens_kernel<float>, dim3(R), dim3(256), 0, S(stream), tok, pos,
+                       (const float*)wte, (const float*)wpe, D, x);
+  ZS_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int zs_argmax_finalize(const float* part_val, const int* part_idx, int M, int nblk,
+                                  int* idx, void* stream) {
+  ZS_REQUIRE(M > 0 && nblk > 0, "zs_argmax_finalize: bad shape");
+  hipLaunchKernelGGL(argmax_finalize_kernel, dim3(cdiv(M, 4)), dim3(256), 0, S(stream), part_val,
+                     part_idx, M, nblk, idx);
+  ZS_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int zs_greedy_step(const float* part_val, const int* part_idx, int R, int nblk,
+                              int* step_ctr, int max_steps, int stop0, int stop1, int* out_ids,
+                              int* out_len, int* done, int* pos, int* next_tok, int* all_done,
+                              void* stream) {
+  ZS_REQUIRE(R > 0 && nblk > 0 && max_steps > 0, "zs_greedy_step: bad shape");
+  hipLaunchKernelGGL(greedy_step_kernel, dim3(1), dim3(1024), 0, S(stream), part_val, part_idx, R,
+                     nblk, step_ctr, max_steps, stop0, stop1, out_ids, out_len, done, pos,
+                     next_tok, all_done);
+  ZS_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int zs_beam_step(const float* part_stat, const float* part_val, const int* part_idx,
+                            int C, int beam, int nblk, int topk, int first, int stop,
+                            int* step_ctr, int max_steps, float* scores, float* seq_len,
+                            int* stopped, int* tokens, int* tokens_tmp, int* kvrow,
+                            int* kvrow_tmp, int Lmax, int* pos, int* next_tok, int* all_done,
+                            void* stream) {
+  ZS_REQUIRE(C > 0 && beam >= 1 && beam <= 8 && topk >= beam && nblk > 0,
+             "zs_beam_step: 1 <= beam <= 8, topk >= beam");
+  hipLaunchKernelGGL(beam_step_kernel, dim3(C), dim3(256), 0, S(stream), part_stat, part_val,
+                     part_idx, beam, nblk, topk, first, stop, step_ctr, max_steps, scores, seq_len,
+                     stopped, tokens, tokens_tmp, kvrow, kvrow_tmp, Lmax, pos, next_tok);
+  ZS_LAUNCH_CHECK();
+  hipLaunchKernelGGL(beam_advance_kernel, dim3(1), dim3(1024), 0, S(stream), stopped, C * beam,
+                     step_ctr, max_steps, all_done);
+  ZS_LAUNCH_CHECK();
+  return 0;
+}

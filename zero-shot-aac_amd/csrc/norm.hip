@@ -1,0 +1,170 @@
+// Row-wise normalisation kernels: LayerNorm (GPT-2 ln_1/ln_2/ln_f, HTSAT norm1/norm2, mapper
+// norm1/norm2), PatchMerging gather + LayerNorm, final LayerNorm + mean-pool, L2 normalisation.
+// One wave per row, two-pass mean/variance in f32 (matches torch's LayerNorm numerics closely).
+#include "common.h"
+
+namespace zs {
+
+template <typename TO>
+__global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict__ x, int M, int C,
+                                                        int ldx, const int* __restrict__ rows,
+                                                        const float* __restrict__ w,
+                                                        const float* __restrict__ b, float eps,
+                                                        TO* __restrict__ y, int ldy) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= M) return;
+  const float* xr = x + (long)(rows ? rows[row] : row) * ldx;
+  float s = 0.f;
+  for (int c = lane; c < C; c += 64) s += xr[c];
+  const float mean = wave_sum(s) / C;
+  float v = 0.f;
+  for (int c = lane; c < C; c += 64) {
+    float d = xr[c] - mean;
+    v += d * d;
+  }
+  const float rstd = rsqrtf(wave_sum(v) / C + eps);
+  TO* yr = y + (long)row * ldy;
+  for (int c = lane; c < C; c += 64) stf(yr + c, (xr[c] - mean) * rstd * w[c] + b[c]);
+}
+
+// PatchMerging (htsat.py:492-511): out token (i,j) = LN([x(2i,2j), x(2i+1,2j), x(2i,2j+1),
+// x(2i+1,2j+1)]) over 4C.  One 256-thread block per output token.
+template <typename TO>
+__global__ __launch_bounds__(256) void patch_merge_ln_kernel(const float* __restrict__ x, int H,
+                                                             int W, int C,
+                                                             const float* __restrict__ w,
+                                                             const float* __restrict__ b,
+                                                             TO* __restrict__ y) {
+  __shared__ float red[4];
+  const int Ho = H / 2, Wo = W / 2;
+  const int tok = blockIdx.x;
+  const int bb = tok / (Ho * Wo), ij = tok % (Ho * Wo), i = ij / Wo, j = ij % Wo;
+  const int C4 = 4 * C;
+  auto src = [&](int c) -> float {
+    const int part = c / C, cc = c % C;
+    const int hh = 2 * i + (part & 1), ww = 2 * j + (part >> 1);
+    return x[(((long)bb * H + hh) * W + ww) * C + cc];
+  };
+  float s = 0.f;
+  for (int c = threadIdx.x; c < C4; c += 256) s += src(c);
+  const float mean = block_sum(s, red) / C4;
+  float v = 0.f;
+  for (int c = threadIdx.x; c < C4; c += 256) {
+    float d = src(c) - mean;
+    v += d * d;
+  }
+  const float rstd = rsqrtf(block_sum(v, red) / C4 + 1e-5f);
+  TO* yr = y + (long)tok * C4;
+  for (int c = threadIdx.x; c < C4; c += 256) stf(yr + c, (src(c) - mean) * rstd * w[c] + b[c]);
+}
+
+// final LayerNorm + mean over N tokens (htsat.py:830,838-847): one block per clip
+__global__ __launch_bounds__(256) void ln_meanpool_kernel(const float* __restrict__ x, int N, int C,
+                                                          const float* __restrict__ w,
+                                                          const float* __restrict__ b,
+                                                          float* __restrict__ out) {
+  extern __shared__ float acc[];  // [4 waves][C]
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  for (int c = threadIdx.x; c < 4 * C; c += 256) acc[c] = 0.f;
+  __syncthreads();
+  const float* xb = x + (long)blockIdx.x * N * C;
+  for (int t = wid; t < N; t += 4) {
+    const float* xr = xb + (long)t * C;
+    float s = 0.f;
+    for (int c = lane; c < C; c += 64) s += xr[c];
+    const float mean = wave_sum(s) / C;
+    float v = 0.f;
+    for (int c = lane; c < C; c += 64) {
+      float d = xr[c] - mean;
+      v += d * d;
+    }
+    const float rstd = rsqrtf(wave_sum(v) / C + 1e-5f);
+    for (int c = lane; c < C; c += 64) acc[wid * C + c] += (xr[c] - mean) * rstd * w[c] + b[c];
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < C; c += 256)
+    out[(long)blockIdx.x * C + c] = (acc[c] + acc[C + c] + acc[2 * C + c] + acc[3 * C + c]) / N;
+}
+
+__global__ __launch_bounds__(256) void l2norm_kernel(const float* __restrict__ x, int M, int C,
+                                                     float eps, float* __restrict__ y) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= M) return;
+  const float* xr = x + (long)row * C;
+  float s = 0.f;
+  for (int c = lane; c < C; c += 64) s += xr[c] * xr[c];
+  const float inv = 1.0f / fmaxf(sqrtf(wave_sum(s)), eps);
+  for (int c = lane; c < C; c += 64) y[(long)row * C + c] = xr[c] * inv;
+}
+
+template <typename TO>
+__global__ void cast_kernel(const float* __restrict__ x, long n, TO* __restrict__ y) {
+  long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) stf(y + i, x[i]);
+}
+
+}  // namespace zs
+
+using namespace zs;
+
+extern "C" int zs_layernorm(const float* x, int M, int C, int ldx, const int* rows, const float* w,
+                            const float* b, float eps, void* y, int ldy, int ydtype,
+                            void* stream) {
+  ZS_REQUIRE(M >= 0 && C > 0 && ldx >= C && ldy >= C, "zs_layernorm: bad shape");
+  if (M == 0) return 0;
+  dim3 grid(cdiv(M, 4));
+  if (ydtype == ZS_BF16)
+    hipLaunchKernelGGL(layernorm_kernel<bf16_t>, grid, dim3(256), 0, S(stream), x, M, C, ldx, rows, w,
+                       b, eps, (bf16_t*)y, ldy);
+  else
+    hipLaunchKernelGGL(layernorm_kernel<float>, grid, dim3(256), 0, S(stream), x, M, C, ldx, rows, w,
+                       b, eps, (float*)y, ldy);
+  ZS_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int zs_patch_merge_ln(const float* x, int B, int H, int W, int C, const float* ln_w,
+                                 const float* ln_b, void* y, int dtype, void* stream) {
+  ZS_REQUIRE(B > 0 && H % 2 == 0 && W % 2 == 0 && C > 0, "zs_patch_merge_ln: bad shape");
+  dim3 grid(B * (H / 2) * (W / 2));
+  if (dtype == ZS_BF16)
+    hipLaunchKernelGGL(patch_merge_ln_kernel<bf16_t>, grid, dim3(256), 0, S(stream), x, H, W, C,
+                       ln_w, ln_b, (bf16_t*)y);
+  else
+    hipLaunchKernelGGL(patch_merge_ln_kernel<float>, grid, dim3(256), 0, S(stream), x, H, W, C,
+                       ln_w, ln_b, (float*)y);
+  ZS_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int zs_ln_meanpool(const float* x, int B, int N, int C, const float* ln_w,
+                              const float* ln_b, float* out, void* stream) {
+  ZS_REQUIRE(B > 0 && N > 0 && C > 0 && C <= 4096, "zs_ln_meanpool: bad shape");
+  hipLaunchKernelGGL(ln_meanpool_kernel, dim3(B), dim3(256), 4 * C * sizeof(float), S(stream), x,
+                     N, C, ln_w, ln_b, out);
+  ZS_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int zs_l2norm_rows(const float* x, int M, int C, float eps, float* y, void* stream) {
+  ZS_REQUIRE(M >= 0 && C > 0, "zs_l2norm_rows: bad shape");
+  if (M == 0) return 0;
+  hipLaunchKernelGGL(l2norm_kernel, dim3(cdiv(M, 4)), dim3(256), 0, S(stream), x, M, C, eps, y);
+  ZS_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int zs_cast(const float* x, long n, void* y, int dtype, void* stream) {
+  ZS_REQUIRE(n >= 0, "zs_cast: n");
+  if (n == 0) return 0;
+  if (dtype == ZS_BF16)
+    hipLaunchKernelGGL(cast_kernel<bf16_t>, dim3(cdiv(n, 256)), dim3(256), 0, S(stream), x, n,
+                       (bf16_t*)y);
+  else
+    hipLaunchKernelGGL(cast_kernel<float>, dim3(cdiv(n, 256)), dim3(256), 0, S(stream), x, n,
+                       (float*)y);
+  ZS_LAUNCH_CHECK();
+  return 0;
+}

@@ -1,0 +1,369 @@
+"""Prefix mappers + GPT-2 decode (greedy / beam, KV cache) on the HIP kernels.
+
+Replaces, for a whole batch of clips at once:
+  * ``MLP`` / ``TransformerMapper`` (models/mapper.py) and ``clap_to_gpt``
+    (models/caption_model.py:315-329),
+  * ``get_prefix_tokens`` (gpt2_prefix_eval.py:271-278),
+  * ``generate2`` (gpt2_prefix_eval.py:161-222) and ``generate_beam`` (99-158).
+
+The reference decodes one clip at a time and recomputes the whole sequence every step
+(``model.gpt(inputs_embeds=generated)``); here every clip is a row of a batched KV-cache decode
+with per-row prompt lengths and positions.  Stop handling, tie rules and the beam arithmetic are
+kept.  The per-step work — embed, 12 blocks, ln_f, LM head + row reduction, step
+bookkeeping — runs on device and is captured once into a hipGraph (``torch.cuda.CUDAGraph``) that
+is replayed until every row has stopped; the host only checks a flag every ``chunk`` steps.
+"""
+from __future__ import annotations
+
+import math
+from typing import Dict, List, Optional, Tuple
+
+import torch
+
+from . import ops
+
+D, NH, HD, NL = 768, 12, 64, 12
+STOP_DOT, STOP_SPACE_DOT = 13, 764
+
+
+def _f32(t, dev):
+    return t.detach().to(device=dev, dtype=torch.float32).contiguous()
+
+
+def _w(t, dev, dtype):
+    return t.detach().to(device=dev, dtype=dtype).contiguous()
+
+
+# ------------------------------------------------------------------------------- mappers
+class MlpMapper:
+    """MLP((1024, 3840, 7680)) + Tanh (mapper.py:6-18): prefix [B,1024] -> soft [B, 10*768]."""
+
+    def __init__(self, sd, device, dtype, max_batch, prefix="clap_project.model."):
+        self.dtype = dtype
+        self.w0, self.b0 = _w(sd[prefix + "0.weight"], device, dtype), _f32(sd[prefix + "0.bias"], device)
+        self.w2, self.b2 = _w(sd[prefix + "2.weight"], device, dtype), _f32(sd[prefix + "2.bias"], device)
+        self.in_dim = self.w0.shape[1]
+        self.out_dim = self.w2.shape[0]
+        self.x_t = torch.empty(max_batch, self.in_dim, device=device, dtype=dtype)
+        self.h = torch.empty(max_batch, self.w0.shape[0], device=device, dtype=dtype)
+        self.out = torch.empty(max_batch, self.out_dim, device=device)
+        self.soft_ld = self.out_dim
+
+    def __call__(self, prefix):
+        B = prefix.shape[0]
+        ops.cast(prefix, self.x_t[:B])
+        ops.gemm(self.x_t[:B], self.w0, self.h[:B], bias=self.b0, act=ops.ACT_TANH)
+        ops.gemm(self.h[:B], self.w2, self.out[:B], bias=self.b2)
+        return self.out[:B]           # clip b's soft prefix at out + b*soft_ld
+
+
+class TransformerMapperEngine:
+    """TransformerMapper (mapper.py:125-139): linear -> concat prefix_const -> 8 pre-LN layers
+    (8 heads x 96, no q/kv bias, softmax over keys, ReLU MLP x2) -> rows clip_length: ."""
+
+    def __init__(self, sd, device, dtype, max_batch, prefix="clap_project.", clip_length=10,
+                 num_layers=8, heads=8):
+        self.dtype, self.cl, self.heads = dtype, clip_length, heads
+        self.lin_w = _w(sd[prefix + "linear.weight"], device, dtype)
+        self.lin_b = _f32(sd[prefix + "linear.bias"], device)
+        self.pc = _f32(sd[prefix + "prefix_const"], device)
+        self.pl = self.pc.shape[0]
+        self.L = clip_length + self.pl
+        self.layers = []
+        for i in range(num_layers):
+            p = prefix + f"transformer.layers.{i}."
+            self.layers.append({
+                "n1": (_f32(sd[p + "norm1.weight"], device), _f32(sd[p + "norm1.bias"], device)),
+                "q": _w(sd[p + "attn.to_queries.weight"], device, dtype),
+                "kv": _w(sd[p + "attn.to_keys_values.weight"], device, dtype),
+                "proj_w": _w(sd[p + "attn.project.weight"], device, dtype),
+                "proj_b": _f32(sd[p + "attn.project.bias"], device),
+                "n2": (_f32(sd[p + "norm2.weight"], device), _f32(sd[p + "norm2.bias"], device)),
+                "fc1_w": _w(sd[p + "mlp.fc1.weight"], device, dtype),
+                "fc1_b": _f32(sd[p + "mlp.fc1.bias"], device),
+                "fc2_w": _w(sd[p + "mlp.fc2.weight"], device, dtype),
+                "fc2_b": _f32(sd[p + "mlp.fc2.bias"], device),
+            })
+        B, L = max_batch, self.L
+        self.in_dim = self.lin_w.shape[1]
+        self.x_t = torch.empty(B, self.in_dim, device=device, dtype=dtype)
+        self.hs = torch.empty(B, L, D, device=device)
+        self.a = torch.empty(B * L, D, device=device, dtype=dtype)
+        self.q = torch.empty(B * L, D, device=device, dtype=dtype)
+        self.kv = torch.empty(B * L, 2 * D, device=device, dtype=dtype)
+        self.o = torch.empty(B * L, D, device=device, dtype=dtype)
+        self.mid = torch.empty(B * L, 2 * D, device=device, dtype=dtype)
+        self.soft_ld = L * D
+
+    def __call__(self, prefix):
+        B, L = prefix.shape[0], self.L
+        ops.cast(prefix, self.x_t[:B])
+        hs = self.hs[:B]
+        # linear(x).view(B, clip_length, D) written straight into rows 0..cl-1 of every clip
+        ops.gemm(self.x_t[:B], self.lin_w, hs.view(B, L * D)[:, :self.cl * D], bias=self.lin_b)
+        hs[:, self.cl:].copy_(self.pc.unsqueeze(0).expand(B, -1, -1))
+        x = hs.view(B * L, D)
+        scale = (D // self.heads) ** -0.5
+        for ly in self.layers:
+            M = B * L
+            ops.layernorm(x, *ly["n1"], out=self.a[:M])
+            ops.gemm(self.a[:M], ly["q"], self.q[:M])
+            ops.gemm(self.a[:M], ly["kv"], self.kv[:M])
+            kv = self.kv[:M]
+            ops.row_attention(self.q[:M], D, kv, kv[:, D:], 2 * D, B, L, self.heads, D // self.heads,
+                              False, scale, self.o[:M], D)
+            ops.gemm(self.o[:M], ly["proj_w"], x, bias=ly["proj_b"], residual=x)
+            ops.layernorm(x, *ly["n2"], out=self.a[:M])
+            ops.gemm(self.a[:M], ly["fc1_w"], self.mid[:M], bias=ly["fc1_b"], act=ops.ACT_RELU)
+            ops.gemm(self.mid[:M], ly["fc2_w"], x, bias=ly["fc2_b"], residual=x)
+        return hs.view(B, L * D)[:, self.cl * D:]   # clip b's soft prefix at base + b*soft_ld
+
+
+def build_mapper(sd, mapping_type, device, dtype, max_batch):
+    if mapping_type == "mlp":
+        return MlpMapper(sd, device, dtype, max_batch)
+    return TransformerMapperEngine(sd, device, dtype, max_batch)
+
+
+# ------------------------------------------------------------------------------- GPT-2
+class Gpt2Weights:
+    """HF GPT-2 small (``gpt.`` keys under ClapCaption_prompt): Conv1D [in,out] -> [out,in]."""
+
+    def __init__(self, sd, device, dtype, prefix="gpt.transformer."):
+        self.dtype = dtype
+        p = prefix
+        self.wte = _w(sd[p + "wte.weight"], device, dtype)
+        self.wpe = _w(sd[p + "wpe.weight"], device, dtype)
+        wn = torch.nn.functional.normalize(sd[p + "wte.weight"].float(), 2, 1)
+        self.wte_norm = _w(wn, device, dtype)          # predict_prompt.py:117-118
+        self.V = self.wte.shape[0]
+        self.layers = []
+        for i in range(NL):
+            h = p + f"h.{i}."
+            t = lambda k: _w(sd[h + k].t(), device, dtype)
+            self.layers.append({
+                "ln1": (_f32(sd[h + "ln_1.weight"], device), _f32(sd[h + "ln_1.bias"], device)),
+                "attn_w": t("attn.c_attn.weight"), "attn_b": _f32(sd[h + "attn.c_attn.bias"], device),
+                "proj_w": t("attn.c_proj.weight"), "proj_b": _f32(sd[h + "attn.c_proj.bias"], device),
+                "ln2": (_f32(sd[h + "ln_2.weight"], device), _f32(sd[h + "ln_2.bias"], device)),
+                "fc_w": t("mlp.c_fc.weight"), "fc_b": _f32(sd[h + "mlp.c_fc.bias"], device),
+                "mproj_w": t("mlp.c_proj.weight"), "mproj_b": _f32(sd[h + "mlp.c_proj.bias"], device),
+            })
+        self.lnf = (_f32(sd[p + "ln_f.weight"], device), _f32(sd[p + "ln_f.bias"], device))
+
+    def nbytes(self) -> int:
+        n = self.wte.numel() + self.wpe.numel()
+        for ly in self.layers:
+            n += sum(ly[k].numel() for k in ("attn_w", "proj_w", "fc_w", "mproj_w"))
+        return n * self.wte.element_size()
+
+
+class Gpt2Decoder:
+    """Batched GPT-2 prefix decoder with a KV cache.
+
+    ``max_rows`` decode rows (B for greedy, C*beam for beam), prompts up to ``max_prompt``
+    tokens, ``max_steps`` generated tokens (entry_length)."""
+
+    def __init__(self, w: Gpt2Weights, max_rows: int, max_prompt: int, max_steps: int = 67,
+                 max_prefill_rows: Optional[int] = None, topk: int = 8, chunk: int = 8,
+                 use_graph: bool = True):
+        self.w, self.dtype = w, w.dtype
+        dev = w.wte.device
+        self.dev = dev
+        self.R = max_rows
+        self.Rp = max_prefill_rows or max_rows
+        self.Pmax = max_prompt
+        self.max_steps = max_steps
+        self.topk, self.chunk, self.use_graph = topk, chunk, use_graph
+        # + chunk: a replayed graph chunk may run a few steps past entry_length (no-ops)
+        self.Lmax = max_prompt + max_steps + chunk + 1
+        dt = self.dtype
+        Mp = max(self.Rp * max_prompt, self.R)
+        self.x = torch.empty(Mp, D, device=dev)
+        self.h = torch.empty(Mp, D, device=dev, dtype=dt)
+        self.qkv = torch.empty(Mp, 3 * D, device=dev, dtype=dt)
+        self.att = torch.empty(Mp, D, device=dev, dtype=dt)
+        self.hid = torch.empty(Mp, 4 * D, device=dev, dtype=dt)
+        self.kc = [torch.empty(self.R, NH, self.Lmax, HD, device=dev, dtype=dt) for _ in range(NL)]
+        self.vc = [torch.empty(self.R, NH, self.Lmax, HD, device=dev, dtype=dt) for _ in range(NL)]
+        self.hf = torch.empty(max(self.R, self.Rp), D, device=dev, dtype=dt)
+        self.nblk = ops.lmhead_nblk(w.V)
+        R = max(self.R, self.Rp)
+        self.pstat = torch.empty(R, self.nblk, 2, device=dev)
+        self.pval = torch.empty(R, self.nblk, topk, device=dev)
+        self.pidx = torch.empty(R, self.nblk, topk, device=dev, dtype=torch.int32)
+        self.pval1 = torch.empty(R, self.nblk, 1, device=dev)
+        self.pidx1 = torch.empty(R, self.nblk, 1, device=dev, dtype=torch.int32)
+        # decode state
+        i32 = dict(device=dev, dtype=torch.int32)
+        self.pos = torch.zeros(self.R, **i32)
+        self.next_tok = torch.zeros(self.R, **i32)
+        self.done = torch.zeros(self.R, **i32)
+        self.out_ids = torch.zeros(self.R, max_steps, **i32)
+        self.out_len = torch.zeros(self.R, **i32)
+        self.step_ctr = torch.zeros(1, **i32)
+        self.all_done = torch.zeros(1, **i32)
+        self.plen = torch.zeros(self.Rp, **i32)
+        self.last_row = torch.zeros(self.Rp, **i32)
+        # beam state
+        self.scores = torch.zeros(self.R, device=dev)
+        self.seq_len = torch.ones(self.R, device=dev)
+        self.kvrow = torch.zeros(self.R, self.Lmax, **i32)
+        self.kvrow_tmp = torch.zeros(self.R, self.Lmax, **i32)
+        self.tok_tmp = torch.zeros(self.R, max_steps, **i32)
+        self.graphs: Dict[Tuple, torch.cuda.CUDAGraph] = {}
+
+    # ---------------------------------------------------------------- blocks
+    def _layers(self, M, attn_fn):
+        x = self.x[:M]
+        for l, ly in enumerate(self.w.layers):
+            h, qkv, att, hid = self.h[:M], self.qkv[:M], self.att[:M], self.hid[:M]
+            ops.layernorm(x, *ly["ln1"], out=h)
+            ops.gemm(h, ly["attn_w"], qkv, bias=ly["attn_b"])
+            attn_fn(l, qkv, att)
+            ops.gemm(att, ly["proj_w"], x, bias=ly["proj_b"], residual=x)
+            ops.layernorm(x, *ly["ln2"], out=h)
+            ops.gemm(h, ly["fc_w"], hid, bias=ly["fc_b"], act=ops.ACT_GELU_TANH)
+            ops.gemm(hid, ly["mproj_w"], x, bias=ly["mproj_b"], residual=x)
+
+    def prefill(self, B: int, Pmax: int, row_stride: int = 1):
+        """Runs the prompt rows already in ``self.x[:B*Pmax]`` (zs_gpt2_prefill_embed) through the
+        12 blocks, fills the KV cache (row b -> cache row b*row_stride) and leaves ln_f of every
+        row's last prompt position in ``self.hf[:B]``."""
+        M = B * Pmax
+
+        def attn(l, qkv, att):
+            ops.kv_write(qkv, B, Pmax, D, NH, self.kc[l], self.vc[l], self.Lmax, row_stride=row_stride)
+            ops.row_attention(qkv, 3 * D, qkv[:, D:], qkv[:, 2 * D:], 3 * D, B, Pmax, NH, HD, True,
+                              1.0 / math.sqrt(HD), att, D, lens=self.plen[:B])
+
+        self._layers(M, attn)
+        ops.layernorm(self.x, *self.w.lnf, out=self.hf[:B], rows=self.last_row[:B])
+
+    def _decode_forward(self, R, kvrow=None):
+        ops.embed_tokens(self.next_tok[:R], self.pos[:R], self.w.wte, self.w.wpe, self.x[:R])
+
+        def attn(l, qkv, att):
+            ops.decode_attention(qkv, R, D, NH, self.kc[l], self.vc[l], self.Lmax, self.pos[:R],
+                                 att, kvrow=kvrow)
+
+        self._layers(R, attn)
+        ops.layernorm(self.x[:R], *self.w.lnf, out=self.hf[:R])
+
+    def _greedy_step_body(self, R):
+        self._decode_forward(R)
+        ops.lmhead_topk(self.hf[:R], self.w.wte, 1, self.pstat, self.pval1, self.pidx1)
+        ops.greedy_step(self.pval1, self.pidx1, R, self.nblk, self.step_ctr, self.max_steps,
+                        STOP_DOT, STOP_SPACE_DOT, self.out_ids, self.out_len, self.done, self.pos,
+                        self.next_tok, self.all_done)
+
+    def _run_steps(self, key, body):
+        """Replays ``body`` (one decode step) ``chunk`` at a time until all_done."""
+        if self.use_graph:
+            g = self.graphs.get(key)
+            if g is None:
+                # warm up once on a side stream, then capture `chunk` steps
+                s = torch.cuda.Stream()
+                s.wait_stream(torch.cuda.current_stream())
+                saved = [t.clone() for t in self._state()]
+                with torch.cuda.stream(s):
+                    body()
+                torch.cuda.current_stream().wait_stream(s)
+                for t, v in zip(self._state(), saved):
+                    t.copy_(v)
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g):
+                    for _ in range(self.chunk):
+                        body()
+                self.graphs[key] = g
+            n = 0
+            while True:
+                g.replay()
+                n += self.chunk
+                if n >= self.max_steps or int(self.all_done.item()):
+                    break
+        else:
+            for _ in range(self.max_steps):
+                body()
+                if int(self.all_done.item()):
+                    break
+
+    def _state(self):
+        return [self.pos, self.next_tok, self.done, self.out_ids, self.out_len, self.step_ctr,
+                self.all_done, self.scores, self.seq_len, self.kvrow, self.kvrow_tmp, self.tok_tmp]
+
+    # ---------------------------------------------------------------- greedy (generate2)
+    def greedy(self, B: int, Pmax: int):
+        """After :meth:`prefill` (row_stride 1): generate2 for all B rows.
+        Returns (ids [B, max_steps] int32, lengths [B] int32) device tensors."""
+        R = B
+        ops.lmhead_topk(self.hf[:R], self.w.wte, 1, self.pstat, self.pval1, self.pidx1)
+        self.pos[:R].copy_(self.plen[:R] - 1)
+        for t in (self.done, self.out_len, self.step_ctr, self.all_done, self.out_ids):
+            t.zero_()
+        ops.greedy_step(self.pval1, self.pidx1, R, self.nblk, self.step_ctr, self.max_steps,
+                        STOP_DOT, STOP_SPACE_DOT, self.out_ids, self.out_len, self.done, self.pos,
+                        self.next_tok, self.all_done)
+        if self.max_steps > 1 and not int(self.all_done.item()):
+            self._run_steps(("greedy", R), lambda: self._greedy_step_body(R))
+        return self.out_ids[:R], self.out_len[:R]
+
+    # ---------------------------------------------------------------- beam (generate_beam)
+    def _beam_step_body(self, C, beam):
+        R = C * beam
+        self._decode_forward(R, kvrow=self.kvrow[:R])
+        ops.lmhead_topk(self.hf[:R], self.w.wte, self.topk, self.pstat, self.pval, self.pidx)
+        ops.beam_step(self.pstat, self.pval, self.pidx, C, beam, self.nblk, self.topk, False,
+                      STOP_DOT, self.step_ctr, self.max_steps, self.scores, self.seq_len,
+                      self.done, self.out_ids, self.tok_tmp, self.kvrow, self.kvrow_tmp, self.Lmax,
+                      self.pos, self.next_tok, self.all_done)
+
+    def beam(self, C: int, beam: int, Pmax: int):
+        """After :meth:`prefill` (C rows, row_stride=beam): generate_beam per clip.
+        Returns (tokens [C, beam, steps], seq_len [C, beam], scores [C, beam]) device tensors
+        (rows unsorted; the caller orders by scores/seq_len like the reference)."""
+        assert beam <= self.topk and C * beam <= self.R
+        R = C * beam
+        ops.lmhead_topk(self.hf[:C], self.w.wte, self.topk, self.pstat, self.pval, self.pidx)
+        for t in (self.done, self.step_ctr, self.all_done, self.out_ids, self.scores):
+            t.zero_()
+        self.seq_len.fill_(1.0)
+        self.pos[:R].view(C, beam)[:, 0].copy_(self.plen[:C])
+        ops.beam_step(self.pstat, self.pval, self.pidx, C, beam, self.nblk, self.topk, True,
+                      STOP_DOT, self.step_ctr, self.max_steps, self.scores, self.seq_len,
+                      self.done, self.out_ids, self.tok_tmp, self.kvrow, self.kvrow_tmp, self.Lmax,
+                      self.pos, self.next_tok, self.all_done)
+        if self.max_steps > 1 and not int(self.all_done.item()):
+            self._run_steps(("beam", C, beam), lambda: self._beam_step_body(C, beam))
+        return (self.out_ids[:R].view(C, beam, -1), self.seq_len[:R].view(C, beam),
+                self.scores[:R].view(C, beam))
+
+    # ---------------------------------------------------------------- get_prefix_tokens
+    def prefix_tokens(self, embed_rows: torch.Tensor, out_idx: torch.Tensor):
+        """argmax_n cos(embed_row, wte[n]) for every row of ``embed_rows`` [M, 768] f32."""
+        M = embed_rows.shape[0]
+        a = self.h[:M]
+        ops.cast(embed_rows, a)
+        ops.lmhead_topk(a, self.w.wte_norm, 1, self.pstat_big(M), self.pval_big(M), self.pidx_big(M),
+                        row_norm=True)
+        ops.argmax_finalize(self._pv_big, self._pi_big, M, self.nblk, out_idx)
+        return out_idx
+
+    def _ensure_big(self, M):
+        if getattr(self, "_big_M", 0) < M:
+            self._ps_big = torch.empty(M, self.nblk, 2, device=self.dev)
+            self._pv_big = torch.empty(M, self.nblk, 1, device=self.dev)
+            self._pi_big = torch.empty(M, self.nblk, 1, device=self.dev, dtype=torch.int32)
+            self._big_M = M
+
+    def pstat_big(self, M):
+        self._ensure_big(M)
+        return self._ps_big
+
+    def pval_big(self, M):
+        self._ensure_big(M)
+        return self._pv_big
+
+    def pidx_big(self, M):
+        self._ensure_big(M)
+        return self._pi_big

@@ -1,0 +1,226 @@
+"""Thin, validated torch-tensor wrappers over the C-ABI (one function per zs_* entry point).
+
+Tensors are device memory owned by the caller; every call is enqueued on the current torch
+stream (``torch.cuda.current_stream()``), performs no allocation and no synchronisation, and is
+therefore safe inside ``torch.cuda.graph`` capture.  Shape/dtype checks happen here on the host
+before the launch (the kernels assume them).
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+
+from ._lib import (ACT_GELU_ERF, ACT_GELU_TANH, ACT_NONE, ACT_RELU, ACT_TANH, ZS_BF16, ZS_F32,
+                   ZsError, call)
+
+__all__ = ["dt", "ACT_NONE", "ACT_GELU_ERF", "ACT_GELU_TANH", "ACT_RELU", "ACT_TANH"]
+
+
+def dt(t) -> int:
+    d = t.dtype if isinstance(t, torch.Tensor) else t
+    if d == torch.float32:
+        return ZS_F32
+    if d == torch.bfloat16:
+        return ZS_BF16
+    raise ZsError(f"unsupported dtype {d} (float32 / bfloat16)")
+
+
+def _p(t: Optional[torch.Tensor]):
+    if t is None:
+        return None
+    if not t.is_cuda:
+        raise ZsError("zsaac ops take device tensors (no CPU fallback)")
+    return t.data_ptr()
+
+
+def _s():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _need(cond, msg):
+    if not cond:
+        raise ZsError(msg)
+
+
+def _i32(t, name):
+    _need(t is None or t.dtype == torch.int32, f"{name} must be int32")
+
+
+# ---------------------------------------------------------------- front end
+def logmel(wav, tables, bn=None, out=None):
+    """wav [B,T] f32 -> [B, T//320+1, 64] f32 (log-mel, optionally bn0'd)."""
+    B, T = wav.shape
+    nf = T // 320 + 1
+    out = out if out is not None else torch.empty(B, nf, 64, device=wav.device)
+    bm, bv, bw, bb = (bn if bn is not None else (None, None, None, None))
+    call("zs_logmel", _p(wav), B, T, _p(tables["window"]), _p(tables["twiddle"]),
+         _p(tables["melW"]), _p(tables["mel_lo"]), _p(tables["mel_hi"]), _p(bm), _p(bv), _p(bw),
+         _p(bb), _p(out), _s())
+    return out
+
+
+def wav2img(logmel_t, out=None):
+    B, T_in, F = logmel_t.shape
+    _need(F == 64, "wav2img expects 64 mel bins")
+    out = out if out is not None else torch.empty(B, 256, 256, device=logmel_t.device)
+    call("zs_wav2img", _p(logmel_t), B, T_in, _p(out), _s())
+    return out
+
+
+def patch_embed(img, w, b, ln_w, ln_b, out=None):
+    B = img.shape[0]
+    out = out if out is not None else torch.empty(B * 4096, 96, device=img.device)
+    call("zs_patch_embed", _p(img), B, _p(w), _p(b), _p(ln_w), _p(ln_b), _p(out), _s())
+    return out
+
+
+# ---------------------------------------------------------------- generic
+def layernorm(x, w, b, out, eps=1e-5, rows=None, M=None):
+    C = x.shape[-1]
+    M = M if M is not None else (rows.numel() if rows is not None else x.numel() // C)
+    _i32(rows, "rows")
+    call("zs_layernorm", _p(x), M, C, x.stride(-2) if x.dim() > 1 else C, _p(rows), _p(w), _p(b),
+         float(eps), _p(out), out.stride(-2) if out.dim() > 1 else C, dt(out), _s())
+    return out
+
+
+def gemm(a, w, out, bias=None, residual=None, act=ACT_NONE, split_k=1, workspace=None, M=None):
+    """out = act(a @ w.T + bias) + residual;  a [M,K], w [N,K] (same dtype), out f32/bf16."""
+    K = a.shape[-1]
+    N = w.shape[0]
+    M = M if M is not None else a.numel() // K
+    _need(w.shape[1] == K and a.dtype == w.dtype, f"gemm: a{tuple(a.shape)} w{tuple(w.shape)}")
+    _need(K % 32 == 0, f"gemm: K={K} must be a multiple of 32")
+    lda = a.stride(-2) if a.dim() > 1 else K
+    ldo = out.stride(-2) if out.dim() > 1 else N
+    ldr = (residual.stride(-2) if residual.dim() > 1 else N) if residual is not None else 0
+    _need(bias is None or bias.dtype == torch.float32, "gemm: bias must be f32")
+    _need(residual is None or residual.dtype == torch.float32, "gemm: residual must be f32")
+    call("zs_gemm", M, N, K, dt(a), _p(a), lda, _p(w), w.stride(0), _p(bias), _p(residual), ldr,
+         _p(out), ldo, dt(out), act, split_k, _p(workspace), _s())
+    return out
+
+
+def l2norm(x, out=None, eps=1e-12):
+    out = out if out is not None else torch.empty_like(x)
+    C = x.shape[-1]
+    call("zs_l2norm_rows", _p(x), x.numel() // C, C, float(eps), _p(out), _s())
+    return out
+
+
+def cast(x, out):
+    _need(x.dtype == torch.float32 and x.numel() == out.numel(), "cast: f32 in, same numel")
+    call("zs_cast", _p(x), x.numel(), _p(out), dt(out), _s())
+    return out
+
+
+# ---------------------------------------------------------------- HTSAT
+def window_attention(qkv, B, H, W, C, heads, shift, rel_table, out, ws=8):
+    call("zs_window_attention", _p(qkv), B, H, W, C, heads, ws, shift, _p(rel_table), _p(out),
+         dt(qkv), _s())
+    return out
+
+
+def patch_merge_ln(x, B, H, W, C, ln_w, ln_b, out):
+    call("zs_patch_merge_ln", _p(x), B, H, W, C, _p(ln_w), _p(ln_b), _p(out), dt(out), _s())
+    return out
+
+
+def ln_meanpool(x, B, N, C, ln_w, ln_b, out):
+    call("zs_ln_meanpool", _p(x), B, N, C, _p(ln_w), _p(ln_b), _p(out), _s())
+    return out
+
+
+# ---------------------------------------------------------------- CNN14
+def conv3x3_bn_relu(x, B, H, W, Cin, w, Cout, scale, shift, out):
+    call("zs_conv3x3_bn_relu", _p(x), B, H, W, Cin, _p(w), Cout, _p(scale), _p(shift), _p(out),
+         dt(x), _s())
+    return out
+
+
+def avgpool2(x, B, H, W, C, out):
+    call("zs_avgpool2", _p(x), B, H, W, C, _p(out), dt(x), _s())
+    return out
+
+
+def cnn_head(x, B, H, W, C, out):
+    call("zs_cnn_head", _p(x), B, H, W, C, _p(out), dt(x), _s())
+    return out
+
+
+# ---------------------------------------------------------------- prompt / mapper
+def prompt_assemble(emb, labels, k, label_tok, label_len, hard_ids, hard_len, chosen=None):
+    B, D = emb.shape
+    L = labels.shape[0]
+    for t, n in ((label_tok, "label_tok"), (label_len, "label_len"), (hard_ids, "hard_ids"),
+                 (hard_len, "hard_len"), (chosen, "chosen")):
+        _i32(t, n)
+    call("zs_prompt_assemble", _p(emb), B, D, _p(labels), L, k, _p(label_tok), _p(label_len),
+         label_tok.shape[1], _p(hard_ids), hard_ids.shape[1], _p(hard_len), _p(chosen), _s())
+
+
+def row_attention(q, ldq, k, v, ldkv, B, L, heads, hd, causal, scale, out, ldo, lens=None):
+    _i32(lens, "lens")
+    call("zs_row_attention", _p(q), ldq, _p(k), _p(v), ldkv, B, L, _p(lens), heads, hd,
+         int(causal), float(scale), _p(out), ldo, dt(out), _s())
+    return out
+
+
+# ---------------------------------------------------------------- GPT-2
+def prefill_embed(hard_ids, hard_len, soft, soft_ld, n_soft, wte, wpe, B, Pmax, embed, x, plen,
+                  last_row):
+    D = wte.shape[1]
+    call("zs_gpt2_prefill_embed", _p(hard_ids), _p(hard_len), hard_ids.shape[1], _p(soft),
+         soft_ld, n_soft, _p(wte), _p(wpe), B, Pmax, D, _p(embed), _p(x), _p(plen),
+         _p(last_row), dt(wte), _s())
+
+
+def kv_write(qkv, R, n, D, heads, kc, vc, Lmax, pos0=None, row_stride=1):
+    call("zs_kv_write", _p(qkv), R, n, D, heads, _p(pos0), row_stride, _p(kc), _p(vc), Lmax,
+         dt(qkv), _s())
+
+
+def decode_attention(qkv, R, D, heads, kc, vc, Lmax, pos, out, kvrow=None):
+    call("zs_decode_attention", _p(qkv), R, D, heads, _p(kc), _p(vc), Lmax, _p(pos), _p(kvrow),
+         _p(out), dt(qkv), _s())
+    return out
+
+
+def embed_tokens(tok, pos, wte, wpe, x, R=None):
+    R = R if R is not None else tok.numel()
+    call("zs_embed_tokens", _p(tok), _p(pos), _p(wte), _p(wpe), R, wte.shape[1], _p(x), dt(wte),
+         _s())
+    return x
+
+
+def lmhead_nblk(V: int) -> int:
+    return call("zs_lmhead_nblk", V)
+
+
+def lmhead_topk(a, w, topk, part_stat, part_val, part_idx, row_norm=False, M=None):
+    K = a.shape[-1]
+    M = M if M is not None else a.numel() // K
+    _need(a.dtype == w.dtype and w.shape[1] == K, "lmhead: dtype/shape mismatch")
+    call("zs_lmhead_topk", M, K, w.shape[0], dt(a), _p(a), a.stride(-2) if a.dim() > 1 else K,
+         _p(w), topk, int(row_norm), _p(part_stat), _p(part_val), _p(part_idx), _s())
+
+
+def argmax_finalize(part_val, part_idx, M, nblk, idx):
+    call("zs_argmax_finalize", _p(part_val), _p(part_idx), M, nblk, _p(idx), _s())
+    return idx
+
+
+def greedy_step(part_val, part_idx, R, nblk, step_ctr, max_steps, stop0, stop1, out_ids, out_len,
+                done, pos, next_tok, all_done):
+    call("zs_greedy_step", _p(part_val), _p(part_idx), R, nblk, _p(step_ctr), max_steps, stop0,
+         stop1, _p(out_ids), _p(out_len), _p(done), _p(pos), _p(next_tok), _p(all_done), _s())
+
+
+def beam_step(part_stat, part_val, part_idx, C, beam, nblk, topk, first, stop, step_ctr,
+              max_steps, scores, seq_len, stopped, tokens, tokens_tmp, kvrow, kvrow_tmp, Lmax,
+              pos, next_tok, all_done):
+    call("zs_beam_step", _p(part_stat), _p(part_val), _p(part_idx), C, beam, nblk, topk,
+         int(first), stop, _p(step_ctr), max_steps, _p(scores), _p(seq_len), _p(stopped),
+         _p(tokens), _p(tokens_tmp), _p(kvrow), _p(kvrow_tmp), Lmax, _p(pos), _p(next_tok),
+         _p(all_done), _s())

@@ -1,0 +1,140 @@
+"""End-to-end batched caption pipeline (the hot path of BASELINE.json ``north_star``):
+
+  wav [B, 320000] --zs_logmel(+bn0)--> HTSAT/CNN14 --audio_proj, L2--> CLAP emb [B,1024]
+  --zs_prompt_assemble--> hard prompt ids --normalize_prefix--> mapper --prefill_embed-->
+  GPT-2 prefill (KV cache) --get_prefix_tokens--> greedy (generate2) or beam (generate_beam)
+  --> token ids [B, <=67] (+ lengths), all on one GPU, one stream.
+
+What the reference does per clip in Python (predict_prompt.py:129-148 over the dataset of
+dataset/dataset.py:441-453 fed by data_handing/embeddings_generator.py:44-73) is done here for a
+batch of clips.  Multi-GPU sharding and the token-id all-gather live in zsaac/dist.py.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import List, Optional, Sequence
+
+import numpy as np
+import torch
+
+from . import ops
+from .decoder import Gpt2Decoder, Gpt2Weights, build_mapper
+from .encoder import AudioEncoder
+
+
+@dataclass
+class CaptionConfig:
+    encoder: str = "htsat"            # "htsat" | "cnn14"
+    mapping_type: str = "mlp"         # "mlp" | "transformer"
+    dtype: torch.dtype = torch.bfloat16
+    batch: int = 64
+    sound_effect_num: int = 3
+    normalize_prefix: bool = True
+    prefix_length: int = 10
+    entry_length: int = 67
+    beam: int = 0                     # 0 -> greedy generate2, else generate_beam(beam_size)
+    prefix_tokens: bool = True        # also compute get_prefix_tokens (predict_prompt.py:137)
+    use_graph: bool = True
+
+
+@dataclass
+class CaptionBatch:
+    ids: torch.Tensor          # greedy: [B, steps] int32; beam: [B, beam, steps]
+    lengths: torch.Tensor      # greedy: [B] int32; beam: [B, beam] f32 seq_len
+    scores: Optional[torch.Tensor]
+    hard_ids: torch.Tensor     # [B, h_cap] int32 (0-padded)
+    hard_len: torch.Tensor     # [B]
+    plen: torch.Tensor         # [B] prompt length H + 10
+    prefix_ids: Optional[torch.Tensor]   # [B, Pmax] int32 get_prefix_tokens ids
+    clap_emb: torch.Tensor     # [B, 1024]
+
+    def captions(self) -> List[List[int]]:
+        """Per clip: the reference's output token list (beam: best beam first)."""
+        if self.scores is None:
+            ids, ln = self.ids.cpu().numpy(), self.lengths.cpu().numpy()
+            return [ids[b, :ln[b]].tolist() for b in range(ids.shape[0])]
+        return [beams[0] for beams in self.beams()]
+
+    def beams(self) -> List[List[List[int]]]:
+        ids = self.ids.cpu().numpy()
+        ln = self.lengths.cpu().numpy()
+        sc = self.scores.cpu().numpy()
+        out = []
+        for c in range(ids.shape[0]):
+            avg = sc[c] / ln[c]                       # scores / seq_lengths (line 153)
+            order = np.argsort(-avg, kind="stable")   # scores.argsort(descending=True)
+            out.append([ids[c, i, :int(ln[c, i])].tolist() for i in order])
+        return out
+
+    def prefix_token_lists(self) -> List[List[int]]:
+        pid, pl = self.prefix_ids.cpu().numpy(), self.plen.cpu().numpy()
+        return [pid[b, :pl[b]].tolist() for b in range(pid.shape[0])]
+
+
+class CaptionPipeline:
+    """Weights from reference-keyed state dicts; all buffers sized for ``cfg.batch`` clips."""
+
+    def __init__(self, caption_sd, audio_sd, label_table: torch.Tensor,
+                 label_tokens: Sequence[Sequence[int]], cfg: CaptionConfig = CaptionConfig(),
+                 device="cuda"):
+        self.cfg = cfg
+        dev = torch.device(device)
+        self.dev = dev
+        B = cfg.batch
+        self.encoder = AudioEncoder(audio_sd, cfg.encoder, cfg.dtype, B, dev) if audio_sd else None
+        self.labels = label_table.to(device=dev, dtype=torch.float32).contiguous()
+        mt = max(len(t) for t in label_tokens)
+        lt = np.zeros((len(label_tokens), mt), dtype=np.int32)
+        for i, t in enumerate(label_tokens):
+            lt[i, :len(t)] = t
+        self.label_tok = torch.from_numpy(lt).to(dev)
+        self.label_len = torch.tensor([len(t) for t in label_tokens], dtype=torch.int32, device=dev)
+        k = cfg.sound_effect_num
+        # longest possible hard prompt: "There are" + k labels + (k-1) commas + " in this audio."
+        self.h_cap = 2 + k * mt + max(k - 1, 0) + 4 if k > 0 else 7
+        self.Pmax = self.h_cap + cfg.prefix_length
+        self.mapper = build_mapper(caption_sd, cfg.mapping_type, dev, cfg.dtype, B)
+        self.gpt = Gpt2Weights(caption_sd, dev, cfg.dtype)
+        beam = max(cfg.beam, 1)
+        self.decoder = Gpt2Decoder(self.gpt, B * beam, self.Pmax, cfg.entry_length,
+                                   max_prefill_rows=B, use_graph=cfg.use_graph)
+        i32 = dict(device=dev, dtype=torch.int32)
+        self.hard_ids = torch.zeros(B, self.h_cap, **i32)
+        self.hard_len = torch.zeros(B, **i32)
+        self.prefix = torch.empty(B, 1024, device=dev)
+        self.embed = torch.empty(B * self.Pmax, 768, device=dev)
+        self.prefix_ids = torch.zeros(B * self.Pmax, **i32)
+
+    def caption_wav(self, wav: torch.Tensor) -> CaptionBatch:
+        assert self.encoder is not None, "no audio encoder weights"
+        return self.caption_emb(self.encoder.encode(wav))
+
+    def caption_emb(self, emb: torch.Tensor) -> CaptionBatch:
+        """From CLAP audio embeddings [B, 1024] (the pickle's ``audio_embedding``)."""
+        cfg, B, Pmax = self.cfg, emb.shape[0], self.Pmax
+        assert B <= cfg.batch
+        ops.prompt_assemble(emb, self.labels, cfg.sound_effect_num, self.label_tok, self.label_len,
+                            self.hard_ids[:B], self.hard_len[:B])
+        prefix = self.prefix[:B]
+        if cfg.normalize_prefix:
+            ops.l2norm(emb, out=prefix)               # dataset.py:448-449
+        else:
+            prefix.copy_(emb)
+        soft = self.mapper(prefix)
+        dec = self.decoder
+        ops.prefill_embed(self.hard_ids[:B], self.hard_len[:B], soft, self.mapper.soft_ld,
+                          cfg.prefix_length, self.gpt.wte, self.gpt.wpe, B, Pmax,
+                          self.embed[:B * Pmax], dec.x, dec.plen, dec.last_row)
+        prefix_ids = None
+        if cfg.prefix_tokens:
+            dec.prefix_tokens(self.embed[:B * Pmax], self.prefix_ids[:B * Pmax])
+            prefix_ids = self.prefix_ids[:B * Pmax].view(B, Pmax)
+        if cfg.beam:
+            dec.prefill(B, Pmax, row_stride=cfg.beam)
+            ids, ln, sc = dec.beam(B, cfg.beam, Pmax)
+        else:
+            dec.prefill(B, Pmax)
+            ids, ln = dec.greedy(B, Pmax)
+            sc = None
+        return CaptionBatch(ids, ln, sc, self.hard_ids[:B], self.hard_len[:B], dec.plen[:B],
+                            prefix_ids, emb)
