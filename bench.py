@@ -1,0 +1,247 @@
+#!/usr/bin/env python3
+"""Benchmark of the zero-shot audio-captioning hot path on MI355X (BASELINE.json metric):
+
+    audio clips/sec end-to-end (encode + mapper + GPT-2 decode), Clotho-eval bs=64
+
+Workload (BASELINE.json configs[1], "C2"): synthetic 10 s / 32 kHz waveforms (randn*0.1, clipped)
+already resident in HBM -> STFT/log-mel + bn0 -> HTSAT -> audio_proj + L2 -> sound-effect hard
+prompt -> MLP mapper -> GPT-2 small prefill + get_prefix_tokens + greedy generate2
+(entry_length 67, stop ids 13/764), bf16 operands / f32 accumulation, batch 64 clips per GPU.
+One "step" = one batch of 64 clips through the whole path on every rank, plus the RCCL
+all-gather of the batch's generated token ids (the only collective).  Weights are
+seeded random init at the reference architecture (no checkpoints offline).
+
+    python bench.py [--gpus N --steps K --warmup W]
+    torchrun --nproc-per-node N bench.py --gpus N ...      (one process per GPU, RCCL)
+
+Rank 0 prints ONE JSON line.  Besides the contract fields it carries
+  roofline:     the dominant kernel (GPT-2 decode MLP up-projection GEMM, M=64: HBM-bound
+                weight stream) — algorithmic bytes per launch / its average duration, timed live
+                with HIP events on the stream it runs on;
+  cpu_baseline: the oracle (reference semantics: batch 1, full recompute, fp32) on a bounded
+                sample of the same workload, timed on this host's CPU (rank 0, N=1 only).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "zero-shot-aac_amd"))
+
+import torch  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+GPT2_KW = dict(seed=0, std=0.1, emb_std=0.1, stop_boost=2.0)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--batch", type=int, default=64)
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "f32"])
+    ap.add_argument("--encoder", default="htsat", choices=["htsat", "cnn14"])
+    ap.add_argument("--mapper", default="mlp", choices=["mlp", "transformer"])
+    ap.add_argument("--beam", type=int, default=0)
+    ap.add_argument("--entry-length", type=int, default=67)
+    ap.add_argument("--cpu-baseline-clips", type=int, default=2)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--stages", action="store_true", help="also report per-stage ms (extra syncs)")
+    return ap.parse_args()
+
+
+def dist_setup(args):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))   # RCCL on ROCm
+    else:
+        torch.cuda.set_device(0)
+    return world, rank, local
+
+
+def build(args, device):
+    from zsaac import synthetic as S
+    from zsaac.pipeline import CaptionConfig, CaptionPipeline
+    dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
+    csd = S.gpt2_state_dict(**GPT2_KW)
+    csd.update(S.mlp_mapper_state_dict(1) if args.mapper == "mlp" else S.transformer_mapper_state_dict(2))
+    if args.encoder == "htsat":
+        asd = S.htsat_state_dict(3)
+        asd.update(S.audio_proj_state_dict(5, audio_width=768))
+    else:
+        asd = S.cnn14_state_dict(4)
+        asd.update(S.audio_proj_state_dict(5, audio_width=2048))
+    cfg = CaptionConfig(encoder=args.encoder, mapping_type=args.mapper, dtype=dtype, batch=args.batch,
+                        beam=args.beam, entry_length=args.entry_length)
+    pipe = CaptionPipeline(csd, asd, S.label_table(), S.label_token_table(), cfg, device=device)
+    return pipe, csd, asd
+
+
+def kernel_roofline(pipe, reps=200):
+    """Average duration of the dominant kernel — the decode-step MLP up-projection GEMM
+    (c_fc: out[64,3072] = gelu_new(h[64,768] @ W[3072,768]^T + b), HBM-bound on W) — measured
+    with HIP events on its own stream over `reps` back-to-back launches captured in a graph.
+    Algorithmic bytes per launch = W + A + bias + out (SURVEY §8d per-unit: 2 B per weight)."""
+    from zsaac import ops
+    dec = pipe.decoder
+    ly = pipe.gpt.layers[0]
+    M = pipe.cfg.batch
+    h, hid = dec.h[:M], dec.hid[:M]
+    W, b = ly["fc_w"], ly["fc_b"]
+    N, K = W.shape
+    es = W.element_size()
+    algo_bytes = N * K * es + M * K * es + N * 4 + M * N * es
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        for _ in range(3):
+            ops.gemm(h, W, hid, bias=b, act=ops.ACT_GELU_TANH)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s):
+            for _ in range(reps):
+                ops.gemm(h, W, hid, bias=b, act=ops.ACT_GELU_TANH)
+        g.replay()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(s)
+        for _ in range(5):
+            g.replay()
+        e1.record(s)
+    e1.synchronize()
+    avg_s = e0.elapsed_time(e1) / 1e3 / (5 * reps)
+    achieved = algo_bytes / avg_s / 1e9
+    return {"kernel": "gemm_skinny_kernel<bf16> decode c_fc [64x768]x[768x3072] +gelu_new",
+            "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+            "avg_launch_us": round(avg_s * 1e6, 3), "algo_bytes_per_launch": algo_bytes}
+
+
+def cpu_baseline(args, csd, asd, n_clips):
+    """Oracle = reference semantics (batch 1 per clip, full-sequence recompute every step, fp32)
+    on `n_clips` clips of the same synthetic workload, on this host's CPU."""
+    sys.path.insert(0, ROOT)
+    from oracle import audio as A, caption as OC, frontend as OF
+    from zsaac import synthetic as S
+    threads = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    table, lt = S.label_table(), S.label_token_table()
+    wav = S.synthetic_waveforms(n_clips, seed=777)
+    t0 = time.perf_counter()
+    ntok = 0
+    with torch.no_grad():
+        for i in range(n_clips):
+            lm = OF.logmel(wav[i:i + 1])
+            if args.encoder == "htsat":
+                feat = A.htsat_embedding(lm, asd)
+            else:
+                feat = A.cnn14_embedding(lm, asd)
+            emb = A.audio_project(feat, asd)
+            idx = OC.sound_effect_choice(emb, table, 3)[0].tolist()
+            hard = torch.tensor([OC.prompt_ids(idx, lt)])
+            pe = OC.clap_to_gpt(torch.nn.functional.normalize(emb, dim=-1)[None], hard, csd,
+                                args.mapper)
+            OC.prefix_tokens(pe, csd)
+            if args.beam:
+                OC.generate_beam(pe, csd, beam_size=args.beam, entry_length=args.entry_length)
+            else:
+                ntok += len(OC.generate2(pe, csd, entry_length=args.entry_length))
+    dt = time.perf_counter() - t0
+    return {"value": round(n_clips / dt, 4), "unit": "clips/s", "cores": threads, "kind": "port",
+            "sample": f"{n_clips} clips of the same workload, batch 1, full recompute per step "
+                      f"(reference semantics), fp32, {ntok} tokens, {dt:.1f} s"}
+
+
+def main():
+    args = parse()
+    world, rank, local = dist_setup(args)
+    device = torch.device("cuda", local)
+    from zsaac import synthetic as S
+    pipe, csd, asd = build(args, device)
+    B = args.batch
+    # input pool resident in HBM before timing: distinct synthetic clips per step and rank
+    pool = []
+    g = torch.Generator(device=device).manual_seed(1234 + rank)
+    for _ in range(min(4, args.steps + args.warmup)):
+        pool.append((torch.randn(B, 320000, device=device, generator=g) * 0.1).clamp_(-1, 1))
+    ids_all = None
+    if world > 1:
+        import torch.distributed as dist
+        steps_w = args.entry_length
+        ids_all = torch.empty(world * B * steps_w, dtype=torch.int32, device=device)
+        len_all = torch.empty(world * B, dtype=torch.int32, device=device)
+
+    def step(i):
+        out = pipe.caption_wav(pool[i % len(pool)])
+        if world > 1:
+            import torch.distributed as dist
+            ids = out.ids if out.ids.dim() == 2 else out.ids[:, 0]
+            dist.all_gather_into_tensor(ids_all, ids.contiguous().view(-1))
+            dist.all_gather_into_tensor(len_all, out.hard_len.contiguous())
+        return out
+
+    for i in range(args.warmup):
+        step(i)
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    ntok = 0
+    last = None
+    for i in range(args.steps):
+        last = step(args.warmup + i)
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt], device=device, dtype=torch.float64)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        dt = float(t)
+    if last is not None:
+        ntok = int(last.lengths.sum()) if last.scores is None else int(last.lengths[:, 0].sum())
+    clips = world * B * args.steps
+    res = {
+        "metric": "audio clips/sec end-to-end (encode+mapper+GPT-2 decode), Clotho-eval bs=64",
+        "value": round(clips / dt, 2),
+        "unit": "clips/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(dt / args.steps * 1e3, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "bf16" if args.dtype == "bf16" else "f32",
+        "data": "synthetic 10 s / 32 kHz waveforms (randn*0.1) resident in HBM; seeded random-init "
+                "weights at the reference architecture (no checkpoints offline)",
+        "config": {"workload": "C2 Clotho-eval: STFT/log-mel + " + args.encoder.upper() + " + "
+                               + args.mapper + " mapper + GPT-2 small "
+                               + ("greedy generate2" if not args.beam else f"beam {args.beam}")
+                               + f", entry_length {args.entry_length}, + get_prefix_tokens",
+                   "batch_per_gpu": B, "global_batch": B * world,
+                   "parallelism": f"dp{world} (clip-sharded, RCCL all-gather of token ids)",
+                   "tokens_last_batch_rank0": ntok},
+    }
+    if rank == 0 and not args.no_roofline:
+        res["roofline"] = kernel_roofline(pipe)
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and args.cpu_baseline_clips > 0:
+        res["cpu_baseline"] = cpu_baseline(args, csd, asd, args.cpu_baseline_clips)
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

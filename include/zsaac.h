@@ -34,6 +34,7 @@ enum zs_act { ZS_ACT_NONE = 0, ZS_ACT_GELU_ERF = 1, ZS_ACT_GELU_TANH = 2, ZS_ACT
 int zs_version(void);                         /* ABI version, bumped on signature change */
 int zs_last_error(char* buf, size_t len);     /* copies the thread-local last error message */
 int zs_device_arch(char* buf, size_t len);    /* gcnArchName of the current device (e.g. gfx950) */
+int zs_tune_set(const char* key, int value);  /* tuning knobs, e.g. "skinny_mode" (0 fence, 1 sc1) */
 
 /* ------------------------------------------------------------------ audio front end
  * zs_logmel: retrieval/models/feature_extractor.py:34-38 (torchlibrosa Spectrogram +
@@ -68,11 +69,16 @@ int zs_layernorm(const float* x, int M, int C, int ldx, const int* rows, const f
 /* zs_gemm: out[m][n] = act(sum_k A[m][k] * W[n][k] + bias[n]) + residual[m][n]
  *   A [M][lda], W [N][ldw] in `dtype`; bias f32 or NULL; residual f32 [M][ldr] or NULL (may alias
  *   out); out in `out_dtype`.  K % 32 == 0.  split_k > 1 needs a f32 workspace of
- *   split_k*M*N floats (deterministic slab reduction, no atomics).
+ *   split_k*M*N floats (deterministic slab reduction, no atomics).  split_k == 0 = auto: for
+ *   M <= 64 (decode) a weight-streaming split-K kernel whose last-arriving workgroup reduces the
+ *   slabs in order (deterministic); it needs a workspace of zs_gemm_workspace_floats(M,N,K) floats
+ *   ZEROED ONCE at allocation (its tile counters re-arm themselves).
  *   Replaces every nn.Linear / HF Conv1D on the path (Conv1D weights are repacked to [N][K]). */
 int zs_gemm(int M, int N, int K, int dtype, const void* A, int lda, const void* W, int ldw,
             const float* bias, const float* residual, int ldr, void* out, int ldo, int out_dtype,
             int act, int split_k, float* workspace, void* stream);
+
+int zs_gemm_workspace_floats(int M, int N, int K);
 
 /* zs_l2norm_rows: y = x / max(||x||_2, eps) per row (F.normalize, ase_model.py:54). in-place ok */
 int zs_l2norm_rows(const float* x, int M, int C, float eps, float* y, void* stream);

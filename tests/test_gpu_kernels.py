@@ -48,6 +48,40 @@ def test_gemm(cuda, dtype, M, N, K):
     assert torch.equal(out2, out3)
 
 
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("M,N,K", [(64, 2304, 768), (64, 768, 768), (64, 3072, 768), (64, 768, 3072),
+                                   (50, 7680, 3840), (3, 1024, 768), (64, 100, 64)])
+def test_gemm_skinny(cuda, dtype, M, N, K):
+    """M <= 64 auto mode: weight-streaming split-K with in-kernel last-arriver reduction."""
+    from zsaac import ops
+    ops.reserve_skinny_workspace(cuda, M, N, K)
+    g = torch.Generator(device="cuda").manual_seed(N + K)
+    a = torch.randn(M, K, device=cuda, generator=g).to(dtype)
+    w = torch.randn(N, K, device=cuda, generator=g).div(math.sqrt(K)).to(dtype)
+    bias = torch.randn(N, device=cuda, generator=g)
+    res = torch.randn(M, N, device=cuda, generator=g)
+    ref = a.float() @ w.float().t() + bias
+    tol = 1e-4 if dtype == torch.float32 else 1e-2
+    out = torch.empty(M, N, device=cuda)
+    ops.gemm(a, w, out, bias=bias, act=ops.ACT_GELU_TANH)
+    assert _rel(out, torch.nn.functional.gelu(ref, approximate="tanh")) < tol
+    out2 = res.clone()
+    ops.gemm(a, w, out2, bias=bias, residual=out2)
+    assert _rel(out2, ref + res) < tol
+    outs = []
+    for _ in range(3):    # counters re-arm themselves; result is bitwise deterministic
+        o = torch.empty(M, N, device=cuda, dtype=dtype)
+        ops.gemm(a, w, o, bias=bias)
+        outs.append(o)
+    assert torch.equal(outs[0], outs[1]) and torch.equal(outs[1], outs[2])
+    if dtype == torch.float32:
+        ai = torch.randint(-3, 4, (M, K), device=cuda, generator=g).float()
+        wi = torch.randint(-3, 4, (N, K), device=cuda, generator=g).float()
+        oi = torch.empty(M, N, device=cuda)
+        ops.gemm(ai, wi, oi)
+        assert torch.equal(oi, ai @ wi.t())
+
+
 def test_gemm_f32_exact_small_ints(cuda):
     """f32 mode with small integers is exact: catches any fragment/layout transposition."""
     from zsaac import ops
@@ -282,3 +316,20 @@ def test_conv3x3(cuda):
         p = torch.empty(B, H // 2, W // 2, cout, device=cuda)
         ops.avgpool2(out, B, H, W, cout, p)
         assert _rel(p.cpu().permute(0, 3, 1, 2), torch.nn.functional.avg_pool2d(ref, 2)) < 1e-5
+
+
+def test_gemm_skinny_shared_workspace(cuda):
+    """Shapes with different tile counts share one workspace: slabs of one GEMM must never be
+    read as another GEMM's tile counters (regression)."""
+    from zsaac import ops
+    shapes = [(64, 2304, 768), (3, 7680, 3840), (64, 768, 3072), (3, 3840, 1024), (64, 768, 768)]
+    for M, N, K in shapes:
+        ops.reserve_skinny_workspace(cuda, M, N, K)
+    g = torch.Generator(device="cuda").manual_seed(9)
+    for rep in range(2):
+        for M, N, K in shapes:
+            a = torch.randn(M, K, device=cuda, generator=g)
+            w = torch.randn(N, K, device=cuda, generator=g) / math.sqrt(K)
+            out = torch.empty(M, N, device=cuda)
+            ops.gemm(a, w, out)
+            assert _rel(out, a @ w.t()) < 1e-4, (rep, M, N, K)

@@ -1,0 +1,90 @@
+#!/usr/bin/env python3
+"""Micro-benchmarks of individual zsaac kernels on the GPU (graph-replayed back-to-back launches,
+HIP events on the launching stream).  Used to choose kernel variants; not part of the product.
+
+    python tools/mbench.py gemm      # decode-shaped GEMMs, skinny modes vs tiled vs torch
+    python tools/mbench.py attn      # decode attention
+"""
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "zero-shot-aac_amd"))
+
+import torch  # noqa: E402
+
+
+def timeit(fn, reps=100, rounds=5):
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        for _ in range(3):
+            fn()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s):
+            for _ in range(reps):
+                fn()
+        g.replay()
+        ts = []
+        for _ in range(rounds):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(s)
+            g.replay()
+            e1.record(s)
+            e1.synchronize()
+            ts.append(e0.elapsed_time(e1) * 1e3 / reps)
+    torch.cuda.current_stream().wait_stream(s)
+    ts.sort()
+    return ts[len(ts) // 2]
+
+
+def bench_gemm():
+    from zsaac import ops
+    from zsaac._lib import call
+    dev = torch.device("cuda", 0)
+    shapes = [(64, 2304, 768, "qkv"), (64, 768, 768, "proj"), (64, 3072, 768, "fc"),
+              (64, 768, 3072, "mproj"), (64, 7680, 3840, "mlp2"), (64, 50304, 768, "lm-ish")]
+    for M, N, K, name in shapes:
+        ops.reserve_skinny_workspace(dev, M, N, K)
+        a = torch.randn(M, K, device=dev).bfloat16()
+        w = (torch.randn(N, K, device=dev) * 0.02).bfloat16()
+        b = torch.randn(N, device=dev)
+        out = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+        wbytes = N * K * 2
+        res = {}
+        for mode in (0, 1):
+            call("zs_tune_set", b"skinny_mode", mode)
+            res[f"skinny{mode}"] = timeit(lambda: ops.gemm(a, w, out, bias=b))
+        call("zs_tune_set", b"skinny_mode", 1)
+        res["tiled"] = timeit(lambda: ops.gemm(a, w, out, bias=b, split_k=1))
+        res["torch"] = timeit(lambda: torch.nn.functional.linear(a, w, b.bfloat16()))
+        print(f"{name:6s} M{M} N{N} K{K} W={wbytes / 1e6:.1f}MB  " +
+              "  ".join(f"{k}={v:7.2f}us ({wbytes / v / 1e3:6.0f} GB/s)" for k, v in res.items()),
+              flush=True)
+
+
+def bench_attn():
+    from zsaac import ops
+    dev = torch.device("cuda", 0)
+    R, D, H = 64, 768, 12
+    for L, Lmax in ((30, 96), (60, 96), (90, 96)):
+        qkv = torch.randn(R, 3 * D, device=dev).bfloat16()
+        kc = torch.randn(R, H, Lmax, 64, device=dev).bfloat16()
+        vc = torch.randn_like(kc)
+        pos = torch.full((R,), L - 1, device=dev, dtype=torch.int32)
+        out = torch.empty(R, D, device=dev, dtype=torch.bfloat16)
+        t = timeit(lambda: ops.decode_attention(qkv, R, D, H, kc, vc, Lmax, pos, out))
+        byts = R * L * D * 2 * 2
+        print(f"decode_attn L={L}: {t:7.2f}us  KV {byts / 1e6:.1f}MB  {byts / t / 1e3:6.0f} GB/s")
+    x = torch.randn(64, 768, device=dev)
+    w, bb = torch.randn(768, device=dev), torch.randn(768, device=dev)
+    y = torch.empty(64, 768, device=dev, dtype=torch.bfloat16)
+    print(f"layernorm 64x768: {timeit(lambda: ops.layernorm(x, w, bb, out=y)):7.2f}us")
+    print(f"empty-ish (cast 64 elems): {timeit(lambda: ops.cast(x[:1, :64], y[:1, :64])):7.2f}us")
+
+
+if __name__ == "__main__":
+    which = sys.argv[1:] or ["gemm", "attn"]
+    for wname in which:
+        {"gemm": bench_gemm, "attn": bench_attn}[wname]()

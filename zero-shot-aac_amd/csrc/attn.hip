@@ -124,7 +124,86 @@ __global__ __launch_bounds__(64) void row_attn_kernel(const T* __restrict__ q, i
 }
 
 // ------------------------------------------------------------------ GPT-2 decode attention
-// grid (R, heads), block 64 (hd == 64): append k/v of the new token at pos[r], attend 0..pos[r].
+// grid (R, heads), block 256 (hd == 64): append k/v of the new token at pos[r], then attend
+// 0..pos[r].  The row's K block ([pos][64], contiguous per (row, head) in the cache) is staged
+// into LDS with 16-byte coalesced loads, one thread per key computes its score from LDS, the
+// softmax is a block reduction, and P.V reads each V row coalesced (wave w takes keys j = w mod 4).
+template <typename T>
+__global__ __launch_bounds__(256) void decode_attn4_kernel(const T* __restrict__ qkv, int D,
+                                                           int heads, T* __restrict__ kc,
+                                                           T* __restrict__ vc, int Lmax,
+                                                           const int* __restrict__ pos,
+                                                           const int* __restrict__ kvrow,
+                                                           T* __restrict__ out) {
+  constexpr int HD = 64, KP = HD + 1;
+  constexpr int EPC = 16 / sizeof(T);          // elements per 16-byte chunk
+  constexpr int CPR = HD / EPC;                // chunks per key row
+  extern __shared__ float sm[];
+  float* qs = sm;                    // [64]
+  float* vnew = sm + 64;             // [64]
+  float* red = sm + 128;             // [16]
+  float* po = sm + 144;              // [4][64] partial outputs
+  float* sc = sm + 144 + 256;        // [Lmax] scores
+  float* ks = sc + Lmax;             // [Lmax][65] keys
+  const int r = blockIdx.x, h = blockIdx.y, tid = threadIdx.x;
+  const int lane = tid & 63, wid = tid >> 6;
+  const int p = min(pos[r], Lmax - 1);
+  const T* row = qkv + (long)r * 3 * D + h * HD;
+  const long base_rh = ((long)r * heads + h) * Lmax;
+  if (tid < HD) {
+    qs[tid] = ldf(row + tid) * 0.125f;              // q * 1/sqrt(64) (exact power of two)
+    const T kn = row[D + tid], vn = row[2 * D + tid];
+    kc[(base_rh + p) * HD + tid] = kn;
+    vc[(base_rh + p) * HD + tid] = vn;
+    ks[p * KP + tid] = Cvt<T>::to_f(kn);
+    vnew[tid] = Cvt<T>::to_f(vn);
+  }
+  // stage keys 0..p-1
+  for (int c = tid; c < p * CPR; c += 256) {
+    const int j = c / CPR, part = c % CPR;
+    const int pr = kvrow ? kvrow[(long)r * Lmax + j] : r;
+    const uint4 u = *reinterpret_cast<const uint4*>(
+        kc + ((((long)pr * heads + h) * Lmax + j) * HD) + part * EPC);
+    const T* e = reinterpret_cast<const T*>(&u);
+#pragma unroll
+    for (int q = 0; q < EPC; ++q) ks[j * KP + part * EPC + q] = Cvt<T>::to_f(e[q]);
+  }
+  __syncthreads();
+  float mx = -INFINITY;
+  for (int j = tid; j <= p; j += 256) {
+    float s = 0.f;
+#pragma unroll 16
+    for (int e = 0; e < HD; ++e) s += qs[e] * ks[j * KP + e];
+    sc[j] = s;
+    mx = fmaxf(mx, s);
+  }
+  mx = wave_max(mx);
+  if (lane == 0) red[wid] = mx;
+  __syncthreads();
+  mx = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  float sum = 0.f;
+  for (int j = tid; j <= p; j += 256) {
+    const float e = expf(sc[j] - mx);
+    sc[j] = e;
+    sum += e;
+  }
+  sum = wave_sum(sum);
+  if (lane == 0) red[4 + wid] = sum;
+  __syncthreads();
+  const float inv = 1.0f / (red[4] + red[5] + red[6] + red[7]);
+  float o = 0.f;
+  for (int j = wid; j < p; j += 4) {
+    const int pr = kvrow ? kvrow[(long)r * Lmax + j] : r;
+    o += sc[j] * ldf(vc + (((long)pr * heads + h) * Lmax + j) * HD + lane);
+  }
+  if (wid == (p & 3)) o += sc[p] * vnew[lane];
+  po[wid * 64 + lane] = o;
+  __syncthreads();
+  if (wid == 0)
+    stf(out + (long)r * D + h * HD + lane,
+        (po[lane] + po[64 + lane] + po[128 + lane] + po[192 + lane]) * inv);
+}
+
 template <typename T>
 __global__ __launch_bounds__(64) void decode_attn_kernel(const T* __restrict__ qkv, int D,
                                                          int heads, T* __restrict__ kc,
@@ -264,6 +343,19 @@ extern "C" int zs_decode_attention(const void* qkv, int R, int D, int heads, voi
              "zs_decode_attention: head_dim must be 64");
   ZS_REQUIRE(Lmax > 0 && Lmax <= 4096, "zs_decode_attention: Lmax");
   dim3 grid(R, heads);
+  if (Lmax <= 512) {
+    const size_t smem = (400 + 66 * (size_t)Lmax) * sizeof(float);
+    if (dtype == ZS_BF16)
+      hipLaunchKernelGGL(decode_attn4_kernel<bf16_t>, grid, dim3(256), smem, S(stream),
+                         (const bf16_t*)qkv, D, heads, (bf16_t*)kc, (bf16_t*)vc, Lmax, pos, kvrow,
+                         (bf16_t*)out);
+    else
+      hipLaunchKernelGGL(decode_attn4_kernel<float>, grid, dim3(256), smem, S(stream),
+                         (const float*)qkv, D, heads, (float*)kc, (float*)vc, Lmax, pos, kvrow,
+                         (float*)out);
+    ZS_LAUNCH_CHECK();
+    return 0;
+  }
   const size_t smem = (128 + (size_t)Lmax) * sizeof(float);
   if (dtype == ZS_BF16)
     hipLaunchKernelGGL(decode_attn_kernel<bf16_t>, grid, dim3(64), smem, S(stream),

@@ -64,6 +64,7 @@ __global__ __launch_bounds__(256) void logmel_kernel(
 // bicubic (A = -0.75, align_corners = True) along time T_in -> 1024, identity along the 64 mels,
 // then fold: img[r = chunk*64 + mel][c] = resized[t = chunk*256 + c][mel]
 __global__ void wav2img_kernel(const float* __restrict__ in, int T_in, float* __restrict__ img) {
+#pragma clang fp contract(off)   // torch rounds scale*t before `- floor` and each weight term
   const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
   const int c = e % 256, r = (e / 256) % 256, b = e / 65536;
   const int chunk = r / 64, mel = r % 64;

@@ -218,6 +218,11 @@ __global__ __launch_bounds__(256) void lmhead_kernel(int M, int K, int V, const 
 
 using namespace zs;
 
+extern "C" __attribute__((visibility("hidden"))) int zs_gemm_skinny_internal(
+    int M, int N, int K, int dtype, const void* A, int lda, const void* W, int ldw,
+    const float* bias, const float* residual, int ldr, void* out, int ldo, int out_dtype, int act,
+    float* workspace, void* stream);
+
 extern "C" int zs_gemm(int M, int N, int K, int dtype, const void* A, int lda, const void* W,
                        int ldw, const float* bias, const float* residual, int ldr, void* out,
                        int ldo, int out_dtype, int act, int split_k, float* workspace,
@@ -225,9 +230,15 @@ extern "C" int zs_gemm(int M, int N, int K, int dtype, const void* A, int lda, c
   ZS_REQUIRE(M >= 0 && N > 0 && K > 0, "zs_gemm: bad shape M=%d N=%d K=%d", M, N, K);
   ZS_REQUIRE(K % BK == 0, "zs_gemm: K=%d must be a multiple of 32", K);
   ZS_REQUIRE(lda % 8 == 0 && ldw % 8 == 0, "zs_gemm: lda/ldw must be multiples of 8");
-  ZS_REQUIRE(split_k >= 1, "zs_gemm: split_k >= 1");
+  ZS_REQUIRE(split_k >= 0, "zs_gemm: split_k >= 0");
   ZS_REQUIRE(dtype == ZS_F32 || dtype == ZS_BF16, "zs_gemm: dtype");
   if (M == 0) return 0;
+  if (split_k == 0) {   // auto: weight-streaming skinny kernel for decode-sized M
+    if (M <= 64 && K % 64 == 0 && workspace != nullptr)
+      return zs_gemm_skinny_internal(M, N, K, dtype, A, lda, W, ldw, bias, residual, ldr, out,
+                                     ldo, out_dtype, act, workspace, stream);
+    split_k = 1;
+  }
   GemmArgs g{M, N, K, lda, ldw, ldr, ldo, A, W, bias, residual, out, out_dtype, act, 1, K, workspace};
   if (split_k > 1) {
     int kps = cdiv(cdiv(K, split_k), BK) * BK;

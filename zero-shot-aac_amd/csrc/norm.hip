@@ -28,6 +28,53 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict_
   for (int c = lane; c < C; c += 64) stf(yr + c, (xr[c] - mean) * rstd * w[c] + b[c]);
 }
 
+// Single-pass variant for C % 4 == 0, C <= 256*NV: one wave per row, the row held in registers
+// as float4 (one 16-byte load per lane per 256 elements), mean and variance from registers.
+template <typename TO, int NV>
+__global__ __launch_bounds__(256) void layernorm_reg_kernel(const float* __restrict__ x, int M,
+                                                            int C, int ldx,
+                                                            const int* __restrict__ rows,
+                                                            const float* __restrict__ w,
+                                                            const float* __restrict__ b, float eps,
+                                                            TO* __restrict__ y, int ldy) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= M) return;
+  const float4* xr = reinterpret_cast<const float4*>(x + (long)(rows ? rows[row] : row) * ldx);
+  const int C4 = C >> 2;
+  float4 v[NV];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c = lane + 64 * i;
+    v[i] = c < C4 ? xr[c] : make_float4(0.f, 0.f, 0.f, 0.f);
+    s += (v[i].x + v[i].y) + (v[i].z + v[i].w);
+  }
+  const float mean = wave_sum(s) / C;
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    if (lane + 64 * i < C4) {
+      const float a = v[i].x - mean, bb = v[i].y - mean, c = v[i].z - mean, d = v[i].w - mean;
+      q += (a * a + bb * bb) + (c * c + d * d);
+    }
+  }
+  const float rstd = rsqrtf(wave_sum(q) / C + eps);
+  TO* yr = y + (long)row * ldy;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c = lane + 64 * i;
+    if (c < C4) {
+      const float4 ww = reinterpret_cast<const float4*>(w)[c];
+      const float4 bv = reinterpret_cast<const float4*>(b)[c];
+      stf(yr + 4 * c + 0, (v[i].x - mean) * rstd * ww.x + bv.x);
+      stf(yr + 4 * c + 1, (v[i].y - mean) * rstd * ww.y + bv.y);
+      stf(yr + 4 * c + 2, (v[i].z - mean) * rstd * ww.z + bv.z);
+      stf(yr + 4 * c + 3, (v[i].w - mean) * rstd * ww.w + bv.w);
+    }
+  }
+}
+
 // PatchMerging (htsat.py:492-511): out token (i,j) = LN([x(2i,2j), x(2i+1,2j), x(2i,2j+1),
 // x(2i+1,2j+1)]) over 4C.  One 256-thread block per output token.
 template <typename TO>
@@ -115,6 +162,19 @@ extern "C" int zs_layernorm(const float* x, int M, int C, int ldx, const int* ro
   ZS_REQUIRE(M >= 0 && C > 0 && ldx >= C && ldy >= C, "zs_layernorm: bad shape");
   if (M == 0) return 0;
   dim3 grid(cdiv(M, 4));
+  if (C % 4 == 0 && ldx % 4 == 0 && C <= 1024) {
+    const int nv = cdiv(C / 4, 64);
+#define LNR(TO, NV_)                                                                           \
+  hipLaunchKernelGGL((layernorm_reg_kernel<TO, NV_>), grid, dim3(256), 0, S(stream), x, M, C,    \
+                     ldx, rows, w, b, eps, (TO*)y, ldy)
+#define LNR_T(TO) do { if (nv == 1) LNR(TO, 1); else if (nv == 2) LNR(TO, 2); \
+                       else if (nv == 3) LNR(TO, 3); else LNR(TO, 4); } while (0)
+    if (ydtype == ZS_BF16) LNR_T(bf16_t); else LNR_T(float);
+#undef LNR_T
+#undef LNR
+    ZS_LAUNCH_CHECK();
+    return 0;
+  }
   if (ydtype == ZS_BF16)
     hipLaunchKernelGGL(layernorm_kernel<bf16_t>, grid, dim3(256), 0, S(stream), x, M, C, ldx, rows, w,
                        b, eps, (bf16_t*)y, ldy);

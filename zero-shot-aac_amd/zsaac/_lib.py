@@ -29,11 +29,13 @@ SIGNATURES = {
     "zs_version": [],
     "zs_last_error": [C.c_char_p, C.c_size_t],
     "zs_device_arch": [C.c_char_p, C.c_size_t],
+    "zs_tune_set": [C.c_char_p, I],
     "zs_logmel": [P, I, I, P, P, P, P, P, P, P, P, P, P, P],
     "zs_wav2img": [P, I, I, P, P],
     "zs_patch_embed": [P, I, P, P, P, P, P, P],
     "zs_layernorm": [P, I, I, I, P, P, P, F, P, I, I, P],
     "zs_gemm": [I, I, I, I, P, I, P, I, P, P, I, P, I, I, I, I, P, P],
+    "zs_gemm_workspace_floats": [I, I, I],
     "zs_l2norm_rows": [P, I, I, F, P, P],
     "zs_window_attention": [P, I, I, I, I, I, I, I, P, P, I, P],
     "zs_patch_merge_ln": [P, I, I, I, I, P, P, P, I, P],

@@ -48,6 +48,9 @@ class MlpMapper:
         self.h = torch.empty(max_batch, self.w0.shape[0], device=device, dtype=dtype)
         self.out = torch.empty(max_batch, self.out_dim, device=device)
         self.soft_ld = self.out_dim
+        if max_batch <= 64:
+            ops.reserve_skinny_workspace(device, max_batch, self.w0.shape[0], self.in_dim)
+            ops.reserve_skinny_workspace(device, max_batch, self.out_dim, self.w2.shape[1])
 
     def __call__(self, prefix):
         B = prefix.shape[0]
@@ -212,6 +215,10 @@ class Gpt2Decoder:
         self.kvrow_tmp = torch.zeros(self.R, self.Lmax, **i32)
         self.tok_tmp = torch.zeros(self.R, max_steps, **i32)
         self.graphs: Dict[Tuple, torch.cuda.CUDAGraph] = {}
+        for M in {self.R, self.Rp}:
+            if M <= 64:
+                for N, K in ((3 * D, D), (D, D), (4 * D, D), (D, 4 * D)):
+                    ops.reserve_skinny_workspace(dev, M, N, K)
 
     # ---------------------------------------------------------------- blocks
     def _layers(self, M, attn_fn):

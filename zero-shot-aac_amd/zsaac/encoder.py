@@ -131,6 +131,9 @@ class AudioEncoder:
         self.feat_t = torch.empty(B, width, device=dev, dtype=dtype)
         self.proj_h = torch.empty(B, 1024, device=dev, dtype=dtype)
         self.emb = torch.empty(B, 1024, device=dev)
+        if B <= 64:
+            ops.reserve_skinny_workspace(dev, B, 1024, width)
+            ops.reserve_skinny_workspace(dev, B, 1024, 1024)
         if kind == "htsat":
             M = B * 4096
             self.img = torch.empty(B, 256, 256, device=dev)

@@ -85,13 +85,48 @@ def layernorm(x, w, b, out, eps=1e-5, rows=None, M=None):
     return out
 
 
-def gemm(a, w, out, bias=None, residual=None, act=ACT_NONE, split_k=1, workspace=None, M=None):
-    """out = act(a @ w.T + bias) + residual;  a [M,K], w [N,K] (same dtype), out f32/bf16."""
+_SKINNY_WS = {}
+
+
+def _devkey(device):
+    dev = torch.device(device)
+    if dev.index is None:
+        dev = torch.device(dev.type, torch.cuda.current_device())
+    return dev
+
+
+def reserve_skinny_workspace(device, M, N, K):
+    """Allocate (once, zeroed, before any graph capture) the workspace the auto-mode skinny GEMM
+    (M <= 64) needs for this shape; shared by every skinny GEMM on the device's stream order."""
+    need = call("zs_gemm_workspace_floats", M, N, K)
+    dev = _devkey(device)
+    cur = _SKINNY_WS.get(dev)
+    if need and (cur is None or cur.numel() < need):
+        if cur is not None:
+            _RETIRED.append(cur)     # a captured graph may still reference it: never free
+        _SKINNY_WS[dev] = torch.zeros(max(need, 4 << 20), device=dev)
+    return _SKINNY_WS.get(dev)
+
+
+_RETIRED = []
+
+
+def gemm(a, w, out, bias=None, residual=None, act=ACT_NONE, split_k=0, workspace=None, M=None):
+    """out = act(a @ w.T + bias) + residual;  a [M,K], w [N,K] (same dtype), out f32/bf16.
+    split_k=0 (auto): M <= 64 uses the weight-streaming skinny kernel when a workspace was
+    reserved for the device (reserve_skinny_workspace), else the tiled kernel."""
     K = a.shape[-1]
     N = w.shape[0]
     M = M if M is not None else a.numel() // K
     _need(w.shape[1] == K and a.dtype == w.dtype, f"gemm: a{tuple(a.shape)} w{tuple(w.shape)}")
     _need(K % 32 == 0, f"gemm: K={K} must be a multiple of 32")
+    if split_k == 0:
+        if workspace is None and M <= 64:
+            workspace = _SKINNY_WS.get(_devkey(a.device))
+            if workspace is not None and call("zs_gemm_workspace_floats", M, N, K) > workspace.numel():
+                workspace = None
+        if workspace is None:
+            split_k = 1
     lda = a.stride(-2) if a.dim() > 1 else K
     ldo = out.stride(-2) if out.dim() > 1 else N
     ldr = (residual.stride(-2) if residual.dim() > 1 else N) if residual is not None else 0
