@@ -248,8 +248,27 @@ def gen_prompt():
     del enc
 
 
+def gen_keys():
+    """Reference state-dict key -> shape maps of the modules the drop-ins mirror."""
+    import json
+    from models.caption_model import ClapCaption_prompt
+    from retrieval.models.audio_encoder import AudioEncoder
+    out = {}
+    for mt in ("mlp", "transformer"):
+        m = ClapCaption_prompt(10, clip_length=10, prefix_size=1024, num_layers=8, mapping_type=mt)
+        out[f"ClapCaption_prompt[{mt}]"] = {k: list(v.shape) for k, v in m.state_dict().items()}
+    for kind in ("transformer", "cnn"):
+        enc = AudioEncoder(_audio_config(kind))
+        out[f"AudioEncoder[{kind}]"] = {k: list(v.shape) for k, v in enc.state_dict().items()}
+    path = os.path.join(HERE, "state_dict_keys.json")
+    with open(path, "w") as f:
+        json.dump(out, f, indent=0, sort_keys=True)
+    print("wrote", path)
+
+
+
 ALL = {"prompt": gen_prompt, "mappers": gen_mappers, "htsat": gen_htsat, "cnn14": gen_cnn14,
-       "beam": gen_beam, "c1": gen_c1}
+       "beam": gen_beam, "c1": gen_c1, "keys": gen_keys}
 
 if __name__ == "__main__":
     torch.set_num_threads(os.cpu_count() or 8)
@@ -259,3 +278,4 @@ if __name__ == "__main__":
         print(f"[{name}]", flush=True)
         ALL[name]()
         print(f"[{name}] done in {time.time() - t:.1f}s", flush=True)
+

@@ -1,0 +1,108 @@
+"""Drop-in for the reference's decoding entry points (gpt2_prefix_eval.py):
+
+    generate2(model, tokenizer, tokens=None, prompt=None, embed=None, entry_count=1,
+              entry_length=67, top_p=0.8, temperature=1., stop_token='.') -> str      (161-222)
+    generate_beam(model, tokenizer, beam_size=5, prompt=None, embed=None, entry_length=67,
+                  temperature=1., stop_token='.') -> list[str]                        (99-158)
+    get_prefix_tokens(prefix_embed, embeddings, tokenizer) -> (str,)                  (271-278)
+
+``model`` is a ClapCaption_prompt drop-in (anything whose ``.gpt`` is a
+zsaac.modules.ZsGPT2LMHeadModel); ``tokenizer`` is duck-typed (``encode``/``decode``).  Decoding
+runs on the MI355X kernels with a KV cache (the reference recomputes the whole sequence every
+step; identical math).  For throughput use the batched zsaac.pipeline.CaptionPipeline: these
+functions keep the reference's one-clip-per-call signature.
+
+Deviations (documented): temperature must be 1 (the reference's only value on this
+path); a stop token emitted as the very first token returns that one-token caption (the reference
+crashes there: ``tokens.squeeze()`` is 0-d, gpt2_prefix_eval.py:218).
+"""
+from typing import List
+
+import torch
+import torch.nn.functional as nnf
+
+from zsaac import ops
+from zsaac.modules import require_device
+
+__all__ = ["generate2", "generate_beam", "get_prefix_tokens"]
+
+
+def _decoder(model, embed, entry_length, beam):
+    require_device(embed, "generate")
+    if embed.shape[0] != 1:
+        raise ValueError("the reference decodes one clip per call (batch 1); use "
+                         "zsaac.pipeline.CaptionPipeline for batches")
+    P = embed.shape[1]
+    dec = model.gpt.engine(max(beam, 1), P, entry_length, embed.device)
+    w = dec.w
+    zeros = torch.zeros(1, 1, dtype=torch.int32, device=embed.device)
+    hl = torch.zeros(1, dtype=torch.int32, device=embed.device)
+    emb = embed.float().contiguous()
+    ops.prefill_embed(zeros, hl, emb, P * w.wte.shape[1], P, w.wte, w.wpe, 1, P, None, dec.x,
+                      dec.plen, dec.last_row)
+    return dec, P
+
+
+def _check_temperature(temperature):
+    if temperature != 1.0:
+        raise NotImplementedError("temperature != 1 is not supported on the HIP decode path")
+
+
+def generate2(model, tokenizer, tokens=None, prompt=None, embed=None, entry_count=1, entry_length=67,
+              top_p=0.8, temperature=1., stop_token: str = '.'):
+    """Greedy: the top-p filter never removes the highest-probability token, so the pick is the
+    argmax (gpt2_prefix_eval.py:194-212); stop after appending ``stop_token`` or 764 (' .')."""
+    _check_temperature(temperature)
+    if embed is None:
+        if tokens is None:
+            tokens = torch.tensor(tokenizer.encode(prompt)).unsqueeze(0)
+        dev = next(model.parameters()).device
+        embed = model.gpt.transformer.wte(tokens.to(dev))
+    stop = tokenizer.encode(stop_token)[0]
+    dec, P = _decoder(model, embed, entry_length, 1)
+    dec.prefill(1, P)
+    dec.stop0 = stop
+    ids, ln = dec.greedy(1, P)
+    out = ids[0, :int(ln[0])].tolist()
+    return tokenizer.decode(out)
+
+
+def generate_beam(model, tokenizer, beam_size: int = 5, prompt=None, embed=None, entry_length=67,
+                  temperature=1., stop_token: str = '.') -> List[str]:
+    """Length-normalised beam search with log(softmax) scores, stopped beams extended by id 0 at
+    zero cost; texts sorted by score/length descending (gpt2_prefix_eval.py:99-158)."""
+    _check_temperature(temperature)
+    if embed is None:
+        tokens = torch.tensor(tokenizer.encode(prompt)).unsqueeze(0)
+        dev = next(model.parameters()).device
+        embed = model.gpt.transformer.wte(tokens.to(dev))
+    stop = tokenizer.encode(stop_token)[0]
+    dec, P = _decoder(model, embed, entry_length, beam_size)
+    dec.prefill(1, P, row_stride=beam_size)
+    dec.stop0 = stop
+    ids, ln, sc = dec.beam(1, beam_size, P)
+    ids, ln, sc = ids[0].cpu(), ln[0].cpu(), sc[0].cpu()
+    texts = [tokenizer.decode(ids[i, :int(ln[i])].tolist()) for i in range(beam_size)]
+    order = (sc / ln).argsort(descending=True)
+    return [texts[i] for i in order]
+
+
+def get_prefix_tokens(prefix_embed, embeddings, tokenizer) -> str:
+    """argmax_n cos(prefix_embed[0, p], embeddings[n]) per position, decoded token by token and
+    joined; returns a 1-tuple like the reference (trailing comma at line 275)."""
+    require_device(prefix_embed, "get_prefix_tokens")
+    x = prefix_embed[0].float().contiguous()
+    M, K = x.shape
+    w = embeddings.float().contiguous() if embeddings.dtype != torch.bfloat16 else embeddings.contiguous()
+    a = x if w.dtype == torch.float32 else x.to(w.dtype)
+    V = w.shape[0]
+    nblk = ops.lmhead_nblk(V)
+    ps = torch.empty(M, nblk, 2, device=x.device)
+    pv = torch.empty(M, nblk, 1, device=x.device)
+    pi = torch.empty(M, nblk, 1, device=x.device, dtype=torch.int32)
+    ops.lmhead_topk(a, w, 1, ps, pv, pi, row_norm=True)
+    idx = torch.empty(M, device=x.device, dtype=torch.int32)
+    ops.argmax_finalize(pv, pi, M, nblk, idx)
+    prefix_tokens = [tokenizer.decode(int(t)) for t in idx.cpu()]
+    prefix_sentence = "".join(prefix_tokens),
+    return prefix_sentence

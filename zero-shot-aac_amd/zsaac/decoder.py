@@ -178,6 +178,7 @@ class Gpt2Decoder:
         self.Pmax = max_prompt
         self.max_steps = max_steps
         self.topk, self.chunk, self.use_graph = topk, chunk, use_graph
+        self.stop0, self.stop1 = STOP_DOT, STOP_SPACE_DOT   # generate2 stops on '.' and ' .'
         # + chunk: a replayed graph chunk may run a few steps past entry_length (no-ops)
         self.Lmax = max_prompt + max_steps + chunk + 1
         dt = self.dtype
@@ -261,7 +262,7 @@ class Gpt2Decoder:
         self._decode_forward(R)
         ops.lmhead_topk(self.hf[:R], self.w.wte, 1, self.pstat, self.pval1, self.pidx1)
         ops.greedy_step(self.pval1, self.pidx1, R, self.nblk, self.step_ctr, self.max_steps,
-                        STOP_DOT, STOP_SPACE_DOT, self.out_ids, self.out_len, self.done, self.pos,
+                        self.stop0, self.stop1, self.out_ids, self.out_len, self.done, self.pos,
                         self.next_tok, self.all_done)
 
     def _run_steps(self, key, body):
@@ -309,10 +310,10 @@ class Gpt2Decoder:
         for t in (self.done, self.out_len, self.step_ctr, self.all_done, self.out_ids):
             t.zero_()
         ops.greedy_step(self.pval1, self.pidx1, R, self.nblk, self.step_ctr, self.max_steps,
-                        STOP_DOT, STOP_SPACE_DOT, self.out_ids, self.out_len, self.done, self.pos,
+                        self.stop0, self.stop1, self.out_ids, self.out_len, self.done, self.pos,
                         self.next_tok, self.all_done)
         if self.max_steps > 1 and not int(self.all_done.item()):
-            self._run_steps(("greedy", R), lambda: self._greedy_step_body(R))
+            self._run_steps(("greedy", R, self.stop0, self.stop1), lambda: self._greedy_step_body(R))
         return self.out_ids[:R], self.out_len[:R]
 
     # ---------------------------------------------------------------- beam (generate_beam)
@@ -321,7 +322,7 @@ class Gpt2Decoder:
         self._decode_forward(R, kvrow=self.kvrow[:R])
         ops.lmhead_topk(self.hf[:R], self.w.wte, self.topk, self.pstat, self.pval, self.pidx)
         ops.beam_step(self.pstat, self.pval, self.pidx, C, beam, self.nblk, self.topk, False,
-                      STOP_DOT, self.step_ctr, self.max_steps, self.scores, self.seq_len,
+                      self.stop0, self.step_ctr, self.max_steps, self.scores, self.seq_len,
                       self.done, self.out_ids, self.tok_tmp, self.kvrow, self.kvrow_tmp, self.Lmax,
                       self.pos, self.next_tok, self.all_done)
 
@@ -337,11 +338,11 @@ class Gpt2Decoder:
         self.seq_len.fill_(1.0)
         self.pos[:R].view(C, beam)[:, 0].copy_(self.plen[:C])
         ops.beam_step(self.pstat, self.pval, self.pidx, C, beam, self.nblk, self.topk, True,
-                      STOP_DOT, self.step_ctr, self.max_steps, self.scores, self.seq_len,
+                      self.stop0, self.step_ctr, self.max_steps, self.scores, self.seq_len,
                       self.done, self.out_ids, self.tok_tmp, self.kvrow, self.kvrow_tmp, self.Lmax,
                       self.pos, self.next_tok, self.all_done)
         if self.max_steps > 1 and not int(self.all_done.item()):
-            self._run_steps(("beam", C, beam), lambda: self._beam_step_body(C, beam))
+            self._run_steps(("beam", C, beam, self.stop0), lambda: self._beam_step_body(C, beam))
         return (self.out_ids[:R].view(C, beam, -1), self.seq_len[:R].view(C, beam),
                 self.scores[:R].view(C, beam))
 

@@ -124,7 +124,8 @@ class AudioEncoder:
         else:
             raise ValueError(kind)
         self.width = width
-        self.proj = AudioProjWeights(sd, self.dev, dtype)
+        # audio_proj is optional: the bare HTSAT/CNN14 drop-ins return the encoder features
+        self.proj = AudioProjWeights(sd, self.dev, dtype) if "audio_proj.0.weight" in sd else None
         B, dev = max_batch, self.dev
         self.logmel = torch.empty(B, self.n_frames, 64, device=dev)
         self.feat = torch.empty(B, width, device=dev)
@@ -218,10 +219,13 @@ class AudioEncoder:
             self._htsat(B)
         else:
             self._cnn14(B)
+        if self.proj is None:
+            return self.feat[:B]
         return self.project(self.feat[:B])
 
     def project(self, feat):
         B = feat.shape[0]
+        assert self.proj is not None, "no audio_proj weights"
         ops.cast(feat, self.feat_t[:B])
         ops.gemm(self.feat_t[:B], self.proj.w0, self.proj_h[:B], bias=self.proj.b0, act=ops.ACT_RELU)
         ops.gemm(self.proj_h[:B], self.proj.w2, self.emb[:B], bias=self.proj.b2)

@@ -55,6 +55,16 @@ def hann_periodic(n=N_FFT) -> np.ndarray:
     return 0.5 - 0.5 * np.cos(2.0 * np.pi * k / n)
 
 
+def dft_conv_weights(n_fft=N_FFT):
+    """torchlibrosa STFT ``conv_real`` / ``conv_imag`` weights [n_fft//2+1, 1, n_fft] (the
+    windowed DFT rows), kept only so reference checkpoints load into the drop-in AudioFeature;
+    the kernel computes the same transform as an FFT."""
+    n = np.arange(n_fft)
+    W = np.exp(-2j * np.pi * np.outer(n, n[: n_fft // 2 + 1]) / n_fft) * hann_periodic(n_fft)[:, None]
+    return (torch.from_numpy(np.real(W).T.astype(np.float32))[:, None, :],
+            torch.from_numpy(np.imag(W).T.astype(np.float32))[:, None, :])
+
+
 def make_tables(device, melW: Optional[np.ndarray] = None) -> Dict[str, torch.Tensor]:
     """Device tables for zs_logmel.  ``melW`` [64, 513] overrides the computed filterbank."""
     mel = slaney_mel() if melW is None else np.asarray(melW, dtype=np.float32)
