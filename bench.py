@@ -7,9 +7,13 @@ Workload (BASELINE.json configs[1], "C2"): synthetic 10 s / 32 kHz waveforms (ra
 already resident in HBM -> STFT/log-mel + bn0 -> HTSAT -> audio_proj + L2 -> sound-effect hard
 prompt -> MLP mapper -> GPT-2 small prefill + get_prefix_tokens + greedy generate2
 (entry_length 67, stop ids 13/764), bf16 operands / f32 accumulation, batch 64 clips per GPU.
-One "step" = one batch of 64 clips through the whole path on every rank, plus the RCCL
-all-gather of the batch's generated token ids (the only collective).  Weights are
-seeded random init at the reference architecture (no checkpoints offline).
+One "step" = one batch of 64 clips through the whole path on every rank.  --inflight (default 4)
+independent bs=64 batches are decoded concurrently per GPU on separate HIP streams (pipeline
+twins sharing the weights, zsaac/pipeline.py ConcurrentRunner) — the batch size the reference
+evaluates with stays 64; the GPU just works on several such batches at once.  After the K timed
+steps, ONE RCCL all-gather of every batch's generated token ids + lengths (the only collective,
+SURVEY §8e) is inside the timed region.  Weights are seeded random init at the reference
+architecture (no checkpoints offline).
 
     python bench.py [--gpus N --steps K --warmup W]
     torchrun --nproc-per-node N bench.py --gpus N ...      (one process per GPU, RCCL)
@@ -41,14 +45,16 @@ GPT2_KW = dict(seed=0, std=0.1, emb_std=0.1, stop_boost=2.0)
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=16)
+    ap.add_argument("--warmup", type=int, default=4)
     ap.add_argument("--batch", type=int, default=64)
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "f32"])
     ap.add_argument("--encoder", default="htsat", choices=["htsat", "cnn14"])
     ap.add_argument("--mapper", default="mlp", choices=["mlp", "transformer"])
     ap.add_argument("--beam", type=int, default=0)
     ap.add_argument("--entry-length", type=int, default=67)
+    ap.add_argument("--inflight", type=int, default=4,
+                    help="independent bs=--batch batches decoding concurrently per GPU (streams)")
     ap.add_argument("--cpu-baseline-clips", type=int, default=2)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
@@ -125,6 +131,37 @@ def kernel_roofline(pipe, reps=200):
             "avg_launch_us": round(avg_s * 1e6, 3), "algo_bytes_per_launch": algo_bytes}
 
 
+def stage_times(pipe, wav, reps=3):
+    """Per-stage device time of one batch (events between stages; extra syncs, so outside the
+    timed region): front end + encoder + proj, prompt + mapper + prefill + prefix tokens, decode."""
+    from zsaac import ops
+    dec, cfg = pipe.decoder, pipe.cfg
+    B, Pmax = wav.shape[0], pipe.Pmax
+    out = {"encode": [], "prompt_mapper_prefill": [], "decode": []}
+    for _ in range(reps):
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+        ev[0].record()
+        emb = pipe.encoder.encode(wav)
+        ev[1].record()
+        ops.prompt_assemble(emb, pipe.labels, cfg.sound_effect_num, pipe.label_tok, pipe.label_len,
+                            pipe.hard_ids[:B], pipe.hard_len[:B])
+        soft = pipe.mapper(ops.l2norm(emb, out=pipe.prefix[:B]))
+        ops.prefill_embed(pipe.hard_ids[:B], pipe.hard_len[:B], soft, pipe.mapper.soft_ld,
+                          cfg.prefix_length, pipe.gpt.wte, pipe.gpt.wpe, B, Pmax,
+                          pipe.embed[:B * Pmax], dec.x, dec.plen, dec.last_row)
+        dec.prefix_tokens(pipe.embed[:B * Pmax], pipe.prefix_ids[:B * Pmax])
+        dec.prefill(B, Pmax)
+        ev[2].record()
+        dec.greedy(B, Pmax)
+        ev[3].record()
+        torch.cuda.synchronize()
+        for i, k in enumerate(out):
+            out[k].append(ev[i].elapsed_time(ev[i + 1]))
+    res = {k: round(sorted(v)[len(v) // 2], 3) for k, v in out.items()}
+    res["decode_steps"] = int(dec.step_ctr.item())
+    return res
+
+
 def cpu_baseline(args, csd, asd, n_clips):
     """Oracle = reference semantics (batch 1 per clip, full-sequence recompute every step, fp32)
     on `n_clips` clips of the same synthetic workload, on this host's CPU."""
@@ -172,33 +209,34 @@ def main():
     g = torch.Generator(device=device).manual_seed(1234 + rank)
     for _ in range(min(4, args.steps + args.warmup)):
         pool.append((torch.randn(B, 320000, device=device, generator=g) * 0.1).clamp_(-1, 1))
-    ids_all = None
-    if world > 1:
-        import torch.distributed as dist
-        steps_w = args.entry_length
-        ids_all = torch.empty(world * B * steps_w, dtype=torch.int32, device=device)
-        len_all = torch.empty(world * B, dtype=torch.int32, device=device)
+    from zsaac.pipeline import ConcurrentRunner
+    runner = ConcurrentRunner(pipe, max(1, args.inflight))
 
-    def step(i):
-        out = pipe.caption_wav(pool[i % len(pool)])
-        if world > 1:
+    def run(first, n):
+        """n batches through the runner (inflight batches decoding concurrently on separate
+        streams), then ONE RCCL all-gather of every batch's token ids + lengths in input order
+        (completion order is timing-dependent, so no per-batch collective)."""
+        outs = runner.run([pool[(first + i) % len(pool)] for i in range(n)])
+        if world > 1 and outs:
             import torch.distributed as dist
-            ids = out.ids if out.ids.dim() == 2 else out.ids[:, 0]
-            dist.all_gather_into_tensor(ids_all, ids.contiguous().view(-1))
-            dist.all_gather_into_tensor(len_all, out.hard_len.contiguous())
-        return out
+            ids = torch.cat([(o.ids if o.ids.dim() == 2 else o.ids[:, 0]).reshape(-1) for o in outs])
+            ln = torch.cat([(o.lengths if o.lengths.dim() == 1 else o.lengths[:, 0]).int() for o in outs])
+            ids_all = torch.empty(world * ids.numel(), dtype=ids.dtype, device=device)
+            len_all = torch.empty(world * ln.numel(), dtype=ln.dtype, device=device)
+            dist.all_gather_into_tensor(ids_all, ids)
+            dist.all_gather_into_tensor(len_all, ln)
+        return outs
 
-    for i in range(args.warmup):
-        step(i)
+    runner.warmup(pool[0])          # one batch per twin: captures every decode graph
+    run(0, args.warmup)
     torch.cuda.synchronize()
     if world > 1:
         torch.distributed.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     ntok = 0
-    last = None
-    for i in range(args.steps):
-        last = step(args.warmup + i)
+    outs = run(args.warmup, args.steps)
+    last = outs[-1] if outs else None
     torch.cuda.synchronize()
     if world > 1:
         torch.distributed.barrier()
@@ -230,9 +268,12 @@ def main():
                                + ("greedy generate2" if not args.beam else f"beam {args.beam}")
                                + f", entry_length {args.entry_length}, + get_prefix_tokens",
                    "batch_per_gpu": B, "global_batch": B * world,
+                   "batches_in_flight_per_gpu": max(1, args.inflight),
                    "parallelism": f"dp{world} (clip-sharded, RCCL all-gather of token ids)",
                    "tokens_last_batch_rank0": ntok},
     }
+    if args.stages and rank == 0:
+        res["stages_ms"] = stage_times(pipe, pool[0])
     if rank == 0 and not args.no_roofline:
         res["roofline"] = kernel_roofline(pipe)
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.cpu_baseline_clips > 0:

@@ -84,7 +84,30 @@ def bench_attn():
     print(f"empty-ish (cast 64 elems): {timeit(lambda: ops.cast(x[:1, :64], y[:1, :64])):7.2f}us")
 
 
+def bench_inflight():
+    """End-to-end clips/s vs the number of concurrently decoded bs=64 batches."""
+    sys.path.insert(0, ROOT)
+    import bench
+    from zsaac.pipeline import ConcurrentRunner
+
+    class A:
+        batch, dtype, encoder, mapper, beam, entry_length = 64, "bf16", "htsat", "mlp", 0, 67
+    pipe, _, _ = bench.build(A, torch.device("cuda", 0))
+    g = torch.Generator(device="cuda").manual_seed(1)
+    wavs = [(torch.randn(64, 320000, device="cuda", generator=g) * 0.1).clamp_(-1, 1) for _ in range(8)]
+    for k in (1, 2, 4, 6, 8):
+        runner = ConcurrentRunner(pipe, k)
+        runner.warmup(wavs[0])
+        torch.cuda.synchronize()
+        nb = max(8, 3 * k)
+        t = time.perf_counter()
+        runner.run([wavs[i % len(wavs)] for i in range(nb)])
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t
+        print(f"inflight={k}: {nb * 64 / dt:8.1f} clips/s  ({dt / nb * 1e3:.1f} ms/batch)", flush=True)
+
+
 if __name__ == "__main__":
     which = sys.argv[1:] or ["gemm", "attn"]
     for wname in which:
-        {"gemm": bench_gemm, "attn": bench_attn}[wname]()
+        {"gemm": bench_gemm, "attn": bench_attn, "inflight": bench_inflight}[wname]()

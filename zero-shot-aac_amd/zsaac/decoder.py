@@ -15,6 +15,7 @@ is replayed until every row has stopped; the host only checks a flag every ``chu
 """
 from __future__ import annotations
 
+import copy
 import math
 from typing import Dict, List, Optional, Tuple
 
@@ -44,19 +45,29 @@ class MlpMapper:
         self.w2, self.b2 = _w(sd[prefix + "2.weight"], device, dtype), _f32(sd[prefix + "2.bias"], device)
         self.in_dim = self.w0.shape[1]
         self.out_dim = self.w2.shape[0]
+        self.soft_ld = self.out_dim
+        self.device, self.max_batch = device, max_batch
+        self._alloc()
+
+    def _alloc(self):
+        device, max_batch, dtype = self.device, self.max_batch, self.dtype
         self.x_t = torch.empty(max_batch, self.in_dim, device=device, dtype=dtype)
         self.h = torch.empty(max_batch, self.w0.shape[0], device=device, dtype=dtype)
         self.out = torch.empty(max_batch, self.out_dim, device=device)
-        self.soft_ld = self.out_dim
-        if max_batch <= 64:
-            ops.reserve_skinny_workspace(device, max_batch, self.w0.shape[0], self.in_dim)
-            ops.reserve_skinny_workspace(device, max_batch, self.out_dim, self.w2.shape[1])
+        self.ws = ops.skinny_workspace(device, [(max_batch, self.w0.shape[0], self.in_dim),
+                                                (max_batch, self.out_dim, self.w2.shape[1])])
+
+    def twin(self):
+        """Same weights, private activation buffers/workspace (for another stream)."""
+        t = copy.copy(self)
+        t._alloc()
+        return t
 
     def __call__(self, prefix):
         B = prefix.shape[0]
         ops.cast(prefix, self.x_t[:B])
-        ops.gemm(self.x_t[:B], self.w0, self.h[:B], bias=self.b0, act=ops.ACT_TANH)
-        ops.gemm(self.h[:B], self.w2, self.out[:B], bias=self.b2)
+        ops.gemm(self.x_t[:B], self.w0, self.h[:B], bias=self.b0, act=ops.ACT_TANH, workspace=self.ws)
+        ops.gemm(self.h[:B], self.w2, self.out[:B], bias=self.b2, workspace=self.ws)
         return self.out[:B]           # clip b's soft prefix at out + b*soft_ld
 
 
@@ -87,8 +98,18 @@ class TransformerMapperEngine:
                 "fc2_w": _w(sd[p + "mlp.fc2.weight"], device, dtype),
                 "fc2_b": _f32(sd[p + "mlp.fc2.bias"], device),
             })
-        B, L = max_batch, self.L
         self.in_dim = self.lin_w.shape[1]
+        self.soft_ld = self.L * D
+        self.device, self.max_batch = device, max_batch
+        self._alloc()
+
+    def twin(self):
+        t = copy.copy(self)
+        t._alloc()
+        return t
+
+    def _alloc(self):
+        device, dtype, B, L = self.device, self.dtype, self.max_batch, self.L
         self.x_t = torch.empty(B, self.in_dim, device=device, dtype=dtype)
         self.hs = torch.empty(B, L, D, device=device)
         self.a = torch.empty(B * L, D, device=device, dtype=dtype)
@@ -96,7 +117,6 @@ class TransformerMapperEngine:
         self.kv = torch.empty(B * L, 2 * D, device=device, dtype=dtype)
         self.o = torch.empty(B * L, D, device=device, dtype=dtype)
         self.mid = torch.empty(B * L, 2 * D, device=device, dtype=dtype)
-        self.soft_ld = L * D
 
     def __call__(self, prefix):
         B, L = prefix.shape[0], self.L
@@ -168,8 +188,12 @@ class Gpt2Decoder:
     tokens, ``max_steps`` generated tokens (entry_length)."""
 
     def __init__(self, w: Gpt2Weights, max_rows: int, max_prompt: int, max_steps: int = 67,
-                 max_prefill_rows: Optional[int] = None, topk: int = 8, chunk: int = 8,
+                 max_prefill_rows: Optional[int] = None, topk: int = 8, chunk: int = 0,
                  use_graph: bool = True):
+        if chunk <= 0:   # a divisor of the steps after step 0, near 6 (no wasted tail steps)
+            n = max(max_steps - 1, 1)
+            cands = [c for c in range(4, 13) if n % c == 0]
+            chunk = min(cands, key=lambda c: abs(c - 6)) if cands else 6
         self.w, self.dtype = w, w.dtype
         dev = w.wte.device
         self.dev = dev
@@ -216,10 +240,8 @@ class Gpt2Decoder:
         self.kvrow_tmp = torch.zeros(self.R, self.Lmax, **i32)
         self.tok_tmp = torch.zeros(self.R, max_steps, **i32)
         self.graphs: Dict[Tuple, torch.cuda.CUDAGraph] = {}
-        for M in {self.R, self.Rp}:
-            if M <= 64:
-                for N, K in ((3 * D, D), (D, D), (4 * D, D), (D, 4 * D)):
-                    ops.reserve_skinny_workspace(dev, M, N, K)
+        self.ws = ops.skinny_workspace(dev, [(M, N, K) for M in {self.R, self.Rp}
+                                             for N, K in ((3 * D, D), (D, D), (4 * D, D), (D, 4 * D))])
 
     # ---------------------------------------------------------------- blocks
     def _layers(self, M, attn_fn):
@@ -227,12 +249,12 @@ class Gpt2Decoder:
         for l, ly in enumerate(self.w.layers):
             h, qkv, att, hid = self.h[:M], self.qkv[:M], self.att[:M], self.hid[:M]
             ops.layernorm(x, *ly["ln1"], out=h)
-            ops.gemm(h, ly["attn_w"], qkv, bias=ly["attn_b"])
+            ops.gemm(h, ly["attn_w"], qkv, bias=ly["attn_b"], workspace=self.ws)
             attn_fn(l, qkv, att)
-            ops.gemm(att, ly["proj_w"], x, bias=ly["proj_b"], residual=x)
+            ops.gemm(att, ly["proj_w"], x, bias=ly["proj_b"], residual=x, workspace=self.ws)
             ops.layernorm(x, *ly["ln2"], out=h)
-            ops.gemm(h, ly["fc_w"], hid, bias=ly["fc_b"], act=ops.ACT_GELU_TANH)
-            ops.gemm(hid, ly["mproj_w"], x, bias=ly["mproj_b"], residual=x)
+            ops.gemm(h, ly["fc_w"], hid, bias=ly["fc_b"], act=ops.ACT_GELU_TANH, workspace=self.ws)
+            ops.gemm(hid, ly["mproj_w"], x, bias=ly["mproj_b"], residual=x, workspace=self.ws)
 
     def prefill(self, B: int, Pmax: int, row_stride: int = 1):
         """Runs the prompt rows already in ``self.x[:B*Pmax]`` (zs_gpt2_prefill_embed) through the
@@ -265,45 +287,67 @@ class Gpt2Decoder:
                         self.stop0, self.stop1, self.out_ids, self.out_len, self.done, self.pos,
                         self.next_tok, self.all_done)
 
-    def _run_steps(self, key, body):
-        """Replays ``body`` (one decode step) ``chunk`` at a time until all_done."""
-        if self.use_graph:
-            g = self.graphs.get(key)
-            if g is None:
-                # warm up once on a side stream, then capture `chunk` steps
-                s = torch.cuda.Stream()
-                s.wait_stream(torch.cuda.current_stream())
-                saved = [t.clone() for t in self._state()]
-                with torch.cuda.stream(s):
-                    body()
-                torch.cuda.current_stream().wait_stream(s)
-                for t, v in zip(self._state(), saved):
-                    t.copy_(v)
-                g = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g):
-                    for _ in range(self.chunk):
-                        body()
-                self.graphs[key] = g
-            n = 0
-            while True:
-                g.replay()
-                n += self.chunk
-                if n >= self.max_steps or int(self.all_done.item()):
-                    break
-        else:
-            for _ in range(self.max_steps):
+    def _graph(self, key, body):
+        """The captured hipGraph of ``chunk`` consecutive decode steps (captured on first use:
+        one eager warm-up step on a side stream with the decode state saved/restored, then
+        capture)."""
+        g = self.graphs.get(key)
+        if g is None:
+            cur = torch.cuda.current_stream()
+            s = torch.cuda.Stream()
+            s.wait_stream(cur)
+            saved = [t.clone() for t in self._state()]
+            with torch.cuda.stream(s):
                 body()
-                if int(self.all_done.item()):
-                    break
+            cur.wait_stream(s)
+            for t, v in zip(self._state(), saved):
+                t.copy_(v)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                for _ in range(self.chunk):
+                    body()
+            cur.wait_stream(torch.cuda.current_stream())
+            self.graphs[key] = g
+        return g
+
+    @property
+    def n_chunks(self) -> int:
+        """Chunks after the prefill step that cover entry_length (step 0 runs with the prefill)."""
+        return max(0, -(-(self.max_steps - 1) // self.chunk))
+
+    def step_chunk(self):
+        """Enqueue ``chunk`` decode steps of the active decode (no host sync)."""
+        key, body = self._active
+        if self.use_graph:
+            self._graph(key, body).replay()
+        else:
+            for _ in range(self.chunk):
+                body()
+
+    def finished_async(self):
+        """Enqueue a copy of all_done to pinned host memory; returns (event, host tensor)."""
+        if not hasattr(self, "_flag_host"):
+            self._flag_host = torch.zeros(1, dtype=torch.int32, pin_memory=True)
+        self._flag_host.copy_(self.all_done, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        return ev, self._flag_host
+
+    def run_to_completion(self):
+        """Synchronous loop: replay chunks until every row stopped or entry_length reached."""
+        for _ in range(self.n_chunks):
+            if int(self.all_done.item()):
+                break
+            self.step_chunk()
 
     def _state(self):
         return [self.pos, self.next_tok, self.done, self.out_ids, self.out_len, self.step_ctr,
                 self.all_done, self.scores, self.seq_len, self.kvrow, self.kvrow_tmp, self.tok_tmp]
 
     # ---------------------------------------------------------------- greedy (generate2)
-    def greedy(self, B: int, Pmax: int):
-        """After :meth:`prefill` (row_stride 1): generate2 for all B rows.
-        Returns (ids [B, max_steps] int32, lengths [B] int32) device tensors."""
+    def greedy_begin(self, B: int):
+        """Enqueue step 0 of generate2 from the prefill rows (no host sync); afterwards
+        :meth:`step_chunk` advances ``chunk`` steps at a time."""
         R = B
         ops.lmhead_topk(self.hf[:R], self.w.wte, 1, self.pstat, self.pval1, self.pidx1)
         self.pos[:R].copy_(self.plen[:R] - 1)
@@ -312,9 +356,14 @@ class Gpt2Decoder:
         ops.greedy_step(self.pval1, self.pidx1, R, self.nblk, self.step_ctr, self.max_steps,
                         self.stop0, self.stop1, self.out_ids, self.out_len, self.done, self.pos,
                         self.next_tok, self.all_done)
-        if self.max_steps > 1 and not int(self.all_done.item()):
-            self._run_steps(("greedy", R, self.stop0, self.stop1), lambda: self._greedy_step_body(R))
-        return self.out_ids[:R], self.out_len[:R]
+        self._active = (("greedy", R, self.stop0, self.stop1), lambda: self._greedy_step_body(R))
+
+    def greedy(self, B: int, Pmax: int):
+        """After :meth:`prefill` (row_stride 1): generate2 for all B rows.
+        Returns (ids [B, max_steps] int32, lengths [B] int32) device tensors."""
+        self.greedy_begin(B)
+        self.run_to_completion()
+        return self.out_ids[:B], self.out_len[:B]
 
     # ---------------------------------------------------------------- beam (generate_beam)
     def _beam_step_body(self, C, beam):
@@ -330,6 +379,13 @@ class Gpt2Decoder:
         """After :meth:`prefill` (C rows, row_stride=beam): generate_beam per clip.
         Returns (tokens [C, beam, steps], seq_len [C, beam], scores [C, beam]) device tensors
         (rows unsorted; the caller orders by scores/seq_len like the reference)."""
+        self.beam_begin(C, beam)
+        self.run_to_completion()
+        R = C * beam
+        return (self.out_ids[:R].view(C, beam, -1), self.seq_len[:R].view(C, beam),
+                self.scores[:R].view(C, beam))
+
+    def beam_begin(self, C: int, beam: int):
         assert beam <= self.topk and C * beam <= self.R
         R = C * beam
         ops.lmhead_topk(self.hf[:C], self.w.wte, self.topk, self.pstat, self.pval, self.pidx)
@@ -341,10 +397,7 @@ class Gpt2Decoder:
                       self.stop0, self.step_ctr, self.max_steps, self.scores, self.seq_len,
                       self.done, self.out_ids, self.tok_tmp, self.kvrow, self.kvrow_tmp, self.Lmax,
                       self.pos, self.next_tok, self.all_done)
-        if self.max_steps > 1 and not int(self.all_done.item()):
-            self._run_steps(("beam", C, beam, self.stop0), lambda: self._beam_step_body(C, beam))
-        return (self.out_ids[:R].view(C, beam, -1), self.seq_len[:R].view(C, beam),
-                self.scores[:R].view(C, beam))
+        self._active = (("beam", C, beam, self.stop0), lambda: self._beam_step_body(C, beam))
 
     # ---------------------------------------------------------------- get_prefix_tokens
     def prefix_tokens(self, embed_rows: torch.Tensor, out_idx: torch.Tensor):

@@ -9,6 +9,7 @@ Activations: residual stream f32, GEMM operands in the compute dtype.
 """
 from __future__ import annotations
 
+import copy
 from typing import Dict
 
 import torch
@@ -126,15 +127,22 @@ class AudioEncoder:
         self.width = width
         # audio_proj is optional: the bare HTSAT/CNN14 drop-ins return the encoder features
         self.proj = AudioProjWeights(sd, self.dev, dtype) if "audio_proj.0.weight" in sd else None
-        B, dev = max_batch, self.dev
+        self._alloc()
+
+    def twin(self):
+        """Same packed weights, private activation buffers (for another stream)."""
+        t = copy.copy(self)
+        t._alloc()
+        return t
+
+    def _alloc(self):
+        B, dev, dtype, width, kind = self.B, self.dev, self.dtype, self.width, self.kind
         self.logmel = torch.empty(B, self.n_frames, 64, device=dev)
         self.feat = torch.empty(B, width, device=dev)
         self.feat_t = torch.empty(B, width, device=dev, dtype=dtype)
         self.proj_h = torch.empty(B, 1024, device=dev, dtype=dtype)
         self.emb = torch.empty(B, 1024, device=dev)
-        if B <= 64:
-            ops.reserve_skinny_workspace(dev, B, 1024, width)
-            ops.reserve_skinny_workspace(dev, B, 1024, 1024)
+        self.ws = ops.skinny_workspace(dev, [(B, 1024, width), (B, 1024, 1024)])
         if kind == "htsat":
             M = B * 4096
             self.img = torch.empty(B, 256, 256, device=dev)
@@ -227,6 +235,7 @@ class AudioEncoder:
         B = feat.shape[0]
         assert self.proj is not None, "no audio_proj weights"
         ops.cast(feat, self.feat_t[:B])
-        ops.gemm(self.feat_t[:B], self.proj.w0, self.proj_h[:B], bias=self.proj.b0, act=ops.ACT_RELU)
-        ops.gemm(self.proj_h[:B], self.proj.w2, self.emb[:B], bias=self.proj.b2)
+        ops.gemm(self.feat_t[:B], self.proj.w0, self.proj_h[:B], bias=self.proj.b0, act=ops.ACT_RELU,
+                 workspace=self.ws)
+        ops.gemm(self.proj_h[:B], self.proj.w2, self.emb[:B], bias=self.proj.b2, workspace=self.ws)
         return ops.l2norm(self.emb[:B], out=self.emb[:B])

@@ -111,6 +111,14 @@ def reserve_skinny_workspace(device, M, N, K):
 _RETIRED = []
 
 
+def skinny_workspace(device, shapes):
+    """A private zeroed workspace for the skinny GEMMs of one engine (one stream): sized for the
+    largest of ``shapes`` [(M, N, K)].  Engines that may run concurrently on different streams
+    must not share a workspace (its tile counters and slabs are per launch)."""
+    need = max([call("zs_gemm_workspace_floats", M, N, K) for M, N, K in shapes] + [0])
+    return torch.zeros(max(need, 1), device=device) if need else None
+
+
 def gemm(a, w, out, bias=None, residual=None, act=ACT_NONE, split_k=0, workspace=None, M=None):
     """out = act(a @ w.T + bias) + residual;  a [M,K], w [N,K] (same dtype), out f32/bf16.
     split_k=0 (auto): M <= 64 uses the weight-streaming skinny kernel when a workspace was
@@ -127,6 +135,9 @@ def gemm(a, w, out, bias=None, residual=None, act=ACT_NONE, split_k=0, workspace
                 workspace = None
         if workspace is None:
             split_k = 1
+        elif M <= 64:
+            need = call("zs_gemm_workspace_floats", M, N, K)
+            _need(need <= workspace.numel(), f"gemm: workspace {workspace.numel()} < {need} floats")
     lda = a.stride(-2) if a.dim() > 1 else K
     ldo = out.stride(-2) if out.dim() > 1 else N
     ldr = (residual.stride(-2) if residual.dim() > 1 else N) if residual is not None else 0

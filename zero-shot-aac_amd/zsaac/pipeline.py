@@ -11,6 +11,8 @@ batch of clips.  Multi-GPU sharding and the token-id all-gather live in zsaac/di
 """
 from __future__ import annotations
 
+import copy
+import time
 from dataclasses import dataclass
 from typing import List, Optional, Sequence
 
@@ -82,6 +84,35 @@ class CaptionPipeline:
         self.dev = dev
         B = cfg.batch
         self.encoder = AudioEncoder(audio_sd, cfg.encoder, cfg.dtype, B, dev) if audio_sd else None
+        self.mapper = build_mapper(caption_sd, cfg.mapping_type, dev, cfg.dtype, B)
+        self.gpt = Gpt2Weights(caption_sd, dev, cfg.dtype)
+        self._setup_tables(label_table, label_tokens)
+        self._alloc()
+
+    def twin(self) -> "CaptionPipeline":
+        """A pipeline sharing every packed weight with this one but owning its activation
+        buffers, KV cache, skinny-GEMM workspace and decode graphs — so it can run a different
+        batch concurrently on another HIP stream (ConcurrentRunner)."""
+        t = copy.copy(self)
+        t.encoder = self.encoder.twin() if self.encoder is not None else None
+        t.mapper = self.mapper.twin()
+        t._alloc()
+        return t
+
+    def _alloc(self):
+        cfg, dev, B = self.cfg, self.dev, self.cfg.batch
+        beam = max(cfg.beam, 1)
+        self.decoder = Gpt2Decoder(self.gpt, B * beam, self.Pmax, cfg.entry_length,
+                                   max_prefill_rows=B, use_graph=cfg.use_graph)
+        i32 = dict(device=dev, dtype=torch.int32)
+        self.hard_ids = torch.zeros(B, self.h_cap, **i32)
+        self.hard_len = torch.zeros(B, **i32)
+        self.prefix = torch.empty(B, 1024, device=dev)
+        self.embed = torch.empty(B * self.Pmax, 768, device=dev)
+        self.prefix_ids = torch.zeros(B * self.Pmax, **i32)
+
+    def _setup_tables(self, label_table, label_tokens):
+        cfg, dev = self.cfg, self.dev
         self.labels = label_table.to(device=dev, dtype=torch.float32).contiguous()
         mt = max(len(t) for t in label_tokens)
         lt = np.zeros((len(label_tokens), mt), dtype=np.int32)
@@ -93,17 +124,6 @@ class CaptionPipeline:
         # longest possible hard prompt: "There are" + k labels + (k-1) commas + " in this audio."
         self.h_cap = 2 + k * mt + max(k - 1, 0) + 4 if k > 0 else 7
         self.Pmax = self.h_cap + cfg.prefix_length
-        self.mapper = build_mapper(caption_sd, cfg.mapping_type, dev, cfg.dtype, B)
-        self.gpt = Gpt2Weights(caption_sd, dev, cfg.dtype)
-        beam = max(cfg.beam, 1)
-        self.decoder = Gpt2Decoder(self.gpt, B * beam, self.Pmax, cfg.entry_length,
-                                   max_prefill_rows=B, use_graph=cfg.use_graph)
-        i32 = dict(device=dev, dtype=torch.int32)
-        self.hard_ids = torch.zeros(B, self.h_cap, **i32)
-        self.hard_len = torch.zeros(B, **i32)
-        self.prefix = torch.empty(B, 1024, device=dev)
-        self.embed = torch.empty(B * self.Pmax, 768, device=dev)
-        self.prefix_ids = torch.zeros(B * self.Pmax, **i32)
 
     def caption_wav(self, wav: torch.Tensor) -> CaptionBatch:
         assert self.encoder is not None, "no audio encoder weights"
@@ -111,7 +131,33 @@ class CaptionPipeline:
 
     def caption_emb(self, emb: torch.Tensor) -> CaptionBatch:
         """From CLAP audio embeddings [B, 1024] (the pickle's ``audio_embedding``)."""
+        self.begin_emb(emb)
+        self.decoder.run_to_completion()
+        return self.result()
+
+    # ------------------------------------------------------------------ async (no host sync)
+    def begin_wav(self, wav: torch.Tensor):
+        assert self.encoder is not None, "no audio encoder weights"
+        self.begin_emb(self.encoder.encode(wav))
+
+    def result(self) -> CaptionBatch:
+        """Views of the current batch's outputs (valid until the next begin_*)."""
+        B, cfg, dec = self._B, self.cfg, self.decoder
+        if cfg.beam:
+            R = B * cfg.beam
+            ids = dec.out_ids[:R].view(B, cfg.beam, -1)
+            ln, sc = dec.seq_len[:R].view(B, cfg.beam), dec.scores[:R].view(B, cfg.beam)
+        else:
+            ids, ln, sc = dec.out_ids[:B], dec.out_len[:B], None
+        pid = self.prefix_ids[:B * self.Pmax].view(B, self.Pmax) if cfg.prefix_tokens else None
+        return CaptionBatch(ids, ln, sc, self.hard_ids[:B], self.hard_len[:B], dec.plen[:B], pid,
+                            self._emb)
+
+    def begin_emb(self, emb: torch.Tensor):
+        """Enqueue prompt assembly, mapper, prefill, get_prefix_tokens and decode step 0 for a
+        batch of CLAP embeddings, without any host synchronisation."""
         cfg, B, Pmax = self.cfg, emb.shape[0], self.Pmax
+        self._B, self._emb = B, emb
         assert B <= cfg.batch
         ops.prompt_assemble(emb, self.labels, cfg.sound_effect_num, self.label_tok, self.label_len,
                             self.hard_ids[:B], self.hard_len[:B])
@@ -125,16 +171,94 @@ class CaptionPipeline:
         ops.prefill_embed(self.hard_ids[:B], self.hard_len[:B], soft, self.mapper.soft_ld,
                           cfg.prefix_length, self.gpt.wte, self.gpt.wpe, B, Pmax,
                           self.embed[:B * Pmax], dec.x, dec.plen, dec.last_row)
-        prefix_ids = None
         if cfg.prefix_tokens:
             dec.prefix_tokens(self.embed[:B * Pmax], self.prefix_ids[:B * Pmax])
-            prefix_ids = self.prefix_ids[:B * Pmax].view(B, Pmax)
         if cfg.beam:
             dec.prefill(B, Pmax, row_stride=cfg.beam)
-            ids, ln, sc = dec.beam(B, cfg.beam, Pmax)
+            dec.beam_begin(B, cfg.beam)
         else:
             dec.prefill(B, Pmax)
-            ids, ln = dec.greedy(B, Pmax)
-            sc = None
-        return CaptionBatch(ids, ln, sc, self.hard_ids[:B], self.hard_len[:B], dec.plen[:B],
-                            prefix_ids, emb)
+            dec.greedy_begin(B)
+
+
+class ConcurrentRunner:
+    """Keeps several independent bs=`cfg.batch` batches in flight on one GPU: pipeline twins
+    (shared weights, private buffers/KV cache/graphs), each on its own HIP stream.  A batch is
+    encode + mapper + prefill enqueued at once, then its decode graph chunks are enqueued one at a
+    time; the host only polls events and a pinned all-done flag (no blocking syncs), so while
+    one batch waits on a latency-bound decode kernel the others' kernels fill the chip.
+
+    Results are copied out on the pipeline's stream before it takes the next batch."""
+
+    def __init__(self, pipe: CaptionPipeline, n_inflight: int = 2):
+        self.pipes = [pipe] + [pipe.twin() for _ in range(n_inflight - 1)]
+        self.streams = [torch.cuda.Stream(device=pipe.dev) for _ in self.pipes]
+
+    def warmup(self, wav: torch.Tensor):
+        """Runs one batch per pipeline synchronously (captures every decode graph)."""
+        for p, s in zip(self.pipes, self.streams):
+            s.wait_stream(torch.cuda.current_stream(p.dev))
+            with torch.cuda.stream(s):
+                p.caption_wav(wav)
+            s.synchronize()
+
+    def warmup_emb(self, emb: torch.Tensor):
+        for p, s in zip(self.pipes, self.streams):
+            s.wait_stream(torch.cuda.current_stream(p.dev))
+            with torch.cuda.stream(s):
+                p.caption_emb(emb)
+            s.synchronize()
+
+    def run(self, batches: Sequence[torch.Tensor], keep=None, inputs: str = "wav") -> List[CaptionBatch]:
+        """Captions every batch (waveforms [B, n] or, with inputs="emb", CLAP embeddings
+        [B, 1024]; B <= cfg.batch, ragged last batch allowed); returns CaptionBatch copies in
+        input order.  ``keep`` optionally post-processes a result on its pipeline's stream; the
+        completion order is timing-dependent, so it must not issue collectives (gather after
+        run() instead, in input order — see bench.py)."""
+        assert inputs in ("wav", "emb")
+        results: List[Optional[CaptionBatch]] = [None] * len(batches)
+        caller = torch.cuda.current_stream(self.pipes[0].dev)
+        for s in self.streams:           # inputs were produced on the caller's stream
+            s.wait_stream(caller)
+        active = {}
+        nxt = 0
+        while nxt < len(batches) or active:
+            progressed = False
+            for i, (p, s) in enumerate(zip(self.pipes, self.streams)):
+                st = active.get(i)
+                if st is None:
+                    if nxt < len(batches):
+                        with torch.cuda.stream(s):
+                            (p.begin_wav if inputs == "wav" else p.begin_emb)(batches[nxt])
+                            ev, flag = p.decoder.finished_async()
+                        active[i] = (nxt, 0, ev, flag)
+                        nxt += 1
+                        progressed = True
+                    continue
+                bi, n, ev, flag = st
+                if not ev.query():
+                    continue
+                progressed = True
+                if int(flag[0]) or n >= p.decoder.n_chunks:
+                    with torch.cuda.stream(s):
+                        r = p.result()
+                        results[bi] = _copy_batch(r)
+                        if keep is not None:
+                            keep(results[bi])
+                    del active[i]
+                else:
+                    with torch.cuda.stream(s):
+                        p.decoder.step_chunk()
+                        ev, flag = p.decoder.finished_async()
+                    active[i] = (bi, n + 1, ev, flag)
+            if not progressed:
+                time.sleep(20e-6)
+        for s in self.streams:           # results are consumed on the caller's stream
+            caller.wait_stream(s)
+        return results
+
+
+def _copy_batch(r: CaptionBatch) -> CaptionBatch:
+    c = lambda t: None if t is None else t.clone()
+    return CaptionBatch(c(r.ids), c(r.lengths), c(r.scores), c(r.hard_ids), c(r.hard_len),
+                        c(r.plen), c(r.prefix_ids), c(r.clap_emb))
