@@ -181,7 +181,9 @@ int zs_argmax_finalize(const float* part_val, const int* part_idx, int M, int nb
  * tok = argmax(partials); rows already done keep emitting nothing; out_ids[r][step] = tok,
  * out_len[r] = step+1 while not done; done |= tok in {stop0, stop1}; pos[r] += 1 (next position);
  * next_tok[r] = tok.  `step` is read from *step_ctr (device) and *step_ctr += 1 by the last
- * block, so a captured graph replays without host arguments.  all_done[0] = AND(done). */
+ * block, so a captured graph replays without host arguments.  all_done[0] = AND(done);
+ * all_done[1] is the blocks' arrival counter: zero it once before the first call (every call
+ * re-arms it). */
 int zs_greedy_step(const float* part_val, const int* part_idx, int R, int nblk, int* step_ctr,
                    int max_steps, int stop0, int stop1, int* out_ids, int* out_len, int* done,
                    int* pos, int* next_tok, int* all_done, void* stream);

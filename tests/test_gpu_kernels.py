@@ -50,9 +50,11 @@ def test_gemm(cuda, dtype, M, N, K):
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("M,N,K", [(64, 2304, 768), (64, 768, 768), (64, 3072, 768), (64, 768, 3072),
-                                   (50, 7680, 3840), (3, 1024, 768), (64, 100, 64)])
+                                   (50, 7680, 3840), (3, 1024, 768), (64, 100, 64),
+                                   (256, 2304, 768), (200, 768, 3072), (65, 3072, 768)])
 def test_gemm_skinny(cuda, dtype, M, N, K):
-    """M <= 64 auto mode: weight-streaming split-K with in-kernel last-arriver reduction."""
+    """M <= 256 auto mode: weight-streaming split-K with in-kernel last-arriver reduction over
+    up to 4 row blocks of 64 (ragged last block)."""
     from zsaac import ops
     ops.reserve_skinny_workspace(cuda, M, N, K)
     g = torch.Generator(device="cuda").manual_seed(N + K)
@@ -208,6 +210,48 @@ def test_decode_attention_matches_prefill(cuda):
     assert torch.equal(kc[:, :, n - 1], last[:, D:2 * D].view(R, H, 64))
 
 
+@pytest.mark.parametrize("use_kvrow", [False, True])
+@pytest.mark.parametrize("variant", [1, 0])
+def test_decode_attention_bf16(cuda, use_kvrow, variant):
+    """bf16 decode attention (register-resident decode_attn5, and the LDS-staged decode_attn4)
+    vs an fp32 torch reference: ragged positions 0..Lmax-1 per row, optional beam kvrow
+    indirection, and the new token's k/v appended to the cache."""
+    from zsaac import ops
+    from zsaac._lib import call
+    R, D, H, Lmax = 40, 768, 12, 103
+    g = torch.Generator(device="cuda").manual_seed(11)
+    kc = torch.randn(R, H, Lmax, 64, device=cuda, generator=g).bfloat16()
+    vc = torch.randn(R, H, Lmax, 64, device=cuda, generator=g).bfloat16()
+    if use_kvrow:     # beam rows all share one position; keys come from other rows
+        pos = torch.full((R,), 57, device=cuda, dtype=torch.int32)
+        kvrow = torch.randint(0, R, (R, Lmax), device=cuda, generator=g, dtype=torch.int32)
+    else:
+        pos = torch.randint(0, Lmax, (R,), device=cuda, generator=g, dtype=torch.int32)
+        pos[0], pos[1] = 0, Lmax - 1
+        kvrow = None
+    qkv = torch.randn(R, 3 * D, device=cuda, generator=g).bfloat16()
+    k0, v0 = kc.float().clone(), vc.float().clone()
+    out = torch.empty(R, D, device=cuda, dtype=torch.bfloat16)
+    call("zs_tune_set", b"decode_attn5", variant)
+    try:
+        ops.decode_attention(qkv, R, D, H, kc, vc, Lmax, pos, out, kvrow=kvrow)
+    finally:
+        call("zs_tune_set", b"decode_attn5", 1)
+    qf = qkv.float()
+    for r in range(R):
+        p = int(pos[r])
+        src = kvrow[r, :p].long() if use_kvrow else torch.full((p,), r, device=cuda, dtype=torch.long)
+        for h in range(H):
+            K = torch.cat([k0[src, h, torch.arange(p, device=cuda)], qf[r, D + 64 * h:D + 64 * h + 64][None]])
+            V = torch.cat([v0[src, h, torch.arange(p, device=cuda)], qf[r, 2 * D + 64 * h:2 * D + 64 * h + 64][None]])
+            att = torch.softmax(K @ (qf[r, 64 * h:64 * h + 64] * 0.125), 0)
+            ref = att @ V
+            got = out[r, 64 * h:64 * h + 64].float()
+            assert float((got - ref).abs().max()) < 2e-2 * float(ref.abs().max()) + 1e-2, (r, h, p)
+        assert torch.equal(kc[r, :, p], qkv[r, D:2 * D].view(H, 64))
+        assert torch.equal(vc[r, :, p], qkv[r, 2 * D:].view(H, 64))
+
+
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 def test_lmhead_topk(cuda, dtype):
     from zsaac import ops
@@ -318,11 +362,29 @@ def test_conv3x3(cuda):
         assert _rel(p.cpu().permute(0, 3, 1, 2), torch.nn.functional.avg_pool2d(ref, 2)) < 1e-5
 
 
+def test_gemm_skinny_rows_independent(cuda):
+    """A row's result does not depend on how many rows share the launch (row blocks of a
+    256-row launch == the same rows launched alone): continuous batching keeps f32 parity."""
+    from zsaac import ops
+    g = torch.Generator(device="cuda").manual_seed(5)
+    for N, K in ((2304, 768), (768, 3072)):
+        a = torch.randn(256, K, device=cuda, generator=g)
+        w = torch.randn(N, K, device=cuda, generator=g) / math.sqrt(K)
+        ws = ops.skinny_workspace(cuda, [(256, N, K)])
+        full = torch.empty(256, N, device=cuda)
+        ops.gemm(a, w, full, workspace=ws)
+        for r0, r1 in ((0, 64), (64, 128), (130, 190), (250, 256)):
+            part = torch.empty(r1 - r0, N, device=cuda)
+            ops.gemm(a[r0:r1], w, part, workspace=ws)
+            assert torch.equal(part, full[r0:r1]), (N, K, r0, r1)
+
+
 def test_gemm_skinny_shared_workspace(cuda):
     """Shapes with different tile counts share one workspace: slabs of one GEMM must never be
     read as another GEMM's tile counters (regression)."""
     from zsaac import ops
-    shapes = [(64, 2304, 768), (3, 7680, 3840), (64, 768, 3072), (3, 3840, 1024), (64, 768, 768)]
+    shapes = [(64, 2304, 768), (3, 7680, 3840), (64, 768, 3072), (3, 3840, 1024), (64, 768, 768),
+              (256, 768, 3072), (130, 2304, 768)]
     for M, N, K in shapes:
         ops.reserve_skinny_workspace(cuda, M, N, K)
     g = torch.Generator(device="cuda").manual_seed(9)

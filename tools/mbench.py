@@ -64,6 +64,58 @@ def bench_gemm():
               flush=True)
 
 
+def bench_gemm_m():
+    """Decode GEMM shapes at M = 64..1280 (continuous batching / beam rows): ours vs hipBLASLt."""
+    from zsaac import ops
+    dev = torch.device("cuda", 0)
+    for M in (64, 256, 1280, 1856, 16384, 65536):
+        for N, K, name in ((2304, 768, "qkv"), (768, 768, "proj"), (3072, 768, "fc"), (768, 3072, "mproj")):
+            ws = ops.skinny_workspace(dev, [(M, N, K)])
+            a = torch.randn(M, K, device=dev).bfloat16()
+            w = (torch.randn(N, K, device=dev) * 0.02).bfloat16()
+            b = torch.randn(N, device=dev)
+            out = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+            from zsaac._lib import call
+            res = {}
+            if ws is not None:
+                res["skinny"] = timeit(lambda: ops.gemm(a, w, out, bias=b, workspace=ws))
+            res["fast"] = timeit(lambda: ops.gemm(a, w, out, bias=b, split_k=1))
+            call("zs_tune_set", b"gemm_fast", 0)
+            res["old"] = timeit(lambda: ops.gemm(a, w, out, bias=b, split_k=1))
+            call("zs_tune_set", b"gemm_fast", 1)
+            res["torch"] = timeit(lambda: torch.nn.functional.linear(a, w, b.bfloat16()))
+            print(f"M{M:5d} {name:6s} N{N} K{K}  " + "  ".join(f"{k}={v:7.2f}us" for k, v in res.items()),
+                  flush=True)
+
+
+def bench_gemm_htsat():
+    """HTSAT encoder GEMM shapes for one 64-clip batch: tokens 4096/1024/256/64 per clip."""
+    from zsaac import ops
+    from zsaac._lib import call
+    dev = torch.device("cuda", 0)
+    for C, T in ((96, 4096), (192, 1024), (384, 256), (768, 64)):
+        M = 64 * T
+        shapes = [(3 * C, C, "qkv"), (C, C, "proj"), (4 * C, C, "fc1"), (C, 4 * C, "fc2")]
+        if C < 768:
+            shapes.append((2 * C, 4 * C, "merge"))
+            Mm = M // 4
+        for N, K, name in shapes:
+            Mr = Mm if name == "merge" else M
+            a = torch.randn(Mr, K, device=dev).bfloat16()
+            w = (torch.randn(N, K, device=dev) * 0.02).bfloat16()
+            b = torch.randn(N, device=dev)
+            out = torch.empty(Mr, N, device=dev)
+            res = {"fast": timeit(lambda: ops.gemm(a, w, out, bias=b, split_k=1), reps=20)}
+            call("zs_tune_set", b"gemm_fast", 0)
+            res["old"] = timeit(lambda: ops.gemm(a, w, out, bias=b, split_k=1), reps=20)
+            call("zs_tune_set", b"gemm_fast", 1)
+            res["torch"] = timeit(lambda: torch.nn.functional.linear(a, w, b.bfloat16()), reps=20)
+            byts = Mr * K * 2 + Mr * N * 4
+            print(f"C{C:4d} M{Mr:7d} {name:6s} N{N:5d} K{K:5d}  " +
+                  "  ".join(f"{k}={v:8.2f}us" for k, v in res.items()) +
+                  f"  ({byts / res['fast'] / 1e3:6.0f} GB/s fast)", flush=True)
+
+
 def bench_attn():
     from zsaac import ops
     dev = torch.device("cuda", 0)
@@ -104,10 +156,11 @@ def bench_inflight():
         runner.run([wavs[i % len(wavs)] for i in range(nb)])
         torch.cuda.synchronize()
         dt = time.perf_counter() - t
-        print(f"inflight={k}: {nb * 64 / dt:8.1f} clips/s  ({dt / nb * 1e3:.1f} ms/batch)", flush=True)
+        print(f"inflight={k}: {nb * 64 / dt:8.1f} clips/s  ({dt / nb * 1e3:.1f} ms/batch)  "
+              f"decode steps {runner.decode_steps}", flush=True)
 
 
 if __name__ == "__main__":
     which = sys.argv[1:] or ["gemm", "attn"]
     for wname in which:
-        {"gemm": bench_gemm, "attn": bench_attn, "inflight": bench_inflight}[wname]()
+        {"gemm": bench_gemm, "gemm_m": bench_gemm_m, "gemm_htsat": bench_gemm_htsat, "attn": bench_attn, "inflight": bench_inflight}[wname]()

@@ -1,0 +1,83 @@
+#!/usr/bin/env python3
+"""HBM traffic of bench.py's roofline kernel from rocprofv3 PMC counters (roofline.traffic).
+
+Two counter passes (FETCH_SIZE and WRITE_SIZE do not fit one gfx950 TCC pass), each with eager
+launches of exactly the launches bench.py times (roofline_setup: cold weights), then a parse:
+
+    rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o run --output-format csv -- python3 tools/pmc_traffic.py run
+    rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write -o run --output-format csv -- python3 tools/pmc_traffic.py run
+    python3 tools/pmc_traffic.py parse gpurun_out/pmc_fetch gpurun_out/pmc_write gpurun_out/pmc_traffic_r1.json
+
+Corrections (MI355X_MICROARCH.md §HBM): FETCH_SIZE is in KiB and on gfx950 reports half the
+bytes of a 16-B/lane coalesced streaming read (the skinny kernel's W and A loads are all 16 B per
+lane), so read bytes = 2 * 1024 * FETCH_SIZE; WRITE_SIZE (KiB) is exact for 16-B/lane stores
+(the split-K slabs) and uncalibrated for the 2-B bf16 epilogue stores (64 KiB of 5 MB).
+"""
+import csv
+import glob
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "zero-shot-aac_amd"))
+
+
+def run():
+    import torch
+    import bench
+
+    class A:
+        batch, dtype, encoder, mapper, beam, entry_length = 64, "bf16", "htsat", "mlp", 0, 67
+    pipe, _, _ = bench.build(A, torch.device("cuda", 0))
+    launch, algo, ncopy = bench.roofline_setup(pipe)
+    for i in range(2 * ncopy):
+        launch(i)
+    torch.cuda.synchronize()
+    print(json.dumps({"algo_bytes_per_launch": algo, "launches": 2 * ncopy}))
+
+
+def _per_dispatch(d, counter):
+    files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
+    if not files:
+        raise SystemExit(f"no counter_collection.csv under {d}")
+    vals = {}
+    for fn in files:
+        with open(fn) as f:
+            for row in csv.DictReader(f):
+                if row.get("Counter_Name") != counter or "gemm_skinny_kernel" not in row.get("Kernel_Name", ""):
+                    continue
+                key = (fn, row.get("Dispatch_Id") or row.get("Correlation_Id"))
+                vals[key] = vals.get(key, 0.0) + float(row["Counter_Value"])
+    if not vals:
+        raise SystemExit(f"no {counter} rows for gemm_skinny_kernel under {d}")
+    v = sorted(vals.values())
+    return v[len(v) // 2], len(v)
+
+
+def parse(dfetch, dwrite, out):
+    fetch_kib, n_f = _per_dispatch(dfetch, "FETCH_SIZE")
+    write_kib, n_w = _per_dispatch(dwrite, "WRITE_SIZE")
+    rd = 2 * 1024 * fetch_kib
+    wr = 1024 * write_kib
+    sys.path.insert(0, ROOT)
+    res = {"kernel": "gemm_skinny_kernel<bf16> decode c_fc (cold weights)",
+           "fetch_size_kib_median": fetch_kib, "write_size_kib_median": write_kib,
+           "dispatches": [n_f, n_w], "hbm_read_bytes_per_launch": int(rd),
+           "hbm_write_bytes_per_launch": int(wr), "hbm_bytes_per_launch": int(rd + wr),
+           "corrections": "read = 2*1024*FETCH_SIZE (gfx950 16B/lane streaming reads); "
+                          "write = 1024*WRITE_SIZE"}
+    # the algorithmic byte count bench.py checks against (shape-only, no GPU needed)
+    M, N, K = 64, 3072, 768
+    res["algo_bytes_per_launch"] = N * K * 2 + M * K * 2 + N * 4 + M * N * 2
+    with open(out, "w") as f:
+        json.dump(res, f, indent=1)
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    if sys.argv[1] == "run":
+        run()
+    else:
+        parse(*sys.argv[2:5])

@@ -9,6 +9,8 @@
 
 namespace zs {
 
+int g_decode_attn5 = 1;   // zs_tune_set("decode_attn5", 0): LDS-staged decode_attn4 for bf16
+
 // ------------------------------------------------------------------ HTSAT window attention
 // grid (B * nWh * nWw, heads), block 64: thread i = token i of the 8x8 window.
 template <typename T, int HD>
@@ -204,6 +206,104 @@ __global__ __launch_bounds__(256) void decode_attn4_kernel(const T* __restrict__
         (po[lane] + po[64 + lane] + po[128 + lane] + po[192 + lane]) * inv);
 }
 
+// Register-resident decode attention (bf16, Lmax <= DA5_MAXK): one wave per (row, head), 4 heads
+// of a row per block.  A lane owns 8 head dims (one 16-byte chunk) of key j = 8*i + lane/8, so one
+// wave-instruction reads 8 consecutive cached keys = 1 KiB contiguous (the cache is
+// [row][head][pos][64]); every K and V load of the row is issued up front (no LDS, no barrier),
+// the q.k partial is reduced over the key's 8 lanes (xor 1,2,4), the softmax statistics and the
+// P.V partials over the 8 key groups (xor 8,16,32).  The new token's k/v (position pos[r]) comes
+// from the qkv row in registers and is written to the cache for later steps.  HBM-bound on the
+// K/V bytes: 2 * (pos+1) * 64 * 2 B per (row, head).
+constexpr int DA5_MAXI = 16;                 // key groups of 8 -> up to 128 positions
+template <typename T>
+__global__ __launch_bounds__(256) void decode_attn5_kernel(const T* __restrict__ qkv, int D,
+                                                           int heads, T* __restrict__ kc,
+                                                           T* __restrict__ vc, int Lmax,
+                                                           const int* __restrict__ pos,
+                                                           const int* __restrict__ kvrow,
+                                                           T* __restrict__ out) {
+  static_assert(sizeof(T) == 2, "bf16 only");
+  constexpr int HD = 64, EPC = 8;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int r = blockIdx.x, h = blockIdx.y * 4 + wid;
+  if (h >= heads) return;
+  const int grp = lane >> 3, sub = lane & 7;
+  const int p = min(pos[r], Lmax - 1);
+  const T* row = qkv + (long)r * 3 * D + h * HD + sub * EPC;
+  const uint4 qu = *reinterpret_cast<const uint4*>(row);
+  const uint4 knu = *reinterpret_cast<const uint4*>(row + D);
+  const uint4 vnu = *reinterpret_cast<const uint4*>(row + 2 * D);
+  const long rh = ((long)r * heads + h) * Lmax;
+  if (grp == 0) {        // append this step's k/v to the cache
+    *reinterpret_cast<uint4*>(kc + (rh + p) * HD + sub * EPC) = knu;
+    *reinterpret_cast<uint4*>(vc + (rh + p) * HD + sub * EPC) = vnu;
+  }
+  float q[EPC];
+  {
+    const T* e = reinterpret_cast<const T*>(&qu);
+#pragma unroll
+    for (int t = 0; t < EPC; ++t) q[t] = ldf(e + t) * 0.125f;   // 1/sqrt(64), exact
+  }
+  const int nI = (p + 1 + 7) >> 3;
+  uint4 kr[DA5_MAXI], vr[DA5_MAXI];
+#pragma unroll
+  for (int i = 0; i < DA5_MAXI; ++i) {
+    const int j = i * 8 + grp;
+    kr[i] = make_uint4(0, 0, 0, 0);
+    vr[i] = make_uint4(0, 0, 0, 0);
+    if (i < nI && j < p) {
+      const long src = kvrow ? ((long)kvrow[(long)r * Lmax + j] * heads + h) * Lmax : rh;
+      kr[i] = *reinterpret_cast<const uint4*>(kc + (src + j) * HD + sub * EPC);
+      vr[i] = *reinterpret_cast<const uint4*>(vc + (src + j) * HD + sub * EPC);
+    } else if (j == p) {
+      kr[i] = knu;
+      vr[i] = vnu;
+    }
+  }
+  float sc[DA5_MAXI];
+  float mx = -INFINITY;
+#pragma unroll
+  for (int i = 0; i < DA5_MAXI; ++i) {
+    const T* e = reinterpret_cast<const T*>(&kr[i]);
+    float s = 0.f;
+#pragma unroll
+    for (int t = 0; t < EPC; ++t) s += q[t] * ldf(e + t);
+    s += __shfl_xor(s, 1, 64);
+    s += __shfl_xor(s, 2, 64);
+    s += __shfl_xor(s, 4, 64);
+    sc[i] = (i * 8 + grp <= p) ? s : -INFINITY;
+    mx = fmaxf(mx, sc[i]);
+  }
+  mx = fmaxf(mx, __shfl_xor(mx, 8, 64));
+  mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+  mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+  float sum = 0.f, o[EPC];
+#pragma unroll
+  for (int t = 0; t < EPC; ++t) o[t] = 0.f;
+#pragma unroll
+  for (int i = 0; i < DA5_MAXI; ++i) {
+    const float e = (i * 8 + grp <= p) ? expf(sc[i] - mx) : 0.f;
+    sum += e;
+    const T* v = reinterpret_cast<const T*>(&vr[i]);
+#pragma unroll
+    for (int t = 0; t < EPC; ++t) o[t] += e * ldf(v + t);
+  }
+#pragma unroll
+  for (int d = 8; d < 64; d <<= 1) {
+    sum += __shfl_xor(sum, d, 64);
+#pragma unroll
+    for (int t = 0; t < EPC; ++t) o[t] += __shfl_xor(o[t], d, 64);
+  }
+  if (grp == 0) {
+    const float inv = 1.0f / sum;
+    uint4 ou;
+    T* oe = reinterpret_cast<T*>(&ou);
+#pragma unroll
+    for (int t = 0; t < EPC; ++t) stf(oe + t, o[t] * inv);
+    *reinterpret_cast<uint4*>(out + (long)r * D + h * HD + sub * EPC) = ou;
+  }
+}
+
 template <typename T>
 __global__ __launch_bounds__(64) void decode_attn_kernel(const T* __restrict__ qkv, int D,
                                                          int heads, T* __restrict__ kc,
@@ -343,6 +443,13 @@ extern "C" int zs_decode_attention(const void* qkv, int R, int D, int heads, voi
              "zs_decode_attention: head_dim must be 64");
   ZS_REQUIRE(Lmax > 0 && Lmax <= 4096, "zs_decode_attention: Lmax");
   dim3 grid(R, heads);
+  if (dtype == ZS_BF16 && Lmax <= 8 * DA5_MAXI && g_decode_attn5) {
+    hipLaunchKernelGGL(decode_attn5_kernel<bf16_t>, dim3(R, cdiv(heads, 4)), dim3(256), 0,
+                       S(stream), (const bf16_t*)qkv, D, heads, (bf16_t*)kc, (bf16_t*)vc, Lmax,
+                       pos, kvrow, (bf16_t*)out);
+    ZS_LAUNCH_CHECK();
+    return 0;
+  }
   if (Lmax <= 512) {
     const size_t smem = (400 + 66 * (size_t)Lmax) * sizeof(float);
     if (dtype == ZS_BF16)

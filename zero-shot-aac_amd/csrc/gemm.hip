@@ -9,9 +9,11 @@
 // v_mfma_f32_32x32x2f32 with lane-half h owning k in [16h,16h+16) so both dtypes share one LDS
 // image ([row][32 + 16B pad], read 16 B per lane).  Global->LDS is register staged and double
 // buffered (next tile's loads issued before the current tile's MFMAs).
-#include "gemm_core.h"
+#include "gemm_fast.h"
 
 namespace zs {
+
+int g_gemm_fast = 1;   // zs_tune_set("gemm_fast", 0) selects the register-staged bf16 loop
 
 __device__ __forceinline__ void store_out(void* out, int out_dtype, long idx, float v) {
   if (out_dtype == ZS_BF16) reinterpret_cast<bf16_t*>(out)[idx] = f2bf(v);
@@ -67,6 +69,62 @@ __global__ void splitk_reduce_kernel(GemmArgs g) {
   store_out(g.out, g.out_dtype, (long)m * g.ldo + n, v);
 }
 
+// bf16: the LDS-DMA staged main loop (gemm_fast.h), same epilogue as gemm_kernel
+template <int BM, int BN, int NS>
+__global__ __launch_bounds__(256) void gemm_fast_kernel(GemmArgs g) {
+  __shared__ __attribute__((aligned(16))) char lds[NS * FastTile<BM, BN>::STAGE];
+  constexpr int TM = BM / 64, TN = BN / 64;
+  const int n0 = blockIdx.x * BN, m0 = blockIdx.y * BM, z = blockIdx.z;
+  const int kbeg = z * g.k_per_split, kend = min(g.K, kbeg + g.k_per_split);
+  f32x16_t acc[TM][TN];
+  const DenseRows A{(const bf16_t*)g.A, g.lda, g.M, m0};
+  const DenseRows B{(const bf16_t*)g.W, g.ldw, g.N, n0};
+  fast_mainloop<BM, BN, NS>(A, B, kbeg, kend, lds, acc);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int wr0 = (wid >> 1) * (BM / 2), wc0 = (wid & 1) * (BN / 2);
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int n = n0 + wc0 + j * 32 + (lane & 31);
+      if (n >= g.N) continue;
+      const float bias = (g.split_k == 1 && g.bias) ? g.bias[n] : 0.f;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int m = m0 + wr0 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5);
+        if (m >= g.M) continue;
+        float v = acc[i][j][e];
+        if (g.split_k > 1) {
+          g.ws[((long)z * g.M + m) * g.N + n] = v;
+        } else {
+          v = act_apply(v + bias, g.act);
+          if (g.residual) v += g.residual[(long)m * g.ldr + n];
+          store_out(g.out, g.out_dtype, (long)m * g.ldo + n, v);
+        }
+      }
+    }
+}
+
+template <int BM, int BN, int NS>
+static int launch_fast(GemmArgs& g, hipStream_t st) {
+  dim3 grid(cdiv(g.N, BN), cdiv(g.M, BM), g.split_k);
+  hipLaunchKernelGGL((gemm_fast_kernel<BM, BN, NS>), grid, dim3(256), 0, st, g);
+  ZS_LAUNCH_CHECK();
+  return 0;
+}
+
+static long nblocks(const GemmArgs& g, int bm, int bn) {
+  return (long)cdiv(g.M, bm) * cdiv(g.N, bn) * g.split_k;
+}
+
+// largest tile that still puts >= 1 block on every CU, else the smallest
+static int dispatch_fast(GemmArgs& g, hipStream_t st) {
+  if (nblocks(g, 128, 128) >= 256) return launch_fast<128, 128, 2>(g, st);
+  if (nblocks(g, 128, 64) >= 256) return g.M >= g.N ? launch_fast<128, 64, 3>(g, st)
+                                                     : launch_fast<64, 128, 3>(g, st);
+  return launch_fast<64, 64, 4>(g, st);
+}
+
 template <typename T, int BM, int BN>
 static int launch_gemm(GemmArgs& g, hipStream_t st) {
   dim3 grid(cdiv(g.N, BN), cdiv(g.M, BM), g.split_k);
@@ -77,6 +135,7 @@ static int launch_gemm(GemmArgs& g, hipStream_t st) {
 
 template <typename T>
 static int dispatch_gemm(GemmArgs& g, hipStream_t st) {
+  if (sizeof(T) == 2 && g_gemm_fast) return dispatch_fast(g, st);
   const bool small_m = g.M <= 64;
   const bool wide_n = g.N >= 2048 && !small_m;
   if (small_m) return wide_n ? launch_gemm<T, 64, 128>(g, st) : launch_gemm<T, 64, 64>(g, st);
@@ -97,14 +156,23 @@ __global__ __launch_bounds__(256) void lmhead_kernel(int M, int K, int V, const 
   constexpr int TM = BM / 64, TN = LM_BN / 64;
   constexpr int SM_MAIN = 2 * (BM + LM_BN) * LDW * (int)sizeof(T);
   constexpr int SM_EPI = BM * (LM_BN + 1) * 4;
-  constexpr int SM = SM_MAIN > SM_EPI ? SM_MAIN : SM_EPI;
-  __shared__ __attribute__((aligned(16))) char smem_raw[SM];
-  __shared__ float inv_norm[BM];
+  constexpr bool FAST = sizeof(T) == 2;
+  constexpr int SM_LOOP = FAST ? 2 * FastTile<BM, LM_BN>::STAGE : SM_MAIN;
+  constexpr int SM = SM_LOOP > SM_EPI ? SM_LOOP : SM_EPI;
+  // ONE __shared__ array (a second object can de-pipeline the DMA loop: §5 item 4(a))
+  __shared__ __attribute__((aligned(16))) char smem_raw[SM + BM * 4];
+  float* inv_norm = reinterpret_cast<float*>(smem_raw + SM);
   const int n0 = blockIdx.x * LM_BN, m0 = blockIdx.y * BM;
   const int nblk = gridDim.x;
   f32x16_t acc[TM][TN];
-  DenseA<T, BM> la{A, lda, M, m0};
-  gemm_mainloop<T, BM, LM_BN>(la, W, K, V, n0, 0, K, (T*)smem_raw, acc);
+  if constexpr (FAST) {
+    const DenseRows ra{(const bf16_t*)A, lda, M, m0};
+    const DenseRows rw{(const bf16_t*)W, K, V, n0};
+    fast_mainloop<BM, LM_BN>(ra, rw, 0, K, smem_raw, acc);
+  } else {
+    DenseA<T, BM> la{A, lda, M, m0};
+    gemm_mainloop<T, BM, LM_BN>(la, W, K, V, n0, 0, K, (T*)smem_raw, acc);
+  }
   // row norms for get_prefix_tokens (normalize(a) . w == (a . w) / max(||a||, 1e-12))
   if (row_norm) {
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -234,7 +302,11 @@ extern "C" int zs_gemm(int M, int N, int K, int dtype, const void* A, int lda, c
   ZS_REQUIRE(dtype == ZS_F32 || dtype == ZS_BF16, "zs_gemm: dtype");
   if (M == 0) return 0;
   if (split_k == 0) {   // auto: weight-streaming skinny kernel for decode-sized M
-    if (M <= 64 && K % 64 == 0 && workspace != nullptr)
+    // M <= 64 always; up to 256 rows only where the tiled kernel has too few blocks to cover
+    // a long K (mproj-like shapes); everything else goes to the tiled kernel
+    const bool few_blocks = (long)cdiv(M, 64) * cdiv(N, 64) < 96 && K >= 2048;
+    const bool skinny = M <= 64 || (M <= 256 && (dtype != ZS_BF16 || !g_gemm_fast || few_blocks));
+    if (skinny && K % 64 == 0 && workspace != nullptr)
       return zs_gemm_skinny_internal(M, N, K, dtype, A, lda, W, ldw, bias, residual, ldr, out,
                                      ldo, out_dtype, act, workspace, stream);
     split_k = 1;

@@ -1,16 +1,21 @@
-// Skinny GEMM for M <= 64 (GPT-2 decode step, mapper, audio_proj): the weight matrix is streamed
-// from HBM exactly once by ~256-320 workgroups.
+// Weight-streaming GEMM for M <= 256 (GPT-2 decode step over up to 4 row blocks of 64, mapper,
+// audio_proj): the weight matrix is streamed from HBM once per launch by ~256-1152 workgroups.
 //
-//   grid = (ceil(N/32) column tiles) x (splits of K);  block = 4 waves;
+//   work unit = (32-column tile, K split, 64-row block);  block = 4 waves;
 //   wave w of a workgroup owns k in [k0 + w*KS/4, k0 + (w+1)*KS/4) and computes the full 64x32
 //   partial with two 32x32 MFMA tiles, loading its A and W fragments straight from global into
 //   registers (all k-steps issued up front: no LDS round trip for a once-read operand,
 //   cdna_hip_programming.md §5 "GEMV / M <= 16" row);
 //   the 4 wave partials are summed through LDS in wave order; with splits > 1 each workgroup
-//   stores its 64x32 f32 slab, and the LAST arriving workgroup of the column tile (agent-scope
-//   release/acquire + relaxed counter, cdna_hip_programming.md §5 "In-launch split-K reduction")
-//   sums the slabs in split order — deterministic, no atomics on data — and applies the epilogue
-//   (bias, activation, residual, dtype) exactly like zs_gemm.
+//   stores its 64x32 f32 slab, and the LAST arriving workgroup of the (row block, column tile)
+//   (sc1 write-through slabs + relaxed agent-scope counter, cdna_hip_programming.md §5
+//   "In-launch split-K reduction") sums the slabs in split order — deterministic, no atomics on
+//   data — and applies the epilogue (bias, activation, residual, dtype) exactly like zs_gemm.
+//   Every row's arithmetic (K partition, summation order) depends only on (N, K), never on M or
+//   on the row block, so a clip's results do not depend on how many clips share the launch.
+//   The row blocks of one (tile, split) are consecutive work units and the linear block id is
+//   remapped bijectively so that consecutive units run on the same XCD (each XCD has its own
+//   L2): the W slice they share is fetched from HBM once per XCD.
 #include <cstring>
 #include "common.h"
 
@@ -24,17 +29,19 @@ constexpr int SK_TILE = 64 * SK_BN;     // floats per slab
 // workspace = [SK_MAX_TILES int counters (fixed, so no GEMM shape ever places slabs over another
 // shape's counters)][slabs]
 constexpr int SK_MAX_TILES = 4096;
+constexpr int SK_MAX_M = 256;           // up to 4 row blocks of 64
 
 struct SkinnyArgs {
   int M, N, K, lda, ldw, ldr, ldo, splits, ks;   // ks = K per workgroup
+  int rblocks, ntiles;                            // 64-row blocks, 32-column tiles
   const void* A;
   const void* W;
   const float* bias;
   const float* residual;
   void* out;
   int out_dtype, act;
-  int* counters;      // [ntiles], zero on first use, reset by the reducer
-  float* slabs;       // [splits][ntiles][64*32]
+  int* counters;      // [rblocks][ntiles], zero on first use, reset by the reducer
+  float* slabs;       // [rblocks][splits][ntiles][64*32]
 };
 
 // per-wave partial over kw..kw+len (len % 16 == 0), bf16
@@ -122,15 +129,22 @@ typedef __attribute__((ext_vector_type(4))) unsigned int u32x4_t;
 template <typename T, int MODE>
 __global__ __launch_bounds__(256) void gemm_skinny_kernel(SkinnyArgs g) {
   __shared__ __attribute__((aligned(16))) float red[4 * SK_TILE + 4];   // wave partials + flag
-  const int tile = blockIdx.x, z = blockIdx.y;
+  // XCD-aware bijective remap (cdna_hip_programming.md §5 "XCD swizzle must be bijective"):
+  // blocks id, id+8, id+16, ... share an XCD; give them consecutive work units
+  const int nwg = gridDim.x, id = blockIdx.x, xcd = id & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int u = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (id >> 3);
+  const int rb = u % g.rblocks, rest = u / g.rblocks;
+  const int z = rest % g.splits, tile = rest / g.splits;
   const int n0 = tile * SK_BN;
   const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int kq = g.ks / 4;
   const int kw = z * g.ks + wid * kq;
+  const int Mr = min(64, g.M - rb * 64);           // rows of this block
   f32x16s_t c0, c1;
 #pragma unroll
   for (int e = 0; e < 16; ++e) { c0[e] = 0.f; c1[e] = 0.f; }
-  wave_partial((const T*)g.A, g.lda, g.M, (const T*)g.W, g.ldw, g.N, n0, kw, kq, c0, c1);
+  wave_partial((const T*)g.A + (long)rb * 64 * g.lda, g.lda, Mr, (const T*)g.W, g.ldw, g.N, n0,
+               kw, kq, c0, c1);
   // wave partial -> LDS [wave][row][col]
   float* mine = red + wid * SK_TILE;
 #pragma unroll
@@ -154,13 +168,15 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(SkinnyArgs g) {
   if (g.splits == 1) {
 #pragma unroll
     for (int i = 0; i < PER; ++i)
-      if (m < g.M && nb + i < g.N) skinny_store(g, m, nb + i, part[i]);
+      if (m < Mr && nb + i < g.N) skinny_store(g, rb * 64 + m, nb + i, part[i]);
     return;
   }
-  const int ntiles = gridDim.x;
+  const int ntiles = g.ntiles;
+  float* slabs = g.slabs + (long)rb * g.splits * ntiles * SK_TILE;
+  int* counter = g.counters + rb * ntiles + tile;
   const long slab_off = ((long)z * ntiles + tile) * SK_TILE + e0;
   __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
-      g.slabs, (short)0, g.splits * ntiles * SK_TILE * 4, 0x00020000);
+      slabs, (short)0, g.splits * ntiles * SK_TILE * 4, 0x00020000);
   if (MODE == 1) {
 #pragma unroll
     for (int q = 0; q < PER / 4; ++q) {
@@ -171,7 +187,7 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(SkinnyArgs g) {
   } else {
 #pragma unroll
     for (int q = 0; q < PER / 4; ++q)
-      *reinterpret_cast<float4*>(g.slabs + slab_off + 4 * q) =
+      *reinterpret_cast<float4*>(slabs + slab_off + 4 * q) =
           make_float4(part[4 * q], part[4 * q + 1], part[4 * q + 2], part[4 * q + 3]);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -182,11 +198,10 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(SkinnyArgs g) {
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
-    const int old = __hip_atomic_fetch_add(&g.counters[tile], 1, __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_AGENT);
+    const int old = __hip_atomic_fetch_add(counter, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const int last = old == g.splits - 1;
     if (last) {
-      __hip_atomic_store(&g.counters[tile], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(counter, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (MODE == 0) {
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -209,17 +224,19 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(SkinnyArgs g) {
         f = make_float4(__uint_as_float(u.x), __uint_as_float(u.y), __uint_as_float(u.z),
                         __uint_as_float(u.w));
       } else {
-        f = *reinterpret_cast<const float4*>(g.slabs + off + 4 * q);
+        f = *reinterpret_cast<const float4*>(slabs + off + 4 * q);
       }
       v[4 * q] += f.x; v[4 * q + 1] += f.y; v[4 * q + 2] += f.z; v[4 * q + 3] += f.w;
     }
   }
 #pragma unroll
   for (int i = 0; i < PER; ++i)
-    if (m < g.M && nb + i < g.N) skinny_store(g, m, nb + i, v[i]);
+    if (m < Mr && nb + i < g.N) skinny_store(g, rb * 64 + m, nb + i, v[i]);
 }
 
 static int g_skinny_mode = 1;
+extern int g_gemm_fast;     // gemm.hip
+extern int g_decode_attn5;  // attn.hip
 
 // choose K per workgroup: a multiple of 64 dividing K, each wave <= 128 deep, ~256-320 WGs
 static int skinny_splits(int N, int K) {
@@ -243,16 +260,18 @@ using namespace zs;
 extern "C" int zs_tune_set(const char* key, int value) {
   if (!key) return ZS_ERR_ARG;
   if (!strcmp(key, "skinny_mode")) { g_skinny_mode = value; return 0; }
+  if (!strcmp(key, "gemm_fast")) { g_gemm_fast = value; return 0; }
+  if (!strcmp(key, "decode_attn5")) { g_decode_attn5 = value; return 0; }
   return fail(ZS_ERR_ARG, "zs_tune_set: unknown key %s", key);
 }
 
 extern "C" int zs_gemm_workspace_floats(int M, int N, int K) {
-  if (M > 64) return 0;
+  if (M <= 0 || M > SK_MAX_M) return 0;
   const int s = skinny_splits(N, K);
   if (s < 0) return 0;
-  const int ntiles = cdiv(N, SK_BN);
-  if (ntiles > SK_MAX_TILES) return 0;
-  return SK_MAX_TILES + s * ntiles * SK_TILE;
+  const int ntiles = cdiv(N, SK_BN), rb = cdiv(M, 64);
+  if (ntiles * rb > SK_MAX_TILES) return 0;
+  return SK_MAX_TILES + rb * s * ntiles * SK_TILE;
 }
 
 // internal entry used by zs_gemm for M <= 64 with split_k == 0 (auto)
@@ -260,16 +279,15 @@ extern "C" __attribute__((visibility("hidden"))) int zs_gemm_skinny_internal(int
                                        const void* W, int ldw, const float* bias,
                                        const float* residual, int ldr, void* out, int ldo,
                                        int out_dtype, int act, float* workspace, void* stream) {
-  ZS_REQUIRE(M > 0 && M <= 64, "skinny gemm: M <= 64");
+  ZS_REQUIRE(M > 0 && M <= SK_MAX_M, "skinny gemm: M <= %d", SK_MAX_M);
   const int s = skinny_splits(N, K);
   ZS_REQUIRE(s > 0, "skinny gemm: K=%d must be a multiple of 64", K);
-  const int ntiles = cdiv(N, SK_BN);
+  const int ntiles = cdiv(N, SK_BN), rb = cdiv(M, 64);
   ZS_REQUIRE(s == 1 || workspace != nullptr, "skinny gemm: needs the zeroed workspace");
-  ZS_REQUIRE(ntiles <= SK_MAX_TILES, "skinny gemm: N too large");
-  SkinnyArgs g{M, N, K, lda, ldw, ldr, ldo, s, K / s, A, W, bias, residual, out, out_dtype, act,
-               reinterpret_cast<int*>(workspace),
-               workspace + SK_MAX_TILES};
-  dim3 grid(ntiles, s);
+  ZS_REQUIRE(ntiles * rb <= SK_MAX_TILES, "skinny gemm: N too large");
+  SkinnyArgs g{M, N, K, lda, ldw, ldr, ldo, s, K / s, rb, ntiles, A, W, bias, residual, out,
+               out_dtype, act, reinterpret_cast<int*>(workspace), workspace + SK_MAX_TILES};
+  dim3 grid(ntiles * s * rb);
 #define SKL(T, MODE_) hipLaunchKernelGGL((gemm_skinny_kernel<T, MODE_>), grid, dim3(256), 0, S(stream), g)
   if (dtype == ZS_BF16) {
     if (g_skinny_mode == 1) SKL(bf16_t, 1); else SKL(bf16_t, 0);

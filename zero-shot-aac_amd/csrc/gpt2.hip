@@ -147,19 +147,22 @@ __global__ void argmax_finalize_kernel(const float* __restrict__ pv, const int* 
   if (lane == 0) idx[r] = t;
 }
 
-// one block (1024 threads = 16 waves) for all R rows
-__global__ __launch_bounds__(1024) void greedy_step_kernel(
+// one wave per row, 4 rows per block.  The blocks combine "rows still alive" and their arrival
+// in ONE relaxed agent-scope atomic on all_done[1] (arrivals in the low 16 bits, alive rows in
+// the high 16): the block that draws the last ticket knows every block has read *step_ctr and
+// added its alive count, so it alone writes all_done[0], advances *step_ctr and re-arms the
+// counter (no data hand-off between blocks, so no release/acquire is needed).
+__global__ __launch_bounds__(256) void greedy_step_kernel(
     const float* __restrict__ pv, const int* __restrict__ pi, int R, int nblk, int* step_ctr,
     int max_steps, int stop0, int stop1, int* __restrict__ out_ids, int* __restrict__ out_len,
     int* __restrict__ done, int* __restrict__ pos, int* __restrict__ next_tok,
     int* __restrict__ all_done) {
-  __shared__ int s_step;
-  __shared__ int s_alive;
-  if (threadIdx.x == 0) { s_step = *step_ctr; s_alive = 0; }
-  __syncthreads();
-  const int step = s_step;
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
-  for (int r = wid; r < R; r += nw) {
+  __shared__ int s_alive[5];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int step = __hip_atomic_load(step_ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const int r = blockIdx.x * 4 + wid;
+  int alive = 0;
+  if (r < R) {
     const int t = row_argmax(pv, pi, r, nblk, lane);
     if (lane == 0) {
       int d = done[r];
@@ -169,15 +172,23 @@ __global__ __launch_bounds__(1024) void greedy_step_kernel(
         if (t == stop0 || t == stop1) d = 1;
         done[r] = d;
       }
-      if (!d) atomicAdd(&s_alive, 1);
+      alive = !d;
       next_tok[r] = t;
       if (step < max_steps) pos[r] += 1;   // past entry_length the graph tail re-runs in place
     }
   }
+  if (lane == 0) s_alive[wid] = alive;
   __syncthreads();
   if (threadIdx.x == 0) {
-    *step_ctr = step + 1;
-    all_done[0] = (s_alive == 0 || step + 1 >= max_steps) ? 1 : 0;
+    const int a = s_alive[0] + s_alive[1] + s_alive[2] + s_alive[3];
+    const int old = __hip_atomic_fetch_add(&all_done[1], 1 + (a << 16), __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+    if ((old & 0xffff) == (int)gridDim.x - 1) {
+      const int total = (old >> 16) + a;
+      all_done[0] = (total == 0 || step + 1 >= max_steps) ? 1 : 0;
+      __hip_atomic_store(step_ctr, step + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&all_done[1], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
   }
 }
 
@@ -415,8 +426,8 @@ extern "C" int zs_greedy_step(const float* part_val, const int* part_idx, int R,
                               int* step_ctr, int max_steps, int stop0, int stop1, int* out_ids,
                               int* out_len, int* done, int* pos, int* next_tok, int* all_done,
                               void* stream) {
-  ZS_REQUIRE(R > 0 && nblk > 0 && max_steps > 0, "zs_greedy_step: bad shape");
-  hipLaunchKernelGGL(greedy_step_kernel, dim3(1), dim3(1024), 0, S(stream), part_val, part_idx, R,
+  ZS_REQUIRE(R > 0 && R < 65536 && nblk > 0 && max_steps > 0, "zs_greedy_step: bad shape");
+  hipLaunchKernelGGL(greedy_step_kernel, dim3(cdiv(R, 4)), dim3(256), 0, S(stream), part_val, part_idx, R,
                      nblk, step_ctr, max_steps, stop0, stop1, out_ids, out_len, done, pos,
                      next_tok, all_done);
   ZS_LAUNCH_CHECK();

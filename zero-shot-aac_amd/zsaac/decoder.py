@@ -230,7 +230,7 @@ class Gpt2Decoder:
         self.out_ids = torch.zeros(self.R, max_steps, **i32)
         self.out_len = torch.zeros(self.R, **i32)
         self.step_ctr = torch.zeros(1, **i32)
-        self.all_done = torch.zeros(1, **i32)
+        self.all_done = torch.zeros(2, **i32)    # [flag, greedy_step arrival counter]
         self.plen = torch.zeros(self.Rp, **i32)
         self.last_row = torch.zeros(self.Rp, **i32)
         # beam state
@@ -328,7 +328,7 @@ class Gpt2Decoder:
         """Enqueue a copy of all_done to pinned host memory; returns (event, host tensor)."""
         if not hasattr(self, "_flag_host"):
             self._flag_host = torch.zeros(1, dtype=torch.int32, pin_memory=True)
-        self._flag_host.copy_(self.all_done, non_blocking=True)
+        self._flag_host.copy_(self.all_done[:1], non_blocking=True)
         ev = torch.cuda.Event()
         ev.record()
         return ev, self._flag_host
@@ -336,7 +336,7 @@ class Gpt2Decoder:
     def run_to_completion(self):
         """Synchronous loop: replay chunks until every row stopped or entry_length reached."""
         for _ in range(self.n_chunks):
-            if int(self.all_done.item()):
+            if int(self.all_done[0].item()):
                 break
             self.step_chunk()
 

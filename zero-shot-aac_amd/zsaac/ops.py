@@ -95,9 +95,12 @@ def _devkey(device):
     return dev
 
 
+SKINNY_MAX_M = 256     # gemm_skinny.hip SK_MAX_M (4 row blocks of 64)
+
+
 def reserve_skinny_workspace(device, M, N, K):
     """Allocate (once, zeroed, before any graph capture) the workspace the auto-mode skinny GEMM
-    (M <= 64) needs for this shape; shared by every skinny GEMM on the device's stream order."""
+    (M <= SKINNY_MAX_M) needs for this shape; shared by every skinny GEMM on the device's stream order."""
     need = call("zs_gemm_workspace_floats", M, N, K)
     dev = _devkey(device)
     cur = _SKINNY_WS.get(dev)
@@ -121,23 +124,27 @@ def skinny_workspace(device, shapes):
 
 def gemm(a, w, out, bias=None, residual=None, act=ACT_NONE, split_k=0, workspace=None, M=None):
     """out = act(a @ w.T + bias) + residual;  a [M,K], w [N,K] (same dtype), out f32/bf16.
-    split_k=0 (auto): M <= 64 uses the weight-streaming skinny kernel when a workspace was
-    reserved for the device (reserve_skinny_workspace), else the tiled kernel."""
+    split_k=0 (auto): M <= SKINNY_MAX_M uses the weight-streaming skinny kernel when a
+    workspace is given or was reserved for the device (reserve_skinny_workspace), else the tiled
+    kernel."""
     K = a.shape[-1]
     N = w.shape[0]
     M = M if M is not None else a.numel() // K
     _need(w.shape[1] == K and a.dtype == w.dtype, f"gemm: a{tuple(a.shape)} w{tuple(w.shape)}")
     _need(K % 32 == 0, f"gemm: K={K} must be a multiple of 32")
     if split_k == 0:
-        if workspace is None and M <= 64:
+        need = call("zs_gemm_workspace_floats", M, N, K) if M <= SKINNY_MAX_M else 0
+        if workspace is None and need:
             workspace = _SKINNY_WS.get(_devkey(a.device))
-            if workspace is not None and call("zs_gemm_workspace_floats", M, N, K) > workspace.numel():
+            if workspace is not None and need > workspace.numel():
                 workspace = None
+        elif workspace is not None and need > workspace.numel():
+            # an engine's private workspace is sized for its decode shapes: M <= 64 must fit,
+            # larger M simply takes the tiled kernel
+            _need(M > 64, f"gemm: workspace {workspace.numel()} < {need} floats")
+            workspace = None
         if workspace is None:
             split_k = 1
-        elif M <= 64:
-            need = call("zs_gemm_workspace_floats", M, N, K)
-            _need(need <= workspace.numel(), f"gemm: workspace {workspace.numel()} < {need} floats")
     lda = a.stride(-2) if a.dim() > 1 else K
     ldo = out.stride(-2) if out.dim() > 1 else N
     ldr = (residual.stride(-2) if residual.dim() > 1 else N) if residual is not None else 0

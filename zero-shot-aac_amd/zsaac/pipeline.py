@@ -222,6 +222,7 @@ class ConcurrentRunner:
             s.wait_stream(caller)
         active = {}
         nxt = 0
+        self.decode_steps = [0] * len(batches)     # per batch: decode steps actually enqueued
         while nxt < len(batches) or active:
             progressed = False
             for i, (p, s) in enumerate(zip(self.pipes, self.streams)):
@@ -240,6 +241,7 @@ class ConcurrentRunner:
                     continue
                 progressed = True
                 if int(flag[0]) or n >= p.decoder.n_chunks:
+                    self.decode_steps[bi] = 1 + n * p.decoder.chunk
                     with torch.cuda.stream(s):
                         r = p.result()
                         results[bi] = _copy_batch(r)
