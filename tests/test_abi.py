@@ -57,7 +57,10 @@ def test_load_and_error_path(libpath):
     with pytest.raises(_lib.ZsError):
         _lib.call("zs_tune_set", b"no_such_knob", 1)
     assert lib.zs_gemm_workspace_floats(64, 768, 3072) > 0
-    assert lib.zs_gemm_workspace_floats(128, 768, 3072) == 0
+    # 4 row blocks of 64: a 256-row launch needs 4x the slabs of a 64-row one (same counters)
+    w64, w256 = lib.zs_gemm_workspace_floats(64, 768, 3072), lib.zs_gemm_workspace_floats(256, 768, 3072)
+    assert w256 - 4096 == 4 * (w64 - 4096)
+    assert lib.zs_gemm_workspace_floats(257, 768, 3072) == 0
     assert lib.zs_lmhead_nblk(50257) == 393
 
 
