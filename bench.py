@@ -53,7 +53,10 @@ def parse():
     ap.add_argument("--mapper", default="mlp", choices=["mlp", "transformer"])
     ap.add_argument("--beam", type=int, default=0)
     ap.add_argument("--entry-length", type=int, default=67)
-    ap.add_argument("--inflight", type=int, default=4,
+    ap.add_argument("--group", type=int, default=16,
+                    help="eval batches of --batch clips decoded together (one decode step over "
+                         "group*batch rows); each is still encoded as its own batch")
+    ap.add_argument("--inflight", type=int, default=2,
                     help="independent bs=--batch batches decoding concurrently per GPU (streams)")
     ap.add_argument("--cpu-baseline-clips", type=int, default=2)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -87,7 +90,8 @@ def build(args, device):
     else:
         asd = S.cnn14_state_dict(4)
         asd.update(S.audio_proj_state_dict(5, audio_width=2048))
-    cfg = CaptionConfig(encoder=args.encoder, mapping_type=args.mapper, dtype=dtype, batch=args.batch,
+    cfg = CaptionConfig(encoder=args.encoder, mapping_type=args.mapper, dtype=dtype,
+                        batch=args.batch * getattr(args, "group", 1), encoder_batch=args.batch,
                         beam=args.beam, entry_length=args.entry_length)
     pipe = CaptionPipeline(csd, asd, S.label_table(), S.label_token_table(), cfg, device=device)
     return pipe, csd, asd
@@ -170,7 +174,7 @@ def stage_times(pipe, wav, reps=3):
     for _ in range(reps):
         ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
         ev[0].record()
-        emb = pipe.encoder.encode(wav)
+        emb = pipe.encode(wav)
         ev[1].record()
         ops.prompt_assemble(emb, pipe.labels, cfg.sound_effect_num, pipe.label_tok, pipe.label_len,
                             pipe.hard_ids[:B], pipe.hard_len[:B])
@@ -232,7 +236,7 @@ def main():
     device = torch.device("cuda", local)
     from zsaac import synthetic as S
     pipe, csd, asd = build(args, device)
-    B = args.batch
+    B = args.batch * args.group           # clips per step (group eval batches, decoded together)
     # input pool resident in HBM before timing: distinct synthetic clips per step and rank
     pool = []
     g = torch.Generator(device=device).manual_seed(1234 + rank)
@@ -296,8 +300,9 @@ def main():
                                + args.mapper + " mapper + GPT-2 small "
                                + ("greedy generate2" if not args.beam else f"beam {args.beam}")
                                + f", entry_length {args.entry_length}, + get_prefix_tokens",
+                   "eval_batch": args.batch, "eval_batches_per_step": args.group,
                    "batch_per_gpu": B, "global_batch": B * world,
-                   "batches_in_flight_per_gpu": max(1, args.inflight),
+                   "steps_in_flight_per_gpu": max(1, args.inflight),
                    "parallelism": f"dp{world} (clip-sharded, RCCL all-gather of token ids)",
                    "tokens_last_batch_rank0": ntok,
                    "decode_steps_mean": round(sum(runner.decode_steps) / max(1, len(runner.decode_steps)), 2)},

@@ -37,6 +37,9 @@ class CaptionConfig:
     beam: int = 0                     # 0 -> greedy generate2, else generate_beam(beam_size)
     prefix_tokens: bool = True        # also compute get_prefix_tokens (predict_prompt.py:137)
     use_graph: bool = True
+    encoder_batch: int = 64           # clips per encoder pass (the reference's eval batch size);
+                                      # a larger ``batch`` is encoded in chunks of this size and
+                                      # decoded together (clip results do not depend on it)
 
 
 @dataclass
@@ -83,7 +86,8 @@ class CaptionPipeline:
         dev = torch.device(device)
         self.dev = dev
         B = cfg.batch
-        self.encoder = AudioEncoder(audio_sd, cfg.encoder, cfg.dtype, B, dev) if audio_sd else None
+        eb = min(B, max(1, cfg.encoder_batch))
+        self.encoder = AudioEncoder(audio_sd, cfg.encoder, cfg.dtype, eb, dev) if audio_sd else None
         self.mapper = build_mapper(caption_sd, cfg.mapping_type, dev, cfg.dtype, B)
         self.gpt = Gpt2Weights(caption_sd, dev, cfg.dtype)
         self._setup_tables(label_table, label_tokens)
@@ -110,6 +114,7 @@ class CaptionPipeline:
         self.prefix = torch.empty(B, 1024, device=dev)
         self.embed = torch.empty(B * self.Pmax, 768, device=dev)
         self.prefix_ids = torch.zeros(B * self.Pmax, **i32)
+        self.emb_buf = torch.empty(B, 1024, device=dev)
 
     def _setup_tables(self, label_table, label_tokens):
         cfg, dev = self.cfg, self.dev
@@ -125,9 +130,19 @@ class CaptionPipeline:
         self.h_cap = 2 + k * mt + max(k - 1, 0) + 4 if k > 0 else 7
         self.Pmax = self.h_cap + cfg.prefix_length
 
-    def caption_wav(self, wav: torch.Tensor) -> CaptionBatch:
+    def encode(self, wav: torch.Tensor) -> torch.Tensor:
+        """CLAP embeddings [B, 1024] of a waveform batch, encoder_batch clips per pass."""
         assert self.encoder is not None, "no audio encoder weights"
-        return self.caption_emb(self.encoder.encode(wav))
+        B, eb = wav.shape[0], self.encoder.B
+        if B <= eb:
+            return self.encoder.encode(wav)
+        for c0 in range(0, B, eb):
+            c1 = min(B, c0 + eb)
+            self.emb_buf[c0:c1].copy_(self.encoder.encode(wav[c0:c1]))
+        return self.emb_buf[:B]
+
+    def caption_wav(self, wav: torch.Tensor) -> CaptionBatch:
+        return self.caption_emb(self.encode(wav))
 
     def caption_emb(self, emb: torch.Tensor) -> CaptionBatch:
         """From CLAP audio embeddings [B, 1024] (the pickle's ``audio_embedding``)."""
@@ -137,8 +152,7 @@ class CaptionPipeline:
 
     # ------------------------------------------------------------------ async (no host sync)
     def begin_wav(self, wav: torch.Tensor):
-        assert self.encoder is not None, "no audio encoder weights"
-        self.begin_emb(self.encoder.encode(wav))
+        self.begin_emb(self.encode(wav))
 
     def result(self) -> CaptionBatch:
         """Views of the current batch's outputs (valid until the next begin_*)."""
