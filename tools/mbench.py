@@ -104,16 +104,46 @@ def bench_gemm_htsat():
             a = torch.randn(Mr, K, device=dev).bfloat16()
             w = (torch.randn(N, K, device=dev) * 0.02).bfloat16()
             b = torch.randn(N, device=dev)
-            out = torch.empty(Mr, N, device=dev)
-            res = {"fast": timeit(lambda: ops.gemm(a, w, out, bias=b, split_k=1), reps=20)}
+            out = torch.empty(Mr, N, device=dev, dtype=torch.bfloat16)
+            res = {}
+            for t, nm in ((4, "128x128"), (5, "128/32x4"), (1, "256/32x4"), (6, "256/64x2"), (2, "256x128"), (3, "128x256")):
+                call("zs_tune_set", b"fast_tile", t)
+                res[nm] = timeit(lambda: ops.gemm(a, w, out, bias=b, split_k=1), reps=20)
+            call("zs_tune_set", b"fast_tile", 0)
             call("zs_tune_set", b"gemm_fast", 0)
             res["old"] = timeit(lambda: ops.gemm(a, w, out, bias=b, split_k=1), reps=20)
             call("zs_tune_set", b"gemm_fast", 1)
             res["torch"] = timeit(lambda: torch.nn.functional.linear(a, w, b.bfloat16()), reps=20)
-            byts = Mr * K * 2 + Mr * N * 4
             print(f"C{C:4d} M{Mr:7d} {name:6s} N{N:5d} K{K:5d}  " +
-                  "  ".join(f"{k}={v:8.2f}us" for k, v in res.items()) +
-                  f"  ({byts / res['fast'] / 1e3:6.0f} GB/s fast)", flush=True)
+                  "  ".join(f"{k}={v:8.2f}us" for k, v in res.items()), flush=True)
+
+
+def bench_gemm_dbg():
+    """Where the fast GEMM's time goes: full / no-MFMA / no-DMA at a few encoder shapes."""
+    from zsaac import ops
+    from zsaac._lib import call
+    dev = torch.device("cuda", 0)
+    shapes = [(4096, 2304, 768), (16384, 1152, 384), (65536, 768, 192), (262144, 288, 96),
+              (65536, 2304, 768)]
+    if os.environ.get("ZS_DBG_SHAPES"):
+        shapes = [tuple(int(x) for x in t.split("x")) for t in os.environ["ZS_DBG_SHAPES"].split(",")]
+    for M, N, K in shapes:
+        a = torch.randn(M, K, device=dev).bfloat16()
+        w = (torch.randn(N, K, device=dev) * 0.02).bfloat16()
+        out = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+        res = {}
+        for t, nm, pers in ((4, "128x128", 0), (4, "128x128P", 1), (1, "256x256P", 1)):
+            call("zs_tune_set", b"fast_tile", t)
+            call("zs_tune_set", b"fast_persist", pers)
+            for d, dn in ((0, "full"), (3, "noLoop"), (4, "noEpi")):
+                call("zs_tune_set", b"gemm_dbg", d)
+                res[f"{nm}/{dn}"] = timeit(lambda: ops.gemm(a, w, out, split_k=1), reps=20)
+        call("zs_tune_set", b"gemm_dbg", 0)
+        call("zs_tune_set", b"fast_tile", 0)
+        call("zs_tune_set", b"fast_persist", 1)
+        res["torch"] = timeit(lambda: torch.nn.functional.linear(a, w), reps=20)
+        print(f"M{M:6d} N{N:5d} K{K:4d} " + "  ".join(f"{k}={v:7.1f}" for k, v in res.items()),
+              flush=True)
 
 
 def bench_attn():
@@ -163,4 +193,4 @@ def bench_inflight():
 if __name__ == "__main__":
     which = sys.argv[1:] or ["gemm", "attn"]
     for wname in which:
-        {"gemm": bench_gemm, "gemm_m": bench_gemm_m, "gemm_htsat": bench_gemm_htsat, "attn": bench_attn, "inflight": bench_inflight}[wname]()
+        {"gemm": bench_gemm, "gemm_m": bench_gemm_m, "gemm_htsat": bench_gemm_htsat, "gemm_dbg": bench_gemm_dbg, "attn": bench_attn, "inflight": bench_inflight}[wname]()

@@ -28,7 +28,7 @@ int fail(int code, const char* fmt, ...);
 #define ZS_LAUNCH_CHECK() ZS_CHECK_HIP(hipGetLastError())
 
 inline hipStream_t S(void* s) { return reinterpret_cast<hipStream_t>(s); }
-inline int cdiv(long a, long b) { return (int)((a + b - 1) / b); }
+__host__ __device__ inline int cdiv(long a, long b) { return (int)((a + b - 1) / b); }
 
 // ---------------------------------------------------------------- bf16 helpers
 typedef uint16_t bf16_t;  // storage type (raw bits)

@@ -9,11 +9,13 @@
 // v_mfma_f32_32x32x2f32 with lane-half h owning k in [16h,16h+16) so both dtypes share one LDS
 // image ([row][32 + 16B pad], read 16 B per lane).  Global->LDS is register staged and double
 // buffered (next tile's loads issued before the current tile's MFMAs).
+#include <algorithm>
 #include "gemm_fast.h"
 
 namespace zs {
 
 int g_gemm_fast = 1;   // zs_tune_set("gemm_fast", 0) selects the register-staged bf16 loop
+int g_gemm_dbg = 0;
 
 __device__ __forceinline__ void store_out(void* out, int out_dtype, long idx, float v) {
   if (out_dtype == ZS_BF16) reinterpret_cast<bf16_t*>(out)[idx] = f2bf(v);
@@ -69,46 +71,150 @@ __global__ void splitk_reduce_kernel(GemmArgs g) {
   store_out(g.out, g.out_dtype, (long)m * g.ldo + n, v);
 }
 
-// bf16: the LDS-DMA staged main loop (gemm_fast.h), same epilogue as gemm_kernel
-template <int BM, int BN, int NS>
-__global__ __launch_bounds__(256) void gemm_fast_kernel(GemmArgs g) {
-  __shared__ __attribute__((aligned(16))) char lds[NS * FastTile<BM, BN>::STAGE];
-  constexpr int TM = BM / 64, TN = BN / 64;
-  const int n0 = blockIdx.x * BN, m0 = blockIdx.y * BM, z = blockIdx.z;
+// One wave's parked [32][WN] f32 slab -> out rows mr0..mr0+31, cols nc0..nc0+WN-1: each lane
+// owns 8 consecutive columns (two ds_read_b128), so bias / residual loads and the bf16 store are
+// 16 B per lane over contiguous row segments; ACT is a template parameter (no per-element switch).
+template <int ACT, int WN>
+__device__ __forceinline__ void epi_slab(const GemmArgs& g, const float* slab, int mr0, int nc0,
+                                         int z, bool vec_out, bool vec_res) {
+  constexpr int Q = WN / 8;
+  const int lane = threadIdx.x & 63;
+  for (int idx = lane; idx < 32 * Q; idx += 64) {
+    const int r = idx / Q, c = (idx % Q) * 8;
+    const int m = mr0 + r, n = nc0 + c;
+    if (m >= g.M || n >= g.N) continue;
+    const float4 a0 = *reinterpret_cast<const float4*>(slab + r * WN + c);
+    const float4 a1 = *reinterpret_cast<const float4*>(slab + r * WN + c + 4);
+    float v[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+    const int nv = min(8, g.N - n);
+    const bool full = nv == 8;
+    if (g.split_k > 1) {
+      float* dst = g.ws + ((long)z * g.M + m) * g.N + n;
+      if (full && g.N % 4 == 0) {
+        reinterpret_cast<float4*>(dst)[0] = make_float4(v[0], v[1], v[2], v[3]);
+        reinterpret_cast<float4*>(dst)[1] = make_float4(v[4], v[5], v[6], v[7]);
+      } else {
+        for (int q = 0; q < nv; ++q) dst[q] = v[q];
+      }
+      continue;
+    }
+    if (g.bias) {
+      if (full && ((uintptr_t)g.bias & 15) == 0) {
+        const float4 b0 = reinterpret_cast<const float4*>(g.bias + n)[0];
+        const float4 b1 = reinterpret_cast<const float4*>(g.bias + n)[1];
+        v[0] += b0.x; v[1] += b0.y; v[2] += b0.z; v[3] += b0.w;
+        v[4] += b1.x; v[5] += b1.y; v[6] += b1.z; v[7] += b1.w;
+      } else {
+        for (int q = 0; q < nv; ++q) v[q] += g.bias[n + q];
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < 8; ++q) v[q] = act_apply(v[q], ACT);
+    if (g.residual) {
+      const float* rp = g.residual + (long)m * g.ldr + n;
+      if (full && vec_res) {
+        const float4 r0 = reinterpret_cast<const float4*>(rp)[0];
+        const float4 r1 = reinterpret_cast<const float4*>(rp)[1];
+        v[0] += r0.x; v[1] += r0.y; v[2] += r0.z; v[3] += r0.w;
+        v[4] += r1.x; v[5] += r1.y; v[6] += r1.z; v[7] += r1.w;
+      } else {
+        for (int q = 0; q < nv; ++q) v[q] += rp[q];
+      }
+    }
+    const long o = (long)m * g.ldo + n;
+    if (full && vec_out) {
+      if (g.out_dtype == ZS_BF16) {
+        uint4 u;
+        u.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+        u.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+        u.z = (uint32_t)f2bf(v[4]) | ((uint32_t)f2bf(v[5]) << 16);
+        u.w = (uint32_t)f2bf(v[6]) | ((uint32_t)f2bf(v[7]) << 16);
+        *reinterpret_cast<uint4*>(reinterpret_cast<bf16_t*>(g.out) + o) = u;
+      } else {
+        float4* d = reinterpret_cast<float4*>(reinterpret_cast<float*>(g.out) + o);
+        d[0] = make_float4(v[0], v[1], v[2], v[3]);
+        d[1] = make_float4(v[4], v[5], v[6], v[7]);
+      }
+    } else {
+      for (int q = 0; q < nv; ++q) store_out(g.out, g.out_dtype, o + q, v[q]);
+    }
+  }
+}
+
+// bf16: the LDS-DMA staged main loop (gemm_fast.h).  Epilogue through LDS: each wave parks one
+// 32-row slab of its accumulators ([32][WN] f32, static register indexing), then re-reads it
+// row-wise so every lane owns 4 consecutive columns: bias / activation / residual / store move
+// 16 B (f32) or 8 B (bf16) per lane in full rows instead of 2-4 B column-strided scalars.
+template <int BM, int BN, int NS, int WGM, int WGN, int BK_>
+__global__ __launch_bounds__(64 * WGM * WGN) void gemm_fast_kernel(GemmArgs g) {
+  using FT = FastTile<BM, BN, WGM, WGN, BK_>;
+  __shared__ __attribute__((aligned(16))) char lds[NS * FT::STAGE];
+  constexpr int TM = FT::TM, TN = FT::TN, WN = FT::WN;
+  static_assert(FT::NW * 32 * WN * 4 <= NS * FT::STAGE, "epilogue slab must fit the stage ring");
+  // persistent: a grid of (CUs x resident blocks) walks the tiles (n fastest, then m, then the
+  // k split), so the per-workgroup dispatch cost is paid once per resident block, not per tile
+  const int ntn = cdiv(g.N, BN), ntm = cdiv(g.M, BM);
+  const int ntiles = ntn * ntm * g.split_k;
+  for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
+  const int n0 = (t % ntn) * BN, m0 = ((t / ntn) % ntm) * BM, z = t / (ntn * ntm);
   const int kbeg = z * g.k_per_split, kend = min(g.K, kbeg + g.k_per_split);
   f32x16_t acc[TM][TN];
   const DenseRows A{(const bf16_t*)g.A, g.lda, g.M, m0};
   const DenseRows B{(const bf16_t*)g.W, g.ldw, g.N, n0};
-  fast_mainloop<BM, BN, NS>(A, B, kbeg, kend, lds, acc);
+  fast_mainloop<BM, BN, NS, WGM, WGN, BK_>(A, B, kbeg, kend, lds, acc, g.dbg);   // ends with a barrier
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int wr0 = (wid >> 1) * (BM / 2), wc0 = (wid & 1) * (BN / 2);
+  const int wr0 = (wid / WGN) * FT::WM, wc0 = (wid % WGN) * WN;
+  float* slab = reinterpret_cast<float*>(lds) + wid * 32 * WN;
+  if (g.dbg == 4) {   // experiment: no epilogue (keep the accumulators alive)
+    float t = 0.f;
 #pragma unroll
-  for (int i = 0; i < TM; ++i)
+    for (int i = 0; i < TM; ++i)
 #pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const int n = n0 + wc0 + j * 32 + (lane & 31);
-      if (n >= g.N) continue;
-      const float bias = (g.split_k == 1 && g.bias) ? g.bias[n] : 0.f;
+      for (int j = 0; j < TN; ++j) t += acc[i][j][0];
+    if (t == 12345.f) reinterpret_cast<float*>(g.out)[0] = t;
+    continue;
+  }
+  // 16-byte stores need 8-element (bf16) / 4-element (f32) aligned rows and bias
+  const bool vec_out = (g.split_k > 1) ||
+                       (g.ldo % 8 == 0 && ((uintptr_t)g.out & 15) == 0);
+  const bool vec_res = g.residual == nullptr ||
+                       (g.ldr % 4 == 0 && ((uintptr_t)g.residual & 15) == 0);
 #pragma unroll
-      for (int e = 0; e < 16; ++e) {
-        const int m = m0 + wr0 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5);
-        if (m >= g.M) continue;
-        float v = acc[i][j][e];
-        if (g.split_k > 1) {
-          g.ws[((long)z * g.M + m) * g.N + n] = v;
-        } else {
-          v = act_apply(v + bias, g.act);
-          if (g.residual) v += g.residual[(long)m * g.ldr + n];
-          store_out(g.out, g.out_dtype, (long)m * g.ldo + n, v);
-        }
-      }
+  for (int i = 0; i < TM; ++i) {
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e)
+        slab[((e & 3) + 8 * (e >> 2) + 4 * (lane >> 5)) * WN + j * 32 + (lane & 31)] = acc[i][j][e];
+    // the slab is private to this wave and a wave's LDS accesses complete in issue order, so
+    // no barrier: a __syncthreads() here would also wait for every outstanding global store
+    // (vmcnt(0)) and serialise one full write round trip per row slab
+    const int mr0 = m0 + wr0 + i * 32, nc0 = n0 + wc0;
+    switch (g.act) {
+      case ACT_GELU_ERF: epi_slab<ACT_GELU_ERF, WN>(g, slab, mr0, nc0, z, vec_out, vec_res); break;
+      case ACT_GELU_TANH: epi_slab<ACT_GELU_TANH, WN>(g, slab, mr0, nc0, z, vec_out, vec_res); break;
+      case ACT_RELU: epi_slab<ACT_RELU, WN>(g, slab, mr0, nc0, z, vec_out, vec_res); break;
+      case ACT_TANH: epi_slab<ACT_TANH, WN>(g, slab, mr0, nc0, z, vec_out, vec_res); break;
+      default: epi_slab<ACT_NONE, WN>(g, slab, mr0, nc0, z, vec_out, vec_res); break;
     }
+  }
+  // every wave has read its slab before the next tile's DMAs refill the LDS (LDS-only wait:
+  // the stores stay in flight)
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  }
 }
 
-template <int BM, int BN, int NS>
+int g_fast_persist = 1;   // zs_tune_set("fast_persist", 0): one workgroup per tile
+
+template <int BM, int BN, int NS, int WGM = 2, int WGN = 2, int BK_ = 64>
 static int launch_fast(GemmArgs& g, hipStream_t st) {
-  dim3 grid(cdiv(g.N, BN), cdiv(g.M, BM), g.split_k);
-  hipLaunchKernelGGL((gemm_fast_kernel<BM, BN, NS>), grid, dim3(256), 0, st, g);
+  using FT = FastTile<BM, BN, WGM, WGN, BK_>;
+  const long nt = (long)cdiv(g.N, BN) * cdiv(g.M, BM) * g.split_k;
+  const int per_cu = max(1, min(160 * 1024 / (NS * FT::STAGE), 8 / FT::NW * 2));
+  dim3 grid(g_fast_persist ? (int)std::min<long>(nt, 256L * per_cu) : (int)nt);
+  hipLaunchKernelGGL((gemm_fast_kernel<BM, BN, NS, WGM, WGN, BK_>), grid, dim3(64 * WGM * WGN), 0,
+                     st, g);
   ZS_LAUNCH_CHECK();
   return 0;
 }
@@ -117,9 +223,25 @@ static long nblocks(const GemmArgs& g, int bm, int bn) {
   return (long)cdiv(g.M, bm) * cdiv(g.N, bn) * g.split_k;
 }
 
+int g_fast_ns = 2;     // zs_tune_set("fast_ns", n): stages of the 128x128 tile (experiment knob)
+int g_fast_tile = 0;   // zs_tune_set("fast_tile", t): force a tile (see dispatch_fast)
+
 // largest tile that still puts >= 1 block on every CU, else the smallest
 static int dispatch_fast(GemmArgs& g, hipStream_t st) {
-  if (nblocks(g, 128, 128) >= 256) return launch_fast<128, 128, 2>(g, st);
+  switch (g_fast_tile) {
+    case 1: return launch_fast<256, 256, 4, 2, 4, 32>(g, st);
+    case 2: return launch_fast<256, 128, 4, 4, 2, 32>(g, st);
+    case 3: return launch_fast<128, 256, 4, 2, 4, 32>(g, st);
+    case 4: return launch_fast<128, 128, 2>(g, st);
+    case 5: return launch_fast<128, 128, 4, 2, 2, 32>(g, st);
+    case 6: return launch_fast<256, 256, 2, 2, 4, 64>(g, st);
+    default: break;
+  }
+  if (nblocks(g, 128, 128) >= 256) {
+    if (g_fast_ns == 3) return launch_fast<128, 128, 3>(g, st);
+    if (g_fast_ns == 4) return launch_fast<128, 128, 4>(g, st);
+    return launch_fast<128, 128, 2>(g, st);
+  }
   if (nblocks(g, 128, 64) >= 256) return g.M >= g.N ? launch_fast<128, 64, 3>(g, st)
                                                      : launch_fast<64, 128, 3>(g, st);
   return launch_fast<64, 64, 4>(g, st);
@@ -157,7 +279,7 @@ __global__ __launch_bounds__(256) void lmhead_kernel(int M, int K, int V, const 
   constexpr int SM_MAIN = 2 * (BM + LM_BN) * LDW * (int)sizeof(T);
   constexpr int SM_EPI = BM * (LM_BN + 1) * 4;
   constexpr bool FAST = sizeof(T) == 2;
-  constexpr int SM_LOOP = FAST ? 2 * FastTile<BM, LM_BN>::STAGE : SM_MAIN;
+  constexpr int SM_LOOP = FAST ? 2 * FastTile<BM, LM_BN>::STAGE : SM_MAIN;  // 4 waves (2x2)
   constexpr int SM = SM_LOOP > SM_EPI ? SM_LOOP : SM_EPI;
   // ONE __shared__ array (a second object can de-pipeline the DMA loop: §5 item 4(a))
   __shared__ __attribute__((aligned(16))) char smem_raw[SM + BM * 4];
@@ -311,7 +433,8 @@ extern "C" int zs_gemm(int M, int N, int K, int dtype, const void* A, int lda, c
                                      ldo, out_dtype, act, workspace, stream);
     split_k = 1;
   }
-  GemmArgs g{M, N, K, lda, ldw, ldr, ldo, A, W, bias, residual, out, out_dtype, act, 1, K, workspace};
+  GemmArgs g{M, N, K, lda, ldw, ldr, ldo, A, W, bias, residual, out, out_dtype, act, 1, K, workspace,
+             g_gemm_dbg};
   if (split_k > 1) {
     int kps = cdiv(cdiv(K, split_k), BK) * BK;
     int s = cdiv(K, kps);

@@ -29,6 +29,7 @@ struct GemmArgs {
   void* out;
   int out_dtype, act, split_k, k_per_split;
   float* ws;
+  int dbg;   // experiment knob (zs_tune_set "gemm_dbg"): 1 = skip MFMA, 2 = skip DMA
 };
 
 // Loads a ROWS x 32 tile (row-major, K-contiguous) of a [nrows][ld] matrix into registers.

@@ -1,18 +1,17 @@
-// bf16 MFMA GEMM main loop staged by LDS-DMA (global_load_lds_dwordx4), BK = 64.
+// bf16 MFMA GEMM main loop staged by LDS-DMA (global_load_lds_dwordx4), BK = 32 or 64.
 //
-// One LDS stage holds the block's A rows [BM][64] and W rows [BN][64] as 128-byte rows.  A
-// glds wave-instruction writes 1 KiB lane-linearly (8 rows x 128 B: lane l -> row l/8, 16-byte
-// slot l%8), so the bank swizzle is applied on the SOURCE address: slot s of row r holds the
-// logical 16-byte chunk c = s ^ ((r >> 1) & 7), and the MFMA fragment read of chunk c of row r
-// reads slot c ^ ((r >> 1) & 7) — the same involution on both sides (cdna_hip_programming.md
-// §5.4 rule 21).  A 16-lane ds_read_b128 group reads 16 consecutive rows at one logical chunk;
-// (r & 1, (r >> 1) & 7) is then a bijection onto the 16 slots of the 256-byte bank row:
-// conflict-free.
+// One LDS stage holds the block's A rows [BM][BK] and W rows [BN][BK] as RB = 2*BK-byte rows.
+// A glds wave-instruction writes 1 KiB lane-linearly (1024/RB rows; lane l -> row l/(RB/16),
+// 16-byte slot l%(RB/16)), so the bank swizzle is applied on the SOURCE address: slot s of row r
+// holds the logical 16-byte chunk c = s ^ swz(r) with swz(r) = (r / (256/RB)) % (RB/16), and the
+// MFMA fragment read of chunk c of row r reads slot c ^ swz(r) — the same involution on both
+// sides (cdna_hip_programming.md §5.4 rule 21).  A 16-lane ds_read_b128 group reads 16
+// consecutive rows at one logical chunk; (r % (256/RB), swz(r)) is then a bijection onto the 16
+// slots of the 256-byte bank row: conflict-free (SQ_LDS_BANK_CONFLICT = 0 measured).
 //
-// Two stages: at the top of k-tile t one barrier (its implicit vmcnt(0) retires stage t's
-// DMAs, and every wave has finished reading stage t-1), then the DMAs of tile t+1 are issued
-// into the other stage and overlap tile t's MFMAs.  Out-of-range rows and the K tail read a
-// 16-byte zero chunk instead (no predicated DMA, no stale LDS), so any M, N and K % 32 == 0 work.
+// NS-stage ring with counted `s_waitcnt vmcnt` + raw s_barrier (see fast_mainloop).  Out-of-range
+// rows and the K tail read a 16-byte zero chunk instead (no predicated DMA, no stale LDS), so any
+// M, N and K % 32 == 0 work.
 #pragma once
 #include "gemm_core.h"
 
@@ -20,8 +19,6 @@ namespace zs {
 
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 typedef __attribute__((address_space(1))) void* gptr_t;
-
-constexpr int FBK = 64;   // k per stage
 
 static __device__ __attribute__((aligned(16))) uint4 g_zero_chunk[1];
 
@@ -37,61 +34,73 @@ struct DenseRows {
   }
 };
 
-__device__ __forceinline__ int fswz(int row) { return (row >> 1) & 7; }
-
-template <int BM, int BN>
+// BM x BN block tile computed by WGM x WGN waves, each owning a WM x WN = (BM/WGM) x (BN/WGN)
+// wave tile of TM x TN 32x32 MFMA fragments; k staged BK at a time
+template <int BM, int BN, int WGM = 2, int WGN = 2, int BK_ = 64>
 struct FastTile {
+  static constexpr int BKT = BK_;
+  static constexpr int RB = 2 * BK_;                // bytes per staged row
+  static constexpr int SPR = RB / 16;               // 16-byte slots per row
+  static constexpr int RPI = 1024 / RB;             // rows per DMA wave-instruction
+  static constexpr int RP256 = 256 / RB;            // rows per 256-byte bank row
+  static constexpr int NW = WGM * WGN;              // waves per block
   static constexpr int ROWS = BM + BN;
-  static constexpr int STAGE = ROWS * 128;          // bytes
-  static constexpr int NI = ROWS / 8;               // DMA instructions per stage
-  static_assert(NI % 4 == 0, "rows per stage must be a multiple of 32");
-  static constexpr int WM = BM / 2, WN = BN / 2;    // wave tile (2 x 2 waves)
+  static constexpr int STAGE = ROWS * RB;           // bytes
+  static constexpr int NI = ROWS / RPI;             // DMA instructions per stage
+  static_assert(BK_ == 32 || BK_ == 64, "BK");
+  static_assert(BM % (RPI * NW) == 0 && BN % (RPI * NW) == 0, "DMA rows per wave");
+  static constexpr int WM = BM / WGM, WN = BN / WGN;
   static constexpr int TM = WM / 32, TN = WN / 32;
   static_assert(TM >= 1 && TN >= 1, "wave tile >= 32x32");
+  __device__ static __forceinline__ int swz(int row) { return (row / RP256) % SPR; }
 };
 
-template <int BM, int BN, typename ASrc, typename BSrc>
-__device__ __forceinline__ void fast_issue(const ASrc& A, const BSrc& B, int k0, int kend,
-                                           char* stage) {
+template <int BM, int BN, int WGM, int WGN, int BK_, typename ASrc, typename BSrc>
+__device__ __forceinline__ void fast_issue_t(const ASrc& A, const BSrc& B, int k0, int kend,
+                                             char* stage) {
+  using FT = FastTile<BM, BN, WGM, WGN, BK_>;
+  constexpr int NW = FT::NW;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  // A rows: BM/8 wave-instructions, then W rows: BN/8 (both multiples of 4: no branch on A/W)
+  const int rsub = lane / FT::SPR, slot = lane % FT::SPR;
+  // A rows: BM/RPI wave-instructions, then W rows (both multiples of NW: no branch on A/W)
 #pragma unroll
-  for (int j = 0; j < BM / 32; ++j) {
-    const int i = wid + 4 * j;
-    const int row = 8 * i + (lane >> 3);
-    const int k = k0 + 8 * ((lane & 7) ^ fswz(row));
+  for (int j = 0; j < BM / (FT::RPI * NW); ++j) {
+    const int i = wid + NW * j;
+    const int row = FT::RPI * i + rsub;
+    const int k = k0 + 8 * (slot ^ FT::swz(row));
     __builtin_amdgcn_global_load_lds((gptr_t)A.chunk(row, k, kend), (lds_ptr_t)(stage + i * 1024),
                                      16, 0, 0);
   }
 #pragma unroll
-  for (int j = 0; j < BN / 32; ++j) {
-    const int i = BM / 8 + wid + 4 * j;
-    const int row = 8 * i + (lane >> 3);
-    const int k = k0 + 8 * ((lane & 7) ^ fswz(row));
+  for (int j = 0; j < BN / (FT::RPI * NW); ++j) {
+    const int i = BM / FT::RPI + wid + NW * j;
+    const int row = FT::RPI * i + rsub;
+    const int k = k0 + 8 * (slot ^ FT::swz(row));
     __builtin_amdgcn_global_load_lds((gptr_t)B.chunk(row - BM, k, kend),
                                      (lds_ptr_t)(stage + i * 1024), 16, 0, 0);
   }
 }
 
-template <int BM, int BN>
-__device__ __forceinline__ void fast_compute(const char* stage,
-                                             f32x16_t (&acc)[BM / 64][BN / 64]) {
-  using FT = FastTile<BM, BN>;
+template <int BM, int BN, int WGM, int WGN, int BK_>
+__device__ __forceinline__ void fast_compute(
+    const char* stage,
+    f32x16_t (&acc)[FastTile<BM, BN, WGM, WGN, BK_>::TM][FastTile<BM, BN, WGM, WGN, BK_>::TN]) {
+  using FT = FastTile<BM, BN, WGM, WGN, BK_>;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, r = lane & 31, h = lane >> 5;
-  const int wr0 = (wid >> 1) * FT::WM, wc0 = BM + (wid & 1) * FT::WN;
+  const int wr0 = (wid / WGN) * FT::WM, wc0 = BM + (wid % WGN) * FT::WN;
 #pragma unroll
-  for (int s = 0; s < FBK / 16; ++s) {
+  for (int s = 0; s < BK_ / 16; ++s) {
     const int c = 2 * s + h;
     bf16x8_t a[FT::TM], b[FT::TN];
 #pragma unroll
     for (int i = 0; i < FT::TM; ++i) {
       const int row = wr0 + i * 32 + r;
-      a[i] = *reinterpret_cast<const bf16x8_t*>(stage + row * 128 + 16 * (c ^ fswz(row)));
+      a[i] = *reinterpret_cast<const bf16x8_t*>(stage + row * FT::RB + 16 * (c ^ FT::swz(row)));
     }
 #pragma unroll
     for (int j = 0; j < FT::TN; ++j) {
       const int row = wc0 + j * 32 + r;
-      b[j] = *reinterpret_cast<const bf16x8_t*>(stage + row * 128 + 16 * (c ^ fswz(row)));
+      b[j] = *reinterpret_cast<const bf16x8_t*>(stage + row * FT::RB + 16 * (c ^ FT::swz(row)));
     }
 #pragma unroll
     for (int i = 0; i < FT::TM; ++i)
@@ -107,7 +116,7 @@ __device__ __forceinline__ void wait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-// acc[i][j] (wave tile (BM/2) x (BN/2) as TM x TN 32x32 fragments; the C/D layout of §3:
+// acc[i][j] (wave tile WM x WN as TM x TN 32x32 fragments; the C/D layout of §3:
 // col = lane & 31, row = (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5)) over k in [kbeg, kend).
 //
 // NS-stage ring: tiles t+1 .. t+NS-1 stay in flight while tile t is computed.  Per k-tile:
@@ -115,12 +124,16 @@ __device__ __forceinline__ void wait_vm() {
 // outstanding), a raw s_barrier (every wave's tile-t DMAs retired and every wave done reading
 // tile t-1, whose stage is refilled next), the DMAs of tile t+NS-1, then tile t's MFMAs.  A
 // __syncthreads() here would drain all DMAs (vmcnt(0)): cdna_hip_programming.md §5
-// "Pipelining across barriers".
-template <int BM, int BN, int NS = 2, typename ASrc, typename BSrc>
-__device__ __forceinline__ void fast_mainloop(const ASrc& A, const BSrc& B, int kbeg, int kend,
-                                              char* lds, f32x16_t (&acc)[BM / 64][BN / 64]) {
-  using FT = FastTile<BM, BN>;
-  constexpr int IPW = FT::NI / 4;                 // DMA instructions per wave per tile
+// "Pipelining across barriers".  Under full-chip streaming a DMA takes ~2-3 us to land, so the
+// ring depth (NS-1 tiles in flight), not the MFMA count, sets the k-loop rate.
+template <int BM, int BN, int NS = 2, int WGM = 2, int WGN = 2, int BK_ = 64, typename ASrc,
+          typename BSrc>
+__device__ __forceinline__ void fast_mainloop(
+    const ASrc& A, const BSrc& B, int kbeg, int kend, char* lds,
+    f32x16_t (&acc)[FastTile<BM, BN, WGM, WGN, BK_>::TM][FastTile<BM, BN, WGM, WGN, BK_>::TN],
+    int dbg = 0) {
+  using FT = FastTile<BM, BN, WGM, WGN, BK_>;
+  constexpr int IPW = FT::NI / FT::NW;            // DMA instructions per wave per tile
   static_assert(NS >= 2 && (NS - 2) * IPW < 64, "stages");
 #pragma unroll
   for (int i = 0; i < FT::TM; ++i)
@@ -128,22 +141,23 @@ __device__ __forceinline__ void fast_mainloop(const ASrc& A, const BSrc& B, int 
     for (int j = 0; j < FT::TN; ++j)
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
-  const int nk = (kend - kbeg + FBK - 1) / FBK;
+  const int nk = (kend - kbeg + BK_ - 1) / BK_;
   if (nk <= 0) return;
 #pragma unroll
   for (int p = 0; p < NS - 1; ++p)
-    if (p < nk) fast_issue<BM, BN>(A, B, kbeg + p * FBK, kend, lds + p * FT::STAGE);
+    if (p < nk)
+      fast_issue_t<BM, BN, WGM, WGN, BK_>(A, B, kbeg + p * BK_, kend, lds + p * FT::STAGE);
   int st = 0;                                     // stage of tile kt
   for (int kt = 0; kt < nk; ++kt) {
     if (kt + NS - 2 < nk) wait_vm<(NS - 2) * IPW>();   // tiles kt+1..kt+NS-2 may stay in flight
     else wait_vm<0>();
     __builtin_amdgcn_s_barrier();
     const int tn = kt + NS - 1;
-    if (tn < nk) {
+    if (tn < nk && dbg != 2 && dbg != 3) {
       const int sn = st == 0 ? NS - 1 : st - 1;   // (kt + NS - 1) % NS == stage of tile kt-1
-      fast_issue<BM, BN>(A, B, kbeg + tn * FBK, kend, lds + sn * FT::STAGE);
+      fast_issue_t<BM, BN, WGM, WGN, BK_>(A, B, kbeg + tn * BK_, kend, lds + sn * FT::STAGE);
     }
-    fast_compute<BM, BN>(lds + st * FT::STAGE, acc);
+    if (dbg != 1 && dbg != 3) fast_compute<BM, BN, WGM, WGN, BK_>(lds + st * FT::STAGE, acc);
     st = st == NS - 1 ? 0 : st + 1;
   }
   __syncthreads();   // callers may reuse the LDS for the epilogue
