@@ -285,12 +285,22 @@ def test_lmhead_topk(cuda, dtype):
     ops.argmax_finalize(pv1, pi1, M, nblk, am)
     if dtype == torch.float32:
         assert torch.equal(am.long(), logits.argmax(-1))
+    else:   # bf16 operands, f32 accumulation: the picked logit is the max up to rounding
+        picked = logits.gather(1, am.long()[:, None])[:, 0]
+        assert float((logits.max(-1).values - picked).max()) < 1e-3
+    # the topk-1 partials carry the same log-sum-exp (register epilogue in bf16)
+    mx1 = ps[..., 0].max(1).values
+    lse1 = mx1 + (ps[..., 1] * torch.exp(ps[..., 0] - mx1[:, None])).sum(1).log()
+    assert float((lse1 - torch.logsumexp(logits, -1)).abs().max()) < tol * 10
     # row-normalised variant (get_prefix_tokens)
     ops.lmhead_topk(a, w, 1, ps, pv1, pi1, row_norm=True)
     ops.argmax_finalize(pv1, pi1, M, nblk, am)
+    cos = torch.nn.functional.normalize(a.float(), dim=-1) @ w.float().t()
     if dtype == torch.float32:
-        ref2 = (torch.nn.functional.normalize(a.float(), dim=-1) @ w.float().t()).argmax(-1)
-        assert torch.equal(am.long(), ref2)
+        assert torch.equal(am.long(), cos.argmax(-1))
+    else:
+        picked = cos.gather(1, am.long()[:, None])[:, 0]
+        assert float((cos.max(-1).values - picked).max()) < 1e-4
 
 
 def test_logmel_vs_oracle(cuda):

@@ -146,6 +146,27 @@ def bench_gemm_dbg():
               flush=True)
 
 
+def bench_lmhead():
+    """LM head GEMM + fused row reductions at decode row counts (topk 1 greedy, 8 beam)."""
+    from zsaac import ops
+    dev = torch.device("cuda", 0)
+    V, K = 50257, 768
+    w = (torch.randn(V, K, device=dev) * 0.05).bfloat16()
+    nblk = ops.lmhead_nblk(V)
+    for M in (64, 256, 1024):
+        a = torch.randn(M, K, device=dev).bfloat16()
+        ps = torch.empty(M, nblk, 2, device=dev)
+        res = {}
+        for k in (1, 5):
+            pv = torch.empty(M, nblk, k, device=dev)
+            pi = torch.empty(M, nblk, k, device=dev, dtype=torch.int32)
+            res[f"topk{k}"] = timeit(lambda: ops.lmhead_topk(a, w, k, ps, pv, pi), reps=20)
+        res["torch_gemm"] = timeit(lambda: a @ w.t(), reps=20)
+        fl = 2 * M * V * K
+        print(f"lmhead M{M:5d} " + "  ".join(f"{k}={v:8.2f}us ({fl / v / 1e6:6.0f} TF/s)" for k, v in res.items()),
+              flush=True)
+
+
 def bench_attn():
     from zsaac import ops
     dev = torch.device("cuda", 0)
@@ -193,4 +214,4 @@ def bench_inflight():
 if __name__ == "__main__":
     which = sys.argv[1:] or ["gemm", "attn"]
     for wname in which:
-        {"gemm": bench_gemm, "gemm_m": bench_gemm_m, "gemm_htsat": bench_gemm_htsat, "gemm_dbg": bench_gemm_dbg, "attn": bench_attn, "inflight": bench_inflight}[wname]()
+        {"gemm": bench_gemm, "gemm_m": bench_gemm_m, "gemm_htsat": bench_gemm_htsat, "gemm_dbg": bench_gemm_dbg, "lmhead": bench_lmhead, "attn": bench_attn, "inflight": bench_inflight}[wname]()

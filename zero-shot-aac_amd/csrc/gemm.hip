@@ -287,7 +287,14 @@ __global__ __launch_bounds__(256) void lmhead_kernel(int M, int K, int V, const 
   const int n0 = blockIdx.x * LM_BN, m0 = blockIdx.y * BM;
   const int nblk = gridDim.x;
   f32x16_t acc[TM][TN];
-  if constexpr (FAST) {
+  // greedy / get_prefix_tokens (bf16, top-1): transposed product, vocab on the MFMA row axis,
+  // so a token's 128 logits of this block sit in registers of one lane pair (see below)
+  f32x16_t acct[LM_BN / 64][BM / 64];
+  if constexpr (FAST && KMAX == 1) {
+    const DenseRows ra{(const bf16_t*)A, lda, M, m0};
+    const DenseRows rw{(const bf16_t*)W, K, V, n0};
+    fast_mainloop<LM_BN, BM>(rw, ra, 0, K, smem_raw, acct);
+  } else if constexpr (FAST) {
     const DenseRows ra{(const bf16_t*)A, lda, M, m0};
     const DenseRows rw{(const bf16_t*)W, K, V, n0};
     fast_mainloop<BM, LM_BN>(ra, rw, 0, K, smem_raw, acc);
@@ -310,6 +317,68 @@ __global__ __launch_bounds__(256) void lmhead_kernel(int M, int K, int V, const 
     }
   }
   __syncthreads();
+  if constexpr (FAST && KMAX == 1) {
+    // acct[i][j][e]: vocab n0 + wr0 + i*32 + (e&3) + 8*(e>>2) + 4*(lane>>5), token
+    // m0 + wc0 + j*32 + (lane&31).  Per token: max / argmax / sum-exp over the lane's 32 vocab
+    // entries in registers, one xor-32 exchange with the partner lane, then the two waves that
+    // hold the other 64 vocab rows of the same tokens combine through LDS.  Ties keep the lower
+    // vocab index (torch argmax / the LDS path).
+    constexpr int TMV = LM_BN / 64, TNT = BM / 64;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int wr0 = (wid >> 1) * (LM_BN / 2), wc0 = (wid & 1) * (BM / 2), wg = wid >> 1;
+    float* xm = reinterpret_cast<float*>(smem_raw);          // [2][BM] max
+    float* xs = xm + 2 * BM;                                  // [2][BM] sum-exp
+    int* xi = reinterpret_cast<int*>(xs + 2 * BM);            // [2][BM] argmax
+#pragma unroll
+    for (int j = 0; j < TNT; ++j) {
+      const int r = wc0 + j * 32 + (lane & 31);                // token within the block
+      const float sc = row_norm ? inv_norm[r] : 1.0f;
+      float bv = -INFINITY;
+      int bi = 0x7fffffff;
+#pragma unroll
+      for (int i = 0; i < TMV; ++i)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int n = n0 + wr0 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5);
+          const float v = n < V ? acct[i][j][e] * sc : -INFINITY;
+          if (v > bv) { bv = v; bi = n; }      // n increases with (i, e): strict > keeps lower
+        }
+      {
+        const float ov = __shfl_xor(bv, 32, 64);
+        const int oi = __shfl_xor(bi, 32, 64);
+        if (ov > bv || (ov == bv && oi < bi)) { bv = ov; bi = oi; }
+      }
+      float se = 0.f;
+      if (bv != -INFINITY) {
+#pragma unroll
+        for (int i = 0; i < TMV; ++i)
+#pragma unroll
+          for (int e = 0; e < 16; ++e) {
+            const int n = n0 + wr0 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5);
+            if (n < V) se += expf(acct[i][j][e] * sc - bv);
+          }
+      }
+      se += __shfl_xor(se, 32, 64);
+      if (lane < 32) { xm[wg * BM + r] = bv; xs[wg * BM + r] = se; xi[wg * BM + r] = bi; }
+    }
+    __syncthreads();
+    for (int r = threadIdx.x; r < BM; r += 256) {
+      const int m = m0 + r;
+      if (m >= M) continue;
+      const float m0v = xm[r], m1v = xm[BM + r];
+      const int i0 = xi[r], i1 = xi[BM + r];
+      const float g = fmaxf(m0v, m1v);
+      const float se = (m0v == -INFINITY ? 0.f : xs[r] * expf(m0v - g)) +
+                       (m1v == -INFINITY ? 0.f : xs[BM + r] * expf(m1v - g));
+      const bool take1 = m1v > m0v || (m1v == m0v && i1 < i0);
+      const long o = (long)m * nblk + blockIdx.x;
+      part_stat[o * 2 + 0] = g;
+      part_stat[o * 2 + 1] = se;
+      part_val[o] = take1 ? m1v : m0v;
+      part_idx[o] = take1 ? i1 : i0;
+    }
+    return;
+  }
   float* tile = reinterpret_cast<float*>(smem_raw);   // [BM][LM_BN+1]
   {
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
