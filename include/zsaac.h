@@ -42,7 +42,7 @@ int zs_tune_set(const char* key, int value);  /* tuning knobs, e.g. "skinny_mode
  * 10*log10(max(x,1e-10))) fused with bn0 (htsat.py:949-951 / cnns.py:176-178):
  *   wav [B][T] f32 -> out [B][n_frames][64] f32, n_frames = T/hop + 1.
  * window[1024], twiddle[1024] = (cos, sin)(-2*pi*k/1024) interleaved for k < 512 (the DFT is a
- * radix-2 FFT in LDS: 1 block per frame), melW[64][513] (librosa.filters.mel, row m nonzero on
+ * radix-4 FFT in LDS, two real frames packed per complex FFT), melW[64][513] (librosa.filters.mel, row m nonzero on
  * [mel_lo[m], mel_hi[m])), bn_{mean,var,weight,bias}[64] (eval BatchNorm, eps 1e-5; pass NULL
  * bn_mean to skip bn0). */
 int zs_logmel(const float* wav, int B, int T, const float* window, const float* twiddle,

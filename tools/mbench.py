@@ -167,6 +167,28 @@ def bench_lmhead():
               flush=True)
 
 
+def bench_front():
+    """Front end + HTSAT edge kernels for one 64-clip batch."""
+    from zsaac import ops
+    from zsaac.frontend import make_tables
+    dev = torch.device("cuda", 0)
+    B = 64
+    wav = (torch.randn(B, 320000, device=dev) * 0.1).clamp_(-1, 1)
+    tabs = make_tables(dev)
+    lm = torch.empty(B, 1001, 64, device=dev)
+    print(f"logmel B64:      {timeit(lambda: ops.logmel(wav, tabs, out=lm), reps=10):8.1f}us", flush=True)
+    img = torch.empty(B, 256, 256, device=dev)
+    print(f"wav2img B64:     {timeit(lambda: ops.wav2img(lm, out=img), reps=10):8.1f}us", flush=True)
+    w, b = torch.randn(96, 16, device=dev), torch.randn(96, device=dev)
+    lw, lb = torch.randn(96, device=dev), torch.randn(96, device=dev)
+    x = torch.empty(B * 4096, 96, device=dev)
+    print(f"patch_embed B64: {timeit(lambda: ops.patch_embed(img, w, b, lw, lb, out=x), reps=10):8.1f}us", flush=True)
+    xs = torch.randn(B * 64, 768, device=dev)
+    lw2, lb2 = torch.randn(768, device=dev), torch.randn(768, device=dev)
+    feat = torch.empty(B, 768, device=dev)
+    print(f"ln_meanpool B64: {timeit(lambda: ops.ln_meanpool(xs, B, 64, 768, lw2, lb2, feat), reps=10):8.1f}us", flush=True)
+
+
 def bench_attn():
     from zsaac import ops
     dev = torch.device("cuda", 0)
@@ -214,4 +236,4 @@ def bench_inflight():
 if __name__ == "__main__":
     which = sys.argv[1:] or ["gemm", "attn"]
     for wname in which:
-        {"gemm": bench_gemm, "gemm_m": bench_gemm_m, "gemm_htsat": bench_gemm_htsat, "gemm_dbg": bench_gemm_dbg, "lmhead": bench_lmhead, "attn": bench_attn, "inflight": bench_inflight}[wname]()
+        {"gemm": bench_gemm, "gemm_m": bench_gemm_m, "gemm_htsat": bench_gemm_htsat, "gemm_dbg": bench_gemm_dbg, "lmhead": bench_lmhead, "front": bench_front, "attn": bench_attn, "inflight": bench_inflight}[wname]()

@@ -2,62 +2,143 @@
 // LogmelFilterBank, retrieval/models/feature_extractor.py:16-38; bn0 htsat.py:949-951), the
 // HTSAT bicubic resize + fold (htsat.py:908-923) and PatchEmbed + LayerNorm (htsat.py:115-125).
 //
-// STFT: one 256-thread block per frame; the reflect-padded, Hann-windowed 1024-sample frame is
-// loaded (coalesced) into LDS in bit-reversed order, transformed with a radix-2 complex FFT
-// (10 stages, 2 butterflies/thread/stage, twiddles from a host table), |X_k|^2 for k <= 512, then
-// 64 threads contract the power spectrum with their mel filter's nonzero band.
+// STFT: one 256-thread block per LM_PAIRS pairs of frames: two real, reflect-padded,
+// Hann-windowed 1024-sample frames are packed as z = a + i*b, loaded (coalesced) into padded LDS
+// rows in natural order and transformed with a radix-4 decimation-in-frequency complex FFT (5
+// stages, one radix-4 butterfly per thread per pair per stage, twiddles from a host table staged
+// in LDS; the output lands in base-4 digit-reversed order); the two spectra are
+// separated as A_k = (Z_k + conj Z_{N-k})/2, B_k = (Z_k - conj Z_{N-k})/2i, |.|^2 for k <= 512,
+// then 64 threads per frame contract the power spectrum with their mel filter's nonzero band.
 #include "common.h"
 
 namespace zs {
 
 constexpr int NFFT = 1024, HOP = 320, NMEL = 64, NBIN = NFFT / 2 + 1;
 
+__device__ __forceinline__ int digrev4(int n) {   // reverse the 5 base-4 digits of n < 1024
+  int r = 0;
+#pragma unroll
+  for (int d = 0; d < 5; ++d) { r = (r << 2) | (n & 3); n >>= 2; }
+  return r;
+}
+
+constexpr int LM_PAIRS = 2;               // frame pairs (complex FFTs) per 256-thread block
+constexpr int LPAD = NFFT + NFFT / 16;     // padded LDS row: element i lives at i + i/16
+__device__ __forceinline__ int lp(int i) { return i + (i >> 4); }
+
 __global__ __launch_bounds__(256) void logmel_kernel(
-    const float* __restrict__ wav, int T, int n_frames, const float* __restrict__ window,
-    const float* __restrict__ twiddle, const float* __restrict__ melW,
-    const int* __restrict__ mel_lo, const int* __restrict__ mel_hi,
+    const float* __restrict__ wav, int T, int n_frames, int total_frames,
+    const float* __restrict__ window, const float* __restrict__ twiddle,
+    const float* __restrict__ melW, const int* __restrict__ mel_lo, const int* __restrict__ mel_hi,
     const float* __restrict__ bn_mean, const float* __restrict__ bn_var,
     const float* __restrict__ bn_w, const float* __restrict__ bn_b, float* __restrict__ out) {
-  __shared__ float re[NFFT], im[NFFT];
-  __shared__ float pw[NBIN];
-  const int f = blockIdx.x % n_frames, b = blockIdx.x / n_frames;
-  const float* x = wav + (long)b * T;
-  const int start = f * HOP - NFFT / 2;
-  for (int n = threadIdx.x; n < NFFT; n += 256) {
-    int o = start + n;
-    if (o < 0) o = -o;                       // reflect (no edge repeat), torch F.pad 'reflect'
-    if (o >= T) o = 2 * (T - 1) - o;
-    const float v = x[o] * window[n];
-    const int rev = __brev(n) >> (32 - 10);
-    re[rev] = v;
-    im[rev] = 0.f;
+  constexpr int NP = LM_PAIRS;
+  __shared__ float re[NP][LPAD], im[NP][LPAD];
+  __shared__ float tw[NFFT];              // (cos, sin)(-2 pi k / 1024), k < 512
+  __shared__ float mw[2 * NBIN];          // the mel filters' nonzero bands, packed
+  __shared__ float pw[2 * NP][NBIN];
+  __shared__ int moff[NMEL + 1], mlo[NMEL];
+  const int g0 = 2 * NP * blockIdx.x;     // flattened (clip, frame) index of the first frame
+  for (int n = threadIdx.x; n < NFFT; n += 256) tw[n] = twiddle[n];
+  if (threadIdx.x < 64) {                 // band offsets: wave-wide inclusive scan of the widths
+    const int m = threadIdx.x;
+    const int lo = mel_lo[m], len = mel_hi[m] - lo;
+    int inc = len;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const int o = __shfl_up(inc, d, 64);
+      if (m >= d) inc += o;
+    }
+    mlo[m] = lo;
+    moff[m + 1] = inc;
+    if (m == 0) moff[0] = 0;
+  }
+  // natural-order load (coalesced global reads, conflict-free LDS writes)
+  for (int n = threadIdx.x; n < NP * NFFT; n += 256) {
+    const int p = n / NFFT, k = n % NFFT;
+    float v[2];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int g = g0 + 2 * p + q;
+      v[q] = 0.f;
+      if (g < total_frames) {
+        const int b = g / n_frames, f = g % n_frames;
+        int o = f * HOP - NFFT / 2 + k;
+        if (o < 0) o = -o;                       // reflect (no edge repeat), torch F.pad 'reflect'
+        if (o >= T) o = 2 * (T - 1) - o;
+        v[q] = wav[(long)b * T + o] * window[k];
+      }
+    }
+    re[p][lp(k)] = v[0];
+    im[p][lp(k)] = v[1];
   }
   __syncthreads();
-  // iterative radix-2 DIT: stage with half-size `half`, twiddle stride NFFT/(2*half)
-  for (int half = 1; half < NFFT; half <<= 1) {
-    const int tstride = NFFT / (2 * half);
-    for (int bf = threadIdx.x; bf < NFFT / 2; bf += 256) {
-      const int grp = bf / half, j = bf % half;
-      const int i0 = grp * 2 * half + j, i1 = i0 + half;
-      const float wr = twiddle[2 * (j * tstride)], wi = twiddle[2 * (j * tstride) + 1];
-      const float xr = re[i1], xi = im[i1];
-      const float tr = xr * wr - xi * wi, ti = xr * wi + xi * wr;
-      const float ur = re[i0], ui = im[i0];
-      re[i0] = ur + tr; im[i0] = ui + ti;
-      re[i1] = ur - tr; im[i1] = ui - ti;
+  {   // pack the bands: 4 threads per mel filter
+    const int m = threadIdx.x >> 2, s0 = threadIdx.x & 3;
+    const int lo = mlo[m], len = moff[m + 1] - moff[m];
+    for (int k = s0; k < len; k += 4) mw[moff[m] + k] = melW[m * NBIN + lo + k];
+  }
+  // radix-4 DIF (natural-order in, base-4 digit-reversed out):
+  // y0 = x0+x1+x2+x3, y1 = (x0-x2) - i(x1-x3), y2 = (x0+x2) - (x1+x3), y3 = (x0-x2) + i(x1-x3),
+  // then y_p *= W_{4L}^{p j} = W_1024^{p j S}
+  for (int L = NFFT / 4, S = 1; L >= 1; L >>= 2, S <<= 2) {
+    const int bf = threadIdx.x, grp = bf / L, j = bf % L;
+    const int i0 = grp * 4 * L + j;
+    float wr[4], wi[4];
+#pragma unroll
+    for (int q = 1; q < 4; ++q) {
+      const int e = j * q * S;                   // < 768
+      if (e < 512) { wr[q] = tw[2 * e]; wi[q] = tw[2 * e + 1]; }
+      else { wr[q] = -tw[2 * (e - 512)]; wi[q] = -tw[2 * (e - 512) + 1]; }
+    }
+    float xr[NP][4], xi[NP][4];
+#pragma unroll
+    for (int p = 0; p < NP; ++p)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) { xr[p][q] = re[p][lp(i0 + q * L)]; xi[p][q] = im[p][lp(i0 + q * L)]; }
+    __syncthreads();
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+      const float s02r = xr[p][0] + xr[p][2], s02i = xi[p][0] + xi[p][2];
+      const float d02r = xr[p][0] - xr[p][2], d02i = xi[p][0] - xi[p][2];
+      const float s13r = xr[p][1] + xr[p][3], s13i = xi[p][1] + xi[p][3];
+      const float d13r = xr[p][1] - xr[p][3], d13i = xi[p][1] - xi[p][3];
+      float yr[4], yi[4];
+      yr[0] = s02r + s13r; yi[0] = s02i + s13i;
+      yr[1] = d02r + d13i; yi[1] = d02i - d13r;
+      yr[2] = s02r - s13r; yi[2] = s02i - s13i;
+      yr[3] = d02r - d13i; yi[3] = d02i + d13r;
+      re[p][lp(i0)] = yr[0];
+      im[p][lp(i0)] = yi[0];
+#pragma unroll
+      for (int q = 1; q < 4; ++q) {
+        re[p][lp(i0 + q * L)] = yr[q] * wr[q] - yi[q] * wi[q];
+        im[p][lp(i0 + q * L)] = yr[q] * wi[q] + yi[q] * wr[q];
+      }
     }
     __syncthreads();
   }
-  for (int k = threadIdx.x; k < NBIN; k += 256) pw[k] = re[k] * re[k] + im[k] * im[k];
+  // X[k] sits at digrev4(k); separate the two real spectra, |.|^2 for k <= 512
+  for (int n = threadIdx.x; n < NP * NBIN; n += 256) {
+    const int p = n / NBIN, k = n % NBIN;
+    const int a = lp(digrev4(k)), c = lp(digrev4((NFFT - k) & (NFFT - 1)));
+    const float zr = re[p][a], zi = im[p][a], cr = re[p][c], ci = -im[p][c];   // conj Z_{N-k}
+    const float ar = zr + cr, ai = zi + ci;        // 2 A_k
+    const float br = zi - ci, bi = cr - zr;        // 2 B_k = (Z - conj Z_{N-k}) / i
+    pw[2 * p][k] = 0.25f * (ar * ar + ai * ai);
+    pw[2 * p + 1][k] = 0.25f * (br * br + bi * bi);
+  }
   __syncthreads();
-  if (threadIdx.x < NMEL) {
-    const int m = threadIdx.x;
-    const float* wrow = melW + m * NBIN;
+  for (int o = threadIdx.x; o < 2 * NP * NMEL; o += 256) {
+    const int fr = o / NMEL, m = o % NMEL;
+    const int g = g0 + fr;
+    if (g >= total_frames) continue;
+    const int lo = mlo[m], base = moff[m], len = moff[m + 1] - base;
     float acc = 0.f;
-    for (int k = mel_lo[m]; k < mel_hi[m]; ++k) acc += pw[k] * wrow[k];
+    for (int k = 0; k < len; ++k) acc += pw[fr][lo + k] * mw[base + k];
     float v = 10.0f * log10f(fmaxf(acc, 1e-10f));   // power_to_db, ref 1.0 -> offset 0
     if (bn_mean) v = (v - bn_mean[m]) / sqrtf(bn_var[m] + 1e-5f) * bn_w[m] + bn_b[m];
-    out[((long)b * n_frames + f) * NMEL + m] = v;
+    out[(long)g * NMEL + m] = v;
   }
 }
 
@@ -87,7 +168,9 @@ __global__ void wav2img_kernel(const float* __restrict__ in, int T_in, float* __
   img[e] = v;
 }
 
-// PatchEmbed: one wave per token; lanes own channels c = lane and lane+64 (< 96)
+// PatchEmbed: one thread per token (a 4x4 patch -> 96 channels in registers, LayerNorm in-thread);
+// 256 threads = 4 rows of the 64x64 patch grid, weights / bias / LN params broadcast from LDS.
+// A lane's 16 pixels are four 16-byte loads, contiguous across the wave.
 __global__ __launch_bounds__(256) void patch_embed_kernel(const float* __restrict__ img,
                                                           const float* __restrict__ w,
                                                           const float* __restrict__ bias,
@@ -95,38 +178,46 @@ __global__ __launch_bounds__(256) void patch_embed_kernel(const float* __restric
                                                           const float* __restrict__ lnb,
                                                           float* __restrict__ x, long ntok) {
   constexpr int C = 96;
-  const int lane = threadIdx.x & 63;
-  const long tok = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  __shared__ float sw[C * 16], sb[C], sg[C], sbeta[C];
+  for (int i = threadIdx.x; i < C * 16; i += 256) sw[i] = w[i];
+  if (threadIdx.x < C) {
+    sb[threadIdx.x] = bias[threadIdx.x];
+    sg[threadIdx.x] = lnw[threadIdx.x];
+    sbeta[threadIdx.x] = lnb[threadIdx.x];
+  }
+  __syncthreads();
+  const long tok = (long)blockIdx.x * 256 + threadIdx.x;
   if (tok >= ntok) return;
   const int b = tok / 4096, t = tok % 4096, ph = t / 64, pwc = t % 64;
   const float* base = img + (long)b * 65536 + (ph * 4) * 256 + pwc * 4;
   float px[16];
 #pragma unroll
-  for (int ky = 0; ky < 4; ++ky)
-#pragma unroll
-    for (int kx = 0; kx < 4; ++kx) px[ky * 4 + kx] = base[ky * 256 + kx];
-  float v0 = 0.f, v1 = 0.f;
-  {
-    const float* wr = w + lane * 16;
-    float a = bias[lane];
-#pragma unroll
-    for (int q = 0; q < 16; ++q) a += wr[q] * px[q];
-    v0 = a;
+  for (int ky = 0; ky < 4; ++ky) {
+    const float4 r = *reinterpret_cast<const float4*>(base + ky * 256);
+    px[ky * 4 + 0] = r.x; px[ky * 4 + 1] = r.y; px[ky * 4 + 2] = r.z; px[ky * 4 + 3] = r.w;
   }
-  const bool has1 = lane + 64 < C;
-  if (has1) {
-    const float* wr = w + (lane + 64) * 16;
-    float a = bias[lane + 64];
+  float v[C];
+  float sum = 0.f;
 #pragma unroll
-    for (int q = 0; q < 16; ++q) a += wr[q] * px[q];
-    v1 = a;
+  for (int c = 0; c < C; ++c) {
+    float a = sb[c];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) a += sw[c * 16 + q] * px[q];
+    v[c] = a;
+    sum += a;
   }
-  const float mean = wave_sum(v0 + (has1 ? v1 : 0.f)) / C;
-  const float d0 = v0 - mean, d1 = has1 ? v1 - mean : 0.f;
-  const float rstd = rsqrtf(wave_sum(d0 * d0 + d1 * d1) / C + 1e-5f);
-  float* xr = x + tok * C;
-  xr[lane] = d0 * rstd * lnw[lane] + lnb[lane];
-  if (has1) xr[lane + 64] = d1 * rstd * lnw[lane + 64] + lnb[lane + 64];
+  const float mean = sum / C;
+  float var = 0.f;
+#pragma unroll
+  for (int c = 0; c < C; ++c) { const float d = v[c] - mean; var += d * d; }
+  const float rstd = rsqrtf(var / C + 1e-5f);
+  float4* xr = reinterpret_cast<float4*>(x + tok * C);
+#pragma unroll
+  for (int c = 0; c < C; c += 4)
+    xr[c / 4] = make_float4((v[c] - mean) * rstd * sg[c] + sbeta[c],
+                            (v[c + 1] - mean) * rstd * sg[c + 1] + sbeta[c + 1],
+                            (v[c + 2] - mean) * rstd * sg[c + 2] + sbeta[c + 2],
+                            (v[c + 3] - mean) * rstd * sg[c + 3] + sbeta[c + 3]);
 }
 
 }  // namespace zs
@@ -139,9 +230,10 @@ extern "C" int zs_logmel(const float* wav, int B, int T, const float* window, co
                          const float* bn_bias, float* out, void* stream) {
   ZS_REQUIRE(B > 0 && T > NFFT / 2, "zs_logmel: need T > 512 samples for reflect padding");
   const int n_frames = T / HOP + 1;
-  hipLaunchKernelGGL(logmel_kernel, dim3((long)B * n_frames), dim3(256), 0, S(stream), wav, T,
-                     n_frames, window, twiddle, melW, mel_lo, mel_hi, bn_mean, bn_var, bn_weight,
-                     bn_bias, out);
+  const int total = B * n_frames;
+  hipLaunchKernelGGL(logmel_kernel, dim3(cdiv(total, 2 * LM_PAIRS)), dim3(256), 0, S(stream), wav, T,
+                     n_frames, total, window, twiddle, melW, mel_lo, mel_hi, bn_mean, bn_var,
+                     bn_weight, bn_bias, out);
   ZS_LAUNCH_CHECK();
   return 0;
 }
@@ -158,7 +250,7 @@ extern "C" int zs_patch_embed(const float* img, int B, const float* w, const flo
                               const float* ln_w, const float* ln_b, float* x, void* stream) {
   ZS_REQUIRE(B > 0, "zs_patch_embed: B");
   const long ntok = (long)B * 4096;
-  hipLaunchKernelGGL(patch_embed_kernel, dim3(cdiv(ntok, 4)), dim3(256), 0, S(stream), img, w, b,
+  hipLaunchKernelGGL(patch_embed_kernel, dim3(cdiv(ntok, 256)), dim3(256), 0, S(stream), img, w, b,
                      ln_w, ln_b, x, ntok);
   ZS_LAUNCH_CHECK();
   return 0;

@@ -106,32 +106,55 @@ __global__ __launch_bounds__(256) void patch_merge_ln_kernel(const float* __rest
   for (int c = threadIdx.x; c < C4; c += 256) stf(yr + c, (src(c) - mean) * rstd * w[c] + b[c]);
 }
 
-// final LayerNorm + mean over N tokens (htsat.py:830,838-847): one block per clip
-__global__ __launch_bounds__(256) void ln_meanpool_kernel(const float* __restrict__ x, int N, int C,
-                                                          const float* __restrict__ w,
-                                                          const float* __restrict__ b,
-                                                          float* __restrict__ out) {
-  extern __shared__ float acc[];  // [4 waves][C]
+// final LayerNorm + mean over N tokens (htsat.py:830,838-847): one 1024-thread block per clip,
+// wave w normalises tokens w, w+16, ... with the row held in registers (CPL values per lane);
+// the 16 per-wave partial sums are added in wave order (deterministic).
+template <int CPL>
+__global__ __launch_bounds__(1024) void ln_meanpool_kernel(const float* __restrict__ x, int N,
+                                                           int C, const float* __restrict__ w,
+                                                           const float* __restrict__ b,
+                                                           float* __restrict__ out) {
+  extern __shared__ float part[];  // [16 waves][C]
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  for (int c = threadIdx.x; c < 4 * C; c += 256) acc[c] = 0.f;
-  __syncthreads();
+  float acc[CPL];
+#pragma unroll
+  for (int q = 0; q < CPL; ++q) acc[q] = 0.f;
   const float* xb = x + (long)blockIdx.x * N * C;
-  for (int t = wid; t < N; t += 4) {
+  for (int t = wid; t < N; t += 16) {
     const float* xr = xb + (long)t * C;
-    float s = 0.f;
-    for (int c = lane; c < C; c += 64) s += xr[c];
-    const float mean = wave_sum(s) / C;
-    float v = 0.f;
-    for (int c = lane; c < C; c += 64) {
-      float d = xr[c] - mean;
-      v += d * d;
+    float v[CPL], s = 0.f;
+#pragma unroll
+    for (int q = 0; q < CPL; ++q) {
+      const int c = lane + 64 * q;
+      v[q] = c < C ? xr[c] : 0.f;
+      s += v[q];
     }
-    const float rstd = rsqrtf(wave_sum(v) / C + 1e-5f);
-    for (int c = lane; c < C; c += 64) acc[wid * C + c] += (xr[c] - mean) * rstd * w[c] + b[c];
+    const float mean = wave_sum(s) / C;
+    float d2 = 0.f;
+#pragma unroll
+    for (int q = 0; q < CPL; ++q) {
+      const int c = lane + 64 * q;
+      const float d = c < C ? v[q] - mean : 0.f;
+      d2 += d * d;
+    }
+    const float rstd = rsqrtf(wave_sum(d2) / C + 1e-5f);
+#pragma unroll
+    for (int q = 0; q < CPL; ++q) {
+      const int c = lane + 64 * q;
+      if (c < C) acc[q] += (v[q] - mean) * rstd * w[c] + b[c];
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < CPL; ++q) {
+    const int c = lane + 64 * q;
+    if (c < C) part[wid * C + c] = acc[q];
   }
   __syncthreads();
-  for (int c = threadIdx.x; c < C; c += 256)
-    out[(long)blockIdx.x * C + c] = (acc[c] + acc[C + c] + acc[2 * C + c] + acc[3 * C + c]) / N;
+  for (int c = threadIdx.x; c < C; c += 1024) {
+    float s = 0.f;
+    for (int k = 0; k < 16; ++k) s += part[k * C + c];
+    out[(long)blockIdx.x * C + c] = s / N;
+  }
 }
 
 __global__ __launch_bounds__(256) void l2norm_kernel(const float* __restrict__ x, int M, int C,
@@ -201,9 +224,13 @@ extern "C" int zs_patch_merge_ln(const float* x, int B, int H, int W, int C, con
 
 extern "C" int zs_ln_meanpool(const float* x, int B, int N, int C, const float* ln_w,
                               const float* ln_b, float* out, void* stream) {
-  ZS_REQUIRE(B > 0 && N > 0 && C > 0 && C <= 4096, "zs_ln_meanpool: bad shape");
-  hipLaunchKernelGGL(ln_meanpool_kernel, dim3(B), dim3(256), 4 * C * sizeof(float), S(stream), x,
-                     N, C, ln_w, ln_b, out);
+  ZS_REQUIRE(B > 0 && N > 0 && C > 0 && C <= 2048, "zs_ln_meanpool: bad shape (C <= 2048)");
+  const size_t smem = 16 * C * sizeof(float);
+#define LMP(CPL_)                                                                              \
+  hipLaunchKernelGGL(ln_meanpool_kernel<CPL_>, dim3(B), dim3(1024), smem, S(stream), x, N, C,   \
+                     ln_w, ln_b, out)
+  if (C <= 256) LMP(4); else if (C <= 768) LMP(12); else LMP(32);
+#undef LMP
   ZS_LAUNCH_CHECK();
   return 0;
 }
