@@ -53,7 +53,7 @@ def parse():
     ap.add_argument("--mapper", default="mlp", choices=["mlp", "transformer"])
     ap.add_argument("--beam", type=int, default=0)
     ap.add_argument("--entry-length", type=int, default=67)
-    ap.add_argument("--group", type=int, default=16,
+    ap.add_argument("--group", type=int, default=32,
                     help="eval batches of --batch clips decoded together (one decode step over "
                          "group*batch rows); each is still encoded as its own batch")
     ap.add_argument("--inflight", type=int, default=2,

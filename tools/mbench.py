@@ -189,6 +189,28 @@ def bench_front():
     print(f"ln_meanpool B64: {timeit(lambda: ops.ln_meanpool(xs, B, 64, 768, lw2, lb2, feat), reps=10):8.1f}us", flush=True)
 
 
+def bench_window():
+    """HTSAT window attention per stage for one 64-clip batch: MFMA vs VALU kernel."""
+    from zsaac import ops
+    from zsaac._lib import call
+    dev = torch.device("cuda", 0)
+    B = 64
+    for res, heads, shift in ((64, 4, 4), (32, 8, 4), (16, 16, 4), (8, 32, 0)):
+        C = 24 * heads
+        qkv = torch.randn(B * res * res, 3 * C, device=dev).bfloat16()
+        table = torch.randn(225, heads, device=dev)
+        out = torch.empty(B * res * res, C, device=dev, dtype=torch.bfloat16)
+        res_t = {}
+        for v in (1, 0):
+            call("zs_tune_set", b"window_mfma", v)
+            res_t["mfma" if v else "valu"] = timeit(
+                lambda: ops.window_attention(qkv, B, res, res, C, heads, shift, table, out), reps=10)
+        call("zs_tune_set", b"window_mfma", 1)
+        byts = qkv.numel() * 2 + out.numel() * 2
+        print(f"window res{res:3d} heads{heads:3d} " + "  ".join(f"{k}={v:8.1f}us" for k, v in res_t.items())
+              + f"  ({byts / res_t['mfma'] / 1e3:6.0f} GB/s mfma)", flush=True)
+
+
 def bench_attn():
     from zsaac import ops
     dev = torch.device("cuda", 0)
@@ -236,4 +258,4 @@ def bench_inflight():
 if __name__ == "__main__":
     which = sys.argv[1:] or ["gemm", "attn"]
     for wname in which:
-        {"gemm": bench_gemm, "gemm_m": bench_gemm_m, "gemm_htsat": bench_gemm_htsat, "gemm_dbg": bench_gemm_dbg, "lmhead": bench_lmhead, "front": bench_front, "attn": bench_attn, "inflight": bench_inflight}[wname]()
+        {"gemm": bench_gemm, "gemm_m": bench_gemm_m, "gemm_htsat": bench_gemm_htsat, "gemm_dbg": bench_gemm_dbg, "lmhead": bench_lmhead, "front": bench_front, "window": bench_window, "attn": bench_attn, "inflight": bench_inflight}[wname]()

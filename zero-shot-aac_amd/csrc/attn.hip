@@ -9,7 +9,8 @@
 
 namespace zs {
 
-int g_decode_attn5 = 1;   // zs_tune_set("decode_attn5", 0): LDS-staged decode_attn4 for bf16
+int g_decode_attn5 = 1;
+int g_window_mfma = 1;    // zs_tune_set("window_mfma", 0): VALU window attention for bf16   // zs_tune_set("decode_attn5", 0): LDS-staged decode_attn4 for bf16
 
 // ------------------------------------------------------------------ HTSAT window attention
 // grid (B * nWh * nWw, heads), block 64: thread i = token i of the 8x8 window.
@@ -77,6 +78,171 @@ __global__ __launch_bounds__(64) void window_attn_kernel(const T* __restrict__ q
   T* orow = out + tok * C + head * HD;
 #pragma unroll
   for (int d = 0; d < HD; ++d) stf(orow + d, o[d]);
+}
+
+// MFMA window attention (bf16, head_dim <= 32, zero-padded to 32): one wave per (window, head).
+//   S^T[key][query] = K . Q^T           (2x2 tiles of v_mfma_f32_32x32x16_bf16, K-dim = head dim)
+//   + rel-pos bias + shift mask, softmax over keys per query column: a lane holds 32 of a query's
+//     64 keys, the other 32 sit in lane^32 (one xor-32 exchange)
+//   O^T[dim][query] = V^T . P^T         (P^T straight from the S^T accumulators as the B operand)
+// The accumulator's key order within a 16-deep k-step is {0-3, 8-11} for lane half 0 and
+// {4-7, 12-15} for half 1, so the A operand V^T is read with the same key permutation (the sum
+// over keys is order-free).  Q and K are staged [token][32] with the 16-byte slot XOR-swizzled by
+// (token >> 2) & 3; V^T [dim][64] with 8-byte key chunks XOR-swizzled by dim & 15: the fragment
+// reads are bank-conflict-free.  1/sqrt(hd) is applied to the scores (htsat.py:320 scales q).
+typedef __attribute__((ext_vector_type(8))) __bf16 wa_bf16x8_t;
+typedef __attribute__((ext_vector_type(16))) float wa_f32x16_t;
+constexpr int WA_NW = 4;   // windows-heads (waves) per block
+__global__ __launch_bounds__(64 * WA_NW) void window_attn_mfma_kernel(
+    const bf16_t* __restrict__ qkv, int H, int W, int C, int heads, int hd, int shift,
+    const float* __restrict__ table, bf16_t* __restrict__ out, int total) {
+  constexpr int WS = 8, N = 64;
+  __shared__ __attribute__((aligned(16))) bf16_t sQ[WA_NW][N * 32];
+  __shared__ __attribute__((aligned(16))) bf16_t sK[WA_NW][N * 32];
+  __shared__ __attribute__((aligned(16))) bf16_t sVt[WA_NW][32 * N];
+  __shared__ float sB[WA_NW][225];
+  __shared__ int sReg[WA_NW][N];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int item = blockIdx.x * WA_NW + wv;          // (window, head) index, head fastest
+  if (item >= total) return;
+  const int head = item % heads, win = item / heads;
+  const int nWw = W / WS, nWh = H / WS;
+  const int b = win / (nWh * nWw), wyx = win % (nWh * nWw), wy = wyx / nWw, wx = wyx % nWw;
+  bf16_t* Q = sQ[wv];
+  bf16_t* K = sK[wv];
+  bf16_t* Vt = sVt[wv];
+  float* Bt = sB[wv];
+  int* Rg = sReg[wv];
+  // ---- stage: lane = token of the window
+  {
+    const int i = lane, iy = i / WS, ix = i % WS;
+    const int sy = wy * WS + iy, sx = wx * WS + ix;           // coords in the rolled image
+    const int hh = (sy + shift) % H, ww = (sx + shift) % W;   // natural coords (roll(-shift))
+    const long tok = ((long)b * H + hh) * W + ww;
+    const bf16_t* row = qkv + tok * 3 * C + head * hd;
+    const int sw = (i >> 2) & 3;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      uint4 qv = make_uint4(0, 0, 0, 0), kv = make_uint4(0, 0, 0, 0);
+      if (8 * c < hd) {
+        qv = *reinterpret_cast<const uint4*>(row + 8 * c);
+        kv = *reinterpret_cast<const uint4*>(row + C + 8 * c);
+      }
+      *reinterpret_cast<uint4*>(Q + i * 32 + 8 * (c ^ sw)) = qv;
+      *reinterpret_cast<uint4*>(K + i * 32 + 8 * (c ^ sw)) = kv;
+    }
+    // V^T: element (d, key i) at row d, 4-key chunk (i/4) ^ (d & 15), slot i % 4
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      uint4 vv = make_uint4(0, 0, 0, 0);
+      if (8 * c < hd) vv = *reinterpret_cast<const uint4*>(row + 2 * C + 8 * c);
+      const bf16_t* e = reinterpret_cast<const bf16_t*>(&vv);
+#pragma unroll
+      for (int t = 0; t < 8; ++t) {
+        const int d = 8 * c + t;
+        Vt[d * N + 4 * ((i >> 2) ^ (d & 15)) + (i & 3)] = e[t];
+      }
+    }
+    for (int r = lane; r < 225; r += 64) Bt[r] = table[r * heads + head];
+    int reg = 0;
+    if (shift > 0) {
+      const int ry = sy < H - WS ? 0 : (sy < H - shift ? 1 : 2);
+      const int rx = sx < W - WS ? 0 : (sx < W - shift ? 1 : 2);
+      reg = ry * 3 + rx;
+    }
+    Rg[i] = reg;
+  }
+  // the staged tiles are private to this wave: its LDS accesses complete in issue order
+  const int r = lane & 31, h = lane >> 5;
+  // ---- S^T = K . Q^T : tiles (key block kb, query block qb)
+  wa_f32x16_t st[2][2];
+#pragma unroll
+  for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+    for (int qb = 0; qb < 2; ++qb)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) st[kb][qb][e] = 0.f;
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) {                    // head-dim slices of 16
+    const int c = 2 * ks + h;                         // 16-byte slot of this lane half
+    wa_bf16x8_t a[2], bq[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int row = 32 * t + r;
+      a[t] = *reinterpret_cast<const wa_bf16x8_t*>(K + row * 32 + 8 * (c ^ ((row >> 2) & 3)));
+      bq[t] = *reinterpret_cast<const wa_bf16x8_t*>(Q + row * 32 + 8 * (c ^ ((row >> 2) & 3)));
+    }
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int qb = 0; qb < 2; ++qb)
+        st[kb][qb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[kb], bq[qb], st[kb][qb], 0, 0, 0);
+  }
+  // ---- bias + mask + softmax over keys (per query column)
+  const float scale = rsqrtf((float)hd);
+  wa_f32x16_t ot[2];
+#pragma unroll
+  for (int qb = 0; qb < 2; ++qb) {
+    const int qi = 32 * qb + r, qy = qi / WS, qx = qi % WS, qreg = Rg[qi];
+    float mx = -INFINITY;
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int kj = 32 * kb + (e & 3) + 8 * (e >> 2) + 4 * h, ky = kj / WS, kx = kj % WS;
+        float v = st[kb][qb][e] * scale + Bt[(qy - ky + WS - 1) * (2 * WS - 1) + (qx - kx + WS - 1)];
+        if (shift > 0 && Rg[kj] != qreg) v += -100.0f;
+        st[kb][qb][e] = v;
+        mx = fmaxf(mx, v);
+      }
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    float sum = 0.f;
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const float p = expf(st[kb][qb][e] - mx);
+        st[kb][qb][e] = p;
+        sum += p;
+      }
+    sum += __shfl_xor(sum, 32, 64);
+    // ---- O^T[dim][query] = V^T . P^T over 64 keys (4 k-steps of 16)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) ot[qb][e] = 0.f;
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        wa_bf16x8_t pb;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) pb[u] = (__bf16)st[kb][qb][8 * t + u];
+        // A: V^T rows d = r, keys 32kb + 16t + {0-3, 8-11} (+4 for half 1)
+        const int k0 = 32 * kb + 16 * t + 4 * h;
+        const int d = r;
+        typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4_t;
+        const bf16x4_t lo = *reinterpret_cast<const bf16x4_t*>(Vt + d * N + 4 * ((k0 >> 2) ^ (d & 15)));
+        const bf16x4_t hi = *reinterpret_cast<const bf16x4_t*>(Vt + d * N + 4 * (((k0 + 8) >> 2) ^ (d & 15)));
+        wa_bf16x8_t va;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) { va[u] = lo[u]; va[4 + u] = hi[u]; }
+        ot[qb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(va, pb, ot[qb], 0, 0, 0);
+      }
+    // ---- normalise and store: lane holds dims (e&3) + 8(e>>2) + 4h of query qi
+    const float inv = 1.0f / sum;
+    const int sy = wy * WS + qy, sx = wx * WS + qx;
+    const int hh = (sy + shift) % H, ww = (sx + shift) % W;
+    bf16_t* orow = out + (((long)b * H + hh) * W + ww) * C + head * hd;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int d0 = 8 * g + 4 * h;
+      if (d0 < hd) {
+        uint2 u;
+        u.x = (uint32_t)f2bf(ot[qb][4 * g] * inv) | ((uint32_t)f2bf(ot[qb][4 * g + 1] * inv) << 16);
+        u.y = (uint32_t)f2bf(ot[qb][4 * g + 2] * inv) | ((uint32_t)f2bf(ot[qb][4 * g + 3] * inv) << 16);
+        *reinterpret_cast<uint2*>(orow + d0) = u;
+      }
+    }
+  }
 }
 
 // ------------------------------------------------------------------ dense row attention
@@ -398,6 +564,14 @@ extern "C" int zs_window_attention(const void* qkv, int B, int H, int W, int C, 
   const int hd = C / heads;
   dim3 grid(B * (H / ws) * (W / ws), heads);
   hipStream_t st = S(stream);
+  if (dtype == ZS_BF16 && hd <= 32 && hd % 8 == 0 && g_window_mfma) {
+    const int total = B * (H / ws) * (W / ws) * heads;
+    hipLaunchKernelGGL(window_attn_mfma_kernel, dim3(cdiv(total, WA_NW)), dim3(64 * WA_NW), 0, st,
+                       (const bf16_t*)qkv, H, W, C, heads, hd, shift, rel_table, (bf16_t*)out,
+                       total);
+    ZS_LAUNCH_CHECK();
+    return 0;
+  }
 #define WA(T, HD_)                                                                             \
   hipLaunchKernelGGL((window_attn_kernel<T, HD_>), grid, dim3(64), 0, st, (const T*)qkv, H, W, C, \
                      heads, shift, rel_table, (T*)out)

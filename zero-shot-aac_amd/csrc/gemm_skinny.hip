@@ -237,6 +237,7 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(SkinnyArgs g) {
 static int g_skinny_mode = 1;
 extern int g_gemm_fast;     // gemm.hip
 extern int g_decode_attn5;  // attn.hip
+extern int g_window_mfma;   // attn.hip
 extern int g_fast_ns;       // gemm.hip
 extern int g_fast_tile;     // gemm.hip
 extern int g_gemm_dbg;      // gemm.hip
@@ -266,6 +267,7 @@ extern "C" int zs_tune_set(const char* key, int value) {
   if (!strcmp(key, "skinny_mode")) { g_skinny_mode = value; return 0; }
   if (!strcmp(key, "gemm_fast")) { g_gemm_fast = value; return 0; }
   if (!strcmp(key, "decode_attn5")) { g_decode_attn5 = value; return 0; }
+  if (!strcmp(key, "window_mfma")) { g_window_mfma = value; return 0; }
   if (!strcmp(key, "fast_ns")) { g_fast_ns = value; return 0; }
   if (!strcmp(key, "fast_tile")) { g_fast_tile = value; return 0; }
   if (!strcmp(key, "gemm_dbg")) { g_gemm_dbg = value; return 0; }
