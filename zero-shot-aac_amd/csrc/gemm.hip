@@ -72,13 +72,22 @@ __global__ void splitk_reduce_kernel(GemmArgs g) {
 }
 
 // One wave's parked [32][WN] f32 slab -> out rows mr0..mr0+31, cols nc0..nc0+WN-1: each lane
-// owns 8 consecutive columns (two ds_read_b128), so bias / residual loads and the bf16 store are
-// 16 B per lane over contiguous row segments; ACT is a template parameter (no per-element switch).
+// owns 8 consecutive columns (two ds_read_b128), so residual loads and the bf16 store are 16 B
+// per lane over contiguous row segments; ACT is a template parameter (no per-element switch).
+// (A fully unrolled variant with every load hoisted raised the kernel to >256 VGPRs and lost
+// occupancy: slower on every HTSAT shape.)
 template <int ACT, int WN>
 __device__ __forceinline__ void epi_slab(const GemmArgs& g, const float* slab, int mr0, int nc0,
                                          int z, bool vec_out, bool vec_res) {
   constexpr int Q = WN / 8;
   const int lane = threadIdx.x & 63;
+  // a lane's 8 columns are the same in every iteration (64 % Q == 0): bias loaded once
+  float bb[8];
+  {
+    const int n = nc0 + (lane % Q) * 8, nv = min(8, g.N - n);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) bb[q] = (g.bias && q < nv) ? g.bias[n + q] : 0.f;
+  }
   for (int idx = lane; idx < 32 * Q; idx += 64) {
     const int r = idx / Q, c = (idx % Q) * 8;
     const int m = mr0 + r, n = nc0 + c;
@@ -98,18 +107,8 @@ __device__ __forceinline__ void epi_slab(const GemmArgs& g, const float* slab, i
       }
       continue;
     }
-    if (g.bias) {
-      if (full && ((uintptr_t)g.bias & 15) == 0) {
-        const float4 b0 = reinterpret_cast<const float4*>(g.bias + n)[0];
-        const float4 b1 = reinterpret_cast<const float4*>(g.bias + n)[1];
-        v[0] += b0.x; v[1] += b0.y; v[2] += b0.z; v[3] += b0.w;
-        v[4] += b1.x; v[5] += b1.y; v[6] += b1.z; v[7] += b1.w;
-      } else {
-        for (int q = 0; q < nv; ++q) v[q] += g.bias[n + q];
-      }
-    }
 #pragma unroll
-    for (int q = 0; q < 8; ++q) v[q] = act_apply(v[q], ACT);
+    for (int q = 0; q < 8; ++q) v[q] = act_apply(v[q] + bb[q], ACT);
     if (g.residual) {
       const float* rp = g.residual + (long)m * g.ldr + n;
       if (full && vec_res) {
