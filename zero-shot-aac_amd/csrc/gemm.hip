@@ -286,23 +286,26 @@ __global__ __launch_bounds__(256) void lmhead_kernel(int M, int K, int V, const 
   const int n0 = blockIdx.x * LM_BN, m0 = blockIdx.y * BM;
   const int nblk = gridDim.x;
   f32x16_t acc[TM][TN];
-  // greedy / get_prefix_tokens (bf16, top-1): transposed product, vocab on the MFMA row axis,
-  // so a token's 128 logits of this block sit in registers of one lane pair (see below)
+  // bf16: transposed product, vocab on the MFMA row axis, so a token's 128 logits of this block
+  // sit in registers of one lane pair (see the epilogue below)
   f32x16_t acct[LM_BN / 64][BM / 64];
-  if constexpr (FAST && KMAX == 1) {
+  float ssq[BM / 64];     // per lane: its half of the squared norm of token wc0 + j*32 + (lane&31)
+  if constexpr (FAST) {
     const DenseRows ra{(const bf16_t*)A, lda, M, m0};
     const DenseRows rw{(const bf16_t*)W, K, V, n0};
-    fast_mainloop<LM_BN, BM>(rw, ra, 0, K, smem_raw, acct);
-  } else if constexpr (FAST) {
-    const DenseRows ra{(const bf16_t*)A, lda, M, m0};
-    const DenseRows rw{(const bf16_t*)W, K, V, n0};
-    fast_mainloop<BM, LM_BN>(ra, rw, 0, K, smem_raw, acc);
+#pragma unroll
+    for (int j = 0; j < BM / 64; ++j) ssq[j] = 0.f;
+    if (row_norm)
+      fast_mainloop<LM_BN, BM, 2, 2, 2, 64, true>(rw, ra, 0, K, smem_raw, acct, 0, ssq);
+    else
+      fast_mainloop<LM_BN, BM>(rw, ra, 0, K, smem_raw, acct);
   } else {
     DenseA<T, BM> la{A, lda, M, m0};
     gemm_mainloop<T, BM, LM_BN>(la, W, K, V, n0, 0, K, (T*)smem_raw, acc);
   }
-  // row norms for get_prefix_tokens (normalize(a) . w == (a . w) / max(||a||, 1e-12))
-  if (row_norm) {
+  // row norms for get_prefix_tokens (normalize(a) . w == (a . w) / max(||a||, 1e-12)); the
+  // transposed top-1 path gets them from its own B fragments instead (see below)
+  if (row_norm && !FAST) {
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     for (int r = wid; r < BM; r += 4) {
       float s = 0.f;
@@ -316,37 +319,71 @@ __global__ __launch_bounds__(256) void lmhead_kernel(int M, int K, int V, const 
     }
   }
   __syncthreads();
-  if constexpr (FAST && KMAX == 1) {
+  if constexpr (FAST) {
     // acct[i][j][e]: vocab n0 + wr0 + i*32 + (e&3) + 8*(e>>2) + 4*(lane>>5), token
-    // m0 + wc0 + j*32 + (lane&31).  Per token: max / argmax / sum-exp over the lane's 32 vocab
-    // entries in registers, one xor-32 exchange with the partner lane, then the two waves that
-    // hold the other 64 vocab rows of the same tokens combine through LDS.  Ties keep the lower
-    // vocab index (torch argmax / the LDS path).
+    // m0 + wc0 + j*32 + (lane&31).  Per token: a descending top-KMAX list and the sum-exp over the
+    // lane's 32 vocab entries in registers, one xor-32 exchange with the partner lane, then the
+    // two waves holding the other 64 vocab rows of the same tokens merge through LDS.  Ties keep
+    // the lower vocab index (torch argmax / topk order).
     constexpr int TMV = LM_BN / 64, TNT = BM / 64;
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const int wr0 = (wid >> 1) * (LM_BN / 2), wc0 = (wid & 1) * (BM / 2), wg = wid >> 1;
     float* xm = reinterpret_cast<float*>(smem_raw);          // [2][BM] max
     float* xs = xm + 2 * BM;                                  // [2][BM] sum-exp
-    int* xi = reinterpret_cast<int*>(xs + 2 * BM);            // [2][BM] argmax
+    float* xv = xs + 2 * BM;                                  // [2][BM][KMAX] top values
+    int* xi = reinterpret_cast<int*>(xv + 2 * BM * KMAX);     // [2][BM][KMAX] top indices
+    auto better = [](float v, int i, float w, int k) { return v > w || (v == w && i < k); };
 #pragma unroll
     for (int j = 0; j < TNT; ++j) {
       const int r = wc0 + j * 32 + (lane & 31);                // token within the block
-      const float sc = row_norm ? inv_norm[r] : 1.0f;
-      float bv = -INFINITY;
-      int bi = 0x7fffffff;
+      float sc = 1.0f;
+      if (row_norm) {
+        const float t = ssq[j] + __shfl_xor(ssq[j], 32, 64);
+        sc = 1.0f / fmaxf(sqrtf(t), 1e-12f);
+      }
+      float tv[KMAX];
+      int ti[KMAX];
+#pragma unroll
+      for (int q = 0; q < KMAX; ++q) { tv[q] = -INFINITY; ti[q] = 0x7fffffff; }
 #pragma unroll
       for (int i = 0; i < TMV; ++i)
 #pragma unroll
         for (int e = 0; e < 16; ++e) {
           const int n = n0 + wr0 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5);
-          const float v = n < V ? acct[i][j][e] * sc : -INFINITY;
-          if (v > bv) { bv = v; bi = n; }      // n increases with (i, e): strict > keeps lower
+          float cv = n < V ? acct[i][j][e] * sc : -INFINITY;
+          int ci = n;
+          // n increases with (i, e): strict > keeps the lower index first among equals
+          if (cv > tv[KMAX - 1]) {
+#pragma unroll
+            for (int q = 0; q < KMAX; ++q)
+              if (cv > tv[q]) { const float t = tv[q]; const int u = ti[q]; tv[q] = cv; ti[q] = ci; cv = t; ci = u; }
+          }
         }
+      // merge with the partner lane's list (both lanes end with the same top-KMAX)
+      float pv[KMAX];
+      int pi[KMAX];
+#pragma unroll
+      for (int q = 0; q < KMAX; ++q) { pv[q] = __shfl_xor(tv[q], 32, 64); pi[q] = __shfl_xor(ti[q], 32, 64); }
       {
-        const float ov = __shfl_xor(bv, 32, 64);
-        const int oi = __shfl_xor(bi, 32, 64);
-        if (ov > bv || (ov == bv && oi < bi)) { bv = ov; bi = oi; }
+        float mv[KMAX];
+        int mi[KMAX];
+        int a = 0, b = 0;
+#pragma unroll
+        for (int q = 0; q < KMAX; ++q) {
+          float av = -INFINITY, bv2 = -INFINITY;
+          int ai = 0x7fffffff, bi2 = 0x7fffffff;
+#pragma unroll
+          for (int t = 0; t < KMAX; ++t) {
+            if (t == a) { av = tv[t]; ai = ti[t]; }
+            if (t == b) { bv2 = pv[t]; bi2 = pi[t]; }
+          }
+          if (better(av, ai, bv2, bi2)) { mv[q] = av; mi[q] = ai; ++a; }
+          else { mv[q] = bv2; mi[q] = bi2; ++b; }
+        }
+#pragma unroll
+        for (int q = 0; q < KMAX; ++q) { tv[q] = mv[q]; ti[q] = mi[q]; }
       }
+      const float bv = tv[0];
       float se = 0.f;
       if (bv != -INFINITY) {
 #pragma unroll
@@ -358,23 +395,38 @@ __global__ __launch_bounds__(256) void lmhead_kernel(int M, int K, int V, const 
           }
       }
       se += __shfl_xor(se, 32, 64);
-      if (lane < 32) { xm[wg * BM + r] = bv; xs[wg * BM + r] = se; xi[wg * BM + r] = bi; }
+      if (lane < 32) {
+        xm[wg * BM + r] = bv;
+        xs[wg * BM + r] = se;
+#pragma unroll
+        for (int q = 0; q < KMAX; ++q) {
+          xv[(wg * BM + r) * KMAX + q] = tv[q];
+          xi[(wg * BM + r) * KMAX + q] = ti[q];
+        }
+      }
     }
     __syncthreads();
     for (int r = threadIdx.x; r < BM; r += 256) {
       const int m = m0 + r;
       if (m >= M) continue;
       const float m0v = xm[r], m1v = xm[BM + r];
-      const int i0 = xi[r], i1 = xi[BM + r];
       const float g = fmaxf(m0v, m1v);
       const float se = (m0v == -INFINITY ? 0.f : xs[r] * expf(m0v - g)) +
                        (m1v == -INFINITY ? 0.f : xs[BM + r] * expf(m1v - g));
-      const bool take1 = m1v > m0v || (m1v == m0v && i1 < i0);
       const long o = (long)m * nblk + blockIdx.x;
       part_stat[o * 2 + 0] = g;
       part_stat[o * 2 + 1] = se;
-      part_val[o] = take1 ? m1v : m0v;
-      part_idx[o] = take1 ? i1 : i0;
+      const float* l0v = xv + r * KMAX;
+      const int* l0i = xi + r * KMAX;
+      const float* l1v = xv + (BM + r) * KMAX;
+      const int* l1i = xi + (BM + r) * KMAX;
+      int a = 0, b = 0;
+      for (int q = 0; q < topk; ++q) {
+        const bool ta = b >= KMAX || (a < KMAX && better(l0v[a], l0i[a], l1v[b], l1i[b]));
+        part_val[o * topk + q] = ta ? l0v[a] : l1v[b];
+        part_idx[o * topk + q] = ta ? l0i[a] : l1i[b];
+        if (ta) ++a; else ++b;
+      }
     }
     return;
   }

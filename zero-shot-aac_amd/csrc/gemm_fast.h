@@ -81,10 +81,14 @@ __device__ __forceinline__ void fast_issue_t(const ASrc& A, const BSrc& B, int k
   }
 }
 
-template <int BM, int BN, int WGM, int WGN, int BK_>
+// SSQ: also accumulate, per lane, the sum of squares of the B fragments it reads (row
+// wc0 + j*32 + (lane & 31), its half of every k-slice): with the xor-32 partner's sum that is
+// the squared norm of the B row — the LM head's get_prefix_tokens row norms for free
+template <int BM, int BN, int WGM, int WGN, int BK_, bool SSQ = false>
 __device__ __forceinline__ void fast_compute(
     const char* stage,
-    f32x16_t (&acc)[FastTile<BM, BN, WGM, WGN, BK_>::TM][FastTile<BM, BN, WGM, WGN, BK_>::TN]) {
+    f32x16_t (&acc)[FastTile<BM, BN, WGM, WGN, BK_>::TM][FastTile<BM, BN, WGM, WGN, BK_>::TN],
+    float* ssq = nullptr) {
   using FT = FastTile<BM, BN, WGM, WGN, BK_>;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, r = lane & 31, h = lane >> 5;
   const int wr0 = (wid / WGN) * FT::WM, wc0 = BM + (wid % WGN) * FT::WN;
@@ -101,6 +105,10 @@ __device__ __forceinline__ void fast_compute(
     for (int j = 0; j < FT::TN; ++j) {
       const int row = wc0 + j * 32 + r;
       b[j] = *reinterpret_cast<const bf16x8_t*>(stage + row * FT::RB + 16 * (c ^ FT::swz(row)));
+      if constexpr (SSQ) {
+#pragma unroll
+        for (int u = 0; u < 8; ++u) { const float x = (float)b[j][u]; ssq[j] += x * x; }
+      }
     }
 #pragma unroll
     for (int i = 0; i < FT::TM; ++i)
@@ -126,12 +134,12 @@ __device__ __forceinline__ void wait_vm() {
 // __syncthreads() here would drain all DMAs (vmcnt(0)): cdna_hip_programming.md §5
 // "Pipelining across barriers".  Under full-chip streaming a DMA takes ~2-3 us to land, so the
 // ring depth (NS-1 tiles in flight), not the MFMA count, sets the k-loop rate.
-template <int BM, int BN, int NS = 2, int WGM = 2, int WGN = 2, int BK_ = 64, typename ASrc,
-          typename BSrc>
+template <int BM, int BN, int NS = 2, int WGM = 2, int WGN = 2, int BK_ = 64, bool SSQ = false,
+          typename ASrc, typename BSrc>
 __device__ __forceinline__ void fast_mainloop(
     const ASrc& A, const BSrc& B, int kbeg, int kend, char* lds,
     f32x16_t (&acc)[FastTile<BM, BN, WGM, WGN, BK_>::TM][FastTile<BM, BN, WGM, WGN, BK_>::TN],
-    int dbg = 0) {
+    int dbg = 0, float* ssq = nullptr) {
   using FT = FastTile<BM, BN, WGM, WGN, BK_>;
   constexpr int IPW = FT::NI / FT::NW;            // DMA instructions per wave per tile
   static_assert(NS >= 2 && (NS - 2) * IPW < 64, "stages");
@@ -157,7 +165,8 @@ __device__ __forceinline__ void fast_mainloop(
       const int sn = st == 0 ? NS - 1 : st - 1;   // (kt + NS - 1) % NS == stage of tile kt-1
       fast_issue_t<BM, BN, WGM, WGN, BK_>(A, B, kbeg + tn * BK_, kend, lds + sn * FT::STAGE);
     }
-    if (dbg != 1 && dbg != 3) fast_compute<BM, BN, WGM, WGN, BK_>(lds + st * FT::STAGE, acc);
+    if (dbg != 1 && dbg != 3)
+      fast_compute<BM, BN, WGM, WGN, BK_, SSQ>(lds + st * FT::STAGE, acc, ssq);
     st = st == NS - 1 ? 0 : st + 1;
   }
   __syncthreads();   // callers may reuse the LDS for the epilogue
