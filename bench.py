@@ -19,9 +19,10 @@ architecture (no checkpoints offline).
     torchrun --nproc-per-node N bench.py --gpus N ...      (one process per GPU, RCCL)
 
 Rank 0 prints ONE JSON line.  Besides the contract fields it carries
-  roofline:     the dominant kernel (GPT-2 decode MLP up-projection GEMM, M=64: HBM-bound
-                weight stream) — algorithmic bytes per launch / its average duration, timed live
-                with HIP events on the stream it runs on;
+  roofline:     the dominant kernel family (bf16 MFMA GEMM) at the decode MLP up-projection
+                shape the bench runs (R = decode rows) — algorithmic flops per launch / its
+                average duration, timed live with HIP events on the stream it runs on;
+                roofline_decode_attention: the HBM-bound decode attention, same method;
   cpu_baseline: the oracle (reference semantics: batch 1, full recompute, fp32) on a bounded
                 sample of the same workload, timed on this host's CPU (rank 0, N=1 only).
 """
@@ -97,41 +98,39 @@ def build(args, device):
     return pipe, csd, asd
 
 
-ROOFLINE_KERNEL = "gemm_skinny_kernel"
 PMC_FILE = os.path.join(ROOT, "profiles", "pmc_traffic_r1.json")
+MFMA_BF16_PEAK_TFLOPS = 2500.0   # MI355X_MICROARCH.md: dense bf16 MFMA (no sparsity)
 
 
 def roofline_setup(pipe, cold_bytes=640 << 20):
-    """The dominant kernel's operands: the decode-step MLP up-projection GEMM
-    (c_fc: out[64,3072] = gelu_new(h[64,768] @ W[3072,768]^T + b)).  Launches rotate over enough
-    distinct copies of W (> the 256 MiB Infinity Cache) that every launch streams its weights
-    from HBM, as in the real decode, where ~250 MB of GPT-2 weights pass between two uses of one
-    layer's W.  Returns (launch fn taking a launch index, algorithmic bytes per launch)."""
+    """The dominant kernel family is the bf16 MFMA GEMM (gemm_fast_kernel: HTSAT linears and the
+    GPT-2 decode/prefill linears).  Its roofline is taken at the decode-step MLP up-projection
+    as the bench runs it: c_fc out[R,3072] = gelu_new(h[R,768] @ W[3072,768]^T + b), R = the
+    decode rows of one step (eval batches x 64), through ops.gemm exactly as the decoder calls
+    it.  Launches rotate over enough distinct copies of W (> the 256 MiB Infinity Cache) that
+    every launch streams its weights from HBM, as in the real decode.  Returns (launch fn,
+    algorithmic flops, algorithmic bytes, number of W copies, kernel-name substring)."""
     from zsaac import ops
     dec = pipe.decoder
     ly = pipe.gpt.layers[0]
-    M = pipe.cfg.batch
+    M = pipe.cfg.batch * max(1, pipe.cfg.beam)
     h, hid = dec.h[:M], dec.hid[:M]
     W, b = ly["fc_w"], ly["fc_b"]
     N, K = W.shape
     es = W.element_size()
     copies = [W] + [W.clone() for _ in range(max(0, -(-cold_bytes // W.nbytes) - 1))]
+    flops = 2 * M * N * K
     algo_bytes = N * K * es + M * K * es + N * 4 + M * N * es
-
-    from zsaac._lib import call
-    assert call("zs_gemm_workspace_floats", M, N, K) <= dec.ws.numel(), "not the skinny path"
+    kname = "gemm_skinny_kernel" if M <= 64 else "gemm_fast_kernel"
 
     def launch(i):
         ops.gemm(h, copies[i % len(copies)], hid, bias=b, act=ops.ACT_GELU_TANH, workspace=dec.ws)
-    return launch, algo_bytes, len(copies)
+    return launch, flops, algo_bytes, len(copies), kname, (M, N, K)
 
 
-def kernel_roofline(pipe):
-    """Average duration of the dominant kernel measured with HIP events on the stream it is
-    launched on, over back-to-back launches (cold weights, see roofline_setup) captured in a
-    graph.  Algorithmic bytes per launch = W + A + bias + out (2 B per weight)."""
-    launch, algo_bytes, ncopy = roofline_setup(pipe)
-    reps = 2 * ncopy
+def _graph_time(launch, reps):
+    """Average duration of `reps` back-to-back launches captured in one graph, HIP events on the
+    launching stream, 5 replays."""
     s = torch.cuda.Stream()
     s.wait_stream(torch.cuda.current_stream())
     with torch.cuda.stream(s):
@@ -148,20 +147,57 @@ def kernel_roofline(pipe):
             g.replay()
         e1.record(s)
     e1.synchronize()
-    avg_s = e0.elapsed_time(e1) / 1e3 / (5 * reps)
-    achieved = algo_bytes / avg_s / 1e9
+    torch.cuda.current_stream().wait_stream(s)
+    return e0.elapsed_time(e1) / 1e3 / (5 * reps)
+
+
+def kernel_roofline(pipe):
+    """roofline (dominant kernel, MFMA-bound at the bench's decode rows) + a secondary HBM-bound
+    entry for the decode attention (the largest single-shape kernel)."""
+    launch, flops, algo_bytes, ncopy, kname, (M, N, K) = roofline_setup(pipe)
+    avg_s = _graph_time(launch, 2 * ncopy)
+    tflops = flops / avg_s / 1e12
     traffic, tsrc = None, None
     if os.path.exists(PMC_FILE):          # rocprofv3 --pmc passes of tools/pmc_traffic.py
         with open(PMC_FILE) as f:
             pmc = json.load(f)
-        if pmc.get("algo_bytes_per_launch") == algo_bytes:
+        if pmc.get("shape") == [M, N, K]:
             traffic, tsrc = pmc["hbm_bytes_per_launch"], os.path.relpath(PMC_FILE, ROOT)
-    return {"kernel": "gemm_skinny_kernel<bf16> decode c_fc [64x768]x[768x3072] +gelu_new "
-                      "(cold weights)",
-            "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-            "traffic_source": tsrc, "avg_launch_us": round(avg_s * 1e6, 3),
-            "algo_bytes_per_launch": algo_bytes}
+    res = {"kernel": f"{kname}<bf16> decode c_fc [{M}x{K}]x[{K}x{N}] +bias +gelu_new (cold W)",
+           "bound": "mfma", "achieved": round(tflops, 1), "peak": MFMA_BF16_PEAK_TFLOPS,
+           "unit": "TFLOP/s", "frac": round(tflops / MFMA_BF16_PEAK_TFLOPS, 4),
+           "traffic": traffic, "traffic_source": tsrc, "avg_launch_us": round(avg_s * 1e6, 3),
+           "algo_flops_per_launch": flops, "algo_bytes_per_launch": algo_bytes,
+           "hbm_GBps_algorithmic": round(algo_bytes / avg_s / 1e9, 1)}
+    return res, attention_roofline(pipe)
+
+
+def attention_roofline(pipe, L_mean=None):
+    """decode_attn5_kernel at the bench's decode rows, every row at the mean key count of a
+    67-step greedy decode (prompt Pmax + 34): algorithmic bytes = K and V of every key read once
+    + q/k/v of the new token + the output, per (row, head)."""
+    from zsaac import ops
+    dec = pipe.decoder
+    R = pipe.cfg.batch * max(1, pipe.cfg.beam)
+    D, H, Lmax = 768, 12, dec.Lmax
+    L = L_mean or min(Lmax - 1, pipe.Pmax + 34)
+    lay = dec.kc[0] if isinstance(dec.kc, (list, tuple)) else None
+    kc = lay if lay is not None else torch.randn(R, H, Lmax, 64, device=pipe.dev).bfloat16()
+    vc = (dec.vc[0] if isinstance(dec.vc, (list, tuple)) else torch.randn_like(kc))
+    qkv = dec.qkv[:R] if hasattr(dec, "qkv") else torch.randn(R, 3 * D, device=pipe.dev).bfloat16()
+    pos = torch.full((R,), L - 1, device=pipe.dev, dtype=torch.int32)
+    out = torch.empty(R, D, device=pipe.dev, dtype=qkv.dtype)
+
+    def launch(i):
+        ops.decode_attention(qkv, R, D, H, kc, vc, Lmax, pos, out)
+    avg_s = _graph_time(launch, 50)
+    es = qkv.element_size()
+    byts = R * H * (2 * L * 64 * es) + R * 3 * D * es + R * D * es
+    gbs = byts / avg_s / 1e9
+    return {"kernel": f"decode_attn5_kernel<bf16> R={R} heads=12 keys={L}", "bound": "hbm",
+            "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(gbs / HBM_PEAK_GBS, 4), "avg_launch_us": round(avg_s * 1e6, 3),
+            "algo_bytes_per_launch": byts}
 
 
 def stage_times(pipe, wav, reps=3):
@@ -310,7 +346,7 @@ def main():
     if args.stages and rank == 0:
         res["stages_ms"] = stage_times(pipe, pool[0])
     if rank == 0 and not args.no_roofline:
-        res["roofline"] = kernel_roofline(pipe)
+        res["roofline"], res["roofline_decode_attention"] = kernel_roofline(pipe)
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.cpu_baseline_clips > 0:
         res["cpu_baseline"] = cpu_baseline(args, csd, asd, args.cpu_baseline_clips)
     if rank == 0:

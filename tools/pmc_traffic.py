@@ -9,9 +9,9 @@ launches of exactly the launches bench.py times (roofline_setup: cold weights), 
     python3 tools/pmc_traffic.py parse gpurun_out/pmc_fetch gpurun_out/pmc_write gpurun_out/pmc_traffic_r1.json
 
 Corrections (MI355X_MICROARCH.md §HBM): FETCH_SIZE is in KiB and on gfx950 reports half the
-bytes of a 16-B/lane coalesced streaming read (the skinny kernel's W and A loads are all 16 B per
-lane), so read bytes = 2 * 1024 * FETCH_SIZE; WRITE_SIZE (KiB) is exact for 16-B/lane stores
-(the split-K slabs) and uncalibrated for the 2-B bf16 epilogue stores (64 KiB of 5 MB).
+bytes of a 16-B/lane coalesced streaming read (the GEMM's LDS-DMA loads are all 16 B per lane),
+so read bytes = 2 * 1024 * FETCH_SIZE; WRITE_SIZE (KiB) is exact for 16-B/lane stores (the
+epilogue's bf16 rows are 16-B/lane stores).
 """
 import csv
 import glob
@@ -28,17 +28,18 @@ def run():
     import torch
     import bench
 
-    class A:
-        batch, dtype, encoder, mapper, beam, entry_length = 64, "bf16", "htsat", "mlp", 0, 67
+    class A:       # bench.py defaults: eval batch 64, group 32 -> 2048 decode rows
+        batch, group, dtype, encoder, mapper, beam, entry_length = 64, 32, "bf16", "htsat", "mlp", 0, 67
     pipe, _, _ = bench.build(A, torch.device("cuda", 0))
-    launch, algo, ncopy = bench.roofline_setup(pipe)
+    launch, flops, algo, ncopy, kname, shape = bench.roofline_setup(pipe)
     for i in range(2 * ncopy):
         launch(i)
     torch.cuda.synchronize()
-    print(json.dumps({"algo_bytes_per_launch": algo, "launches": 2 * ncopy}))
+    print(json.dumps({"algo_bytes_per_launch": algo, "launches": 2 * ncopy, "kernel": kname,
+                      "shape": shape}))
 
 
-def _per_dispatch(d, counter):
+def _per_dispatch(d, counter, kname):
     files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
     if not files:
         raise SystemExit(f"no counter_collection.csv under {d}")
@@ -46,30 +47,30 @@ def _per_dispatch(d, counter):
     for fn in files:
         with open(fn) as f:
             for row in csv.DictReader(f):
-                if row.get("Counter_Name") != counter or "gemm_skinny_kernel" not in row.get("Kernel_Name", ""):
+                if row.get("Counter_Name") != counter or kname not in row.get("Kernel_Name", ""):
                     continue
                 key = (fn, row.get("Dispatch_Id") or row.get("Correlation_Id"))
                 vals[key] = vals.get(key, 0.0) + float(row["Counter_Value"])
     if not vals:
-        raise SystemExit(f"no {counter} rows for gemm_skinny_kernel under {d}")
+        raise SystemExit(f"no {counter} rows for {kname} under {d}")
     v = sorted(vals.values())
     return v[len(v) // 2], len(v)
 
 
-def parse(dfetch, dwrite, out):
-    fetch_kib, n_f = _per_dispatch(dfetch, "FETCH_SIZE")
-    write_kib, n_w = _per_dispatch(dwrite, "WRITE_SIZE")
+def parse(dfetch, dwrite, out, M=2048, N=3072, K=768, kname="gemm_fast_kernel"):
+    fetch_kib, n_f = _per_dispatch(dfetch, "FETCH_SIZE", kname)
+    write_kib, n_w = _per_dispatch(dwrite, "WRITE_SIZE", kname)
     rd = 2 * 1024 * fetch_kib
     wr = 1024 * write_kib
     sys.path.insert(0, ROOT)
-    res = {"kernel": "gemm_skinny_kernel<bf16> decode c_fc (cold weights)",
+    res = {"kernel": f"{kname}<bf16> decode c_fc [{M}x{K}]x[{K}x{N}] (cold weights)",
            "fetch_size_kib_median": fetch_kib, "write_size_kib_median": write_kib,
            "dispatches": [n_f, n_w], "hbm_read_bytes_per_launch": int(rd),
            "hbm_write_bytes_per_launch": int(wr), "hbm_bytes_per_launch": int(rd + wr),
            "corrections": "read = 2*1024*FETCH_SIZE (gfx950 16B/lane streaming reads); "
                           "write = 1024*WRITE_SIZE"}
-    # the algorithmic byte count bench.py checks against (shape-only, no GPU needed)
-    M, N, K = 64, 3072, 768
+    # the shape bench.py checks against before quoting the traffic
+    res["shape"] = [M, N, K]
     res["algo_bytes_per_launch"] = N * K * 2 + M * K * 2 + N * 4 + M * N * 2
     with open(out, "w") as f:
         json.dump(res, f, indent=1)
