@@ -63,6 +63,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--stages", action="store_true", help="also report per-stage ms (extra syncs)")
+    ap.add_argument("--embeddings-only", action="store_true",
+                    help="C4: batched HTSAT/CNN14 encode_audio + one RCCL all-gather of the "
+                         "[N,1024] embeddings (no caption decode)")
     return ap.parse_args()
 
 
@@ -266,12 +269,64 @@ def cpu_baseline(args, csd, asd, n_clips):
                       f"(reference semantics), fp32, {ntok} tokens, {dt:.1f} s"}
 
 
+def main_embeddings(args, world, rank, device, pipe):
+    """BASELINE.json configs[3] (C4): embedding extraction, data_handing/embeddings_generator.py
+    realised as batched encode_audio over synthetic clips sharded across ranks, then one RCCL
+    all-gather of the [N,1024] f32 embeddings (SURVEY §8d "C4 reinterpretation")."""
+    B = args.batch * args.group
+    g = torch.Generator(device=device).manual_seed(1234 + rank)
+    pool = [(torch.randn(B, 320000, device=device, generator=g) * 0.1).clamp_(-1, 1)
+            for _ in range(min(2, args.steps + args.warmup))]
+    embs = torch.empty(args.steps, B, 1024, device=device)
+
+    def run(first, n, keep):
+        for i in range(n):
+            e = pipe.encode(pool[(first + i) % len(pool)])
+            if keep:
+                embs[i].copy_(e)
+        if keep and world > 1:
+            gathered = torch.empty(world * embs.numel(), device=device)
+            torch.distributed.all_gather_into_tensor(gathered, embs.view(-1))
+    run(0, args.warmup, False)
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    run(args.warmup, args.steps, True)
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt], device=device, dtype=torch.float64)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        dt = float(t)
+    res = {"metric": "audio clips/sec embedding extraction (STFT/log-mel + " + args.encoder.upper()
+                     + " + audio_proj + L2), C4",
+           "value": round(world * B * args.steps / dt, 2), "unit": "clips/s", "n_gpus": world,
+           "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 3),
+           "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+           "dtype": "bf16" if args.dtype == "bf16" else "f32",
+           "data": "synthetic 10 s / 32 kHz waveforms (randn*0.1) resident in HBM; seeded weights",
+           "config": {"workload": "C4 embedding extraction, RCCL all-gather of [N,1024] f32",
+                      "encoder_batch": args.batch, "batch_per_gpu": B, "global_batch": B * world,
+                      "parallelism": f"dp{world} (clip-sharded)"}}
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
 def main():
     args = parse()
     world, rank, local = dist_setup(args)
     device = torch.device("cuda", local)
     from zsaac import synthetic as S
     pipe, csd, asd = build(args, device)
+    if args.embeddings_only:
+        return main_embeddings(args, world, rank, device, pipe)
     B = args.batch * args.group           # clips per step (group eval batches, decoded together)
     # input pool resident in HBM before timing: distinct synthetic clips per step and rank
     pool = []
@@ -332,7 +387,8 @@ def main():
         "dtype": "bf16" if args.dtype == "bf16" else "f32",
         "data": "synthetic 10 s / 32 kHz waveforms (randn*0.1) resident in HBM; seeded random-init "
                 "weights at the reference architecture (no checkpoints offline)",
-        "config": {"workload": "C2 Clotho-eval: STFT/log-mel + " + args.encoder.upper() + " + "
+        "config": {"workload": ("C3 AudioCaps-eval" if args.beam else "C2 Clotho-eval")
+                               + ": STFT/log-mel + " + args.encoder.upper() + " + "
                                + args.mapper + " mapper + GPT-2 small "
                                + ("greedy generate2" if not args.beam else f"beam {args.beam}")
                                + f", entry_length {args.entry_length}, + get_prefix_tokens",

@@ -214,6 +214,34 @@ def bench_window():
               + f"  ({byts / res_t['mfma'] / 1e3:6.0f} GB/s mfma)", flush=True)
 
 
+def bench_decode_gemm():
+    """Decode-step GEMMs at 2048 rows with cold weights (rotating > 256 MiB of W copies), per tile."""
+    from zsaac import ops
+    from zsaac._lib import call
+    dev = torch.device("cuda", 0)
+    M = int(os.environ.get("ZS_M", "2048"))
+    for N, K, name in ((2304, 768, "qkv"), (768, 768, "proj"), (3072, 768, "fc"), (768, 3072, "mproj")):
+        a = torch.randn(M, K, device=dev).bfloat16()
+        w0 = (torch.randn(N, K, device=dev) * 0.02).bfloat16()
+        ws = [w0] + [w0.clone() for _ in range(max(1, (640 << 20) // w0.nbytes))]
+        b = torch.randn(N, device=dev)
+        out = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+        it = [0]
+
+        def run():
+            ops.gemm(a, ws[it[0] % len(ws)], out, bias=b, split_k=1)
+            it[0] += 1
+        res = {}
+        for t, nm in ((0, "auto"), (4, "128x128"), (10, "128x128s3"), (7, "128/32s6"), (5, "128/32s4"),
+                      (8, "128x64"), (9, "64x128"), (1, "256/32s4w8")):
+            call("zs_tune_set", b"fast_tile", t)
+            res[nm] = timeit(run, reps=len(ws))
+        call("zs_tune_set", b"fast_tile", 0)
+        res["torch"] = timeit(lambda: torch.nn.functional.linear(a, ws[it.__setitem__(0, it[0] + 1) or it[0] % len(ws)], b.bfloat16()), reps=len(ws))
+        fl = 2 * M * N * K
+        print(f"M{M} {name:6s} " + "  ".join(f"{k}={v:6.1f}us({fl / v / 1e6:4.0f})" for k, v in res.items()), flush=True)
+
+
 def bench_attn():
     from zsaac import ops
     dev = torch.device("cuda", 0)
@@ -261,4 +289,4 @@ def bench_inflight():
 if __name__ == "__main__":
     which = sys.argv[1:] or ["gemm", "attn"]
     for wname in which:
-        {"gemm": bench_gemm, "gemm_m": bench_gemm_m, "gemm_htsat": bench_gemm_htsat, "gemm_dbg": bench_gemm_dbg, "lmhead": bench_lmhead, "front": bench_front, "window": bench_window, "attn": bench_attn, "inflight": bench_inflight}[wname]()
+        {"gemm": bench_gemm, "gemm_m": bench_gemm_m, "gemm_htsat": bench_gemm_htsat, "gemm_dbg": bench_gemm_dbg, "lmhead": bench_lmhead, "front": bench_front, "window": bench_window, "decode_gemm": bench_decode_gemm, "attn": bench_attn, "inflight": bench_inflight}[wname]()

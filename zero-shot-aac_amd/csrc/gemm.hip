@@ -234,6 +234,10 @@ static int dispatch_fast(GemmArgs& g, hipStream_t st) {
     case 4: return launch_fast<128, 128, 2>(g, st);
     case 5: return launch_fast<128, 128, 4, 2, 2, 32>(g, st);
     case 6: return launch_fast<256, 256, 2, 2, 4, 64>(g, st);
+    case 7: return launch_fast<128, 128, 6, 2, 2, 32>(g, st);
+    case 8: return launch_fast<128, 64, 3>(g, st);
+    case 9: return launch_fast<64, 128, 3>(g, st);
+    case 10: return launch_fast<128, 128, 3>(g, st);
     default: break;
   }
   if (nblocks(g, 128, 128) >= 256) {
