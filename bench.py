@@ -57,8 +57,10 @@ def parse():
     ap.add_argument("--group", type=int, default=32,
                     help="eval batches of --batch clips decoded together (one decode step over "
                          "group*batch rows); each is still encoded as its own batch")
-    ap.add_argument("--inflight", type=int, default=2,
+    ap.add_argument("--inflight", type=int, default=3,
                     help="independent bs=--batch batches decoding concurrently per GPU (streams)")
+    ap.add_argument("--compact", type=int, default=1,
+                    help="greedy bf16: decode only the rows that have not stopped (0 = all rows)")
     ap.add_argument("--cpu-baseline-clips", type=int, default=2)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
@@ -96,7 +98,8 @@ def build(args, device):
         asd.update(S.audio_proj_state_dict(5, audio_width=2048))
     cfg = CaptionConfig(encoder=args.encoder, mapping_type=args.mapper, dtype=dtype,
                         batch=args.batch * getattr(args, "group", 1), encoder_batch=args.batch,
-                        beam=args.beam, entry_length=args.entry_length)
+                        beam=args.beam, entry_length=args.entry_length,
+                        compact_decode=bool(getattr(args, "compact", 1)))
     pipe = CaptionPipeline(csd, asd, S.label_table(), S.label_token_table(), cfg, device=device)
     return pipe, csd, asd
 
@@ -357,6 +360,8 @@ def main():
     if world > 1:
         torch.distributed.barrier()
     torch.cuda.synchronize()
+    cap0 = sum(p.decoder.n_captures for p in runner.pipes)
+    rows0 = sum(p.decoder.rows_stepped for p in runner.pipes)
     t0 = time.perf_counter()
     ntok = 0
     outs = run(args.warmup, args.steps)
@@ -397,6 +402,9 @@ def main():
                    "steps_in_flight_per_gpu": max(1, args.inflight),
                    "parallelism": f"dp{world} (clip-sharded, RCCL all-gather of token ids)",
                    "tokens_last_batch_rank0": ntok,
+                   "decode_rows_stepped_per_clip": round(
+                       (sum(p.decoder.rows_stepped for p in runner.pipes) - rows0) / max(1, args.steps * B), 2),
+                   "graph_captures_timed": sum(p.decoder.n_captures for p in runner.pipes) - cap0,
                    "decode_steps_mean": round(sum(runner.decode_steps) / max(1, len(runner.decode_steps)), 2)},
     }
     if args.stages and rank == 0:

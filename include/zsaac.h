@@ -35,6 +35,12 @@ int zs_version(void);                         /* ABI version, bumped on signatur
 int zs_last_error(char* buf, size_t len);     /* copies the thread-local last error message */
 int zs_device_arch(char* buf, size_t len);    /* gcnArchName of the current device (e.g. gfx950) */
 int zs_tune_set(const char* key, int value);  /* tuning knobs, e.g. "skinny_mode" (0 fence, 1 sc1) */
+/* zs_stream_create: a new non-blocking HIP stream, bound to its hardware queue at once (ROCclr
+ * assigns queues round-robin at a stream's first dispatch), so streams created back to back run
+ * on distinct hardware queues while GPU_MAX_HW_QUEUES allows.  Used for the concurrent batch
+ * streams (two streams sharing a hardware queue serialize). */
+int zs_stream_create(void** stream);
+int zs_stream_destroy(void* stream);
 
 /* ------------------------------------------------------------------ audio front end
  * zs_logmel: retrieval/models/feature_extractor.py:34-38 (torchlibrosa Spectrogram +
@@ -158,9 +164,29 @@ int zs_kv_write(const void* qkv, int R, int n, int D, int heads, const int* pos0
 int zs_decode_attention(const void* qkv, int R, int D, int heads, void* kc, void* vc, int Lmax,
                         const int* pos, const int* kvrow, void* out, int dtype, void* stream);
 
+/* zs_decode_attention_map: zs_decode_attention over a compacted row set (bf16, Lmax <= 128,
+ * no kvrow): qkv/out rows are compact slots c in [0, R); the physical decode row of slot c is
+ * rowmap[c] (pos and the cache are indexed physically).  rowmap[c] >= nphys marks a padding
+ * slot: its out row is zeroed and the cache is untouched. */
+int zs_decode_attention_map(const void* qkv, int R, const int* rowmap, int nphys, int D, int heads,
+                            void* kc, void* vc, int Lmax, const int* pos, void* out, int dtype,
+                            void* stream);
+
 /* zs_embed_tokens: x[r] = wte[tok[r]] + wpe[pos[r]] (f32 out), optional row gather. */
 int zs_embed_tokens(const int* tok, const int* pos, const void* wte, const void* wpe, int R, int D,
                     float* x, int dtype, void* stream);
+
+/* zs_embed_tokens_map: x[c] = wte[tok[rowmap[c]]] + wpe[pos[rowmap[c]]] for compact slots
+ * c in [0, R); padding slots (rowmap[c] >= nphys) get x[c] = 0. */
+int zs_embed_tokens_map(const int* tok, const int* pos, const int* rowmap, int nphys,
+                        const void* wte, const void* wpe, int R, int D, float* x, int dtype,
+                        void* stream);
+
+/* zs_compact_rows: stable compaction of the rows still decoding.  rowmap[0..n) = the r with
+ * done[r] == 0 in increasing order, rowmap[n..nrows) = nrows (padding), *n_active = n.
+ * Lets a greedy decode skip the rows that already emitted a stop token (the reference keeps
+ * computing them, gpt2_prefix_eval.py:200-215; their outputs are discarded either way). */
+int zs_compact_rows(const int* done, int nrows, int* rowmap, int* n_active, void* stream);
 
 /* zs_lmhead_topk: per row m of A [M][K] (dtype) against W [V][K] (dtype; tied wte):
  *   logits = A W^T, split in column blocks of 128; per (row, block) writes the block's max,
@@ -183,10 +209,17 @@ int zs_argmax_finalize(const float* part_val, const int* part_idx, int M, int nb
  * next_tok[r] = tok.  `step` is read from *step_ctr (device) and *step_ctr += 1 by the last
  * block, so a captured graph replays without host arguments.  all_done[0] = AND(done);
  * all_done[1] is the blocks' arrival counter: zero it once before the first call (every call
- * re-arms it). */
+ * re-arms it); all_done[2] = the number of rows not done after this step. */
 int zs_greedy_step(const float* part_val, const int* part_idx, int R, int nblk, int* step_ctr,
                    int max_steps, int stop0, int stop1, int* out_ids, int* out_len, int* done,
                    int* pos, int* next_tok, int* all_done, void* stream);
+
+/* zs_greedy_step_map: zs_greedy_step where partial row c belongs to physical row rowmap[c]
+ * (out_ids, out_len, done, pos, next_tok are physical); padding slots are skipped. */
+int zs_greedy_step_map(const float* part_val, const int* part_idx, int R, const int* rowmap,
+                       int nphys, int nblk, int* step_ctr, int max_steps, int stop0, int stop1,
+                       int* out_ids, int* out_len, int* done, int* pos, int* next_tok,
+                       int* all_done, void* stream);
 
 /* zs_beam_step: generate_beam's per-step update (gpt2_prefix_eval.py:119-151) for C clips x
  * `beam` rows, from zs_lmhead_topk partials (topk >= beam) with log(softmax) semantics.

@@ -252,6 +252,90 @@ def test_decode_attention_bf16(cuda, use_kvrow, variant):
         assert torch.equal(vc[r, :, p], qkv[r, 2 * D:].view(H, 64))
 
 
+@pytest.mark.parametrize("nrows", [1, 700, 2500])
+def test_compact_rows(cuda, nrows):
+    """Stable compaction of the not-done rows; padding = nrows."""
+    from zsaac import ops
+    g = torch.Generator(device="cpu").manual_seed(nrows)
+    done = (torch.rand(nrows, generator=g) < 0.4).int().to(cuda)
+    rowmap = torch.full((nrows,), -1, device=cuda, dtype=torch.int32)
+    n = torch.zeros(1, device=cuda, dtype=torch.int32)
+    ops.compact_rows(done, nrows, rowmap, n)
+    act = torch.nonzero(done.cpu() == 0).flatten().int()
+    assert int(n) == act.numel()
+    assert torch.equal(rowmap.cpu()[:act.numel()], act)
+    assert bool((rowmap.cpu()[act.numel():] == nrows).all())
+
+
+def test_decode_map_kernels_match_direct(cuda):
+    """The rowmap variants of embed_tokens / decode_attention / greedy_step on a compacted row
+    set give, for every active row, bit-identical results to the direct kernels; padding slots
+    leave physical state untouched."""
+    from zsaac import ops
+    R, D, H, Lmax, V = 96, 768, 12, 100, 50257
+    g = torch.Generator(device="cuda").manual_seed(3)
+    wte = (torch.randn(V, D, device=cuda, generator=g) * 0.05).bfloat16()
+    wpe = (torch.randn(Lmax, D, device=cuda, generator=g) * 0.05).bfloat16()
+    tok = torch.randint(0, V, (R,), device=cuda, generator=g, dtype=torch.int32)
+    pos = torch.randint(0, Lmax - 1, (R,), device=cuda, generator=g, dtype=torch.int32)
+    done = (torch.rand(R, device=cuda, generator=g) < 0.5).int()
+    rowmap = torch.empty(R, device=cuda, dtype=torch.int32)
+    n = torch.zeros(1, device=cuda, dtype=torch.int32)
+    ops.compact_rows(done, R, rowmap, n)
+    na = int(n)
+    Rb = na + 5                          # a few padding slots
+    act = rowmap[:na].long()
+    # embed
+    x_full = torch.empty(R, D, device=cuda)
+    ops.embed_tokens(tok, pos, wte, wpe, x_full)
+    x_c = torch.full((Rb, D), 7.0, device=cuda)
+    ops.embed_tokens_map(tok, pos, rowmap, R, wte, wpe, x_c, Rb)
+    assert torch.equal(x_c[:na], x_full[act]) and bool((x_c[na:] == 0).all())
+    # decode attention
+    kc = torch.randn(R, H, Lmax, 64, device=cuda, generator=g).bfloat16()
+    vc = torch.randn(R, H, Lmax, 64, device=cuda, generator=g).bfloat16()
+    kc2, vc2 = kc.clone(), vc.clone()
+    qkv = torch.randn(R, 3 * D, device=cuda, generator=g).bfloat16()
+    out = torch.empty(R, D, device=cuda, dtype=torch.bfloat16)
+    ops.decode_attention(qkv, R, D, H, kc, vc, Lmax, pos, out)
+    qkv_c = torch.zeros(Rb, 3 * D, device=cuda, dtype=torch.bfloat16)
+    qkv_c[:na] = qkv[act]
+    out_c = torch.empty(Rb, D, device=cuda, dtype=torch.bfloat16)
+    ops.decode_attention_map(qkv_c, Rb, rowmap, R, D, H, kc2, vc2, Lmax, pos, out_c)
+    assert torch.equal(out_c[:na], out[act]) and bool((out_c[na:] == 0).all())
+    dn = done.bool()
+    assert torch.equal(kc2[~dn], kc[~dn]) and torch.equal(vc2[~dn], vc[~dn])
+    # greedy step
+    nblk = ops.lmhead_nblk(V)
+    pv = torch.randn(R, nblk, 1, device=cuda, generator=g)
+    pi = torch.randint(0, V, (R, nblk, 1), device=cuda, generator=g, dtype=torch.int32)
+    st = [t.clone() for t in (done, pos, tok)]
+    kw = dict(max_steps=67, stop0=13, stop1=764)
+
+    def state():
+        return dict(step=torch.tensor([5], device=cuda, dtype=torch.int32),
+                    out_ids=torch.zeros(R, 67, device=cuda, dtype=torch.int32),
+                    out_len=torch.full((R,), 3, device=cuda, dtype=torch.int32),
+                    done=st[0].clone(), pos=st[1].clone(), tok=st[2].clone(),
+                    flag=torch.zeros(3, device=cuda, dtype=torch.int32))
+    a, b = state(), state()
+    ops.greedy_step(pv, pi, R, nblk, a["step"], kw["max_steps"], kw["stop0"], kw["stop1"],
+                    a["out_ids"], a["out_len"], a["done"], a["pos"], a["tok"], a["flag"])
+    pv_c = torch.zeros(Rb, nblk, 1, device=cuda)
+    pi_c = torch.zeros(Rb, nblk, 1, device=cuda, dtype=torch.int32)
+    pv_c[:na], pi_c[:na] = pv[act], pi[act]
+    ops.greedy_step_map(pv_c, pi_c, Rb, rowmap, R, nblk, b["step"], kw["max_steps"], kw["stop0"],
+                        kw["stop1"], b["out_ids"], b["out_len"], b["done"], b["pos"], b["tok"],
+                        b["flag"])
+    for k in ("out_ids", "out_len", "done"):
+        assert torch.equal(a[k], b[k]), k
+    for k in ("pos", "tok"):
+        assert torch.equal(a[k][act], b[k][act]), k
+        assert torch.equal(b[k][dn], st[("pos", "tok").index(k) + 1][dn]), k
+    assert int(b["step"]) == 6 and a["flag"][[0, 2]].tolist() == b["flag"][[0, 2]].tolist()
+    assert int(b["flag"][2]) == int((b["done"] == 0).sum())
+
+
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 def test_lmhead_topk(cuda, dtype):
     from zsaac import ops

@@ -137,6 +137,40 @@ def test_c1_bf16_logits_and_agreement(cuda, golden, caption_sd):
     print(f"bf16 greedy: {agree}/{int(g['greedy_len'][:B].sum())} leading tokens agree")
 
 
+def test_bf16_compacted_decode_equals_full(cuda, golden, caption_sd):
+    """Greedy row compaction (decode only the rows that have not stopped, in 256-row buckets)
+    gives ids and lengths identical to the uncompacted bf16 decode: 640 clips (buckets 512 and
+    640), through the synchronous loop and the concurrent runner."""
+    from zsaac import synthetic as S
+    from zsaac.pipeline import CaptionConfig, CaptionPipeline, ConcurrentRunner
+    g = golden("c1_greedy.npz")
+    B = 640
+    base = torch.from_numpy(g["clap_emb"]).to(cuda)
+    gen = torch.Generator(device="cpu").manual_seed(7)
+    emb = base[torch.arange(B) % base.shape[0]] + \
+        0.05 * torch.randn(B, base.shape[1], generator=gen).to(cuda)
+    outs = {}
+    for compact in (False, True):
+        cfg = CaptionConfig(dtype=torch.bfloat16, batch=B, compact_decode=compact)
+        pipe = CaptionPipeline(caption_sd, None, S.label_table(), S.label_token_table(), cfg)
+        assert pipe.decoder.compact == compact
+        r = pipe.caption_emb(emb)
+        outs[compact] = (r.ids.cpu().numpy(), r.lengths.cpu().numpy())
+        if compact:
+            runner = ConcurrentRunner(pipe, 2)
+            runner.warmup_emb(emb)
+            rr = runner.run([emb, emb.flip(0)], inputs="emb")
+            outs["runner"] = (rr[0].ids.cpu().numpy(), rr[0].lengths.cpu().numpy())
+            outs["runner_flip"] = (rr[1].ids.cpu().numpy()[::-1], rr[1].lengths.cpu().numpy()[::-1])
+    ln = outs[False][1]
+    print(f"compaction test: mean length {ln.mean():.1f}, stopped early {(ln < 67).mean():.2f}")
+    assert (ln < 67).any(), "no row stopped early: the test would not exercise compaction"
+    for k in (True, "runner", "runner_flip"):
+        assert np.array_equal(outs[k][1], ln), k
+        for b in range(B):
+            assert outs[k][0][b, :ln[b]].tolist() == outs[False][0][b, :ln[b]].tolist(), (k, b)
+
+
 @pytest.mark.parametrize("beam", [5, 3])
 def test_beam_f32(cuda, golden, caption_sd, beam):
     g = golden("beam.npz")

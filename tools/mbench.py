@@ -286,7 +286,78 @@ def bench_inflight():
               f"decode steps {runner.decode_steps}", flush=True)
 
 
+def bench_buckets():
+    """Greedy decode chunk time per compaction bucket (G32 = 2048 rows, one stream) vs the
+    uncompacted chunk: is a step's time proportional to its rows?"""
+    sys.path.insert(0, ROOT)
+    import bench
+
+    class A:
+        batch, dtype, encoder, mapper, beam, entry_length, group = 64, "bf16", "htsat", "mlp", 0, 67, 32
+    pipe, _, _ = bench.build(A, torch.device("cuda", 0))
+    g = torch.Generator(device="cuda").manual_seed(1)
+    wav = (torch.randn(2048, 320000, device="cuda", generator=g) * 0.1).clamp_(-1, 1)
+    pipe.caption_wav(wav)
+    dec = pipe.decoder
+    R = dec._cgreedy
+    print(f"rows {R}, chunk {dec.chunk}, done {int(dec.done.sum())}", flush=True)
+    plans = [("full", dec._active[0], dec._active[1], None)]
+    for Rb in range(dec.min_bucket, R + 1, dec.bucket):
+        plans.append((f"Rb={Rb}",) + dec._chunk_plan(Rb))
+    for name, key, body, pre in plans:
+        gr = dec._graph(key, body, pre)
+        gr.replay()
+        torch.cuda.synchronize()
+        ts = []
+        for _ in range(5):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(4):
+                gr.replay()
+            e1.record()
+            e1.synchronize()
+            ts.append(e0.elapsed_time(e1) / 4 / dec.chunk)
+        ts.sort()
+        print(f"{name:10s} {ts[2] * 1e3:8.1f} us/step", flush=True)
+
+
+def bench_compact_ab():
+    """End-to-end clips/s (G32 batches of 2048) with/without compaction, fixed vs adaptive
+    buckets, 1 and 2 batches in flight."""
+    sys.path.insert(0, ROOT)
+    import bench
+    from zsaac.pipeline import ConcurrentRunner
+    g = torch.Generator(device="cuda").manual_seed(1)
+    wavs = [(torch.randn(2048, 320000, device="cuda", generator=g) * 0.1).clamp_(-1, 1) for _ in range(2)]
+    for compact in (0, 1):
+        class A:
+            batch, dtype, encoder, mapper, beam, entry_length, group = 64, "bf16", "htsat", "mlp", 0, 67, 32
+        A.compact = compact
+        pipe, _, _ = bench.build(A, torch.device("cuda", 0))
+        for k in (1, 2):
+            runner = ConcurrentRunner(pipe, k)
+            runner.warmup(wavs[0])
+            for fixed in ((0, 1) if compact else (0,)):
+                for p in runner.pipes:
+                    if fixed:
+                        p.decoder._bucket_rows = lambda R, alive: R
+                    else:
+                        p.decoder.__dict__.pop("_bucket_rows", None)
+                runner.run(wavs[:k])
+                torch.cuda.synchronize()
+                nb = 4
+                t = time.perf_counter()
+                runner.run([wavs[i % 2] for i in range(nb)])
+                torch.cuda.synchronize()
+                dt = time.perf_counter() - t
+                print(f"compact={compact} fixed={fixed} inflight={k}: {nb * 2048 / dt:8.1f} clips/s",
+                      flush=True)
+            del runner
+        del pipe
+        torch.cuda.empty_cache()
+
+
 if __name__ == "__main__":
     which = sys.argv[1:] or ["gemm", "attn"]
     for wname in which:
-        {"gemm": bench_gemm, "gemm_m": bench_gemm_m, "gemm_htsat": bench_gemm_htsat, "gemm_dbg": bench_gemm_dbg, "lmhead": bench_lmhead, "front": bench_front, "window": bench_window, "decode_gemm": bench_decode_gemm, "attn": bench_attn, "inflight": bench_inflight}[wname]()
+        {"gemm": bench_gemm, "gemm_m": bench_gemm_m, "gemm_htsat": bench_gemm_htsat, "gemm_dbg": bench_gemm_dbg, "lmhead": bench_lmhead, "front": bench_front, "window": bench_window, "decode_gemm": bench_decode_gemm, "attn": bench_attn, "inflight": bench_inflight, "buckets": bench_buckets, "compact_ab": bench_compact_ab}[wname]()

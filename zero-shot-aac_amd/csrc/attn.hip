@@ -387,15 +387,23 @@ __global__ __launch_bounds__(256) void decode_attn5_kernel(const T* __restrict__
                                                            T* __restrict__ vc, int Lmax,
                                                            const int* __restrict__ pos,
                                                            const int* __restrict__ kvrow,
-                                                           T* __restrict__ out) {
+                                                           T* __restrict__ out,
+                                                           const int* __restrict__ rowmap,
+                                                           int nphys) {
   static_assert(sizeof(T) == 2, "bf16 only");
   constexpr int HD = 64, EPC = 8;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int r = blockIdx.x, h = blockIdx.y * 4 + wid;
+  const int c = blockIdx.x, h = blockIdx.y * 4 + wid;   // c: compact row of qkv / out
   if (h >= heads) return;
   const int grp = lane >> 3, sub = lane & 7;
+  const int r = rowmap ? rowmap[c] : c;                  // r: physical row of pos / cache
+  if (r >= nphys) {                                      // padding slot of a compacted step
+    if (grp == 0)
+      *reinterpret_cast<uint4*>(out + (long)c * D + h * HD + sub * EPC) = make_uint4(0, 0, 0, 0);
+    return;
+  }
   const int p = min(pos[r], Lmax - 1);
-  const T* row = qkv + (long)r * 3 * D + h * HD + sub * EPC;
+  const T* row = qkv + (long)c * 3 * D + h * HD + sub * EPC;
   const uint4 qu = *reinterpret_cast<const uint4*>(row);
   const uint4 knu = *reinterpret_cast<const uint4*>(row + D);
   const uint4 vnu = *reinterpret_cast<const uint4*>(row + 2 * D);
@@ -466,7 +474,7 @@ __global__ __launch_bounds__(256) void decode_attn5_kernel(const T* __restrict__
     T* oe = reinterpret_cast<T*>(&ou);
 #pragma unroll
     for (int t = 0; t < EPC; ++t) stf(oe + t, o[t] * inv);
-    *reinterpret_cast<uint4*>(out + (long)r * D + h * HD + sub * EPC) = ou;
+    *reinterpret_cast<uint4*>(out + (long)c * D + h * HD + sub * EPC) = ou;
   }
 }
 
@@ -610,6 +618,20 @@ extern "C" int zs_row_attention(const void* q, int ldq, const void* k, const voi
   return 0;
 }
 
+extern "C" int zs_decode_attention_map(const void* qkv, int R, const int* rowmap, int nphys,
+                                       int D, int heads, void* kc, void* vc, int Lmax,
+                                       const int* pos, void* out, int dtype, void* stream) {
+  ZS_REQUIRE(R > 0 && heads > 0 && D / heads == 64 && D % heads == 0 && rowmap && nphys > 0,
+             "zs_decode_attention_map: head_dim must be 64");
+  ZS_REQUIRE(dtype == ZS_BF16 && Lmax > 0 && Lmax <= 8 * DA5_MAXI,
+             "zs_decode_attention_map: bf16 with Lmax <= %d only", 8 * DA5_MAXI);
+  hipLaunchKernelGGL(decode_attn5_kernel<bf16_t>, dim3(R, cdiv(heads, 4)), dim3(256), 0,
+                     S(stream), (const bf16_t*)qkv, D, heads, (bf16_t*)kc, (bf16_t*)vc, Lmax, pos,
+                     (const int*)nullptr, (bf16_t*)out, rowmap, nphys);
+  ZS_LAUNCH_CHECK();
+  return 0;
+}
+
 extern "C" int zs_decode_attention(const void* qkv, int R, int D, int heads, void* kc, void* vc,
                                    int Lmax, const int* pos, const int* kvrow, void* out,
                                    int dtype, void* stream) {
@@ -620,7 +642,7 @@ extern "C" int zs_decode_attention(const void* qkv, int R, int D, int heads, voi
   if (dtype == ZS_BF16 && Lmax <= 8 * DA5_MAXI && g_decode_attn5) {
     hipLaunchKernelGGL(decode_attn5_kernel<bf16_t>, dim3(R, cdiv(heads, 4)), dim3(256), 0,
                        S(stream), (const bf16_t*)qkv, D, heads, (bf16_t*)kc, (bf16_t*)vc, Lmax,
-                       pos, kvrow, (bf16_t*)out);
+                       pos, kvrow, (bf16_t*)out, (const int*)nullptr, R);
     ZS_LAUNCH_CHECK();
     return 0;
   }

@@ -108,11 +108,55 @@ __global__ void prefill_embed_kernel(const int* __restrict__ hard_ids,
 template <typename T>
 __global__ void embed_tokens_kernel(const int* __restrict__ tok, const int* __restrict__ pos,
                                     const T* __restrict__ wte, const T* __restrict__ wpe, int D,
-                                    float* __restrict__ x) {
-  const int r = blockIdx.x;
-  const int t = tok[r], p = pos[r];
+                                    float* __restrict__ x, const int* __restrict__ rowmap,
+                                    int nphys) {
+  const int r = blockIdx.x;                       // compact row (x is compact)
+  const int ph = rowmap ? rowmap[r] : r;           // physical decode row (tok/pos are physical)
+  if (ph >= nphys) {                               // padding slot of a compacted step
+    for (int d = threadIdx.x; d < D; d += blockDim.x) x[(long)r * D + d] = 0.f;
+    return;
+  }
+  const int t = tok[ph], p = pos[ph];
   for (int d = threadIdx.x; d < D; d += blockDim.x)
     x[(long)r * D + d] = ldf(wte + (long)t * D + d) + ldf(wpe + (long)p * D + d);
+}
+
+// active-row compaction (one 1024-thread block): rowmap[0..n) = the rows with done == 0 in
+// increasing order, rowmap[n..nrows) = nrows (padding), *n_active = n.  Deterministic.
+__global__ __launch_bounds__(1024) void compact_rows_kernel(const int* __restrict__ done, int nrows,
+                                                             int* __restrict__ rowmap,
+                                                             int* __restrict__ n_active) {
+  __shared__ int wsum[16];
+  __shared__ int base;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (threadIdx.x == 0) base = 0;
+  __syncthreads();
+  for (int c0 = 0; c0 < nrows; c0 += 1024) {
+    const int r = c0 + threadIdx.x;
+    const int a = (r < nrows && !done[r]) ? 1 : 0;
+    // inclusive scan within the wave
+    int inc = a;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const int o = __shfl_up(inc, d, 64);
+      if (lane >= d) inc += o;
+    }
+    if (lane == 63) wsum[wid] = inc;
+    __syncthreads();
+    int off = base;
+    for (int w = 0; w < wid; ++w) off += wsum[w];
+    if (a) rowmap[off + inc - 1] = r;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      int t = 0;
+      for (int w = 0; w < 16; ++w) t += wsum[w];
+      base += t;
+    }
+    __syncthreads();
+  }
+  const int n = base;
+  for (int r = n + threadIdx.x; r < nrows; r += 1024) rowmap[r] = nrows;
+  if (threadIdx.x == 0) *n_active = n;
 }
 
 // ------------------------------------------------------------------ argmax over LM-head partials
@@ -156,14 +200,15 @@ __global__ __launch_bounds__(256) void greedy_step_kernel(
     const float* __restrict__ pv, const int* __restrict__ pi, int R, int nblk, int* step_ctr,
     int max_steps, int stop0, int stop1, int* __restrict__ out_ids, int* __restrict__ out_len,
     int* __restrict__ done, int* __restrict__ pos, int* __restrict__ next_tok,
-    int* __restrict__ all_done) {
+    int* __restrict__ all_done, const int* __restrict__ rowmap, int nphys) {
   __shared__ int s_alive[5];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int step = __hip_atomic_load(step_ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  const int r = blockIdx.x * 4 + wid;
+  const int c = blockIdx.x * 4 + wid;             // compact row (partials are compact)
+  const int r = c < R ? (rowmap ? rowmap[c] : c) : nphys;   // physical row
   int alive = 0;
-  if (r < R) {
-    const int t = row_argmax(pv, pi, r, nblk, lane);
+  if (c < R && r < nphys) {
+    const int t = row_argmax(pv, pi, c, nblk, lane);
     if (lane == 0) {
       int d = done[r];
       if (!d && step < max_steps) {
@@ -186,6 +231,7 @@ __global__ __launch_bounds__(256) void greedy_step_kernel(
     if ((old & 0xffff) == (int)gridDim.x - 1) {
       const int total = (old >> 16) + a;
       all_done[0] = (total == 0 || step + 1 >= max_steps) ? 1 : 0;
+      all_done[2] = total;             // rows still decoding (sizes the next compacted chunk)
       __hip_atomic_store(step_ctr, step + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(&all_done[1], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
@@ -405,10 +451,33 @@ extern "C" int zs_embed_tokens(const int* tok, const int* pos, const void* wte, 
   ZS_REQUIRE(R > 0 && D > 0, "zs_embed_tokens: bad shape");
   if (dtype == ZS_BF16)
     hipLaunchKernelGGL(embed_tokens_kernel<bf16_t>, dim3(R), dim3(256), 0, S(stream), tok, pos,
-                       (const bf16_t*)wte, (const bf16_t*)wpe, D, x);
+                       (const bf16_t*)wte, (const bf16_t*)wpe, D, x, (const int*)nullptr, R);
   else
     hipLaunchKernelGGL(embed_tokens_kernel<float>, dim3(R), dim3(256), 0, S(stream), tok, pos,
-                       (const float*)wte, (const float*)wpe, D, x);
+                       (const float*)wte, (const float*)wpe, D, x, (const int*)nullptr, R);
+  ZS_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int zs_embed_tokens_map(const int* tok, const int* pos, const int* rowmap, int nphys,
+                                   const void* wte, const void* wpe, int R, int D, float* x,
+                                   int dtype, void* stream) {
+  ZS_REQUIRE(R > 0 && D > 0 && rowmap != nullptr && nphys > 0, "zs_embed_tokens_map: bad shape");
+  if (dtype == ZS_BF16)
+    hipLaunchKernelGGL(embed_tokens_kernel<bf16_t>, dim3(R), dim3(256), 0, S(stream), tok, pos,
+                       (const bf16_t*)wte, (const bf16_t*)wpe, D, x, rowmap, nphys);
+  else
+    hipLaunchKernelGGL(embed_tokens_kernel<float>, dim3(R), dim3(256), 0, S(stream), tok, pos,
+                       (const float*)wte, (const float*)wpe, D, x, rowmap, nphys);
+  ZS_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int zs_compact_rows(const int* done, int nrows, int* rowmap, int* n_active,
+                               void* stream) {
+  ZS_REQUIRE(nrows > 0, "zs_compact_rows: nrows");
+  hipLaunchKernelGGL(compact_rows_kernel, dim3(1), dim3(1024), 0, S(stream), done, nrows, rowmap,
+                     n_active);
   ZS_LAUNCH_CHECK();
   return 0;
 }
@@ -422,6 +491,20 @@ extern "C" int zs_argmax_finalize(const float* part_val, const int* part_idx, in
   return 0;
 }
 
+extern "C" int zs_greedy_step_map(const float* part_val, const int* part_idx, int R,
+                                  const int* rowmap, int nphys, int nblk, int* step_ctr,
+                                  int max_steps, int stop0, int stop1, int* out_ids, int* out_len,
+                                  int* done, int* pos, int* next_tok, int* all_done,
+                                  void* stream) {
+  ZS_REQUIRE(R > 0 && R < 65536 && nblk > 0 && max_steps > 0 && rowmap != nullptr && nphys > 0,
+             "zs_greedy_step_map: bad shape");
+  hipLaunchKernelGGL(greedy_step_kernel, dim3(cdiv(R, 4)), dim3(256), 0, S(stream), part_val,
+                     part_idx, R, nblk, step_ctr, max_steps, stop0, stop1, out_ids, out_len, done,
+                     pos, next_tok, all_done, rowmap, nphys);
+  ZS_LAUNCH_CHECK();
+  return 0;
+}
+
 extern "C" int zs_greedy_step(const float* part_val, const int* part_idx, int R, int nblk,
                               int* step_ctr, int max_steps, int stop0, int stop1, int* out_ids,
                               int* out_len, int* done, int* pos, int* next_tok, int* all_done,
@@ -429,7 +512,7 @@ extern "C" int zs_greedy_step(const float* part_val, const int* part_idx, int R,
   ZS_REQUIRE(R > 0 && R < 65536 && nblk > 0 && max_steps > 0, "zs_greedy_step: bad shape");
   hipLaunchKernelGGL(greedy_step_kernel, dim3(cdiv(R, 4)), dim3(256), 0, S(stream), part_val, part_idx, R,
                      nblk, step_ctr, max_steps, stop0, stop1, out_ids, out_len, done, pos,
-                     next_tok, all_done);
+                     next_tok, all_done, (const int*)nullptr, R);
   ZS_LAUNCH_CHECK();
   return 0;
 }

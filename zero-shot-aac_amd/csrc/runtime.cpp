@@ -39,3 +39,26 @@ extern "C" int zs_device_arch(char* buf, size_t len) {
   std::snprintf(buf, len, "%s", p.gcnArchName);
   return 0;
 }
+
+// A dedicated non-blocking stream, bound to its hardware queue now: ROCclr gives a stream its
+// hardware queue (round-robin over GPU_MAX_HW_QUEUES) at its first dispatch, so streams that
+// stay idle while other code creates and uses streams can end up sharing one queue — and two
+// streams on one queue run strictly one after the other.  One 4-byte fill + sync right after
+// creation makes streams created back to back take consecutive queues.
+extern "C" int zs_stream_create(void** stream) {
+  if (!stream) return ZS_ERR_ARG;
+  static int* scratch = nullptr;
+  if (!scratch) ZS_CHECK_HIP(hipMalloc(&scratch, 256));
+  hipStream_t s = nullptr;
+  ZS_CHECK_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  ZS_CHECK_HIP(hipMemsetAsync(scratch, 0, 4, s));
+  ZS_CHECK_HIP(hipStreamSynchronize(s));
+  *stream = (void*)s;
+  return 0;
+}
+
+extern "C" int zs_stream_destroy(void* stream) {
+  if (!stream) return ZS_ERR_ARG;
+  ZS_CHECK_HIP(hipStreamDestroy((hipStream_t)stream));
+  return 0;
+}

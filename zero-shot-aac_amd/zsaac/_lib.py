@@ -30,6 +30,8 @@ SIGNATURES = {
     "zs_last_error": [C.c_char_p, C.c_size_t],
     "zs_device_arch": [C.c_char_p, C.c_size_t],
     "zs_tune_set": [C.c_char_p, I],
+    "zs_stream_create": [P],
+    "zs_stream_destroy": [P],
     "zs_logmel": [P, I, I, P, P, P, P, P, P, P, P, P, P, P],
     "zs_wav2img": [P, I, I, P, P],
     "zs_patch_embed": [P, I, P, P, P, P, P, P],
@@ -50,6 +52,10 @@ SIGNATURES = {
     "zs_kv_write": [P, I, I, I, I, P, I, P, P, I, I, P],
     "zs_decode_attention": [P, I, I, I, P, P, I, P, P, P, I, P],
     "zs_embed_tokens": [P, P, P, P, I, I, P, I, P],
+    "zs_embed_tokens_map": [P, P, P, I, P, P, I, I, P, I, P],
+    "zs_decode_attention_map": [P, I, P, I, I, I, P, P, I, P, P, I, P],
+    "zs_compact_rows": [P, I, P, P, P],
+    "zs_greedy_step_map": [P, P, I, P, I, I, P, I, I, I, P, P, P, P, P, P, P],
     "zs_lmhead_topk": [I, I, I, I, P, I, P, I, I, P, P, P, P],
     "zs_lmhead_nblk": [I],
     "zs_argmax_finalize": [P, P, I, I, P, P],

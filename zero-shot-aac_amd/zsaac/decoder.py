@@ -189,7 +189,7 @@ class Gpt2Decoder:
 
     def __init__(self, w: Gpt2Weights, max_rows: int, max_prompt: int, max_steps: int = 67,
                  max_prefill_rows: Optional[int] = None, topk: int = 8, chunk: int = 0,
-                 use_graph: bool = True):
+                 use_graph: bool = True, compact: Optional[bool] = None):
         if chunk <= 0:   # a divisor of the steps after step 0, near 6 (no wasted tail steps)
             n = max(max_steps - 1, 1)
             cands = [c for c in range(4, 13) if n % c == 0]
@@ -230,7 +230,20 @@ class Gpt2Decoder:
         self.out_ids = torch.zeros(self.R, max_steps, **i32)
         self.out_len = torch.zeros(self.R, **i32)
         self.step_ctr = torch.zeros(1, **i32)
-        self.all_done = torch.zeros(2, **i32)    # [flag, greedy_step arrival counter]
+        # [flag, greedy_step arrival counter, rows still decoding]
+        self.all_done = torch.zeros(3, **i32)
+        # greedy row compaction: decode only the rows that have not stopped, in buckets of
+        # `bucket` rows (>= `min_bucket`, so the GEMMs stay in the tiled regime); bf16 only
+        # (decode_attn5), and the per-row arithmetic of every kernel is independent of the row
+        # count, so the ids equal the uncompacted decode's.
+        self.bucket, self.min_bucket = 256, 512
+        if compact is None:
+            compact = dt == torch.bfloat16
+        self.compact = (compact and dt == torch.bfloat16 and self.Lmax <= 128
+                        and self.R >= self.min_bucket)
+        self.rowmap = torch.zeros(self.R, **i32)
+        self.n_act = torch.zeros(1, **i32)
+        self._cgreedy = None
         self.plen = torch.zeros(self.Rp, **i32)
         self.last_row = torch.zeros(self.Rp, **i32)
         # beam state
@@ -240,6 +253,8 @@ class Gpt2Decoder:
         self.kvrow_tmp = torch.zeros(self.R, self.Lmax, **i32)
         self.tok_tmp = torch.zeros(self.R, max_steps, **i32)
         self.graphs: Dict[Tuple, torch.cuda.CUDAGraph] = {}
+        self.n_captures = 0
+        self.rows_stepped = 0       # decode rows x steps enqueued by step_chunk (work counter)
         self.ws = ops.skinny_workspace(dev, [(M, N, K) for M in {self.R, self.Rp}
                                              for N, K in ((3 * D, D), (D, D), (4 * D, D), (D, 4 * D))])
 
@@ -280,6 +295,55 @@ class Gpt2Decoder:
         self._layers(R, attn)
         ops.layernorm(self.x[:R], *self.w.lnf, out=self.hf[:R])
 
+    def _decode_forward_c(self, R, Rb):
+        """_decode_forward over the Rb compact slots of rowmap (physical rows < R)."""
+        ops.embed_tokens_map(self.next_tok, self.pos, self.rowmap, R, self.w.wte, self.w.wpe,
+                             self.x[:Rb], Rb)
+
+        def attn(l, qkv, att):
+            ops.decode_attention_map(qkv, Rb, self.rowmap, R, D, NH, self.kc[l], self.vc[l],
+                                     self.Lmax, self.pos, att)
+
+        self._layers(Rb, attn)
+        ops.layernorm(self.x[:Rb], *self.w.lnf, out=self.hf[:Rb])
+
+    def _greedy_step_body_c(self, R, Rb):
+        self._decode_forward_c(R, Rb)
+        ops.lmhead_topk(self.hf[:Rb], self.w.wte, 1, self.pstat, self.pval1, self.pidx1)
+        ops.greedy_step_map(self.pval1, self.pidx1, Rb, self.rowmap, R, self.nblk, self.step_ctr,
+                            self.max_steps, self.stop0, self.stop1, self.out_ids, self.out_len,
+                            self.done, self.pos, self.next_tok, self.all_done)
+
+    def _bucket_rows(self, R, alive):
+        if alive is None:
+            return R
+        return min(R, max(self.min_bucket, -(-alive // self.bucket) * self.bucket))
+
+    def _chunk_plan(self, alive=None):
+        """(graph key, step body, chunk prologue) of the active decode; ``alive`` is the host's
+        latest view of all_done[2] (None = unknown -> every row)."""
+        if self._cgreedy is None:
+            key, body = self._active
+            return key, body, None
+        R = self._cgreedy
+        Rb = self._bucket_rows(R, alive)
+        return (("greedy_c", R, Rb, self.stop0, self.stop1),
+                lambda: self._greedy_step_body_c(R, Rb),
+                lambda: ops.compact_rows(self.done, R, self.rowmap, self.n_act))
+
+    @staticmethod
+    def _rows_of(key):
+        return key[1] * key[2] if key[0] == "beam" else key[1]
+
+    def capture_buckets(self):
+        """Capture every compacted-greedy bucket graph of the active decode up front (so a timed
+        run never captures)."""
+        if self._cgreedy is None or not self.use_graph:
+            return
+        R = self._cgreedy
+        for Rb in sorted({self._bucket_rows(R, a) for a in range(0, R + 1, self.bucket)}):
+            self._graph(*self._chunk_plan(Rb))
+
     def _greedy_step_body(self, R):
         self._decode_forward(R)
         ops.lmhead_topk(self.hf[:R], self.w.wte, 1, self.pstat, self.pval1, self.pidx1)
@@ -287,27 +351,34 @@ class Gpt2Decoder:
                         self.stop0, self.stop1, self.out_ids, self.out_len, self.done, self.pos,
                         self.next_tok, self.all_done)
 
-    def _graph(self, key, body):
-        """The captured hipGraph of ``chunk`` consecutive decode steps (captured on first use:
-        one eager warm-up step on a side stream with the decode state saved/restored, then
-        capture)."""
+    def _graph(self, key, body, pre=None):
+        """The captured hipGraph of ``chunk`` consecutive decode steps, after the optional chunk
+        prologue ``pre`` (captured on first use: one eager warm-up step on a side stream with
+        the decode state saved/restored, then capture)."""
         g = self.graphs.get(key)
         if g is None:
             cur = torch.cuda.current_stream()
-            s = torch.cuda.Stream()
+            if getattr(self, "_cap_stream", None) is None:
+                self._cap_stream = torch.cuda.Stream()    # one side stream per decoder
+            s = self._cap_stream
             s.wait_stream(cur)
             saved = [t.clone() for t in self._state()]
             with torch.cuda.stream(s):
+                if pre is not None:
+                    pre()
                 body()
             cur.wait_stream(s)
             for t, v in zip(self._state(), saved):
                 t.copy_(v)
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):
+                if pre is not None:
+                    pre()
                 for _ in range(self.chunk):
                     body()
             cur.wait_stream(torch.cuda.current_stream())
             self.graphs[key] = g
+            self.n_captures += 1
         return g
 
     @property
@@ -315,20 +386,26 @@ class Gpt2Decoder:
         """Chunks after the prefill step that cover entry_length (step 0 runs with the prefill)."""
         return max(0, -(-(self.max_steps - 1) // self.chunk))
 
-    def step_chunk(self):
-        """Enqueue ``chunk`` decode steps of the active decode (no host sync)."""
-        key, body = self._active
+    def step_chunk(self, alive=None):
+        """Enqueue ``chunk`` decode steps of the active decode (no host sync).  ``alive``: an
+        upper bound on the rows still decoding (all_done[2] read after the previous chunk);
+        it only picks the compaction bucket, so None is always safe."""
+        key, body, pre = self._chunk_plan(alive)
+        self.rows_stepped += (key[2] if key[0] == "greedy_c" else self._rows_of(key)) * self.chunk
         if self.use_graph:
-            self._graph(key, body).replay()
+            self._graph(key, body, pre).replay()
         else:
+            if pre is not None:
+                pre()
             for _ in range(self.chunk):
                 body()
 
     def finished_async(self):
-        """Enqueue a copy of all_done to pinned host memory; returns (event, host tensor)."""
+        """Enqueue a copy of all_done to pinned host memory; returns (event, host tensor):
+        [0] = finished flag, [2] = rows still decoding."""
         if not hasattr(self, "_flag_host"):
-            self._flag_host = torch.zeros(1, dtype=torch.int32, pin_memory=True)
-        self._flag_host.copy_(self.all_done[:1], non_blocking=True)
+            self._flag_host = torch.zeros(3, dtype=torch.int32, pin_memory=True)
+        self._flag_host.copy_(self.all_done, non_blocking=True)
         ev = torch.cuda.Event()
         ev.record()
         return ev, self._flag_host
@@ -336,9 +413,10 @@ class Gpt2Decoder:
     def run_to_completion(self):
         """Synchronous loop: replay chunks until every row stopped or entry_length reached."""
         for _ in range(self.n_chunks):
-            if int(self.all_done[0].item()):
+            flag, _, alive = self.all_done.tolist()
+            if flag:
                 break
-            self.step_chunk()
+            self.step_chunk(alive)
 
     def _state(self):
         return [self.pos, self.next_tok, self.done, self.out_ids, self.out_len, self.step_ctr,
@@ -357,6 +435,7 @@ class Gpt2Decoder:
                         self.stop0, self.stop1, self.out_ids, self.out_len, self.done, self.pos,
                         self.next_tok, self.all_done)
         self._active = (("greedy", R, self.stop0, self.stop1), lambda: self._greedy_step_body(R))
+        self._cgreedy = R if (self.compact and R >= self.min_bucket) else None
 
     def greedy(self, B: int, Pmax: int):
         """After :meth:`prefill` (row_stride 1): generate2 for all B rows.
@@ -398,6 +477,7 @@ class Gpt2Decoder:
                       self.done, self.out_ids, self.tok_tmp, self.kvrow, self.kvrow_tmp, self.Lmax,
                       self.pos, self.next_tok, self.all_done)
         self._active = (("beam", C, beam, self.stop0), lambda: self._beam_step_body(C, beam))
+        self._cgreedy = None
 
     # ---------------------------------------------------------------- get_prefix_tokens
     def prefix_tokens(self, embed_rows: torch.Tensor, out_idx: torch.Tensor):

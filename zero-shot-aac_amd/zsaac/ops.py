@@ -240,6 +240,37 @@ def decode_attention(qkv, R, D, heads, kc, vc, Lmax, pos, out, kvrow=None):
     return out
 
 
+def dedicated_streams(n: int, device) -> list:
+    """n new HIP streams bound to distinct hardware queues (zs_stream_create), as torch streams.
+    torch's pooled streams get their hardware queue at first use, so concurrent batch streams
+    can silently land on one queue and serialize."""
+    import ctypes as C
+    out = []
+    with torch.cuda.device(device):
+        for _ in range(n):
+            h = C.c_void_p()
+            call("zs_stream_create", C.byref(h))
+            out.append(torch.cuda.ExternalStream(h.value, device=device))
+    return out
+
+
+def decode_attention_map(qkv, R, rowmap, nphys, D, heads, kc, vc, Lmax, pos, out):
+    """decode_attention over compact slots c < R whose physical row is rowmap[c]."""
+    call("zs_decode_attention_map", _p(qkv), R, _p(rowmap), nphys, D, heads, _p(kc), _p(vc), Lmax,
+         _p(pos), _p(out), dt(qkv), _s())
+    return out
+
+
+def embed_tokens_map(tok, pos, rowmap, nphys, wte, wpe, x, R):
+    call("zs_embed_tokens_map", _p(tok), _p(pos), _p(rowmap), nphys, _p(wte), _p(wpe), R,
+         wte.shape[1], _p(x), dt(wte), _s())
+    return x
+
+
+def compact_rows(done, nrows, rowmap, n_active):
+    call("zs_compact_rows", _p(done), nrows, _p(rowmap), _p(n_active), _s())
+
+
 def embed_tokens(tok, pos, wte, wpe, x, R=None):
     R = R if R is not None else tok.numel()
     call("zs_embed_tokens", _p(tok), _p(pos), _p(wte), _p(wpe), R, wte.shape[1], _p(x), dt(wte),
@@ -268,6 +299,13 @@ def greedy_step(part_val, part_idx, R, nblk, step_ctr, max_steps, stop0, stop1, 
                 done, pos, next_tok, all_done):
     call("zs_greedy_step", _p(part_val), _p(part_idx), R, nblk, _p(step_ctr), max_steps, stop0,
          stop1, _p(out_ids), _p(out_len), _p(done), _p(pos), _p(next_tok), _p(all_done), _s())
+
+
+def greedy_step_map(part_val, part_idx, R, rowmap, nphys, nblk, step_ctr, max_steps, stop0,
+                    stop1, out_ids, out_len, done, pos, next_tok, all_done):
+    call("zs_greedy_step_map", _p(part_val), _p(part_idx), R, _p(rowmap), nphys, nblk,
+         _p(step_ctr), max_steps, stop0, stop1, _p(out_ids), _p(out_len), _p(done), _p(pos),
+         _p(next_tok), _p(all_done), _s())
 
 
 def beam_step(part_stat, part_val, part_idx, C, beam, nblk, topk, first, stop, step_ctr,

@@ -37,6 +37,7 @@ class CaptionConfig:
     beam: int = 0                     # 0 -> greedy generate2, else generate_beam(beam_size)
     prefix_tokens: bool = True        # also compute get_prefix_tokens (predict_prompt.py:137)
     use_graph: bool = True
+    compact_decode: bool = True       # greedy bf16: decode only the rows that have not stopped
     encoder_batch: int = 64           # clips per encoder pass (the reference's eval batch size);
                                       # a larger ``batch`` is encoded in chunks of this size and
                                       # decoded together (clip results do not depend on it)
@@ -107,7 +108,8 @@ class CaptionPipeline:
         cfg, dev, B = self.cfg, self.dev, self.cfg.batch
         beam = max(cfg.beam, 1)
         self.decoder = Gpt2Decoder(self.gpt, B * beam, self.Pmax, cfg.entry_length,
-                                   max_prefill_rows=B, use_graph=cfg.use_graph)
+                                   max_prefill_rows=B, use_graph=cfg.use_graph,
+                                   compact=cfg.compact_decode)
         i32 = dict(device=dev, dtype=torch.int32)
         self.hard_ids = torch.zeros(B, self.h_cap, **i32)
         self.hard_len = torch.zeros(B, **i32)
@@ -206,7 +208,9 @@ class ConcurrentRunner:
 
     def __init__(self, pipe: CaptionPipeline, n_inflight: int = 2):
         self.pipes = [pipe] + [pipe.twin() for _ in range(n_inflight - 1)]
-        self.streams = [torch.cuda.Stream(device=pipe.dev) for _ in self.pipes]
+        # dedicated streams on distinct hardware queues: pooled torch streams take their queue at
+        # first use and can end up sharing one, which serializes the batches
+        self.streams = ops.dedicated_streams(len(self.pipes), pipe.dev)
 
     def warmup(self, wav: torch.Tensor):
         """Runs one batch per pipeline synchronously (captures every decode graph)."""
@@ -214,6 +218,7 @@ class ConcurrentRunner:
             s.wait_stream(torch.cuda.current_stream(p.dev))
             with torch.cuda.stream(s):
                 p.caption_wav(wav)
+                p.decoder.capture_buckets()
             s.synchronize()
 
     def warmup_emb(self, emb: torch.Tensor):
@@ -221,6 +226,7 @@ class ConcurrentRunner:
             s.wait_stream(torch.cuda.current_stream(p.dev))
             with torch.cuda.stream(s):
                 p.caption_emb(emb)
+                p.decoder.capture_buckets()
             s.synchronize()
 
     def run(self, batches: Sequence[torch.Tensor], keep=None, inputs: str = "wav") -> List[CaptionBatch]:
@@ -264,7 +270,7 @@ class ConcurrentRunner:
                     del active[i]
                 else:
                     with torch.cuda.stream(s):
-                        p.decoder.step_chunk()
+                        p.decoder.step_chunk(int(flag[2]))
                         ev, flag = p.decoder.finished_async()
                     active[i] = (bi, n + 1, ev, flag)
             if not progressed:
