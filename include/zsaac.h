@@ -164,23 +164,25 @@ int zs_kv_write(const void* qkv, int R, int n, int D, int heads, const int* pos0
 int zs_decode_attention(const void* qkv, int R, int D, int heads, void* kc, void* vc, int Lmax,
                         const int* pos, const int* kvrow, void* out, int dtype, void* stream);
 
-/* zs_decode_attention_map: zs_decode_attention over a compacted row set (bf16, Lmax <= 128,
- * no kvrow): qkv/out rows are compact slots c in [0, R); the physical decode row of slot c is
- * rowmap[c] (pos and the cache are indexed physically).  rowmap[c] >= nphys marks a padding
+/* zs_decode_attention_map: zs_decode_attention over a compacted row set (bf16, no kvrow):
+ * qkv/out rows are compact slots c in [0, R); the physical decode row of slot c is rowmap[c]
+ * (the cache is indexed physically).  The position of slot c is cpos[c] when cpos != NULL (as
+ * written by zs_embed_tokens_map), else pos[rowmap[c]].  rowmap[c] >= nphys marks a padding
  * slot: its out row is zeroed and the cache is untouched. */
 int zs_decode_attention_map(const void* qkv, int R, const int* rowmap, int nphys, int D, int heads,
-                            void* kc, void* vc, int Lmax, const int* pos, void* out, int dtype,
-                            void* stream);
+                            void* kc, void* vc, int Lmax, const int* pos, const int* cpos,
+                            void* out, int dtype, void* stream);
 
 /* zs_embed_tokens: x[r] = wte[tok[r]] + wpe[pos[r]] (f32 out), optional row gather. */
 int zs_embed_tokens(const int* tok, const int* pos, const void* wte, const void* wpe, int R, int D,
                     float* x, int dtype, void* stream);
 
 /* zs_embed_tokens_map: x[c] = wte[tok[rowmap[c]]] + wpe[pos[rowmap[c]]] for compact slots
- * c in [0, R); padding slots (rowmap[c] >= nphys) get x[c] = 0. */
+ * c in [0, R); padding slots (rowmap[c] >= nphys) get x[c] = 0.  cpos (optional, [R]) receives
+ * pos[rowmap[c]] (0 for padding) for zs_decode_attention_map. */
 int zs_embed_tokens_map(const int* tok, const int* pos, const int* rowmap, int nphys,
-                        const void* wte, const void* wpe, int R, int D, float* x, int dtype,
-                        void* stream);
+                        const void* wte, const void* wpe, int R, int D, float* x, int* cpos,
+                        int dtype, void* stream);
 
 /* zs_compact_rows: stable compaction of the rows still decoding.  rowmap[0..n) = the r with
  * done[r] == 0 in increasing order, rowmap[n..nrows) = nrows (padding), *n_active = n.

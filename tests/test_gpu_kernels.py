@@ -211,7 +211,7 @@ def test_decode_attention_matches_prefill(cuda):
 
 
 @pytest.mark.parametrize("use_kvrow", [False, True])
-@pytest.mark.parametrize("variant", [1, 0])
+@pytest.mark.parametrize("variant", [2, 1, 0])
 def test_decode_attention_bf16(cuda, use_kvrow, variant):
     """bf16 decode attention (register-resident decode_attn5, and the LDS-staged decode_attn4)
     vs an fp32 torch reference: ragged positions 0..Lmax-1 per row, optional beam kvrow
@@ -236,7 +236,7 @@ def test_decode_attention_bf16(cuda, use_kvrow, variant):
     try:
         ops.decode_attention(qkv, R, D, H, kc, vc, Lmax, pos, out, kvrow=kvrow)
     finally:
-        call("zs_tune_set", b"decode_attn5", 1)
+        call("zs_tune_set", b"decode_attn5", 2)
     qf = qkv.float()
     for r in range(R):
         p = int(pos[r])
@@ -305,6 +305,13 @@ def test_decode_map_kernels_match_direct(cuda):
     assert torch.equal(out_c[:na], out[act]) and bool((out_c[na:] == 0).all())
     dn = done.bool()
     assert torch.equal(kc2[~dn], kc[~dn]) and torch.equal(vc2[~dn], vc[~dn])
+    # compact positions from embed_tokens_map feed the same kernel
+    cpos = torch.full((Rb,), -1, device=cuda, dtype=torch.int32)
+    ops.embed_tokens_map(tok, pos, rowmap, R, wte, wpe, x_c, Rb, cpos=cpos)
+    assert torch.equal(cpos[:na], pos[act]) and bool((cpos[na:] == 0).all())
+    out_c2 = torch.empty_like(out_c)
+    ops.decode_attention_map(qkv_c, Rb, rowmap, R, D, H, kc2, vc2, Lmax, pos, out_c2, cpos=cpos)
+    assert torch.equal(out_c2, out_c)
     # greedy step
     nblk = ops.lmhead_nblk(V)
     pv = torch.randn(R, nblk, 1, device=cuda, generator=g)

@@ -106,7 +106,7 @@ def bench_gemm_htsat():
             b = torch.randn(N, device=dev)
             out = torch.empty(Mr, N, device=dev, dtype=torch.bfloat16)
             res = {}
-            for t, nm in ((4, "128x128"), (5, "128/32x4"), (1, "256/32x4"), (6, "256/64x2"), (2, "256x128"), (3, "128x256")):
+            for t, nm in ((0, "auto"), (4, "128x128"), (8, "128x64"), (11, "128/32s2"), (12, "128/32s3"), (5, "128/32x4"), (13, "64x64s2")):
                 call("zs_tune_set", b"fast_tile", t)
                 res[nm] = timeit(lambda: ops.gemm(a, w, out, bias=b, split_k=1), reps=20)
             call("zs_tune_set", b"fast_tile", 0)
@@ -114,7 +114,8 @@ def bench_gemm_htsat():
             res["old"] = timeit(lambda: ops.gemm(a, w, out, bias=b, split_k=1), reps=20)
             call("zs_tune_set", b"gemm_fast", 1)
             res["torch"] = timeit(lambda: torch.nn.functional.linear(a, w, b.bfloat16()), reps=20)
-            print(f"C{C:4d} M{Mr:7d} {name:6s} N{N:5d} K{K:5d}  " +
+            gbs = (Mr * K + Mr * N + N * K) * 2 / res["auto"] / 1e3
+            print(f"C{C:4d} M{Mr:7d} {name:6s} N{N:5d} K{K:5d} auto {gbs:5.0f} GB/s " +
                   "  ".join(f"{k}={v:8.2f}us" for k, v in res.items()), flush=True)
 
 
@@ -232,8 +233,8 @@ def bench_decode_gemm():
             ops.gemm(a, ws[it[0] % len(ws)], out, bias=b, split_k=1)
             it[0] += 1
         res = {}
-        for t, nm in ((0, "auto"), (4, "128x128"), (10, "128x128s3"), (7, "128/32s6"), (5, "128/32s4"),
-                      (8, "128x64"), (9, "64x128"), (1, "256/32s4w8")):
+        for t, nm in ((0, "auto"), (4, "128x128"), (11, "128/32s2"), (12, "128/32s3"), (5, "128/32s4"),
+                      (8, "128x64"), (9, "64x128"), (13, "64x64s2")):
             call("zs_tune_set", b"fast_tile", t)
             res[nm] = timeit(run, reps=len(ws))
         call("zs_tune_set", b"fast_tile", 0)
@@ -357,7 +358,40 @@ def bench_compact_ab():
         torch.cuda.empty_cache()
 
 
+def bench_host():
+    """Host (Python + ctypes) enqueue time vs GPU time of one group's begin_wav (encode 32 x 64
+    clips + mapper + prefill + step 0), and of one decode chunk."""
+    sys.path.insert(0, ROOT)
+    import bench
+
+    class A:
+        batch, dtype, encoder, mapper, beam, entry_length, group, compact = \
+            64, "bf16", "htsat", "mlp", 0, 67, 32, 1
+    pipe, _, _ = bench.build(A, torch.device("cuda", 0))
+    g = torch.Generator(device="cuda").manual_seed(1)
+    wav = (torch.randn(2048, 320000, device="cuda", generator=g) * 0.1).clamp_(-1, 1)
+    pipe.caption_wav(wav)
+    torch.cuda.synchronize()
+    for what, fn in (("encode 2048", lambda: pipe.encode(wav)), ("begin_wav 2048", lambda: pipe.begin_wav(wav)),
+                     ("encode 64", lambda: pipe.encoder.encode(wav[:64]))):
+        for _ in range(2):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            torch.cuda.synchronize()
+            e0.record()
+            t = time.perf_counter()
+            fn()
+            th = time.perf_counter() - t
+            e1.record()
+            e1.synchronize()
+            print(f"{what:16s} host {th * 1e3:8.2f} ms   gpu {e0.elapsed_time(e1):8.2f} ms", flush=True)
+
+
 if __name__ == "__main__":
+    if os.environ.get("ZS_TUNE"):          # e.g. ZS_TUNE=fast_xcd=0,fast_tile=4
+        from zsaac._lib import call
+        for kv in os.environ["ZS_TUNE"].split(","):
+            k, v = kv.split("=")
+            call("zs_tune_set", k.encode(), int(v))
     which = sys.argv[1:] or ["gemm", "attn"]
     for wname in which:
-        {"gemm": bench_gemm, "gemm_m": bench_gemm_m, "gemm_htsat": bench_gemm_htsat, "gemm_dbg": bench_gemm_dbg, "lmhead": bench_lmhead, "front": bench_front, "window": bench_window, "decode_gemm": bench_decode_gemm, "attn": bench_attn, "inflight": bench_inflight, "buckets": bench_buckets, "compact_ab": bench_compact_ab}[wname]()
+        {"gemm": bench_gemm, "gemm_m": bench_gemm_m, "gemm_htsat": bench_gemm_htsat, "gemm_dbg": bench_gemm_dbg, "lmhead": bench_lmhead, "front": bench_front, "window": bench_window, "decode_gemm": bench_decode_gemm, "attn": bench_attn, "inflight": bench_inflight, "buckets": bench_buckets, "compact_ab": bench_compact_ab, "host": bench_host}[wname]()

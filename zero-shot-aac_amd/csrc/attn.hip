@@ -9,7 +9,7 @@
 
 namespace zs {
 
-int g_decode_attn5 = 1;
+int g_decode_attn5 = 2;   // 2: decode_attn6 (phased), 1: decode_attn5, 0: LDS-staged
 int g_window_mfma = 1;    // zs_tune_set("window_mfma", 0): VALU window attention for bf16   // zs_tune_set("decode_attn5", 0): LDS-staged decode_attn4 for bf16
 
 // ------------------------------------------------------------------ HTSAT window attention
@@ -478,6 +478,114 @@ __global__ __launch_bounds__(256) void decode_attn5_kernel(const T* __restrict__
   }
 }
 
+// decode_attn6: decode_attn5's wave-per-(row, head) layout with the keys taken in phases of 64
+// (8 key groups x 8 keys, one 1 KiB wave-load each for K and V) and an online softmax across
+// phases, so a wave holds 64 keys' K/V in registers instead of 128 (~100 VGPRs: 4 waves per
+// SIMD instead of 2) and any Lmax works.  The per-slot inputs (rowmap, compact position) are
+// loaded together with the qkv row: one dependent round trip before the K/V loads.  With one
+// phase (p < 64) the arithmetic equals decode_attn5's.
+constexpr int DA6_KPP = 64;                  // keys per phase
+template <typename T>
+__global__ __launch_bounds__(256) void decode_attn6_kernel(
+    const T* __restrict__ qkv, int D, int heads, T* __restrict__ kc, T* __restrict__ vc, int Lmax,
+    const int* __restrict__ pos, const int* __restrict__ kvrow, T* __restrict__ out,
+    const int* __restrict__ rowmap, const int* __restrict__ cpos, int nphys) {
+  static_assert(sizeof(T) == 2, "bf16 only");
+  constexpr int HD = 64, EPC = 8, NG = DA6_KPP / 8;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int c = blockIdx.x, h = blockIdx.y * 4 + wid;
+  if (h >= heads) return;
+  const int grp = lane >> 3, sub = lane & 7;
+  const int r = rowmap ? rowmap[c] : c;
+  const int p0 = cpos ? cpos[c] : 0;
+  const T* row = qkv + (long)c * 3 * D + h * HD + sub * EPC;
+  const uint4 qu = *reinterpret_cast<const uint4*>(row);
+  const uint4 knu = *reinterpret_cast<const uint4*>(row + D);
+  const uint4 vnu = *reinterpret_cast<const uint4*>(row + 2 * D);
+  if (r >= nphys) {
+    if (grp == 0)
+      *reinterpret_cast<uint4*>(out + (long)c * D + h * HD + sub * EPC) = make_uint4(0, 0, 0, 0);
+    return;
+  }
+  const int p = min(cpos ? p0 : pos[r], Lmax - 1);
+  const long rh = ((long)r * heads + h) * Lmax;
+  if (grp == 0) {
+    *reinterpret_cast<uint4*>(kc + (rh + p) * HD + sub * EPC) = knu;
+    *reinterpret_cast<uint4*>(vc + (rh + p) * HD + sub * EPC) = vnu;
+  }
+  float q[EPC];
+  {
+    const T* e = reinterpret_cast<const T*>(&qu);
+#pragma unroll
+    for (int t = 0; t < EPC; ++t) q[t] = ldf(e + t) * 0.125f;
+  }
+  float m = -INFINITY, sum = 0.f, o[EPC];
+#pragma unroll
+  for (int t = 0; t < EPC; ++t) o[t] = 0.f;
+  for (int base = 0; base <= p; base += DA6_KPP) {
+    uint4 kr[NG], vr[NG];
+#pragma unroll
+    for (int i = 0; i < NG; ++i) {
+      const int j = base + i * 8 + grp;
+      kr[i] = make_uint4(0, 0, 0, 0);
+      vr[i] = make_uint4(0, 0, 0, 0);
+      if (j < p) {
+        const long src = kvrow ? ((long)kvrow[(long)r * Lmax + j] * heads + h) * Lmax : rh;
+        kr[i] = *reinterpret_cast<const uint4*>(kc + (src + j) * HD + sub * EPC);
+        vr[i] = *reinterpret_cast<const uint4*>(vc + (src + j) * HD + sub * EPC);
+      } else if (j == p) {
+        kr[i] = knu;
+        vr[i] = vnu;
+      }
+    }
+    float sc[NG];
+    float pm = -INFINITY;
+#pragma unroll
+    for (int i = 0; i < NG; ++i) {
+      const T* e = reinterpret_cast<const T*>(&kr[i]);
+      float sv = 0.f;
+#pragma unroll
+      for (int t = 0; t < EPC; ++t) sv += q[t] * ldf(e + t);
+      sv += __shfl_xor(sv, 1, 64);
+      sv += __shfl_xor(sv, 2, 64);
+      sv += __shfl_xor(sv, 4, 64);
+      sc[i] = (base + i * 8 + grp <= p) ? sv : -INFINITY;
+      pm = fmaxf(pm, sc[i]);
+    }
+    pm = fmaxf(pm, __shfl_xor(pm, 8, 64));
+    pm = fmaxf(pm, __shfl_xor(pm, 16, 64));
+    pm = fmaxf(pm, __shfl_xor(pm, 32, 64));
+    const float mn = fmaxf(m, pm);
+    const float scale = expf(m - mn);       // 0 on the first phase (m = -inf)
+    sum *= scale;
+#pragma unroll
+    for (int t = 0; t < EPC; ++t) o[t] *= scale;
+    m = mn;
+#pragma unroll
+    for (int i = 0; i < NG; ++i) {
+      const float e = (base + i * 8 + grp <= p) ? expf(sc[i] - m) : 0.f;
+      sum += e;
+      const T* v = reinterpret_cast<const T*>(&vr[i]);
+#pragma unroll
+      for (int t = 0; t < EPC; ++t) o[t] += e * ldf(v + t);
+    }
+  }
+#pragma unroll
+  for (int d = 8; d < 64; d <<= 1) {
+    sum += __shfl_xor(sum, d, 64);
+#pragma unroll
+    for (int t = 0; t < EPC; ++t) o[t] += __shfl_xor(o[t], d, 64);
+  }
+  if (grp == 0) {
+    const float inv = 1.0f / sum;
+    uint4 ou;
+    T* oe = reinterpret_cast<T*>(&ou);
+#pragma unroll
+    for (int t = 0; t < EPC; ++t) stf(oe + t, o[t] * inv);
+    *reinterpret_cast<uint4*>(out + (long)c * D + h * HD + sub * EPC) = ou;
+  }
+}
+
 template <typename T>
 __global__ __launch_bounds__(64) void decode_attn_kernel(const T* __restrict__ qkv, int D,
                                                          int heads, T* __restrict__ kc,
@@ -620,14 +728,21 @@ extern "C" int zs_row_attention(const void* q, int ldq, const void* k, const voi
 
 extern "C" int zs_decode_attention_map(const void* qkv, int R, const int* rowmap, int nphys,
                                        int D, int heads, void* kc, void* vc, int Lmax,
-                                       const int* pos, void* out, int dtype, void* stream) {
+                                       const int* pos, const int* cpos, void* out, int dtype,
+                                       void* stream) {
   ZS_REQUIRE(R > 0 && heads > 0 && D / heads == 64 && D % heads == 0 && rowmap && nphys > 0,
              "zs_decode_attention_map: head_dim must be 64");
-  ZS_REQUIRE(dtype == ZS_BF16 && Lmax > 0 && Lmax <= 8 * DA5_MAXI,
-             "zs_decode_attention_map: bf16 with Lmax <= %d only", 8 * DA5_MAXI);
-  hipLaunchKernelGGL(decode_attn5_kernel<bf16_t>, dim3(R, cdiv(heads, 4)), dim3(256), 0,
-                     S(stream), (const bf16_t*)qkv, D, heads, (bf16_t*)kc, (bf16_t*)vc, Lmax, pos,
-                     (const int*)nullptr, (bf16_t*)out, rowmap, nphys);
+  ZS_REQUIRE(dtype == ZS_BF16 && Lmax > 0 && Lmax <= 4096,
+             "zs_decode_attention_map: bf16 only, Lmax <= 4096");
+  if (g_decode_attn5 == 2 || cpos != nullptr || Lmax > 8 * DA5_MAXI) {
+    hipLaunchKernelGGL(decode_attn6_kernel<bf16_t>, dim3(R, cdiv(heads, 4)), dim3(256), 0,
+                       S(stream), (const bf16_t*)qkv, D, heads, (bf16_t*)kc, (bf16_t*)vc, Lmax,
+                       pos, (const int*)nullptr, (bf16_t*)out, rowmap, cpos, nphys);
+  } else {
+    hipLaunchKernelGGL(decode_attn5_kernel<bf16_t>, dim3(R, cdiv(heads, 4)), dim3(256), 0,
+                       S(stream), (const bf16_t*)qkv, D, heads, (bf16_t*)kc, (bf16_t*)vc, Lmax,
+                       pos, (const int*)nullptr, (bf16_t*)out, rowmap, nphys);
+  }
   ZS_LAUNCH_CHECK();
   return 0;
 }
@@ -639,6 +754,13 @@ extern "C" int zs_decode_attention(const void* qkv, int R, int D, int heads, voi
              "zs_decode_attention: head_dim must be 64");
   ZS_REQUIRE(Lmax > 0 && Lmax <= 4096, "zs_decode_attention: Lmax");
   dim3 grid(R, heads);
+  if (dtype == ZS_BF16 && g_decode_attn5 == 2) {
+    hipLaunchKernelGGL(decode_attn6_kernel<bf16_t>, dim3(R, cdiv(heads, 4)), dim3(256), 0,
+                       S(stream), (const bf16_t*)qkv, D, heads, (bf16_t*)kc, (bf16_t*)vc, Lmax,
+                       pos, kvrow, (bf16_t*)out, (const int*)nullptr, (const int*)nullptr, R);
+    ZS_LAUNCH_CHECK();
+    return 0;
+  }
   if (dtype == ZS_BF16 && Lmax <= 8 * DA5_MAXI && g_decode_attn5) {
     hipLaunchKernelGGL(decode_attn5_kernel<bf16_t>, dim3(R, cdiv(heads, 4)), dim3(256), 0,
                        S(stream), (const bf16_t*)qkv, D, heads, (bf16_t*)kc, (bf16_t*)vc, Lmax,

@@ -16,6 +16,7 @@ namespace zs {
 
 int g_gemm_fast = 1;   // zs_tune_set("gemm_fast", 0) selects the register-staged bf16 loop
 int g_gemm_dbg = 0;
+int g_fast_xcd = 1;       // zs_tune_set("fast_xcd", 0): n-fastest tile order
 
 __device__ __forceinline__ void store_out(void* out, int out_dtype, long idx, float v) {
   if (out_dtype == ZS_BF16) reinterpret_cast<bf16_t*>(out)[idx] = f2bf(v);
@@ -74,21 +75,19 @@ __global__ void splitk_reduce_kernel(GemmArgs g) {
 // One wave's parked [32][WN] f32 slab -> out rows mr0..mr0+31, cols nc0..nc0+WN-1: each lane
 // owns 8 consecutive columns (two ds_read_b128), so residual loads and the bf16 store are 16 B
 // per lane over contiguous row segments; ACT is a template parameter (no per-element switch).
-// (A fully unrolled variant with every load hoisted raised the kernel to >256 VGPRs and lost
-// occupancy: slower on every HTSAT shape.)
+// `bb` (the lane's 8 bias values) is loaded once per tile by the caller, and the slab's residual
+// rows are loaded before the slab is read back: a residual load issued after the previous
+// row's store would make its wait (vmcnt counts stores too) a full write round trip per row.
 template <int ACT, int WN>
 __device__ __forceinline__ void epi_slab(const GemmArgs& g, const float* slab, int mr0, int nc0,
-                                         int z, bool vec_out, bool vec_res) {
-  constexpr int Q = WN / 8;
+                                         int z, bool vec_out, bool vec_res, const float (&bb)[8],
+                                         const float4 (&res)[WN / 16][2]) {
+  constexpr int Q = WN / 8, IT = 32 * Q / 64;
+  static_assert(IT * 64 == 32 * Q, "slab iterations");
   const int lane = threadIdx.x & 63;
-  // a lane's 8 columns are the same in every iteration (64 % Q == 0): bias loaded once
-  float bb[8];
-  {
-    const int n = nc0 + (lane % Q) * 8, nv = min(8, g.N - n);
 #pragma unroll
-    for (int q = 0; q < 8; ++q) bb[q] = (g.bias && q < nv) ? g.bias[n + q] : 0.f;
-  }
-  for (int idx = lane; idx < 32 * Q; idx += 64) {
+  for (int it = 0; it < IT; ++it) {
+    const int idx = lane + 64 * it;
     const int r = idx / Q, c = (idx % Q) * 8;
     const int m = mr0 + r, n = nc0 + c;
     if (m >= g.M || n >= g.N) continue;
@@ -110,13 +109,12 @@ __device__ __forceinline__ void epi_slab(const GemmArgs& g, const float* slab, i
 #pragma unroll
     for (int q = 0; q < 8; ++q) v[q] = act_apply(v[q] + bb[q], ACT);
     if (g.residual) {
-      const float* rp = g.residual + (long)m * g.ldr + n;
       if (full && vec_res) {
-        const float4 r0 = reinterpret_cast<const float4*>(rp)[0];
-        const float4 r1 = reinterpret_cast<const float4*>(rp)[1];
+        const float4 r0 = res[it][0], r1 = res[it][1];
         v[0] += r0.x; v[1] += r0.y; v[2] += r0.z; v[3] += r0.w;
         v[4] += r1.x; v[5] += r1.y; v[6] += r1.z; v[7] += r1.w;
       } else {
+        const float* rp = g.residual + (long)m * g.ldr + n;
         for (int q = 0; q < nv; ++q) v[q] += rp[q];
       }
     }
@@ -140,12 +138,37 @@ __device__ __forceinline__ void epi_slab(const GemmArgs& g, const float* slab, i
   }
 }
 
+// the residual rows a lane's epi_slab iterations will add (full 8-column segments only)
+template <int WN>
+__device__ __forceinline__ void epi_res_load(const GemmArgs& g, int mr0, int nc0, bool vec_res,
+                                             float4 (&res)[WN / 16][2]) {
+  constexpr int Q = WN / 8, IT = 32 * Q / 64;
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int it = 0; it < IT; ++it) {
+    const int idx = lane + 64 * it;
+    const int m = mr0 + idx / Q, n = nc0 + (idx % Q) * 8;
+    if (g.residual && vec_res && g.split_k == 1 && m < g.M && n + 8 <= g.N) {
+      const float4* rp = reinterpret_cast<const float4*>(g.residual + (long)m * g.ldr + n);
+      res[it][0] = rp[0];
+      res[it][1] = rp[1];
+    } else {
+      res[it][0] = res[it][1] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  }
+}
+
 // bf16: the LDS-DMA staged main loop (gemm_fast.h).  Epilogue through LDS: each wave parks one
 // 32-row slab of its accumulators ([32][WN] f32, static register indexing), then re-reads it
 // row-wise so every lane owns 4 consecutive columns: bias / activation / residual / store move
 // 16 B (f32) or 8 B (bf16) per lane in full rows instead of 2-4 B column-strided scalars.
 template <int BM, int BN, int NS, int WGM, int WGN, int BK_>
-__global__ __launch_bounds__(64 * WGM * WGN) void gemm_fast_kernel(GemmArgs g) {
+// 4-wave tiles are held to 2 waves per SIMD (<= 256 unified VGPRs): two resident blocks per CU,
+// so one block's epilogue and DMA waits overlap the other's MFMAs (at 312 registers the 128x128
+// tile ran one block per CU)
+__global__ __launch_bounds__(64 * WGM * WGN,
+                             (WGM * WGN == 4 && NS * FastTile<BM, BN, WGM, WGN, BK_>::STAGE <= 80 * 1024)
+                                 ? 2 : 1) void gemm_fast_kernel(GemmArgs g) {
   using FT = FastTile<BM, BN, WGM, WGN, BK_>;
   __shared__ __attribute__((aligned(16))) char lds[NS * FT::STAGE];
   constexpr int TM = FT::TM, TN = FT::TN, WN = FT::WN;
@@ -154,8 +177,28 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_fast_kernel(GemmArgs g) {
   // k split), so the per-workgroup dispatch cost is paid once per resident block, not per tile
   const int ntn = cdiv(g.N, BN), ntm = cdiv(g.M, BM);
   const int ntiles = ntn * ntm * g.split_k;
+  // XCD-local order: workgroups are placed round-robin on the 8 XCDs (slot v runs on XCD v % 8
+  // whenever the grid is a multiple of 8 or one slot per tile), and each XCD has its own L2.
+  // Slot v -> u makes the tiles of one XCD a contiguous range (bijective for any count), and u
+  // walks groups of gm M-tiles column by column, so a range is a compact gm x (range/gm) patch
+  // of the output: its A rows and W rows stay in that XCD's L2 instead of every XCD streaming
+  // all of A and W.
+  const int q8 = ntiles >> 3, r8 = ntiles & 7;
+  int gm = (int)(sqrtf((float)max(1, q8) * BN / BM) + 0.5f);
+  gm = max(1, min(gm, ntm));
   for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
-  const int n0 = (t % ntn) * BN, m0 = ((t / ntn) % ntm) * BM, z = t / (ntn * ntm);
+  int n0, m0, z;
+  if (g.xcd) {
+    const int x = t & 7;
+    const int u = (x < r8 ? x * (q8 + 1) : r8 * (q8 + 1) + (x - r8) * q8) + (t >> 3);
+    z = u / (ntn * ntm);
+    const int w = u - z * (ntn * ntm), per = gm * ntn, grp = w / per, fm = grp * gm;
+    const int gs = min(ntm - fm, gm), r = w - grp * per;
+    m0 = (fm + r % gs) * BM;
+    n0 = (r / gs) * BN;
+  } else {
+    n0 = (t % ntn) * BN; m0 = ((t / ntn) % ntm) * BM; z = t / (ntn * ntm);
+  }
   const int kbeg = z * g.k_per_split, kend = min(g.K, kbeg + g.k_per_split);
   f32x16_t acc[TM][TN];
   const DenseRows A{(const bf16_t*)g.A, g.lda, g.M, m0};
@@ -178,8 +221,18 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_fast_kernel(GemmArgs g) {
                        (g.ldo % 8 == 0 && ((uintptr_t)g.out & 15) == 0);
   const bool vec_res = g.residual == nullptr ||
                        (g.ldr % 4 == 0 && ((uintptr_t)g.residual & 15) == 0);
+  // the lane's 8 bias columns are the same in every slab of the tile (64 % (WN/8) == 0)
+  float bb[8];
+  {
+    const int n = n0 + wc0 + (lane % (WN / 8)) * 8, nv = min(8, g.N - n);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) bb[q] = (g.bias && q < nv) ? g.bias[n + q] : 0.f;
+  }
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
+    const int mr0 = m0 + wr0 + i * 32, nc0 = n0 + wc0;
+    float4 res[WN / 16][2];
+    epi_res_load<WN>(g, mr0, nc0, vec_res, res);
 #pragma unroll
     for (int j = 0; j < TN; ++j)
 #pragma unroll
@@ -188,13 +241,12 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_fast_kernel(GemmArgs g) {
     // the slab is private to this wave and a wave's LDS accesses complete in issue order, so
     // no barrier: a __syncthreads() here would also wait for every outstanding global store
     // (vmcnt(0)) and serialise one full write round trip per row slab
-    const int mr0 = m0 + wr0 + i * 32, nc0 = n0 + wc0;
     switch (g.act) {
-      case ACT_GELU_ERF: epi_slab<ACT_GELU_ERF, WN>(g, slab, mr0, nc0, z, vec_out, vec_res); break;
-      case ACT_GELU_TANH: epi_slab<ACT_GELU_TANH, WN>(g, slab, mr0, nc0, z, vec_out, vec_res); break;
-      case ACT_RELU: epi_slab<ACT_RELU, WN>(g, slab, mr0, nc0, z, vec_out, vec_res); break;
-      case ACT_TANH: epi_slab<ACT_TANH, WN>(g, slab, mr0, nc0, z, vec_out, vec_res); break;
-      default: epi_slab<ACT_NONE, WN>(g, slab, mr0, nc0, z, vec_out, vec_res); break;
+      case ACT_GELU_ERF: epi_slab<ACT_GELU_ERF, WN>(g, slab, mr0, nc0, z, vec_out, vec_res, bb, res); break;
+      case ACT_GELU_TANH: epi_slab<ACT_GELU_TANH, WN>(g, slab, mr0, nc0, z, vec_out, vec_res, bb, res); break;
+      case ACT_RELU: epi_slab<ACT_RELU, WN>(g, slab, mr0, nc0, z, vec_out, vec_res, bb, res); break;
+      case ACT_TANH: epi_slab<ACT_TANH, WN>(g, slab, mr0, nc0, z, vec_out, vec_res, bb, res); break;
+      default: epi_slab<ACT_NONE, WN>(g, slab, mr0, nc0, z, vec_out, vec_res, bb, res); break;
     }
   }
   // every wave has read its slab before the next tile's DMAs refill the LDS (LDS-only wait:
@@ -238,6 +290,9 @@ static int dispatch_fast(GemmArgs& g, hipStream_t st) {
     case 8: return launch_fast<128, 64, 3>(g, st);
     case 9: return launch_fast<64, 128, 3>(g, st);
     case 10: return launch_fast<128, 128, 3>(g, st);
+    case 11: return launch_fast<128, 128, 2, 2, 2, 32>(g, st);
+    case 12: return launch_fast<128, 128, 3, 2, 2, 32>(g, st);
+    case 13: return launch_fast<64, 64, 2>(g, st);
     default: break;
   }
   if (nblocks(g, 128, 128) >= 256) {
@@ -558,7 +613,7 @@ extern "C" int zs_gemm(int M, int N, int K, int dtype, const void* A, int lda, c
     split_k = 1;
   }
   GemmArgs g{M, N, K, lda, ldw, ldr, ldo, A, W, bias, residual, out, out_dtype, act, 1, K, workspace,
-             g_gemm_dbg};
+             g_gemm_dbg, g_fast_xcd};
   if (split_k > 1) {
     int kps = cdiv(cdiv(K, split_k), BK) * BK;
     int s = cdiv(K, kps);

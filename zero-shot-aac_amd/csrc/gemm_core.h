@@ -30,6 +30,7 @@ struct GemmArgs {
   int out_dtype, act, split_k, k_per_split;
   float* ws;
   int dbg;   // experiment knob (zs_tune_set "gemm_dbg"): 1 = skip MFMA, 2 = skip DMA
+  int xcd;   // tile order: 1 = XCD-local grouped (zs_tune_set "fast_xcd"), 0 = n-fastest
 };
 
 // Loads a ROWS x 32 tile (row-major, K-contiguous) of a [nrows][ld] matrix into registers.

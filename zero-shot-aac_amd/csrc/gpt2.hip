@@ -109,14 +109,16 @@ template <typename T>
 __global__ void embed_tokens_kernel(const int* __restrict__ tok, const int* __restrict__ pos,
                                     const T* __restrict__ wte, const T* __restrict__ wpe, int D,
                                     float* __restrict__ x, const int* __restrict__ rowmap,
-                                    int nphys) {
+                                    int nphys, int* __restrict__ cpos) {
   const int r = blockIdx.x;                       // compact row (x is compact)
   const int ph = rowmap ? rowmap[r] : r;           // physical decode row (tok/pos are physical)
   if (ph >= nphys) {                               // padding slot of a compacted step
     for (int d = threadIdx.x; d < D; d += blockDim.x) x[(long)r * D + d] = 0.f;
+    if (cpos && threadIdx.x == 0) cpos[r] = 0;
     return;
   }
   const int t = tok[ph], p = pos[ph];
+  if (cpos && threadIdx.x == 0) cpos[r] = p;     // this step's position, in compact order
   for (int d = threadIdx.x; d < D; d += blockDim.x)
     x[(long)r * D + d] = ldf(wte + (long)t * D + d) + ldf(wpe + (long)p * D + d);
 }
@@ -451,24 +453,24 @@ extern "C" int zs_embed_tokens(const int* tok, const int* pos, const void* wte, 
   ZS_REQUIRE(R > 0 && D > 0, "zs_embed_tokens: bad shape");
   if (dtype == ZS_BF16)
     hipLaunchKernelGGL(embed_tokens_kernel<bf16_t>, dim3(R), dim3(256), 0, S(stream), tok, pos,
-                       (const bf16_t*)wte, (const bf16_t*)wpe, D, x, (const int*)nullptr, R);
+                       (const bf16_t*)wte, (const bf16_t*)wpe, D, x, (const int*)nullptr, R, (int*)nullptr);
   else
     hipLaunchKernelGGL(embed_tokens_kernel<float>, dim3(R), dim3(256), 0, S(stream), tok, pos,
-                       (const float*)wte, (const float*)wpe, D, x, (const int*)nullptr, R);
+                       (const float*)wte, (const float*)wpe, D, x, (const int*)nullptr, R, (int*)nullptr);
   ZS_LAUNCH_CHECK();
   return 0;
 }
 
 extern "C" int zs_embed_tokens_map(const int* tok, const int* pos, const int* rowmap, int nphys,
                                    const void* wte, const void* wpe, int R, int D, float* x,
-                                   int dtype, void* stream) {
+                                   int* cpos, int dtype, void* stream) {
   ZS_REQUIRE(R > 0 && D > 0 && rowmap != nullptr && nphys > 0, "zs_embed_tokens_map: bad shape");
   if (dtype == ZS_BF16)
     hipLaunchKernelGGL(embed_tokens_kernel<bf16_t>, dim3(R), dim3(256), 0, S(stream), tok, pos,
-                       (const bf16_t*)wte, (const bf16_t*)wpe, D, x, rowmap, nphys);
+                       (const bf16_t*)wte, (const bf16_t*)wpe, D, x, rowmap, nphys, cpos);
   else
     hipLaunchKernelGGL(embed_tokens_kernel<float>, dim3(R), dim3(256), 0, S(stream), tok, pos,
-                       (const float*)wte, (const float*)wpe, D, x, rowmap, nphys);
+                       (const float*)wte, (const float*)wpe, D, x, rowmap, nphys, cpos);
   ZS_LAUNCH_CHECK();
   return 0;
 }

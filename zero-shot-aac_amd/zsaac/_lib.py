@@ -52,8 +52,8 @@ SIGNATURES = {
     "zs_kv_write": [P, I, I, I, I, P, I, P, P, I, I, P],
     "zs_decode_attention": [P, I, I, I, P, P, I, P, P, P, I, P],
     "zs_embed_tokens": [P, P, P, P, I, I, P, I, P],
-    "zs_embed_tokens_map": [P, P, P, I, P, P, I, I, P, I, P],
-    "zs_decode_attention_map": [P, I, P, I, I, I, P, P, I, P, P, I, P],
+    "zs_embed_tokens_map": [P, P, P, I, P, P, I, I, P, P, I, P],
+    "zs_decode_attention_map": [P, I, P, I, I, I, P, P, I, P, P, P, I, P],
     "zs_compact_rows": [P, I, P, P, P],
     "zs_greedy_step_map": [P, P, I, P, I, I, P, I, I, I, P, P, P, P, P, P, P],
     "zs_lmhead_topk": [I, I, I, I, P, I, P, I, I, P, P, P, P],

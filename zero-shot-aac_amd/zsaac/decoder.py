@@ -242,6 +242,7 @@ class Gpt2Decoder:
         self.compact = (compact and dt == torch.bfloat16 and self.Lmax <= 128
                         and self.R >= self.min_bucket)
         self.rowmap = torch.zeros(self.R, **i32)
+        self.cpos = torch.zeros(self.R, **i32)      # this step's positions in compact order
         self.n_act = torch.zeros(1, **i32)
         self._cgreedy = None
         self.plen = torch.zeros(self.Rp, **i32)
@@ -298,11 +299,11 @@ class Gpt2Decoder:
     def _decode_forward_c(self, R, Rb):
         """_decode_forward over the Rb compact slots of rowmap (physical rows < R)."""
         ops.embed_tokens_map(self.next_tok, self.pos, self.rowmap, R, self.w.wte, self.w.wpe,
-                             self.x[:Rb], Rb)
+                             self.x[:Rb], Rb, cpos=self.cpos)
 
         def attn(l, qkv, att):
             ops.decode_attention_map(qkv, Rb, self.rowmap, R, D, NH, self.kc[l], self.vc[l],
-                                     self.Lmax, self.pos, att)
+                                     self.Lmax, self.pos, att, cpos=self.cpos)
 
         self._layers(Rb, attn)
         ops.layernorm(self.x[:Rb], *self.w.lnf, out=self.hf[:Rb])

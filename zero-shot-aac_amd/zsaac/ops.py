@@ -254,16 +254,16 @@ def dedicated_streams(n: int, device) -> list:
     return out
 
 
-def decode_attention_map(qkv, R, rowmap, nphys, D, heads, kc, vc, Lmax, pos, out):
+def decode_attention_map(qkv, R, rowmap, nphys, D, heads, kc, vc, Lmax, pos, out, cpos=None):
     """decode_attention over compact slots c < R whose physical row is rowmap[c]."""
     call("zs_decode_attention_map", _p(qkv), R, _p(rowmap), nphys, D, heads, _p(kc), _p(vc), Lmax,
-         _p(pos), _p(out), dt(qkv), _s())
+         _p(pos), _p(cpos), _p(out), dt(qkv), _s())
     return out
 
 
-def embed_tokens_map(tok, pos, rowmap, nphys, wte, wpe, x, R):
+def embed_tokens_map(tok, pos, rowmap, nphys, wte, wpe, x, R, cpos=None):
     call("zs_embed_tokens_map", _p(tok), _p(pos), _p(rowmap), nphys, _p(wte), _p(wpe), R,
-         wte.shape[1], _p(x), dt(wte), _s())
+         wte.shape[1], _p(x), _p(cpos), dt(wte), _s())
     return x
 
 
