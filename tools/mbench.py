@@ -133,10 +133,10 @@ def bench_gemm_dbg():
         w = (torch.randn(N, K, device=dev) * 0.02).bfloat16()
         out = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
         res = {}
-        for t, nm, pers in ((4, "128x128", 0), (4, "128x128P", 1), (1, "256x256P", 1)):
+        for t, nm, pers in ((4, "128x128P", 1),):
             call("zs_tune_set", b"fast_tile", t)
             call("zs_tune_set", b"fast_persist", pers)
-            for d, dn in ((0, "full"), (3, "noLoop"), (4, "noEpi")):
+            for d, dn in ((0, "full"), (1, "noMFMA"), (2, "noDMA"), (3, "noLoop"), (4, "noEpi")):
                 call("zs_tune_set", b"gemm_dbg", d)
                 res[f"{nm}/{dn}"] = timeit(lambda: ops.gemm(a, w, out, split_k=1), reps=20)
         call("zs_tune_set", b"gemm_dbg", 0)

@@ -186,27 +186,60 @@ __global__ __launch_bounds__(64 * WGM * WGN,
   const int q8 = ntiles >> 3, r8 = ntiles & 7;
   int gm = (int)(sqrtf((float)max(1, q8) * BN / BM) + 0.5f);
   gm = max(1, min(gm, ntm));
-  for (int t = blockIdx.x; t < ntiles; t += gridDim.x) {
-  int n0, m0, z;
-  if (g.xcd) {
-    const int x = t & 7;
-    const int u = (x < r8 ? x * (q8 + 1) : r8 * (q8 + 1) + (x - r8) * q8) + (t >> 3);
-    z = u / (ntn * ntm);
-    const int w = u - z * (ntn * ntm), per = gm * ntn, grp = w / per, fm = grp * gm;
-    const int gs = min(ntm - fm, gm), r = w - grp * per;
-    m0 = (fm + r % gs) * BM;
-    n0 = (r / gs) * BN;
-  } else {
-    n0 = (t % ntn) * BN; m0 = ((t / ntn) % ntm) * BM; z = t / (ntn * ntm);
+  auto tile = [&](int t, int& m0, int& n0, int& z) {
+    if (g.xcd) {
+      const int x = t & 7;
+      const int u = (x < r8 ? x * (q8 + 1) : r8 * (q8 + 1) + (x - r8) * q8) + (t >> 3);
+      z = u / (ntn * ntm);
+      const int w = u - z * (ntn * ntm), per = gm * ntn, grp = w / per, fm = grp * gm;
+      const int gs = min(ntm - fm, gm), r = w - grp * per;
+      m0 = (fm + r % gs) * BM;
+      n0 = (r / gs) * BN;
+    } else {
+      n0 = (t % ntn) * BN; m0 = ((t / ntn) % ntm) * BM; z = t / (ntn * ntm);
+    }
+  };
+  // Cross-tile prefetch (XPF): the next tile's prologue stages (0 .. NS-2) are issued before this
+  // tile's epilogue, whose slab lives in stage NS-1, so the DMA latency of the next tile's first
+  // k-steps runs under the epilogue, and its first waits may leave the epilogue's stores in
+  // flight (XS = a lower bound on the stores one wave issues for a full tile: >= 1 per slab row
+  // iteration).
+  constexpr bool XPF = FT::NW * 32 * WN * 4 <= FT::STAGE;
+  constexpr int XS = XPF ? TM * (32 * (WN / 8) / 64) : 0;
+  int m0, n0, z;
+  int t = blockIdx.x;
+  if (t < ntiles) tile(t, m0, n0, z);
+  bool pre = false, xs = false;
+  if (XPF && t < ntiles && g.dbg != 2 && g.dbg != 3) {
+    const int kb = z * g.k_per_split;
+    fast_prologue<BM, BN, NS, WGM, WGN, BK_>(DenseRows{(const bf16_t*)g.A, g.lda, g.M, m0},
+                                             DenseRows{(const bf16_t*)g.W, g.ldw, g.N, n0}, kb,
+                                             min(g.K, kb + g.k_per_split), lds);
+    pre = true;
   }
+  for (; t < ntiles; t += gridDim.x) {
   const int kbeg = z * g.k_per_split, kend = min(g.K, kbeg + g.k_per_split);
   f32x16_t acc[TM][TN];
   const DenseRows A{(const bf16_t*)g.A, g.lda, g.M, m0};
   const DenseRows B{(const bf16_t*)g.W, g.ldw, g.N, n0};
-  fast_mainloop<BM, BN, NS, WGM, WGN, BK_>(A, B, kbeg, kend, lds, acc, g.dbg);   // ends with a barrier
+  fast_mainloop<BM, BN, NS, WGM, WGN, BK_, false, XS>(A, B, kbeg, kend, lds, acc, g.dbg, nullptr,
+                                                      pre, xs);   // ends with a barrier
+  const int cm0 = m0, cn0 = n0, cz = z;
+  pre = xs = false;
+  if (XPF && t + (int)gridDim.x < ntiles && g.dbg != 2 && g.dbg != 3) {
+    tile(t + gridDim.x, m0, n0, z);
+    const int kb = z * g.k_per_split;
+    fast_prologue<BM, BN, NS, WGM, WGN, BK_>(DenseRows{(const bf16_t*)g.A, g.lda, g.M, m0},
+                                             DenseRows{(const bf16_t*)g.W, g.ldw, g.N, n0}, kb,
+                                             min(g.K, kb + g.k_per_split), lds);
+    pre = true;
+    xs = g.dbg != 4 && cm0 + BM <= g.M && cn0 + BN <= g.N;   // full tile: >= XS stores follow
+  } else if (t + (int)gridDim.x < ntiles) {
+    tile(t + gridDim.x, m0, n0, z);
+  }
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int wr0 = (wid / WGN) * FT::WM, wc0 = (wid % WGN) * WN;
-  float* slab = reinterpret_cast<float*>(lds) + wid * 32 * WN;
+  float* slab = reinterpret_cast<float*>(lds + (XPF ? (NS - 1) * FT::STAGE : 0)) + wid * 32 * WN;
   if (g.dbg == 4) {   // experiment: no epilogue (keep the accumulators alive)
     float t = 0.f;
 #pragma unroll
@@ -224,13 +257,13 @@ __global__ __launch_bounds__(64 * WGM * WGN,
   // the lane's 8 bias columns are the same in every slab of the tile (64 % (WN/8) == 0)
   float bb[8];
   {
-    const int n = n0 + wc0 + (lane % (WN / 8)) * 8, nv = min(8, g.N - n);
+    const int n = cn0 + wc0 + (lane % (WN / 8)) * 8, nv = min(8, g.N - n);
 #pragma unroll
     for (int q = 0; q < 8; ++q) bb[q] = (g.bias && q < nv) ? g.bias[n + q] : 0.f;
   }
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
-    const int mr0 = m0 + wr0 + i * 32, nc0 = n0 + wc0;
+    const int mr0 = cm0 + wr0 + i * 32, nc0 = cn0 + wc0;
     float4 res[WN / 16][2];
     epi_res_load<WN>(g, mr0, nc0, vec_res, res);
 #pragma unroll
@@ -242,11 +275,11 @@ __global__ __launch_bounds__(64 * WGM * WGN,
     // no barrier: a __syncthreads() here would also wait for every outstanding global store
     // (vmcnt(0)) and serialise one full write round trip per row slab
     switch (g.act) {
-      case ACT_GELU_ERF: epi_slab<ACT_GELU_ERF, WN>(g, slab, mr0, nc0, z, vec_out, vec_res, bb, res); break;
-      case ACT_GELU_TANH: epi_slab<ACT_GELU_TANH, WN>(g, slab, mr0, nc0, z, vec_out, vec_res, bb, res); break;
-      case ACT_RELU: epi_slab<ACT_RELU, WN>(g, slab, mr0, nc0, z, vec_out, vec_res, bb, res); break;
-      case ACT_TANH: epi_slab<ACT_TANH, WN>(g, slab, mr0, nc0, z, vec_out, vec_res, bb, res); break;
-      default: epi_slab<ACT_NONE, WN>(g, slab, mr0, nc0, z, vec_out, vec_res, bb, res); break;
+      case ACT_GELU_ERF: epi_slab<ACT_GELU_ERF, WN>(g, slab, mr0, nc0, cz, vec_out, vec_res, bb, res); break;
+      case ACT_GELU_TANH: epi_slab<ACT_GELU_TANH, WN>(g, slab, mr0, nc0, cz, vec_out, vec_res, bb, res); break;
+      case ACT_RELU: epi_slab<ACT_RELU, WN>(g, slab, mr0, nc0, cz, vec_out, vec_res, bb, res); break;
+      case ACT_TANH: epi_slab<ACT_TANH, WN>(g, slab, mr0, nc0, cz, vec_out, vec_res, bb, res); break;
+      default: epi_slab<ACT_NONE, WN>(g, slab, mr0, nc0, cz, vec_out, vec_res, bb, res); break;
     }
   }
   // every wave has read its slab before the next tile's DMAs refill the LDS (LDS-only wait:

@@ -134,15 +134,34 @@ __device__ __forceinline__ void wait_vm() {
 // __syncthreads() here would drain all DMAs (vmcnt(0)): cdna_hip_programming.md §5
 // "Pipelining across barriers".  Under full-chip streaming a DMA takes ~2-3 us to land, so the
 // ring depth (NS-1 tiles in flight), not the MFMA count, sets the k-loop rate.
+// The ring's prologue: tiles 0 .. NS-2 of [kbeg, kend) into stages 0 .. NS-2.
+template <int BM, int BN, int NS = 2, int WGM = 2, int WGN = 2, int BK_ = 64, typename ASrc,
+          typename BSrc>
+__device__ __forceinline__ void fast_prologue(const ASrc& A, const BSrc& B, int kbeg, int kend,
+                                              char* lds) {
+  using FT = FastTile<BM, BN, WGM, WGN, BK_>;
+  const int nk = (kend - kbeg + BK_ - 1) / BK_;
+#pragma unroll
+  for (int p = 0; p < NS - 1; ++p)
+    if (p < nk)
+      fast_issue_t<BM, BN, WGM, WGN, BK_>(A, B, kbeg + p * BK_, kend, lds + p * FT::STAGE);
+}
+
+// `prologued`: the caller already issued the prologue (fast_prologue), possibly followed by
+// other vector-memory operations of this wave — at least XS of them when `xs` is set (a
+// persistent tile loop issues the next tile's prologue before the current tile's epilogue
+// stores).  vmcnt counts loads, stores and LDS-DMA together in issue order
+// (MI355X_MICROARCH.md), so the waits for the prologue stages may leave those XS younger
+// operations in flight: the stores then drain under the next tile's first k-steps.
 template <int BM, int BN, int NS = 2, int WGM = 2, int WGN = 2, int BK_ = 64, bool SSQ = false,
-          typename ASrc, typename BSrc>
+          int XS = 0, typename ASrc, typename BSrc>
 __device__ __forceinline__ void fast_mainloop(
     const ASrc& A, const BSrc& B, int kbeg, int kend, char* lds,
     f32x16_t (&acc)[FastTile<BM, BN, WGM, WGN, BK_>::TM][FastTile<BM, BN, WGM, WGN, BK_>::TN],
-    int dbg = 0, float* ssq = nullptr) {
+    int dbg = 0, float* ssq = nullptr, bool prologued = false, bool xs = false) {
   using FT = FastTile<BM, BN, WGM, WGN, BK_>;
   constexpr int IPW = FT::NI / FT::NW;            // DMA instructions per wave per tile
-  static_assert(NS >= 2 && (NS - 2) * IPW < 64, "stages");
+  static_assert(NS >= 2 && (NS - 2) * IPW + XS < 64, "stages");
 #pragma unroll
   for (int i = 0; i < FT::TM; ++i)
 #pragma unroll
@@ -151,14 +170,15 @@ __device__ __forceinline__ void fast_mainloop(
       for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
   const int nk = (kend - kbeg + BK_ - 1) / BK_;
   if (nk <= 0) return;
-#pragma unroll
-  for (int p = 0; p < NS - 1; ++p)
-    if (p < nk)
-      fast_issue_t<BM, BN, WGM, WGN, BK_>(A, B, kbeg + p * BK_, kend, lds + p * FT::STAGE);
+  if (!prologued) fast_prologue<BM, BN, NS, WGM, WGN, BK_>(A, B, kbeg, kend, lds);
   int st = 0;                                     // stage of tile kt
   for (int kt = 0; kt < nk; ++kt) {
-    if (kt + NS - 2 < nk) wait_vm<(NS - 2) * IPW>();   // tiles kt+1..kt+NS-2 may stay in flight
-    else wait_vm<0>();
+    const bool young = XS > 0 && xs && kt < NS - 1;   // XS younger ops behind this stage
+    if (kt + NS - 2 < nk) {                       // tiles kt+1..kt+NS-2 may stay in flight
+      if (young) wait_vm<(NS - 2) * IPW + XS>(); else wait_vm<(NS - 2) * IPW>();
+    } else {
+      if (young) wait_vm<XS>(); else wait_vm<0>();
+    }
     __builtin_amdgcn_s_barrier();
     const int tn = kt + NS - 1;
     if (tn < nk && dbg != 2 && dbg != 3) {
