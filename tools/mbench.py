@@ -216,31 +216,36 @@ def bench_window():
 
 
 def bench_decode_gemm():
-    """Decode-step GEMMs at 2048 rows with cold weights (rotating > 256 MiB of W copies), per tile."""
+    """Decode-step GEMMs at 2048 rows with cold weights (rotating > 256 MiB of W copies), per tile,
+    with the decoder's epilogues (proj/mproj: f32 out + residual; fc: GELU), and split-K."""
     from zsaac import ops
     from zsaac._lib import call
     dev = torch.device("cuda", 0)
     M = int(os.environ.get("ZS_M", "2048"))
+    ws = torch.empty(8 * M * 3072, device=dev)
     for N, K, name in ((2304, 768, "qkv"), (768, 768, "proj"), (3072, 768, "fc"), (768, 3072, "mproj")):
         a = torch.randn(M, K, device=dev).bfloat16()
         w0 = (torch.randn(N, K, device=dev) * 0.02).bfloat16()
-        ws = [w0] + [w0.clone() for _ in range(max(1, (640 << 20) // w0.nbytes))]
+        wsl = [w0] + [w0.clone() for _ in range(max(1, (640 << 20) // w0.nbytes))]
         b = torch.randn(N, device=dev)
-        out = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+        f32 = name in ("proj", "mproj")
+        out = torch.empty(M, N, device=dev, dtype=torch.float32 if f32 else torch.bfloat16)
+        res = torch.randn(M, N, device=dev) if f32 else None
+        act = ops.ACT_GELU_TANH if name == "fc" else ops.ACT_NONE
         it = [0]
 
-        def run():
-            ops.gemm(a, ws[it[0] % len(ws)], out, bias=b, split_k=1)
+        def run(sk=1):
+            ops.gemm(a, wsl[it[0] % len(wsl)], out, bias=b, residual=res, act=act, split_k=sk,
+                     workspace=ws if sk > 1 else None)
             it[0] += 1
-        res = {}
-        for t, nm in ((0, "auto"), (4, "128x128"), (11, "128/32s2"), (12, "128/32s3"), (5, "128/32s4"),
-                      (8, "128x64"), (9, "64x128"), (13, "64x64s2")):
+        r = {}
+        for t, nm in ((0, "auto"), (4, "128x128"), (10, "128x128s3"), (14, "128x128s4"), (8, "128x64"),
+                      (9, "64x128"), (13, "64x64s2")):
             call("zs_tune_set", b"fast_tile", t)
-            res[nm] = timeit(run, reps=len(ws))
+            r[nm] = timeit(run, reps=len(wsl))
         call("zs_tune_set", b"fast_tile", 0)
-        res["torch"] = timeit(lambda: torch.nn.functional.linear(a, ws[it.__setitem__(0, it[0] + 1) or it[0] % len(ws)], b.bfloat16()), reps=len(ws))
         fl = 2 * M * N * K
-        print(f"M{M} {name:6s} " + "  ".join(f"{k}={v:6.1f}us({fl / v / 1e6:4.0f})" for k, v in res.items()), flush=True)
+        print(f"M{M} {name:6s} " + "  ".join(f"{k}={v:5.1f}({fl / v / 1e6:4.0f})" for k, v in r.items()), flush=True)
 
 
 def bench_attn():

@@ -104,4 +104,15 @@ __device__ __forceinline__ float act_apply(float x, int act) {
   }
 }
 
+// bf16-output epilogues: the same activations in cheaper forms whose error (a few f32 ulp) is far
+// below bf16 rounding.  gelu_new = x * sigmoid(2u) exactly (0.5 * (1 + tanh u) = sigmoid(2u)),
+// one v_exp_f32 + one reciprocal instead of tanhf; the f32 parity path keeps act_apply.
+__device__ __forceinline__ float act_apply_fast(float x, int act) {
+  if (act == ACT_GELU_TANH) {
+    const float u2 = -1.5957691216057308f * (x + 0.044715f * x * x * x);   // -2*sqrt(2/pi)*(...)
+    return x * __frcp_rn(1.0f + __expf(u2));
+  }
+  return act_apply(x, act);
+}
+
 }  // namespace zs

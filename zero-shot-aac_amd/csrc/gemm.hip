@@ -107,7 +107,7 @@ __device__ __forceinline__ void epi_slab(const GemmArgs& g, const float* slab, i
       continue;
     }
 #pragma unroll
-    for (int q = 0; q < 8; ++q) v[q] = act_apply(v[q] + bb[q], ACT);
+    for (int q = 0; q < 8; ++q) v[q] = act_apply_fast(v[q] + bb[q], ACT);
     if (g.residual) {
       if (full && vec_res) {
         const float4 r0 = res[it][0], r1 = res[it][1];
@@ -183,8 +183,12 @@ __global__ __launch_bounds__(64 * WGM * WGN,
   // walks groups of gm M-tiles column by column, so a range is a compact gm x (range/gm) patch
   // of the output: its A rows and W rows stay in that XCD's L2 instead of every XCD streaming
   // all of A and W.
+  // gm: the patch an XCD works on AT ONCE (its gridDim/8 resident blocks take consecutive u)
+  // is about square, so its A rows + W rows fit the XCD's 4 MB L2 (a gm sized for the whole
+  // per-XCD range made 39 x 2 patches on 65536 x 3072: 7.5 MB of A rows, 43 % L2 misses)
   const int q8 = ntiles >> 3, r8 = ntiles & 7;
-  int gm = (int)(sqrtf((float)max(1, q8) * BN / BM) + 0.5f);
+  const int conc = max(1, min(q8, (int)(gridDim.x >> 3)));
+  int gm = (int)(sqrtf((float)conc * BN / BM) + 0.5f);
   gm = max(1, min(gm, ntm));
   auto tile = [&](int t, int& m0, int& n0, int& z) {
     if (g.xcd) {
@@ -326,6 +330,7 @@ static int dispatch_fast(GemmArgs& g, hipStream_t st) {
     case 11: return launch_fast<128, 128, 2, 2, 2, 32>(g, st);
     case 12: return launch_fast<128, 128, 3, 2, 2, 32>(g, st);
     case 13: return launch_fast<64, 64, 2>(g, st);
+    case 14: return launch_fast<128, 128, 4>(g, st);
     default: break;
   }
   if (nblocks(g, 128, 128) >= 256) {
