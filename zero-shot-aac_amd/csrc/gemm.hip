@@ -366,7 +366,7 @@ constexpr int LM_BN = 128;
 constexpr int MAXK = 8;
 
 template <typename T, int BM, int KMAX>
-__global__ __launch_bounds__(256) void lmhead_kernel(int M, int K, int V, const T* A, int lda,
+__global__ __launch_bounds__(256) void lmhead_kernel(int xcd_order, int M, int K, int V, const T* A, int lda,
                                                      const T* W, int topk, int row_norm,
                                                      float* part_stat, float* part_val,
                                                      int* part_idx) {
@@ -380,8 +380,23 @@ __global__ __launch_bounds__(256) void lmhead_kernel(int M, int K, int V, const 
   // ONE __shared__ array (a second object can de-pipeline the DMA loop: §5 item 4(a))
   __shared__ __attribute__((aligned(16))) char smem_raw[SM + BM * 4];
   float* inv_norm = reinterpret_cast<float*>(smem_raw + SM);
-  const int n0 = blockIdx.x * LM_BN, m0 = blockIdx.y * BM;
-  const int nblk = gridDim.x;
+  // 1-D grid of nblk x ntm blocks.  XCD-local order: workgroup b runs on XCD b % 8; the remap
+  // gives each XCD a contiguous range of u, and u walks the row tiles fastest, so every row tile
+  // of a vocab block runs on the same XCD at about the same time: each 128-token W slice is
+  // fetched into one L2 once and reused by all row tiles (with the vocab block fastest, the
+  // 77 MB of W streamed once per row tile).
+  const int ntm = cdiv(M, BM), nblk = cdiv(V, LM_BN), nwg = nblk * ntm;
+  int vb, mb;
+  if (xcd_order) {
+    const int b = blockIdx.x, x = b & 7, q8 = nwg >> 3, r8 = nwg & 7;
+    const int u = (x < r8 ? x * (q8 + 1) : r8 * (q8 + 1) + (x - r8) * q8) + (b >> 3);
+    vb = u / ntm;
+    mb = u - vb * ntm;
+  } else {
+    vb = blockIdx.x % nblk;
+    mb = blockIdx.x / nblk;
+  }
+  const int n0 = vb * LM_BN, m0 = mb * BM;
   f32x16_t acc[TM][TN];
   // bf16: transposed product, vocab on the MFMA row axis, so a token's 128 logits of this block
   // sit in registers of one lane pair (see the epilogue below)
@@ -510,7 +525,7 @@ __global__ __launch_bounds__(256) void lmhead_kernel(int M, int K, int V, const 
       const float g = fmaxf(m0v, m1v);
       const float se = (m0v == -INFINITY ? 0.f : xs[r] * expf(m0v - g)) +
                        (m1v == -INFINITY ? 0.f : xs[BM + r] * expf(m1v - g));
-      const long o = (long)m * nblk + blockIdx.x;
+      const long o = (long)m * nblk + vb;
       part_stat[o * 2 + 0] = g;
       part_stat[o * 2 + 1] = se;
       const float* l0v = xv + r * KMAX;
@@ -597,7 +612,7 @@ __global__ __launch_bounds__(256) void lmhead_kernel(int M, int K, int V, const 
   for (int q = 0; q < KMAX; ++q) { mv[threadIdx.x * MAXK + q] = tv[q]; mi[threadIdx.x * MAXK + q] = ti[q]; }
   __syncthreads();
   if (sub == 0 && m < M) {
-    const long o = ((long)m * nblk + blockIdx.x);
+    const long o = ((long)m * nblk + vb);
     part_stat[o * 2 + 0] = gmx;
     part_stat[o * 2 + 1] = se;
     int ptr[TPR];
@@ -681,8 +696,8 @@ extern "C" int zs_lmhead_topk(int M, int K, int V, int dtype, const void* A, int
   hipStream_t st = S(stream);
   const int nblk = cdiv(V, LM_BN);
 #define LMH(T, BM_, KM_)                                                                     \
-  hipLaunchKernelGGL((lmhead_kernel<T, BM_, KM_>), dim3(nblk, cdiv(M, BM_)), dim3(256), 0, st, \
-                     M, K, V, (const T*)A, lda, (const T*)W, topk, row_norm, part_stat,       \
+  hipLaunchKernelGGL((lmhead_kernel<T, BM_, KM_>), dim3(nblk * cdiv(M, BM_)), dim3(256), 0, st, \
+                     g_fast_xcd, M, K, V, (const T*)A, lda, (const T*)W, topk, row_norm, part_stat,       \
                      part_val, part_idx)
 #define LMH_K(T, BM_) do { if (topk == 1) LMH(T, BM_, 1); else LMH(T, BM_, 8); } while (0)
   if (M <= 64) {
