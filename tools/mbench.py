@@ -106,7 +106,7 @@ def bench_gemm_htsat():
             b = torch.randn(N, device=dev)
             out = torch.empty(Mr, N, device=dev, dtype=torch.bfloat16)
             res = {}
-            for t, nm in ((0, "auto"), (4, "128x128"), (8, "128x64"), (11, "128/32s2"), (12, "128/32s3"), (5, "128/32x4"), (13, "64x64s2")):
+            for t, nm in ((0, "auto"), (4, "128x128"), (15, "256x128w8"), (16, "128x256w8")):
                 call("zs_tune_set", b"fast_tile", t)
                 res[nm] = timeit(lambda: ops.gemm(a, w, out, bias=b, split_k=1), reps=20)
             call("zs_tune_set", b"fast_tile", 0)
@@ -133,10 +133,10 @@ def bench_gemm_dbg():
         w = (torch.randn(N, K, device=dev) * 0.02).bfloat16()
         out = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
         res = {}
-        for t, nm, pers in ((4, "128x128P", 1),):
+        for t, nm, pers in ((4, "128x128P", 1), (15, "256x128w8", 1), (16, "128x256w8", 1)):
             call("zs_tune_set", b"fast_tile", t)
             call("zs_tune_set", b"fast_persist", pers)
-            for d, dn in ((0, "full"), (1, "noMFMA"), (2, "noDMA"), (3, "noLoop"), (4, "noEpi")):
+            for d, dn in ((0, "full"), (3, "noLoop"), (4, "noEpi")):
                 call("zs_tune_set", b"gemm_dbg", d)
                 res[f"{nm}/{dn}"] = timeit(lambda: ops.gemm(a, w, out, split_k=1), reps=20)
         call("zs_tune_set", b"gemm_dbg", 0)
@@ -239,8 +239,8 @@ def bench_decode_gemm():
                      workspace=ws if sk > 1 else None)
             it[0] += 1
         r = {}
-        for t, nm in ((0, "auto"), (4, "128x128"), (10, "128x128s3"), (14, "128x128s4"), (8, "128x64"),
-                      (9, "64x128"), (13, "64x64s2")):
+        for t, nm in ((0, "auto"), (4, "128x128"), (15, "256x128w8"), (16, "128x256w8"), (8, "128x64"),
+                      (9, "64x128")):
             call("zs_tune_set", b"fast_tile", t)
             r[nm] = timeit(run, reps=len(wsl))
         call("zs_tune_set", b"fast_tile", 0)
@@ -249,23 +249,31 @@ def bench_decode_gemm():
 
 
 def bench_attn():
+    """Decode attention at the bench's decode shape (2048 rows x 12 heads, Lmax 102): attn6 /
+    attn5 / LDS-staged, HBM GB/s of the K/V bytes read."""
     from zsaac import ops
+    from zsaac._lib import call
     dev = torch.device("cuda", 0)
-    R, D, H = 64, 768, 12
-    for L, Lmax in ((30, 96), (60, 96), (90, 96)):
-        qkv = torch.randn(R, 3 * D, device=dev).bfloat16()
-        kc = torch.randn(R, H, Lmax, 64, device=dev).bfloat16()
-        vc = torch.randn_like(kc)
+    R, D, H, Lmax = 2048, 768, 12, 102
+    kc = torch.randn(R, H, Lmax, 64, device=dev).bfloat16()
+    vc = torch.randn_like(kc)
+    qkv = torch.randn(R, 3 * D, device=dev).bfloat16()
+    out = torch.empty(R, D, device=dev, dtype=torch.bfloat16)
+    for L in (32, 64, 96):
         pos = torch.full((R,), L - 1, device=dev, dtype=torch.int32)
-        out = torch.empty(R, D, device=dev, dtype=torch.bfloat16)
-        t = timeit(lambda: ops.decode_attention(qkv, R, D, H, kc, vc, Lmax, pos, out))
-        byts = R * L * D * 2 * 2
-        print(f"decode_attn L={L}: {t:7.2f}us  KV {byts / 1e6:.1f}MB  {byts / t / 1e3:6.0f} GB/s")
-    x = torch.randn(64, 768, device=dev)
+        byts = R * H * L * 64 * 2 * 2
+        r = {}
+        for v in (2, 1, 0):
+            call("zs_tune_set", b"decode_attn5", v)
+            r[v] = timeit(lambda: ops.decode_attention(qkv, R, D, H, kc, vc, Lmax, pos, out), reps=20)
+        call("zs_tune_set", b"decode_attn5", 2)
+        print(f"decode_attn R={R} L={L}: " + "  ".join(
+            f"v{v}={t:7.2f}us ({byts / t / 1e3:5.0f} GB/s)" for v, t in r.items()), flush=True)
+    x = torch.randn(R, 768, device=dev)
     w, bb = torch.randn(768, device=dev), torch.randn(768, device=dev)
-    y = torch.empty(64, 768, device=dev, dtype=torch.bfloat16)
-    print(f"layernorm 64x768: {timeit(lambda: ops.layernorm(x, w, bb, out=y)):7.2f}us")
-    print(f"empty-ish (cast 64 elems): {timeit(lambda: ops.cast(x[:1, :64], y[:1, :64])):7.2f}us")
+    y = torch.empty(R, 768, device=dev, dtype=torch.bfloat16)
+    t = timeit(lambda: ops.layernorm(x, w, bb, out=y))
+    print(f"layernorm {R}x768: {t:7.2f}us ({R * 768 * 6 / t / 1e3:5.0f} GB/s)")
 
 
 def bench_inflight():

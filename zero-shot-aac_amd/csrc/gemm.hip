@@ -229,6 +229,32 @@ __global__ __launch_bounds__(64 * WGM * WGN,
   fast_mainloop<BM, BN, NS, WGM, WGN, BK_, false, XS>(A, B, kbeg, kend, lds, acc, g.dbg, nullptr,
                                                       pre, xs);   // ends with a barrier
   const int cm0 = m0, cn0 = n0, cz = z;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int wr0 = (wid / WGN) * FT::WM, wc0 = (wid % WGN) * WN;
+  // 16-byte stores need 8-element (bf16) / 4-element (f32) aligned rows and bias
+  const bool vec_out = (g.split_k > 1) ||
+                       (g.ldo % 8 == 0 && ((uintptr_t)g.out & 15) == 0);
+  const bool vec_res = g.residual == nullptr ||
+                       (g.ldr % 4 == 0 && ((uintptr_t)g.residual & 15) == 0);
+  // The bias and the first slab's residual rows are loaded BEFORE the next tile's prologue
+  // DMAs: vmcnt retires in issue order, so a load issued after those DMAs could only be
+  // consumed once the DMAs had landed (a full DMA latency per tile).  The lane's 8 bias columns
+  // are the same in every slab of the tile (64 % (WN/8) == 0).
+  float bb[8];
+  {
+    const int n = cn0 + wc0 + (lane % (WN / 8)) * 8, nv = min(8, g.N - n);
+    if (g.bias && nv == 8 && ((uintptr_t)(g.bias + n) & 15) == 0) {
+      const float4 b0 = reinterpret_cast<const float4*>(g.bias + n)[0];
+      const float4 b1 = reinterpret_cast<const float4*>(g.bias + n)[1];
+      bb[0] = b0.x; bb[1] = b0.y; bb[2] = b0.z; bb[3] = b0.w;
+      bb[4] = b1.x; bb[5] = b1.y; bb[6] = b1.z; bb[7] = b1.w;
+    } else {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) bb[q] = (g.bias && q < nv) ? g.bias[n + q] : 0.f;
+    }
+  }
+  float4 res0[WN / 16][2];
+  epi_res_load<WN>(g, cm0 + wr0, cn0 + wc0, vec_res, res0);
   pre = xs = false;
   if (XPF && t + (int)gridDim.x < ntiles && g.dbg != 2 && g.dbg != 3) {
     tile(t + gridDim.x, m0, n0, z);
@@ -241,8 +267,6 @@ __global__ __launch_bounds__(64 * WGM * WGN,
   } else if (t + (int)gridDim.x < ntiles) {
     tile(t + gridDim.x, m0, n0, z);
   }
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int wr0 = (wid / WGN) * FT::WM, wc0 = (wid % WGN) * WN;
   float* slab = reinterpret_cast<float*>(lds + (XPF ? (NS - 1) * FT::STAGE : 0)) + wid * 32 * WN;
   if (g.dbg == 4) {   // experiment: no epilogue (keep the accumulators alive)
     float t = 0.f;
@@ -253,23 +277,16 @@ __global__ __launch_bounds__(64 * WGM * WGN,
     if (t == 12345.f) reinterpret_cast<float*>(g.out)[0] = t;
     continue;
   }
-  // 16-byte stores need 8-element (bf16) / 4-element (f32) aligned rows and bias
-  const bool vec_out = (g.split_k > 1) ||
-                       (g.ldo % 8 == 0 && ((uintptr_t)g.out & 15) == 0);
-  const bool vec_res = g.residual == nullptr ||
-                       (g.ldr % 4 == 0 && ((uintptr_t)g.residual & 15) == 0);
-  // the lane's 8 bias columns are the same in every slab of the tile (64 % (WN/8) == 0)
-  float bb[8];
-  {
-    const int n = cn0 + wc0 + (lane % (WN / 8)) * 8, nv = min(8, g.N - n);
-#pragma unroll
-    for (int q = 0; q < 8; ++q) bb[q] = (g.bias && q < nv) ? g.bias[n + q] : 0.f;
-  }
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
     const int mr0 = cm0 + wr0 + i * 32, nc0 = cn0 + wc0;
     float4 res[WN / 16][2];
-    epi_res_load<WN>(g, mr0, nc0, vec_res, res);
+    if (i == 0) {
+#pragma unroll
+      for (int q = 0; q < WN / 16; ++q) { res[q][0] = res0[q][0]; res[q][1] = res0[q][1]; }
+    } else {
+      epi_res_load<WN>(g, mr0, nc0, vec_res, res);
+    }
 #pragma unroll
     for (int j = 0; j < TN; ++j)
 #pragma unroll
@@ -331,6 +348,8 @@ static int dispatch_fast(GemmArgs& g, hipStream_t st) {
     case 12: return launch_fast<128, 128, 3, 2, 2, 32>(g, st);
     case 13: return launch_fast<64, 64, 2>(g, st);
     case 14: return launch_fast<128, 128, 4>(g, st);
+    case 15: return launch_fast<256, 128, 2, 4, 2, 64>(g, st);
+    case 16: return launch_fast<128, 256, 2, 2, 4, 64>(g, st);
     default: break;
   }
   if (nblocks(g, 128, 128) >= 256) {
