@@ -179,7 +179,7 @@ def kernel_roofline(pipe):
 
 
 def attention_roofline(pipe, L_mean=None):
-    """decode_attn5_kernel at the bench's decode rows, every row at the mean key count of a
+    """decode attention (decode_attn6_kernel, the default) at the bench's decode rows, every row at the mean key count of a
     67-step greedy decode (prompt Pmax + 34): algorithmic bytes = K and V of every key read once
     + q/k/v of the new token + the output, per (row, head)."""
     from zsaac import ops
@@ -200,7 +200,7 @@ def attention_roofline(pipe, L_mean=None):
     es = qkv.element_size()
     byts = R * H * (2 * L * 64 * es) + R * 3 * D * es + R * D * es
     gbs = byts / avg_s / 1e9
-    return {"kernel": f"decode_attn5_kernel<bf16> R={R} heads=12 keys={L}", "bound": "hbm",
+    return {"kernel": f"decode_attn6_kernel<bf16> R={R} heads=12 keys={L}", "bound": "hbm",
             "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(gbs / HBM_PEAK_GBS, 4), "avg_launch_us": round(avg_s * 1e6, 3),
             "algo_bytes_per_launch": byts}
