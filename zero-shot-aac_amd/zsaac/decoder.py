@@ -142,10 +142,15 @@ class TransformerMapperEngine:
         return hs.view(B, L * D)[:, self.cl * D:]   # clip b's soft prefix at base + b*soft_ld
 
 
-def build_mapper(sd, mapping_type, device, dtype, max_batch):
+def build_mapper(sd, mapping_type, device, dtype, max_batch, clip_length=10, num_layers=8):
+    """ClapCaptionModel's clap_project (models/caption_model.py:55-60): MLP, or TransformerMapper
+    with params.json's prefix_length_clip / num_layers."""
     if mapping_type == "mlp":
         return MlpMapper(sd, device, dtype, max_batch)
-    return TransformerMapperEngine(sd, device, dtype, max_batch)
+    if mapping_type != "transformer":
+        raise ValueError(f"mapping_type {mapping_type!r} (mlp | transformer)")
+    return TransformerMapperEngine(sd, device, dtype, max_batch, clip_length=clip_length,
+                                   num_layers=num_layers)
 
 
 # ------------------------------------------------------------------------------- GPT-2

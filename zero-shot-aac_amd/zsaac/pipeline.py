@@ -38,6 +38,8 @@ class CaptionConfig:
     prefix_tokens: bool = True        # also compute get_prefix_tokens (predict_prompt.py:137)
     use_graph: bool = True
     compact_decode: bool = True       # greedy bf16: decode only the rows that have not stopped
+    clip_length: int = 10             # TransformerMapper clip_length (params.json prefix_length_clip)
+    mapper_layers: int = 8            # TransformerMapper num_layers (params.json num_layers)
     encoder_batch: int = 64           # clips per encoder pass (the reference's eval batch size);
                                       # a larger ``batch`` is encoded in chunks of this size and
                                       # decoded together (clip results do not depend on it)
@@ -89,7 +91,8 @@ class CaptionPipeline:
         B = cfg.batch
         eb = min(B, max(1, cfg.encoder_batch))
         self.encoder = AudioEncoder(audio_sd, cfg.encoder, cfg.dtype, eb, dev) if audio_sd else None
-        self.mapper = build_mapper(caption_sd, cfg.mapping_type, dev, cfg.dtype, B)
+        self.mapper = build_mapper(caption_sd, cfg.mapping_type, dev, cfg.dtype, B,
+                                   clip_length=cfg.clip_length, num_layers=cfg.mapper_layers)
         self.gpt = Gpt2Weights(caption_sd, dev, cfg.dtype)
         self._setup_tables(label_table, label_tokens)
         self._alloc()

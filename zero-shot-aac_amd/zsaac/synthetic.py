@@ -242,3 +242,48 @@ def synthetic_clap_embeddings(n: int, seed: int = 4321, dim: int = 1024) -> torc
     g = _gen(seed)
     e = torch.randn(n, dim, generator=g)
     return e / e.norm(dim=-1, keepdim=True)
+
+
+def gpt2_vocab(label_names, n_vocab: int = 50257):
+    """A GPT-2-format BPE vocabulary (vocab dict, merges list) for offline tests of the real-data
+    harness: ids 0..255 are the byte tokens in GPT-2's order (so '.' = 13, ',' = 11 as in GPT-2);
+    the prompt template pieces get their real GPT-2 ids ("There" 1858, " are" 389, " something"
+    1223, " in" 287, " this" 428, " audio" 6597) and " ." is 764; merges build those pieces and a
+    shared " snd" prefix for the synthetic label names; every other id up to n_vocab decodes to a
+    filler string, so any generated id decodes."""
+    from .bpe import bytes_to_unicode
+    b2u = bytes_to_unicode()
+    sp = b2u[ord(" ")]
+    vocab = {b2u[b]: i for i, b in enumerate(b2u)}      # GPT-2's byte order: bytes_to_unicode's
+    merges = []
+    fixed = {"There": 1858, sp + "are": 389, sp + "something": 1223, sp + "in": 287,
+             sp + "this": 428, sp + "audio": 6597, sp + ".": 764}
+    nxt = [256]
+
+    def new_id():
+        while nxt[0] in fixed.values():
+            nxt[0] += 1
+        nxt[0] += 1
+        return nxt[0] - 1
+
+    def chain(word):
+        cur = word[0]
+        for ch in word[1:]:
+            merged = cur + ch
+            if (cur, ch) not in merges:
+                merges.append((cur, ch))
+            if merged not in vocab:
+                vocab[merged] = fixed.get(merged, new_id())
+            cur = merged
+    for w in fixed:
+        chain(w)
+    prefixes = sorted({sp + n.lower()[:3] for n in label_names})
+    for p in prefixes:
+        chain(p)
+    used = set(vocab.values())
+    k = 0
+    for i in range(n_vocab):
+        if i not in used:
+            vocab[f"<{k}>"] = i
+            k += 1
+    return vocab, merges
