@@ -187,6 +187,20 @@ def bench_front():
     lw, lb = torch.randn(96, device=dev), torch.randn(96, device=dev)
     x = torch.empty(B * 4096, 96, device=dev)
     print(f"patch_embed B64: {timeit(lambda: ops.patch_embed(img, w, b, lw, lb, out=x), reps=10):8.1f}us", flush=True)
+    for H, C in ((64, 96), (32, 192), (16, 384)):
+        xm = torch.randn(B * H * H, C, device=dev)
+        yw, yb = torch.randn(4 * C, device=dev), torch.randn(4 * C, device=dev)
+        ym = torch.empty(B * H * H // 4, 4 * C, device=dev, dtype=torch.bfloat16)
+        t = timeit(lambda: ops.patch_merge_ln(xm, B, H, H, C, yw, yb, ym), reps=10)
+        byts = xm.numel() * 4 + ym.numel() * 2
+        print(f"patch_merge_ln H{H} C{C}: {t:8.1f}us ({byts / t / 1e3:5.0f} GB/s)", flush=True)
+    for C in (96, 192, 384, 768):
+        M = B * 4096 * 96 // C
+        xl = torch.randn(M, C, device=dev)
+        ylo = torch.empty(M, C, device=dev, dtype=torch.bfloat16)
+        wl, bl = torch.randn(C, device=dev), torch.randn(C, device=dev)
+        t = timeit(lambda: ops.layernorm(xl, wl, bl, out=ylo), reps=10)
+        print(f"layernorm M{M} C{C}: {t:8.1f}us ({M * C * 6 / t / 1e3:5.0f} GB/s)", flush=True)
     xs = torch.randn(B * 64, 768, device=dev)
     lw2, lb2 = torch.randn(768, device=dev), torch.randn(768, device=dev)
     feat = torch.empty(B, 768, device=dev)

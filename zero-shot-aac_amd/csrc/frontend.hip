@@ -38,7 +38,6 @@ __global__ __launch_bounds__(256) void logmel_kernel(
   __shared__ float mw[2 * NBIN];          // the mel filters' nonzero bands, packed
   __shared__ float pw[2 * NP][NBIN];
   __shared__ int moff[NMEL + 1], mlo[NMEL];
-  const int g0 = 2 * NP * blockIdx.x;     // flattened (clip, frame) index of the first frame
   for (int n = threadIdx.x; n < NFFT; n += 256) tw[n] = twiddle[n];
   if (threadIdx.x < 64) {                 // band offsets: wave-wide inclusive scan of the widths
     const int m = threadIdx.x;
@@ -53,6 +52,14 @@ __global__ __launch_bounds__(256) void logmel_kernel(
     moff[m + 1] = inc;
     if (m == 0) moff[0] = 0;
   }
+  __syncthreads();
+  {   // pack the bands: 4 threads per mel filter
+    const int m = threadIdx.x >> 2, s0 = threadIdx.x & 3;
+    const int lo = mlo[m], len = moff[m + 1] - moff[m];
+    for (int k = s0; k < len; k += 4) mw[moff[m] + k] = melW[m * NBIN + lo + k];
+  }
+  // persistent over frame groups: the twiddles and the packed mel bands are staged once per block
+  for (int g0 = 2 * NP * blockIdx.x; g0 < total_frames; g0 += 2 * NP * gridDim.x) {
   // natural-order load (coalesced global reads, conflict-free LDS writes)
   for (int n = threadIdx.x; n < NP * NFFT; n += 256) {
     const int p = n / NFFT, k = n % NFFT;
@@ -73,11 +80,6 @@ __global__ __launch_bounds__(256) void logmel_kernel(
     im[p][lp(k)] = v[1];
   }
   __syncthreads();
-  {   // pack the bands: 4 threads per mel filter
-    const int m = threadIdx.x >> 2, s0 = threadIdx.x & 3;
-    const int lo = mlo[m], len = moff[m + 1] - moff[m];
-    for (int k = s0; k < len; k += 4) mw[moff[m] + k] = melW[m * NBIN + lo + k];
-  }
   // radix-4 DIF (natural-order in, base-4 digit-reversed out):
   // y0 = x0+x1+x2+x3, y1 = (x0-x2) - i(x1-x3), y2 = (x0+x2) - (x1+x3), y3 = (x0-x2) + i(x1-x3),
   // then y_p *= W_{4L}^{p j} = W_1024^{p j S}
@@ -140,6 +142,8 @@ __global__ __launch_bounds__(256) void logmel_kernel(
     if (bn_mean) v = (v - bn_mean[m]) / sqrtf(bn_var[m] + 1e-5f) * bn_w[m] + bn_b[m];
     out[(long)g * NMEL + m] = v;
   }
+  __syncthreads();   // re/im/pw are refilled by the next group
+  }
 }
 
 // bicubic (A = -0.75, align_corners = True) along time T_in -> 1024, identity along the 64 mels,
@@ -168,27 +172,34 @@ __global__ void wav2img_kernel(const float* __restrict__ in, int T_in, float* __
   img[e] = v;
 }
 
-// PatchEmbed: one thread per token (a 4x4 patch -> 96 channels in registers, LayerNorm in-thread);
-// 256 threads = 4 rows of the 64x64 patch grid, weights / bias / LN params broadcast from LDS.
-// A lane's 16 pixels are four 16-byte loads, contiguous across the wave.
+// PatchEmbed: 4 lanes per token (a 4x4 patch -> 96 channels, 24 per lane, LayerNorm reduced over
+// the lane quad); 256 threads = 64 tokens = one row of the 64x64 patch grid, weights / bias / LN
+// params broadcast from LDS.  Lane g of a quad owns channels 16i + 4g .. 16i + 4g + 3 (i < 6), so
+// each 16-byte store instruction writes 64 contiguous bytes per token.  (One thread per token held
+// 96 values, ran at one wave per SIMD and stored 64 scattered lines per instruction.)
 __global__ __launch_bounds__(256) void patch_embed_kernel(const float* __restrict__ img,
                                                           const float* __restrict__ w,
                                                           const float* __restrict__ bias,
                                                           const float* __restrict__ lnw,
                                                           const float* __restrict__ lnb,
                                                           float* __restrict__ x, long ntok) {
-  constexpr int C = 96;
-  __shared__ float sw[C * 16], sb[C], sg[C], sbeta[C];
-  for (int i = threadIdx.x; i < C * 16; i += 256) sw[i] = w[i];
+  constexpr int C = 96, CPL = C / 4, WS = 20;   // weight row stride: 16 + 4 pad (16-B aligned)
+  // 20-float rows: the quad's 4 lanes read channels 4 apart, whose rows then start 16 banks apart
+  // (a 16-float stride put all four on the same banks: 4-way conflicts on every weight read)
+  __shared__ __attribute__((aligned(16))) float sw[C * WS];
+  __shared__ float sb[C], sg[C], sbeta[C];
+  for (int i = threadIdx.x; i < C * 16; i += 256) sw[(i / 16) * WS + (i % 16)] = w[i];
   if (threadIdx.x < C) {
     sb[threadIdx.x] = bias[threadIdx.x];
     sg[threadIdx.x] = lnw[threadIdx.x];
     sbeta[threadIdx.x] = lnb[threadIdx.x];
   }
   __syncthreads();
-  const long tok = (long)blockIdx.x * 256 + threadIdx.x;
-  if (tok >= ntok) return;
-  const int b = tok / 4096, t = tok % 4096, ph = t / 64, pwc = t % 64;
+  const long tok = (long)blockIdx.x * 64 + (threadIdx.x >> 2);
+  const int g = threadIdx.x & 3;
+  const bool valid = tok < ntok;          // whole quads (ntok is a multiple of 4096)
+  const long tk = valid ? tok : 0;
+  const int b = (int)(tk / 4096), t = (int)(tk % 4096), ph = t / 64, pwc = t % 64;
   const float* base = img + (long)b * 65536 + (ph * 4) * 256 + pwc * 4;
   float px[16];
 #pragma unroll
@@ -196,28 +207,44 @@ __global__ __launch_bounds__(256) void patch_embed_kernel(const float* __restric
     const float4 r = *reinterpret_cast<const float4*>(base + ky * 256);
     px[ky * 4 + 0] = r.x; px[ky * 4 + 1] = r.y; px[ky * 4 + 2] = r.z; px[ky * 4 + 3] = r.w;
   }
-  float v[C];
+  float v[CPL];
   float sum = 0.f;
 #pragma unroll
-  for (int c = 0; c < C; ++c) {
-    float a = sb[c];
+  for (int i = 0; i < CPL / 4; ++i)
 #pragma unroll
-    for (int q = 0; q < 16; ++q) a += sw[c * 16 + q] * px[q];
-    v[c] = a;
-    sum += a;
-  }
+    for (int j = 0; j < 4; ++j) {
+      const int c = 16 * i + 4 * g + j;
+      float a = sb[c];
+#pragma unroll
+      for (int q4 = 0; q4 < 4; ++q4) {
+        const float4 wq = *reinterpret_cast<const float4*>(sw + c * WS + 4 * q4);
+        a += wq.x * px[4 * q4];
+        a += wq.y * px[4 * q4 + 1];
+        a += wq.z * px[4 * q4 + 2];
+        a += wq.w * px[4 * q4 + 3];
+      }
+      v[4 * i + j] = a;
+      sum += a;
+    }
+  sum += __shfl_xor(sum, 1, 64);
+  sum += __shfl_xor(sum, 2, 64);
   const float mean = sum / C;
   float var = 0.f;
 #pragma unroll
-  for (int c = 0; c < C; ++c) { const float d = v[c] - mean; var += d * d; }
+  for (int k = 0; k < CPL; ++k) { const float d = v[k] - mean; var += d * d; }
+  var += __shfl_xor(var, 1, 64);
+  var += __shfl_xor(var, 2, 64);
   const float rstd = rsqrtf(var / C + 1e-5f);
-  float4* xr = reinterpret_cast<float4*>(x + tok * C);
+  if (!valid) return;
 #pragma unroll
-  for (int c = 0; c < C; c += 4)
-    xr[c / 4] = make_float4((v[c] - mean) * rstd * sg[c] + sbeta[c],
-                            (v[c + 1] - mean) * rstd * sg[c + 1] + sbeta[c + 1],
-                            (v[c + 2] - mean) * rstd * sg[c + 2] + sbeta[c + 2],
-                            (v[c + 3] - mean) * rstd * sg[c + 3] + sbeta[c + 3]);
+  for (int i = 0; i < CPL / 4; ++i) {
+    const int c = 16 * i + 4 * g;
+    *reinterpret_cast<float4*>(x + tok * C + c) =
+        make_float4((v[4 * i] - mean) * rstd * sg[c] + sbeta[c],
+                    (v[4 * i + 1] - mean) * rstd * sg[c + 1] + sbeta[c + 1],
+                    (v[4 * i + 2] - mean) * rstd * sg[c + 2] + sbeta[c + 2],
+                    (v[4 * i + 3] - mean) * rstd * sg[c + 3] + sbeta[c + 3]);
+  }
 }
 
 }  // namespace zs
@@ -231,7 +258,8 @@ extern "C" int zs_logmel(const float* wav, int B, int T, const float* window, co
   ZS_REQUIRE(B > 0 && T > NFFT / 2, "zs_logmel: need T > 512 samples for reflect padding");
   const int n_frames = T / HOP + 1;
   const int total = B * n_frames;
-  hipLaunchKernelGGL(logmel_kernel, dim3(cdiv(total, 2 * LM_PAIRS)), dim3(256), 0, S(stream), wav, T,
+  const int groups = cdiv(total, 2 * LM_PAIRS);
+  hipLaunchKernelGGL(logmel_kernel, dim3(std::min(groups, 256 * 8)), dim3(256), 0, S(stream), wav, T,
                      n_frames, total, window, twiddle, melW, mel_lo, mel_hi, bn_mean, bn_var,
                      bn_weight, bn_bias, out);
   ZS_LAUNCH_CHECK();
@@ -250,7 +278,7 @@ extern "C" int zs_patch_embed(const float* img, int B, const float* w, const flo
                               const float* ln_w, const float* ln_b, float* x, void* stream) {
   ZS_REQUIRE(B > 0, "zs_patch_embed: B");
   const long ntok = (long)B * 4096;
-  hipLaunchKernelGGL(patch_embed_kernel, dim3(cdiv(ntok, 256)), dim3(256), 0, S(stream), img, w, b,
+  hipLaunchKernelGGL(patch_embed_kernel, dim3(cdiv(ntok, 64)), dim3(256), 0, S(stream), img, w, b,
                      ln_w, ln_b, x, ntok);
   ZS_LAUNCH_CHECK();
   return 0;

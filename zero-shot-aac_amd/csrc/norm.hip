@@ -106,6 +106,49 @@ __global__ __launch_bounds__(256) void patch_merge_ln_kernel(const float* __rest
   for (int c = threadIdx.x; c < C4; c += 256) stf(yr + c, (src(c) - mean) * rstd * w[c] + b[c]);
 }
 
+// The same, one wave per output token with the 4C-wide row in registers (VPL values per lane):
+// one read of x, wave reductions, no block barriers (the block version above read x three times
+// and synchronised 256 threads twice per token).  Stores move 64 consecutive elements per
+// instruction.
+template <int VPL, typename TO>
+__global__ __launch_bounds__(256) void patch_merge_ln_wave_kernel(const float* __restrict__ x,
+                                                                  int H, int W, int C,
+                                                                  const float* __restrict__ w,
+                                                                  const float* __restrict__ b,
+                                                                  TO* __restrict__ y, long ntok) {
+  const int lane = threadIdx.x & 63;
+  const long tok = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (tok >= ntok) return;
+  const int Ho = H / 2, Wo = W / 2;
+  const int bb = (int)(tok / (Ho * Wo)), ij = (int)(tok % (Ho * Wo)), i = ij / Wo, j = ij % Wo;
+  const int C4 = 4 * C;
+  float v[VPL];
+  float s = 0.f;
+#pragma unroll
+  for (int q = 0; q < VPL; ++q) {
+    const int c = lane + 64 * q;
+    v[q] = 0.f;
+    if (c < C4) {
+      const int part = c / C, cc = c - part * C;
+      const int hh = 2 * i + (part & 1), ww = 2 * j + (part >> 1);
+      v[q] = x[(((long)bb * H + hh) * W + ww) * C + cc];
+      s += v[q];
+    }
+  }
+  const float mean = wave_sum(s) / C4;
+  float var = 0.f;
+#pragma unroll
+  for (int q = 0; q < VPL; ++q)
+    if (lane + 64 * q < C4) { const float d = v[q] - mean; var += d * d; }
+  const float rstd = rsqrtf(wave_sum(var) / C4 + 1e-5f);
+  TO* yr = y + tok * C4;
+#pragma unroll
+  for (int q = 0; q < VPL; ++q) {
+    const int c = lane + 64 * q;
+    if (c < C4) stf(yr + c, (v[q] - mean) * rstd * w[c] + b[c]);
+  }
+}
+
 // final LayerNorm + mean over N tokens (htsat.py:830,838-847): one 1024-thread block per clip,
 // wave w normalises tokens w, w+16, ... with the row held in registers (CPL values per lane);
 // the 16 per-wave partial sums are added in wave order (deterministic).
@@ -211,6 +254,24 @@ extern "C" int zs_layernorm(const float* x, int M, int C, int ldx, const int* ro
 extern "C" int zs_patch_merge_ln(const float* x, int B, int H, int W, int C, const float* ln_w,
                                  const float* ln_b, void* y, int dtype, void* stream) {
   ZS_REQUIRE(B > 0 && H % 2 == 0 && W % 2 == 0 && C > 0, "zs_patch_merge_ln: bad shape");
+  const long ntok = (long)B * (H / 2) * (W / 2);
+  const int C4 = 4 * C;
+  if (C4 <= 64 * 24) {
+    const dim3 grid((unsigned)cdiv(ntok, 4));
+#define PMW(VPL_)                                                                               \
+    do {                                                                                        \
+      if (dtype == ZS_BF16)                                                                     \
+        hipLaunchKernelGGL((patch_merge_ln_wave_kernel<VPL_, bf16_t>), grid, dim3(256), 0,       \
+                           S(stream), x, H, W, C, ln_w, ln_b, (bf16_t*)y, ntok);                \
+      else                                                                                      \
+        hipLaunchKernelGGL((patch_merge_ln_wave_kernel<VPL_, float>), grid, dim3(256), 0,        \
+                           S(stream), x, H, W, C, ln_w, ln_b, (float*)y, ntok);                 \
+    } while (0)
+    if (C4 <= 64 * 6) PMW(6); else if (C4 <= 64 * 12) PMW(12); else PMW(24);
+#undef PMW
+    ZS_LAUNCH_CHECK();
+    return 0;
+  }
   dim3 grid(B * (H / 2) * (W / 2));
   if (dtype == ZS_BF16)
     hipLaunchKernelGGL(patch_merge_ln_kernel<bf16_t>, grid, dim3(256), 0, S(stream), x, H, W, C,
