@@ -211,7 +211,7 @@ def test_decode_attention_matches_prefill(cuda):
 
 
 @pytest.mark.parametrize("use_kvrow", [False, True])
-@pytest.mark.parametrize("variant", [2, 1, 0])
+@pytest.mark.parametrize("variant", [3, 2, 1, 0])
 def test_decode_attention_bf16(cuda, use_kvrow, variant):
     """bf16 decode attention (register-resident decode_attn5, and the LDS-staged decode_attn4)
     vs an fp32 torch reference: ragged positions 0..Lmax-1 per row, optional beam kvrow
@@ -236,7 +236,7 @@ def test_decode_attention_bf16(cuda, use_kvrow, variant):
     try:
         ops.decode_attention(qkv, R, D, H, kc, vc, Lmax, pos, out, kvrow=kvrow)
     finally:
-        call("zs_tune_set", b"decode_attn5", 2)
+        call("zs_tune_set", b"decode_attn5", 3)
     qf = qkv.float()
     for r in range(R):
         p = int(pos[r])

@@ -9,7 +9,7 @@
 
 namespace zs {
 
-int g_decode_attn5 = 2;   // 2: decode_attn6 (phased), 1: decode_attn5, 0: LDS-staged
+int g_decode_attn5 = 3;   // 3/2: decode_attn6 (phases of 32/64 keys), 1: decode_attn5, 0: LDS
 int g_window_mfma = 1;    // zs_tune_set("window_mfma", 0): VALU window attention for bf16   // zs_tune_set("decode_attn5", 0): LDS-staged decode_attn4 for bf16
 
 // ------------------------------------------------------------------ HTSAT window attention
@@ -484,14 +484,13 @@ __global__ __launch_bounds__(256) void decode_attn5_kernel(const T* __restrict__
 // SIMD instead of 2) and any Lmax works.  The per-slot inputs (rowmap, compact position) are
 // loaded together with the qkv row: one dependent round trip before the K/V loads.  With one
 // phase (p < 64) the arithmetic equals decode_attn5's.
-constexpr int DA6_KPP = 64;                  // keys per phase
-template <typename T>
+template <typename T, int KPP = 64>          // KPP: keys per phase (8 per key group)
 __global__ __launch_bounds__(256) void decode_attn6_kernel(
     const T* __restrict__ qkv, int D, int heads, T* __restrict__ kc, T* __restrict__ vc, int Lmax,
     const int* __restrict__ pos, const int* __restrict__ kvrow, T* __restrict__ out,
     const int* __restrict__ rowmap, const int* __restrict__ cpos, int nphys) {
   static_assert(sizeof(T) == 2, "bf16 only");
-  constexpr int HD = 64, EPC = 8, NG = DA6_KPP / 8;
+  constexpr int HD = 64, EPC = 8, NG = KPP / 8;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int c = blockIdx.x, h = blockIdx.y * 4 + wid;
   if (h >= heads) return;
@@ -522,7 +521,7 @@ __global__ __launch_bounds__(256) void decode_attn6_kernel(
   float m = -INFINITY, sum = 0.f, o[EPC];
 #pragma unroll
   for (int t = 0; t < EPC; ++t) o[t] = 0.f;
-  for (int base = 0; base <= p; base += DA6_KPP) {
+  for (int base = 0; base <= p; base += KPP) {
     uint4 kr[NG], vr[NG];
 #pragma unroll
     for (int i = 0; i < NG; ++i) {
@@ -734,14 +733,20 @@ extern "C" int zs_decode_attention_map(const void* qkv, int R, const int* rowmap
              "zs_decode_attention_map: head_dim must be 64");
   ZS_REQUIRE(dtype == ZS_BF16 && Lmax > 0 && Lmax <= 4096,
              "zs_decode_attention_map: bf16 only, Lmax <= 4096");
-  if (g_decode_attn5 == 2 || cpos != nullptr || Lmax > 8 * DA5_MAXI) {
-    hipLaunchKernelGGL(decode_attn6_kernel<bf16_t>, dim3(R, cdiv(heads, 4)), dim3(256), 0,
-                       S(stream), (const bf16_t*)qkv, D, heads, (bf16_t*)kc, (bf16_t*)vc, Lmax,
-                       pos, (const int*)nullptr, (bf16_t*)out, rowmap, cpos, nphys);
-  } else {
+  // the same kernel (and phase length) as zs_decode_attention picks for this knob setting, so a
+  // compacted decode computes exactly what the uncompacted one does
+  if (g_decode_attn5 == 1 && cpos == nullptr && Lmax <= 8 * DA5_MAXI) {
     hipLaunchKernelGGL(decode_attn5_kernel<bf16_t>, dim3(R, cdiv(heads, 4)), dim3(256), 0,
                        S(stream), (const bf16_t*)qkv, D, heads, (bf16_t*)kc, (bf16_t*)vc, Lmax,
                        pos, (const int*)nullptr, (bf16_t*)out, rowmap, nphys);
+  } else if (g_decode_attn5 == 2) {
+    hipLaunchKernelGGL((decode_attn6_kernel<bf16_t, 64>), dim3(R, cdiv(heads, 4)), dim3(256), 0,
+                       S(stream), (const bf16_t*)qkv, D, heads, (bf16_t*)kc, (bf16_t*)vc, Lmax,
+                       pos, (const int*)nullptr, (bf16_t*)out, rowmap, cpos, nphys);
+  } else {
+    hipLaunchKernelGGL((decode_attn6_kernel<bf16_t, 32>), dim3(R, cdiv(heads, 4)), dim3(256), 0,
+                       S(stream), (const bf16_t*)qkv, D, heads, (bf16_t*)kc, (bf16_t*)vc, Lmax,
+                       pos, (const int*)nullptr, (bf16_t*)out, rowmap, cpos, nphys);
   }
   ZS_LAUNCH_CHECK();
   return 0;
@@ -754,6 +759,13 @@ extern "C" int zs_decode_attention(const void* qkv, int R, int D, int heads, voi
              "zs_decode_attention: head_dim must be 64");
   ZS_REQUIRE(Lmax > 0 && Lmax <= 4096, "zs_decode_attention: Lmax");
   dim3 grid(R, heads);
+  if (dtype == ZS_BF16 && g_decode_attn5 == 3) {
+    hipLaunchKernelGGL((decode_attn6_kernel<bf16_t, 32>), dim3(R, cdiv(heads, 4)), dim3(256), 0,
+                       S(stream), (const bf16_t*)qkv, D, heads, (bf16_t*)kc, (bf16_t*)vc, Lmax,
+                       pos, kvrow, (bf16_t*)out, (const int*)nullptr, (const int*)nullptr, R);
+    ZS_LAUNCH_CHECK();
+    return 0;
+  }
   if (dtype == ZS_BF16 && g_decode_attn5 == 2) {
     hipLaunchKernelGGL(decode_attn6_kernel<bf16_t>, dim3(R, cdiv(heads, 4)), dim3(256), 0,
                        S(stream), (const bf16_t*)qkv, D, heads, (bf16_t*)kc, (bf16_t*)vc, Lmax,
