@@ -98,6 +98,23 @@ int zs_l2norm_rows(const float* x, int M, int C, float eps, float* y, void* stre
 int zs_window_attention(const void* qkv, int B, int H, int W, int C, int heads, int ws, int shift,
                         const float* rel_table, void* out, int dtype, void* stream);
 
+/* zs_swin_block: one whole SwinTransformerBlock (htsat.py:427-474, eval) in ONE launch, bf16
+ * operands / f32 residual: x += proj(WindowAttention(LN1(x))); x += fc2(GELU(fc1(LN2(x)))),
+ * with the roll, window partition/reverse, rel-pos bias and -100 shift mask folded in (replaces
+ * the zs_layernorm / zs_gemm / zs_window_attention sequence of one block).  One workgroup per
+ * 8x8 window.  x [B*H*W][C] f32, updated in place.  C in {96, 192, 384}, heads = C / 24.
+ * Weights are fragment-packed bf16 (see csrc/swin.hip): frag(nt, ks)[lane][j] =
+ * W[16 nt + lane%16][32 ks + 8 (lane/16) + j], stored [N/16][K/32][64][8]:
+ *   wqkv_packed: qkv.weight regrouped per pair of heads as rows [q h0, q h1, k h0, k h1, v h0,
+ *   v h1] x 32 (head dim 24 zero-padded to 32) = [heads/2][192][C], then packed;
+ *   bqkv_packed [heads/2][192] f32 (same order, zero pad);  wproj [C][C], w1 [4C][C],
+ *   w2 [C][4C] packed;  biases / LayerNorm params f32;  rel_table [225][heads] f32. */
+int zs_swin_block(float* x, int B, int H, int W, int C, int heads, int shift, const float* ln1_w,
+                  const float* ln1_b, const void* wqkv_packed, const float* bqkv_packed,
+                  const float* rel_table, const void* wproj_packed, const float* bproj,
+                  const float* ln2_w, const float* ln2_b, const void* w1_packed, const float* b1,
+                  const void* w2_packed, const float* b2, void* stream);
+
 /* zs_patch_merge_ln: htsat.py:492-511 gather x0..x3 of each 2x2 patch + LayerNorm(4C):
  * x [B][H][W][C] f32 -> y [B*(H/2)*(W/2)][4C] (dtype); the reduction Linear is a zs_gemm. */
 int zs_patch_merge_ln(const float* x, int B, int H, int W, int C, const float* ln_w,

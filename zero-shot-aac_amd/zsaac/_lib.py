@@ -40,6 +40,7 @@ SIGNATURES = {
     "zs_gemm_workspace_floats": [I, I, I],
     "zs_l2norm_rows": [P, I, I, F, P, P],
     "zs_window_attention": [P, I, I, I, I, I, I, I, P, P, I, P],
+    "zs_swin_block": [P, I, I, I, I, I, I, P, P, P, P, P, P, P, P, P, P, P, P, P, P],
     "zs_patch_merge_ln": [P, I, I, I, I, P, P, P, I, P],
     "zs_ln_meanpool": [P, I, I, I, P, P, P, P],
     "zs_conv3x3_bn_relu": [P, I, I, I, I, P, I, P, P, P, I, P],

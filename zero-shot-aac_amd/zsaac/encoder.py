@@ -10,6 +10,7 @@ Activations: residual stream f32, GEMM operands in the compute dtype.
 from __future__ import annotations
 
 import copy
+import os
 from typing import Dict
 
 import torch
@@ -19,6 +20,32 @@ from .frontend import tables_from_state_dict
 
 DEPTHS, HEADS, EMBED, WIN = (2, 2, 6, 2), (4, 8, 16, 32), 96, 8
 CNN14_CH = (64, 128, 256, 512, 1024, 2048)
+# stages whose blocks run as ONE fused kernel per block (zs_swin_block, bf16 only); the env var
+# ZSAAC_FUSED_SWIN (comma-separated channel widths, "" = none) overrides it for A/B runs
+FUSED_SWIN_C = tuple(int(c) for c in os.environ.get("ZSAAC_FUSED_SWIN", "96,192,384").split(",")
+                     if c.strip())
+
+
+def pack_frags(w: torch.Tensor) -> torch.Tensor:
+    """[N][K] -> MFMA fragment order [N/16][K/32][64][8] (csrc/swin.hip): lane l of fragment
+    (nt, ks) holds W[16 nt + l % 16][32 ks + 8 (l // 16) .. +8]."""
+    N, K = w.shape
+    assert N % 16 == 0 and K % 32 == 0, (N, K)
+    return w.reshape(N // 16, 16, K // 32, 4, 8).permute(0, 2, 3, 1, 4).contiguous()
+
+
+def pack_qkv(w: torch.Tensor, b: torch.Tensor, C: int):
+    """qkv.weight [3C][C] / bias [3C] (htsat.py:286, columns part*C + head*24 + d, 304-309) ->
+    rows regrouped per pair of heads [q h0, q h1, k h0, k h1, v h0, v h1] x 32 (head dim zero-
+    padded 24 -> 32) = [heads/2 * 192][C], fragment-packed; bias [heads/2][192]."""
+    nh = C // 24
+    wp = torch.zeros(3, nh, 32, C, dtype=w.dtype, device=w.device)
+    wp[:, :, :24] = w.reshape(3, nh, 24, C)
+    bp = torch.zeros(3, nh, 32, dtype=b.dtype, device=b.device)
+    bp[:, :, :24] = b.reshape(3, nh, 24)
+    wp = wp.reshape(3, nh // 2, 2, 32, C).permute(1, 0, 2, 3, 4).reshape(nh // 2 * 192, C)
+    bp = bp.reshape(3, nh // 2, 2, 32).permute(1, 0, 2, 3).reshape(nh // 2 * 192)
+    return pack_frags(wp), bp.contiguous()
 
 
 def _f32(t, dev):
@@ -60,6 +87,13 @@ class HtsatWeights:
                     "fc2_w": _w(sd[b + "mlp.fc2.weight"], device, dtype),
                     "fc2_b": _f32(sd[b + "mlp.fc2.bias"], device),
                 })
+                C = EMBED << i
+                if dtype == torch.bfloat16 and C in FUSED_SWIN_C:
+                    blk = stage[-1]
+                    blk["qkv_p"], blk["qkv_bp"] = pack_qkv(blk["qkv_w"], blk["qkv_b"], C)
+                    blk["proj_p"] = pack_frags(blk["proj_w"])
+                    blk["fc1_p"] = pack_frags(blk["fc1_w"])
+                    blk["fc2_p"] = pack_frags(blk["fc2_w"])
             self.blocks.append(stage)
             if i < len(DEPTHS) - 1:
                 d = p + f"layers.{i}.downsample."
@@ -171,6 +205,9 @@ class AudioEncoder:
             for j in range(depth):
                 blk = w.blocks[i][j]
                 shift = 0 if (j % 2 == 0 or res <= WIN) else WIN // 2
+                if "qkv_p" in blk:
+                    ops.swin_block(x, B, res, res, C, heads, shift, blk)
+                    continue
                 h = self.h[:M * C].view(M, C)
                 qkv = self.qkv[:M * 3 * C].view(M, 3 * C)
                 att = self.att[:M * C].view(M, C)

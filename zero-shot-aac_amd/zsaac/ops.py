@@ -175,6 +175,17 @@ def window_attention(qkv, B, H, W, C, heads, shift, rel_table, out, ws=8):
     return out
 
 
+def swin_block(x, B, H, W, C, heads, shift, blk):
+    """One fused SwinTransformerBlock (htsat.py:427-474) in place on the f32 residual stream x
+    [B*H*W, C]; blk holds the fragment-packed bf16 weights (encoder.HtsatWeights)."""
+    _need(x.dtype == torch.float32 and x.is_contiguous(), "swin_block: x must be contiguous f32")
+    call("zs_swin_block", _p(x), B, H, W, C, heads, shift, _p(blk["n1"][0]), _p(blk["n1"][1]),
+         _p(blk["qkv_p"]), _p(blk["qkv_bp"]), _p(blk["rel"]), _p(blk["proj_p"]), _p(blk["proj_b"]),
+         _p(blk["n2"][0]), _p(blk["n2"][1]), _p(blk["fc1_p"]), _p(blk["fc1_b"]), _p(blk["fc2_p"]),
+         _p(blk["fc2_b"]), _s())
+    return x
+
+
 def patch_merge_ln(x, B, H, W, C, ln_w, ln_b, out):
     call("zs_patch_merge_ln", _p(x), B, H, W, C, _p(ln_w), _p(ln_b), _p(out), dt(out), _s())
     return out
