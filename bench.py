@@ -54,6 +54,8 @@ def parse():
     ap.add_argument("--mapper", default="mlp", choices=["mlp", "transformer"])
     ap.add_argument("--beam", type=int, default=0)
     ap.add_argument("--entry-length", type=int, default=67)
+    ap.add_argument("--encoder-batch", type=int, default=256,
+                    help="clips per encoder pass (0 = --batch); per-clip results do not depend on it")
     ap.add_argument("--group", type=int, default=32,
                     help="eval batches of --batch clips decoded together (one decode step over "
                          "group*batch rows); each is still encoded as its own batch")
@@ -97,7 +99,8 @@ def build(args, device):
         asd = S.cnn14_state_dict(4)
         asd.update(S.audio_proj_state_dict(5, audio_width=2048))
     cfg = CaptionConfig(encoder=args.encoder, mapping_type=args.mapper, dtype=dtype,
-                        batch=args.batch * getattr(args, "group", 1), encoder_batch=args.batch,
+                        batch=args.batch * getattr(args, "group", 1),
+                        encoder_batch=getattr(args, "encoder_batch", 0) or args.batch,
                         beam=args.beam, entry_length=args.entry_length,
                         compact_decode=bool(getattr(args, "compact", 1)))
     pipe = CaptionPipeline(csd, asd, S.label_table(), S.label_token_table(), cfg, device=device)

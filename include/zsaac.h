@@ -105,9 +105,9 @@ int zs_window_attention(const void* qkv, int B, int H, int W, int C, int heads, 
  * 8x8 window.  x [B*H*W][C] f32, updated in place.  C in {96, 192, 384}, heads = C / 24.
  * Weights are fragment-packed bf16 (see csrc/swin.hip): frag(nt, ks)[lane][j] =
  * W[16 nt + lane%16][32 ks + 8 (lane/16) + j], stored [N/16][K/32][64][8]:
- *   wqkv_packed: qkv.weight regrouped per pair of heads as rows [q h0, q h1, k h0, k h1, v h0,
- *   v h1] x 32 (head dim 24 zero-padded to 32) = [heads/2][192][C], then packed;
- *   bqkv_packed [heads/2][192] f32 (same order, zero pad);  wproj [C][C], w1 [4C][C],
+ *   wqkv_packed: qkv.weight regrouped per group of G heads (G = 2 for C <= 192, 4 for C = 384)
+ *   as rows [q h0..h(G-1), k h0.., v h0..] x 32 (head dim 24 zero-padded to 32) =
+ *   [heads/G][96 G][C], then packed;  bqkv_packed [heads/G][96 G] f32 (same order, zero pad);  wproj [C][C], w1 [4C][C],
  *   w2 [C][4C] packed;  biases / LayerNorm params f32;  rel_table [225][heads] f32. */
 int zs_swin_block(float* x, int B, int H, int W, int C, int heads, int shift, const float* ln1_w,
                   const float* ln1_b, const void* wqkv_packed, const float* bqkv_packed,

@@ -5,7 +5,7 @@ Replays AudioEncoder._htsat's op sequence with a HIP event around every op (one 
 events bracket exactly that op's kernels) and prints: stage, op, ms per batch, and the op's
 algorithmic HBM bytes / time.  Then times encode() back to back.
 
-    python tools/htsat_profile.py [reps=5]
+    python tools/htsat_profile.py [reps=5] [clips per pass=64]
 """
 import os
 import sys
@@ -23,11 +23,11 @@ from zsaac.encoder import AudioEncoder, DEPTHS, HEADS, WIN  # noqa: E402
 
 def main():
     reps = int(sys.argv[1]) if len(sys.argv) > 1 else 5
+    B = int(sys.argv[2]) if len(sys.argv) > 2 else 64
     dev = torch.device("cuda", 0)
     sd = S.htsat_state_dict(3)
     sd.update(S.audio_proj_state_dict(5))
-    enc = AudioEncoder(sd, "htsat", torch.bfloat16, 64, dev)
-    B = 64
+    enc = AudioEncoder(sd, "htsat", torch.bfloat16, B, dev)
     wav = (torch.randn(B, 320000, device=dev) * 0.1).clamp_(-1, 1)
     enc.encode(wav)
     torch.cuda.synchronize()
@@ -99,14 +99,14 @@ def main():
         print(f"{st:6s} {op:12s} {ms:9.4f} {100 * ms / total:6.1f} {byts[(st, op)] / ms / 1e6:11.0f}")
     for st, ms in per_stage.items():
         print(f"{st:6s} {'TOTAL':12s} {ms:9.4f} {100 * ms / total:6.1f}")
-    print(f"total {total:.3f} ms per 64 clips (single stream, events around every op)")
+    print(f"total {total:.3f} ms per {B} clips (single stream, events around every op)")
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
     for _ in range(reps):
         enc.encode(wav)
     e1.record()
     e1.synchronize()
-    print(f"encode() back to back: {e0.elapsed_time(e1) / reps:.3f} ms per 64 clips")
+    print(f"encode() back to back: {e0.elapsed_time(e1) / reps:.3f} ms per {B} clips")
 
 
 if __name__ == "__main__":

@@ -253,10 +253,16 @@ def bench_decode_gemm():
                      workspace=ws if sk > 1 else None)
             it[0] += 1
         r = {}
-        for t, nm in ((0, "auto"), (4, "128x128"), (15, "256x128w8"), (16, "128x256w8"), (8, "128x64"),
-                      (9, "64x128")):
+        tiles = os.environ.get("ZS_TILES")
+        tl = ([(int(t), f"t{t}") for t in tiles.split(",")] if tiles else
+              [(0, "auto"), (4, "128x128"), (15, "256x128w8"), (16, "128x256w8"), (8, "128x64"),
+               (9, "64x128")])
+        for t, nm in tl:
             call("zs_tune_set", b"fast_tile", t)
             r[nm] = timeit(run, reps=len(wsl))
+        for sk in ((2, 3, 4) if not tiles else ()):
+            call("zs_tune_set", b"fast_tile", 4)
+            r[f"128sk{sk}"] = timeit(lambda: run(sk), reps=len(wsl))
         call("zs_tune_set", b"fast_tile", 0)
         fl = 2 * M * N * K
         print(f"M{M} {name:6s} " + "  ".join(f"{k}={v:5.1f}({fl / v / 1e6:4.0f})" for k, v in r.items()), flush=True)

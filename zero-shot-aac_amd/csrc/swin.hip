@@ -26,8 +26,9 @@
 // Packed weights (prepared once on the host, zsaac/encoder.py):
 //   frag(nt, ks)[lane][j] = W[16 nt + (lane & 15)][32 ks + 8 (lane >> 4) + j]   (W is [N][K])
 //   stored frag-major [N/16][K/32][64][8] bf16.
-//   qkv: per group of 2 heads, rows [q h0, q h1, k h0, k h1, v h0, v h1] x 32 (head dim 24
-//   zero-padded to 32), i.e. [NH/2][192][C] before fragment packing; bias [NH/2][192] f32.
+//   qkv: per group of G heads (G = waves / 2: 2 for C <= 192, 4 for C = 384), rows
+//   [q h0..h(G-1), k h0.., v h0..] x 32 (head dim 24 zero-padded to 32), i.e. [NH/G][96 G][C]
+//   before fragment packing; bias [NH/G][96 G] f32.
 //
 // Attention per (head, 32 queries) wave, as window_attn_mfma_kernel (attn.hip): S^T = K Q^T and
 // O^T = V^T P^T on v_mfma_f32_32x32x16_bf16, rel-pos bias + shift mask, f32 softmax.
@@ -74,31 +75,31 @@ struct WPipe {
   uint4 b[D][NTW];
 };
 
-template <int NTW, int NTOT, int D>
+template <int NTW, int NTOT, int D, int NW>
 __device__ __forceinline__ void wp_load(WPipe<NTW, D>& p, int slot, const uint4* __restrict__ Wp,
                                         int kstot, int ks, int nt0) {
   const int l = threadIdx.x & 63;
 #pragma unroll
   for (int j = 0; j < NTW; ++j)
-    if (NTOT % 4 == 0 || nt0 + 4 * j < NTOT)
-      p.b[slot][j] = Wp[((long)(nt0 + 4 * j) * kstot + ks) * 64 + l];
+    if (NTOT % NW == 0 || nt0 + NW * j < NTOT)
+      p.b[slot][j] = Wp[((long)(nt0 + NW * j) * kstot + ks) * 64 + l];
 }
 
-template <int NTW, int NTOT, int D>
+template <int NTW, int NTOT, int D, int NW>
 __device__ __forceinline__ void wp_prefetch(WPipe<NTW, D>& p, const uint4* __restrict__ Wp,
                                             int kstot, int ks0, int nt0) {
 #pragma unroll
-  for (int s = 0; s < D; ++s) wp_load<NTW, NTOT, D>(p, s, Wp, kstot, ks0 + s, nt0);
+  for (int s = 0; s < D; ++s) wp_load<NTW, NTOT, D, NW>(p, s, Wp, kstot, ks0 + s, nt0);
 }
 
-// acc[mi][j] += A[16 mi .. +16][k] * W[n-tile nt0 + 4 j][k] over KS k-steps of 32 starting at
+// acc[mi][j] += A[16 mi .. +16][k] * W[n-tile nt0 + NW j][k] over KS k-steps of 32 starting at
 // global k-step ks0 of a packed matrix with kstot k-steps per n-tile; the pipe must hold k-steps
 // ks0 .. ks0 + D - 1 (wp_prefetch).  A: LDS, row stride lda (elements).  Slots j with
-// nt0 + 4 j >= NTOT are skipped (wave-uniform).
+// nt0 + NW j >= NTOT are skipped (wave-uniform; NW = waves per workgroup).
 //   TRMASK bit j set: slot j is computed transposed (acc = W . A^T): lane -> token 16 mi + (l & 15),
 //   registers i -> columns 16 nt + 4 (l >> 4) + i.  Clear: lane -> column 16 nt + (l & 15),
 //   registers i -> tokens 16 mi + 4 (l >> 4) + i.
-template <int NTW, int KS, int NTOT, int D, int TRMASK = (1 << NTW) - 1>
+template <int NTW, int KS, int NTOT, int D, int NW, int TRMASK = (1 << NTW) - 1>
 __device__ __forceinline__ void win_gemm(const bf16_t* A, int lda, WPipe<NTW, D>& p,
                                          const uint4* __restrict__ Wp, int kstot, int ks0, int nt0,
                                          sw_f32x4 (&acc)[4][NTW]) {
@@ -114,7 +115,7 @@ __device__ __forceinline__ void win_gemm(const bf16_t* A, int lda, WPipe<NTW, D>
     const int slot = ks % D;
 #pragma unroll
     for (int j = 0; j < NTW; ++j)
-      if (NTOT % 4 == 0 || nt0 + 4 * j < NTOT) {
+      if (NTOT % NW == 0 || nt0 + NW * j < NTOT) {
 #pragma unroll
         for (int mi = 0; mi < 4; ++mi)
           acc[mi][j] = ((TRMASK >> j) & 1)
@@ -123,46 +124,50 @@ __device__ __forceinline__ void win_gemm(const bf16_t* A, int lda, WPipe<NTW, D>
                            : __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[mi], as_bf8(p.b[slot][j]),
                                                                      acc[mi][j], 0, 0, 0);
       }
-    if (ks + D < KS) wp_load<NTW, NTOT, D>(p, slot, Wp, kstot, ks0 + ks + D, nt0);
+    if (ks + D < KS) wp_load<NTW, NTOT, D, NW>(p, slot, Wp, kstot, ks0 + ks + D, nt0);
   }
 }
 
 template <int C>
 struct SwinCfg {
+  static constexpr int NW = C >= 384 ? 8 : 4;  // waves per workgroup (2 per SIMD either way)
+  static constexpr int G = NW / 2;           // heads per q/k/v group: one (head, 32 queries) per wave
   static constexpr int NH = C / 24;          // heads (head dim 24)
-  static constexpr int NG = NH / 2;          // head groups of 2
+  static constexpr int NG = NH / G;          // head groups
   static constexpr int LD = C + 16;          // H / ATT row stride (elements): conflict-free reads
-  static constexpr int HC = 192;             // MLP hidden chunk
+  static constexpr int HC = 48 * NW;         // MLP hidden chunk (3 n-tiles per wave)
   static constexpr int LDH = HC + 16;
   static constexpr int NCH = 4 * C / HC;
   static constexpr int NTP = C / 16;         // n-tiles of proj / fc2
-  static constexpr int NTW = (NTP + 3) / 4;  // per wave (max)
+  static constexpr int NTW = (NTP + NW - 1) / NW;   // per wave (max)
   static constexpr int DA = C <= 96 ? 3 : 2;   // weight pipe depth (k-steps): qkv / fc1
   static constexpr int DB = C <= 96 ? 3 : 2;   // proj / fc2
   static constexpr int SZ_H = 64 * LD * 2;
   static constexpr int OFF_H = 0, OFF_ATT = SZ_H, OFF_QKV = 2 * SZ_H;
-  static constexpr int SZ_QKV = 3 * 2 * 64 * 32 * 2;   // Qs[2][64][32], Ks[2][64][32], Vt[2][32][64]
-  static constexpr int OFF_BT = OFF_QKV + SZ_QKV;      // [2][225] f32
-  static constexpr int OFF_RG = OFF_BT + 1808;         // [64] int8 shift-mask regions
+  static constexpr int SZ_QKV = 3 * G * 64 * 32 * 2;   // Qs[G][64][32], Ks[G][64][32], Vt[G][32][64]
+  static constexpr int OFF_BT = OFF_QKV + SZ_QKV;      // [G][225] f32
+  static constexpr int OFF_RG = OFF_BT + ((G * 225 * 4 + 15) & ~15);   // [64] int8 mask regions
   static constexpr int OFF_ROW = OFF_RG + 64;          // [64] int token rows
   static constexpr int LDS = OFF_ROW + 256;
   static constexpr int LDX = C + 4;                    // final f32 staging [64][C+4]
   static_assert(64 * LDX * 4 <= LDS, "output staging fits");
   static_assert(64 * LDH * 2 <= SZ_H + SZ_QKV, "hidden chunk fits ATT + QKV");
-  static_assert(2 * 4 * 64 * 4 <= SZ_QKV, "LN2 reduction fits QKV");
-  static_assert(C % 96 == 0 && NH % 2 == 0 && (4 * C) % HC == 0, "C");
+  static_assert(2 * NW * 64 * 4 <= SZ_QKV, "LN2 reduction fits QKV");
+  static_assert(LDS <= 160 * 1024, "LDS");
+  static_assert(C % 96 == 0 && NH % G == 0 && (4 * C) % HC == 0 && C % (16 * NW / 4) == 0, "C");
 };
 
 template <int C>
-__global__ __launch_bounds__(256, C <= 192 ? 2 : 1) void swin_block_kernel(SwinArgs g) {
+__global__ __launch_bounds__(64 * SwinCfg<C>::NW, 2) void swin_block_kernel(SwinArgs g) {
   using CF = SwinCfg<C>;
-  constexpr int LD = CF::LD, NTW = CF::NTW, NTP = CF::NTP, KS = C / 32;
+  constexpr int LD = CF::LD, NTW = CF::NTW, NTP = CF::NTP, KS = C / 32, NW = CF::NW, G = CF::G;
+  constexpr int NT = 64 * NW, TPT = NW;      // threads; threads per token in the row passes
   __shared__ __attribute__((aligned(16))) char lds[CF::LDS];
   bf16_t* sH = reinterpret_cast<bf16_t*>(lds + CF::OFF_H);
   bf16_t* sATT = reinterpret_cast<bf16_t*>(lds + CF::OFF_ATT);
   bf16_t* sQ = reinterpret_cast<bf16_t*>(lds + CF::OFF_QKV);
-  bf16_t* sK = sQ + 2 * 64 * 32;
-  bf16_t* sVt = sK + 2 * 64 * 32;
+  bf16_t* sK = sQ + G * 64 * 32;
+  bf16_t* sVt = sK + G * 64 * 32;
   float* sBt = reinterpret_cast<float*>(lds + CF::OFF_BT);
   signed char* sRg = reinterpret_cast<signed char*>(lds + CF::OFF_RG);
   int* sRow = reinterpret_cast<int*>(lds + CF::OFF_ROW);
@@ -171,17 +176,17 @@ __global__ __launch_bounds__(256, C <= 192 ? 2 : 1) void swin_block_kernel(SwinA
   constexpr int DA = CF::DA, DB = CF::DB, KH = CF::HC / 32;
   WPipe<3, DA> pa;        // qkv / fc1 weight fragments in flight
   WPipe<NTW, DB> pb;      // proj / fc2
-  wp_prefetch<3, 12, DA>(pa, g.wqkv, KS, 0, w);
+  wp_prefetch<3, 3 * NW, DA, NW>(pa, g.wqkv, KS, 0, w);
   const int H = g.H, W = g.W, shift = g.shift;
   const int nWw = W / 8, nWh = H / 8;
   const int win = blockIdx.x;
   const int b = win / (nWh * nWw), wyx = win % (nWh * nWw), wy = wyx / nWw, wx = wyx % nWw;
 
-  // ---- P1: LN1.  thread = (token t = tid / 4, quarter q = tid % 4); the row is read as float4
-  // chunks q, q+4, ... so the 4 threads of a token cover 64 contiguous bytes per load.
+  // ---- P1: LN1.  thread = (token t = tid / TPT, part q = tid % TPT); the row is read as float4
+  // chunks q, q+TPT, ... so the TPT threads of a token cover 16 TPT contiguous bytes per load.
   {
-    constexpr int NQ = C / 16;                      // float4 chunks per thread
-    const int t = tid >> 2, q = tid & 3;
+    constexpr int NQ = C / (4 * TPT);               // float4 chunks per thread
+    const int t = tid / TPT, q = tid % TPT;
     const int sy = wy * 8 + (t >> 3), sx = wx * 8 + (t & 7);     // rolled coords
     const int hh = (sy + shift) % H, ww = (sx + shift) % W;      // natural (roll(-shift))
     const int row = (b * H + hh) * W + ww;
@@ -200,11 +205,11 @@ __global__ __launch_bounds__(256, C <= 192 ? 2 : 1) void swin_block_kernel(SwinA
     float s = 0.f;
 #pragma unroll
     for (int j = 0; j < NQ; ++j) {
-      v[j] = xr[4 * j + q];
+      v[j] = xr[TPT * j + q];
       s += (v[j].x + v[j].y) + (v[j].z + v[j].w);
     }
-    s += __shfl_xor(s, 1, 64);
-    s += __shfl_xor(s, 2, 64);
+#pragma unroll
+    for (int o = 1; o < TPT; o <<= 1) s += __shfl_xor(s, o, 64);
     const float mean = s * (1.0f / C);
     float ss = 0.f;
 #pragma unroll
@@ -212,12 +217,12 @@ __global__ __launch_bounds__(256, C <= 192 ? 2 : 1) void swin_block_kernel(SwinA
       const float a0 = v[j].x - mean, a1 = v[j].y - mean, a2 = v[j].z - mean, a3 = v[j].w - mean;
       ss += (a0 * a0 + a1 * a1) + (a2 * a2 + a3 * a3);
     }
-    ss += __shfl_xor(ss, 1, 64);
-    ss += __shfl_xor(ss, 2, 64);
+#pragma unroll
+    for (int o = 1; o < TPT; o <<= 1) ss += __shfl_xor(ss, o, 64);
     const float rstd = rsqrtf(ss * (1.0f / C) + 1e-5f);
 #pragma unroll
     for (int j = 0; j < NQ; ++j) {
-      const int c0 = (4 * j + q) * 4;
+      const int c0 = (TPT * j + q) * 4;
       const float4 gw = *reinterpret_cast<const float4*>(g.ln1_w + c0);
       const float4 gb = *reinterpret_cast<const float4*>(g.ln1_b + c0);
       uint2 u;
@@ -239,19 +244,20 @@ __global__ __launch_bounds__(256, C <= 192 ? 2 : 1) void swin_block_kernel(SwinA
       for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
         for (int j = 0; j < 3; ++j) acc[mi][j] = sw_f32x4{0.f, 0.f, 0.f, 0.f};
-      // slot j of wave w is n-tile w + 4 j = part j (q, k, v) of head w / 2, dims 16 (w & 1)..+16;
+      // slot j of wave w is n-tile w + NW j = part j (q, k, v) of head w / 2, dims 16 (w & 1)..+16;
       // q and k transposed (token rows for the attention fragments), v natural (V^T rows)
-      win_gemm<3, KS, 12, DA, 3>(sH, LD, pa, g.wqkv + (long)grp * 12 * KS * 64, KS, 0, w, acc);
-      if (grp + 1 < CF::NG) wp_prefetch<3, 12, DA>(pa, g.wqkv + (long)(grp + 1) * 12 * KS * 64, KS, 0, w);
-      else wp_prefetch<NTW, NTP, DB>(pb, g.wproj, KS, 0, w);
-      for (int i = tid; i < 2 * 225; i += 256)
-        sBt[i] = g.rel[(i % 225) * CF::NH + 2 * grp + i / 225];
+      constexpr long GS = 3L * NW * KS * 64;       // fragments per head group
+      win_gemm<3, KS, 3 * NW, DA, NW, 3>(sH, LD, pa, g.wqkv + grp * GS, KS, 0, w, acc);
+      if (grp + 1 < CF::NG) wp_prefetch<3, 3 * NW, DA, NW>(pa, g.wqkv + (grp + 1) * GS, KS, 0, w);
+      else wp_prefetch<NTW, NTP, DB, NW>(pb, g.wproj, KS, 0, w);
+      for (int i = tid; i < G * 225; i += NT)
+        sBt[i] = g.rel[(i % 225) * CF::NH + G * grp + i / 225];
       const int hh = w >> 1;
-      const float* bq = g.bqkv + grp * 192;
+      const float* bq = g.bqkv + grp * 48 * NW;
 #pragma unroll
       for (int j = 0; j < 2; ++j) {                      // q, k: lane = token, 4 dims
         const int d0 = (w & 1) * 16 + 4 * (l >> 4);
-        const float4 bias = *reinterpret_cast<const float4*>(bq + (w + 4 * j) * 16 + 4 * (l >> 4));
+        const float4 bias = *reinterpret_cast<const float4*>(bq + (w + NW * j) * 16 + 4 * (l >> 4));
         bf16_t* base = (j == 0 ? sQ : sK) + hh * 2048;
 #pragma unroll
         for (int mi = 0; mi < 4; ++mi) {
@@ -264,7 +270,7 @@ __global__ __launch_bounds__(256, C <= 192 ? 2 : 1) void swin_block_kernel(SwinA
       }
       {                                                  // v: lane = dim, 4 tokens -> V^T
         const int d = (w & 1) * 16 + (l & 15);
-        const float bias = bq[(w + 8) * 16 + (l & 15)];
+        const float bias = bq[(w + 2 * NW) * 16 + (l & 15)];
 #pragma unroll
         for (int mi = 0; mi < 4; ++mi) {
           const int t0 = 16 * mi + 4 * (l >> 4);
@@ -365,7 +371,7 @@ __global__ __launch_bounds__(256, C <= 192 ? 2 : 1) void swin_block_kernel(SwinA
           ot = __builtin_amdgcn_mfma_f32_32x32x16_bf16(va, pb, ot, 0, 0, 0);
         }
       const float inv = 1.0f / sum;
-      bf16_t* orow = sATT + qi * LD + (2 * grp + hh) * 24;
+      bf16_t* orow = sATT + qi * LD + (G * grp + hh) * 24;
 #pragma unroll
       for (int gq = 0; gq < 3; ++gq) {       // dims 8 gq + 4 h2 .. +3 (< 24)
         const int d0 = 8 * gq + 4 * h2;
@@ -379,18 +385,18 @@ __global__ __launch_bounds__(256, C <= 192 ? 2 : 1) void swin_block_kernel(SwinA
   }
 
   // ---- P3: proj (transposed) + bias + residual -> x1 (registers: lane = token 16 mi + (l & 15),
-  // x1[mi][j][i] = column 16 (w + 4 j) + 4 (l >> 4) + i)
+  // x1[mi][j][i] = column 16 (w + NW j) + 4 (l >> 4) + i)
   sw_f32x4 x1[4][NTW];
 #pragma unroll
   for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
     for (int j = 0; j < NTW; ++j) x1[mi][j] = sw_f32x4{0.f, 0.f, 0.f, 0.f};
-  win_gemm<NTW, KS, NTP, DB>(sATT, LD, pb, g.wproj, KS, 0, w, x1);
-  wp_prefetch<3, 12, DA>(pa, g.w1, KS, 0, w);
+  win_gemm<NTW, KS, NTP, DB, NW>(sATT, LD, pb, g.wproj, KS, 0, w, x1);
+  wp_prefetch<3, 3 * NW, DA, NW>(pa, g.w1, KS, 0, w);
 #pragma unroll
   for (int j = 0; j < NTW; ++j) {
-    if (NTP % 4 == 0 || w + 4 * j < NTP) {
-      const int c0 = (w + 4 * j) * 16 + 4 * (l >> 4);
+    if (NTP % NW == 0 || w + NW * j < NTP) {
+      const int c0 = (w + NW * j) * 16 + 4 * (l >> 4);
       const float4 bias = *reinterpret_cast<const float4*>(g.bproj + c0);
 #pragma unroll
       for (int mi = 0; mi < 4; ++mi) {
@@ -407,7 +413,7 @@ __global__ __launch_bounds__(256, C <= 192 ? 2 : 1) void swin_block_kernel(SwinA
   // ---- P4: LN2 over x1: per-lane partial row sums, the 4 lanes of a token (xor 16, 32), then
   // the 4 waves through LDS; two passes (mean, then centred squares) as LN1
   {
-    float* red = reinterpret_cast<float*>(lds + CF::OFF_QKV);     // [2][4][64]
+    float* red = reinterpret_cast<float*>(lds + CF::OFF_QKV);     // [2][NW][64]
     float mean[4], rstd[4];
 #pragma unroll
     for (int pass = 0; pass < 2; ++pass) {
@@ -416,7 +422,7 @@ __global__ __launch_bounds__(256, C <= 192 ? 2 : 1) void swin_block_kernel(SwinA
         float a = 0.f;
 #pragma unroll
         for (int j = 0; j < NTW; ++j)
-          if (NTP % 4 == 0 || w + 4 * j < NTP) {
+          if (NTP % NW == 0 || w + NW * j < NTP) {
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
               const float v = pass == 0 ? x1[mi][j][i] : x1[mi][j][i] - mean[mi];
@@ -425,22 +431,23 @@ __global__ __launch_bounds__(256, C <= 192 ? 2 : 1) void swin_block_kernel(SwinA
           }
         a += __shfl_xor(a, 16, 64);
         a += __shfl_xor(a, 32, 64);
-        if (l < 16) red[pass * 256 + w * 64 + 16 * mi + l] = a;
+        if (l < 16) red[pass * NW * 64 + w * 64 + 16 * mi + l] = a;
       }
       __syncthreads();
 #pragma unroll
       for (int mi = 0; mi < 4; ++mi) {
         const int t = 16 * mi + (l & 15);
-        const float tot = (red[pass * 256 + t] + red[pass * 256 + 64 + t]) +
-                          (red[pass * 256 + 128 + t] + red[pass * 256 + 192 + t]);
+        float tot = 0.f;
+#pragma unroll
+        for (int u = 0; u < NW; ++u) tot += red[pass * NW * 64 + u * 64 + t];
         if (pass == 0) mean[mi] = tot * (1.0f / C);
         else rstd[mi] = rsqrtf(tot * (1.0f / C) + 1e-5f);
       }
     }
 #pragma unroll
     for (int j = 0; j < NTW; ++j) {
-      if (NTP % 4 == 0 || w + 4 * j < NTP) {
-        const int c0 = (w + 4 * j) * 16 + 4 * (l >> 4);
+      if (NTP % NW == 0 || w + NW * j < NTP) {
+        const int c0 = (w + NW * j) * 16 + 4 * (l >> 4);
         const float4 gw = *reinterpret_cast<const float4*>(g.ln2_w + c0);
         const float4 gb = *reinterpret_cast<const float4*>(g.ln2_b + c0);
 #pragma unroll
@@ -472,11 +479,11 @@ __global__ __launch_bounds__(256, C <= 192 ? 2 : 1) void swin_block_kernel(SwinA
       for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
         for (int j = 0; j < 3; ++j) acc1[mi][j] = sw_f32x4{0.f, 0.f, 0.f, 0.f};
-      win_gemm<3, KS, 12, DA>(sH, LD, pa, g.w1 + (long)ch * 12 * KS * 64, KS, 0, w, acc1);
-      wp_prefetch<NTW, NTP, DB>(pb, g.w2, 4 * C / 32, ch * KH, w);
+      win_gemm<3, KS, 3 * NW, DA, NW>(sH, LD, pa, g.w1 + (long)ch * 3 * NW * KS * 64, KS, 0, w, acc1);
+      wp_prefetch<NTW, NTP, DB, NW>(pb, g.w2, 4 * C / 32, ch * KH, w);
 #pragma unroll
       for (int j = 0; j < 3; ++j) {
-        const int c0 = (w + 4 * j) * 16 + 4 * (l >> 4);
+        const int c0 = (w + NW * j) * 16 + 4 * (l >> 4);
         const float4 bias = *reinterpret_cast<const float4*>(g.b1 + ch * CF::HC + c0);
 #pragma unroll
         for (int mi = 0; mi < 4; ++mi) {
@@ -495,8 +502,9 @@ __global__ __launch_bounds__(256, C <= 192 ? 2 : 1) void swin_block_kernel(SwinA
       }
     }
     __syncthreads();
-    win_gemm<NTW, KH, NTP, DB>(sHID, CF::LDH, pb, g.w2, 4 * C / 32, ch * KH, w, acc2);
-    if (ch + 1 < CF::NCH) wp_prefetch<3, 12, DA>(pa, g.w1 + (long)(ch + 1) * 12 * KS * 64, KS, 0, w);
+    win_gemm<NTW, KH, NTP, DB, NW>(sHID, CF::LDH, pb, g.w2, 4 * C / 32, ch * KH, w, acc2);
+    if (ch + 1 < CF::NCH)
+      wp_prefetch<3, 3 * NW, DA, NW>(pa, g.w1 + (long)(ch + 1) * 3 * NW * KS * 64, KS, 0, w);
     __syncthreads();
   }
 
@@ -504,8 +512,8 @@ __global__ __launch_bounds__(256, C <= 192 ? 2 : 1) void swin_block_kernel(SwinA
   float* sX = reinterpret_cast<float*>(lds);
 #pragma unroll
   for (int j = 0; j < NTW; ++j) {
-    if (NTP % 4 == 0 || w + 4 * j < NTP) {
-      const int c0 = (w + 4 * j) * 16 + 4 * (l >> 4);
+    if (NTP % NW == 0 || w + NW * j < NTP) {
+      const int c0 = (w + NW * j) * 16 + 4 * (l >> 4);
       const float4 bias = *reinterpret_cast<const float4*>(g.b2 + c0);
 #pragma unroll
       for (int mi = 0; mi < 4; ++mi) {
@@ -518,11 +526,11 @@ __global__ __launch_bounds__(256, C <= 192 ? 2 : 1) void swin_block_kernel(SwinA
   }
   __syncthreads();
   {
-    const int t = tid >> 2, q = tid & 3;
+    const int t = tid / TPT, q = tid % TPT;
     float4* xr = reinterpret_cast<float4*>(g.x + (long)sRow[t] * C);
 #pragma unroll
-    for (int j = 0; j < C / 16; ++j)
-      xr[4 * j + q] = *reinterpret_cast<const float4*>(sX + t * CF::LDX + (4 * j + q) * 4);
+    for (int j = 0; j < C / (4 * TPT); ++j)
+      xr[TPT * j + q] = *reinterpret_cast<const float4*>(sX + t * CF::LDX + (TPT * j + q) * 4);
   }
 }
 
@@ -547,9 +555,9 @@ extern "C" int zs_swin_block(float* x, int B, int H, int W, int C, int heads, in
              (const uint4*)w2_packed, b2, g_swin_dbg};
   dim3 grid(B * (H / 8) * (W / 8));
   hipStream_t st = S(stream);
-  if (C == 96) hipLaunchKernelGGL(swin_block_kernel<96>, grid, dim3(256), 0, st, a);
-  else if (C == 192) hipLaunchKernelGGL(swin_block_kernel<192>, grid, dim3(256), 0, st, a);
-  else hipLaunchKernelGGL(swin_block_kernel<384>, grid, dim3(256), 0, st, a);
+  if (C == 96) hipLaunchKernelGGL(swin_block_kernel<96>, grid, dim3(64 * SwinCfg<96>::NW), 0, st, a);
+  else if (C == 192) hipLaunchKernelGGL(swin_block_kernel<192>, grid, dim3(64 * SwinCfg<192>::NW), 0, st, a);
+  else hipLaunchKernelGGL(swin_block_kernel<384>, grid, dim3(64 * SwinCfg<384>::NW), 0, st, a);
   ZS_LAUNCH_CHECK();
   return 0;
 }

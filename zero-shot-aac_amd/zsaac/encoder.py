@@ -34,17 +34,23 @@ def pack_frags(w: torch.Tensor) -> torch.Tensor:
     return w.reshape(N // 16, 16, K // 32, 4, 8).permute(0, 2, 3, 1, 4).contiguous()
 
 
+def swin_group(C: int) -> int:
+    """Heads per q/k/v group of the fused Swin kernel (csrc/swin.hip SwinCfg::G): one
+    (head, 32 queries) per wave, 4 waves for C <= 192, 8 for C = 384."""
+    return 4 if C >= 384 else 2
+
+
 def pack_qkv(w: torch.Tensor, b: torch.Tensor, C: int):
     """qkv.weight [3C][C] / bias [3C] (htsat.py:286, columns part*C + head*24 + d, 304-309) ->
-    rows regrouped per pair of heads [q h0, q h1, k h0, k h1, v h0, v h1] x 32 (head dim zero-
-    padded 24 -> 32) = [heads/2 * 192][C], fragment-packed; bias [heads/2][192]."""
-    nh = C // 24
+    rows regrouped per group of G heads [q h0.., k h0.., v h0..] x 32 (head dim zero-padded
+    24 -> 32) = [heads/G * 96 G][C], fragment-packed; bias [heads/G][96 G]."""
+    nh, G = C // 24, swin_group(C)
     wp = torch.zeros(3, nh, 32, C, dtype=w.dtype, device=w.device)
     wp[:, :, :24] = w.reshape(3, nh, 24, C)
     bp = torch.zeros(3, nh, 32, dtype=b.dtype, device=b.device)
     bp[:, :, :24] = b.reshape(3, nh, 24)
-    wp = wp.reshape(3, nh // 2, 2, 32, C).permute(1, 0, 2, 3, 4).reshape(nh // 2 * 192, C)
-    bp = bp.reshape(3, nh // 2, 2, 32).permute(1, 0, 2, 3).reshape(nh // 2 * 192)
+    wp = wp.reshape(3, nh // G, G, 32, C).permute(1, 0, 2, 3, 4).reshape(nh * 96, C)
+    bp = bp.reshape(3, nh // G, G, 32).permute(1, 0, 2, 3).reshape(nh * 96)
     return pack_frags(wp), bp.contiguous()
 
 
@@ -182,10 +188,15 @@ class AudioEncoder:
             self.img = torch.empty(B, 256, 256, device=dev)
             self.x = torch.empty(M * 96, device=dev)            # residual stream (f32), ping
             self.x2 = torch.empty(M * 96 // 2, device=dev)      # after a merge, pong
-            self.h = torch.empty(M * 96, device=dev, dtype=dtype)
-            self.qkv = torch.empty(M * 288, device=dev, dtype=dtype)
-            self.att = torch.empty(M * 96, device=dev, dtype=dtype)
-            self.hid = torch.empty(M * 384, device=dev, dtype=dtype)
+            # activations of the unfused block sequence: M*C is the same at every stage
+            # (tokens / 4, channels * 2 per merge), so size for the first unfused stage only
+            # (stages run by zs_swin_block keep theirs in LDS)
+            unf = [i for i in range(len(DEPTHS)) if "qkv_p" not in self.w.blocks[i][0]]
+            mc = M * 96 if unf else 0
+            self.h = torch.empty(mc, device=dev, dtype=dtype)
+            self.qkv = torch.empty(mc * 3, device=dev, dtype=dtype)
+            self.att = torch.empty(mc, device=dev, dtype=dtype)
+            self.hid = torch.empty(mc * 4, device=dev, dtype=dtype)
             self.mrg = torch.empty(M * 96, device=dev, dtype=dtype)
         else:
             H, W = self.n_frames, 64
