@@ -211,7 +211,9 @@ int zs_compact_rows(const int* done, int nrows, int* rowmap, int* n_active, void
  *   logits = A W^T, split in column blocks of 128; per (row, block) writes the block's max,
  *   sum(exp(logit - max)) and its top-`topk` (value, index) (ties -> lower index).
  *   part_stat [M][nblk][2] f32, part_val [M][nblk][topk] f32, part_idx [M][nblk][topk] int32,
- *   nblk = ceil(V/128).  topk <= 8.  With row_norm != 0 each A row is L2-normalised first
+ *   nblk = ceil(V/128).  topk <= 8.  part_stat may be NULL (argmax callers: greedy generate2,
+ *   get_prefix_tokens): the max / sum-exp pass is then skipped.  With row_norm != 0 each A row
+ *   is L2-normalised first
  *   (get_prefix_tokens, gpt2_prefix_eval.py:271-278: W must then be normalize(wte)). */
 int zs_lmhead_topk(int M, int K, int V, int dtype, const void* A, int lda, const void* W,
                    int topk, int row_norm, float* part_stat, float* part_val, int* part_idx,

@@ -133,10 +133,12 @@ def bench_gemm_dbg():
         w = (torch.randn(N, K, device=dev) * 0.02).bfloat16()
         out = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
         res = {}
-        for t, nm, pers in ((4, "128x128P", 1), (15, "256x128w8", 1), (16, "128x256w8", 1)):
+        tiles = [(int(t), f"t{t}", 1) for t in os.environ.get("ZS_TILES", "").split(",") if t]
+        dbgs = [(int(d), f"d{d}") for d in os.environ.get("ZS_DBGS", "").split(",") if d]
+        for t, nm, pers in (tiles or ((4, "128x128P", 1), (15, "256x128w8", 1), (16, "128x256w8", 1))):
             call("zs_tune_set", b"fast_tile", t)
             call("zs_tune_set", b"fast_persist", pers)
-            for d, dn in ((0, "full"), (3, "noLoop"), (4, "noEpi")):
+            for d, dn in (dbgs or ((0, "full"), (3, "noLoop"), (4, "noEpi"))):
                 call("zs_tune_set", b"gemm_dbg", d)
                 res[f"{nm}/{dn}"] = timeit(lambda: ops.gemm(a, w, out, split_k=1), reps=20)
         call("zs_tune_set", b"gemm_dbg", 0)
@@ -145,6 +147,28 @@ def bench_gemm_dbg():
         res["torch"] = timeit(lambda: torch.nn.functional.linear(a, w), reps=20)
         print(f"M{M:6d} N{N:5d} K{K:4d} " + "  ".join(f"{k}={v:7.1f}" for k, v in res.items()),
               flush=True)
+
+
+def bench_overhead():
+    """Per-launch cost of tiny kernels in a graph-replayed chain (the floor every decode-step
+    kernel pays): cast of 64 floats, LayerNorm at 64 / 2048 rows, a 128x128x64 GEMM."""
+    from zsaac import ops
+    dev = torch.device("cuda", 0)
+    x = torch.randn(2048, 768, device=dev)
+    y = torch.empty(2048, 768, device=dev, dtype=torch.bfloat16)
+    w = torch.ones(768, device=dev)
+    b = torch.zeros(768, device=dev)
+    t = torch.empty(64, device=dev, dtype=torch.bfloat16)
+    a = torch.randn(128, 64, device=dev).bfloat16()
+    wt = torch.randn(128, 64, device=dev).bfloat16()
+    o = torch.empty(128, 128, device=dev, dtype=torch.bfloat16)
+    r = {
+        "cast64": timeit(lambda: ops.cast(x.view(-1)[:64], t), reps=200),
+        "ln64": timeit(lambda: ops.layernorm(x[:64], w, b, out=y[:64]), reps=200),
+        "ln2048": timeit(lambda: ops.layernorm(x, w, b, out=y), reps=200),
+        "gemm128": timeit(lambda: ops.gemm(a, wt, o, split_k=1), reps=200),
+    }
+    print("  ".join(f"{k}={v:6.2f}us" for k, v in r.items()), flush=True)
 
 
 def bench_lmhead():
@@ -427,4 +451,4 @@ if __name__ == "__main__":
             call("zs_tune_set", k.encode(), int(v))
     which = sys.argv[1:] or ["gemm", "attn"]
     for wname in which:
-        {"gemm": bench_gemm, "gemm_m": bench_gemm_m, "gemm_htsat": bench_gemm_htsat, "gemm_dbg": bench_gemm_dbg, "lmhead": bench_lmhead, "front": bench_front, "window": bench_window, "decode_gemm": bench_decode_gemm, "attn": bench_attn, "inflight": bench_inflight, "buckets": bench_buckets, "compact_ab": bench_compact_ab, "host": bench_host}[wname]()
+        {"gemm": bench_gemm, "gemm_m": bench_gemm_m, "gemm_htsat": bench_gemm_htsat, "gemm_dbg": bench_gemm_dbg, "lmhead": bench_lmhead, "overhead": bench_overhead, "front": bench_front, "window": bench_window, "decode_gemm": bench_decode_gemm, "attn": bench_attn, "inflight": bench_inflight, "buckets": bench_buckets, "compact_ab": bench_compact_ab, "host": bench_host}[wname]()

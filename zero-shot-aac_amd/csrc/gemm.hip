@@ -516,16 +516,18 @@ __global__ __launch_bounds__(256) void lmhead_kernel(int xcd_order, int M, int K
       }
       const float bv = tv[0];
       float se = 0.f;
-      if (bv != -INFINITY) {
+      // the softmax denominator only for callers that need log-probabilities (beam search);
+      // greedy argmax and get_prefix_tokens pass part_stat = NULL and skip these 64 exps/lane
+      if (part_stat != nullptr && bv != -INFINITY) {
 #pragma unroll
         for (int i = 0; i < TMV; ++i)
 #pragma unroll
           for (int e = 0; e < 16; ++e) {
             const int n = n0 + wr0 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5);
-            if (n < V) se += expf(acct[i][j][e] * sc - bv);
+            if (n < V) se += __expf(acct[i][j][e] * sc - bv);
           }
+        se += __shfl_xor(se, 32, 64);
       }
-      se += __shfl_xor(se, 32, 64);
       if (lane < 32) {
         xm[wg * BM + r] = bv;
         xs[wg * BM + r] = se;
@@ -545,8 +547,10 @@ __global__ __launch_bounds__(256) void lmhead_kernel(int xcd_order, int M, int K
       const float se = (m0v == -INFINITY ? 0.f : xs[r] * expf(m0v - g)) +
                        (m1v == -INFINITY ? 0.f : xs[BM + r] * expf(m1v - g));
       const long o = (long)m * nblk + vb;
-      part_stat[o * 2 + 0] = g;
-      part_stat[o * 2 + 1] = se;
+      if (part_stat != nullptr) {
+        part_stat[o * 2 + 0] = g;
+        part_stat[o * 2 + 1] = se;
+      }
       const float* l0v = xv + r * KMAX;
       const int* l0i = xi + r * KMAX;
       const float* l1v = xv + (BM + r) * KMAX;
@@ -616,7 +620,7 @@ __global__ __launch_bounds__(256) void lmhead_kernel(int xcd_order, int M, int K
 #pragma unroll
   for (int o = 1; o < TPR; o <<= 1) gmx = fmaxf(gmx, __shfl_xor(gmx, o, 64));
   float se = 0.f;
-  for (int c = sub * CPT; c < sub * CPT + CPT; ++c) {
+  for (int c = sub * CPT; part_stat != nullptr && c < sub * CPT + CPT; ++c) {
     const int n = n0 + c;
     if (n >= V) break;
     se += expf(tile[r * (LM_BN + 1) + c] * scale - gmx);
@@ -632,8 +636,10 @@ __global__ __launch_bounds__(256) void lmhead_kernel(int xcd_order, int M, int K
   __syncthreads();
   if (sub == 0 && m < M) {
     const long o = ((long)m * nblk + vb);
-    part_stat[o * 2 + 0] = gmx;
-    part_stat[o * 2 + 1] = se;
+    if (part_stat != nullptr) {
+      part_stat[o * 2 + 0] = gmx;
+      part_stat[o * 2 + 1] = se;
+    }
     int ptr[TPR];
 #pragma unroll
     for (int t = 0; t < TPR; ++t) ptr[t] = 0;

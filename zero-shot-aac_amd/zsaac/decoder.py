@@ -315,7 +315,7 @@ class Gpt2Decoder:
 
     def _greedy_step_body_c(self, R, Rb):
         self._decode_forward_c(R, Rb)
-        ops.lmhead_topk(self.hf[:Rb], self.w.wte, 1, self.pstat, self.pval1, self.pidx1)
+        ops.lmhead_topk(self.hf[:Rb], self.w.wte, 1, None, self.pval1, self.pidx1)
         ops.greedy_step_map(self.pval1, self.pidx1, Rb, self.rowmap, R, self.nblk, self.step_ctr,
                             self.max_steps, self.stop0, self.stop1, self.out_ids, self.out_len,
                             self.done, self.pos, self.next_tok, self.all_done)
@@ -352,7 +352,7 @@ class Gpt2Decoder:
 
     def _greedy_step_body(self, R):
         self._decode_forward(R)
-        ops.lmhead_topk(self.hf[:R], self.w.wte, 1, self.pstat, self.pval1, self.pidx1)
+        ops.lmhead_topk(self.hf[:R], self.w.wte, 1, None, self.pval1, self.pidx1)
         ops.greedy_step(self.pval1, self.pidx1, R, self.nblk, self.step_ctr, self.max_steps,
                         self.stop0, self.stop1, self.out_ids, self.out_len, self.done, self.pos,
                         self.next_tok, self.all_done)
@@ -433,7 +433,7 @@ class Gpt2Decoder:
         """Enqueue step 0 of generate2 from the prefill rows (no host sync); afterwards
         :meth:`step_chunk` advances ``chunk`` steps at a time."""
         R = B
-        ops.lmhead_topk(self.hf[:R], self.w.wte, 1, self.pstat, self.pval1, self.pidx1)
+        ops.lmhead_topk(self.hf[:R], self.w.wte, 1, None, self.pval1, self.pidx1)
         self.pos[:R].copy_(self.plen[:R] - 1)
         for t in (self.done, self.out_len, self.step_ctr, self.all_done, self.out_ids):
             t.zero_()
@@ -491,7 +491,7 @@ class Gpt2Decoder:
         M = embed_rows.shape[0]
         a = self.h[:M]
         ops.cast(embed_rows, a)
-        ops.lmhead_topk(a, self.w.wte_norm, 1, self.pstat_big(M), self.pval_big(M), self.pidx_big(M),
+        ops.lmhead_topk(a, self.w.wte_norm, 1, None, self.pval_big(M), self.pidx_big(M),
                         row_norm=True)
         ops.argmax_finalize(self._pv_big, self._pi_big, M, self.nblk, out_idx)
         return out_idx
