@@ -20,7 +20,9 @@ def test_arch(cuda):
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("M,N,K", [(64, 768, 768), (100, 300, 96), (1536, 2304, 768), (7, 50, 64),
-                                   (4096, 384, 96), (64, 768, 3072)])
+                                   (4096, 384, 96), (64, 768, 3072),
+                                   # 64x64 tiles with 128-deep k-steps (decode proj / c_proj)
+                                   (2048, 768, 768), (2048, 768, 3072), (300, 768, 3072)])
 def test_gemm(cuda, dtype, M, N, K):
     from zsaac import ops
     g = torch.Generator(device="cuda").manual_seed(M * 7 + N)

@@ -172,6 +172,7 @@ __global__ __launch_bounds__(64 * WGM * WGN,
   using FT = FastTile<BM, BN, WGM, WGN, BK_>;
   __shared__ __attribute__((aligned(16))) char lds[NS * FT::STAGE];
   constexpr int TM = FT::TM, TN = FT::TN, WN = FT::WN;
+  if (g.dbg == 5) return;   // experiment: launch cost only
   static_assert(FT::NW * 32 * WN * 4 <= NS * FT::STAGE, "epilogue slab must fit the stage ring");
   // persistent: a grid of (CUs x resident blocks) walks the tiles (n fastest, then m, then the
   // k split), so the per-workgroup dispatch cost is paid once per resident block, not per tile
@@ -350,6 +351,7 @@ static int dispatch_fast(GemmArgs& g, hipStream_t st) {
     case 14: return launch_fast<128, 128, 4>(g, st);
     case 15: return launch_fast<256, 128, 2, 4, 2, 64>(g, st);
     case 16: return launch_fast<128, 256, 2, 2, 4, 64>(g, st);
+    case 17: return launch_fast<64, 64, 2, 2, 2, 128>(g, st);
     default: break;
   }
   if (nblocks(g, 128, 128) >= 256) {
@@ -359,6 +361,10 @@ static int dispatch_fast(GemmArgs& g, hipStream_t st) {
   }
   if (nblocks(g, 128, 64) >= 256) return g.M >= g.N ? launch_fast<128, 64, 3>(g, st)
                                                      : launch_fast<64, 128, 3>(g, st);
+  // small tiles are bound by the per-k-step skeleton (counted wait + barrier + DMA issue,
+  // ~300 cycles) rather than by their 4 MFMAs per wave: 128-deep k-steps halve the step count
+  // (decode proj / c_proj at 2048 rows: 12.5 -> 11.7 us, 32 -> 28 us)
+  if (g.k_per_split % 128 == 0) return launch_fast<64, 64, 2, 2, 2, 128>(g, st);
   return launch_fast<64, 64, 4>(g, st);
 }
 

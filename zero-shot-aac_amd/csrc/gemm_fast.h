@@ -47,7 +47,7 @@ struct FastTile {
   static constexpr int ROWS = BM + BN;
   static constexpr int STAGE = ROWS * RB;           // bytes
   static constexpr int NI = ROWS / RPI;             // DMA instructions per stage
-  static_assert(BK_ == 32 || BK_ == 64, "BK");
+  static_assert(BK_ == 32 || BK_ == 64 || BK_ == 128, "BK");
   static_assert(BM % (RPI * NW) == 0 && BN % (RPI * NW) == 0, "DMA rows per wave");
   static constexpr int WM = BM / WGM, WN = BN / WGN;
   static constexpr int TM = WM / 32, TN = WN / 32;
