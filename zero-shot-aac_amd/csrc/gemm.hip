@@ -15,7 +15,8 @@
 namespace zs {
 
 int g_gemm_fast = 1;   // zs_tune_set("gemm_fast", 0) selects the register-staged bf16 loop
-int g_gemm_dbg = 0;
+int g_gemm_dbg = 0;   // experiments: 1 no MFMA, 2 no DMA, 3 neither, 4 no epilogue, 5 launch
+                      // only, 6 no global stores (tools/mbench.py gemm_dbg)
 int g_fast_xcd = 1;       // zs_tune_set("fast_xcd", 0): n-fastest tile order
 
 __device__ __forceinline__ void store_out(void* out, int out_dtype, long idx, float v) {
@@ -126,7 +127,8 @@ __device__ __forceinline__ void epi_slab(const GemmArgs& g, const float* slab, i
         u.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
         u.z = (uint32_t)f2bf(v[4]) | ((uint32_t)f2bf(v[5]) << 16);
         u.w = (uint32_t)f2bf(v[6]) | ((uint32_t)f2bf(v[7]) << 16);
-        *reinterpret_cast<uint4*>(reinterpret_cast<bf16_t*>(g.out) + o) = u;
+        if (g.dbg != 6 || u.x == 0x7fc17fc1u)   // dbg 6 (experiment): no global stores
+          *reinterpret_cast<uint4*>(reinterpret_cast<bf16_t*>(g.out) + o) = u;
       } else {
         float4* d = reinterpret_cast<float4*>(reinterpret_cast<float*>(g.out) + o);
         d[0] = make_float4(v[0], v[1], v[2], v[3]);
