@@ -56,9 +56,10 @@ def parse():
     ap.add_argument("--entry-length", type=int, default=67)
     ap.add_argument("--encoder-batch", type=int, default=256,
                     help="clips per encoder pass (0 = --batch); per-clip results do not depend on it")
-    ap.add_argument("--group", type=int, default=32,
+    ap.add_argument("--group", type=int, default=64,
                     help="eval batches of --batch clips decoded together (one decode step over "
-                         "group*batch rows); each is still encoded as its own batch")
+                         "group*batch rows; 64 -> 4096 rows: 11.4k vs 10.9k clips/s at 32); "
+                         "encoded --encoder-batch clips per pass")
     ap.add_argument("--inflight", type=int, default=3,
                     help="independent bs=--batch batches decoding concurrently per GPU (streams)")
     ap.add_argument("--compact", type=int, default=1,
