@@ -283,6 +283,9 @@ def bench_decode_gemm():
                (9, "64x128")])
         for t, nm in tl:
             call("zs_tune_set", b"fast_tile", t)
+            lean = os.environ.get("ZS_LEAN")
+            if lean is not None:
+                call("zs_tune_set", b"gemm_lean", int(lean))
             r[nm] = timeit(run, reps=len(wsl))
         for sk in ((2, 3, 4) if not tiles else ()):
             call("zs_tune_set", b"fast_tile", 4)

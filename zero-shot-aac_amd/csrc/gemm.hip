@@ -313,6 +313,128 @@ __global__ __launch_bounds__(64 * WGM * WGN,
   }
 }
 
+// ------------------------------------------------------------------ lean tile kernel
+// One output tile per workgroup, no persistent loop, no split-K, K % BK == 0: the decode-step
+// shapes (M = 256..4096 rows, N = 768..3072, K = 768 / 3072).  Same swizzled LDS-DMA ring as
+// gemm_fast_kernel, but the per-lane DMA source pointers are computed ONCE per tile (rows
+// clamped into the matrix instead of a per-chunk zero-chunk select; clamped rows only feed
+// outputs the store guard drops), and the k-loop carries nothing but the counted wait, the raw
+// barrier, IPW pointer adds + DMAs and the MFMAs: gemm_fast_kernel's persistent / cross-tile /
+// split-K / experiment control flow spilled SGPRs into VGPR lanes and cost ~300 cycles of
+// scalar work per k-step, more than a 64x64 tile's MFMAs.
+template <int BM, int BN, int NS, int BK_>
+__global__ __launch_bounds__(256, 2) void gemm_lean_kernel(GemmArgs g) {
+  using FT = FastTile<BM, BN, 2, 2, BK_>;
+  constexpr int TM = FT::TM, TN = FT::TN, WN = FT::WN, NW = 4;
+  constexpr int IPW = FT::NI / NW;                 // DMA instructions per wave per stage
+  static_assert(NW * 32 * WN * 4 <= NS * FT::STAGE, "epilogue slab fits the ring");
+  __shared__ __attribute__((aligned(16))) char lds[NS * FT::STAGE];
+  const int ntn = cdiv(g.N, BN), ntm = cdiv(g.M, BM), ntiles = ntn * ntm;
+  // XCD-local grouped tile order (see gemm_fast_kernel): slot b runs on XCD b % 8
+  int m0, n0;
+  {
+    const int b = blockIdx.x, x = b & 7, q8 = ntiles >> 3, r8 = ntiles & 7;
+    const int u = (x < r8 ? x * (q8 + 1) : r8 * (q8 + 1) + (x - r8) * q8) + (b >> 3);
+    const int conc = max(1, min(q8, 64));
+    int gm = (int)(sqrtf((float)conc * BN / BM) + 0.5f);
+    gm = max(1, min(gm, ntm));
+    const int per = gm * ntn, grp = u / per, fm = grp * gm;
+    const int gs = min(ntm - fm, gm), r = u - grp * per;
+    m0 = (fm + r % gs) * BM;
+    n0 = (r / gs) * BN;
+  }
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const bf16_t* src[IPW];
+  {
+    const int rsub = lane / FT::SPR, slot = lane % FT::SPR;
+#pragma unroll
+    for (int j = 0; j < IPW; ++j) {
+      const int i = wid + NW * j;                   // DMA instruction: rows RPI*i .. +RPI
+      const int row = FT::RPI * i + rsub;
+      const int c = 8 * (slot ^ FT::swz(row));
+      if (row < BM) {                               // wave-uniform (BM multiple of RPI*NW)
+        const int ar = min(m0 + row, g.M - 1);
+        src[j] = (const bf16_t*)g.A + (long)ar * g.lda + c;
+      } else {
+        const int wr = min(n0 + row - BM, g.N - 1);
+        src[j] = (const bf16_t*)g.W + (long)wr * g.ldw + c;
+      }
+    }
+  }
+  auto issue = [&](int stage, int k0) {
+#pragma unroll
+    for (int j = 0; j < IPW; ++j)
+      __builtin_amdgcn_global_load_lds((gptr_t)(src[j] + k0),
+                                       (lds_ptr_t)(lds + stage * FT::STAGE + (wid + NW * j) * 1024),
+                                       16, 0, 0);
+  };
+  f32x16_t acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+  const int nk = g.K / BK_;
+#pragma unroll
+  for (int p = 0; p < NS - 1; ++p)
+    if (p < nk) issue(p, p * BK_);
+  int st = 0;
+  for (int kt = 0; kt < nk; ++kt) {
+    if (kt + NS - 2 < nk) wait_vm<(NS - 2) * IPW>(); else wait_vm<0>();
+    __builtin_amdgcn_s_barrier();
+    if (kt + NS - 1 < nk) issue(st == 0 ? NS - 1 : st - 1, (kt + NS - 1) * BK_);
+    fast_compute<BM, BN, 2, 2, BK_>(lds + st * FT::STAGE, acc);
+    st = st == NS - 1 ? 0 : st + 1;
+  }
+  __syncthreads();
+  const int wr0 = (wid >> 1) * FT::WM, wc0 = (wid & 1) * WN;
+  const bool vec_out = g.ldo % 8 == 0 && ((uintptr_t)g.out & 15) == 0;
+  const bool vec_res = g.residual == nullptr || (g.ldr % 4 == 0 && ((uintptr_t)g.residual & 15) == 0);
+  float bb[8];
+  {
+    const int n = n0 + wc0 + (lane % (WN / 8)) * 8, nv = min(8, g.N - n);
+    if (g.bias && nv == 8 && ((uintptr_t)(g.bias + n) & 15) == 0) {
+      const float4 b0 = reinterpret_cast<const float4*>(g.bias + n)[0];
+      const float4 b1 = reinterpret_cast<const float4*>(g.bias + n)[1];
+      bb[0] = b0.x; bb[1] = b0.y; bb[2] = b0.z; bb[3] = b0.w;
+      bb[4] = b1.x; bb[5] = b1.y; bb[6] = b1.z; bb[7] = b1.w;
+    } else {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) bb[q] = (g.bias && q < nv) ? g.bias[n + q] : 0.f;
+    }
+  }
+  float* slab = reinterpret_cast<float*>(lds) + wid * 32 * WN;
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int mr0 = m0 + wr0 + i * 32, nc0 = n0 + wc0;
+    float4 res[WN / 16][2];
+    epi_res_load<WN>(g, mr0, nc0, vec_res, res);
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e)
+        slab[((e & 3) + 8 * (e >> 2) + 4 * (lane >> 5)) * WN + j * 32 + (lane & 31)] = acc[i][j][e];
+    switch (g.act) {
+      case ACT_GELU_ERF: epi_slab<ACT_GELU_ERF, WN>(g, slab, mr0, nc0, 0, vec_out, vec_res, bb, res); break;
+      case ACT_GELU_TANH: epi_slab<ACT_GELU_TANH, WN>(g, slab, mr0, nc0, 0, vec_out, vec_res, bb, res); break;
+      case ACT_RELU: epi_slab<ACT_RELU, WN>(g, slab, mr0, nc0, 0, vec_out, vec_res, bb, res); break;
+      case ACT_TANH: epi_slab<ACT_TANH, WN>(g, slab, mr0, nc0, 0, vec_out, vec_res, bb, res); break;
+      default: epi_slab<ACT_NONE, WN>(g, slab, mr0, nc0, 0, vec_out, vec_res, bb, res); break;
+    }
+  }
+}
+
+int g_gemm_lean = 1;   // zs_tune_set("gemm_lean", 0): decode-shaped GEMMs on gemm_fast_kernel
+
+template <int BM, int BN, int NS, int BK_>
+static int launch_lean(GemmArgs& g, hipStream_t st) {
+  hipLaunchKernelGGL((gemm_lean_kernel<BM, BN, NS, BK_>), dim3(cdiv(g.N, BN) * cdiv(g.M, BM)),
+                     dim3(256), 0, st, g);
+  ZS_LAUNCH_CHECK();
+  return 0;
+}
+
 int g_fast_persist = 1;   // zs_tune_set("fast_persist", 0): one workgroup per tile
 
 template <int BM, int BN, int NS, int WGM = 2, int WGN = 2, int BK_ = 64>
@@ -355,6 +477,18 @@ static int dispatch_fast(GemmArgs& g, hipStream_t st) {
     case 16: return launch_fast<128, 256, 2, 2, 4, 64>(g, st);
     case 17: return launch_fast<64, 64, 2, 2, 2, 128>(g, st);
     default: break;
+  }
+  if (g_gemm_lean && g.split_k == 1 && g.K % 64 == 0 && nblocks(g, 128, 128) <= 1536) {
+    // measured (tools/mbench.py decode_gemm, M = 1024 / 2048 / 4096 x the four decode shapes):
+    // 128x128 while it makes 1-2 tiles per 2-block CU slot, 128x64 beyond that and when 128x128
+    // leaves CUs idle, else 64x64 with a 4-deep ring
+    const int lt = g_fast_tile >= 100 ? g_fast_tile - 100 : 0;   // experiment: force a lean tile
+    const long n128 = nblocks(g, 128, 128);
+    if (lt == 1 || (!lt && n128 >= 256 && n128 <= 512)) return launch_lean<128, 128, 2, 64>(g, st);
+    if (lt == 2 || (!lt && nblocks(g, 128, 64) >= 256))
+      return g.M >= g.N ? launch_lean<128, 64, 3, 64>(g, st) : launch_lean<64, 128, 3, 64>(g, st);
+    if (lt == 3) return launch_lean<64, 64, 2, 128>(g, st);
+    return launch_lean<64, 64, 4, 64>(g, st);
   }
   if (nblocks(g, 128, 128) >= 256) {
     if (g_fast_ns == 3) return launch_fast<128, 128, 3>(g, st);

@@ -98,6 +98,11 @@ def lib():
                 fn = getattr(h, name)
                 fn.argtypes = args
                 fn.restype = C.c_int
+            # experiment knobs for A/B runs, e.g. ZSAAC_TUNE="gemm_lean=0,fast_xcd=0"
+            for kv in filter(None, os.environ.get("ZSAAC_TUNE", "").split(",")):
+                k, v = kv.split("=")
+                if h.zs_tune_set(k.strip().encode(), int(v)) != 0:
+                    raise ZsError(f"ZSAAC_TUNE: unknown knob {k!r}")
             _lib = h
     return _lib
 
