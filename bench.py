@@ -318,7 +318,7 @@ def main_embeddings(args, world, rank, device, pipe):
            "dtype": "bf16" if args.dtype == "bf16" else "f32",
            "data": "synthetic 10 s / 32 kHz waveforms (randn*0.1) resident in HBM; seeded weights",
            "config": {"workload": "C4 embedding extraction, RCCL all-gather of [N,1024] f32",
-                      "encoder_batch": args.batch, "batch_per_gpu": B, "global_batch": B * world,
+                      "encoder_batch": pipe.encoder.B, "batch_per_gpu": B, "global_batch": B * world,
                       "parallelism": f"dp{world} (clip-sharded)"}}
     if rank == 0:
         print(json.dumps(res), flush=True)
