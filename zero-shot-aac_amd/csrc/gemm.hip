@@ -478,13 +478,15 @@ static int dispatch_fast(GemmArgs& g, hipStream_t st) {
     case 17: return launch_fast<64, 64, 2, 2, 2, 128>(g, st);
     default: break;
   }
-  if (g_gemm_lean && g.split_k == 1 && g.K % 64 == 0 && nblocks(g, 128, 128) <= 1536) {
-    // measured (tools/mbench.py decode_gemm, M = 1024 / 2048 / 4096 x the four decode shapes):
-    // 128x128 while it makes 1-2 tiles per 2-block CU slot, 128x64 beyond that and when 128x128
-    // leaves CUs idle, else 64x64 with a 4-deep ring
+  if (g_gemm_lean && g.split_k == 1 && g.K % 64 == 0) {
+    // measured (tools/mbench.py decode_gemm / gemm_dbg; M = 1024..98304 x the GPT-2 and HTSAT
+    // shapes): 128x128 for big grids and while it makes 1-2 tiles per 2-block CU slot, 128x64
+    // in between (4096-row decode qkv: 28.9 vs 34.3 us) and when 128x128 leaves CUs idle, else
+    // 64x64 with a 4-deep ring
     const int lt = g_fast_tile >= 100 ? g_fast_tile - 100 : 0;   // experiment: force a lean tile
     const long n128 = nblocks(g, 128, 128);
-    if (lt == 1 || (!lt && n128 >= 256 && n128 <= 512)) return launch_lean<128, 128, 2, 64>(g, st);
+    if (lt == 1 || (!lt && (n128 > 1536 || (n128 >= 256 && n128 <= 512))))
+      return launch_lean<128, 128, 2, 64>(g, st);
     if (lt == 2 || (!lt && nblocks(g, 128, 64) >= 256))
       return g.M >= g.N ? launch_lean<128, 64, 3, 64>(g, st) : launch_lean<64, 128, 3, 64>(g, st);
     if (lt == 3) return launch_lean<64, 64, 2, 128>(g, st);
