@@ -326,7 +326,6 @@ template <int BM, int BN, int NS, int BK_>
 __global__ __launch_bounds__(256, 2) void gemm_lean_kernel(GemmArgs g) {
   using FT = FastTile<BM, BN, 2, 2, BK_>;
   constexpr int TM = FT::TM, TN = FT::TN, WN = FT::WN, NW = 4;
-  constexpr int IPW = FT::NI / NW;                 // DMA instructions per wave per stage
   static_assert(NW * 32 * WN * 4 <= NS * FT::STAGE, "epilogue slab fits the ring");
   __shared__ __attribute__((aligned(16))) char lds[NS * FT::STAGE];
   const int ntn = cdiv(g.N, BN), ntm = cdiv(g.M, BM), ntiles = ntn * ntm;
@@ -344,50 +343,9 @@ __global__ __launch_bounds__(256, 2) void gemm_lean_kernel(GemmArgs g) {
     n0 = (r / gs) * BN;
   }
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const bf16_t* src[IPW];
-  {
-    const int rsub = lane / FT::SPR, slot = lane % FT::SPR;
-#pragma unroll
-    for (int j = 0; j < IPW; ++j) {
-      const int i = wid + NW * j;                   // DMA instruction: rows RPI*i .. +RPI
-      const int row = FT::RPI * i + rsub;
-      const int c = 8 * (slot ^ FT::swz(row));
-      if (row < BM) {                               // wave-uniform (BM multiple of RPI*NW)
-        const int ar = min(m0 + row, g.M - 1);
-        src[j] = (const bf16_t*)g.A + (long)ar * g.lda + c;
-      } else {
-        const int wr = min(n0 + row - BM, g.N - 1);
-        src[j] = (const bf16_t*)g.W + (long)wr * g.ldw + c;
-      }
-    }
-  }
-  auto issue = [&](int stage, int k0) {
-#pragma unroll
-    for (int j = 0; j < IPW; ++j)
-      __builtin_amdgcn_global_load_lds((gptr_t)(src[j] + k0),
-                                       (lds_ptr_t)(lds + stage * FT::STAGE + (wid + NW * j) * 1024),
-                                       16, 0, 0);
-  };
   f32x16_t acc[TM][TN];
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j)
-#pragma unroll
-      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
-  const int nk = g.K / BK_;
-#pragma unroll
-  for (int p = 0; p < NS - 1; ++p)
-    if (p < nk) issue(p, p * BK_);
-  int st = 0;
-  for (int kt = 0; kt < nk; ++kt) {
-    if (kt + NS - 2 < nk) wait_vm<(NS - 2) * IPW>(); else wait_vm<0>();
-    __builtin_amdgcn_s_barrier();
-    if (kt + NS - 1 < nk) issue(st == 0 ? NS - 1 : st - 1, (kt + NS - 1) * BK_);
-    fast_compute<BM, BN, 2, 2, BK_>(lds + st * FT::STAGE, acc);
-    st = st == NS - 1 ? 0 : st + 1;
-  }
-  __syncthreads();
+  lean_mainloop<BM, BN, NS, 2, 2, BK_>((const bf16_t*)g.A, g.lda, g.M, m0, (const bf16_t*)g.W,
+                                      g.ldw, g.N, n0, g.K, lds, acc);
   const int wr0 = (wid >> 1) * FT::WM, wc0 = (wid & 1) * WN;
   const bool vec_out = g.ldo % 8 == 0 && ((uintptr_t)g.out & 15) == 0;
   const bool vec_res = g.residual == nullptr || (g.ldr % 4 == 0 && ((uintptr_t)g.residual & 15) == 0);
@@ -570,10 +528,18 @@ __global__ __launch_bounds__(256) void lmhead_kernel(int xcd_order, int M, int K
     const DenseRows rw{(const bf16_t*)W, K, V, n0};
 #pragma unroll
     for (int j = 0; j < BM / 64; ++j) ssq[j] = 0.f;
-    if (row_norm)
+    if (K % 64 == 0) {
+      if (row_norm)
+        lean_mainloop<LM_BN, BM, 2, 2, 2, 64, true>((const bf16_t*)W, K, V, n0, (const bf16_t*)A,
+                                                    lda, M, m0, K, smem_raw, acct, ssq);
+      else
+        lean_mainloop<LM_BN, BM, 2, 2, 2, 64>((const bf16_t*)W, K, V, n0, (const bf16_t*)A, lda,
+                                              M, m0, K, smem_raw, acct);
+    } else if (row_norm) {
       fast_mainloop<LM_BN, BM, 2, 2, 2, 64, true>(rw, ra, 0, K, smem_raw, acct, 0, ssq);
-    else
+    } else {
       fast_mainloop<LM_BN, BM>(rw, ra, 0, K, smem_raw, acct);
+    }
   } else {
     DenseA<T, BM> la{A, lda, M, m0};
     gemm_mainloop<T, BM, LM_BN>(la, W, K, V, n0, 0, K, (T*)smem_raw, acc);

@@ -192,4 +192,58 @@ __device__ __forceinline__ void fast_mainloop(
   __syncthreads();   // callers may reuse the LDS for the epilogue
 }
 
+// Lean variant of the ring (gemm_lean_kernel, lmhead_kernel): the per-lane DMA source pointers
+// of the tile's A rows [m0, m0+BM) and W rows [n0, n0+BN) are computed once (rows clamped into
+// the matrices; clamped rows only feed outputs the caller's store guard drops) and K % BK == 0,
+// so a k-step carries just the counted wait, the raw barrier, IPW pointer adds + DMAs and the
+// MFMAs (fast_mainloop's per-chunk zero-chunk selects and 64-bit row products are gone).
+template <int BM, int BN, int NS, int WGM, int WGN, int BK_, bool SSQ = false>
+__device__ __forceinline__ void lean_mainloop(
+    const bf16_t* A, int lda, int M, int m0, const bf16_t* W, int ldw, int N, int n0, int K,
+    char* lds,
+    f32x16_t (&acc)[FastTile<BM, BN, WGM, WGN, BK_>::TM][FastTile<BM, BN, WGM, WGN, BK_>::TN],
+    float* ssq = nullptr) {
+  using FT = FastTile<BM, BN, WGM, WGN, BK_>;
+  constexpr int NW = FT::NW, IPW = FT::NI / NW;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const bf16_t* src[IPW];
+  {
+    const int rsub = lane / FT::SPR, slot = lane % FT::SPR;
+#pragma unroll
+    for (int j = 0; j < IPW; ++j) {
+      const int i = wid + NW * j;                   // DMA instruction: rows RPI*i .. +RPI
+      const int row = FT::RPI * i + rsub;
+      const int c = 8 * (slot ^ FT::swz(row));
+      if (row < BM) src[j] = A + (long)min(m0 + row, M - 1) * lda + c;   // wave-uniform branch
+      else src[j] = W + (long)min(n0 + row - BM, N - 1) * ldw + c;
+    }
+  }
+  auto issue = [&](int stage, int k0) {
+#pragma unroll
+    for (int j = 0; j < IPW; ++j)
+      __builtin_amdgcn_global_load_lds((gptr_t)(src[j] + k0),
+                                       (lds_ptr_t)(lds + stage * FT::STAGE + (wid + NW * j) * 1024),
+                                       16, 0, 0);
+  };
+#pragma unroll
+  for (int i = 0; i < FT::TM; ++i)
+#pragma unroll
+    for (int j = 0; j < FT::TN; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+  const int nk = K / BK_;
+#pragma unroll
+  for (int p = 0; p < NS - 1; ++p)
+    if (p < nk) issue(p, p * BK_);
+  int st = 0;
+  for (int kt = 0; kt < nk; ++kt) {
+    if (kt + NS - 2 < nk) wait_vm<(NS - 2) * IPW>(); else wait_vm<0>();
+    __builtin_amdgcn_s_barrier();
+    if (kt + NS - 1 < nk) issue(st == 0 ? NS - 1 : st - 1, (kt + NS - 1) * BK_);
+    fast_compute<BM, BN, WGM, WGN, BK_, SSQ>(lds + st * FT::STAGE, acc, ssq);
+    st = st == NS - 1 ? 0 : st + 1;
+  }
+  __syncthreads();   // callers may reuse the LDS for the epilogue
+}
+
 }  // namespace zs
