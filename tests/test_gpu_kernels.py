@@ -192,6 +192,42 @@ def test_row_attention(cuda, causal, hd, L):
         assert _rel(got[valid], ref[valid]) < 1e-5
 
 
+@pytest.mark.parametrize("causal,L", [(True, 27), (False, 32), (True, 5), (True, 32)])
+def test_row_attention_bf16_mfma(cuda, causal, L):
+    """bf16, head dim 64, L <= 32: the MFMA row attention (GPT-2 prompt prefill) against the fp32
+    reference of the same bf16 inputs (bf16 P / output rounding: 2e-2) and the scalar kernel."""
+    from zsaac import ops
+    from zsaac._lib import call
+    B, H, hd = 5, 12, 64
+    D = H * hd
+    g = torch.Generator(device="cuda").manual_seed(L)
+    q = torch.randn(B * L, D, device=cuda, generator=g).bfloat16()
+    kv = torch.randn(B * L, 2 * D, device=cuda, generator=g).bfloat16()
+    lens = torch.tensor([L, max(1, L - 5), min(3, L), 1, L], device=cuda, dtype=torch.int32)
+    scale = hd ** -0.5
+    outs = []
+    for mode in (1, 0):
+        call("zs_tune_set", b"row_mfma", mode)
+        out = torch.zeros(B * L, D, device=cuda, dtype=torch.bfloat16)
+        ops.row_attention(q, D, kv, kv[:, D:], 2 * D, B, L, H, hd, causal, scale, out, D, lens=lens)
+        outs.append(out.float())
+    call("zs_tune_set", b"row_mfma", 1)
+    qh = q.float().view(B, L, H, hd).transpose(1, 2)
+    kh = kv[:, :D].float().reshape(B, L, H, hd).transpose(1, 2)
+    vh = kv[:, D:].float().reshape(B, L, H, hd).transpose(1, 2)
+    s = (qh @ kh.transpose(-1, -2)) * scale
+    for b in range(B):
+        n = int(lens[b])
+        mask = torch.ones(L, L, dtype=torch.bool, device=cuda)
+        mask[:, n:] = False
+        if causal:
+            mask &= torch.ones(L, L, dtype=torch.bool, device=cuda).tril()
+        ref = (s[b].masked_fill(~mask, float("-inf")).softmax(-1) @ vh[b]).transpose(0, 1).reshape(L, D)
+        valid = torch.arange(L, device=cuda) < (n if causal else L)
+        assert _rel(outs[0].view(B, L, D)[b][valid], ref[valid]) < 2e-2
+        assert _rel(outs[0].view(B, L, D)[b][valid], outs[1].view(B, L, D)[b][valid]) < 2e-2
+
+
 def test_decode_attention_matches_prefill(cuda):
     """KV-cache decode of the last token == causal prefill row attention of that token."""
     from zsaac import ops

@@ -291,6 +291,115 @@ __global__ __launch_bounds__(64) void row_attn_kernel(const T* __restrict__ q, i
   for (int d = 0; d < HD; ++d) stf(orow + d, o[d] * inv);
 }
 
+// MFMA row attention for short rows (bf16, head dim 64, L <= 32: the GPT-2 prompt prefill, P =
+// hard prompt + 10 soft tokens <= 27): one wave per (row, head), 4 per block.
+//   S^T[key][query] = K . Q^T   4 x v_mfma_f32_32x32x16_bf16 (head dim in 16-deep steps), both
+//                               operands loaded straight from global as 16-byte fragments
+//   mask (key < len, causal key <= query), scale, f32 softmax over keys per query column (a lane
+//   holds 16 of its query's 32 keys, the other 16 sit in lane ^ 32)
+//   O^T[dim][query] = V^T . P^T 2 dim tiles x 2 key steps; P^T straight from the S^T accumulators
+//                               (bf16), V^T staged in LDS (swizzled 4-key chunks, 8-byte reads)
+// The scalar row_attn_kernel (one thread per query, 64-dim dot products from LDS) ran ~4k VALU
+// instructions per thread for what is 8 MFMAs per wave here.
+constexpr int RA_NW = 4;
+__global__ __launch_bounds__(64 * RA_NW) void row_attn_mfma_kernel(
+    const bf16_t* __restrict__ q, int ldq, const bf16_t* __restrict__ k,
+    const bf16_t* __restrict__ v, int ldkv, int L, const int* __restrict__ lens, int causal,
+    float scale, bf16_t* __restrict__ out, int ldo, int B, int heads) {
+  __shared__ __attribute__((aligned(16))) bf16_t sVt[RA_NW][64 * 32];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int item = blockIdx.x * RA_NW + wv;
+  if (item >= B * heads) return;
+  const int b = item / heads, hh = item % heads;
+  const int len = lens ? lens[b] : L;
+  const int r = lane & 31, h = lane >> 5;
+  bf16_t* Vt = sVt[wv];
+  // V^T [dim][key]: element (d, key j) at d*32 + 4*((j >> 2) ^ (d & 7)) + (j & 3)
+#pragma unroll
+  for (int it = 0; it < 4; ++it) {
+    const int j = 8 * it + (lane >> 3), d0 = 8 * (lane & 7);
+    uint4 u = make_uint4(0, 0, 0, 0);
+    if (j < L) u = *reinterpret_cast<const uint4*>(v + ((long)b * L + j) * ldkv + hh * 64 + d0);
+    const bf16_t* e = reinterpret_cast<const bf16_t*>(&u);
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+      const int d = d0 + t;
+      Vt[d * 32 + 4 * ((j >> 2) ^ (d & 7)) + (j & 3)] = e[t];
+    }
+  }
+  // S^T = K . Q^T over the 64 head dims
+  wa_f32x16_t st;
+#pragma unroll
+  for (int e = 0; e < 16; ++e) st[e] = 0.f;
+  const bf16_t* krow = k + ((long)b * L + r) * ldkv + hh * 64 + 8 * h;
+  const bf16_t* qrow = q + ((long)b * L + r) * ldq + hh * 64 + 8 * h;
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) {
+    uint4 ku = make_uint4(0, 0, 0, 0), qu = make_uint4(0, 0, 0, 0);
+    if (r < L) {
+      ku = *reinterpret_cast<const uint4*>(krow + 16 * ks);
+      qu = *reinterpret_cast<const uint4*>(qrow + 16 * ks);
+    }
+    st = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(wa_bf16x8_t, ku),
+                                                  __builtin_bit_cast(wa_bf16x8_t, qu), st, 0, 0, 0);
+  }
+  // softmax over the keys of query column r
+  float mx = -INFINITY;
+#pragma unroll
+  for (int e = 0; e < 16; ++e) {
+    const int j = (e & 3) + 8 * (e >> 2) + 4 * h;
+    const bool ok = j < len && (!causal || j <= r);
+    st[e] = ok ? st[e] * scale : -INFINITY;
+    mx = fmaxf(mx, st[e]);
+  }
+  mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+  float sum = 0.f;
+#pragma unroll
+  for (int e = 0; e < 16; ++e) {
+    const float p = st[e] == -INFINITY ? 0.f : __expf(st[e] - mx);
+    st[e] = p;
+    sum += p;
+  }
+  sum += __shfl_xor(sum, 32, 64);
+  // V^T is private to this wave and a wave's LDS accesses complete in issue order: no barrier
+  wa_bf16x8_t pb[2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int u = 0; u < 8; ++u) pb[t][u] = (__bf16)st[8 * t + u];
+  const float inv = sum > 0.f ? 1.0f / sum : 0.f;
+  typedef __attribute__((ext_vector_type(4))) __bf16 ra_bf16x4_t;
+#pragma unroll
+  for (int dt = 0; dt < 2; ++dt) {
+    wa_f32x16_t ot;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) ot[e] = 0.f;
+    const int d = 32 * dt + r;
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int k0 = 16 * t + 4 * h;
+      const ra_bf16x4_t lo = *reinterpret_cast<const ra_bf16x4_t*>(Vt + d * 32 + 4 * ((k0 >> 2) ^ (d & 7)));
+      const ra_bf16x4_t hi = *reinterpret_cast<const ra_bf16x4_t*>(Vt + d * 32 + 4 * (((k0 + 8) >> 2) ^ (d & 7)));
+      wa_bf16x8_t va;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) { va[u] = lo[u]; va[4 + u] = hi[u]; }
+      ot = __builtin_amdgcn_mfma_f32_32x32x16_bf16(va, pb[t], ot, 0, 0, 0);
+    }
+    if (r < L) {
+      bf16_t* orow = out + ((long)b * L + r) * ldo + hh * 64 + 32 * dt;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {      // dims 8 g + 4 h .. +3 of this tile
+        uint2 u;
+        u.x = (uint32_t)f2bf(ot[4 * g] * inv) | ((uint32_t)f2bf(ot[4 * g + 1] * inv) << 16);
+        u.y = (uint32_t)f2bf(ot[4 * g + 2] * inv) | ((uint32_t)f2bf(ot[4 * g + 3] * inv) << 16);
+        *reinterpret_cast<uint2*>(orow + 8 * g + 4 * h) = u;
+      }
+    }
+  }
+}
+
+int g_row_mfma = 1;   // zs_tune_set("row_mfma", 0): the scalar row_attn_kernel for bf16 too
+
 // ------------------------------------------------------------------ GPT-2 decode attention
 // grid (R, heads), block 256 (hd == 64): append k/v of the new token at pos[r], then attend
 // 0..pos[r].  The row's K block ([pos][64], contiguous per (row, head) in the cache) is staged
@@ -710,6 +819,14 @@ extern "C" int zs_row_attention(const void* q, int ldq, const void* k, const voi
   ZS_REQUIRE(smem <= 160 * 1024, "zs_row_attention: L*hd too large for LDS");
   dim3 grid(B, heads, cdiv(L, 64));
   hipStream_t st = S(stream);
+  if (g_row_mfma && dtype == ZS_BF16 && hd == 64 && L <= 32 && ldq % 8 == 0 && ldkv % 8 == 0 &&
+      ldo % 4 == 0) {
+    hipLaunchKernelGGL(row_attn_mfma_kernel, dim3(cdiv((long)B * heads, RA_NW)), dim3(64 * RA_NW), 0,
+                       st, (const bf16_t*)q, ldq, (const bf16_t*)k, (const bf16_t*)v, ldkv, L, len,
+                       causal, scale, (bf16_t*)out, ldo, B, heads);
+    ZS_LAUNCH_CHECK();
+    return 0;
+  }
 #define RA(T, HD_)                                                                              \
   hipLaunchKernelGGL((row_attn_kernel<T, HD_>), grid, dim3(64), smem, st, (const T*)q, ldq,       \
                      (const T*)k, (const T*)v, ldkv, L, len, causal, scale, (T*)out, ldo)

@@ -140,8 +140,8 @@ struct SwinCfg {
   static constexpr int NCH = 4 * C / HC;
   static constexpr int NTP = C / 16;         // n-tiles of proj / fc2
   static constexpr int NTW = (NTP + NW - 1) / NW;   // per wave (max)
-  static constexpr int DA = C <= 96 ? 3 : 2;   // weight pipe depth (k-steps): qkv / fc1
-  static constexpr int DB = C <= 96 ? 3 : 2;   // proj / fc2
+  static constexpr int DA = (C <= 96 || C >= 384) ? 3 : 2;   // weight pipe depth (k-steps): qkv / fc1
+  static constexpr int DB = (C <= 96 || C >= 384) ? 3 : 2;   // proj / fc2
   static constexpr int SZ_H = 64 * LD * 2;
   static constexpr int OFF_H = 0, OFF_ATT = SZ_H, OFF_QKV = 2 * SZ_H;
   static constexpr int SZ_QKV = 3 * G * 64 * 32 * 2;   // Qs[G][64][32], Ks[G][64][32], Vt[G][32][64]
