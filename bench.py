@@ -228,7 +228,7 @@ def stage_times(pipe, wav, reps=3):
         ops.prefill_embed(pipe.hard_ids[:B], pipe.hard_len[:B], soft, pipe.mapper.soft_ld,
                           cfg.prefix_length, pipe.gpt.wte, pipe.gpt.wpe, B, Pmax,
                           pipe.embed[:B * Pmax], dec.x, dec.plen, dec.last_row)
-        dec.prefix_tokens(pipe.embed[:B * Pmax], pipe.prefix_ids[:B * Pmax])
+        pipe.prefix_tokens(B, soft)
         dec.prefill(B, Pmax)
         ev[2].record()
         dec.greedy(B, Pmax)

@@ -224,6 +224,15 @@ int zs_lmhead_nblk(int V);
 int zs_argmax_finalize(const float* part_val, const int* part_idx, int M, int nblk, int* idx,
                        void* stream);
 
+/* zs_prefix_ids_assemble: get_prefix_tokens (gpt2_prefix_eval.py:271-278) with the argmax run
+ * only over the soft-prompt rows: out[b][p] = hard_ids[b][p] for p < hard_len[b] (a hard row is
+ * wte[id] and its own cosine is the maximum — the caller verifies that every possible hard id
+ * beats every other vocabulary row by a margin before taking this path), soft_idx[b][p - H_b]
+ * for the n_soft rows after it, 0 for padding rows (zero embeddings: all cosines 0).
+ * hard_ids [B][h_cap], soft_idx [B][n_soft], out [B][Pmax] int32. */
+int zs_prefix_ids_assemble(const int* hard_ids, int h_cap, const int* hard_len, const int* soft_idx,
+                           int n_soft, int B, int Pmax, int* out, void* stream);
+
 /* zs_greedy_step: generate2's per-step bookkeeping (gpt2_prefix_eval.py:208-215) for R rows:
  * tok = argmax(partials); rows already done keep emitting nothing; out_ids[r][step] = tok,
  * out_len[r] = step+1 while not done; done |= tok in {stop0, stop1}; pos[r] += 1 (next position);

@@ -71,6 +71,33 @@ def test_c1_greedy_f32_bit_exact(cuda, golden, caption_sd):
     assert not mism, f"greedy mismatch on clips {mism}"
 
 
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_prefix_tokens_soft_rows_equal_full(cuda, golden, caption_sd, dtype):
+    """get_prefix_tokens over the soft rows + hard ids (zs_prefix_ids_assemble) gives exactly the
+    ids of the cosine argmax over every prefix row; the margin check passes for these weights."""
+    g = golden("c1_greedy.npz")
+    pipe = _pipeline(caption_sd, dtype, 50)
+    assert pipe.hard_skip
+    out = pipe.caption_emb(torch.from_numpy(g["clap_emb"]).to(cuda))
+    fast = out.prefix_ids.clone()
+    full = torch.zeros_like(pipe.prefix_ids[:50 * pipe.Pmax])
+    pipe.decoder.prefix_tokens(pipe.embed[:50 * pipe.Pmax], full)
+    full = full.view(50, pipe.Pmax)
+    pl = out.plen.cpu().numpy()
+    for b in range(50):
+        assert fast[b, :pl[b]].tolist() == full[b, :pl[b]].tolist(), b
+    # an id whose own row is NOT its cosine argmax (a duplicated wte row) disables the shortcut
+    w = pipe.gpt.wte
+    saved = w[5].clone()
+    w[5].copy_(w[7])
+    pipe.gpt.wte_norm[5].copy_(pipe.gpt.wte_norm[7])
+    try:
+        assert not pipe.decoder.hard_rows_safe([5, 11], 1e-4)
+    finally:
+        w[5].copy_(saved)
+        pipe.gpt.wte_norm[5].copy_(torch.nn.functional.normalize(saved.float(), dim=0).to(w.dtype))
+
+
 def test_concurrent_runner_f32_bit_exact(cuda, golden, caption_sd):
     """3 pipeline twins in flight on separate streams, 7 batches of <=8 clips (ragged last batch
     of 2): every clip's generate2 ids still equal the reference's, in input order."""

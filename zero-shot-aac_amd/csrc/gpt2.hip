@@ -484,6 +484,30 @@ extern "C" int zs_compact_rows(const int* done, int nrows, int* rowmap, int* n_a
   return 0;
 }
 
+// get_prefix_tokens over the soft rows only (see zs_prefix_ids_assemble): row b, position p of
+// the [B][Pmax] result = the hard id (p < H_b), the soft-row argmax (H_b <= p < H_b + n_soft) or
+// 0 (padding: a zero embedding row's cosines are all 0, argmax = index 0)
+__global__ void prefix_ids_kernel(const int* __restrict__ hard_ids, int h_cap,
+                                  const int* __restrict__ hard_len, const int* __restrict__ soft_idx,
+                                  int n_soft, int B, int Pmax, int* __restrict__ out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= B * Pmax) return;
+  const int b = i / Pmax, p = i % Pmax, H = hard_len[b];
+  out[i] = p < H ? hard_ids[(long)b * h_cap + p]
+                 : (p < H + n_soft ? soft_idx[(long)b * n_soft + p - H] : 0);
+}
+
+extern "C" int zs_prefix_ids_assemble(const int* hard_ids, int h_cap, const int* hard_len,
+                                      const int* soft_idx, int n_soft, int B, int Pmax, int* out,
+                                      void* stream) {
+  ZS_REQUIRE(B > 0 && Pmax > 0 && h_cap >= 0 && n_soft >= 0 && h_cap + n_soft <= Pmax,
+             "zs_prefix_ids_assemble: bad shape");
+  hipLaunchKernelGGL(prefix_ids_kernel, dim3(cdiv((long)B * Pmax, 256)), dim3(256), 0, S(stream),
+                     hard_ids, h_cap, hard_len, soft_idx, n_soft, B, Pmax, out);
+  ZS_LAUNCH_CHECK();
+  return 0;
+}
+
 extern "C" int zs_argmax_finalize(const float* part_val, const int* part_idx, int M, int nblk,
                                   int* idx, void* stream) {
   ZS_REQUIRE(M > 0 && nblk > 0, "zs_argmax_finalize: bad shape");

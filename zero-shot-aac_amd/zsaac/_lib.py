@@ -60,6 +60,7 @@ SIGNATURES = {
     "zs_lmhead_topk": [I, I, I, I, P, I, P, I, I, P, P, P, P],
     "zs_lmhead_nblk": [I],
     "zs_argmax_finalize": [P, P, I, I, P, P],
+    "zs_prefix_ids_assemble": [P, I, P, P, I, I, I, P, P],
     "zs_greedy_step": [P, P, I, I, P, I, I, I, P, P, P, P, P, P, P],
     "zs_beam_step": [P, P, P, I, I, I, I, I, I, P, I, P, P, P, P, P, P, P, I, P, P, P, P],
 }

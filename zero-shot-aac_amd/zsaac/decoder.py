@@ -496,6 +496,42 @@ class Gpt2Decoder:
         ops.argmax_finalize(self._pv_big, self._pi_big, M, self.nblk, out_idx)
         return out_idx
 
+    def prefix_tokens_soft(self, soft_rows: torch.Tensor, hard_ids: torch.Tensor,
+                           hard_len: torch.Tensor, B: int, Pmax: int, out_idx: torch.Tensor):
+        """get_prefix_tokens with the cosine argmax over the soft-prompt rows only
+        (``soft_rows`` [B * n_soft, 768] f32, contiguous): a hard row is wte[id], whose own
+        cosine is the maximum whenever :meth:`hard_rows_safe` holds for every possible id, so its
+        result is the id itself (zs_prefix_ids_assemble)."""
+        M = soft_rows.shape[0]
+        n_soft = M // B
+        a = self.h[:M]
+        ops.cast(soft_rows, a)
+        ops.lmhead_topk(a, self.w.wte_norm, 1, None, self.pval_big(M), self.pidx_big(M),
+                        row_norm=True)
+        if getattr(self, "_soft_idx", None) is None or self._soft_idx.numel() < M:
+            self._soft_idx = torch.empty(M, device=self.dev, dtype=torch.int32)
+        ops.argmax_finalize(self._pv_big, self._pi_big, M, self.nblk, self._soft_idx)
+        return ops.prefix_ids_assemble(hard_ids, hard_len, self._soft_idx, n_soft, B, Pmax, out_idx)
+
+    def hard_rows_safe(self, ids, margin) -> bool:
+        """True when for every token id in ``ids`` the cosine argmax of the row wte[id] against
+        normalize(wte) — computed by the same LM-head kernel get_prefix_tokens uses — is id
+        itself, ahead of every other vocabulary row by more than ``margin``."""
+        ids = torch.as_tensor(sorted(set(int(i) for i in ids)), device=self.dev, dtype=torch.long)
+        C = ids.numel()
+        if C == 0:
+            return True
+        a = self.w.wte.index_select(0, ids).contiguous()
+        pv = torch.empty(C, self.nblk, 2, device=self.dev)
+        pi = torch.empty(C, self.nblk, 2, device=self.dev, dtype=torch.int32)
+        ops.lmhead_topk(a, self.w.wte_norm, 2, None, pv, pi, row_norm=True)
+        v, i = pv.view(C, -1), pi.view(C, -1).long()
+        own = i == ids[:, None]
+        neg = torch.full_like(v, -float("inf"))
+        best_own = torch.where(own, v, neg).amax(1)
+        best_other = torch.where(own, neg, v).amax(1)
+        return bool(((best_own - best_other) > margin).all())
+
     def _ensure_big(self, M):
         if getattr(self, "_big_M", 0) < M:
             self._ps_big = torch.empty(M, self.nblk, 2, device=self.dev)

@@ -306,6 +306,13 @@ def argmax_finalize(part_val, part_idx, M, nblk, idx):
     return idx
 
 
+def prefix_ids_assemble(hard_ids, hard_len, soft_idx, n_soft, B, Pmax, out):
+    _i32(hard_ids, "hard_ids"), _i32(hard_len, "hard_len"), _i32(soft_idx, "soft_idx"), _i32(out, "out")
+    call("zs_prefix_ids_assemble", _p(hard_ids), hard_ids.shape[-1], _p(hard_len), _p(soft_idx),
+         n_soft, B, Pmax, _p(out), _s())
+    return out
+
+
 def greedy_step(part_val, part_idx, R, nblk, step_ctr, max_steps, stop0, stop1, out_ids, out_len,
                 done, pos, next_tok, all_done):
     call("zs_greedy_step", _p(part_val), _p(part_idx), R, nblk, _p(step_ctr), max_steps, stop0,

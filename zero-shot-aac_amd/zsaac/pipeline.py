@@ -79,6 +79,11 @@ class CaptionBatch:
         return [pid[b, :pl[b]].tolist() for b in range(pid.shape[0])]
 
 
+# token ids prompt_kernel (csrc/gpt2.hip) writes around the labels: "There", " are",
+# " something", ",", " in", " this", " audio", "."
+PROMPT_TEMPLATE_IDS = (1858, 389, 1223, 11, 287, 428, 6597, 13)
+
+
 class CaptionPipeline:
     """Weights from reference-keyed state dicts; all buffers sized for ``cfg.batch`` clips."""
 
@@ -96,6 +101,12 @@ class CaptionPipeline:
         self.gpt = Gpt2Weights(caption_sd, dev, cfg.dtype)
         self._setup_tables(label_table, label_tokens)
         self._alloc()
+        # get_prefix_tokens on the soft rows only when every id a hard prompt can hold (the
+        # template tokens of prompt_kernel, gpt2.hip, and the label table's tokens) is its own
+        # cosine argmax by a margin above the dtype's rounding (bf16 2e-2, f32 1e-4)
+        cand = list(PROMPT_TEMPLATE_IDS) + [t for toks in label_tokens for t in toks]
+        margin = 2e-2 if cfg.dtype == torch.bfloat16 else 1e-4
+        self.hard_skip = cfg.prefix_tokens and self.decoder.hard_rows_safe(cand, margin)
 
     def twin(self) -> "CaptionPipeline":
         """A pipeline sharing every packed weight with this one but owning its activation
@@ -172,6 +183,17 @@ class CaptionPipeline:
         return CaptionBatch(ids, ln, sc, self.hard_ids[:B], self.hard_len[:B], dec.plen[:B], pid,
                             self._emb)
 
+    def prefix_tokens(self, B: int, soft: torch.Tensor):
+        """get_prefix_tokens ids of the current batch into prefix_ids (after prefill_embed)."""
+        n, Pmax, dec = self.cfg.prefix_length, self.Pmax, self.decoder
+        if (self.hard_skip and self.mapper.soft_ld == n * 768 and soft.is_contiguous()
+                and soft.dtype == torch.float32):
+            dec.prefix_tokens_soft(soft.reshape(-1)[:B * n * 768].view(B * n, 768),
+                                   self.hard_ids[:B], self.hard_len[:B], B, Pmax,
+                                   self.prefix_ids[:B * Pmax])
+        else:
+            dec.prefix_tokens(self.embed[:B * Pmax], self.prefix_ids[:B * Pmax])
+
     def begin_emb(self, emb: torch.Tensor):
         """Enqueue prompt assembly, mapper, prefill, get_prefix_tokens and decode step 0 for a
         batch of CLAP embeddings, without any host synchronisation."""
@@ -191,7 +213,7 @@ class CaptionPipeline:
                           cfg.prefix_length, self.gpt.wte, self.gpt.wpe, B, Pmax,
                           self.embed[:B * Pmax], dec.x, dec.plen, dec.last_row)
         if cfg.prefix_tokens:
-            dec.prefix_tokens(self.embed[:B * Pmax], self.prefix_ids[:B * Pmax])
+            self.prefix_tokens(B, soft)
         if cfg.beam:
             dec.prefill(B, Pmax, row_stride=cfg.beam)
             dec.beam_begin(B, cfg.beam)
