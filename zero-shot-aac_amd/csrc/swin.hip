@@ -146,8 +146,7 @@ struct SwinCfg {
   static constexpr int OFF_H = 0, OFF_ATT = SZ_H, OFF_QKV = 2 * SZ_H;
   static constexpr int SZ_QKV = 3 * G * 64 * 32 * 2;   // Qs[G][64][32], Ks[G][64][32], Vt[G][32][64]
   static constexpr int OFF_BT = OFF_QKV + SZ_QKV;      // [G][225] f32
-  static constexpr int OFF_RG = OFF_BT + ((G * 225 * 4 + 15) & ~15);   // [64] int8 mask regions
-  static constexpr int OFF_ROW = OFF_RG + 64;          // [64] int token rows
+  static constexpr int OFF_ROW = OFF_BT + ((G * 225 * 4 + 15) & ~15);  // [64] int token rows
   static constexpr int LDS = OFF_ROW + 256;
   static constexpr int LDX = C + 4;                    // final f32 staging [64][C+4]
   static_assert(64 * LDX * 4 <= LDS, "output staging fits");
@@ -157,7 +156,7 @@ struct SwinCfg {
   static_assert(C % 96 == 0 && NH % G == 0 && (4 * C) % HC == 0 && C % (16 * NW / 4) == 0, "C");
 };
 
-template <int C>
+template <int C, bool SH>   // SH: shifted windows (shift = ws / 2 = 4, odd blocks)
 __global__ __launch_bounds__(64 * SwinCfg<C>::NW, 2) void swin_block_kernel(SwinArgs g) {
   using CF = SwinCfg<C>;
   constexpr int LD = CF::LD, NTW = CF::NTW, NTP = CF::NTP, KS = C / 32, NW = CF::NW, G = CF::G;
@@ -169,7 +168,6 @@ __global__ __launch_bounds__(64 * SwinCfg<C>::NW, 2) void swin_block_kernel(Swin
   bf16_t* sK = sQ + G * 64 * 32;
   bf16_t* sVt = sK + G * 64 * 32;
   float* sBt = reinterpret_cast<float*>(lds + CF::OFF_BT);
-  signed char* sRg = reinterpret_cast<signed char*>(lds + CF::OFF_RG);
   int* sRow = reinterpret_cast<int*>(lds + CF::OFF_ROW);
 
   const int tid = threadIdx.x, l = tid & 63, w = tid >> 6;
@@ -177,7 +175,8 @@ __global__ __launch_bounds__(64 * SwinCfg<C>::NW, 2) void swin_block_kernel(Swin
   WPipe<3, DA> pa;        // qkv / fc1 weight fragments in flight
   WPipe<NTW, DB> pb;      // proj / fc2
   wp_prefetch<3, 3 * NW, DA, NW>(pa, g.wqkv, KS, 0, w);
-  const int H = g.H, W = g.W, shift = g.shift;
+  const int H = g.H, W = g.W;
+  constexpr int shift = SH ? 4 : 0;
   const int nWw = W / 8, nWh = H / 8;
   const int win = blockIdx.x;
   const int b = win / (nWh * nWw), wyx = win % (nWh * nWw), wy = wyx / nWw, wx = wyx % nWw;
@@ -190,16 +189,7 @@ __global__ __launch_bounds__(64 * SwinCfg<C>::NW, 2) void swin_block_kernel(Swin
     const int sy = wy * 8 + (t >> 3), sx = wx * 8 + (t & 7);     // rolled coords
     const int hh = (sy + shift) % H, ww = (sx + shift) % W;      // natural (roll(-shift))
     const int row = (b * H + hh) * W + ww;
-    if (q == 0) {
-      sRow[t] = row;
-      int reg = 0;
-      if (shift > 0) {
-        const int ry = sy < H - 8 ? 0 : (sy < H - shift ? 1 : 2);
-        const int rx = sx < W - 8 ? 0 : (sx < W - shift ? 1 : 2);
-        reg = ry * 3 + rx;
-      }
-      sRg[t] = (signed char)reg;
-    }
+    if (q == 0) sRow[t] = row;
     const float4* xr = reinterpret_cast<const float4*>(g.x + (long)row * C);
     float4 v[NQ];
     float s = 0.f;
@@ -309,7 +299,7 @@ __global__ __launch_bounds__(64 * SwinCfg<C>::NW, 2) void swin_block_kernel(Swin
         }
       }
       const float scale = 0.20412414523193148f;    // 24 ** -0.5 (htsat.py:285, 320)
-      const int qi = 32 * qb + r32, qy = qi >> 3, qx = qi & 7, qreg = sRg[qi];
+      const int qi = 32 * qb + r32, qy = qi >> 3, qx = qi & 7;
       // key of register e of block kb: kj = 32 kb + (e & 3) + 8 (e >> 2) + 4 h2, i.e. key row
       // ky = 4 kb + (e >> 2), key column kx = 4 h2 + (e & 3): the bias index
       // (qy - ky + 7) * 15 + (qx - kx + 7) is a per-lane base minus a compile-time constant, so
@@ -320,7 +310,7 @@ __global__ __launch_bounds__(64 * SwinCfg<C>::NW, 2) void swin_block_kernel(Swin
       // (ky >= 4) == kb and its region column (kx >= 4) == h2, so the mask is per (lane, kb)
       const bool lastr = wy == nWh - 1, lastc = wx == nWw - 1;
       float mk[2] = {0.f, 0.f};
-      if (shift == 4) {
+      if (SH) {
 #pragma unroll
         for (int kb = 0; kb < 2; ++kb)
           mk[kb] = ((lastr && kb != (qy >= 4)) || (lastc && h2 != (qx >= 4))) ? -100.0f : 0.f;
@@ -333,10 +323,6 @@ __global__ __launch_bounds__(64 * SwinCfg<C>::NW, 2) void swin_block_kernel(Swin
           float v = st[kb][e] * scale;
           if (!(g.dbg & 2)) {
             v += bt0[108 - 15 * (4 * kb + (e >> 2)) - (e & 3)] + mk[kb];
-            if (shift > 0 && shift != 4) {
-              const int kj = 32 * kb + (e & 3) + 8 * (e >> 2) + 4 * h2;
-              if (sRg[kj] != qreg) v += -100.0f;
-            }
           }
           st[kb][e] = v;
           mx = fmaxf(mx, v);
@@ -548,16 +534,19 @@ extern "C" int zs_swin_block(float* x, int B, int H, int W, int C, int heads, in
              "zs_swin_block: H, W multiples of 8 (window 8)");
   ZS_REQUIRE((C == 96 || C == 192 || C == 384) && heads * 24 == C,
              "zs_swin_block: C in {96,192,384}, head dim 24 (C=%d heads=%d)", C, heads);
-  ZS_REQUIRE(shift >= 0 && shift < 8, "zs_swin_block: shift");
+  ZS_REQUIRE(shift == 0 || shift == 4, "zs_swin_block: shift must be 0 or ws/2 = 4");
   ZS_REQUIRE((long)B * H * W <= (1L << 31) - 1, "zs_swin_block: too many tokens");
   SwinArgs a{x, H, W, shift, ln1_w, ln1_b, (const uint4*)wqkv_packed, bqkv_packed, rel_table,
              (const uint4*)wproj_packed, bproj, ln2_w, ln2_b, (const uint4*)w1_packed, b1,
              (const uint4*)w2_packed, b2, g_swin_dbg};
   dim3 grid(B * (H / 8) * (W / 8));
   hipStream_t st = S(stream);
-  if (C == 96) hipLaunchKernelGGL(swin_block_kernel<96>, grid, dim3(64 * SwinCfg<96>::NW), 0, st, a);
-  else if (C == 192) hipLaunchKernelGGL(swin_block_kernel<192>, grid, dim3(64 * SwinCfg<192>::NW), 0, st, a);
-  else hipLaunchKernelGGL(swin_block_kernel<384>, grid, dim3(64 * SwinCfg<384>::NW), 0, st, a);
+#define SWL(C_, SH_) \
+  hipLaunchKernelGGL((swin_block_kernel<C_, SH_>), grid, dim3(64 * SwinCfg<C_>::NW), 0, st, a)
+  if (C == 96) { if (shift) SWL(96, true); else SWL(96, false); }
+  else if (C == 192) { if (shift) SWL(192, true); else SWL(192, false); }
+  else { if (shift) SWL(384, true); else SWL(384, false); }
+#undef SWL
   ZS_LAUNCH_CHECK();
   return 0;
 }
