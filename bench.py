@@ -56,12 +56,13 @@ def parse():
     ap.add_argument("--entry-length", type=int, default=67)
     ap.add_argument("--encoder-batch", type=int, default=256,
                     help="clips per encoder pass (0 = --batch); per-clip results do not depend on it")
-    ap.add_argument("--group", type=int, default=64,
+    ap.add_argument("--group", type=int, default=128,
                     help="eval batches of --batch clips decoded together (one decode step over "
-                         "group*batch rows; 64 -> 4096 rows: 11.4k vs 10.9k clips/s at 32); "
-                         "encoded --encoder-batch clips per pass")
-    ap.add_argument("--inflight", type=int, default=3,
-                    help="independent bs=--batch batches decoding concurrently per GPU (streams)")
+                         "group*batch rows; measured 32 -> 64 -> 128: 10.9k -> 12.1k -> 12.3k "
+                         "clips/s); encoded --encoder-batch clips per pass")
+    ap.add_argument("--inflight", type=int, default=2,
+                    help="independent groups in flight per GPU, each on its own HIP stream "
+                         "(2 and 3 measure the same at group 128; 1: -11 %%)")
     ap.add_argument("--compact", type=int, default=1,
                     help="greedy bf16: decode only the rows that have not stopped (0 = all rows)")
     ap.add_argument("--cpu-baseline-clips", type=int, default=2)

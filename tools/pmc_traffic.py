@@ -28,8 +28,8 @@ def run():
     import torch
     import bench
 
-    class A:       # bench.py defaults: eval batch 64, group 64 -> 4096 decode rows
-        batch, group, dtype, encoder, mapper, beam, entry_length = 64, 64, "bf16", "htsat", "mlp", 0, 67
+    class A:       # bench.py defaults: eval batch 64, group 128 -> 8192 decode rows
+        batch, group, dtype, encoder, mapper, beam, entry_length = 64, 128, "bf16", "htsat", "mlp", 0, 67
     pipe, _, _ = bench.build(A, torch.device("cuda", 0))
     launch, flops, algo, ncopy, kname, shape = bench.roofline_setup(pipe)
     for i in range(2 * ncopy):
