@@ -114,7 +114,7 @@ MFMA_BF16_PEAK_TFLOPS = 2500.0   # MI355X_MICROARCH.md: dense bf16 MFMA (no spar
 
 
 def roofline_setup(pipe, cold_bytes=640 << 20):
-    """The dominant kernel family is the bf16 MFMA GEMM (gemm_fast_kernel: HTSAT linears and the
+    """The dominant kernel family is the bf16 MFMA GEMM (gemm_lean_kernel: HTSAT stage 4 and the
     GPT-2 decode/prefill linears).  Its roofline is taken at the decode-step MLP up-projection
     as the bench runs it: c_fc out[R,3072] = gelu_new(h[R,768] @ W[3072,768]^T + b), R = the
     decode rows of one step (eval batches x 64), through ops.gemm exactly as the decoder calls
@@ -132,7 +132,7 @@ def roofline_setup(pipe, cold_bytes=640 << 20):
     copies = [W] + [W.clone() for _ in range(max(0, -(-cold_bytes // W.nbytes) - 1))]
     flops = 2 * M * N * K
     algo_bytes = N * K * es + M * K * es + N * 4 + M * N * es
-    kname = "gemm_skinny_kernel" if M <= 64 else "gemm_fast_kernel"
+    kname = "gemm_skinny_kernel" if M <= 64 else "gemm_lean_kernel"
 
     def launch(i):
         ops.gemm(h, copies[i % len(copies)], hid, bias=b, act=ops.ACT_GELU_TANH, workspace=dec.ws)

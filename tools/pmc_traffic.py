@@ -57,7 +57,7 @@ def _per_dispatch(d, counter, kname):
     return v[len(v) // 2], len(v)
 
 
-def parse(dfetch, dwrite, out, M=2048, N=3072, K=768, kname="gemm_fast_kernel"):
+def parse(dfetch, dwrite, out, M=8192, N=3072, K=768, kname="gemm_lean_kernel"):
     fetch_kib, n_f = _per_dispatch(dfetch, "FETCH_SIZE", kname)
     write_kib, n_w = _per_dispatch(dwrite, "WRITE_SIZE", kname)
     rd = 2 * 1024 * fetch_kib
