@@ -344,8 +344,11 @@ __global__ __launch_bounds__(256, 2) void gemm_lean_kernel(GemmArgs g) {
   }
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   f32x16_t acc[TM][TN];
-  lean_mainloop<BM, BN, NS, 2, 2, BK_>((const bf16_t*)g.A, g.lda, g.M, m0, (const bf16_t*)g.W,
-                                      g.ldw, g.N, n0, g.K, lds, acc);
+  // s_setprio(1) around each MFMA cluster (cdna_hip_programming.md T5): -2..-4 % at the
+  // 8192-row decode shapes, neutral elsewhere
+  lean_mainloop<BM, BN, NS, 2, 2, BK_, false, true>((const bf16_t*)g.A, g.lda, g.M, m0,
+                                                    (const bf16_t*)g.W, g.ldw, g.N, n0, g.K, lds,
+                                                    acc);
   const int wr0 = (wid >> 1) * FT::WM, wc0 = (wid & 1) * WN;
   const bool vec_out = g.ldo % 8 == 0 && ((uintptr_t)g.out & 15) == 0;
   const bool vec_res = g.residual == nullptr || (g.ldr % 4 == 0 && ((uintptr_t)g.residual & 15) == 0);

@@ -84,7 +84,7 @@ __device__ __forceinline__ void fast_issue_t(const ASrc& A, const BSrc& B, int k
 // SSQ: also accumulate, per lane, the sum of squares of the B fragments it reads (row
 // wc0 + j*32 + (lane & 31), its half of every k-slice): with the xor-32 partner's sum that is
 // the squared norm of the B row — the LM head's get_prefix_tokens row norms for free
-template <int BM, int BN, int WGM, int WGN, int BK_, bool SSQ = false>
+template <int BM, int BN, int WGM, int WGN, int BK_, bool SSQ = false, bool PRIO = false>
 __device__ __forceinline__ void fast_compute(
     const char* stage,
     f32x16_t (&acc)[FastTile<BM, BN, WGM, WGN, BK_>::TM][FastTile<BM, BN, WGM, WGN, BK_>::TN],
@@ -110,11 +110,13 @@ __device__ __forceinline__ void fast_compute(
         for (int u = 0; u < 8; ++u) { const float x = (float)b[j][u]; ssq[j] += x * x; }
       }
     }
+    if (PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int i = 0; i < FT::TM; ++i)
 #pragma unroll
       for (int j = 0; j < FT::TN; ++j)
         acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+    if (PRIO) __builtin_amdgcn_s_setprio(0);
   }
 }
 
@@ -197,7 +199,7 @@ __device__ __forceinline__ void fast_mainloop(
 // the matrices; clamped rows only feed outputs the caller's store guard drops) and K % BK == 0,
 // so a k-step carries just the counted wait, the raw barrier, IPW pointer adds + DMAs and the
 // MFMAs (fast_mainloop's per-chunk zero-chunk selects and 64-bit row products are gone).
-template <int BM, int BN, int NS, int WGM, int WGN, int BK_, bool SSQ = false>
+template <int BM, int BN, int NS, int WGM, int WGN, int BK_, bool SSQ = false, bool PRIO = false>
 __device__ __forceinline__ void lean_mainloop(
     const bf16_t* A, int lda, int M, int m0, const bf16_t* W, int ldw, int N, int n0, int K,
     char* lds,
@@ -240,7 +242,7 @@ __device__ __forceinline__ void lean_mainloop(
     if (kt + NS - 2 < nk) wait_vm<(NS - 2) * IPW>(); else wait_vm<0>();
     __builtin_amdgcn_s_barrier();
     if (kt + NS - 1 < nk) issue(st == 0 ? NS - 1 : st - 1, (kt + NS - 1) * BK_);
-    fast_compute<BM, BN, WGM, WGN, BK_, SSQ>(lds + st * FT::STAGE, acc, ssq);
+    fast_compute<BM, BN, WGM, WGN, BK_, SSQ, PRIO>(lds + st * FT::STAGE, acc, ssq);
     st = st == NS - 1 ? 0 : st + 1;
   }
   __syncthreads();   // callers may reuse the LDS for the epilogue
