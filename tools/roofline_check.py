@@ -31,8 +31,11 @@ def main(pdir, bench_log):
         name = r["Kernel_Name"]
         if "gemm_lean_kernel<" not in name:
             return None
-        bm, bn = (int(v) for v in name.split("gemm_lean_kernel<")[1].split(",")[:2])
-        g = -(-3072 // bn) * -(-mm // bm) * 256
+        targs = [int(v.strip(" >()")) for v in
+                 name.split("gemm_lean_kernel<")[1].split(">")[0].split(",")]
+        bm, bn = targs[:2]
+        threads = 64 * targs[4] * targs[5] if len(targs) >= 6 else 256
+        g = -(-3072 // bn) * -(-mm // bm) * threads
         return g if int(r["Grid_Size_X"]) == g else None
 
     durs, grid, run = [], None, []

@@ -322,10 +322,10 @@ __global__ __launch_bounds__(64 * WGM * WGN,
 // barrier, IPW pointer adds + DMAs and the MFMAs: gemm_fast_kernel's persistent / cross-tile /
 // split-K / experiment control flow spilled SGPRs into VGPR lanes and cost ~300 cycles of
 // scalar work per k-step, more than a 64x64 tile's MFMAs.
-template <int BM, int BN, int NS, int BK_>
-__global__ __launch_bounds__(256, 2) void gemm_lean_kernel(GemmArgs g) {
-  using FT = FastTile<BM, BN, 2, 2, BK_>;
-  constexpr int TM = FT::TM, TN = FT::TN, WN = FT::WN, NW = 4;
+template <int BM, int BN, int NS, int BK_, int WGM = 2, int WGN = 2>
+__global__ __launch_bounds__(64 * WGM * WGN, WGM * WGN == 4 ? 2 : 1) void gemm_lean_kernel(GemmArgs g) {
+  using FT = FastTile<BM, BN, WGM, WGN, BK_>;
+  constexpr int TM = FT::TM, TN = FT::TN, WN = FT::WN, NW = WGM * WGN;
   static_assert(NW * 32 * WN * 4 <= NS * FT::STAGE, "epilogue slab fits the ring");
   __shared__ __attribute__((aligned(16))) char lds[NS * FT::STAGE];
   const int ntn = cdiv(g.N, BN), ntm = cdiv(g.M, BM), ntiles = ntn * ntm;
@@ -346,10 +346,10 @@ __global__ __launch_bounds__(256, 2) void gemm_lean_kernel(GemmArgs g) {
   f32x16_t acc[TM][TN];
   // s_setprio(1) around each MFMA cluster (cdna_hip_programming.md T5): -2..-4 % at the
   // 8192-row decode shapes, neutral elsewhere
-  lean_mainloop<BM, BN, NS, 2, 2, BK_, false, true>((const bf16_t*)g.A, g.lda, g.M, m0,
-                                                    (const bf16_t*)g.W, g.ldw, g.N, n0, g.K, lds,
-                                                    acc);
-  const int wr0 = (wid >> 1) * FT::WM, wc0 = (wid & 1) * WN;
+  lean_mainloop<BM, BN, NS, WGM, WGN, BK_, false, true>((const bf16_t*)g.A, g.lda, g.M, m0,
+                                                        (const bf16_t*)g.W, g.ldw, g.N, n0, g.K,
+                                                        lds, acc);
+  const int wr0 = (wid / WGN) * FT::WM, wc0 = (wid % WGN) * WN;
   const bool vec_out = g.ldo % 8 == 0 && ((uintptr_t)g.out & 15) == 0;
   const bool vec_res = g.residual == nullptr || (g.ldr % 4 == 0 && ((uintptr_t)g.residual & 15) == 0);
   float bb[8];
@@ -388,10 +388,10 @@ __global__ __launch_bounds__(256, 2) void gemm_lean_kernel(GemmArgs g) {
 
 int g_gemm_lean = 1;   // zs_tune_set("gemm_lean", 0): decode-shaped GEMMs on gemm_fast_kernel
 
-template <int BM, int BN, int NS, int BK_>
+template <int BM, int BN, int NS, int BK_, int WGM = 2, int WGN = 2>
 static int launch_lean(GemmArgs& g, hipStream_t st) {
-  hipLaunchKernelGGL((gemm_lean_kernel<BM, BN, NS, BK_>), dim3(cdiv(g.N, BN) * cdiv(g.M, BM)),
-                     dim3(256), 0, st, g);
+  hipLaunchKernelGGL((gemm_lean_kernel<BM, BN, NS, BK_, WGM, WGN>),
+                     dim3(cdiv(g.N, BN) * cdiv(g.M, BM)), dim3(64 * WGM * WGN), 0, st, g);
   ZS_LAUNCH_CHECK();
   return 0;
 }
@@ -446,11 +446,27 @@ static int dispatch_fast(GemmArgs& g, hipStream_t st) {
     // 64x64 with a 4-deep ring
     const int lt = g_fast_tile >= 100 ? g_fast_tile - 100 : 0;   // experiment: force a lean tile
     const long n128 = nblocks(g, 128, 128);
-    if (lt == 1 || (!lt && (n128 > 1536 || (n128 >= 256 && n128 <= 512))))
-      return launch_lean<128, 128, 2, 64>(g, st);
+    // (re-measured with the s_setprio main loop, tools/mbench.py gemm_dbg at M = 1024..8192 x
+    // the GPT-2 shapes: 128x128 beats 128x64 at every n128 >= 256 — 8192x2304x768 46.9 vs 57.2
+    // us, 4096x3072x768 30.8 vs 38.1; the 8-wave 256x128 3-stage tile at one block per CU is
+    // best for the 8192-row c_fc, 57.5 vs 60.8; the 8-wave 128x128 4-stage tile for
+    // 128 <= n128 < 256, 4096x768x3072 32.0 vs 34.8, 1024x3072x768 12.0 vs 13.3)
+    if (!lt && g.N >= 3072 && n128 >= 1024 && n128 <= 4096)
+      return launch_lean<256, 128, 3, 64, 2, 4>(g, st);
+    if (lt == 1 || (!lt && n128 >= 256)) return launch_lean<128, 128, 2, 64>(g, st);
+    if (!lt && n128 >= 128) return launch_lean<128, 128, 4, 64, 2, 4>(g, st);
     if (lt == 2 || (!lt && nblocks(g, 128, 64) >= 256))
       return g.M >= g.N ? launch_lean<128, 64, 3, 64>(g, st) : launch_lean<64, 128, 3, 64>(g, st);
     if (lt == 3) return launch_lean<64, 64, 2, 128>(g, st);
+    // 8-wave tiles at one block per CU (experiments)
+    if (lt == 5) return launch_lean<256, 128, 2, 64, 4, 2>(g, st);
+    if (lt == 6) return launch_lean<128, 256, 2, 64, 2, 4>(g, st);
+    if (lt == 7) return launch_lean<256, 256, 2, 64, 2, 4>(g, st);
+    if (lt == 8) return launch_lean<256, 128, 3, 64, 4, 2>(g, st);
+    if (lt == 9) return launch_lean<128, 256, 3, 64, 2, 4>(g, st);
+    if (lt == 10) return launch_lean<256, 128, 3, 64, 2, 4>(g, st);
+    if (lt == 11) return launch_lean<128, 128, 3, 64, 2, 4>(g, st);
+    if (lt == 12) return launch_lean<128, 128, 4, 64, 2, 4>(g, st);
     return launch_lean<64, 64, 4, 64>(g, st);
   }
   if (nblocks(g, 128, 128) >= 256) {
