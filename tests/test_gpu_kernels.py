@@ -432,21 +432,28 @@ def test_lmhead_topk(cuda, dtype):
         assert float((cos.max(-1).values - picked).max()) < 1e-4
 
 
-def test_logmel_vs_oracle(cuda):
+@pytest.mark.parametrize("wave", [1, 0])        # wave-per-FFT kernel / block-per-4-frames kernel
+@pytest.mark.parametrize("B", [1, 2])           # 1 clip: an odd frame count (half-empty last pair)
+def test_logmel_vs_oracle(cuda, wave, B):
     from oracle import frontend as OF
     from zsaac import ops
+    from zsaac._lib import call
     from zsaac.frontend import make_tables
     from zsaac.synthetic import synthetic_waveforms
-    wav = synthetic_waveforms(2)
+    wav = synthetic_waveforms(B)
     ref = OF.logmel(wav)[:, 0]            # [B, 1001, 64]
-    out = ops.logmel(wav.to(cuda), make_tables(cuda))
-    assert out.shape == ref.shape
-    assert float((out.cpu() - ref).abs().max()) < 2e-3     # dB, f32 FFT vs f32 conv-DFT
-    # bn0 folded in
-    bn = [torch.rand(64, device=cuda) + 0.5 for _ in range(4)]
-    out2 = ops.logmel(wav.to(cuda), make_tables(cuda), bn=bn)
-    m, v, w, b = bn
-    assert _rel(out2, (out - m) / torch.sqrt(v + 1e-5) * w + b) < 1e-5
+    call("zs_tune_set", b"logmel_wave", wave)
+    try:
+        out = ops.logmel(wav.to(cuda), make_tables(cuda))
+        assert out.shape == ref.shape
+        assert float((out.cpu() - ref).abs().max()) < 2e-3     # dB, f32 FFT vs f32 conv-DFT
+        # bn0 folded in
+        bn = [torch.rand(64, device=cuda) + 0.5 for _ in range(4)]
+        out2 = ops.logmel(wav.to(cuda), make_tables(cuda), bn=bn)
+        m, v, w, b = bn
+        assert _rel(out2, (out - m) / torch.sqrt(v + 1e-5) * w + b) < 1e-5
+    finally:
+        call("zs_tune_set", b"logmel_wave", 1)
 
 
 def test_wav2img_patch_embed(cuda):

@@ -204,7 +204,11 @@ def bench_front():
     wav = (torch.randn(B, 320000, device=dev) * 0.1).clamp_(-1, 1)
     tabs = make_tables(dev)
     lm = torch.empty(B, 1001, 64, device=dev)
-    print(f"logmel B64:      {timeit(lambda: ops.logmel(wav, tabs, out=lm), reps=10):8.1f}us", flush=True)
+    from zsaac._lib import call
+    for wv in (1, 0):
+        call("zs_tune_set", b"logmel_wave", wv)
+        print(f"logmel B64 wave={wv}: {timeit(lambda: ops.logmel(wav, tabs, out=lm), reps=10):8.1f}us", flush=True)
+    call("zs_tune_set", b"logmel_wave", 1)
     img = torch.empty(B, 256, 256, device=dev)
     print(f"wav2img B64:     {timeit(lambda: ops.wav2img(lm, out=img), reps=10):8.1f}us", flush=True)
     w, b = torch.randn(96, 16, device=dev), torch.randn(96, device=dev)

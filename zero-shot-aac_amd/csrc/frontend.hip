@@ -146,6 +146,268 @@ __global__ __launch_bounds__(256) void logmel_kernel(
   }
 }
 
+// ------------------------------------------------------------------ wave-per-FFT front end
+// One wave per frame pair (complex 1024-point FFT), 4 independent waves per block, no block
+// barriers in the frame loop.  The same radix-4 DIF as logmel_kernel (same twiddles, same
+// butterfly arithmetic), but with the 16 points a lane holds two stages run in registers between
+// LDS exchanges (3 exchanges instead of 5 block-wide stage round trips):
+//   phase 1: lane l holds n = 256a + 64b + l            -> stages over a, b
+//   phase 2: lane (p1, p2, e) holds 256p1+64p2+16c+4d+e -> stages over c, d
+//   phase 3: lane l holds 16l + 4r + e (r = 0..3)        -> the last stage over e
+// Every exchange is conflict-free in the padded row (i + i/16).  The wave's row then holds the
+// spectrum in base-4 digit-reversed order; the two real spectra are separated into power rows
+// (aliasing the row: each lane's reads finish before its writes, LDS ops of a wave are in
+// order) and lane m contracts mel band m for both frames.
+__device__ __forceinline__ float2 twd(const float* tw, int e) {   // W_1024^e, e < 1024
+  if (e < 512) return make_float2(tw[2 * e], tw[2 * e + 1]);
+  return make_float2(-tw[2 * (e - 512)], -tw[2 * (e - 512) + 1]);
+}
+__device__ __forceinline__ void bfly4(float (&xr)[4], float (&xi)[4]) {
+  const float s02r = xr[0] + xr[2], s02i = xi[0] + xi[2];
+  const float d02r = xr[0] - xr[2], d02i = xi[0] - xi[2];
+  const float s13r = xr[1] + xr[3], s13i = xi[1] + xi[3];
+  const float d13r = xr[1] - xr[3], d13i = xi[1] - xi[3];
+  xr[0] = s02r + s13r; xi[0] = s02i + s13i;
+  xr[1] = d02r + d13i; xi[1] = d02i - d13r;
+  xr[2] = s02r - s13r; xi[2] = s02i - s13i;
+  xr[3] = d02r - d13i; xi[3] = d02i + d13r;
+}
+__device__ __forceinline__ void twmul(float& r, float& i, float2 w) {
+  const float t = r * w.x - i * w.y;
+  i = r * w.y + i * w.x;
+  r = t;
+}
+// W_1024^{64 m} = W_16^m (m < 16): exact-rounded constants, folded after unrolling
+__device__ __forceinline__ float2 w16(int m) {
+  constexpr float C[16] = {1.f, 0.92387953f, 0.70710678f, 0.38268343f, 0.f, -0.38268343f,
+                           -0.70710678f, -0.92387953f, -1.f, -0.92387953f, -0.70710678f,
+                           -0.38268343f, 0.f, 0.38268343f, 0.70710678f, 0.92387953f};
+  return make_float2(C[m & 15], C[(m + 4) & 15]);   // (cos, -sin)(2 pi m / 16)
+}
+__device__ __forceinline__ float2 cmul(float2 a, float2 b) {
+  return make_float2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
+}
+// orders this wave's LDS accesses for the compiler (the hardware keeps a wave's LDS ops in order)
+__device__ __forceinline__ void wave_lds_order() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_wave_barrier();
+}
+
+int g_logmel_wave = 1;   // zs_tune_set("logmel_wave", 0): the block-per-4-frames kernel
+
+__global__ __launch_bounds__(256, 3) void logmel_wave_kernel(
+    const float* __restrict__ wav, int T, int n_frames, int total_frames,
+    const float* __restrict__ window, const float* __restrict__ twiddle,
+    const float* __restrict__ melW, const int* __restrict__ mel_lo, const int* __restrict__ mel_hi,
+    const float* __restrict__ bn_mean, const float* __restrict__ bn_var,
+    const float* __restrict__ bn_w, const float* __restrict__ bn_b, float* __restrict__ out) {
+  __shared__ float rows[4][2][LPAD];      // per wave: re, im (later: the two power rows)
+  __shared__ float tw[NFFT];
+  __shared__ float swin[NFFT];
+  __shared__ float mw[2 * NBIN];
+  __shared__ int moff[NMEL + 1], mlo[NMEL];
+  for (int n = threadIdx.x; n < NFFT; n += 256) { tw[n] = twiddle[n]; swin[n] = window[n]; }
+  if (threadIdx.x < 64) {
+    const int m = threadIdx.x;
+    const int lo = mel_lo[m], len = mel_hi[m] - lo;
+    int inc = len;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const int o = __shfl_up(inc, d, 64);
+      if (m >= d) inc += o;
+    }
+    mlo[m] = lo;
+    moff[m + 1] = inc;
+    if (m == 0) moff[0] = 0;
+  }
+  __syncthreads();
+  {
+    const int m = threadIdx.x >> 2, s0 = threadIdx.x & 3;
+    const int lo = mlo[m], len = moff[m + 1] - moff[m];
+    for (int k = s0; k < len; k += 4) mw[moff[m] + k] = melW[m * NBIN + lo + k];
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  float* re = rows[wid][0];
+  float* im = rows[wid][1];
+  const int npairs = (total_frames + 1) >> 1;
+  // raw samples of a pair (zero for a missing second frame); the next pair's are fetched before
+  // the current pair's FFT so their HBM latency overlaps it
+  auto fetch = [&](int gp, float (&sr)[16], float (&si)[16]) {
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int g = 2 * gp + q;
+      const bool valid = g < total_frames;
+      const int gb = valid ? g / n_frames : 0, f = valid ? g % n_frames : 0;
+      const float* src = wav + (long)gb * T;
+      const int base = f * HOP - NFFT / 2;
+      if (valid && base >= 0 && base + NFFT <= T) {   // interior frame (wave-uniform): one
+        const float* p = src + base + lane;            // pointer, immediate offsets
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          if (q == 0) sr[i] = p[64 * i]; else si[i] = p[64 * i];
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          int o = base + 64 * i + lane;
+          if (o < 0) o = -o;                       // reflect (no edge repeat), torch F.pad 'reflect'
+          if (o >= T) o = 2 * (T - 1) - o;
+          const float v = valid ? src[o] : 0.f;
+          if (q == 0) sr[i] = v; else si[i] = v;
+        }
+      }
+    }
+  };
+  const int stride = gridDim.x * 4;
+  float cr_[16], ci_[16];
+  int gp = blockIdx.x * 4 + wid;
+  if (gp < npairs) fetch(gp, cr_, ci_);
+  for (; gp < npairs; gp += stride) {
+    float zr[4][4], zi[4][4];             // phase 1: [a][b], n = 256a + 64b + lane
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        const float wv = swin[256 * a + 64 * b + lane];
+        zr[a][b] = cr_[4 * a + b] * wv;
+        zi[a][b] = ci_[4 * a + b] * wv;
+      }
+    if (gp + stride < npairs) fetch(gp + stride, cr_, ci_);
+    // stage 1 (over a), twiddle W_1024^{p (64b + lane)} = W_1024^{p lane} W_16^{p b} (three
+    // table twiddles per lane instead of twelve: they stay in registers across the frame loop)
+    const float2 t1[4] = {make_float2(1.f, 0.f), twd(tw, lane), twd(tw, 2 * lane), twd(tw, 3 * lane)};
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      float xr[4] = {zr[0][b], zr[1][b], zr[2][b], zr[3][b]};
+      float xi[4] = {zi[0][b], zi[1][b], zi[2][b], zi[3][b]};
+      bfly4(xr, xi);
+#pragma unroll
+      for (int p = 1; p < 4; ++p) twmul(xr[p], xi[p], b == 0 ? t1[p] : cmul(t1[p], w16(p * b)));
+#pragma unroll
+      for (int p = 0; p < 4; ++p) { zr[p][b] = xr[p]; zi[p][b] = xi[p]; }
+    }
+    // stage 2 (over b), twiddle W_1024^{4 p lane}
+    {
+      const float2 w1 = twd(tw, 4 * lane), w2 = twd(tw, 8 * lane), w3 = twd(tw, 12 * lane);
+#pragma unroll
+      for (int p1 = 0; p1 < 4; ++p1) {
+        float xr[4] = {zr[p1][0], zr[p1][1], zr[p1][2], zr[p1][3]};
+        float xi[4] = {zi[p1][0], zi[p1][1], zi[p1][2], zi[p1][3]};
+        bfly4(xr, xi);
+        twmul(xr[1], xi[1], w1);
+        twmul(xr[2], xi[2], w2);
+        twmul(xr[3], xi[3], w3);
+#pragma unroll
+        for (int p = 0; p < 4; ++p) { zr[p1][p] = xr[p]; zi[p1][p] = xi[p]; }
+      }
+    }
+    wave_lds_order();                      // previous pair's mel reads of this row are done
+#pragma unroll
+    for (int p1 = 0; p1 < 4; ++p1)
+#pragma unroll
+      for (int p2 = 0; p2 < 4; ++p2) {
+        re[lp(256 * p1 + 64 * p2 + lane)] = zr[p1][p2];
+        im[lp(256 * p1 + 64 * p2 + lane)] = zi[p1][p2];
+      }
+    wave_lds_order();
+    // phase 2: lane = 16 p1 + 4 p2 + e holds pb + 16c + 4d
+    const int E = lane & 3;
+    const int pb = 256 * (lane >> 4) + 64 * ((lane >> 2) & 3) + E;
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int d = 0; d < 4; ++d) {
+        zr[c][d] = re[lp(pb + 16 * c + 4 * d)];
+        zi[c][d] = im[lp(pb + 16 * c + 4 * d)];
+      }
+    // stage 3 (over c), twiddle W_1024^{16 p (4d + e)} = W_1024^{16 p e} W_16^{p d}
+    const float2 t3[4] = {make_float2(1.f, 0.f), twd(tw, 16 * E), twd(tw, 32 * E), twd(tw, 48 * E)};
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      float xr[4] = {zr[0][d], zr[1][d], zr[2][d], zr[3][d]};
+      float xi[4] = {zi[0][d], zi[1][d], zi[2][d], zi[3][d]};
+      bfly4(xr, xi);
+#pragma unroll
+      for (int p = 1; p < 4; ++p) twmul(xr[p], xi[p], d == 0 ? t3[p] : cmul(t3[p], w16(p * d)));
+#pragma unroll
+      for (int p = 0; p < 4; ++p) { zr[p][d] = xr[p]; zi[p][d] = xi[p]; }
+    }
+    // stage 4 (over d), twiddle W_1024^{64 p e}
+    {
+      const float2 w1 = twd(tw, 64 * E), w2 = twd(tw, 128 * E), w3 = twd(tw, 192 * E);
+#pragma unroll
+      for (int p3 = 0; p3 < 4; ++p3) {
+        float xr[4] = {zr[p3][0], zr[p3][1], zr[p3][2], zr[p3][3]};
+        float xi[4] = {zi[p3][0], zi[p3][1], zi[p3][2], zi[p3][3]};
+        bfly4(xr, xi);
+        twmul(xr[1], xi[1], w1);
+        twmul(xr[2], xi[2], w2);
+        twmul(xr[3], xi[3], w3);
+#pragma unroll
+        for (int p = 0; p < 4; ++p) { zr[p3][p] = xr[p]; zi[p3][p] = xi[p]; }
+      }
+    }
+    wave_lds_order();
+#pragma unroll
+    for (int p3 = 0; p3 < 4; ++p3)
+#pragma unroll
+      for (int p4 = 0; p4 < 4; ++p4) {
+        re[lp(pb + 16 * p3 + 4 * p4)] = zr[p3][p4];
+        im[lp(pb + 16 * p3 + 4 * p4)] = zi[p3][p4];
+      }
+    wave_lds_order();
+    // phase 3: lane holds 16 lane + 4r + e; the last stage (twiddle 1), written back in place
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float xr[4], xi[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) { xr[e] = re[lp(16 * lane + 4 * r + e)]; xi[e] = im[lp(16 * lane + 4 * r + e)]; }
+      bfly4(xr, xi);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) { re[lp(16 * lane + 4 * r + e)] = xr[e]; im[lp(16 * lane + 4 * r + e)] = xi[e]; }
+    }
+    wave_lds_order();
+    // X[k] sits at digrev4(k): separate the two real spectra, |.|^2 for k <= 512
+    float pa[9], pq[9];
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const int k = min(lane + 64 * t, NBIN - 1);
+      const int a = lp(digrev4(k)), c = lp(digrev4((NFFT - k) & (NFFT - 1)));
+      const float zr_ = re[a], zi_ = im[a], cr = re[c], ci = -im[c];
+      const float ar = zr_ + cr, ai = zi_ + ci;
+      const float br = zi_ - ci, bi = cr - zr_;
+      pa[t] = 0.25f * (ar * ar + ai * ai);
+      pq[t] = 0.25f * (br * br + bi * bi);
+    }
+    wave_lds_order();
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const int k = lane + 64 * t;
+      if (k < NBIN) { re[k] = pa[t]; im[k] = pq[t]; }
+    }
+    wave_lds_order();
+    {
+      const int m = lane;
+      const int lo = mlo[m], base = moff[m], len = moff[m + 1] - base;
+      float acc0 = 0.f, acc1 = 0.f;
+      for (int k = 0; k < len; ++k) {
+        const float wv = mw[base + k];
+        acc0 += re[lo + k] * wv;
+        acc1 += im[lo + k] * wv;
+      }
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const int g = 2 * gp + q;
+        if (g >= total_frames) continue;
+        float v = 10.0f * log10f(fmaxf(q ? acc1 : acc0, 1e-10f));   // power_to_db, ref 1.0
+        if (bn_mean) v = (v - bn_mean[m]) / sqrtf(bn_var[m] + 1e-5f) * bn_w[m] + bn_b[m];
+        out[(long)g * NMEL + m] = v;
+      }
+    }
+  }
+}
+
 // bicubic (A = -0.75, align_corners = True) along time T_in -> 1024, identity along the 64 mels,
 // then fold: img[r = chunk*64 + mel][c] = resized[t = chunk*256 + c][mel]
 __global__ void wav2img_kernel(const float* __restrict__ in, int T_in, float* __restrict__ img) {
@@ -258,6 +520,15 @@ extern "C" int zs_logmel(const float* wav, int B, int T, const float* window, co
   ZS_REQUIRE(B > 0 && T > NFFT / 2, "zs_logmel: need T > 512 samples for reflect padding");
   const int n_frames = T / HOP + 1;
   const int total = B * n_frames;
+  if (g_logmel_wave) {
+    const int npairs = cdiv(total, 2);
+    // 3 blocks per CU fit the LDS (47.6 KB each): one resident wave of blocks, no tail round
+    hipLaunchKernelGGL(logmel_wave_kernel, dim3(std::min(cdiv(npairs, 4), 256 * 3)), dim3(256), 0,
+                       S(stream), wav, T, n_frames, total, window, twiddle, melW, mel_lo, mel_hi,
+                       bn_mean, bn_var, bn_weight, bn_bias, out);
+    ZS_LAUNCH_CHECK();
+    return 0;
+  }
   const int groups = cdiv(total, 2 * LM_PAIRS);
   hipLaunchKernelGGL(logmel_kernel, dim3(std::min(groups, 256 * 8)), dim3(256), 0, S(stream), wav, T,
                      n_frames, total, window, twiddle, melW, mel_lo, mel_hi, bn_mean, bn_var,

@@ -246,6 +246,7 @@ extern int g_fast_xcd;      // gemm.hip
 extern int g_swin_dbg;      // swin.hip
 extern int g_gemm_lean;     // gemm.hip
 extern int g_row_mfma;      // attn.hip
+extern int g_logmel_wave;   // frontend.hip
 
 // choose K per workgroup: a multiple of 64 dividing K, each wave <= 128 deep, ~256-320 WGs
 static int skinny_splits(int N, int K) {
@@ -280,6 +281,7 @@ extern "C" int zs_tune_set(const char* key, int value) {
   if (!strcmp(key, "swin_dbg")) { g_swin_dbg = value; return 0; }
   if (!strcmp(key, "gemm_lean")) { g_gemm_lean = value; return 0; }
   if (!strcmp(key, "row_mfma")) { g_row_mfma = value; return 0; }
+  if (!strcmp(key, "logmel_wave")) { g_logmel_wave = value; return 0; }
   return fail(ZS_ERR_ARG, "zs_tune_set: unknown key %s", key);
 }
 

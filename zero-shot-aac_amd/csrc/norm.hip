@@ -67,10 +67,17 @@ __global__ __launch_bounds__(256) void layernorm_reg_kernel(const float* __restr
     if (c < C4) {
       const float4 ww = reinterpret_cast<const float4*>(w)[c];
       const float4 bv = reinterpret_cast<const float4*>(b)[c];
-      stf(yr + 4 * c + 0, (v[i].x - mean) * rstd * ww.x + bv.x);
-      stf(yr + 4 * c + 1, (v[i].y - mean) * rstd * ww.y + bv.y);
-      stf(yr + 4 * c + 2, (v[i].z - mean) * rstd * ww.z + bv.z);
-      stf(yr + 4 * c + 3, (v[i].w - mean) * rstd * ww.w + bv.w);
+      const float o0 = (v[i].x - mean) * rstd * ww.x + bv.x, o1 = (v[i].y - mean) * rstd * ww.y + bv.y;
+      const float o2 = (v[i].z - mean) * rstd * ww.z + bv.z, o3 = (v[i].w - mean) * rstd * ww.w + bv.w;
+      // one 8-byte (bf16) / 16-byte (f32) store per lane: the caller guarantees the alignment
+      if constexpr (sizeof(TO) == 2) {
+        uint2 u;
+        u.x = (uint32_t)f2bf(o0) | ((uint32_t)f2bf(o1) << 16);
+        u.y = (uint32_t)f2bf(o2) | ((uint32_t)f2bf(o3) << 16);
+        *reinterpret_cast<uint2*>(yr + 4 * c) = u;
+      } else {
+        *reinterpret_cast<float4*>(yr + 4 * c) = make_float4(o0, o1, o2, o3);
+      }
     }
   }
 }
@@ -228,7 +235,9 @@ extern "C" int zs_layernorm(const float* x, int M, int C, int ldx, const int* ro
   ZS_REQUIRE(M >= 0 && C > 0 && ldx >= C && ldy >= C, "zs_layernorm: bad shape");
   if (M == 0) return 0;
   dim3 grid(cdiv(M, 4));
-  if (C % 4 == 0 && ldx % 4 == 0 && C <= 1024) {
+  const int yal = ydtype == ZS_BF16 ? 8 : 16;
+  if (C % 4 == 0 && ldx % 4 == 0 && C <= 1024 && ldy % 4 == 0 && ((uintptr_t)x & 15) == 0 &&
+      ((uintptr_t)y & (yal - 1)) == 0) {
     const int nv = cdiv(C / 4, 64);
 #define LNR(TO, NV_)                                                                           \
   hipLaunchKernelGGL((layernorm_reg_kernel<TO, NV_>), grid, dim3(256), 0, S(stream), x, M, C,    \
