@@ -50,6 +50,31 @@ def test_gemm(cuda, dtype, M, N, K):
     assert torch.equal(out2, out3)
 
 
+@pytest.mark.parametrize("tile", [101, 102, 103, 105, 106, 107, 108, 109, 110, 111, 112, 113])
+def test_gemm_lean_tiles(cuda, tile):
+    """Every forced lean-GEMM tile (zs_tune_set fast_tile 100 + t: 4- and 8-wave, 1-3 stage rings,
+    the 128x96 4x1 tile) at ragged shapes, with bias + gelu and with a residual."""
+    from zsaac import ops
+    from zsaac._lib import call
+    call("zs_tune_set", b"fast_tile", tile)
+    try:
+        for M, N, K in ((1000, 2304, 768), (333, 768, 3072), (520, 770, 64)):
+            g = torch.Generator(device="cuda").manual_seed(M + N + tile)
+            a = torch.randn(M, K, device=cuda, generator=g).bfloat16()
+            w = torch.randn(N, K, device=cuda, generator=g).div(math.sqrt(K)).bfloat16()
+            bias = torch.randn(N, device=cuda, generator=g)
+            res = torch.randn(M, N, device=cuda, generator=g)
+            ref = a.float() @ w.float().t() + bias
+            out = torch.empty(M, N, device=cuda, dtype=torch.bfloat16)
+            ops.gemm(a, w, out, bias=bias, act=ops.ACT_GELU_ERF, split_k=1)
+            assert _rel(out, torch.nn.functional.gelu(ref)) < 1e-2, (M, N, K)
+            out = res.clone()
+            ops.gemm(a, w, out, bias=bias, residual=out, split_k=1)
+            assert _rel(out, ref + res) < 1e-2, (M, N, K)
+    finally:
+        call("zs_tune_set", b"fast_tile", 0)
+
+
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("M,N,K", [(64, 2304, 768), (64, 768, 768), (64, 3072, 768), (64, 768, 3072),
                                    (50, 7680, 3840), (3, 1024, 768), (64, 100, 64),

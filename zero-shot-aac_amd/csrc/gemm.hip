@@ -107,8 +107,14 @@ __device__ __forceinline__ void epi_slab(const GemmArgs& g, const float* slab, i
       }
       continue;
     }
+    if constexpr (64 % Q == 0) {   // a lane's 8 columns are the same in every iteration
 #pragma unroll
-    for (int q = 0; q < 8; ++q) v[q] = act_apply_fast(v[q] + bb[q], ACT);
+      for (int q = 0; q < 8; ++q) v[q] = act_apply_fast(v[q] + bb[q], ACT);
+    } else {                       // (WN = 96: they move with the iteration)
+#pragma unroll
+      for (int q = 0; q < 8; ++q)
+        v[q] = act_apply_fast(v[q] + ((g.bias && q < nv) ? g.bias[n + q] : 0.f), ACT);
+    }
     if (g.residual) {
       if (full && vec_res) {
         const float4 r0 = res[it][0], r1 = res[it][1];
@@ -387,6 +393,10 @@ __global__ __launch_bounds__(64 * WGM * WGN, WGM * WGN == 4 ? 2 : 1) void gemm_l
 }
 
 int g_gemm_lean = 1;   // zs_tune_set("gemm_lean", 0): decode-shaped GEMMs on gemm_fast_kernel
+int g_lean96 = 0;      // zs_tune_set("lean96", 1): 128x96 tiles for the N = 768 projections
+                       // (faster alone, but -2 % end to end with the decode groups co-running)
+int g_lean8w = 0;      // zs_tune_set("lean8w", 1): 8-wave 256x128 tile for the 8192-row c_fc
+                       // (57.5 vs 60.8 us alone, but -0.6 % end to end: A/B in one box)
 
 template <int BM, int BN, int NS, int BK_, int WGM = 2, int WGN = 2>
 static int launch_lean(GemmArgs& g, hipStream_t st) {
@@ -451,13 +461,17 @@ static int dispatch_fast(GemmArgs& g, hipStream_t st) {
     // us, 4096x3072x768 30.8 vs 38.1; the 8-wave 256x128 3-stage tile at one block per CU is
     // best for the 8192-row c_fc, 57.5 vs 60.8; the 8-wave 128x128 4-stage tile for
     // 128 <= n128 < 256, 4096x768x3072 32.0 vs 34.8, 1024x3072x768 12.0 vs 13.3)
-    if (!lt && g.N >= 3072 && n128 >= 1024 && n128 <= 4096)
+    if (!lt && g_lean8w && g.N >= 3072 && n128 >= 1024 && n128 <= 4096)
       return launch_lean<256, 128, 3, 64, 2, 4>(g, st);
+    // 128x96 (4 waves as 4x1, 32x96 wave tiles) for the N = 768 projections at >= 6144 rows:
+    // 8 column tiles, 2 blocks per CU (8192x768x3072 56.4 vs 59.2 us, 6144x768x3072 50.2 vs 53.7)
+    if (!lt && g_lean96 && g.N % 96 == 0 && g.N <= 1536 && nblocks(g, 128, 96) >= 384)
+      return launch_lean<128, 96, 2, 64, 4, 1>(g, st);
     if (lt == 1 || (!lt && n128 >= 256)) return launch_lean<128, 128, 2, 64>(g, st);
     if (!lt && n128 >= 128) return launch_lean<128, 128, 4, 64, 2, 4>(g, st);
     if (lt == 2 || (!lt && nblocks(g, 128, 64) >= 256))
       return g.M >= g.N ? launch_lean<128, 64, 3, 64>(g, st) : launch_lean<64, 128, 3, 64>(g, st);
-    if (lt == 3) return launch_lean<64, 64, 2, 128>(g, st);
+    if (lt == 3 && g.K % 128 == 0) return launch_lean<64, 64, 2, 128>(g, st);
     // 8-wave tiles at one block per CU (experiments)
     if (lt == 5) return launch_lean<256, 128, 2, 64, 4, 2>(g, st);
     if (lt == 6) return launch_lean<128, 256, 2, 64, 2, 4>(g, st);
@@ -467,6 +481,7 @@ static int dispatch_fast(GemmArgs& g, hipStream_t st) {
     if (lt == 10) return launch_lean<256, 128, 3, 64, 2, 4>(g, st);
     if (lt == 11) return launch_lean<128, 128, 3, 64, 2, 4>(g, st);
     if (lt == 12) return launch_lean<128, 128, 4, 64, 2, 4>(g, st);
+    if (lt == 13) return launch_lean<128, 96, 2, 64, 4, 1>(g, st);
     return launch_lean<64, 64, 4, 64>(g, st);
   }
   if (nblocks(g, 128, 128) >= 256) {
