@@ -60,9 +60,10 @@ def parse():
                     help="eval batches of --batch clips decoded together (one decode step over "
                          "group*batch rows; measured 32 -> 64 -> 128: 10.9k -> 12.1k -> 12.3k "
                          "clips/s); encoded --encoder-batch clips per pass")
-    ap.add_argument("--inflight", type=int, default=2,
+    ap.add_argument("--inflight", type=int, default=3,
                     help="independent groups in flight per GPU, each on its own HIP stream "
-                         "(2 and 3 measure the same at group 128; 1: -11 %%)")
+                         "(A/B in one box at group 128: 3 -> 12.73-12.75k, 2 -> 12.51-12.60k, "
+                         "4 -> 12.70k clips/s; 1: -11 %%)")
     ap.add_argument("--compact", type=int, default=1,
                     help="greedy bf16: decode only the rows that have not stopped (0 = all rows)")
     ap.add_argument("--cpu-baseline-clips", type=int, default=2)
