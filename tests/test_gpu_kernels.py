@@ -274,7 +274,7 @@ def test_decode_attention_matches_prefill(cuda):
 
 
 @pytest.mark.parametrize("use_kvrow", [False, True])
-@pytest.mark.parametrize("variant", [4, 3, 2, 1, 0])
+@pytest.mark.parametrize("variant", [5, 4, 3, 2, 1, 0])
 def test_decode_attention_bf16(cuda, use_kvrow, variant):
     """bf16 decode attention (register-resident decode_attn5, and the LDS-staged decode_attn4)
     vs an fp32 torch reference: ragged positions 0..Lmax-1 per row, optional beam kvrow

@@ -305,7 +305,7 @@ def bench_attn():
     from zsaac import ops
     from zsaac._lib import call
     dev = torch.device("cuda", 0)
-    R, D, H, Lmax = 2048, 768, 12, 102
+    R, D, H, Lmax = int(os.environ.get("ZS_M", 2048)), 768, 12, 102
     kc = torch.randn(R, H, Lmax, 64, device=dev).bfloat16()
     vc = torch.randn_like(kc)
     qkv = torch.randn(R, 3 * D, device=dev).bfloat16()
@@ -314,7 +314,7 @@ def bench_attn():
         pos = torch.full((R,), L - 1, device=dev, dtype=torch.int32)
         byts = R * H * L * 64 * 2 * 2
         r = {}
-        for v in (3, 2, 1):
+        for v in [int(x) for x in os.environ.get("ZS_VARIANTS", "3,2,1").split(",")]:
             call("zs_tune_set", b"decode_attn5", v)
             r[v] = timeit(lambda: ops.decode_attention(qkv, R, D, H, kc, vc, Lmax, pos, out), reps=20)
         call("zs_tune_set", b"decode_attn5", 2)

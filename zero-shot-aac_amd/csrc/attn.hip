@@ -9,7 +9,7 @@
 
 namespace zs {
 
-int g_decode_attn5 = 4;   // 4/3/2: decode_attn6 (phases of 16/32/64 keys), 1: decode_attn5, 0: LDS
+int g_decode_attn5 = 4;   // 5: decode_attn6 16-key phases + next-phase prefetch; 4/3/2: decode_attn6 (phases of 16/32/64 keys), 1: decode_attn5, 0: LDS
 int g_window_mfma = 1;    // zs_tune_set("window_mfma", 0): VALU window attention for bf16   // zs_tune_set("decode_attn5", 0): LDS-staged decode_attn4 for bf16
 
 // ------------------------------------------------------------------ HTSAT window attention
@@ -593,7 +593,9 @@ __global__ __launch_bounds__(256) void decode_attn5_kernel(const T* __restrict__
 // SIMD instead of 2) and any Lmax works.  The per-slot inputs (rowmap, compact position) are
 // loaded together with the qkv row: one dependent round trip before the K/V loads.  With one
 // phase (p < 64) the arithmetic equals decode_attn5's.
-template <typename T, int KPP = 64>          // KPP: keys per phase (8 per key group)
+// PF: the next phase's K/V loads are issued before the current phase's math (two phases in
+// flight per wave; the wait lands after the math instead of before it)
+template <typename T, int KPP = 64, bool PF = false>   // KPP: keys per phase (8 per key group)
 __global__ __launch_bounds__(256) void decode_attn6_kernel(
     const T* __restrict__ qkv, int D, int heads, T* __restrict__ kc, T* __restrict__ vc, int Lmax,
     const int* __restrict__ pos, const int* __restrict__ kvrow, T* __restrict__ out,
@@ -630,8 +632,7 @@ __global__ __launch_bounds__(256) void decode_attn6_kernel(
   float m = -INFINITY, sum = 0.f, o[EPC];
 #pragma unroll
   for (int t = 0; t < EPC; ++t) o[t] = 0.f;
-  for (int base = 0; base <= p; base += KPP) {
-    uint4 kr[NG], vr[NG];
+  auto load_phase = [&](int base, uint4 (&kr)[NG], uint4 (&vr)[NG]) {
 #pragma unroll
     for (int i = 0; i < NG; ++i) {
       const int j = base + i * 8 + grp;
@@ -645,6 +646,15 @@ __global__ __launch_bounds__(256) void decode_attn6_kernel(
         kr[i] = knu;
         vr[i] = vnu;
       }
+    }
+  };
+  uint4 kr[NG], vr[NG], kx[NG], vx[NG];
+  if (PF) load_phase(0, kr, vr);
+  for (int base = 0; base <= p; base += KPP) {
+    if (PF) {
+      if (base + KPP <= p) load_phase(base + KPP, kx, vx);
+    } else {
+      load_phase(base, kr, vr);
     }
     float sc[NG];
     float pm = -INFINITY;
@@ -676,6 +686,10 @@ __global__ __launch_bounds__(256) void decode_attn6_kernel(
       const T* v = reinterpret_cast<const T*>(&vr[i]);
 #pragma unroll
       for (int t = 0; t < EPC; ++t) o[t] += e * ldf(v + t);
+    }
+    if (PF) {
+#pragma unroll
+      for (int i = 0; i < NG; ++i) { kr[i] = kx[i]; vr[i] = vx[i]; }
     }
   }
 #pragma unroll
@@ -864,6 +878,10 @@ extern "C" int zs_decode_attention_map(const void* qkv, int R, const int* rowmap
     hipLaunchKernelGGL((decode_attn6_kernel<bf16_t, 16>), dim3(R, cdiv(heads, 4)), dim3(256), 0,
                        S(stream), (const bf16_t*)qkv, D, heads, (bf16_t*)kc, (bf16_t*)vc, Lmax,
                        pos, (const int*)nullptr, (bf16_t*)out, rowmap, cpos, nphys);
+  } else if (g_decode_attn5 == 5) {
+    hipLaunchKernelGGL((decode_attn6_kernel<bf16_t, 16, true>), dim3(R, cdiv(heads, 4)), dim3(256),
+                       0, S(stream), (const bf16_t*)qkv, D, heads, (bf16_t*)kc, (bf16_t*)vc, Lmax,
+                       pos, (const int*)nullptr, (bf16_t*)out, rowmap, cpos, nphys);
   } else {
     hipLaunchKernelGGL((decode_attn6_kernel<bf16_t, 32>), dim3(R, cdiv(heads, 4)), dim3(256), 0,
                        S(stream), (const bf16_t*)qkv, D, heads, (bf16_t*)kc, (bf16_t*)vc, Lmax,
@@ -883,6 +901,13 @@ extern "C" int zs_decode_attention(const void* qkv, int R, int D, int heads, voi
   if (dtype == ZS_BF16 && g_decode_attn5 == 4) {
     hipLaunchKernelGGL((decode_attn6_kernel<bf16_t, 16>), dim3(R, cdiv(heads, 4)), dim3(256), 0,
                        S(stream), (const bf16_t*)qkv, D, heads, (bf16_t*)kc, (bf16_t*)vc, Lmax,
+                       pos, kvrow, (bf16_t*)out, (const int*)nullptr, (const int*)nullptr, R);
+    ZS_LAUNCH_CHECK();
+    return 0;
+  }
+  if (dtype == ZS_BF16 && g_decode_attn5 == 5) {
+    hipLaunchKernelGGL((decode_attn6_kernel<bf16_t, 16, true>), dim3(R, cdiv(heads, 4)), dim3(256),
+                       0, S(stream), (const bf16_t*)qkv, D, heads, (bf16_t*)kc, (bf16_t*)vc, Lmax,
                        pos, kvrow, (bf16_t*)out, (const int*)nullptr, (const int*)nullptr, R);
     ZS_LAUNCH_CHECK();
     return 0;
