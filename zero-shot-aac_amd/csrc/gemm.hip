@@ -519,6 +519,7 @@ static int dispatch_gemm(GemmArgs& g, hipStream_t st) {
 // ------------------------------------------------------------------ LM head (+ row reductions)
 constexpr int LM_BN = 128;
 constexpr int MAXK = 8;
+int g_lm_prio = 1;   // zs_tune_set("lm_prio", 0): LM head main loop without s_setprio
 
 template <typename T, int BM, int KMAX>
 __global__ __launch_bounds__(256) void lmhead_kernel(int xcd_order, int M, int K, int V, const T* A, int lda,
@@ -542,7 +543,7 @@ __global__ __launch_bounds__(256) void lmhead_kernel(int xcd_order, int M, int K
   // 77 MB of W streamed once per row tile).
   const int ntm = cdiv(M, BM), nblk = cdiv(V, LM_BN), nwg = nblk * ntm;
   int vb, mb;
-  if (xcd_order) {
+  if (xcd_order & 1) {
     const int b = blockIdx.x, x = b & 7, q8 = nwg >> 3, r8 = nwg & 7;
     const int u = (x < r8 ? x * (q8 + 1) : r8 * (q8 + 1) + (x - r8) * q8) + (b >> 3);
     vb = u / ntm;
@@ -566,6 +567,10 @@ __global__ __launch_bounds__(256) void lmhead_kernel(int xcd_order, int M, int K
       if (row_norm)
         lean_mainloop<LM_BN, BM, 2, 2, 2, 64, true>((const bf16_t*)W, K, V, n0, (const bf16_t*)A,
                                                     lda, M, m0, K, smem_raw, acct, ssq);
+      else if (xcd_order & 2)   // s_setprio around the MFMA clusters, as gemm_lean_kernel
+        lean_mainloop<LM_BN, BM, 2, 2, 2, 64, false, true>((const bf16_t*)W, K, V, n0,
+                                                           (const bf16_t*)A, lda, M, m0, K,
+                                                           smem_raw, acct);
       else
         lean_mainloop<LM_BN, BM, 2, 2, 2, 64>((const bf16_t*)W, K, V, n0, (const bf16_t*)A, lda,
                                               M, m0, K, smem_raw, acct);
@@ -866,7 +871,8 @@ extern "C" int zs_lmhead_topk(int M, int K, int V, int dtype, const void* A, int
   const int nblk = cdiv(V, LM_BN);
 #define LMH(T, BM_, KM_)                                                                     \
   hipLaunchKernelGGL((lmhead_kernel<T, BM_, KM_>), dim3(nblk * cdiv(M, BM_)), dim3(256), 0, st, \
-                     g_fast_xcd, M, K, V, (const T*)A, lda, (const T*)W, topk, row_norm, part_stat,       \
+                     (g_fast_xcd ? 1 : 0) | (g_lm_prio ? 2 : 0), M, K, V, (const T*)A, lda,       \
+                     (const T*)W, topk, row_norm, part_stat,                                      \
                      part_val, part_idx)
 #define LMH_K(T, BM_) do { if (topk == 1) LMH(T, BM_, 1); else LMH(T, BM_, 8); } while (0)
   if (M <= 64) {

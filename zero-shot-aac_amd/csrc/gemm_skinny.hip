@@ -249,6 +249,7 @@ extern int g_row_mfma;      // attn.hip
 extern int g_logmel_wave;   // frontend.hip
 extern int g_lean96;        // gemm.hip
 extern int g_lean8w;        // gemm.hip
+extern int g_lm_prio;       // gemm.hip
 
 // choose K per workgroup: a multiple of 64 dividing K, each wave <= 128 deep, ~256-320 WGs
 static int skinny_splits(int N, int K) {
@@ -286,6 +287,7 @@ extern "C" int zs_tune_set(const char* key, int value) {
   if (!strcmp(key, "logmel_wave")) { g_logmel_wave = value; return 0; }
   if (!strcmp(key, "lean96")) { g_lean96 = value; return 0; }
   if (!strcmp(key, "lean8w")) { g_lean8w = value; return 0; }
+  if (!strcmp(key, "lm_prio")) { g_lm_prio = value; return 0; }
   return fail(ZS_ERR_ARG, "zs_tune_set: unknown key %s", key);
 }
 
