@@ -274,7 +274,7 @@ def test_decode_attention_matches_prefill(cuda):
 
 
 @pytest.mark.parametrize("use_kvrow", [False, True])
-@pytest.mark.parametrize("variant", [5, 4, 3, 2, 1, 0])
+@pytest.mark.parametrize("variant", [6, 5, 4, 3, 2, 1, 0])
 def test_decode_attention_bf16(cuda, use_kvrow, variant):
     """bf16 decode attention (register-resident decode_attn5, and the LDS-staged decode_attn4)
     vs an fp32 torch reference: ragged positions 0..Lmax-1 per row, optional beam kvrow
@@ -313,6 +313,31 @@ def test_decode_attention_bf16(cuda, use_kvrow, variant):
             assert float((got - ref).abs().max()) < 2e-2 * float(ref.abs().max()) + 1e-2, (r, h, p)
         assert torch.equal(kc[r, :, p], qkv[r, D:2 * D].view(H, 64))
         assert torch.equal(vc[r, :, p], qkv[r, 2 * D:].view(H, 64))
+
+
+def test_decode_attention_dpp_bitwise(cuda):
+    """Variant 6 (DPP in-group reductions) performs the same additions in the same order as
+    variant 4 (ds_bpermute shuffles): outputs are bitwise equal."""
+    from zsaac import ops
+    from zsaac._lib import call
+    g = torch.Generator(device="cuda").manual_seed(6)
+    R, H, Lmax = 300, 12, 70
+    D = 64 * H
+    kc0 = torch.randn(R, H, Lmax, 64, device=cuda, generator=g).bfloat16()
+    vc0 = torch.randn(R, H, Lmax, 64, device=cuda, generator=g).bfloat16()
+    qkv = torch.randn(R, 3 * D, device=cuda, generator=g).bfloat16()
+    pos = torch.randint(0, Lmax, (R,), device=cuda, generator=g, dtype=torch.int32)
+    outs = []
+    for v in (4, 6):
+        kc, vc = kc0.clone(), vc0.clone()
+        out = torch.empty(R, D, device=cuda, dtype=torch.bfloat16)
+        call("zs_tune_set", b"decode_attn5", v)
+        try:
+            ops.decode_attention(qkv, R, D, H, kc, vc, Lmax, pos, out)
+        finally:
+            call("zs_tune_set", b"decode_attn5", 4)
+        outs.append(out)
+    assert torch.equal(outs[0], outs[1])
 
 
 @pytest.mark.parametrize("nrows", [1, 700, 2500])

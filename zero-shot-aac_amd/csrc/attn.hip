@@ -593,9 +593,26 @@ __global__ __launch_bounds__(256) void decode_attn5_kernel(const T* __restrict__
 // SIMD instead of 2) and any Lmax works.  The per-slot inputs (rowmap, compact position) are
 // loaded together with the qkv row: one dependent round trip before the K/V loads.  With one
 // phase (p < 64) the arithmetic equals decode_attn5's.
+// DPP lane exchanges for the reductions inside a wave (VALU, no LDS round trip):
+// xor 1 / xor 2 = quad_perm [1,0,3,2] / [2,3,0,1]; the other quad of an 8-lane group via
+// row_half_mirror (lane i <-> 7 - i), valid once the value is uniform within each quad; the other
+// 8-lane group of a 16-lane row via row_mirror (i <-> 15 - i), valid once uniform within groups
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xf, 0xf, false));
+}
+// sum over the 8 lanes of a group: the same additions, in the same order, as
+// s += shfl_xor(s, 1); s += shfl_xor(s, 2); s += shfl_xor(s, 4)  (bitwise equal results)
+__device__ __forceinline__ float group8_sum_dpp(float s) {
+  s += dpp_f<0xB1>(s);
+  s += dpp_f<0x4E>(s);
+  return s + dpp_f<0x141>(s);
+}
+
 // PF: the next phase's K/V loads are issued before the current phase's math (two phases in
-// flight per wave; the wait lands after the math instead of before it)
-template <typename T, int KPP = 64, bool PF = false>   // KPP: keys per phase (8 per key group)
+// flight per wave; the wait lands after the math instead of before it).  DPP: the in-group dot
+// product reduction and the first step of the cross-group max by DPP instead of ds_bpermute.
+template <typename T, int KPP = 64, bool PF = false, bool DPP = false>   // KPP: keys per phase
 __global__ __launch_bounds__(256) void decode_attn6_kernel(
     const T* __restrict__ qkv, int D, int heads, T* __restrict__ kc, T* __restrict__ vc, int Lmax,
     const int* __restrict__ pos, const int* __restrict__ kvrow, T* __restrict__ out,
@@ -664,13 +681,17 @@ __global__ __launch_bounds__(256) void decode_attn6_kernel(
       float sv = 0.f;
 #pragma unroll
       for (int t = 0; t < EPC; ++t) sv += q[t] * ldf(e + t);
-      sv += __shfl_xor(sv, 1, 64);
-      sv += __shfl_xor(sv, 2, 64);
-      sv += __shfl_xor(sv, 4, 64);
+      if (DPP) {
+        sv = group8_sum_dpp(sv);
+      } else {
+        sv += __shfl_xor(sv, 1, 64);
+        sv += __shfl_xor(sv, 2, 64);
+        sv += __shfl_xor(sv, 4, 64);
+      }
       sc[i] = (base + i * 8 + grp <= p) ? sv : -INFINITY;
       pm = fmaxf(pm, sc[i]);
     }
-    pm = fmaxf(pm, __shfl_xor(pm, 8, 64));
+    pm = fmaxf(pm, DPP ? dpp_f<0x140>(pm) : __shfl_xor(pm, 8, 64));
     pm = fmaxf(pm, __shfl_xor(pm, 16, 64));
     pm = fmaxf(pm, __shfl_xor(pm, 32, 64));
     const float mn = fmaxf(m, pm);
@@ -882,6 +903,11 @@ extern "C" int zs_decode_attention_map(const void* qkv, int R, const int* rowmap
     hipLaunchKernelGGL((decode_attn6_kernel<bf16_t, 16, true>), dim3(R, cdiv(heads, 4)), dim3(256),
                        0, S(stream), (const bf16_t*)qkv, D, heads, (bf16_t*)kc, (bf16_t*)vc, Lmax,
                        pos, (const int*)nullptr, (bf16_t*)out, rowmap, cpos, nphys);
+  } else if (g_decode_attn5 == 6) {
+    hipLaunchKernelGGL((decode_attn6_kernel<bf16_t, 16, false, true>), dim3(R, cdiv(heads, 4)),
+                       dim3(256), 0, S(stream), (const bf16_t*)qkv, D, heads, (bf16_t*)kc,
+                       (bf16_t*)vc, Lmax, pos, (const int*)nullptr, (bf16_t*)out, rowmap, cpos,
+                       nphys);
   } else {
     hipLaunchKernelGGL((decode_attn6_kernel<bf16_t, 32>), dim3(R, cdiv(heads, 4)), dim3(256), 0,
                        S(stream), (const bf16_t*)qkv, D, heads, (bf16_t*)kc, (bf16_t*)vc, Lmax,
@@ -902,6 +928,14 @@ extern "C" int zs_decode_attention(const void* qkv, int R, int D, int heads, voi
     hipLaunchKernelGGL((decode_attn6_kernel<bf16_t, 16>), dim3(R, cdiv(heads, 4)), dim3(256), 0,
                        S(stream), (const bf16_t*)qkv, D, heads, (bf16_t*)kc, (bf16_t*)vc, Lmax,
                        pos, kvrow, (bf16_t*)out, (const int*)nullptr, (const int*)nullptr, R);
+    ZS_LAUNCH_CHECK();
+    return 0;
+  }
+  if (dtype == ZS_BF16 && g_decode_attn5 == 6) {
+    hipLaunchKernelGGL((decode_attn6_kernel<bf16_t, 16, false, true>), dim3(R, cdiv(heads, 4)),
+                       dim3(256), 0, S(stream), (const bf16_t*)qkv, D, heads, (bf16_t*)kc,
+                       (bf16_t*)vc, Lmax, pos, kvrow, (bf16_t*)out, (const int*)nullptr,
+                       (const int*)nullptr, R);
     ZS_LAUNCH_CHECK();
     return 0;
   }
