@@ -86,6 +86,16 @@ int zs_gemm(int M, int N, int K, int dtype, const void* A, int lda, const void* 
 
 int zs_gemm_workspace_floats(int M, int N, int K);
 
+/* zs_gemm_ln: out[m][n] = act(sum_k LN(x[m])[k] * W[n][k] + bias[n]) + residual[m][n] for
+ *   M <= 64 rows (the GPT-2 decode step at the reference's eval batch of 64): LayerNorm over K
+ *   (eps; ln_w / ln_b f32) of the f32 rows x [M][ldx], rounded to bf16, times bf16 W [N][ldw].
+ *   Replaces the ln_1 -> attn.c_attn and ln_2 -> mlp.c_fc launch pairs of transformers'
+ *   GPT2Block (the zs_layernorm + zs_gemm sequence).  K % 128 == 0, K <= 1024; x, ln_w, ln_b
+ *   and W 16-byte aligned.  One launch, no workspace. */
+int zs_gemm_ln(int M, int N, int K, const float* x, int ldx, const float* ln_w, const float* ln_b,
+               float eps, const void* W, int ldw, const float* bias, const float* residual,
+               int ldr, void* out, int ldo, int out_dtype, int act, void* stream);
+
 /* zs_l2norm_rows: y = x / max(||x||_2, eps) per row (F.normalize, ase_model.py:54). in-place ok */
 int zs_l2norm_rows(const float* x, int M, int C, float eps, float* y, void* stream);
 

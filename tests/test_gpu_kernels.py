@@ -81,7 +81,18 @@ def test_gemm_lean_tiles(cuda, tile):
                                    (256, 2304, 768), (200, 768, 3072), (65, 3072, 768)])
 def test_gemm_skinny(cuda, dtype, M, N, K):
     """M <= 256 auto mode: weight-streaming split-K with in-kernel last-arriver reduction over
-    up to 4 row blocks of 64 (ragged last block)."""
+    up to 4 row blocks of 64 (ragged last block).  bf16 at M <= 64 takes the row-group kernel by
+    default (test_gemm_rows); it is switched off here so the skinny kernel stays covered."""
+    from zsaac import ops
+    from zsaac._lib import call
+    call("zs_tune_set", b"gemm_rows", 0)
+    try:
+        _gemm_skinny_body(cuda, dtype, M, N, K)
+    finally:
+        call("zs_tune_set", b"gemm_rows", 1)
+
+
+def _gemm_skinny_body(cuda, dtype, M, N, K):
     from zsaac import ops
     ops.reserve_skinny_workspace(cuda, M, N, K)
     g = torch.Generator(device="cuda").manual_seed(N + K)
@@ -109,6 +120,76 @@ def test_gemm_skinny(cuda, dtype, M, N, K):
         oi = torch.empty(M, N, device=cuda)
         ops.gemm(ai, wi, oi)
         assert torch.equal(oi, ai @ wi.t())
+
+
+@pytest.mark.parametrize("M", [1, 16, 37, 64])
+@pytest.mark.parametrize("N,K", [(2304, 768), (768, 768), (3072, 768), (768, 3072), (7680, 3840),
+                                 (1024, 768), (100, 1024)])
+def test_gemm_rows(cuda, M, N, K):
+    """bf16 M <= 64 auto mode = the row-group kernel (16-row groups x NT columns, full K per
+    workgroup, K split over its waves): epilogues, ragged rows / columns, exact small integers,
+    bitwise determinism, and a row's result independent of M."""
+    from zsaac import ops
+    g = torch.Generator(device="cuda").manual_seed(M * 31 + N + K)
+    a = torch.randn(M, K, device=cuda, generator=g).bfloat16()
+    w = torch.randn(N, K, device=cuda, generator=g).div(math.sqrt(K)).bfloat16()
+    bias = torch.randn(N, device=cuda, generator=g)
+    res = torch.randn(M, N, device=cuda, generator=g)
+    ref = a.float() @ w.float().t() + bias
+    out = torch.empty(M, N, device=cuda)
+    ops.gemm(a, w, out, bias=bias, act=ops.ACT_GELU_TANH)
+    assert _rel(out, torch.nn.functional.gelu(ref, approximate="tanh")) < 1e-2
+    ob = torch.empty(M, N, device=cuda, dtype=torch.bfloat16)
+    ops.gemm(a, w, ob, bias=bias, act=ops.ACT_TANH)
+    assert _rel(ob, torch.tanh(ref)) < 1e-2
+    out2 = res.clone()
+    ops.gemm(a, w, out2, bias=bias, residual=out2)
+    assert _rel(out2, ref + res) < 1e-2
+    o1 = torch.empty(M, N, device=cuda)
+    ops.gemm(a, w, o1, bias=bias)
+    assert _rel(o1, ref) < 1e-2
+    o2 = torch.empty_like(o1)
+    ops.gemm(a, w, o2, bias=bias)
+    assert torch.equal(o1, o2)
+    # rows do not interact: the first row alone gives the same bits
+    o3 = torch.empty(1, N, device=cuda)
+    ops.gemm(a[:1], w, o3, bias=bias)
+    assert torch.equal(o3[0], o1[0])
+    ai = torch.randint(-3, 4, (M, K), device=cuda, generator=g).bfloat16()
+    wi = torch.randint(-3, 4, (N, K), device=cuda, generator=g).bfloat16()
+    oi = torch.empty(M, N, device=cuda)
+    ops.gemm(ai, wi, oi)
+    assert torch.equal(oi, ai.float() @ wi.float().t())
+
+
+@pytest.mark.parametrize("M", [1, 20, 64])
+@pytest.mark.parametrize("N", [2304, 3072, 200])
+def test_gemm_ln(cuda, M, N):
+    """zs_gemm_ln = zs_layernorm (bf16 out) followed by the bf16 GEMM, in one launch."""
+    from zsaac import ops
+    K = 768
+    g = torch.Generator(device="cuda").manual_seed(M + N)
+    x = torch.randn(M, K, device=cuda, generator=g) * 3 + 0.5
+    x[:, 5] += 40.0                          # a GPT-2-like outlier dimension
+    lw = torch.randn(K, device=cuda, generator=g) * 0.2 + 1
+    lb = torch.randn(K, device=cuda, generator=g) * 0.1
+    w = torch.randn(N, K, device=cuda, generator=g).div(math.sqrt(K)).bfloat16()
+    bias = torch.randn(N, device=cuda, generator=g)
+    h = torch.nn.functional.layer_norm(x, (K,), lw, lb, 1e-5).bfloat16()
+    ref = h.float() @ w.float().t() + bias
+    out = torch.empty(M, N, device=cuda, dtype=torch.bfloat16)
+    ops.gemm_ln(x, lw, lb, w, out, bias=bias, act=ops.ACT_GELU_TANH)
+    assert _rel(out, torch.nn.functional.gelu(ref, approximate="tanh")) < 1e-2
+    out = torch.empty(M, N, device=cuda)
+    ops.gemm_ln(x, lw, lb, w, out, bias=bias)
+    assert _rel(out, ref) < 1e-2
+    # same bf16 LN rows as zs_layernorm -> the same GEMM inputs
+    h2 = torch.empty(M, K, device=cuda, dtype=torch.bfloat16)
+    ops.layernorm(x, lw, lb, out=h2)
+    assert float((h2.float() - h.float()).abs().max()) <= 2 ** -7 * float(h.float().abs().max())
+    o1 = torch.empty(1, N, device=cuda)
+    ops.gemm_ln(x[:1].contiguous(), lw, lb, w, o1, bias=bias)
+    assert torch.equal(o1[0], out[0])
 
 
 def test_gemm_f32_exact_small_ints(cuda):
@@ -274,14 +355,27 @@ def test_decode_attention_matches_prefill(cuda):
 
 
 @pytest.mark.parametrize("use_kvrow", [False, True])
-@pytest.mark.parametrize("variant", [6, 5, 4, 3, 2, 1, 0])
+@pytest.mark.parametrize("variant", ["small", 6, 5, 4, 3, 2, 1, 0])
 def test_decode_attention_bf16(cuda, use_kvrow, variant):
     """bf16 decode attention (register-resident decode_attn5, and the LDS-staged decode_attn4)
     vs an fp32 torch reference: ragged positions 0..Lmax-1 per row, optional beam kvrow
-    indirection, and the new token's k/v appended to the cache."""
+    indirection, and the new token's k/v appended to the cache.  "small" = the R <= 128 kernel
+    (64-key phases, next phase prefetched) the bs=64 decode takes; the numbered variants are the
+    large-R knobs (small_attn off)."""
     from zsaac import ops
     from zsaac._lib import call
     R, D, H, Lmax = 40, 768, 12, 103
+    call("zs_tune_set", b"small_attn", 1 if variant == "small" else 0)
+    try:
+        _decode_attention_bf16_body(cuda, use_kvrow, 4 if variant == "small" else variant,
+                                    R, D, H, Lmax)
+    finally:
+        call("zs_tune_set", b"small_attn", 1)
+
+
+def _decode_attention_bf16_body(cuda, use_kvrow, variant, R, D, H, Lmax):
+    from zsaac import ops
+    from zsaac._lib import call
     g = torch.Generator(device="cuda").manual_seed(11)
     kc = torch.randn(R, H, Lmax, 64, device=cuda, generator=g).bfloat16()
     vc = torch.randn(R, H, Lmax, 64, device=cuda, generator=g).bfloat16()
@@ -358,7 +452,17 @@ def test_compact_rows(cuda, nrows):
 def test_decode_map_kernels_match_direct(cuda):
     """The rowmap variants of embed_tokens / decode_attention / greedy_step on a compacted row
     set give, for every active row, bit-identical results to the direct kernels; padding slots
-    leave physical state untouched."""
+    leave physical state untouched.  (Compaction runs at >= 512 rows, where the direct decode
+    attention is the large-R kernel: small_attn is off here.)"""
+    from zsaac._lib import call
+    call("zs_tune_set", b"small_attn", 0)
+    try:
+        _decode_map_body(cuda)
+    finally:
+        call("zs_tune_set", b"small_attn", 1)
+
+
+def _decode_map_body(cuda):
     from zsaac import ops
     R, D, H, Lmax, V = 96, 768, 12, 100, 50257
     g = torch.Generator(device="cuda").manual_seed(3)

@@ -149,6 +149,29 @@ def bench_gemm_dbg():
               flush=True)
 
 
+def bench_rows():
+    """Row-group GEMM (M <= 64) and its LN-fused form at decode shapes vs rows / columns / K,
+    hot weights (graph-replayed back-to-back launches); launch floor for comparison."""
+    from zsaac import ops
+    dev = torch.device("cuda", 0)
+    t_empty = timeit(lambda: torch.cuda._sleep(0), reps=100) if False else None
+    x = torch.randn(64, 768, device=dev)
+    lw, lb = torch.ones(768, device=dev), torch.zeros(768, device=dev)
+    for N, K in ((768, 768), (2304, 768), (3072, 768), (768, 3072), (256, 768), (64, 768)):
+        w = (torch.randn(N, K, device=dev) * 0.02).bfloat16()
+        bias = torch.randn(N, device=dev)
+        r = {}
+        for M in (1, 16, 64):
+            a = torch.randn(M, K, device=dev).bfloat16()
+            o = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+            of = torch.empty(M, N, device=dev)
+            r[f"M{M}"] = timeit(lambda: ops.gemm(a, w, o))
+            r[f"M{M}+b+r"] = timeit(lambda: ops.gemm(a, w, of, bias=bias, residual=of))
+            if K == 768:
+                r[f"M{M}ln"] = timeit(lambda: ops.gemm_ln(x[:M], lw, lb, w, o, bias=bias))
+        print(f"rows N{N} K{K} " + "  ".join(f"{k}={v:6.2f}" for k, v in r.items()), flush=True)
+
+
 def bench_overhead():
     """Per-launch cost of tiny kernels in a graph-replayed chain (the floor every decode-step
     kernel pays): cast of 64 floats, LayerNorm at 64 / 2048 rows, a 128x128x64 GEMM."""
@@ -458,4 +481,4 @@ if __name__ == "__main__":
             call("zs_tune_set", k.encode(), int(v))
     which = sys.argv[1:] or ["gemm", "attn"]
     for wname in which:
-        {"gemm": bench_gemm, "gemm_m": bench_gemm_m, "gemm_htsat": bench_gemm_htsat, "gemm_dbg": bench_gemm_dbg, "lmhead": bench_lmhead, "overhead": bench_overhead, "front": bench_front, "window": bench_window, "decode_gemm": bench_decode_gemm, "attn": bench_attn, "inflight": bench_inflight, "buckets": bench_buckets, "compact_ab": bench_compact_ab, "host": bench_host}[wname]()
+        {"gemm": bench_gemm, "rows": bench_rows, "gemm_m": bench_gemm_m, "gemm_htsat": bench_gemm_htsat, "gemm_dbg": bench_gemm_dbg, "lmhead": bench_lmhead, "overhead": bench_overhead, "front": bench_front, "window": bench_window, "decode_gemm": bench_decode_gemm, "attn": bench_attn, "inflight": bench_inflight, "buckets": bench_buckets, "compact_ab": bench_compact_ab, "host": bench_host}[wname]()

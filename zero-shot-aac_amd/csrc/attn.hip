@@ -9,6 +9,7 @@
 
 namespace zs {
 
+int g_small_attn = 1;     // R <= 128: decode_attn6 with 128-key phases
 int g_decode_attn5 = 4;   // 5: decode_attn6 16-key phases + next-phase prefetch; 4/3/2: decode_attn6 (phases of 16/32/64 keys), 1: decode_attn5, 0: LDS
 int g_window_mfma = 1;    // zs_tune_set("window_mfma", 0): VALU window attention for bf16   // zs_tune_set("decode_attn5", 0): LDS-staged decode_attn4 for bf16
 
@@ -612,6 +613,25 @@ __device__ __forceinline__ float group8_sum_dpp(float s) {
 // PF: the next phase's K/V loads are issued before the current phase's math (two phases in
 // flight per wave; the wait lands after the math instead of before it).  DPP: the in-group dot
 // product reduction and the first step of the cross-group max by DPP instead of ds_bpermute.
+// 8 bf16 in a uint4 <-> 8 floats by bit operations (element t in the low / high half of word
+// t / 2): no type-punned pointer into a register array, which kept such arrays in scratch memory
+__device__ __forceinline__ void bf8_unpack(const uint4& u, float (&f)[8]) {
+  f[0] = __uint_as_float(u.x << 16); f[1] = __uint_as_float(u.x & 0xffff0000u);
+  f[2] = __uint_as_float(u.y << 16); f[3] = __uint_as_float(u.y & 0xffff0000u);
+  f[4] = __uint_as_float(u.z << 16); f[5] = __uint_as_float(u.z & 0xffff0000u);
+  f[6] = __uint_as_float(u.w << 16); f[7] = __uint_as_float(u.w & 0xffff0000u);
+}
+// component-wise select (a select of whole uint4 structs went through scratch memory)
+__device__ __forceinline__ uint4 sel_u4(bool c, const uint4& a, const uint4& b) {
+  return make_uint4(c ? a.x : b.x, c ? a.y : b.y, c ? a.z : b.z, c ? a.w : b.w);
+}
+__device__ __forceinline__ uint4 bf8_pack(const float (&f)[8]) {
+  return make_uint4((uint32_t)f2bf(f[0]) | ((uint32_t)f2bf(f[1]) << 16),
+                    (uint32_t)f2bf(f[2]) | ((uint32_t)f2bf(f[3]) << 16),
+                    (uint32_t)f2bf(f[4]) | ((uint32_t)f2bf(f[5]) << 16),
+                    (uint32_t)f2bf(f[6]) | ((uint32_t)f2bf(f[7]) << 16));
+}
+
 template <typename T, int KPP = 64, bool PF = false, bool DPP = false>   // KPP: keys per phase
 __global__ __launch_bounds__(256) void decode_attn6_kernel(
     const T* __restrict__ qkv, int D, int heads, T* __restrict__ kc, T* __restrict__ vc, int Lmax,
@@ -634,53 +654,67 @@ __global__ __launch_bounds__(256) void decode_attn6_kernel(
       *reinterpret_cast<uint4*>(out + (long)c * D + h * HD + sub * EPC) = make_uint4(0, 0, 0, 0);
     return;
   }
-  const int p = min(cpos ? p0 : pos[r], Lmax - 1);
+  // wave-uniform (one (row, head) per wave): scalar branches for the phase loop and prefetch
+  const int p = __builtin_amdgcn_readfirstlane(min(cpos ? p0 : pos[r], Lmax - 1));
   const long rh = ((long)r * heads + h) * Lmax;
   if (grp == 0) {
     *reinterpret_cast<uint4*>(kc + (rh + p) * HD + sub * EPC) = knu;
     *reinterpret_cast<uint4*>(vc + (rh + p) * HD + sub * EPC) = vnu;
   }
   float q[EPC];
-  {
-    const T* e = reinterpret_cast<const T*>(&qu);
+  bf8_unpack(qu, q);
 #pragma unroll
-    for (int t = 0; t < EPC; ++t) q[t] = ldf(e + t) * 0.125f;
-  }
+  for (int t = 0; t < EPC; ++t) q[t] *= 0.125f;
   float m = -INFINITY, sum = 0.f, o[EPC];
 #pragma unroll
   for (int t = 0; t < EPC; ++t) o[t] = 0.f;
-  auto load_phase = [&](int base, uint4 (&kr)[NG], uint4 (&vr)[NG]) {
+  // Branch-free phase load: every lane loads a valid cache slot (keys past p - 1 re-read slot
+  // min(j, p - 1), or slot 0 at p == 0) and the key is then chosen by value: cached for j < p,
+  // the new token for j == p, zero past it.  (Loads under a divergent `if` were each waited
+  // for inside their branch: one round trip per key group instead of one per phase.)
+  uint4 kr[NG], vr[NG], kx[NG], vx[NG];
+  // (beam: the kvrow source rows of the whole phase are loaded first, under one uniform branch)
+#define ZS_LOAD_PHASE(BASE, KA, VA)                                                            \
+  do {                                                                                         \
+    int jc[NG], srow[NG];                                                                      \
+    _Pragma("unroll") for (int i = 0; i < NG; ++i) {                                           \
+      jc[i] = max(min((BASE) + i * 8 + grp, p - 1), 0);                                        \
+      srow[i] = r;                                                                             \
+    }                                                                                          \
+    if (kvrow) {                                                                               \
+      _Pragma("unroll") for (int i = 0; i < NG; ++i) srow[i] = kvrow[(long)r * Lmax + jc[i]];  \
+    }                                                                                          \
+    _Pragma("unroll") for (int i = 0; i < NG; ++i) {                                           \
+      const long src = ((long)srow[i] * heads + h) * Lmax + jc[i];                             \
+      KA[i] = *reinterpret_cast<const uint4*>(kc + src * HD + sub * EPC);                      \
+      VA[i] = *reinterpret_cast<const uint4*>(vc + src * HD + sub * EPC);                      \
+    }                                                                                          \
+  } while (0)
+  if (PF) ZS_LOAD_PHASE(0, kr, vr);
+  for (int base = 0; base <= p; base += KPP) {
+    if (PF) {
+      if (base + KPP <= p) ZS_LOAD_PHASE(base + KPP, kx, vx);
+    } else {
+      ZS_LOAD_PHASE(base, kr, vr);
+    }
+    // the by-value key choice, applied where the phase is consumed (a prefetched phase is not
+    // waited for early)
 #pragma unroll
     for (int i = 0; i < NG; ++i) {
       const int j = base + i * 8 + grp;
-      kr[i] = make_uint4(0, 0, 0, 0);
-      vr[i] = make_uint4(0, 0, 0, 0);
-      if (j < p) {
-        const long src = kvrow ? ((long)kvrow[(long)r * Lmax + j] * heads + h) * Lmax : rh;
-        kr[i] = *reinterpret_cast<const uint4*>(kc + (src + j) * HD + sub * EPC);
-        vr[i] = *reinterpret_cast<const uint4*>(vc + (src + j) * HD + sub * EPC);
-      } else if (j == p) {
-        kr[i] = knu;
-        vr[i] = vnu;
-      }
-    }
-  };
-  uint4 kr[NG], vr[NG], kx[NG], vx[NG];
-  if (PF) load_phase(0, kr, vr);
-  for (int base = 0; base <= p; base += KPP) {
-    if (PF) {
-      if (base + KPP <= p) load_phase(base + KPP, kx, vx);
-    } else {
-      load_phase(base, kr, vr);
+      const uint4 z = make_uint4(0, 0, 0, 0);
+      kr[i] = sel_u4(j < p, kr[i], sel_u4(j == p, knu, z));
+      vr[i] = sel_u4(j < p, vr[i], sel_u4(j == p, vnu, z));
     }
     float sc[NG];
     float pm = -INFINITY;
 #pragma unroll
     for (int i = 0; i < NG; ++i) {
-      const T* e = reinterpret_cast<const T*>(&kr[i]);
+      float kf[EPC];
+      bf8_unpack(kr[i], kf);
       float sv = 0.f;
 #pragma unroll
-      for (int t = 0; t < EPC; ++t) sv += q[t] * ldf(e + t);
+      for (int t = 0; t < EPC; ++t) sv += q[t] * kf[t];
       if (DPP) {
         sv = group8_sum_dpp(sv);
       } else {
@@ -704,15 +738,17 @@ __global__ __launch_bounds__(256) void decode_attn6_kernel(
     for (int i = 0; i < NG; ++i) {
       const float e = (base + i * 8 + grp <= p) ? expf(sc[i] - m) : 0.f;
       sum += e;
-      const T* v = reinterpret_cast<const T*>(&vr[i]);
+      float vf[EPC];
+      bf8_unpack(vr[i], vf);
 #pragma unroll
-      for (int t = 0; t < EPC; ++t) o[t] += e * ldf(v + t);
+      for (int t = 0; t < EPC; ++t) o[t] += e * vf[t];
     }
     if (PF) {
 #pragma unroll
       for (int i = 0; i < NG; ++i) { kr[i] = kx[i]; vr[i] = vx[i]; }
     }
   }
+#undef ZS_LOAD_PHASE
 #pragma unroll
   for (int d = 8; d < 64; d <<= 1) {
     sum += __shfl_xor(sum, d, 64);
@@ -721,11 +757,10 @@ __global__ __launch_bounds__(256) void decode_attn6_kernel(
   }
   if (grp == 0) {
     const float inv = 1.0f / sum;
-    uint4 ou;
-    T* oe = reinterpret_cast<T*>(&ou);
+    float of[EPC];
 #pragma unroll
-    for (int t = 0; t < EPC; ++t) stf(oe + t, o[t] * inv);
-    *reinterpret_cast<uint4*>(out + (long)c * D + h * HD + sub * EPC) = ou;
+    for (int t = 0; t < EPC; ++t) of[t] = o[t] * inv;
+    *reinterpret_cast<uint4*>(out + (long)c * D + h * HD + sub * EPC) = bf8_pack(of);
   }
 }
 
@@ -924,6 +959,16 @@ extern "C" int zs_decode_attention(const void* qkv, int R, int D, int heads, voi
              "zs_decode_attention: head_dim must be 64");
   ZS_REQUIRE(Lmax > 0 && Lmax <= 4096, "zs_decode_attention: Lmax");
   dim3 grid(R, heads);
+  if (dtype == ZS_BF16 && R <= 128 && g_small_attn) {
+    // few waves (R x heads): nothing hides a phase's round trip, so take 128-key phases: every
+    // key of a row in flight at once, one HBM round trip at L <= 128
+    hipLaunchKernelGGL((decode_attn6_kernel<bf16_t, 128, false, true>), dim3(R, cdiv(heads, 4)),
+                       dim3(256), 0, S(stream), (const bf16_t*)qkv, D, heads, (bf16_t*)kc,
+                       (bf16_t*)vc, Lmax, pos, kvrow, (bf16_t*)out, (const int*)nullptr,
+                       (const int*)nullptr, R);
+    ZS_LAUNCH_CHECK();
+    return 0;
+  }
   if (dtype == ZS_BF16 && g_decode_attn5 == 4) {
     hipLaunchKernelGGL((decode_attn6_kernel<bf16_t, 16>), dim3(R, cdiv(heads, 4)), dim3(256), 0,
                        S(stream), (const bf16_t*)qkv, D, heads, (bf16_t*)kc, (bf16_t*)vc, Lmax,

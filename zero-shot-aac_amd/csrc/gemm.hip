@@ -819,6 +819,10 @@ extern "C" __attribute__((visibility("hidden"))) int zs_gemm_skinny_internal(
     const float* bias, const float* residual, int ldr, void* out, int ldo, int out_dtype, int act,
     float* workspace, void* stream);
 
+extern "C" __attribute__((visibility("hidden"))) int zs_gemm_rows_internal(
+    int M, int N, int K, const void* A, int lda, const void* W, int ldw, const float* bias,
+    const float* residual, int ldr, void* out, int ldo, int out_dtype, int act, void* stream);
+
 extern "C" int zs_gemm(int M, int N, int K, int dtype, const void* A, int lda, const void* W,
                        int ldw, const float* bias, const float* residual, int ldr, void* out,
                        int ldo, int out_dtype, int act, int split_k, float* workspace,
@@ -826,9 +830,17 @@ extern "C" int zs_gemm(int M, int N, int K, int dtype, const void* A, int lda, c
   ZS_REQUIRE(M >= 0 && N > 0 && K > 0, "zs_gemm: bad shape M=%d N=%d K=%d", M, N, K);
   ZS_REQUIRE(K % BK == 0, "zs_gemm: K=%d must be a multiple of 32", K);
   ZS_REQUIRE(lda % 8 == 0 && ldw % 8 == 0, "zs_gemm: lda/ldw must be multiples of 8");
+  // the tiled and skinny kernels load A and W rows with 16-byte LDS-DMA / vector loads
+  ZS_REQUIRE(((uintptr_t)A & 15) == 0 && ((uintptr_t)W & 15) == 0,
+             "zs_gemm: A and W must be 16-byte aligned");
   ZS_REQUIRE(split_k >= 0, "zs_gemm: split_k >= 0");
   ZS_REQUIRE(dtype == ZS_F32 || dtype == ZS_BF16, "zs_gemm: dtype");
   if (M == 0) return 0;
+  if (split_k == 0 && dtype == ZS_BF16 && M <= 64) {   // decode-sized: row-group kernel
+    const int rc = zs_gemm_rows_internal(M, N, K, A, lda, W, ldw, bias, residual, ldr, out, ldo,
+                                         out_dtype, act, stream);
+    if (rc <= 0) return rc;                             // 1 = shape not covered
+  }
   if (split_k == 0) {   // auto: weight-streaming skinny kernel for decode-sized M
     // M <= 64 always; up to 256 rows only where the tiled kernel has too few blocks to cover
     // a long K (mproj-like shapes); everything else goes to the tiled kernel
@@ -866,6 +878,8 @@ extern "C" int zs_lmhead_topk(int M, int K, int V, int dtype, const void* A, int
                               float* part_val, int* part_idx, void* stream) {
   ZS_REQUIRE(M > 0 && K > 0 && V > 0, "zs_lmhead_topk: bad shape");
   ZS_REQUIRE(K % BK == 0 && lda % 8 == 0, "zs_lmhead_topk: K %% 32, lda %% 8");
+  ZS_REQUIRE(((uintptr_t)A & 15) == 0 && ((uintptr_t)W & 15) == 0,
+             "zs_lmhead_topk: A and W must be 16-byte aligned");
   ZS_REQUIRE(topk >= 1 && topk <= MAXK, "zs_lmhead_topk: 1 <= topk <= 8");
   hipStream_t st = S(stream);
   const int nblk = cdiv(V, LM_BN);

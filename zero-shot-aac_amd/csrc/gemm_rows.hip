@@ -1,0 +1,304 @@
+// Row-group GEMM for M <= 64 rows (the GPT-2 decode step at the reference's eval batch of 64,
+// the mapper and audio_proj at small batches), bf16 operands, f32 accumulation.
+//
+// At 64 rows a decode-step GEMM moves 1-5 MB of weights and almost no flops: its time is the
+// dependency chain of one launch (dispatch, first loads, reduction, stores), not bandwidth.  The
+// split-K skinny kernel (gemm_skinny.hip) pays two extra chip-wide round trips for its slab
+// reduction (sc1 slab stores -> atomic ticket -> slab loads by the last arriver).  Here the
+// parallelism comes from the ROWS instead: a work unit is (16-row group, NT-column tile) with the
+// full K in one workgroup; the K range is split over the workgroup's waves only, whose partials
+// are summed through LDS.  No global slabs, no atomics, one round trip from the first load to the
+// store.  The 4 row groups of a column tile are consecutive work units on one XCD (bijective
+// remap, cdna_hip_programming.md §5 T1), so the weight tile they share crosses HBM once.
+//
+// LN mode (zs_gemm_ln): the A operand is LayerNorm(x) of the f32 residual stream, computed in the
+// prologue: the workgroup loads its 16 rows of x (48 KB at C = 768) while its weight loads are in
+// flight, forms mean / variance in registers (two passes over the held values), and writes the
+// normalised bf16 rows to LDS, from where the waves read their MFMA A fragments.  This replaces
+// GPT-2's ln_1 -> c_attn and ln_2 -> c_fc launch pairs (transformers GPT2Block, eps 1e-5).
+//
+// MFMA: v_mfma_f32_16x16x32_bf16; lane l holds A[row l&15][k 8(l>>4)..+8] and
+// W[n l&15][k 8(l>>4)..+8] (B = W^T), C col = l&15, rows 4(l>>4)+i.
+// Per-row arithmetic depends only on (N, K): a row's result does not depend on M or on its row
+// group, so a clip's result does not depend on how many clips share the launch.
+#include "common.h"
+
+namespace zs {
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8r_t;
+typedef __attribute__((ext_vector_type(4))) float f32x4r_t;
+
+constexpr int RG = 16;              // rows per group
+constexpr int RG_MAX_M = 64;
+constexpr int RG_MAX_LOADS = 36;    // 16-byte loads in flight per lane (VGPR budget)
+
+struct RowsArgs {
+  int M, N, K;
+  const bf16_t* A; int lda;                 // bf16 A operand (plain mode)
+  const float* X; int ldx;                  // f32 rows (LN mode)
+  const float* ln_w; const float* ln_b; float eps;
+  const bf16_t* W; int ldw;
+  const float* bias;
+  const float* residual; int ldr;
+  void* out; int ldo; int out_dtype; int act;
+  int rgroups, ntiles;
+};
+
+template <int NT, int WAVES, bool LN, int S>
+__global__ __launch_bounds__(64 * WAVES) void gemm_rows_kernel(RowsArgs g) {
+  // S = 32-deep k-steps per wave (K = 32 * WAVES * S), a template parameter so that every load
+  // is issued unconditionally and up front (a runtime trip count put each load in its own
+  // branch and the compiler waited for it there: one round trip per load)
+  constexpr int NB = NT / 16;
+  constexpr int NTHR = 64 * WAVES;
+  constexpr int K = 32 * WAVES * S, KW = K / WAVES;
+  static_assert(S * (LN ? NB : NB + 1) <= RG_MAX_LOADS, "rows kernel: VGPR budget");
+  // LDS: [LN rows: 16 x (K + 8) bf16] [partials: WAVES x 16 x NT f32]
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  // XCD-aware bijective remap: blocks id, id+8, ... share an XCD -> consecutive work units
+  const int nwg = gridDim.x, id = blockIdx.x, xcd = id & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int u = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (id >> 3);
+  const int rg = u % g.rgroups, tile = u / g.rgroups;
+  const int m0 = rg * RG, n0 = tile * NT;
+  const int kw = wid * KW;
+  constexpr int ldh = K + 8;                // padded LDS row (conflict-free b128 fragment reads)
+  bf16_t* hs = reinterpret_cast<bf16_t*>(smem);
+  float* red = reinterpret_cast<float*>(smem + (LN ? RG * ldh * 2 : 0));
+
+  const int fr = lane & 15, fk = 8 * (lane >> 4);
+  // rows / columns past M / N load the last valid row / column (every load unconditional);
+  // their outputs are never stored
+  const int am = min(m0 + fr, g.M - 1);
+
+  // weight fragments for every k-step of this wave, issued first (they do not depend on x)
+  bf16x8r_t b[S * NB];
+  bf16x8r_t a[LN ? 1 : S];
+  const bf16_t* wrow[NB];
+#pragma unroll
+  for (int nb = 0; nb < NB; ++nb) wrow[nb] = g.W + (long)min(n0 + 16 * nb + fr, g.N - 1) * g.ldw;
+#pragma unroll
+  for (int s = 0; s < S; ++s) {
+    const int k = kw + 32 * s + fk;
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb)
+      b[s * NB + nb] = *reinterpret_cast<const bf16x8r_t*>(wrow[nb] + k);
+    if constexpr (!LN) a[s] = *reinterpret_cast<const bf16x8r_t*>(g.A + (long)am * g.lda + k);
+  }
+  // epilogue operands (one column quad of one row per thread), fetched now so their latency
+  // hides under the operand loads; loads clamped in range, masked by value
+  constexpr int NQ = NT / 4;
+  static_assert(RG * NQ <= NTHR, "one epilogue quad per thread");
+  const bool epi = threadIdx.x < RG * NQ;
+  const int erow = threadIdx.x / NQ, ecq = threadIdx.x % NQ;
+  const int em = m0 + erow, en = n0 + 4 * ecq;
+  float4 eb = make_float4(0.f, 0.f, 0.f, 0.f), er = eb;
+  if (epi) {
+    if (g.bias) {
+      eb.x = g.bias[min(en, g.N - 1)];     eb.y = g.bias[min(en + 1, g.N - 1)];
+      eb.z = g.bias[min(en + 2, g.N - 1)]; eb.w = g.bias[min(en + 3, g.N - 1)];
+    }
+    if (g.residual) {
+      const float* rr = g.residual + (long)min(em, g.M - 1) * g.ldr;
+      er.x = rr[min(en, g.N - 1)];     er.y = rr[min(en + 1, g.N - 1)];
+      er.z = rr[min(en + 2, g.N - 1)]; er.w = rr[min(en + 3, g.N - 1)];
+    }
+  }
+  // LN operands: 16 rows, TPR threads per row, NV float4 per thread (column quads t, t+TPR, ..)
+  constexpr int TPR = NTHR / RG, NV = LN ? K / (4 * TPR) : 1;
+  static_assert(!LN || K % (4 * TPR) == 0, "LN rows: K % (4 * threads per row)");
+  const int lr = threadIdx.x / TPR, lt = threadIdx.x % TPR;
+  float4 xv[NV], lw[NV], lb[NV];
+  if constexpr (LN) {
+    const float4* xr = reinterpret_cast<const float4*>(g.X + (long)min(m0 + lr, g.M - 1) * g.ldx);
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      xv[i] = xr[lt + TPR * i];
+      lw[i] = reinterpret_cast<const float4*>(g.ln_w)[lt + TPR * i];
+      lb[i] = reinterpret_cast<const float4*>(g.ln_b)[lt + TPR * i];
+    }
+  }
+  // keep every load above in flight before any of them is used (the scheduler otherwise sinks
+  // loads next to their MFMAs and waits on each group)
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+
+  if constexpr (LN) {
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) s += (xv[i].x + xv[i].y) + (xv[i].z + xv[i].w);
+#pragma unroll
+    for (int o = TPR / 2; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+    const float mean = s * (1.0f / K);
+    float q = 0.f;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const float a0 = xv[i].x - mean, a1 = xv[i].y - mean, a2 = xv[i].z - mean, a3 = xv[i].w - mean;
+      q += (a0 * a0 + a1 * a1) + (a2 * a2 + a3 * a3);
+    }
+#pragma unroll
+    for (int o = TPR / 2; o > 0; o >>= 1) q += __shfl_xor(q, o, 64);
+    const float rstd = rsqrtf(q * (1.0f / K) + g.eps);
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int c = lt + TPR * i;
+      uint2 pk;
+      pk.x = (uint32_t)f2bf((xv[i].x - mean) * rstd * lw[i].x + lb[i].x) |
+             ((uint32_t)f2bf((xv[i].y - mean) * rstd * lw[i].y + lb[i].y) << 16);
+      pk.y = (uint32_t)f2bf((xv[i].z - mean) * rstd * lw[i].z + lb[i].z) |
+             ((uint32_t)f2bf((xv[i].w - mean) * rstd * lw[i].w + lb[i].w) << 16);
+      *reinterpret_cast<uint2*>(hs + lr * ldh + 4 * c) = pk;
+    }
+    __syncthreads();
+  }
+
+  f32x4r_t acc[NB];
+#pragma unroll
+  for (int nb = 0; nb < NB; ++nb) acc[nb] = f32x4r_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int s = 0; s < S; ++s) {
+    bf16x8r_t af;
+    if constexpr (LN)
+      af = *reinterpret_cast<const bf16x8r_t*>(hs + fr * ldh + kw + 32 * s + fk);
+    else
+      af = a[s];
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb)
+      acc[nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, b[s * NB + nb], acc[nb], 0, 0, 0);
+  }
+
+  // wave partials -> LDS [wave][row][col], summed in wave order
+  float* mine = red + wid * RG * NT;
+#pragma unroll
+  for (int nb = 0; nb < NB; ++nb)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) mine[(4 * (lane >> 4) + i) * NT + 16 * nb + fr] = acc[nb][i];
+  __syncthreads();
+  if (!epi) return;
+  float4 sum = *reinterpret_cast<const float4*>(red + erow * NT + 4 * ecq);
+#pragma unroll
+  for (int w = 1; w < WAVES; ++w) {
+    const float4 p = *reinterpret_cast<const float4*>(red + (w * RG + erow) * NT + 4 * ecq);
+    sum.x += p.x; sum.y += p.y; sum.z += p.z; sum.w += p.w;
+  }
+  if (em >= g.M) return;
+  float v[4] = {sum.x + eb.x, sum.y + eb.y, sum.z + eb.z, sum.w + eb.w};
+  const bool bf = g.out_dtype == ZS_BF16;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) v[j] = bf ? act_apply_fast(v[j], g.act) : act_apply(v[j], g.act);
+  v[0] += er.x; v[1] += er.y; v[2] += er.z; v[3] += er.w;
+  if (en + 3 < g.N && (g.ldo & 3) == 0 && ((uintptr_t)g.out & 15) == 0) {
+    if (bf) {
+      uint2 pk;
+      pk.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+      pk.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+      *reinterpret_cast<uint2*>(reinterpret_cast<bf16_t*>(g.out) + (long)em * g.ldo + en) = pk;
+    } else {
+      *reinterpret_cast<float4*>(reinterpret_cast<float*>(g.out) + (long)em * g.ldo + en) =
+          make_float4(v[0], v[1], v[2], v[3]);
+    }
+  } else {
+    for (int j = 0; j < 4; ++j) {
+      if (en + j >= g.N) break;
+      if (bf) reinterpret_cast<bf16_t*>(g.out)[(long)em * g.ldo + en + j] = f2bf(v[j]);
+      else reinterpret_cast<float*>(g.out)[(long)em * g.ldo + en + j] = v[j];
+    }
+  }
+}
+
+int g_gemm_rows = 1;   // A/B knob (zs_tune_set "gemm_rows"): 0 = skinny split-K kernel for M <= 64
+
+// shape plan: waves (K split), k-steps per wave, column tile; waves < 0 when not covered
+struct RowsPlan { int waves, steps, nt; };
+static RowsPlan rows_plan(int N, int K, bool ln) {
+  const int waves = K >= 2048 ? 8 : 4;
+  if (K % (32 * waves)) return {-1, 0, 0};
+  const int S = K / (32 * waves);
+  const bool ok = ln ? (waves == 4 && (S == 6 || S == 8))
+                     : (waves == 4 ? (S == 2 || S == 4 || S == 6 || S == 8 || S == 12)
+                                   : (S == 8 || S == 12 || S == 15 || S == 16));
+  if (!ok) return {-1, 0, 0};
+  const int per = ln ? 2 : 3;               // loads per k-step at NT = 32
+  if (S * per <= RG_MAX_LOADS && N >= 1536) return {waves, S, 32};
+  return {waves, S, 16};
+}
+
+template <bool LN, int NT, int W, int S>
+static void launch_rows_k(const RowsArgs& g, dim3 grid, size_t lds, hipStream_t st) {
+  if constexpr (S * (LN ? NT / 16 : NT / 16 + 1) <= RG_MAX_LOADS)   // rows_plan never asks more
+    hipLaunchKernelGGL((gemm_rows_kernel<NT, W, LN, S>), grid, dim3(64 * W), lds, st, g);
+}
+
+template <bool LN, int NT, int W>
+static void launch_rows_s(const RowsArgs& g, int S, dim3 grid, size_t lds, hipStream_t st) {
+#define RL(S_) launch_rows_k<LN, NT, W, S_>(g, grid, lds, st)
+  if constexpr (LN) {
+    if (S == 6) RL(6); else RL(8);
+  } else if constexpr (W == 4) {
+    switch (S) { case 2: RL(2); break; case 4: RL(4); break; case 6: RL(6); break;
+                 case 8: RL(8); break; default: RL(12); }
+  } else {
+    switch (S) { case 8: RL(8); break; case 12: RL(12); break; case 15: RL(15); break;
+                 default: RL(16); }
+  }
+#undef RL
+}
+
+template <bool LN>
+static int launch_rows(const RowsArgs& g0, RowsPlan p, hipStream_t st) {
+  RowsArgs g = g0;
+  g.rgroups = cdiv(g.M, RG);
+  g.ntiles = cdiv(g.N, p.nt);
+  const dim3 grid(g.rgroups * g.ntiles);
+  const size_t lds = (LN ? (size_t)RG * (g.K + 8) * 2 : 0) + (size_t)p.waves * RG * p.nt * 4;
+  if constexpr (LN) {                       // rows_plan: LN at 4 waves only
+    if (p.nt == 32) launch_rows_s<LN, 32, 4>(g, p.steps, grid, lds, st);
+    else launch_rows_s<LN, 16, 4>(g, p.steps, grid, lds, st);
+  } else if (p.nt == 32) {
+    if (p.waves == 8) launch_rows_s<LN, 32, 8>(g, p.steps, grid, lds, st);
+    else launch_rows_s<LN, 32, 4>(g, p.steps, grid, lds, st);
+  } else {
+    if (p.waves == 8) launch_rows_s<LN, 16, 8>(g, p.steps, grid, lds, st);
+    else launch_rows_s<LN, 16, 4>(g, p.steps, grid, lds, st);
+  }
+  ZS_LAUNCH_CHECK();
+  return 0;
+}
+
+}  // namespace zs
+
+using namespace zs;
+
+// used by zs_gemm (auto mode) for bf16 M <= 64; returns 1 when the shape is not covered
+extern "C" __attribute__((visibility("hidden"))) int zs_gemm_rows_internal(
+    int M, int N, int K, const void* A, int lda, const void* W, int ldw, const float* bias,
+    const float* residual, int ldr, void* out, int ldo, int out_dtype, int act, void* stream) {
+  if (!g_gemm_rows || M > RG_MAX_M || (lda & 7) || (ldw & 7)) return 1;
+  const RowsPlan p = rows_plan(N, K, false);
+  if (p.waves < 0) return 1;
+  RowsArgs g{};
+  g.M = M; g.N = N; g.K = K; g.A = (const bf16_t*)A; g.lda = lda; g.W = (const bf16_t*)W;
+  g.ldw = ldw; g.bias = bias; g.residual = residual; g.ldr = ldr; g.out = out; g.ldo = ldo;
+  g.out_dtype = out_dtype; g.act = act;
+  return launch_rows<false>(g, p, S(stream));
+}
+
+extern "C" int zs_gemm_ln(int M, int N, int K, const float* x, int ldx, const float* ln_w,
+                          const float* ln_b, float eps, const void* W, int ldw, const float* bias,
+                          const float* residual, int ldr, void* out, int ldo, int out_dtype,
+                          int act, void* stream) {
+  ZS_REQUIRE(M > 0 && M <= RG_MAX_M && N > 0 && K > 0, "zs_gemm_ln: M in 1..%d (got M=%d N=%d K=%d)",
+             RG_MAX_M, M, N, K);
+  ZS_REQUIRE(x && ln_w && ln_b && W && out, "zs_gemm_ln: null pointer");
+  ZS_REQUIRE(ldx % 4 == 0 && ((uintptr_t)x & 15) == 0 && ((uintptr_t)ln_w & 15) == 0 &&
+             ((uintptr_t)ln_b & 15) == 0, "zs_gemm_ln: x / LN params must be 16-byte aligned");
+  ZS_REQUIRE(ldw % 8 == 0 && ((uintptr_t)W & 15) == 0, "zs_gemm_ln: W must be 16-byte aligned");
+  ZS_REQUIRE(out_dtype == ZS_BF16 || out_dtype == ZS_F32, "zs_gemm_ln: out dtype");
+  const RowsPlan p = rows_plan(N, K, true);
+  ZS_REQUIRE(p.waves > 0, "zs_gemm_ln: unsupported K=%d (768 or 1024)", K);
+  RowsArgs g{};
+  g.M = M; g.N = N; g.K = K; g.X = x; g.ldx = ldx; g.ln_w = ln_w; g.ln_b = ln_b; g.eps = eps;
+  g.W = (const bf16_t*)W; g.ldw = ldw; g.bias = bias; g.residual = residual; g.ldr = ldr;
+  g.out = out; g.ldo = ldo; g.out_dtype = out_dtype; g.act = act;
+  return launch_rows<true>(g, p, S(stream));
+}

@@ -227,11 +227,13 @@ __global__ __launch_bounds__(256) void greedy_step_kernel(
   if (lane == 0) s_alive[wid] = alive;
   __syncthreads();
   if (threadIdx.x == 0) {
-    const int a = s_alive[0] + s_alive[1] + s_alive[2] + s_alive[3];
-    const int old = __hip_atomic_fetch_add(&all_done[1], 1 + (a << 16), __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_AGENT);
-    if ((old & 0xffff) == (int)gridDim.x - 1) {
-      const int total = (old >> 16) + a;
+    // unsigned: the alive field (bits 16-31) holds up to 65535 rows (R < 65536 at the ABI)
+    const unsigned a = s_alive[0] + s_alive[1] + s_alive[2] + s_alive[3];
+    const unsigned old = __hip_atomic_fetch_add(reinterpret_cast<unsigned*>(&all_done[1]),
+                                                1u + (a << 16), __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_AGENT);
+    if ((old & 0xffffu) == gridDim.x - 1) {
+      const int total = (int)((old >> 16) + a);
       all_done[0] = (total == 0 || step + 1 >= max_steps) ? 1 : 0;
       all_done[2] = total;             // rows still decoding (sizes the next compacted chunk)
       __hip_atomic_store(step_ctr, step + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

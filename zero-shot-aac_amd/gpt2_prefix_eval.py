@@ -51,29 +51,37 @@ def _check_temperature(temperature):
 def generate2(model, tokenizer, tokens=None, prompt=None, embed=None, entry_count=1, entry_length=67,
               top_p=0.8, temperature=1., stop_token: str = '.'):
     """Greedy: the top-p filter never removes the highest-probability token, so the pick is the
-    argmax (gpt2_prefix_eval.py:194-212); stop after appending ``stop_token`` or 764 (' .')."""
+    argmax (gpt2_prefix_eval.py:194-212); stop after appending ``stop_token`` or 764 (' .').
+    Like the reference, the returned text starts with the prompt tokens (``tokens`` or the
+    encoded ``prompt``) when no ``embed`` is given (lines 182-184, 209-210, 218)."""
     _check_temperature(temperature)
     if embed is None:
         if tokens is None:
             tokens = torch.tensor(tokenizer.encode(prompt)).unsqueeze(0)
         dev = next(model.parameters()).device
         embed = model.gpt.transformer.wte(tokens.to(dev))
+    head = [] if tokens is None else [int(t) for t in torch.as_tensor(tokens).reshape(-1).tolist()]
     stop = tokenizer.encode(stop_token)[0]
     dec, P = _decoder(model, embed, entry_length, 1)
     dec.prefill(1, P)
     dec.stop0 = stop
     ids, ln = dec.greedy(1, P)
-    out = ids[0, :int(ln[0])].tolist()
+    out = head + ids[0, :int(ln[0])].tolist()
     return tokenizer.decode(out)
 
 
 def generate_beam(model, tokenizer, beam_size: int = 5, prompt=None, embed=None, entry_length=67,
                   temperature=1., stop_token: str = '.') -> List[str]:
     """Length-normalised beam search with log(softmax) scores, stopped beams extended by id 0 at
-    zero cost; texts sorted by score/length descending (gpt2_prefix_eval.py:99-158)."""
+    zero cost; texts sorted by score/length descending (gpt2_prefix_eval.py:99-158).  With a
+    ``prompt`` and no ``embed`` each beam's token row starts with the prompt ids and is cut at
+    ``seq_length`` (which counts generated tokens only), as the reference does (lines 112-130,
+    154-155)."""
     _check_temperature(temperature)
+    head = []
     if embed is None:
         tokens = torch.tensor(tokenizer.encode(prompt)).unsqueeze(0)
+        head = [int(t) for t in tokens.reshape(-1).tolist()]
         dev = next(model.parameters()).device
         embed = model.gpt.transformer.wte(tokens.to(dev))
     stop = tokenizer.encode(stop_token)[0]
@@ -82,7 +90,7 @@ def generate_beam(model, tokenizer, beam_size: int = 5, prompt=None, embed=None,
     dec.stop0 = stop
     ids, ln, sc = dec.beam(1, beam_size, P)
     ids, ln, sc = ids[0].cpu(), ln[0].cpu(), sc[0].cpu()
-    texts = [tokenizer.decode(ids[i, :int(ln[i])].tolist()) for i in range(beam_size)]
+    texts = [tokenizer.decode((head + ids[i].tolist())[:int(ln[i])]) for i in range(beam_size)]
     order = (sc / ln).argsort(descending=True)
     return [texts[i] for i in order]
 

@@ -267,6 +267,17 @@ class Gpt2Decoder:
     # ---------------------------------------------------------------- blocks
     def _layers(self, M, attn_fn):
         x = self.x[:M]
+        if self.dtype == torch.bfloat16 and M <= 64:
+            # decode at the reference's eval batch: LayerNorm fused into the c_attn / c_fc
+            # launches (zs_gemm_ln), row-group GEMMs for the projections (5 launches per block)
+            for l, ly in enumerate(self.w.layers):
+                qkv, att, hid = self.qkv[:M], self.att[:M], self.hid[:M]
+                ops.gemm_ln(x, *ly["ln1"], ly["attn_w"], qkv, bias=ly["attn_b"])
+                attn_fn(l, qkv, att)
+                ops.gemm(att, ly["proj_w"], x, bias=ly["proj_b"], residual=x, workspace=self.ws)
+                ops.gemm_ln(x, *ly["ln2"], ly["fc_w"], hid, bias=ly["fc_b"], act=ops.ACT_GELU_TANH)
+                ops.gemm(hid, ly["mproj_w"], x, bias=ly["mproj_b"], residual=x, workspace=self.ws)
+            return
         for l, ly in enumerate(self.w.layers):
             h, qkv, att, hid = self.h[:M], self.qkv[:M], self.att[:M], self.hid[:M]
             ops.layernorm(x, *ly["ln1"], out=h)

@@ -143,7 +143,9 @@ def gemm(a, w, out, bias=None, residual=None, act=ACT_NONE, split_k=0, workspace
             # larger M simply takes the tiled kernel
             _need(M > 64, f"gemm: workspace {workspace.numel()} < {need} floats")
             workspace = None
-        if workspace is None:
+        # bf16 M <= 64 keeps auto mode without a workspace: zs_gemm takes the row-group kernel
+        # (no workspace), and the tiled kernel for shapes that kernel does not cover
+        if workspace is None and not (a.dtype == torch.bfloat16 and M <= 64):
             split_k = 1
     lda = a.stride(-2) if a.dim() > 1 else K
     ldo = out.stride(-2) if out.dim() > 1 else N
@@ -152,6 +154,22 @@ def gemm(a, w, out, bias=None, residual=None, act=ACT_NONE, split_k=0, workspace
     _need(residual is None or residual.dtype == torch.float32, "gemm: residual must be f32")
     call("zs_gemm", M, N, K, dt(a), _p(a), lda, _p(w), w.stride(0), _p(bias), _p(residual), ldr,
          _p(out), ldo, dt(out), act, split_k, _p(workspace), _s())
+    return out
+
+
+def gemm_ln(x, ln_w, ln_b, w, out, bias=None, residual=None, act=ACT_NONE, eps=1e-5):
+    """out = act(LayerNorm(x) @ w.T + bias) + residual in one launch (zs_gemm_ln): x [M, K] f32
+    rows (M <= 64), w [N, K] bf16.  The LN output is rounded to bf16 like the zs_layernorm ->
+    zs_gemm pair it replaces."""
+    M, K = x.shape
+    N = w.shape[0]
+    _need(w.shape[1] == K and w.dtype == torch.bfloat16 and x.dtype == torch.float32,
+          f"gemm_ln: x{tuple(x.shape)} {x.dtype} w{tuple(w.shape)} {w.dtype}")
+    _need(bias is None or bias.dtype == torch.float32, "gemm_ln: bias must be f32")
+    _need(residual is None or residual.dtype == torch.float32, "gemm_ln: residual must be f32")
+    ldr = residual.stride(0) if residual is not None else 0
+    call("zs_gemm_ln", M, N, K, _p(x), x.stride(0), _p(ln_w), _p(ln_b), float(eps), _p(w),
+         w.stride(0), _p(bias), _p(residual), ldr, _p(out), out.stride(0), dt(out), act, _s())
     return out
 
 

@@ -289,7 +289,7 @@ class ConcurrentRunner:
                     self.decode_steps[bi] = 1 + n * p.decoder.chunk
                     with torch.cuda.stream(s):
                         r = p.result()
-                        results[bi] = _copy_batch(r)
+                        results[bi] = _copy_batch(r, caller)
                         if keep is not None:
                             keep(results[bi])
                     del active[i]
@@ -305,7 +305,16 @@ class ConcurrentRunner:
         return results
 
 
-def _copy_batch(r: CaptionBatch) -> CaptionBatch:
-    c = lambda t: None if t is None else t.clone()
+def _copy_batch(r: CaptionBatch, consumer=None) -> CaptionBatch:
+    """Clones of a result, made on the current (pipeline) stream; ``consumer`` is the stream
+    that will read and free them, recorded so the caching allocator does not recycle the blocks
+    for the pipeline stream while consumer-stream kernels may still read them."""
+    def c(t):
+        if t is None:
+            return None
+        t = t.clone()
+        if consumer is not None:
+            t.record_stream(consumer)
+        return t
     return CaptionBatch(c(r.ids), c(r.lengths), c(r.scores), c(r.hard_ids), c(r.hard_len),
                         c(r.plen), c(r.prefix_ids), c(r.clap_emb))
