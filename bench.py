@@ -3,70 +3,114 @@
 
     audio clips/sec end-to-end (encode + mapper + GPT-2 decode), Clotho-eval bs=64
 
-Workload (BASELINE.json configs[1], "C2"): synthetic 10 s / 32 kHz waveforms (randn*0.1, clipped)
-already resident in HBM -> STFT/log-mel + bn0 -> HTSAT -> audio_proj + L2 -> sound-effect hard
-prompt -> MLP mapper -> GPT-2 small prefill + get_prefix_tokens + greedy generate2
-(entry_length 67, stop ids 13/764), bf16 operands / f32 accumulation, batch 64 clips per GPU.
-One "step" = one batch of 64 clips through the whole path on every rank.  --inflight (default 4)
-independent bs=64 batches are decoded concurrently per GPU on separate HIP streams (pipeline
-twins sharing the weights, zsaac/pipeline.py ConcurrentRunner) — the batch size the reference
-evaluates with stays 64; the GPU just works on several such batches at once.  After the K timed
-steps, ONE RCCL all-gather of every batch's generated token ids + lengths (the only collective,
-SURVEY §8e) is inside the timed region.  Weights are seeded random init at the reference
-architecture (no checkpoints offline).
+Headline (BASELINE.json configs[1], "C2"): a Clotho-eval-sized set of 1045 synthetic 10 s / 32 kHz
+waveforms per rank (randn*0.1, clipped), resident in HBM before the timed region, captioned in
+eval batches of 64 clips exactly as the reference evaluates them: STFT/log-mel + bn0 -> HTSAT ->
+audio_proj + L2 -> sound-effect hard prompt -> MLP mapper -> GPT-2 small prefill +
+get_prefix_tokens + greedy generate2 (entry_length 67, stop ids 13 / 764), bf16 operands / f32
+accumulation.  Every decode GEMM of a batch is a 64-row GEMM.  One "step" = one eval batch of
+64 clips (the last batch of the 1045 holds 21).  --inflight independent batches (default 4) are
+in flight per GPU, each on its own HIP stream (pipeline twins sharing the weights,
+zsaac/pipeline.py ConcurrentRunner); GPU_MAX_HW_QUEUES is raised to --hw-queues (default 8, the
+runtime allows up to 32) so those streams get hardware queues of their own.  With N ranks the
+clips are sharded (zsaac/dist.py shard_range) and ONE RCCL all-gather of the generated token ids
++ lengths (zsaac/dist.py collect_captions) is inside the timed region.
 
-    python bench.py [--gpus N --steps K --warmup W]
-    torchrun --nproc-per-node N bench.py --gpus N ...      (one process per GPU, RCCL)
+    python bench.py                                  # 1045 clips per rank (weak scaling)
+    python bench.py --steps K                        # K full batches of 64 per rank (weak)
+    python bench.py --clips N                        # N clips in total, sharded (strong)
+    torchrun --nproc-per-node N bench.py --gpus N    # one process per GPU, RCCL
 
-Rank 0 prints ONE JSON line.  Besides the contract fields it carries
-  roofline:     the dominant kernel family (bf16 MFMA GEMM) at the decode MLP up-projection
-                shape the bench runs (R = decode rows) — algorithmic flops per launch / its
-                average duration, timed live with HIP events on the stream it runs on;
-                roofline_decode_attention: the HBM-bound decode attention, same method;
-  cpu_baseline: the oracle (reference semantics: batch 1, full recompute, fp32) on a bounded
-                sample of the same workload, timed on this host's CPU (rank 0, N=1 only).
+Rank 0 prints ONE JSON line.  Besides the contract fields (value = whole-job clips/s) it holds
+  roofline:          the dominant kernel of the bs-64 decode (the row-group GEMM with fused
+                     LayerNorm at the c_fc shape [64 x 768] x [768 x 3072]), HBM-bound:
+                     algorithmic bytes per launch / its average duration (HIP events on its
+                     stream, weights cold: the launches rotate over > 256 MiB of weight copies);
+  roofline_*:        the other decode kernels and the whole decode step, same method;
+  throughput_mode:   the same path with 128 eval batches decoded per step (8192-row GEMMs) —
+                     a different configuration, NOT the metric;
+  f32_parity_mode:   the bs-64 headline in f32 (the mode whose greedy ids are bit-exact);
+  id_agreement:      greedy ids against the reference goldens (bf16 and f32), first divergence
+                     and the reference's own top-2 logit margin there (tools/idparity.py);
+  cpu_baseline:      the oracle (reference semantics: batch 1, full recompute, fp32) on bounded
+                     samples of C2 and C1 on this host's CPU (rank 0, N=1 only).
 """
 from __future__ import annotations
 
 import argparse
 import json
+import math
 import os
 import sys
 import time
 
+
+def _hw_queues_from_argv(default=8):
+    for i, a in enumerate(sys.argv):
+        if a == "--hw-queues" and i + 1 < len(sys.argv):
+            return int(sys.argv[i + 1])
+        if a.startswith("--hw-queues="):
+            return int(a.split("=", 1)[1])
+    return default
+
+
+# must precede the HIP runtime's initialisation (the first device call).  The pool's boxes export
+# HIP's default of 4 (one of them the null stream's); the bench's concurrent batch streams each
+# want a queue of their own (measured at 4 in flight: 3.16k clips/s with 4 queues, 3.68k with 8)
+os.environ["GPU_MAX_HW_QUEUES"] = str(min(32, max(1, _hw_queues_from_argv())))
+
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "zero-shot-aac_amd"))
+sys.path.insert(0, ROOT)
 
 import torch  # noqa: E402
 
-HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+HBM_PEAK_GBS = 8000.0           # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+MFMA_BF16_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense bf16 MFMA (no sparsity)
 GPT2_KW = dict(seed=0, std=0.1, emb_std=0.1, stop_boost=2.0)
+CLOTHO_EVAL_CLIPS = 1045
+METRIC = "audio clips/sec end-to-end (encode+mapper+GPT-2 decode), Clotho-eval bs=64"
+DATA = ("synthetic 10 s / 32 kHz waveforms (randn*0.1) resident in HBM; seeded random-init "
+        "weights at the reference architecture (no checkpoints offline)")
+
+
+_T0 = time.time()
+
+
+def log(msg):
+    """Progress on stderr (the JSON line alone goes to stdout)."""
+    print(f"[bench {time.time() - _T0:7.1f}s] {msg}", file=sys.stderr, flush=True)
 
 
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=16)
-    ap.add_argument("--warmup", type=int, default=4)
+    ap.add_argument("--steps", type=int, default=None,
+                    help="eval batches of --batch clips per rank (default: the 1045-clip "
+                         "Clotho-eval set, 17 batches, the last holding 21 clips)")
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--clips", type=int, default=None,
+                    help="strong scaling: this many clips in total, sharded across ranks")
     ap.add_argument("--batch", type=int, default=64)
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "f32"])
     ap.add_argument("--encoder", default="htsat", choices=["htsat", "cnn14"])
     ap.add_argument("--mapper", default="mlp", choices=["mlp", "transformer"])
     ap.add_argument("--beam", type=int, default=0)
     ap.add_argument("--entry-length", type=int, default=67)
-    ap.add_argument("--encoder-batch", type=int, default=256,
-                    help="clips per encoder pass (0 = --batch); per-clip results do not depend on it")
-    ap.add_argument("--group", type=int, default=128,
-                    help="eval batches of --batch clips decoded together (one decode step over "
-                         "group*batch rows; measured 32 -> 64 -> 128: 10.9k -> 12.1k -> 12.3k "
-                         "clips/s); encoded --encoder-batch clips per pass")
-    ap.add_argument("--inflight", type=int, default=3,
-                    help="independent groups in flight per GPU, each on its own HIP stream "
-                         "(A/B in one box at group 128: 3 -> 12.73-12.75k, 2 -> 12.51-12.60k, "
-                         "4 -> 12.70k clips/s; 1: -11 %%)")
+    ap.add_argument("--encoder-batch", type=int, default=0,
+                    help="clips per encoder pass (0 = --batch * --group)")
+    ap.add_argument("--group", type=int, default=1,
+                    help="eval batches decoded together in one decode step (1 = the metric's "
+                         "bs=64; > 1 is the labelled throughput mode)")
+    ap.add_argument("--inflight", type=int, default=4,
+                    help="independent batches in flight per GPU, each on its own HIP stream")
+    ap.add_argument("--hw-queues", type=int, default=8,
+                    help="GPU_MAX_HW_QUEUES for this process (read before HIP initialises)")
     ap.add_argument("--compact", type=int, default=1,
-                    help="greedy bf16: decode only the rows that have not stopped (0 = all rows)")
-    ap.add_argument("--cpu-baseline-clips", type=int, default=2)
+                    help="greedy bf16 at >= 512 rows: decode only the rows that have not stopped")
+    ap.add_argument("--extras", type=int, default=1,
+                    help="N=1: also measure the throughput mode, the f32 mode and id agreement")
+    ap.add_argument("--cpu-baseline-clips", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--stages", action="store_true", help="also report per-stage ms (extra syncs)")
@@ -89,10 +133,11 @@ def dist_setup(args):
     return world, rank, local
 
 
-def build(args, device):
+def build(args, device, dtype=None, group=None, encoder_batch=None):
     from zsaac import synthetic as S
     from zsaac.pipeline import CaptionConfig, CaptionPipeline
-    dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
+    dtype = dtype or (torch.bfloat16 if args.dtype == "bf16" else torch.float32)
+    group = group or args.group
     csd = S.gpt2_state_dict(**GPT2_KW)
     csd.update(S.mlp_mapper_state_dict(1) if args.mapper == "mlp" else S.transformer_mapper_state_dict(2))
     if args.encoder == "htsat":
@@ -101,45 +146,93 @@ def build(args, device):
     else:
         asd = S.cnn14_state_dict(4)
         asd.update(S.audio_proj_state_dict(5, audio_width=2048))
-    cfg = CaptionConfig(encoder=args.encoder, mapping_type=args.mapper, dtype=dtype,
-                        batch=args.batch * getattr(args, "group", 1),
-                        encoder_batch=getattr(args, "encoder_batch", 0) or args.batch,
-                        beam=args.beam, entry_length=args.entry_length,
+    B = args.batch * group
+    eb = encoder_batch or getattr(args, "encoder_batch", 0) or B
+    cfg = CaptionConfig(encoder=args.encoder, mapping_type=args.mapper, dtype=dtype, batch=B,
+                        encoder_batch=eb, beam=args.beam, entry_length=args.entry_length,
                         compact_decode=bool(getattr(args, "compact", 1)))
     pipe = CaptionPipeline(csd, asd, S.label_table(), S.label_token_table(), cfg, device=device)
     return pipe, csd, asd
 
 
-PMC_FILE = os.path.join(ROOT, "profiles", "pmc_traffic_r1.json")
-MFMA_BF16_PEAK_TFLOPS = 2500.0   # MI355X_MICROARCH.md: dense bf16 MFMA (no sparsity)
+def synthetic_clips(n, first, device):
+    """Clips first..first+n-1 of the synthetic eval set (each clip its own seed, so a clip is the
+    same waveform whichever rank or batch takes it)."""
+    out = torch.empty(n, 320000, device=device)
+    g = torch.Generator(device=device)
+    for i in range(n):
+        g.manual_seed(1234 + first + i)
+        out[i].normal_(generator=g).mul_(0.1).clamp_(-1, 1)
+    return out
 
 
-def roofline_setup(pipe, cold_bytes=640 << 20):
-    """The dominant kernel family is the bf16 MFMA GEMM (gemm_lean_kernel: HTSAT stage 4 and the
-    GPT-2 decode/prefill linears).  Its roofline is taken at the decode-step MLP up-projection
-    as the bench runs it: c_fc out[R,3072] = gelu_new(h[R,768] @ W[3072,768]^T + b), R = the
-    decode rows of one step (eval batches x 64), through ops.gemm exactly as the decoder calls
-    it.  Launches rotate over enough distinct copies of W (> the 256 MiB Infinity Cache) that
-    every launch streams its weights from HBM, as in the real decode.  Returns (launch fn,
-    algorithmic flops, algorithmic bytes, number of W copies, kernel-name substring)."""
-    from zsaac import ops
-    dec = pipe.decoder
-    ly = pipe.gpt.layers[0]
-    M = pipe.cfg.batch * max(1, pipe.cfg.beam)
-    h, hid = dec.h[:M], dec.hid[:M]
-    W, b = ly["fc_w"], ly["fc_b"]
-    N, K = W.shape
-    es = W.element_size()
-    copies = [W] + [W.clone() for _ in range(max(0, -(-cold_bytes // W.nbytes) - 1))]
-    flops = 2 * M * N * K
-    algo_bytes = N * K * es + M * K * es + N * 4 + M * N * es
-    kname = "gemm_skinny_kernel" if M <= 64 else "gemm_lean_kernel"
+# ------------------------------------------------------------------ caption runs
+def run_captions(args, world, rank, device, pipe, n_local, first, counts, inflight, warmup):
+    """Times the captioning of this rank's n_local clips (clip ids first..) in batches of
+    pipe.cfg.batch on `inflight` streams, then the all-gather; returns (seconds max over ranks,
+    outs, runner, info)."""
+    from zsaac.pipeline import ConcurrentRunner
+    from zsaac import dist as zd
+    B = pipe.cfg.batch
+    pool = synthetic_clips(n_local, first, device)
+    batches = [pool[i:i + B] for i in range(0, n_local, B)]
+    log(f"{n_local} clips in {len(batches)} batches of <= {B}, {inflight} in flight: capturing")
+    runner = ConcurrentRunner(pipe, max(1, inflight))
+    for size in sorted({b.shape[0] for b in batches}, reverse=True):   # captures every graph
+        runner.warmup(next(b for b in batches if b.shape[0] == size))
+        log(f"captured the decode graphs of {size}-clip batches")
+    if warmup:
+        runner.run([batches[i % len(batches)] for i in range(warmup)])
+        log(f"warmed up ({warmup} batches)")
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    cap0 = sum(p.decoder.n_captures for p in runner.pipes)
+    rows0 = sum(p.decoder.rows_stepped for p in runner.pipes)
+    t0 = time.perf_counter()
+    outs = runner.run(batches)
+    if world > 1:
+        zd.collect_captions(outs, counts)
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt], device=device, dtype=torch.float64)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        dt = float(t)
+    log(f"timed: {n_local} clips in {dt:.3f} s")
+    info = {"graph_captures_timed": sum(p.decoder.n_captures for p in runner.pipes) - cap0,
+            "decode_rows_stepped_per_clip": round(
+                (sum(p.decoder.rows_stepped for p in runner.pipes) - rows0) / max(1, n_local), 2),
+            "decode_steps_mean": round(sum(runner.decode_steps) / max(1, len(runner.decode_steps)), 2),
+            "tokens_rank0": int(sum(int(o.lengths.sum()) if o.scores is None
+                                    else int(o.lengths[:, 0].sum()) for o in outs))}
+    del pool
+    return dt, outs, runner, info
 
-    def launch(i):
-        ops.gemm(h, copies[i % len(copies)], hid, bias=b, act=ops.ACT_GELU_TANH, workspace=dec.ws)
-    return launch, flops, algo_bytes, len(copies), kname, (M, N, K)
+
+def sub_run(args, device, dtype, group, inflight, n_clips, warmup, encoder_batch=None):
+    """A secondary single-GPU configuration (throughput mode / f32 mode): value + config."""
+    pipe, _, _ = build(args, device, dtype=dtype, group=group, encoder_batch=encoder_batch)
+    dt, outs, runner, info = run_captions(args, 1, 0, device, pipe, n_clips, 10 ** 6, [n_clips],
+                                          inflight, warmup)
+    B = pipe.cfg.batch
+    res = {"value": round(n_clips / dt, 2), "unit": "clips/s", "clips": n_clips,
+           "ms_per_step": round(dt / math.ceil(n_clips / B) * 1e3, 3),
+           "dtype": "bf16" if dtype == torch.bfloat16 else "f32",
+           "config": {"eval_batch": args.batch, "eval_batches_per_step": group,
+                      "decode_rows_per_step": B, "encoder_batch": pipe.encoder.B,
+                      "steps_in_flight_per_gpu": inflight, **info}}
+    del runner, pipe, outs
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    return res
 
 
+# ------------------------------------------------------------------ rooflines
 def _graph_time(launch, reps):
     """Average duration of `reps` back-to-back launches captured in one graph, HIP events on the
     launching stream, 5 replays."""
@@ -163,53 +256,123 @@ def _graph_time(launch, reps):
     return e0.elapsed_time(e1) / 1e3 / (5 * reps)
 
 
-def kernel_roofline(pipe):
-    """roofline (dominant kernel, MFMA-bound at the bench's decode rows) + a secondary HBM-bound
-    entry for the decode attention (the largest single-shape kernel)."""
-    launch, flops, algo_bytes, ncopy, kname, (M, N, K) = roofline_setup(pipe)
-    avg_s = _graph_time(launch, 2 * ncopy)
-    tflops = flops / avg_s / 1e12
+def _cold_copies(W, cold_bytes=640 << 20):
+    return [W] + [W.clone() for _ in range(max(0, -(-cold_bytes // W.nbytes) - 1))]
+
+
+def _hbm_entry(kernel, byts, avg_s, extra=None):
+    gbs = byts / avg_s / 1e9
+    r = {"kernel": kernel, "bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS,
+         "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4), "avg_launch_us": round(avg_s * 1e6, 3),
+         "algo_bytes_per_launch": int(byts)}
+    if extra:
+        r.update(extra)
+    return r
+
+
+PMC_FILE = os.path.join(ROOT, "profiles", "r2_pmc_traffic.json")
+
+
+def roofline_gemm_ln(pipe):
+    """Dominant kernel of the bs-64 decode: zs_gemm_ln (row-group GEMM with ln_2 fused) at the
+    c_fc shape out[64, 3072] = gelu_new(LN(x[64, 768]) @ W[3072, 768]^T + b), bf16 out, as the
+    decoder launches it.  Algorithmic bytes = W (bf16) + x (f32) + LN params + bias + out."""
+    from zsaac import ops
+    dec, ly = pipe.decoder, pipe.gpt.layers[0]
+    M = min(64, pipe.cfg.batch)
+    x, hid = dec.x[:M], dec.hid[:M]
+    W, b = ly["fc_w"], ly["fc_b"]
+    N, K = W.shape
+    copies = _cold_copies(W)
+
+    def launch(i):
+        ops.gemm_ln(x, *ly["ln2"], copies[i % len(copies)], hid, bias=b, act=ops.ACT_GELU_TANH)
+    avg = _graph_time(launch, 2 * len(copies))
+    byts = N * K * 2 + M * K * 4 + 2 * K * 4 + N * 4 + M * N * 2
+    flops = 2 * M * N * K
     traffic, tsrc = None, None
-    if os.path.exists(PMC_FILE):          # rocprofv3 --pmc passes of tools/pmc_traffic.py
+    if os.path.exists(PMC_FILE):            # rocprofv3 --pmc passes (tools/pmc_traffic.py)
         with open(PMC_FILE) as f:
             pmc = json.load(f)
-        if pmc.get("shape") == [M, N, K]:
+        if pmc.get("shape") == [M, N, K] and pmc.get("kernel", "").startswith("gemm_rows"):
             traffic, tsrc = pmc["hbm_bytes_per_launch"], os.path.relpath(PMC_FILE, ROOT)
-    res = {"kernel": f"{kname}<bf16> decode c_fc [{M}x{K}]x[{K}x{N}] +bias +gelu_new (cold W)",
-           "bound": "mfma", "achieved": round(tflops, 1), "peak": MFMA_BF16_PEAK_TFLOPS,
-           "unit": "TFLOP/s", "frac": round(tflops / MFMA_BF16_PEAK_TFLOPS, 4),
-           "traffic": traffic, "traffic_source": tsrc, "avg_launch_us": round(avg_s * 1e6, 3),
-           "algo_flops_per_launch": flops, "algo_bytes_per_launch": algo_bytes,
-           "hbm_GBps_algorithmic": round(algo_bytes / avg_s / 1e9, 1)}
-    return res, attention_roofline(pipe)
+    return _hbm_entry(f"gemm_rows_kernel<32,4,LN,6> (zs_gemm_ln) decode c_fc [{M}x{K}]x[{K}x{N}] "
+                      f"+ln_2 +bias +gelu_new (cold W)", byts, avg,
+                      {"traffic": traffic, "traffic_source": tsrc,
+                       "attainable_tflops_at_this_AI": round(flops / byts * HBM_PEAK_GBS / 1e3, 1),
+                       "achieved_tflops": round(flops / avg / 1e12, 2)})
 
 
-def attention_roofline(pipe, L_mean=None):
-    """decode attention (decode_attn6_kernel, the default) at the bench's decode rows, every row at the mean key count of a
-    67-step greedy decode (prompt Pmax + 34): algorithmic bytes = K and V of every key read once
-    + q/k/v of the new token + the output, per (row, head)."""
+def roofline_rows_gemm(pipe, which):
+    from zsaac import ops
+    dec, ly = pipe.decoder, pipe.gpt.layers[0]
+    M = min(64, pipe.cfg.batch)
+    if which == "mproj":
+        a, W, b, K = dec.hid[:M], ly["mproj_w"], ly["mproj_b"], 3072
+    else:
+        a, W, b, K = dec.att[:M], ly["proj_w"], ly["proj_b"], 768
+    N = W.shape[0]
+    out = torch.empty(M, N, device=W.device)
+    copies = _cold_copies(W)
+
+    def launch(i):
+        ops.gemm(a, copies[i % len(copies)], out, bias=b, residual=out, workspace=dec.ws)
+    avg = _graph_time(launch, 2 * len(copies))
+    byts = N * K * 2 + M * K * 2 + N * 4 + 2 * M * N * 4
+    return _hbm_entry(f"gemm_rows_kernel decode {which} [{M}x{K}]x[{K}x{N}] +bias +residual "
+                      f"(cold W)", byts, avg)
+
+
+def roofline_attention(pipe, L_mean=None):
+    """decode attention at the bench's decode rows, every row at the mean key count of a 67-step
+    greedy decode (prompt Pmax + 34): bytes = K and V of every key once + q/k/v + output."""
     from zsaac import ops
     dec = pipe.decoder
     R = pipe.cfg.batch * max(1, pipe.cfg.beam)
     D, H, Lmax = 768, 12, dec.Lmax
     L = L_mean or min(Lmax - 1, pipe.Pmax + 34)
-    lay = dec.kc[0] if isinstance(dec.kc, (list, tuple)) else None
-    kc = lay if lay is not None else torch.randn(R, H, Lmax, 64, device=pipe.dev).bfloat16()
-    vc = (dec.vc[0] if isinstance(dec.vc, (list, tuple)) else torch.randn_like(kc))
-    qkv = dec.qkv[:R] if hasattr(dec, "qkv") else torch.randn(R, 3 * D, device=pipe.dev).bfloat16()
+    kc, vc = dec.kc[0], dec.vc[0]
+    qkv = dec.qkv[:R]
     pos = torch.full((R,), L - 1, device=pipe.dev, dtype=torch.int32)
     out = torch.empty(R, D, device=pipe.dev, dtype=qkv.dtype)
 
     def launch(i):
         ops.decode_attention(qkv, R, D, H, kc, vc, Lmax, pos, out)
-    avg_s = _graph_time(launch, 50)
+    avg = _graph_time(launch, 50)
     es = qkv.element_size()
     byts = R * H * (2 * L * 64 * es) + R * 3 * D * es + R * D * es
-    gbs = byts / avg_s / 1e9
-    return {"kernel": f"decode_attn6_kernel<bf16> R={R} heads=12 keys={L}", "bound": "hbm",
-            "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(gbs / HBM_PEAK_GBS, 4), "avg_launch_us": round(avg_s * 1e6, 3),
-            "algo_bytes_per_launch": byts}
+    return _hbm_entry(f"decode_attn6_kernel<bf16,{128 if R <= 128 else 16}> R={R} heads=12 keys={L}",
+                      byts, avg)
+
+
+def decode_step_roofline(pipe, agg_steps_per_s=None):
+    """One greedy decode step of one batch (graph replay of a chunk, single stream): HBM bytes
+    a step must move (GPT-2 weights incl. the tied LM head + every row's KV at the mean key
+    count) / its time; with the concurrent run's aggregate steps/s when given."""
+    dec = pipe.decoder
+    R = pipe.cfg.batch
+    dec.done.zero_()
+    gr = dec._graph(*dec._chunk_plan(None))
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    reps = 10
+    e0.record()
+    for _ in range(reps):
+        gr.replay()
+    e1.record()
+    e1.synchronize()
+    step_s = e0.elapsed_time(e1) / 1e3 / reps / dec.chunk
+    L = min(dec.Lmax - 1, pipe.Pmax + 34)
+    byts = pipe.gpt.nbytes() + R * L * 12 * 2 * 768 * 2
+    r = _hbm_entry(f"one greedy decode step, {R} rows (12 blocks + ln_f + LM head + greedy step), "
+                   f"single stream", byts, step_s, {"avg_step_us": round(step_s * 1e6, 1)})
+    r.pop("avg_launch_us")
+    if agg_steps_per_s:
+        agg = byts * agg_steps_per_s / 1e9
+        r["concurrent_aggregate"] = {"decode_steps_per_s": round(agg_steps_per_s, 1),
+                                     "achieved_GBps": round(agg, 1),
+                                     "frac": round(agg / HBM_PEAK_GBS, 4)}
+    return r
 
 
 def stage_times(pipe, wav, reps=3):
@@ -243,66 +406,114 @@ def stage_times(pipe, wav, reps=3):
     return res
 
 
-def cpu_baseline(args, csd, asd, n_clips):
+# ------------------------------------------------------------------ CPU baseline
+def _cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
+def cpu_baseline(args, csd, asd, n_c2, n_c1):
     """Oracle = reference semantics (batch 1 per clip, full-sequence recompute every step, fp32)
-    on `n_clips` clips of the same synthetic workload, on this host's CPU."""
-    sys.path.insert(0, ROOT)
+    on bounded samples: n_c2 clips of the C2 workload (wav -> HTSAT -> MLP -> greedy) and n_c1
+    clips of C1 (the reference goldens' CLAP embeddings -> MLP -> greedy), on the CPUs this
+    process may use (sched affinity; os.cpu_count() may count the whole machine)."""
+    import numpy as np
     from oracle import audio as A, caption as OC, frontend as OF
     from zsaac import synthetic as S
-    threads = min(16, os.cpu_count() or 1)
+    visible = os.cpu_count() or 1
+    avail = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else visible
+    # the CPU share this job may use: OMP_NUM_THREADS when the host sets it (a GPU box of the
+    # pool sets it to its per-GPU share; affinity there still lists every core of the machine)
+    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    threads = max(1, min(avail, visible, share) if share > 0 else min(avail, visible))
     torch.set_num_threads(threads)
     table, lt = S.label_table(), S.label_token_table()
-    wav = S.synthetic_waveforms(n_clips, seed=777)
+
+    def caption(emb, ntok):
+        idx = OC.sound_effect_choice(emb, table, 3)[0].tolist()
+        hard = torch.tensor([OC.prompt_ids(idx, lt)])
+        pe = OC.clap_to_gpt(torch.nn.functional.normalize(emb, dim=-1)[None], hard, csd, args.mapper)
+        OC.prefix_tokens(pe, csd)
+        if args.beam:
+            OC.generate_beam(pe, csd, beam_size=args.beam, entry_length=args.entry_length)
+        else:
+            ntok[0] += len(OC.generate2(pe, csd, entry_length=args.entry_length))
+
+    log(f"cpu baseline: C2 {n_c2} clips, C1 {n_c1} clips, {threads} threads")
+    wav = synthetic_clips(n_c2, 777, torch.device("cpu"))
+    ntok = [0]
     t0 = time.perf_counter()
-    ntok = 0
     with torch.no_grad():
-        for i in range(n_clips):
+        for i in range(n_c2):
             lm = OF.logmel(wav[i:i + 1])
-            if args.encoder == "htsat":
-                feat = A.htsat_embedding(lm, asd)
-            else:
-                feat = A.cnn14_embedding(lm, asd)
-            emb = A.audio_project(feat, asd)
-            idx = OC.sound_effect_choice(emb, table, 3)[0].tolist()
-            hard = torch.tensor([OC.prompt_ids(idx, lt)])
-            pe = OC.clap_to_gpt(torch.nn.functional.normalize(emb, dim=-1)[None], hard, csd,
-                                args.mapper)
-            OC.prefix_tokens(pe, csd)
-            if args.beam:
-                OC.generate_beam(pe, csd, beam_size=args.beam, entry_length=args.entry_length)
-            else:
-                ntok += len(OC.generate2(pe, csd, entry_length=args.entry_length))
-    dt = time.perf_counter() - t0
-    return {"value": round(n_clips / dt, 4), "unit": "clips/s", "cores": threads, "kind": "port",
-            "sample": f"{n_clips} clips of the same workload, batch 1, full recompute per step "
-                      f"(reference semantics), fp32, {ntok} tokens, {dt:.1f} s"}
+            feat = A.htsat_embedding(lm, asd) if args.encoder == "htsat" else A.cnn14_embedding(lm, asd)
+            caption(A.audio_project(feat, asd), ntok)
+            log(f"cpu baseline C2 clip {i + 1}/{n_c2}")
+    dt2 = time.perf_counter() - t0
+    c1 = np.load(os.path.join(ROOT, "tests", "golden", "c1_greedy.npz"))
+    emb = torch.from_numpy(c1["clap_emb"][:n_c1])
+    ntok1 = [0]
+    t0 = time.perf_counter()
+    with torch.no_grad():
+        for i in range(n_c1):
+            caption(emb[i:i + 1], ntok1)
+            if i % 4 == 3:
+                log(f"cpu baseline C1 clip {i + 1}/{n_c1}")
+    dt1 = time.perf_counter() - t0
+    return {"value": round(n_c2 / dt2, 4), "unit": "clips/s", "cores": threads, "kind": "port",
+            "threads": threads, "cpus_visible": visible, "cpus_available": avail,
+            "omp_num_threads_env": share or None,
+            "cpu_model": _cpu_model(),
+            "sample": f"C2: {n_c2} clips of the headline workload (wav -> log-mel -> "
+                      f"{args.encoder.upper()} -> audio_proj -> prompt -> {args.mapper} mapper -> "
+                      f"get_prefix_tokens -> greedy, {ntok[0]} tokens) in {dt2:.1f} s; batch 1, "
+                      f"full-sequence recompute per step (reference semantics), fp32, "
+                      f"{threads} threads.  A bounded sample (the full 1045 clips would take "
+                      f"~{CLOTHO_EVAL_CLIPS / max(n_c2 / dt2, 1e-9) / 60:.0f} min)",
+            "c1_plumbing": {"value": round(n_c1 / dt1, 4), "unit": "clips/s", "clips": n_c1,
+                            "tokens": ntok1[0], "seconds": round(dt1, 1),
+                            "sample": "C1: the first clips of the 50 reference-golden CLAP "
+                                      "embeddings -> MLP -> greedy (of 50: bounded to keep the "
+                                      "default run within minutes)"}}
 
 
+# ------------------------------------------------------------------ C4
 def main_embeddings(args, world, rank, device, pipe):
     """BASELINE.json configs[3] (C4): embedding extraction, data_handing/embeddings_generator.py
     realised as batched encode_audio over synthetic clips sharded across ranks, then one RCCL
-    all-gather of the [N,1024] f32 embeddings (SURVEY §8d "C4 reinterpretation")."""
-    B = args.batch * args.group
-    g = torch.Generator(device=device).manual_seed(1234 + rank)
-    pool = [(torch.randn(B, 320000, device=device, generator=g) * 0.1).clamp_(-1, 1)
-            for _ in range(min(2, args.steps + args.warmup))]
-    embs = torch.empty(args.steps, B, 1024, device=device)
+    all-gather of the [N,1024] f32 embeddings (zsaac/dist.py gather_rows)."""
+    from zsaac import dist as zd
+    B = pipe.encoder.B
+    steps = args.steps or 16
+    n_total = args.clips or B * steps * world
+    lo, hi = zd.shard_range(n_total, rank, world)
+    counts = zd.shard_counts(n_total, world)
+    pool = synthetic_clips(min(hi - lo, 2 * B), lo, device)
+    embs = torch.empty(hi - lo, 1024, device=device)
 
-    def run(first, n, keep):
-        for i in range(n):
-            e = pipe.encode(pool[(first + i) % len(pool)])
+    def run(n_batches, keep):
+        for i in range(n_batches):
+            c0 = i * B
+            c1 = min(hi - lo, c0 + B)
+            e = pipe.encode(pool[(c0 % pool.shape[0]):(c0 % pool.shape[0]) + (c1 - c0)])
             if keep:
-                embs[i].copy_(e)
+                embs[c0:c1].copy_(e)
         if keep and world > 1:
-            gathered = torch.empty(world * embs.numel(), device=device)
-            torch.distributed.all_gather_into_tensor(gathered, embs.view(-1))
-    run(0, args.warmup, False)
+            zd.gather_rows(embs, counts)
+    nb = -(-(hi - lo) // B)
+    run(min(args.warmup, nb), False)
     torch.cuda.synchronize()
     if world > 1:
         torch.distributed.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    run(args.warmup, args.steps, True)
+    run(nb, True)
     torch.cuda.synchronize()
     if world > 1:
         torch.distributed.barrier()
@@ -314,13 +525,13 @@ def main_embeddings(args, world, rank, device, pipe):
         dt = float(t)
     res = {"metric": "audio clips/sec embedding extraction (STFT/log-mel + " + args.encoder.upper()
                      + " + audio_proj + L2), C4",
-           "value": round(world * B * args.steps / dt, 2), "unit": "clips/s", "n_gpus": world,
-           "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(dt / args.steps * 1e3, 3),
-           "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-           "dtype": "bf16" if args.dtype == "bf16" else "f32",
-           "data": "synthetic 10 s / 32 kHz waveforms (randn*0.1) resident in HBM; seeded weights",
+           "value": round(n_total / dt, 2), "unit": "clips/s", "n_gpus": world,
+           "steps": nb, "warmup": args.warmup, "ms_per_step": round(dt / nb * 1e3, 3),
+           "higher_is_better": True, "scaling": "strong" if args.clips else "weak",
+           "vs_baseline": None, "dtype": args.dtype,
+           "data": DATA,
            "config": {"workload": "C4 embedding extraction, RCCL all-gather of [N,1024] f32",
-                      "encoder_batch": pipe.encoder.B, "batch_per_gpu": B, "global_batch": B * world,
+                      "encoder_batch": B, "clips_total": n_total, "clips_per_rank": counts,
                       "parallelism": f"dp{world} (clip-sharded)"}}
     if rank == 0:
         print(json.dumps(res), flush=True)
@@ -328,97 +539,84 @@ def main_embeddings(args, world, rank, device, pipe):
         torch.distributed.destroy_process_group()
 
 
+# ------------------------------------------------------------------ main
 def main():
     args = parse()
     world, rank, local = dist_setup(args)
     device = torch.device("cuda", local)
-    from zsaac import synthetic as S
+    from zsaac import dist as zd
     pipe, csd, asd = build(args, device)
     if args.embeddings_only:
         return main_embeddings(args, world, rank, device, pipe)
-    B = args.batch * args.group           # clips per step (group eval batches, decoded together)
-    # input pool resident in HBM before timing: distinct synthetic clips per step and rank
-    pool = []
-    g = torch.Generator(device=device).manual_seed(1234 + rank)
-    for _ in range(min(4, args.steps + args.warmup)):
-        pool.append((torch.randn(B, 320000, device=device, generator=g) * 0.1).clamp_(-1, 1))
-    from zsaac.pipeline import ConcurrentRunner
-    runner = ConcurrentRunner(pipe, max(1, args.inflight))
-
-    def run(first, n):
-        """n batches through the runner (inflight batches decoding concurrently on separate
-        streams), then ONE RCCL all-gather of every batch's token ids + lengths in input order
-        (completion order is timing-dependent, so no per-batch collective)."""
-        outs = runner.run([pool[(first + i) % len(pool)] for i in range(n)])
-        if world > 1 and outs:
-            import torch.distributed as dist
-            ids = torch.cat([(o.ids if o.ids.dim() == 2 else o.ids[:, 0]).reshape(-1) for o in outs])
-            ln = torch.cat([(o.lengths if o.lengths.dim() == 1 else o.lengths[:, 0]).int() for o in outs])
-            ids_all = torch.empty(world * ids.numel(), dtype=ids.dtype, device=device)
-            len_all = torch.empty(world * ln.numel(), dtype=ln.dtype, device=device)
-            dist.all_gather_into_tensor(ids_all, ids)
-            dist.all_gather_into_tensor(len_all, ln)
-        return outs
-
-    runner.warmup(pool[0])          # one batch per twin: captures every decode graph
-    run(0, args.warmup)
-    torch.cuda.synchronize()
-    if world > 1:
-        torch.distributed.barrier()
-    torch.cuda.synchronize()
-    cap0 = sum(p.decoder.n_captures for p in runner.pipes)
-    rows0 = sum(p.decoder.rows_stepped for p in runner.pipes)
-    t0 = time.perf_counter()
-    ntok = 0
-    outs = run(args.warmup, args.steps)
-    last = outs[-1] if outs else None
-    torch.cuda.synchronize()
-    if world > 1:
-        torch.distributed.barrier()
-    torch.cuda.synchronize()
-    dt = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([dt], device=device, dtype=torch.float64)
-        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-        dt = float(t)
-    if last is not None:
-        ntok = int(last.lengths.sum()) if last.scores is None else int(last.lengths[:, 0].sum())
-    clips = world * B * args.steps
+    B = pipe.cfg.batch
+    if args.clips:                              # strong scaling: a fixed clip set, sharded
+        n_total, scaling = args.clips, "strong"
+        lo, hi = zd.shard_range(n_total, rank, world)
+        counts = zd.shard_counts(n_total, world)
+    else:                                       # weak scaling: a fixed clip count per rank
+        per = args.steps * B if args.steps else CLOTHO_EVAL_CLIPS
+        n_total, scaling = per * world, "weak"
+        lo, hi = rank * per, (rank + 1) * per
+        counts = [per] * world
+    n_local = hi - lo
+    steps = -(-n_local // B)
+    dt, outs, runner, info = run_captions(args, world, rank, device, pipe, n_local, lo, counts,
+                                          args.inflight, args.warmup)
+    workload = (("C3 AudioCaps-eval" if args.beam else "C2 Clotho-eval")
+                + (" (1045 clips per rank)" if not (args.steps or args.clips) else "")
+                + ": STFT/log-mel + " + args.encoder.upper() + " + " + args.mapper
+                + " mapper + GPT-2 small " + ("greedy generate2" if not args.beam else f"beam {args.beam}")
+                + f", entry_length {args.entry_length}, + get_prefix_tokens")
+    metric = METRIC if not args.beam and args.group == 1 else (
+        f"audio clips/sec end-to-end (encode+mapper+GPT-2 decode), "
+        + (f"AudioCaps-eval beam {args.beam} bs={args.batch * args.group}" if args.beam
+           else f"Clotho-eval {args.group}x{args.batch} clips per decode step (throughput mode)"))
     res = {
-        "metric": "audio clips/sec end-to-end (encode+mapper+GPT-2 decode), Clotho-eval bs=64",
-        "value": round(clips / dt, 2),
-        "unit": "clips/s",
-        "n_gpus": world,
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "ms_per_step": round(dt / args.steps * 1e3, 3),
-        "higher_is_better": True,
-        "scaling": "weak",
-        "vs_baseline": None,
-        "dtype": "bf16" if args.dtype == "bf16" else "f32",
-        "data": "synthetic 10 s / 32 kHz waveforms (randn*0.1) resident in HBM; seeded random-init "
-                "weights at the reference architecture (no checkpoints offline)",
-        "config": {"workload": ("C3 AudioCaps-eval" if args.beam else "C2 Clotho-eval")
-                               + ": STFT/log-mel + " + args.encoder.upper() + " + "
-                               + args.mapper + " mapper + GPT-2 small "
-                               + ("greedy generate2" if not args.beam else f"beam {args.beam}")
-                               + f", entry_length {args.entry_length}, + get_prefix_tokens",
-                   "eval_batch": args.batch, "eval_batches_per_step": args.group,
-                   "batch_per_gpu": B, "global_batch": B * world,
-                   "steps_in_flight_per_gpu": max(1, args.inflight),
+        "metric": metric, "value": round(n_total / dt, 2), "unit": "clips/s", "n_gpus": world,
+        "steps": steps, "warmup": args.warmup, "ms_per_step": round(dt / steps * 1e3, 3),
+        "higher_is_better": True, "scaling": scaling, "vs_baseline": None,
+        "dtype": "bf16" if args.dtype == "bf16" else "f32", "data": DATA,
+        "config": {"workload": workload, "eval_batch": args.batch,
+                   "eval_batches_per_step": args.group, "batch_per_gpu": B,
+                   "decode_rows_per_gemm": B * max(1, args.beam),
+                   "clips_per_rank": n_local, "clips_total": n_total,
+                   "global_batch": B * world, "steps_in_flight_per_gpu": max(1, args.inflight),
+                   "hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "4")),
+                   "encoder_batch": pipe.encoder.B,
                    "parallelism": f"dp{world} (clip-sharded, RCCL all-gather of token ids)",
-                   "tokens_last_batch_rank0": ntok,
-                   "decode_rows_stepped_per_clip": round(
-                       (sum(p.decoder.rows_stepped for p in runner.pipes) - rows0) / max(1, args.steps * B), 2),
-                   "graph_captures_timed": sum(p.decoder.n_captures for p in runner.pipes) - cap0,
-                   "decode_steps_mean": round(sum(runner.decode_steps) / max(1, len(runner.decode_steps)), 2)},
+                   **info},
     }
-    if args.stages and rank == 0:
-        res["stages_ms"] = stage_times(pipe, pool[0])
-    if rank == 0 and not args.no_roofline:
-        res["roofline"], res["roofline_decode_attention"] = kernel_roofline(pipe)
+    if rank == 0 and args.stages:
+        res["stages_ms"] = stage_times(pipe, synthetic_clips(B, 0, device))
+    if rank == 0 and not args.no_roofline and args.group == 1 and B <= 64 and not args.beam \
+            and args.dtype == "bf16":
+        log("rooflines")
+        res["roofline"] = roofline_gemm_ln(pipe)
+        res["roofline_mproj"] = roofline_rows_gemm(pipe, "mproj")
+        res["roofline_proj"] = roofline_rows_gemm(pipe, "proj")
+        res["roofline_decode_attention"] = roofline_attention(pipe)
+        agg = info["decode_steps_mean"] * steps / dt if world == 1 else None
+        res["roofline_decode_step"] = decode_step_roofline(pipe, agg)
+    del runner, outs
+    if rank == 0 and world == 1 and args.extras and args.group == 1 and not args.beam:
+        del pipe
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
+        log("throughput mode")
+        res["throughput_mode"] = sub_run(args, device, torch.bfloat16, 128, 3, 3 * 8192, 1,
+                                         encoder_batch=256)
+        res["throughput_mode"]["note"] = ("128 eval batches decoded together (8192-row decode "
+                                          "GEMMs), 3 in flight: NOT the metric's bs=64")
+        log("f32 parity mode")
+        res["f32_parity_mode"] = sub_run(args, device, torch.float32, 1, args.inflight, 6 * 64, 1)
+        res["f32_parity_mode"]["note"] = "bs=64 in f32: the mode whose greedy ids are bit-exact"
+        log("id agreement")
+        from tools import idparity
+        res["id_agreement"] = {"bf16": idparity.summary(torch.bfloat16, device),
+                               "f32": idparity.summary(torch.float32, device)}
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.cpu_baseline_clips > 0:
-        res["cpu_baseline"] = cpu_baseline(args, csd, asd, args.cpu_baseline_clips)
+        res["cpu_baseline"] = cpu_baseline(args, csd, asd, args.cpu_baseline_clips,
+                                           max(1, args.cpu_baseline_clips // 2))
     if rank == 0:
         print(json.dumps(res), flush=True)
     if world > 1:

@@ -20,6 +20,8 @@ Fixture list (reference call sites in brackets):
                   audio_proj/normalize (ase_model.py:52-55).
   cnn14.npz       CNN14 forward from log-mel (cnns.py:171-201) + audio_proj/normalize.
   prompt.npz      compose_discrete_prompts strings + padding_captions (utils.py:158-208).
+  c2_margin.npz   generate2 with the reference's top-1/top-2 logit margin at every generated
+  c2_margin_flat.npz  step, on smaller decoder weights (the bf16 id-parity check).
 """
 from __future__ import annotations
 
@@ -36,6 +38,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(os.path.dirname(HERE))
 sys.path.insert(0, HERE)
 sys.path.insert(0, os.path.join(REPO, "zero-shot-aac_amd"))
+sys.path.insert(1, REPO)                 # oracle/ (prompt ids, pinned by tests/test_oracle.py)
 
 import _refshim  # noqa: E402
 
@@ -108,7 +111,7 @@ def gen_c1(n_clips=50, entry_length=67):
                                         sound_effect_num=SOUND_EFFECT_NUM)
     model = _caption_model("mlp")
     embeddings = torch.nn.functional.normalize(model.gpt.get_input_embeddings().weight.data, 2, 1)
-    hard_rows, greedy_rows, pref_rows, pe_keep = [], [], [], []
+    hard_rows, greedy_rows, pref_rows, pe_keep, margin_rows = [], [], [], [], []
     t0 = time.time()
     for i in range(n_clips):
         audio_id, prefix, hard, mask = collate([ds[i]])
@@ -118,9 +121,11 @@ def gen_c1(n_clips=50, entry_length=67):
             pe, _ = model.clap_to_gpt(prefix, emb_h)
             ps = G.get_prefix_tokens(pe, embeddings, _PrefixTok())
             out = G.generate2(model, IdTokenizer(), embed=pe, entry_length=entry_length)
+            ids = [int(t) for t in out.split()]
+            margin_rows.append(_step_margins(model, pe, ids))
         hard_rows.append(hard[0].tolist())
         pref_rows.append([int(t) for t in ps[0].split("|") if t])
-        greedy_rows.append([int(t) for t in out.split()])
+        greedy_rows.append(ids)
         if i < 4:
             pe_keep.append(pe[0].numpy())
         if i % 10 == 0:
@@ -132,10 +137,84 @@ def gen_c1(n_clips=50, entry_length=67):
     pe_pad = np.zeros((len(pe_keep), max(p.shape[0] for p in pe_keep), 768), np.float32)
     for i, p in enumerate(pe_keep):
         pe_pad[i, :p.shape[0]] = p
+    marg = np.zeros(greedy.shape, np.float32)
+    for i, m in enumerate(margin_rows):
+        marg[i, :len(m)] = m
     _save("c1_greedy.npz", clap_emb=emb.numpy(), hard_ids=hard, hard_len=hard_len,
           greedy_ids=greedy, greedy_len=greedy_len, prefix_tokens=pref,
           prefix_embed=pe_pad, entry_length=np.int64(entry_length),
-          sound_effect_num=np.int64(SOUND_EFFECT_NUM), normalize_prefix=np.int64(1))
+          sound_effect_num=np.int64(SOUND_EFFECT_NUM), normalize_prefix=np.int64(1), margin=marg)
+
+
+def _step_margins(model, pe, ids):
+    """The reference's top-1 minus top-2 logit at every generated step: one teacher-forced
+    forward of the reference GPT2LMHeadModel over prompt + generated ids (the computation
+    generate2 repeats at every step, gpt2_prefix_eval.py:187-190); checks its argmax = ids."""
+    seq = torch.cat([pe, model.gpt.transformer.wte(torch.tensor([ids[:-1]]))], 1) \
+        if len(ids) > 1 else pe
+    logits = model.gpt(inputs_embeds=seq).logits[0, pe.shape[1] - 1:]
+    assert torch.equal(logits.argmax(-1), torch.tensor(ids)), "teacher forcing != generate2"
+    top2 = logits.topk(2, -1).values
+    return (top2[:, 0] - top2[:, 1]).tolist()
+
+
+# bf16 id-parity goldens: block weights at std 0.05 give varied captions (10-20 distinct tokens
+# per clip) with step margins from ~0.01 to ~4 (logit std ~3); at GPT-2's own init scale 0.02
+# every caption collapses to one repeated token after a first step whose margin varies by clip
+MARGIN_GPT2_KW = {"c2_margin": dict(seed=7, std=0.05, emb_std=0.1, stop_boost=2.0),
+                  "c2_margin_flat": dict(seed=7, std=0.02, emb_std=0.1, stop_boost=2.0)}
+
+
+def gen_margin(n_clips=32, entry_length=67, name="c2_margin"):
+    """c2_margin.npz / c2_margin_flat.npz: greedy goldens for the bf16 id-parity check, with the
+    reference's top-1 / top-2 logit margin at every generated step (teacher-forced full-sequence
+    forward of the reference GPT2LMHeadModel over the prompt + generated ids: the computation
+    generate2 repeats every step, gpt2_prefix_eval.py:187-190).  Decoder block weights at a
+    smaller scale than the chaotic std-0.1 goldens (MARGIN_GPT2_KW).  Hard prompts as C1
+    (dataset.py:441-453)."""
+    import gpt2_prefix_eval as G
+    from models.caption_model import ClapCaption_prompt
+    kw = MARGIN_GPT2_KW[name]
+    sd = S.gpt2_state_dict(**kw)
+    sd.update(S.mlp_mapper_state_dict(1))
+    model = ClapCaption_prompt(10, clip_length=10, prefix_size=1024, num_layers=8,
+                               mapping_type="mlp", only_prefix=False, only_soft_prompt=False)
+    model.load_state_dict(sd, strict=False)
+    model.eval()
+    from oracle import caption as OC     # prompt ids exactly as dataset.py builds them (pinned)
+    table, label_ids = S.label_table(), S.label_token_table()
+    emb = S.synthetic_clap_embeddings(n_clips, seed=4242)
+    hard_rows, greedy_rows, margin_rows, std_rows = [], [], [], []
+    t0 = time.time()
+    for i in range(n_clips):
+        e = torch.nn.functional.normalize(emb[i:i + 1], dim=-1)
+        idx = OC.sound_effect_choice(emb[i:i + 1], table, SOUND_EFFECT_NUM)[0].tolist()
+        hard = torch.tensor([OC.prompt_ids(idx, label_ids)])
+        with torch.no_grad():
+            pe, _ = model.clap_to_gpt(e.unsqueeze(0), model.gpt.transformer.wte(hard))
+            out = G.generate2(model, IdTokenizer(), embed=pe, entry_length=entry_length)
+            ids = [int(t) for t in out.split()]
+            seq = torch.cat([pe, model.gpt.transformer.wte(torch.tensor([ids[:-1]]))], 1) \
+                if len(ids) > 1 else pe
+            logits = model.gpt(inputs_embeds=seq).logits[0, pe.shape[1] - 1:]
+        hard_rows.append(hard[0].tolist())
+        greedy_rows.append(ids)
+        margin_rows.append(_step_margins(model, pe, ids))
+        std_rows.append(logits.std(-1).tolist())
+        if i % 8 == 0:
+            print(f"  margin clip {i}: gen={len(ids)} min margin {min(margin_rows[-1]):.3g} "
+                  f"logit std {std_rows[-1][0]:.3g} ({time.time() - t0:.0f}s)", flush=True)
+    hard, hard_len = _pad(hard_rows)
+    greedy, greedy_len = _pad(greedy_rows)
+    marg = np.zeros(greedy.shape, np.float32)
+    lstd = np.zeros(greedy.shape, np.float32)
+    for i, (m, s) in enumerate(zip(margin_rows, std_rows)):
+        marg[i, :len(m)] = m
+        lstd[i, :len(s)] = s
+    _save(name + ".npz", clap_emb=emb.numpy(), hard_ids=hard, hard_len=hard_len,
+          greedy_ids=greedy, greedy_len=greedy_len, margin=marg, logit_std=lstd,
+          entry_length=np.int64(entry_length), gpt2_kw=np.array(
+              [kw["seed"], kw["std"], kw["emb_std"], kw["stop_boost"]], np.float64))
 
 
 def gen_beam(n_clips=4, entry_length=67):
@@ -268,7 +347,8 @@ def gen_keys():
 
 
 ALL = {"prompt": gen_prompt, "mappers": gen_mappers, "htsat": gen_htsat, "cnn14": gen_cnn14,
-       "beam": gen_beam, "c1": gen_c1, "keys": gen_keys}
+       "beam": gen_beam, "c1": gen_c1, "keys": gen_keys,
+       "margin": gen_margin, "margin_flat": lambda: gen_margin(name="c2_margin_flat")}
 
 if __name__ == "__main__":
     torch.set_num_threads(os.cpu_count() or 8)

@@ -53,3 +53,64 @@ def test_gather_token_ids_gloo_world2():
         L = c % 5 + 1
         assert lens[c] == L
         assert ids[c][:L] == [c * 100 + t for t in range(L)]
+
+
+def _bench_worker(rank, world, port, n, B, q):
+    """The bench's N>1 path: shard_range over a fixed clip set, per-batch CaptionBatch-like
+    results (greedy and beam), zsaac.dist.collect_captions; and the C4 embedding gather."""
+    import torch.distributed as dist
+    from types import SimpleNamespace
+    from zsaac import dist as zd
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    lo, hi = zd.shard_range(n, rank, world)
+    counts = zd.shard_counts(n, world)
+    T = 9
+    greedy, beam = [], []
+    for b0 in range(lo, hi, B):                  # the rank's eval batches, last one ragged
+        clips = list(range(b0, min(hi, b0 + B)))
+        ids = torch.zeros(len(clips), T, dtype=torch.int32)
+        ln = torch.zeros(len(clips), dtype=torch.int32)
+        bids = torch.zeros(len(clips), 3, T, dtype=torch.int32)
+        bl = torch.ones(len(clips), 3)
+        sc = torch.zeros(len(clips), 3)
+        for i, c in enumerate(clips):
+            L = c % 7 + 1
+            ids[i, :L] = torch.arange(L, dtype=torch.int32) + 1000 * c
+            ln[i] = L
+            best = c % 3                           # beam `best` has the best score / length
+            for k in range(3):
+                bids[i, k, :L] = torch.arange(L, dtype=torch.int32) + 1000 * c + 100 * k
+                bl[i, k] = L
+                sc[i, k] = -10.0 + (5.0 if k == best else 0.0)
+        greedy.append(SimpleNamespace(ids=ids, lengths=ln, scores=None))
+        beam.append(SimpleNamespace(ids=bids, lengths=bl, scores=sc))
+    gi, gl = zd.collect_captions(greedy, counts)
+    bi, bl = zd.collect_captions(beam, counts)
+    emb = torch.arange(lo, hi, dtype=torch.float32).view(-1, 1).repeat(1, 4)
+    ge = zd.gather_rows(emb, counts)
+    if rank == 0:
+        q.put((gi.tolist(), gl.tolist(), bi.tolist(), bl.tolist(), ge.tolist()))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_bench_gather_path_gloo_world2():
+    n, B, world = 45, 8, 2                        # 23 + 22 clips: ragged last batches
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_bench_worker, args=(r, world, port, n, B, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    gi, gl, bi, bl, ge = q.get(timeout=120)
+    for p in ps:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    assert len(gi) == n and len(bi) == n and len(ge) == n
+    for c in range(n):
+        L = c % 7 + 1
+        assert gl[c] == L and gi[c][:L] == [1000 * c + t for t in range(L)]
+        assert bl[c] == L and bi[c][:L] == [1000 * c + 100 * (c % 3) + t for t in range(L)]
+        assert ge[c] == [float(c)] * 4

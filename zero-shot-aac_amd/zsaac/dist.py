@@ -20,32 +20,56 @@ def shard_range(n: int, rank: int, world: int) -> Tuple[int, int]:
     return lo, lo + base + (1 if rank < extra else 0)
 
 
-def gather_token_ids(ids: torch.Tensor, lengths: torch.Tensor, n_per_rank: Sequence[int],
-                     group=None) -> Tuple[torch.Tensor, torch.Tensor]:
-    """All-gather ``ids`` [n_local, T] int32 and ``lengths`` [n_local] from every rank into
-    [sum(n_per_rank), T] / [sum] in rank order.  Ranks pad to max(n_per_rank) rows so the
-    collective is a single fixed-size all_gather_into_tensor (RCCL) or all_gather (gloo)."""
+def shard_counts(n: int, world: int) -> List[int]:
+    """Clips per rank under shard_range."""
+    return [shard_range(n, r, world)[1] - shard_range(n, r, world)[0] for r in range(world)]
+
+
+def gather_rows(t: torch.Tensor, n_per_rank: Sequence[int], group=None) -> torch.Tensor:
+    """All-gather the leading-dimension rows ``t`` [n_local, ...] of every rank into
+    [sum(n_per_rank), ...] in rank order.  Ranks pad to max(n_per_rank) rows so the collective is
+    ONE fixed-size all_gather_into_tensor (RCCL over xGMI) or all_gather (gloo)."""
     import torch.distributed as dist
     world = dist.get_world_size(group)
     nmax = max(n_per_rank)
-    T = ids.shape[1]
-    pad_ids = torch.zeros(nmax, T, dtype=ids.dtype, device=ids.device)
-    pad_len = torch.zeros(nmax, dtype=lengths.dtype, device=lengths.device)
-    pad_ids[:ids.shape[0]] = ids
-    pad_len[:lengths.shape[0]] = lengths
+    pad = torch.zeros((nmax,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+    pad[:t.shape[0]] = t
     if dist.get_backend(group) == "nccl":
-        all_ids = torch.empty(world * nmax, T, dtype=ids.dtype, device=ids.device)
-        all_len = torch.empty(world * nmax, dtype=lengths.dtype, device=lengths.device)
-        dist.all_gather_into_tensor(all_ids, pad_ids, group=group)
-        dist.all_gather_into_tensor(all_len, pad_len, group=group)
+        out = torch.empty((world * nmax,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+        dist.all_gather_into_tensor(out, pad, group=group)
     else:
-        li = [torch.empty_like(pad_ids) for _ in range(world)]
-        ll = [torch.empty_like(pad_len) for _ in range(world)]
-        dist.all_gather(li, pad_ids, group=group)
-        dist.all_gather(ll, pad_len, group=group)
-        all_ids, all_len = torch.cat(li), torch.cat(ll)
+        parts = [torch.empty_like(pad) for _ in range(world)]
+        dist.all_gather(parts, pad, group=group)
+        out = torch.cat(parts)
     keep: List[int] = []
     for r, n in enumerate(n_per_rank):
         keep.extend(range(r * nmax, r * nmax + n))
-    idx = torch.tensor(keep, device=ids.device)
-    return all_ids.index_select(0, idx), all_len.index_select(0, idx)
+    return out.index_select(0, torch.tensor(keep, device=t.device))
+
+
+def gather_token_ids(ids: torch.Tensor, lengths: torch.Tensor, n_per_rank: Sequence[int],
+                     group=None) -> Tuple[torch.Tensor, torch.Tensor]:
+    """All-gather ``ids`` [n_local, T] int32 and ``lengths`` [n_local] from every rank into
+    [sum(n_per_rank), T] / [sum] in rank order (the one collective of the caption path).  The
+    lengths travel as an extra column of the id rows: one all-gather, not two."""
+    T = ids.shape[1]
+    both = torch.cat([ids.to(torch.int32), lengths.to(torch.int32).view(-1, 1)], 1)
+    out = gather_rows(both, n_per_rank, group)
+    return out[:, :T].to(ids.dtype), out[:, T].to(lengths.dtype)
+
+
+def collect_captions(results, n_per_rank: Sequence[int], group=None):
+    """The bench / predict N>1 collective: the local CaptionBatch results (in clip order; greedy
+    ids [b, T] + lengths [b], or beam [b, beam, T] + seq_len / scores [b, beam] of which the best
+    beam is gathered) -> every rank's clips' token ids and lengths, in global clip order."""
+    ids, ln = [], []
+    for r in results:
+        if r.ids.dim() == 2:
+            ids.append(r.ids)
+            ln.append(r.lengths.int())
+        else:      # beam: the best beam (scores / seq_len, first on ties as a stable sort)
+            best = (r.scores / r.lengths).argmax(1)
+            ar = torch.arange(best.numel(), device=best.device)
+            ids.append(r.ids[ar, best])
+            ln.append(r.lengths[ar, best].int())
+    return gather_token_ids(torch.cat(ids), torch.cat(ln), n_per_rank, group)
