@@ -60,6 +60,13 @@ int zs_logmel(const float* wav, int B, int T, const float* window, const float* 
  * the time axis T_in -> 1024 and fold (B,1,1024,64) -> (B,256,256).  in [B][T_in][64] f32. */
 int zs_wav2img(const float* in, int B, int T_in, float* img, void* stream);
 
+/* zs_pack_clips: ragged mono clips (clip b = flat[offsets[b] .. offsets[b] + lengths[b])) ->
+ * out [B][T] f32: each cropped to its first T samples or zero-padded at the end, exactly as
+ * data_handing/embeddings_generator.py:53-59 fits clips to max_length * sr before encode_audio.
+ * T % 4 == 0; out 16-byte aligned. */
+int zs_pack_clips(const float* flat, const long* offsets, const int* lengths, int B, int T,
+                  float* out, void* stream);
+
 /* zs_patch_embed: htsat.py:115-125 PatchEmbed (Conv2d 1->96, k4 s4) + LayerNorm(96):
  * img [B][256][256] f32 -> x [B*4096][96] f32 (token = row*64 + col of the 64x64 patch grid). */
 int zs_patch_embed(const float* img, int B, const float* w /*[96][16]*/, const float* b,
@@ -165,6 +172,22 @@ int zs_prompt_assemble(const float* emb, int B, int D, const float* labels, int 
 int zs_row_attention(const void* q, int ldq, const void* k, const void* v, int ldkv, int B, int L,
                      const int* len, int heads, int hd, int causal, float scale, void* out, int ldo,
                      int dtype, void* stream);
+
+/* zs_cross_attention: nn.MultiheadAttention's core (after in_proj, before out_proj) for short
+ * key sets: out(b, i, h) = softmax_j(scale * q(b,i,h) . k(b,j,h)) v(b,j,h), j < Lk; q rows
+ * b*Lq + i (ldq), k / v rows b*Lk + j (ldkv), head h at columns h*hd.. (dtype).  Serves the
+ * sound-effect cross-attention of ClapCaptionCrossattention[_v2] (models/caption_model.py:100-206,
+ * nn.MultiheadAttention(prefix_size, 4)).  Lk <= 64, hd <= 256. */
+int zs_cross_attention(const void* q, int ldq, const void* k, const void* v, int ldkv, int B,
+                       int Lq, int Lk, int heads, int hd, float scale, void* out, int ldo,
+                       int dtype, void* stream);
+
+/* zs_label_topk: sound_effect_choice (caption_model.py:15-20, utils.py:131-137): per row b the
+ * k labels (of L, rows of labels [L][D] f32) with the highest similarity emb[b] . label, best
+ * first, ties to the lower index (softmax is monotone); idx [B][k] int32 (may be NULL) and the
+ * chosen rows gathered into rows [B][k][D] f32.  k <= 16, (D + L) * 4 <= 64 KB. */
+int zs_label_topk(const float* emb, int B, int D, const float* labels, int L, int k, int* idx,
+                  float* rows, void* stream);
 
 /* ------------------------------------------------------------------ GPT-2 decode
  * zs_gpt2_prefill_embed: clap_to_gpt (caption_model.py:315-329) + the caller's wte lookup

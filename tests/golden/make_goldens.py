@@ -20,6 +20,8 @@ Fixture list (reference call sites in brackets):
                   audio_proj/normalize (ase_model.py:52-55).
   cnn14.npz       CNN14 forward from log-mel (cnns.py:171-201) + audio_proj/normalize.
   prompt.npz      compose_discrete_prompts strings + padding_captions (utils.py:158-208).
+  variants.npz    ClapCaptionModel + sound-effect MLP, ClapCaptionCrossattention[_v2],
+                  ClapCaptionPrefix: clap_to_gpt outputs and generate2 ids.
   c2_margin.npz   generate2 with the reference's top-1/top-2 logit margin at every generated
   c2_margin_flat.npz  step, on smaller decoder weights (the bf16 id-parity check).
 """
@@ -217,6 +219,55 @@ def gen_margin(n_clips=32, entry_length=67, name="c2_margin"):
               [kw["seed"], kw["std"], kw["emb_std"], kw["stop_boost"]], np.float64))
 
 
+VARIANTS = ("se_mlp", "xattn", "xattn_v2", "prefix")
+
+
+def gen_variants(n_clips=3, entry_length=30):
+    """variants.npz: the other caption-model classes of models/caption_model.py on the same
+    decoder weights: ClapCaptionModel with sound_effect_embeddings (sound-effect MLP tokens,
+    lines 15-21, 63-82), ClapCaptionCrossattention (100-149), ClapCaptionCrossattention_v2 at
+    eval (151-206) and ClapCaptionPrefix (90-98): clap_to_gpt outputs for a prefix + text tokens,
+    and generate2 ids (gpt2_prefix_eval.py:161-222) on each clip's clap_to_gpt(prefix)."""
+    import gpt2_prefix_eval as G
+    from models import caption_model as CM
+    table = S.label_table()
+    emb = torch.nn.functional.normalize(S.synthetic_clap_embeddings(n_clips, seed=77), dim=-1)
+    prefix = emb.unsqueeze(1)                                      # [n, 1, 1024]
+    tokens = torch.tensor([[1858, 389, 1223, 287, 428, 6597]] * n_clips)
+    out = {"prefix": prefix.numpy(), "tokens": tokens.numpy(), "table_seed": np.int64(6),
+           "sound_effect_num": np.int64(SOUND_EFFECT_NUM), "entry_length": np.int64(entry_length)}
+    for name in VARIANTS:
+        sd = S.gpt2_state_dict(**GPT2_KW)
+        sd.update(S.mlp_mapper_state_dict(1))
+        kw = dict(prefix_size=1024, mapping_type="mlp")
+        if name == "se_mlp":
+            m = CM.ClapCaptionModel(10, sound_effect_embeddings=table,
+                                    sound_effect_num=SOUND_EFFECT_NUM, **kw)
+            sd.update(S.sound_effect_mlp_state_dict(11))
+        elif name == "prefix":
+            m = CM.ClapCaptionPrefix(10, **kw)
+        else:
+            cls = CM.ClapCaptionCrossattention if name == "xattn" else CM.ClapCaptionCrossattention_v2
+            m = cls(10, sound_effect_embeddings=table, sound_effect_num=SOUND_EFFECT_NUM, **kw)
+            sd.update(S.sound_effect_mha_state_dict(12))
+        missing, unexpected = m.load_state_dict(sd, strict=False)
+        assert not unexpected, unexpected
+        assert all("attn.bias" in k or "masked_bias" in k for k in missing), missing
+        m.eval()
+        with torch.no_grad():
+            cat, _ = m.clap_to_gpt(prefix, m.gpt.transformer.wte(tokens))
+            ids = []
+            for i in range(n_clips):
+                pe, _ = m.clap_to_gpt(prefix[i:i + 1])
+                ids.append([int(t) for t in G.generate2(m, IdTokenizer(), embed=pe,
+                                                        entry_length=entry_length).split()])
+        g_ids, g_len = _pad(ids)
+        out[f"{name}_cat"] = cat.numpy()
+        out[f"{name}_ids"], out[f"{name}_len"] = g_ids, g_len
+        print(f"  {name}: clap_to_gpt {tuple(cat.shape)}, greedy lengths {g_len.tolist()}", flush=True)
+    _save("variants.npz", **out)
+
+
 def gen_beam(n_clips=4, entry_length=67):
     import gpt2_prefix_eval as G
     model = _caption_model("mlp")
@@ -348,7 +399,8 @@ def gen_keys():
 
 ALL = {"prompt": gen_prompt, "mappers": gen_mappers, "htsat": gen_htsat, "cnn14": gen_cnn14,
        "beam": gen_beam, "c1": gen_c1, "keys": gen_keys,
-       "margin": gen_margin, "margin_flat": lambda: gen_margin(name="c2_margin_flat")}
+       "margin": gen_margin, "margin_flat": lambda: gen_margin(name="c2_margin_flat"),
+       "variants": gen_variants}
 
 if __name__ == "__main__":
     torch.set_num_threads(os.cpu_count() or 8)

@@ -98,3 +98,29 @@ def test_ase_encode_audio(cuda):
     with torch.no_grad():
         ref = A.audio_project(A.htsat_embedding(OF.logmel(wav), sd), sd)
     assert float((got - ref).abs().max()) < 2e-3
+
+
+def test_extract_embeddings_ragged(cuda):
+    """Extract_embeddings semantics (embeddings_generator.py:53-59): a 25 s clip is cropped to
+    its first 10 s, a 4 s clip zero-padded, an empty clip skipped; embeddings equal the encoder on
+    the cropped / padded waveforms and the oracle within the bf16 bound; records as the
+    reference's data.pkl."""
+    from oracle import audio as A, frontend as OF
+    from zsaac import synthetic as S
+    from zsaac.extract import EmbeddingExtractor
+    asd = S.htsat_state_dict(3)
+    asd.update(S.audio_proj_state_dict(5))
+    g = torch.Generator(device="cpu").manual_seed(25)
+    clips = [(torch.randn(800000, generator=g) * 0.1).clamp(-1, 1), torch.zeros(0),
+             (torch.randn(128000, generator=g) * 0.1).clamp(-1, 1)]
+    ex = EmbeddingExtractor(asd, "htsat", torch.bfloat16, batch=4, device=cuda)
+    recs = ex.extract(clips, ["a", "empty", "c"], [["cap a"], ["x"], ["cap c"]])
+    assert [r["audio_id"] for r in recs] == ["a", "c"]
+    fitted = torch.stack([clips[0][:320000], torch.nn.functional.pad(clips[2], [0, 192000])])
+    direct = ex.enc.encode(fitted.to(cuda)).cpu()
+    got = torch.cat([r["audio_embedding"] for r in recs])
+    assert torch.equal(got, direct)
+    with torch.no_grad():
+        ref = A.audio_project(A.htsat_embedding(OF.logmel(fitted), asd), asd)
+    cos = torch.nn.functional.cosine_similarity(got, ref, dim=-1)
+    assert float(cos.min()) > 0.995, cos

@@ -747,3 +747,19 @@ def test_gemm_skinny_shared_workspace(cuda):
             out = torch.empty(M, N, device=cuda)
             ops.gemm(a, w, out)
             assert _rel(out, a @ w.t()) < 1e-4, (rep, M, N, K)
+
+
+def test_pack_clips(cuda):
+    """zs_pack_clips: ragged clips cropped to their first T samples or zero-padded."""
+    from zsaac import ops
+    T = 1000
+    lens = [2500, 0, 7, 1000, 999, 1]
+    g = torch.Generator(device="cpu").manual_seed(2)
+    clips = [torch.randn(n, generator=g) for n in lens]
+    flat = torch.cat(clips).to(cuda)
+    offs = torch.tensor([0] + list(torch.tensor(lens).cumsum(0)[:-1]), dtype=torch.int64, device=cuda)
+    out = torch.full((len(lens), T), 7.0, device=cuda)
+    ops.pack_clips(flat, offs, torch.tensor(lens, dtype=torch.int32, device=cuda), T, out)
+    for b, c in enumerate(clips):
+        ref = torch.nn.functional.pad(c[:T], [0, max(0, T - len(c))])
+        assert torch.equal(out[b].cpu(), ref), b

@@ -845,6 +845,48 @@ __global__ void kv_write_kernel(const T* __restrict__ qkv, int R, int n, int D, 
   vc[slot] = qkv[t * 3 * D + 2 * D + c];
 }
 
+// nn.MultiheadAttention's attention core for a few keys (the sound-effect cross-attention of
+// caption_model.py:100-206: one CLAP query against the k chosen label embeddings, 4 heads of 256):
+// one wave per (batch row b, query i, head h); lane l holds dims l, l+64, ... of the head;
+// scores by wave reductions, softmax over the Lk keys in f32, out = sum_j p_j v_j.
+template <typename T>
+__global__ __launch_bounds__(64) void cross_attn_kernel(const T* __restrict__ q, int ldq,
+                                                        const T* __restrict__ k,
+                                                        const T* __restrict__ v, int ldkv, int Lq,
+                                                        int Lk, int hd, float scale,
+                                                        T* __restrict__ out, int ldo) {
+  const int bi = blockIdx.x, h = blockIdx.y, lane = threadIdx.x;
+  const int b = bi / Lq;
+  const T* qr = q + (long)bi * ldq + h * hd;
+  float qv[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) qv[t] = lane + 64 * t < hd ? ldf(qr + lane + 64 * t) : 0.f;
+  float s[64];
+  float mx = -INFINITY;
+  for (int j = 0; j < Lk; ++j) {
+    const T* kr = k + ((long)b * Lk + j) * ldkv + h * hd;
+    float a = 0.f;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) if (lane + 64 * t < hd) a += qv[t] * ldf(kr + lane + 64 * t);
+    a = wave_sum(a) * scale;
+    s[j < 64 ? j : 63] = a;
+    mx = fmaxf(mx, a);
+  }
+  float den = 0.f;
+  for (int j = 0; j < Lk; ++j) { s[j] = expf(s[j] - mx); den += s[j]; }
+  const float inv = 1.0f / den;
+  float o[4] = {0.f, 0.f, 0.f, 0.f};
+  for (int j = 0; j < Lk; ++j) {
+    const T* vr = v + ((long)b * Lk + j) * ldkv + h * hd;
+    const float p = s[j] * inv;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) if (lane + 64 * t < hd) o[t] += p * ldf(vr + lane + 64 * t);
+  }
+  T* orow = out + (long)bi * ldo + h * hd;
+#pragma unroll
+  for (int t = 0; t < 4; ++t) if (lane + 64 * t < hd) stf(orow + lane + 64 * t, o[t]);
+}
+
 }  // namespace zs
 
 using namespace zs;
@@ -948,6 +990,23 @@ extern "C" int zs_decode_attention_map(const void* qkv, int R, const int* rowmap
                        S(stream), (const bf16_t*)qkv, D, heads, (bf16_t*)kc, (bf16_t*)vc, Lmax,
                        pos, (const int*)nullptr, (bf16_t*)out, rowmap, cpos, nphys);
   }
+  ZS_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int zs_cross_attention(const void* q, int ldq, const void* k, const void* v, int ldkv,
+                                  int B, int Lq, int Lk, int heads, int hd, float scale, void* out,
+                                  int ldo, int dtype, void* stream) {
+  ZS_REQUIRE(B > 0 && Lq > 0 && Lk > 0 && Lk <= 64 && heads > 0 && hd > 0 && hd <= 256,
+             "zs_cross_attention: Lk <= 64, hd <= 256");
+  const dim3 grid(B * Lq, heads);
+  if (dtype == ZS_BF16)
+    hipLaunchKernelGGL(cross_attn_kernel<bf16_t>, grid, dim3(64), 0, S(stream), (const bf16_t*)q,
+                       ldq, (const bf16_t*)k, (const bf16_t*)v, ldkv, Lq, Lk, hd, scale,
+                       (bf16_t*)out, ldo);
+  else
+    hipLaunchKernelGGL(cross_attn_kernel<float>, grid, dim3(64), 0, S(stream), (const float*)q, ldq,
+                       (const float*)k, (const float*)v, ldkv, Lq, Lk, hd, scale, (float*)out, ldo);
   ZS_LAUNCH_CHECK();
   return 0;
 }

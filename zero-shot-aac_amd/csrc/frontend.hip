@@ -509,9 +509,41 @@ __global__ __launch_bounds__(256) void patch_embed_kernel(const float* __restric
   }
 }
 
+// Ragged clips -> [B][T] fixed-length rows (data_handing/embeddings_generator.py:53-59): clip b
+// (length len[b], starting at off[b] of one flat buffer) is cropped to its first T samples or
+// zero-padded at the end.  float4 stores; the source is read with scalar loads (clip offsets
+// need not be 16-byte aligned).
+__global__ __launch_bounds__(256) void pack_clips_kernel(const float* __restrict__ flat,
+                                                         const long* __restrict__ off,
+                                                         const int* __restrict__ len, int T,
+                                                         float* __restrict__ out) {
+  const int b = blockIdx.y;
+  const long o = off[b];
+  const int n = min(len[b], T);
+  for (int i = 4 * (blockIdx.x * 256 + threadIdx.x); i < T; i += 4 * 256 * gridDim.x) {
+    float4 v;
+    v.x = i < n ? flat[o + i] : 0.f;
+    v.y = i + 1 < n ? flat[o + i + 1] : 0.f;
+    v.z = i + 2 < n ? flat[o + i + 2] : 0.f;
+    v.w = i + 3 < n ? flat[o + i + 3] : 0.f;
+    *reinterpret_cast<float4*>(out + (long)b * T + i) = v;
+  }
+}
+
 }  // namespace zs
 
 using namespace zs;
+
+extern "C" int zs_pack_clips(const float* flat, const long* offsets, const int* lengths, int B,
+                             int T, float* out, void* stream) {
+  ZS_REQUIRE(B > 0 && T > 0 && T % 4 == 0, "zs_pack_clips: B > 0, T > 0, T %% 4 == 0");
+  ZS_REQUIRE(flat && offsets && lengths && out && ((uintptr_t)out & 15) == 0,
+             "zs_pack_clips: pointers (out 16-byte aligned)");
+  hipLaunchKernelGGL(pack_clips_kernel, dim3(std::min(cdiv(T, 1024), 64), B), dim3(256), 0,
+                     S(stream), flat, offsets, lengths, T, out);
+  ZS_LAUNCH_CHECK();
+  return 0;
+}
 
 extern "C" int zs_logmel(const float* wav, int B, int T, const float* window, const float* twiddle,
                          const float* melW, const int* mel_lo, const int* mel_hi,

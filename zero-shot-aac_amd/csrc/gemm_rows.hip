@@ -28,6 +28,25 @@ namespace zs {
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8r_t;
 typedef __attribute__((ext_vector_type(4))) float f32x4r_t;
 
+#ifdef ZS_STAMPS
+// diagnostic build only (tools/hip/rows_stamps.cpp): s_memrealtime (100 MHz) stamps of each
+// workgroup's phases, written by thread 0 into a buffer no other code reads
+__device__ unsigned long long* zs_stamp_buf;
+extern "C" int zs_set_stamp_buf(void* p) {
+  return (int)hipMemcpyToSymbol(HIP_SYMBOL(zs_stamp_buf), &p, sizeof(p));
+}
+#define ZS_STAMP(slot)                                                                           \
+  do {                                                                                           \
+    __builtin_amdgcn_sched_barrier(0);                                                           \
+    unsigned long long t_;                                                                       \
+    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");              \
+    if (threadIdx.x == 0 && zs_stamp_buf) zs_stamp_buf[blockIdx.x * 8 + (slot)] = t_;            \
+    __builtin_amdgcn_sched_barrier(0);                                                           \
+  } while (0)
+#else
+#define ZS_STAMP(slot) do {} while (0)
+#endif
+
 constexpr int RG = 16;              // rows per group
 constexpr int RG_MAX_M = 64;
 constexpr int RG_MAX_LOADS = 36;    // 16-byte loads in flight per lane (VGPR budget)
@@ -55,6 +74,7 @@ __global__ __launch_bounds__(64 * WAVES) void gemm_rows_kernel(RowsArgs g) {
   static_assert(S * (LN ? NB : NB + 1) <= RG_MAX_LOADS, "rows kernel: VGPR budget");
   // LDS: [LN rows: 16 x (K + 8) bf16] [partials: WAVES x 16 x NT f32]
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  ZS_STAMP(0);
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   // XCD-aware bijective remap: blocks id, id+8, ... share an XCD -> consecutive work units
   const int nwg = gridDim.x, id = blockIdx.x, xcd = id & 7, q8 = nwg >> 3, r8 = nwg & 7;
@@ -122,6 +142,11 @@ __global__ __launch_bounds__(64 * WAVES) void gemm_rows_kernel(RowsArgs g) {
   // loads next to their MFMAs and waits on each group)
   asm volatile("" ::: "memory");
   __builtin_amdgcn_sched_barrier(0);
+  ZS_STAMP(1);
+#ifdef ZS_STAMPS
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  ZS_STAMP(2);
+#endif
 
   if constexpr (LN) {
     float s = 0.f;
@@ -151,6 +176,7 @@ __global__ __launch_bounds__(64 * WAVES) void gemm_rows_kernel(RowsArgs g) {
     }
     __syncthreads();
   }
+  ZS_STAMP(3);
 
   f32x4r_t acc[NB];
 #pragma unroll
@@ -173,7 +199,9 @@ __global__ __launch_bounds__(64 * WAVES) void gemm_rows_kernel(RowsArgs g) {
   for (int nb = 0; nb < NB; ++nb)
 #pragma unroll
     for (int i = 0; i < 4; ++i) mine[(4 * (lane >> 4) + i) * NT + 16 * nb + fr] = acc[nb][i];
+  ZS_STAMP(4);
   __syncthreads();
+  ZS_STAMP(5);
   if (!epi) return;
   float4 sum = *reinterpret_cast<const float4*>(red + erow * NT + 4 * ecq);
 #pragma unroll
@@ -204,6 +232,7 @@ __global__ __launch_bounds__(64 * WAVES) void gemm_rows_kernel(RowsArgs g) {
       else reinterpret_cast<float*>(g.out)[(long)em * g.ldo + en + j] = v[j];
     }
   }
+  ZS_STAMP(6);
 }
 
 int g_gemm_rows = 1;   // A/B knob (zs_tune_set "gemm_rows"): 0 = skinny split-K kernel for M <= 64

@@ -10,19 +10,12 @@
 namespace zs {
 
 // ------------------------------------------------------------------ prompt
-__global__ __launch_bounds__(256) void prompt_kernel(const float* __restrict__ emb, int D,
-                                                     const float* __restrict__ labels, int L,
-                                                     int k, const int* __restrict__ ltok,
-                                                     const int* __restrict__ llen, int max_tok,
-                                                     int* __restrict__ hard_ids, int h_cap,
-                                                     int* __restrict__ hard_len,
-                                                     int* __restrict__ chosen) {
-  extern __shared__ float sm[];
-  float* e = sm;          // [D]
-  float* sim = sm + D;    // [L]
-  __shared__ int sel[16];
-  __shared__ float rv[4];
-  __shared__ int ri[4];
+// sound_effect_choice (utils.py:131-137 / caption_model.py:15-20): the k labels of highest
+// similarity emb . label (softmax is monotone, so top-k of the raw similarities), best first,
+// ties to the lower label index; one 256-thread block per row, result in sel[0..k).
+__device__ __forceinline__ void label_select(const float* __restrict__ emb, int D,
+                                             const float* __restrict__ labels, int L, int k,
+                                             float* e, float* sim, int* sel, float* rv, int* ri) {
   const int b = blockIdx.x;
   for (int d = threadIdx.x; d < D; d += 256) e[d] = emb[(long)b * D + d];
   __syncthreads();
@@ -59,6 +52,21 @@ __global__ __launch_bounds__(256) void prompt_kernel(const float* __restrict__ e
     }
     __syncthreads();
   }
+}
+
+__global__ __launch_bounds__(256) void prompt_kernel(const float* __restrict__ emb, int D,
+                                                     const float* __restrict__ labels, int L,
+                                                     int k, const int* __restrict__ ltok,
+                                                     const int* __restrict__ llen, int max_tok,
+                                                     int* __restrict__ hard_ids, int h_cap,
+                                                     int* __restrict__ hard_len,
+                                                     int* __restrict__ chosen) {
+  extern __shared__ float sm[];
+  __shared__ int sel[16];
+  __shared__ float rv[4];
+  __shared__ int ri[4];
+  const int b = blockIdx.x;
+  label_select(emb, D, labels, L, k, sm, sm + D, sel, rv, ri);
   if (threadIdx.x == 0) {
     int* out = hard_ids + (long)b * h_cap;
     int n = 0;
@@ -78,6 +86,24 @@ __global__ __launch_bounds__(256) void prompt_kernel(const float* __restrict__ e
     hard_len[b] = n < h_cap ? n : h_cap;
     for (int t = n; t < h_cap; ++t) out[t] = 0;
   }
+}
+
+// the chosen labels' rows gathered: rows[b][q][:] = labels[sel[q]][:] (caption_model.py:15-20,
+// sound_effect_embeddings[index].squeeze(1)), and their indices
+__global__ __launch_bounds__(256) void label_topk_kernel(const float* __restrict__ emb, int D,
+                                                         const float* __restrict__ labels, int L,
+                                                         int k, int* __restrict__ idx,
+                                                         float* __restrict__ rows) {
+  extern __shared__ float sm[];
+  __shared__ int sel[16];
+  __shared__ float rv[4];
+  __shared__ int ri[4];
+  const int b = blockIdx.x;
+  label_select(emb, D, labels, L, k, sm, sm + D, sel, rv, ri);
+  if (idx && threadIdx.x < k) idx[(long)b * k + threadIdx.x] = sel[threadIdx.x];
+  for (int q = 0; q < k; ++q)
+    for (int d = threadIdx.x; d < D; d += 256)
+      rows[((long)b * k + q) * D + d] = labels[(long)sel[q] * D + d];
 }
 
 // ------------------------------------------------------------------ embeddings
@@ -428,6 +454,18 @@ extern "C" int zs_prompt_assemble(const float* emb, int B, int D, const float* l
   ZS_REQUIRE(smem <= 64 * 1024, "zs_prompt_assemble: D+L too large");
   hipLaunchKernelGGL(prompt_kernel, dim3(B), dim3(256), smem, S(stream), emb, D, labels, L, k,
                      label_tok, label_len, max_tok, hard_ids, h_cap, hard_len, chosen);
+  ZS_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int zs_label_topk(const float* emb, int B, int D, const float* labels, int L, int k,
+                             int* idx, float* rows, void* stream) {
+  ZS_REQUIRE(B > 0 && D > 0 && L > 0 && k >= 1 && k <= 16 && k <= L, "zs_label_topk: bad shape");
+  ZS_REQUIRE(emb && labels && rows, "zs_label_topk: null pointer");
+  const size_t smem = (size_t)(D + L) * sizeof(float);
+  ZS_REQUIRE(smem <= 64 * 1024, "zs_label_topk: D+L too large");
+  hipLaunchKernelGGL(label_topk_kernel, dim3(B), dim3(256), smem, S(stream), emb, D, labels, L, k,
+                     idx, rows);
   ZS_LAUNCH_CHECK();
   return 0;
 }

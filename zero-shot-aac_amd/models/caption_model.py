@@ -1,14 +1,19 @@
-"""Drop-in for the reference's ``models/caption_model.py`` caption classes on the hot path:
-``ClapCaptionModel`` (caption_model.py:13-89) and ``ClapCaption_prompt`` (291-338).
+"""Drop-in for the reference's ``models/caption_model.py`` caption classes:
+``ClapCaptionModel`` (caption_model.py:13-89) with and without the sound-effect projection,
+``ClapCaptionPrefix`` (90-98), ``ClapCaptionCrossattention`` (100-149),
+``ClapCaptionCrossattention_v2`` (151-206) and ``ClapCaption_prompt`` (291-338).
 
 Same constructor arguments and state-dict keys (``gpt.*`` = HF GPT2LMHeadModel layout, 149 keys,
-plus ``clap_project.*``), so ``load_state_dict(torch.load(best.pth))`` works unchanged.  The only
-construction difference: the reference fetches ``GPT2LMHeadModel.from_pretrained('gpt2')`` by name
-(caption_model.py:52); here ``gpt`` is built at the GPT-2-small architecture and its weights come
-from the checkpoint (``best.pth`` holds all of them).  Forward math runs on the HIP kernels.
+plus ``clap_project.*`` and ``sound_effect_project.*``), so ``load_state_dict(torch.load(...))``
+works unchanged.  The only construction difference: the reference fetches
+``GPT2LMHeadModel.from_pretrained('gpt2')`` by name (caption_model.py:52); here ``gpt`` is built at
+the GPT-2-small architecture and its weights come from the checkpoint.  Every forward runs on the
+HIP kernels: the mappers' GEMMs, sound_effect_choice (zs_label_topk), the cross-attention
+(in_proj / out_proj GEMMs + zs_cross_attention) and GPT-2.
 
-OUT OF SCOPE (not on the captioning hot path): training forward with labels, the sound-effect
-cross-attention variants (ClapCaptionCrossattention*) and the Mistral classes.
+Inference only: ``forward`` (the training forward, with labels and attention masks) serves
+labels=None / mask=None; ClapCaptionCrossattention_v2's training-time random key mask is not
+provided (eval uses no mask, caption_model.py:182-183).  The Mistral classes are not here.
 """
 from enum import Enum
 from typing import Optional
@@ -16,7 +21,8 @@ from typing import Optional
 import torch
 import torch.nn as nn
 
-from zsaac.modules import ZsGPT2LMHeadModel
+from zsaac import ops
+from zsaac.modules import EngineCache, ZsGPT2LMHeadModel, require_device, zs_dtype_of
 
 from .mapper import MLP, TransformerMapper
 
@@ -26,24 +32,105 @@ class MappingType(Enum):
     Transformer = 'transformer'
 
 
+class ZsMultiheadAttention(nn.Module):
+    """``nn.MultiheadAttention(embed_dim, num_heads, batch_first=True)`` (the sound-effect
+    cross-attention, caption_model.py:109, 160) with its parameter names (in_proj_weight,
+    in_proj_bias, out_proj.weight / .bias) and torch's initialisation; inference forward on the
+    HIP kernels: in_proj GEMMs -> zs_cross_attention -> out_proj GEMM (+ ``residual`` fused into
+    its epilogue).  Returns (attn_output, None): the averaged attention weights are not
+    computed (no caller reads them)."""
+
+    def __init__(self, embed_dim: int, num_heads: int, batch_first: bool = True, bias: bool = True):
+        super().__init__()
+        if not batch_first:
+            raise NotImplementedError("batch_first=False")
+        self.embed_dim, self.num_heads, self.batch_first = embed_dim, num_heads, batch_first
+        self.in_proj_weight = nn.Parameter(torch.empty(3 * embed_dim, embed_dim))
+        self.in_proj_bias = nn.Parameter(torch.zeros(3 * embed_dim)) if bias else None
+        self.out_proj = nn.Linear(embed_dim, embed_dim, bias=bias)
+        nn.init.xavier_uniform_(self.in_proj_weight)
+        if bias:
+            nn.init.zeros_(self.out_proj.bias)
+        self._cache = EngineCache()
+
+    def forward(self, query, key, value, attn_mask=None, need_weights=True, residual=None):
+        require_device(query, "MultiheadAttention.forward")
+        if attn_mask is not None:
+            raise NotImplementedError("attention masks (training-time) are not provided")
+        dt = zs_dtype_of(self)
+        E, H = self.embed_dim, self.num_heads
+        B, Lq, _ = query.shape
+        Lk = key.shape[1]
+        w = self._cache.get(self, lambda: (
+            self.in_proj_weight.detach().to(dt).contiguous(),
+            None if self.in_proj_bias is None else self.in_proj_bias.detach().float().contiguous(),
+            self.out_proj.weight.detach().to(dt).contiguous(),
+            None if self.out_proj.bias is None else self.out_proj.bias.detach().float().contiguous()),
+            (dt,))
+        wi, bi, wo, bo = w
+        dev = query.device
+
+        def rows(t, n):
+            r = torch.empty(n, E, device=dev, dtype=dt)
+            ops.cast(t.reshape(n, E).float().contiguous(), r)
+            return r
+        qa = rows(query, B * Lq)
+        q = torch.empty(B * Lq, E, device=dev, dtype=dt)
+        ops.gemm(qa, wi[:E], q, bias=None if bi is None else bi[:E])
+        kv = torch.empty(B * Lk, 2 * E, device=dev, dtype=dt)
+        if key is value:
+            ops.gemm(rows(key, B * Lk), wi[E:], kv, bias=None if bi is None else bi[E:])
+        else:
+            ops.gemm(rows(key, B * Lk), wi[E:2 * E], kv[:, :E], bias=None if bi is None else bi[E:2 * E])
+            ops.gemm(rows(value, B * Lk), wi[2 * E:], kv[:, E:], bias=None if bi is None else bi[2 * E:])
+        att = torch.empty(B * Lq, E, device=dev, dtype=dt)
+        ops.cross_attention(q, kv[:, :E], kv[:, E:], B, Lq, Lk, H, att)
+        out = torch.empty(B * Lq, E, device=dev)
+        res = None if residual is None else residual.reshape(B * Lq, E).float().contiguous()
+        if res is not None:
+            out.copy_(res)
+        ops.gemm(att, wo, out, bias=bo, residual=None if res is None else out)
+        return out.view(B, Lq, E), None
+
+
 class ClapCaptionModel(nn.Module):
+
+    def sound_effect_choice(self, prefix, sound_effect_embeddings, choice_num):
+        """caption_model.py:15-20: the choice_num label embeddings most similar to the prefix
+        (softmax is monotone: top-k of the similarities), [B, choice_num, D]; zs_label_topk."""
+        require_device(prefix, "sound_effect_choice")
+        D = prefix.shape[-1]
+        e = prefix.reshape(-1, D).float().contiguous()
+        rows = torch.empty(e.shape[0], choice_num, D, device=e.device)
+        ops.label_topk(e, sound_effect_embeddings.float().contiguous(), choice_num, rows)
+        return rows
 
     def get_dummy_token(self, batch_size: int, device: torch.device) -> torch.Tensor:
         return torch.zeros(batch_size, self.prefix_length, dtype=torch.int64, device=device)
 
-    def forward(self, *args, **kwargs):
-        raise NotImplementedError("training forward is out of scope; use clap_to_gpt + "
-                                  "gpt2_prefix_eval.generate2/generate_beam")
+    def _check_inference(self, mask, labels):
+        if labels is not None or mask is not None:
+            raise NotImplementedError("the training forward (labels / attention masks) is out of "
+                                      "scope; inference: forward(tokens, prefix)")
+
+    def forward(self, tokens: torch.Tensor, prefix: torch.Tensor, mask: Optional[torch.Tensor] = None,
+                labels: Optional[torch.Tensor] = None):
+        """caption_model.py:25-37 at inference (labels=None, mask=None): (gpt output, logits of
+        the positions after the sound-effect and prefix tokens)."""
+        self._check_inference(mask, labels)
+        embedding_text = self.gpt.transformer.wte(tokens)
+        embedding_cat, mask = self.clap_to_gpt(prefix, embedding_text, mask)
+        out = self.gpt(inputs_embeds=embedding_cat)
+        n = self.prefix_length + (self.sound_effect_num if self.sound_effect_embeddings is not None else 0)
+        return out, out.logits[:, n - 1: -1]
 
     def __init__(self, prefix_length: int, clip_length: Optional[int] = None, prefix_size: int = 512,
                  num_layers: int = 8, mapping_type='mlp', sound_effect_embeddings: torch.Tensor = None,
                  sound_effect_num: Optional[int] = 0, only_prefix: Optional[bool] = False,
                  mask_probability: Optional[float] = 0):
         super(ClapCaptionModel, self).__init__()
-        if sound_effect_embeddings is not None:
-            raise NotImplementedError("sound-effect projection variant is out of scope")
         self.prefix_length = prefix_length
-        self.sound_effect_embeddings = None
+        self.sound_effect_embeddings = sound_effect_embeddings
         self.sound_effect_num = sound_effect_num
         self.only_prefix = only_prefix
         self.mask_probability = mask_probability
@@ -55,19 +142,98 @@ class ClapCaptionModel(nn.Module):
         else:
             self.clap_project = TransformerMapper(prefix_size, self.gpt_embedding_size, prefix_length,
                                                   clip_length, num_layers)
+        if self.sound_effect_embeddings is not None:
+            self.sound_effect_project = MLP((prefix_size, self.gpt_embedding_size // 2,
+                                             self.gpt_embedding_size))
 
     def clap_to_gpt(self, prefix: torch.Tensor, embedding_text: Optional[torch.Tensor] = None,
                     mask: Optional[torch.Tensor] = None):
-        """caption_model.py:66-82 (without the sound-effect branch)."""
+        """caption_model.py:66-82: [sound-effect projections (k) ; mapper(prefix) ; text]."""
         proj = self.clap_project(prefix).view(-1, self.prefix_length, self.gpt_embedding_size)
         emb = proj if embedding_text is None else torch.cat((proj, embedding_text), dim=1)
+        if self.sound_effect_embeddings is not None:
+            se = self.sound_effect_choice(prefix, self.sound_effect_embeddings, self.sound_effect_num)
+            se_proj = self.sound_effect_project(se).view(-1, self.sound_effect_num, self.gpt_embedding_size)
+            emb = torch.cat((se_proj, emb), dim=1)
+            if mask is not None:
+                mask = torch.cat((torch.ones((prefix.shape[0], self.sound_effect_num), device=prefix.device),
+                                  mask), dim=-1)
         return emb, mask
 
     def set_dtype(self, dtype: torch.dtype):
         """float32 = parity mode (default), bfloat16 = perf mode, for every kernel engine."""
-        for m in (self, self.gpt, self.clap_project):
+        mods = [self, self.gpt, self.clap_project]
+        if hasattr(self, "sound_effect_project"):
+            mods.append(self.sound_effect_project)
+        for m in mods:
             m.zs_dtype = dtype
         return self
+
+
+class ClapCaptionPrefix(ClapCaptionModel):
+    """caption_model.py:90-98: only the mapper's parameters are trained; GPT-2 stays in eval."""
+
+    def parameters(self, recurse: bool = True):
+        return self.clap_project.parameters()
+
+    def train(self, mode: bool = True):
+        super(ClapCaptionPrefix, self).train(mode)
+        self.gpt.eval()
+        return self
+
+
+class ClapCaptionCrossattention(ClapCaptionModel):
+    """caption_model.py:100-149: the prefix attends over its k chosen sound-effect label
+    embeddings (nn.MultiheadAttention, 4 heads) and the attention output replaces it before the
+    mapper; no sound-effect tokens in the GPT-2 sequence."""
+
+    RESIDUAL = False
+
+    def __init__(self, prefix_length: int, clip_length: Optional[int] = None, prefix_size: int = 512,
+                 num_layers: int = 8, mapping_type='mlp', sound_effect_embeddings: torch.Tensor = None,
+                 sound_effect_num: Optional[int] = 0, only_prefix: Optional[bool] = False,
+                 mask_probability: Optional[float] = 0):
+        super(ClapCaptionCrossattention, self).__init__(prefix_length, clip_length, prefix_size,
+                                                        num_layers, mapping_type,
+                                                        sound_effect_embeddings, sound_effect_num,
+                                                        only_prefix, mask_probability)
+        if self.sound_effect_embeddings is not None:
+            self.sound_effect_project = ZsMultiheadAttention(prefix_size, 4, batch_first=True)
+
+    def forward(self, tokens: torch.Tensor, prefix: torch.Tensor, mask: Optional[torch.Tensor] = None,
+                labels: Optional[torch.Tensor] = None):
+        self._check_inference(mask, labels)
+        embedding_text = self.gpt.transformer.wte(tokens)
+        embedding_cat, mask = self.clap_to_gpt(prefix, embedding_text, mask)
+        out = self.gpt(inputs_embeds=embedding_cat)
+        return out, out.logits[:, self.prefix_length - 1: -1]
+
+    def clap_to_gpt(self, prefix: torch.Tensor, embedding_text: Optional[torch.Tensor] = None,
+                    mask: Optional[torch.Tensor] = None):
+        """caption_model.py:122-138 (v2, 170-196: the attention output is added to the prefix)."""
+        if self.sound_effect_embeddings is not None:
+            se = self.sound_effect_choice(prefix, self.sound_effect_embeddings, self.sound_effect_num)
+            prefix, _ = self.sound_effect_project(prefix, se, se,
+                                                  residual=prefix if self.RESIDUAL else None)
+        proj = self.clap_project(prefix).view(-1, self.prefix_length, self.gpt_embedding_size)
+        emb = proj if embedding_text is None else torch.cat((proj, embedding_text), dim=1)
+        return emb, mask
+
+
+class ClapCaptionCrossattention_v2(ClapCaptionCrossattention):
+    """caption_model.py:151-206 at inference: prefix = MHA(prefix, sound effects) + prefix."""
+
+    RESIDUAL = True
+
+    def __init__(self, prefix_length: int, clip_length: Optional[int] = None, prefix_size: int = 512,
+                 num_layers: int = 8, mapping_type='mlp', sound_effect_embeddings: torch.Tensor = None,
+                 sound_effect_num: Optional[int] = 0, only_prefix: Optional[bool] = False,
+                 mask_probability: Optional[float] = 0.25):
+        super(ClapCaptionCrossattention_v2, self).__init__(prefix_length, clip_length, prefix_size,
+                                                           num_layers, mapping_type,
+                                                           sound_effect_embeddings,
+                                                           sound_effect_num, only_prefix,
+                                                           mask_probability)
 
 
 class ClapCaption_prompt(ClapCaptionModel):

@@ -8,8 +8,8 @@ Cnn10 / ResNet38 are not provided: in the reference they read a missing ``self.d
 import torch
 import torch.nn as nn
 
-from zsaac.modules import EngineCache, register_tree, require_device, zs_dtype_of
-from zsaac.synthetic import cnn14_state_dict
+from zsaac.modules import (EngineCache, cnn14_reference_spec, register_tree, require_device,
+                           zs_dtype_of)
 
 from .feature_extractor import AudioFeature
 
@@ -19,7 +19,7 @@ class Cnn14(nn.Module):
     def __init__(self, config):
         super(Cnn14, self).__init__()
         self.audio_feats_extractor = AudioFeature(config["audio_args"])
-        register_tree(self, dict(cnn14_state_dict(4, prefix="")))
+        register_tree(self, cnn14_reference_spec())
         self._cache = EngineCache()
 
     def forward(self, input):

@@ -34,6 +34,7 @@ SIGNATURES = {
     "zs_stream_destroy": [P],
     "zs_logmel": [P, I, I, P, P, P, P, P, P, P, P, P, P, P],
     "zs_wav2img": [P, I, I, P, P],
+    "zs_pack_clips": [P, P, P, I, I, P, P],
     "zs_patch_embed": [P, I, P, P, P, P, P, P],
     "zs_layernorm": [P, I, I, I, P, P, P, F, P, I, I, P],
     "zs_gemm": [I, I, I, I, P, I, P, I, P, P, I, P, I, I, I, I, P, P],
@@ -50,6 +51,8 @@ SIGNATURES = {
     "zs_cast": [P, L, P, I, P],
     "zs_prompt_assemble": [P, I, I, P, I, I, P, P, I, P, I, P, P, P],
     "zs_row_attention": [P, I, P, P, I, I, I, P, I, I, I, F, P, I, I, P],
+    "zs_cross_attention": [P, I, P, P, I, I, I, I, I, I, F, P, I, I, P],
+    "zs_label_topk": [P, I, I, P, I, I, P, P, P],
     "zs_gpt2_prefill_embed": [P, P, I, P, I, I, P, P, I, I, I, P, P, P, P, I, P],
     "zs_kv_write": [P, I, I, I, I, P, I, P, P, I, I, P],
     "zs_decode_attention": [P, I, I, I, P, P, I, P, P, P, I, P],

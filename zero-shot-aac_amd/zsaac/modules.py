@@ -84,13 +84,49 @@ def register_tree(module: nn.Module, spec: Dict[str, torch.Tensor], buffers=()) 
             mod.register_parameter(leaf, nn.Parameter(t.clone(), requires_grad=False))
 
 
+# architecture constants (retrieval/models/htsat.py:588-758 with the CLAP args of
+# audio_encoder.py:41-51; retrieval/models/cnns.py:137-201)
+HTSAT_DEPTHS, HTSAT_HEADS, HTSAT_EMBED, HTSAT_WINDOW, HTSAT_CLASSES = (2, 2, 6, 2), (4, 8, 16, 32), 96, 8, 527
+CNN14_CH, N_MELS = (64, 128, 256, 512, 1024, 2048), 64
+
+
+class _RefInit:
+    """The reference modules' own initialisers, from a private generator: trunc_normal(0.02) for
+    HTSAT Linear / rel-pos tables (htsat.py:300, 745-758), xavier_uniform for CNN14 convs
+    (cnns.py:14-29, init_layer), LayerNorm / BatchNorm weight 1 bias 0, running stats 0 / 1."""
+
+    def __init__(self, seed=0):
+        self.g = torch.Generator().manual_seed(seed)
+
+    def trunc_normal(self, shape, std=0.02):
+        return torch.empty(*shape).normal_(0.0, std, generator=self.g).clamp_(-2 * std, 2 * std)
+
+    def xavier(self, shape):
+        fan_in = shape[1] * (shape[2] * shape[3] if len(shape) == 4 else 1)
+        fan_out = shape[0] * (shape[2] * shape[3] if len(shape) == 4 else 1)
+        a = (6.0 / (fan_in + fan_out)) ** 0.5
+        return torch.empty(*shape).uniform_(-a, a, generator=self.g)
+
+    @staticmethod
+    def norm(spec, name, dim, bn=False):
+        spec[name + ".weight"] = torch.ones(dim)
+        spec[name + ".bias"] = torch.zeros(dim)
+        if bn:
+            spec[name + ".running_mean"] = torch.zeros(dim)
+            spec[name + ".running_var"] = torch.ones(dim)
+            spec[name + ".num_batches_tracked"] = torch.tensor(0, dtype=torch.int64)
+
+
 def htsat_reference_spec() -> Dict[str, torch.Tensor]:
     """Every state-dict entry of the reference HTSAT_Swin_Transformer with the CLAP args
     (parameters + persistent buffers relative_position_index / attn_mask), minus the
-    audio_feats_extractor (its own module)."""
-    from .synthetic import HTSAT_DEPTHS, htsat_state_dict
-    spec = dict(htsat_state_dict(3, prefix=""))
-    ws = 8
+    audio_feats_extractor (its own module), initialised as the reference initialises them."""
+    ri, spec = _RefInit(3), {}
+    ri.norm(spec, "bn0", N_MELS, bn=True)
+    spec["patch_embed.proj.weight"] = ri.xavier((HTSAT_EMBED, 1, 4, 4))
+    spec["patch_embed.proj.bias"] = torch.zeros(HTSAT_EMBED)
+    ri.norm(spec, "patch_embed.norm", HTSAT_EMBED)
+    ws = HTSAT_WINDOW
     coords = torch.stack(torch.meshgrid(torch.arange(ws), torch.arange(ws), indexing="ij")).flatten(1)
     rel = (coords[:, :, None] - coords[:, None, :]).permute(1, 2, 0).contiguous()
     rel[:, :, 0] += ws - 1
@@ -98,13 +134,47 @@ def htsat_reference_spec() -> Dict[str, torch.Tensor]:
     rel[:, :, 0] *= 2 * ws - 1
     rpi = rel.sum(-1)
     res = 64
-    for i, depth in enumerate(HTSAT_DEPTHS):
+    for i, (depth, heads) in enumerate(zip(HTSAT_DEPTHS, HTSAT_HEADS)):
+        dim = HTSAT_EMBED * 2 ** i
         for j in range(depth):
             b = f"layers.{i}.blocks.{j}."
+            ri.norm(spec, b + "norm1", dim)
+            spec[b + "attn.relative_position_bias_table"] = ri.trunc_normal(((2 * ws - 1) ** 2, heads))
             spec[b + "attn.relative_position_index"] = rpi
+            for nm, o, k in (("attn.qkv", 3 * dim, dim), ("attn.proj", dim, dim),
+                             ("mlp.fc1", 4 * dim, dim), ("mlp.fc2", dim, 4 * dim)):
+                spec[b + nm + ".weight"] = ri.trunc_normal((o, k))
+                spec[b + nm + ".bias"] = torch.zeros(o)
+            ri.norm(spec, b + "norm2", dim)
             if j % 2 == 1 and res > ws:
                 spec[b + "attn_mask"] = _shift_mask(res, ws, ws // 2)
+        if i < len(HTSAT_DEPTHS) - 1:
+            d = f"layers.{i}.downsample."
+            spec[d + "reduction.weight"] = ri.trunc_normal((2 * dim, 4 * dim))
+            ri.norm(spec, d + "norm", 4 * dim)
         res //= 2
+    nf = HTSAT_EMBED * 2 ** (len(HTSAT_DEPTHS) - 1)
+    ri.norm(spec, "norm", nf)
+    spec["tscam_conv.weight"] = ri.xavier((HTSAT_CLASSES, nf, 2, 3))
+    spec["tscam_conv.bias"] = torch.zeros(HTSAT_CLASSES)
+    spec["head.weight"] = ri.trunc_normal((HTSAT_CLASSES, HTSAT_CLASSES))
+    spec["head.bias"] = torch.zeros(HTSAT_CLASSES)
+    return spec
+
+
+def cnn14_reference_spec() -> Dict[str, torch.Tensor]:
+    """Every state-dict entry of the reference Cnn14 encoder (bn0 + 6 ConvBlocks), initialised as
+    the reference's init_bn / init_layer do (cnns.py:14-29, 36-52)."""
+    ri, spec = _RefInit(4), {}
+    ri.norm(spec, "bn0", N_MELS, bn=True)
+    cin = 1
+    for i, cout in enumerate(CNN14_CH, start=1):
+        b = f"conv_block{i}."
+        spec[b + "conv1.weight"] = ri.xavier((cout, cin, 3, 3))
+        spec[b + "conv2.weight"] = ri.xavier((cout, cout, 3, 3))
+        ri.norm(spec, b + "bn1", cout, bn=True)
+        ri.norm(spec, b + "bn2", cout, bn=True)
+        cin = cout
     return spec
 
 

@@ -60,6 +60,16 @@ def logmel(wav, tables, bn=None, out=None):
     return out
 
 
+def pack_clips(flat, offsets, lengths, T, out):
+    """Ragged clips in one flat f32 device buffer -> out [B, T]: crop / zero-pad (zs_pack_clips)."""
+    _need(flat.dtype == torch.float32 and offsets.dtype == torch.int64 and lengths.dtype == torch.int32,
+          "pack_clips: flat f32, offsets int64, lengths int32")
+    B = lengths.numel()
+    _need(out.shape[0] >= B and out.shape[1] == T, "pack_clips: out [B, T]")
+    call("zs_pack_clips", _p(flat), _p(offsets), _p(lengths), B, T, _p(out), _s())
+    return out[:B]
+
+
 def wav2img(logmel_t, out=None):
     B, T_in, F = logmel_t.shape
     _need(F == 64, "wav2img expects 64 mel bins")
@@ -267,6 +277,28 @@ def decode_attention(qkv, R, D, heads, kc, vc, Lmax, pos, out, kvrow=None):
     call("zs_decode_attention", _p(qkv), R, D, heads, _p(kc), _p(vc), Lmax, _p(pos), _p(kvrow),
          _p(out), dt(qkv), _s())
     return out
+
+
+def cross_attention(q, k, v, B, Lq, Lk, heads, out, scale=None):
+    """softmax(scale q k^T) v per (row, query, head) for Lk <= 64 keys (zs_cross_attention):
+    q [B*Lq, heads*hd], k / v [B*Lk, heads*hd] (row strides taken from the tensors)."""
+    D = q.shape[-1]
+    hd = D // heads
+    _need(D % heads == 0 and q.dtype == k.dtype == v.dtype == out.dtype, "cross_attention: shapes")
+    _need(k.stride(0) == v.stride(0), "cross_attention: k and v share a row stride")
+    scale = hd ** -0.5 if scale is None else scale
+    call("zs_cross_attention", _p(q), q.stride(0), _p(k), _p(v), k.stride(0), B, Lq, Lk, heads, hd,
+         float(scale), _p(out), out.stride(0), dt(q), _s())
+    return out
+
+
+def label_topk(emb, labels, k, rows, idx=None):
+    """sound_effect_choice: the k most similar label rows per embedding (zs_label_topk):
+    emb [B, D] f32, labels [L, D] f32 -> rows [B, k, D] f32 (+ idx [B, k] int32)."""
+    B, D = emb.shape
+    _i32(idx, "idx")
+    call("zs_label_topk", _p(emb), B, D, _p(labels), labels.shape[0], k, _p(idx), _p(rows), _s())
+    return rows
 
 
 def decode_qkv_attention(x, ln_w, ln_b, w_qkv, b_qkv, kc, vc, Lmax, pos, out, eps=1e-5):

@@ -121,6 +121,29 @@ def mlp_mapper_state_dict(seed: int = 1, prefix_size: int = 1024, prefix_length:
     return sd
 
 
+def sound_effect_mlp_state_dict(seed: int = 11, prefix_size: int = 1024, d: int = GPT2_D,
+                                prefix: str = "sound_effect_project.model."):
+    """ClapCaptionModel's ``sound_effect_project = MLP((prefix_size, d // 2, d))`` with Tanh
+    (models/caption_model.py:63-64)."""
+    g = _gen(seed)
+    sd = OrderedDict()
+    _linear(sd, g, prefix + "0", d // 2, prefix_size)
+    _linear(sd, g, prefix + "2", d, d // 2)
+    return sd
+
+
+def sound_effect_mha_state_dict(seed: int = 12, embed_dim: int = 1024,
+                                prefix: str = "sound_effect_project."):
+    """ClapCaptionCrossattention[_v2]'s ``nn.MultiheadAttention(prefix_size, 4, batch_first=True)``
+    (models/caption_model.py:109, 160): in_proj_weight / in_proj_bias / out_proj."""
+    g = _gen(seed)
+    sd = OrderedDict()
+    sd[prefix + "in_proj_weight"] = _randn(g, (3 * embed_dim, embed_dim), 1.0 / math.sqrt(embed_dim))
+    sd[prefix + "in_proj_bias"] = _randn(g, (3 * embed_dim,), 0.02)
+    _linear(sd, g, prefix + "out_proj", embed_dim, embed_dim)
+    return sd
+
+
 def transformer_mapper_state_dict(seed: int = 2, prefix_size: int = 1024, prefix_length: int = 10,
                                   clip_length: int = 10, num_layers: int = 8, d: int = GPT2_D,
                                   prefix: str = "clap_project."):
