@@ -286,9 +286,9 @@ def roofline_gemm_ln(pipe):
     copies = _cold_copies(W)
 
     def launch(i):
-        ops.gemm_ln(x, *ly["ln2"], copies[i % len(copies)], hid, bias=b, act=ops.ACT_GELU_TANH)
+        ops.gemm_ln(x, *ly["ln2_gemm"], copies[i % len(copies)], hid, bias=b, act=ops.ACT_GELU_TANH)
     avg = _graph_time(launch, 2 * len(copies))
-    byts = N * K * 2 + M * K * 4 + 2 * K * 4 + N * 4 + M * N * 2
+    byts = N * K * 2 + M * K * 4 + (2 * K * 4 if ly["ln2_gemm"][0] is not None else 0) + N * 4 + M * N * 2
     flops = 2 * M * N * K
     traffic, tsrc = None, None
     if os.path.exists(PMC_FILE):            # rocprofv3 --pmc passes (tools/pmc_traffic.py)
@@ -296,8 +296,8 @@ def roofline_gemm_ln(pipe):
             pmc = json.load(f)
         if pmc.get("shape") == [M, N, K] and pmc.get("kernel", "").startswith("gemm_rows"):
             traffic, tsrc = pmc["hbm_bytes_per_launch"], os.path.relpath(PMC_FILE, ROOT)
-    return _hbm_entry(f"gemm_rows_kernel<32,4,LN,6> (zs_gemm_ln) decode c_fc [{M}x{K}]x[{K}x{N}] "
-                      f"+ln_2 +bias +gelu_new (cold W)", byts, avg,
+    return _hbm_entry(f"gemm_rows_kernel<48,4,LN,6> (zs_gemm_ln) decode c_fc [{M}x{K}]x[{K}x{N}] "
+                      f"+ln_2 (affine folded into W) +bias +gelu_new (cold W)", byts, avg,
                       {"traffic": traffic, "traffic_source": tsrc,
                        "attainable_tflops_at_this_AI": round(flops / byts * HBM_PEAK_GBS / 1e3, 1),
                        "achieved_tflops": round(flops / avg / 1e12, 2)})

@@ -98,6 +98,51 @@ def install():
     _installed = True
 
 
+def install_bert(vocab, layers):
+    """``BertModel.from_pretrained`` / ``BertTokenizer.from_pretrained`` ('bert-base-uncased',
+    retrieval/models/text_encoder.py:43-47) are name fetches, unavailable offline -> a locally
+    built ``BertModel(BertConfig(vocab_size=len(vocab), num_hidden_layers=layers))`` (eager
+    attention, bert-base geometry otherwise) and a ``BertTokenizer`` over ``vocab``; the caller
+    loads the seeded synthetic state dict into the model."""
+    install()
+    from transformers import BertConfig, BertModel, BertTokenizer
+
+    def _model(*a, add_pooling_layer=True, **k):
+        cfg = BertConfig(vocab_size=len(vocab), num_hidden_layers=layers)
+        cfg._attn_implementation = "eager"
+        return BertModel(cfg, add_pooling_layer=add_pooling_layer)
+    BertModel.from_pretrained = staticmethod(_model)
+    BertTokenizer.from_pretrained = staticmethod(
+        lambda *a, **k: BertTokenizer(vocab={t: i for i, t in enumerate(vocab)}, do_lower_case=True))
+
+
+def legacy_cache(gpt):
+    """The reference's magic decoding handles ``past_key_values`` as transformers 4.24's tuples of
+    per-layer (k, v) (gpt2_prefix_eval.py:471-494); transformers 5.x returns and expects a Cache
+    object.  Wrap ``gpt.forward`` so tuples go in and come out (same tensors, no arithmetic).
+    The candidate steps pass an all-ones ``attention_mask`` of length 1 next to a longer cache
+    (gpt2_prefix_eval.py:419,567): transformers 4.24 turned it into a [B,1,1,1] additive mask of
+    zeros (no key masked); 5.x reads a short mask as covering only the newest key and masks the
+    cache.  An all-ones mask masks nothing under 4.24 whatever its length, so it is dropped."""
+    from transformers import DynamicCache
+    from transformers.cache_utils import Cache
+    orig = gpt.forward
+
+    def fwd(*a, past_key_values=None, **k):
+        m = k.get("attention_mask")
+        if m is not None and bool((m == 1).all()):
+            k.pop("attention_mask")
+        if past_key_values is not None and not isinstance(past_key_values, Cache):
+            past_key_values = DynamicCache(ddp_cache_data=[tuple(x) for x in past_key_values])
+        out = orig(*a, past_key_values=past_key_values, **k)
+        pkv = out.past_key_values
+        if pkv is not None and hasattr(pkv, "layers"):
+            out.past_key_values = tuple((x.keys, x.values) for x in pkv.layers)
+        return out
+    gpt.forward = fwd
+    return gpt
+
+
 def gpt2_from_state_dict(sd_gpt):
     """A reference-config GPT2LMHeadModel (eager attention) holding ``sd_gpt`` (no 'gpt.' prefix)."""
     install()

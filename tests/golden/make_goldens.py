@@ -24,6 +24,10 @@ Fixture list (reference call sites in brackets):
                   ClapCaptionPrefix: clap_to_gpt outputs and generate2 ids.
   c2_margin.npz   generate2 with the reference's top-1/top-2 logit margin at every generated
   c2_margin_flat.npz  step, on smaller decoder weights (the bf16 id-parity check).
+  magic.npz       CLAP-guided decoding: ASE.encode_text on sample texts (text_encoder.py:58-68,
+                  ase_model.py:57-60), generate_beam_magic (gpt2_prefix_eval.py:602-689) at two
+                  (beam, width, alpha, beta) settings and magic_search (341-469), BERT text tower
+                  at MAGIC_BERT_LAYERS layers.
 """
 from __future__ import annotations
 
@@ -397,10 +401,75 @@ def gen_keys():
 
 
 
+MAGIC_BERT_LAYERS = 2
+MAGIC_CFGS = ((3, 25, 0.1, 0.2, 12), (2, 8, 0.3, 1.0, 10))   # beam, width, alpha, beta, entry_length
+
+
+def _clap_ase(layers):
+    """The reference ASE (audio + text towers) with the synthetic BERT loaded (text side)."""
+    _refshim.install_bert(S.bert_vocab(), layers)
+    from retrieval.models.ase_model import ASE
+    cfg = _audio_config("transformer")
+    cfg.update({"embed_size": 1024, "temp": 0.07, "embed_regularization": True,
+                "text_encoder_args": {"type": "bert-base-uncased", "freeze": False}})
+    clap = ASE(cfg)
+    missing, unexpected = clap.load_state_dict(S.bert_state_dict(layers=layers), strict=False)
+    assert not unexpected, unexpected
+    assert all(m.startswith("audio") or "position_ids" in m for m in missing), missing
+    return clap.eval()
+
+
+def gen_magic(n_clips=3):
+    import gpt2_prefix_eval as G
+    from zsaac.tokenizer import WordTokenizer
+    L = MAGIC_BERT_LAYERS
+    clap = _clap_ase(L)
+    tok = WordTokenizer()
+    texts = [tok.decode(t) for t in ([5, 123, 13], [7], [1000, 2005, 3, 11, 764, 49999, 50000],
+                                     list(range(100, 140)), [30000, 30001, 30010])]
+    with torch.no_grad():
+        text_emb = clap.encode_text(texts)
+        bt = clap.text_encoder.tokenizer(texts, padding="longest", truncation=True, max_length=30)
+    model = _caption_model("mlp")
+    _refshim.legacy_cache(model.gpt)
+    emb = S.synthetic_clap_embeddings(n_clips, seed=77)
+    label_ids = S.label_token_table()
+    hard_rows = [[1858, 389] + label_ids[3 * i] + [287, 428, 6597, 13] for i in range(n_clips)]
+    hard, hard_len = _pad(hard_rows)
+    out = {}
+    for c, (beam, width, alpha, beta, entry) in enumerate(MAGIC_CFGS):
+        rows = []
+        for i in range(n_clips):
+            with torch.no_grad():
+                pe, _ = model.clap_to_gpt(emb[i:i + 1].unsqueeze(0),
+                                          model.gpt.transformer.wte(torch.tensor([hard_rows[i]])))
+                res = G.generate_beam_magic(model, clap, tok, audio_embeds=emb[i:i + 1], embed=pe,
+                                            beam_size=beam, entry_length=entry, magic_width=width,
+                                            alpha=alpha, beta=beta)
+            rows.append([WordTokenizer.parse(t) for t in res])
+            print(f"  magic cfg{c} clip {i}: {[len(r) for r in rows[-1]]}", flush=True)
+        ids, lens = _pad([r for clip in rows for r in clip])
+        out[f"beam_cfg{c}_ids"] = ids.reshape(n_clips, beam, -1)
+        out[f"beam_cfg{c}_len"] = lens.reshape(n_clips, beam)
+    search = []
+    for i in range(n_clips):
+        with torch.no_grad():
+            pe, _ = model.clap_to_gpt(emb[i:i + 1].unsqueeze(0),
+                                      model.gpt.transformer.wte(torch.tensor([hard_rows[i]])))
+            t = G.magic_search(model, tok, emb[i:i + 1], clap, embed=pe, beam_width=15,
+                               decoding_len=pe.shape[1] + 10)
+        search.append(WordTokenizer.parse(t))
+    s_ids, s_len = _pad(search)
+    _save("magic.npz", clap_emb=emb.numpy(), hard_ids=hard, hard_len=hard_len,
+          bert_layers=np.int64(L), cfgs=np.array(MAGIC_CFGS, dtype=np.float64),
+          text_ids=_pad(bt["input_ids"])[0], text_emb=text_emb.numpy(),
+          search_ids=s_ids, search_len=s_len, **out)
+
+
 ALL = {"prompt": gen_prompt, "mappers": gen_mappers, "htsat": gen_htsat, "cnn14": gen_cnn14,
        "beam": gen_beam, "c1": gen_c1, "keys": gen_keys,
        "margin": gen_margin, "margin_flat": lambda: gen_margin(name="c2_margin_flat"),
-       "variants": gen_variants}
+       "variants": gen_variants, "magic": gen_magic}
 
 if __name__ == "__main__":
     torch.set_num_threads(os.cpu_count() or 8)

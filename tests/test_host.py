@@ -61,6 +61,24 @@ def test_gpt2_weight_packing_layout():
     assert torch.allclose(w.wte_norm.norm(dim=1), torch.ones(w.V), atol=1e-5)
 
 
+def test_gpt2_bf16_ln_affine_fold():
+    """bf16 packing folds ln_1 / ln_2 (weight, bias) into c_attn / c_fc: normalise-only LN ->
+    folded GEMM equals LN -> GEMM (f32 check of the fold; bf16 rounding of W' only)."""
+    from zsaac.decoder import Gpt2Weights
+    sd = S.gpt2_state_dict(seed=0, std=0.1)
+    w = Gpt2Weights(sd, "cpu", torch.bfloat16)
+    assert w.folded
+    h = "gpt.transformer.h.5."
+    ly = w.layers[5]
+    assert ly["ln2_gemm"] == (None, None) and torch.equal(ly["ln2"][0], torch.ones(768))
+    x = torch.randn(4, 768) * 3 + 1
+    xh = torch.nn.functional.layer_norm(x, (768,), eps=1e-5)
+    ref = torch.nn.functional.layer_norm(x, (768,), sd[h + "ln_2.weight"], sd[h + "ln_2.bias"], 1e-5)
+    ref = ref @ sd[h + "mlp.c_fc.weight"] + sd[h + "mlp.c_fc.bias"]
+    got = xh @ ly["fc_w"].float().t() + ly["fc_b"]
+    assert (got - ref).abs().max() < 0.02 * ref.abs().max()
+
+
 def test_cnn14_packing_and_bn_fold():
     from zsaac.encoder import Cnn14Weights
     sd = S.cnn14_state_dict(4)

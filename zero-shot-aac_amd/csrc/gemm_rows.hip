@@ -63,8 +63,9 @@ struct RowsArgs {
   int rgroups, ntiles;
 };
 
-template <int NT, int WAVES, bool LN, int S>
+template <int NT, int WAVES, int LNM, int S>
 __global__ __launch_bounds__(64 * WAVES) void gemm_rows_kernel(RowsArgs g) {
+  constexpr bool LN = LNM != 0, AFF = LNM == 1;
   // S = 32-deep k-steps per wave (K = 32 * WAVES * S), a template parameter so that every load
   // is issued unconditionally and up front (a runtime trip count put each load in its own
   // branch and the compiler waited for it there: one round trip per load)
@@ -128,14 +129,18 @@ __global__ __launch_bounds__(64 * WAVES) void gemm_rows_kernel(RowsArgs g) {
   constexpr int TPR = NTHR / RG, NV = LN ? K / (4 * TPR) : 1;
   static_assert(!LN || K % (4 * TPR) == 0, "LN rows: K % (4 * threads per row)");
   const int lr = threadIdx.x / TPR, lt = threadIdx.x % TPR;
-  float4 xv[NV], lw[NV], lb[NV];
+  // (AFF: the LN weight / bias quads of this thread's columns; without AFF the caller folded
+  // them into W and the bias, and the 2 x 16 row-threads' redundant loads of them go away)
+  float4 xv[NV], lw[AFF ? NV : 1], lb[AFF ? NV : 1];
   if constexpr (LN) {
     const float4* xr = reinterpret_cast<const float4*>(g.X + (long)min(m0 + lr, g.M - 1) * g.ldx);
 #pragma unroll
     for (int i = 0; i < NV; ++i) {
       xv[i] = xr[lt + TPR * i];
-      lw[i] = reinterpret_cast<const float4*>(g.ln_w)[lt + TPR * i];
-      lb[i] = reinterpret_cast<const float4*>(g.ln_b)[lt + TPR * i];
+      if constexpr (AFF) {
+        lw[i] = reinterpret_cast<const float4*>(g.ln_w)[lt + TPR * i];
+        lb[i] = reinterpret_cast<const float4*>(g.ln_b)[lt + TPR * i];
+      }
     }
   }
   // keep every load above in flight before any of them is used (the scheduler otherwise sinks
@@ -168,10 +173,15 @@ __global__ __launch_bounds__(64 * WAVES) void gemm_rows_kernel(RowsArgs g) {
     for (int i = 0; i < NV; ++i) {
       const int c = lt + TPR * i;
       uint2 pk;
-      pk.x = (uint32_t)f2bf((xv[i].x - mean) * rstd * lw[i].x + lb[i].x) |
-             ((uint32_t)f2bf((xv[i].y - mean) * rstd * lw[i].y + lb[i].y) << 16);
-      pk.y = (uint32_t)f2bf((xv[i].z - mean) * rstd * lw[i].z + lb[i].z) |
-             ((uint32_t)f2bf((xv[i].w - mean) * rstd * lw[i].w + lb[i].w) << 16);
+      if constexpr (AFF) {
+        pk.x = (uint32_t)f2bf((xv[i].x - mean) * rstd * lw[i].x + lb[i].x) |
+               ((uint32_t)f2bf((xv[i].y - mean) * rstd * lw[i].y + lb[i].y) << 16);
+        pk.y = (uint32_t)f2bf((xv[i].z - mean) * rstd * lw[i].z + lb[i].z) |
+               ((uint32_t)f2bf((xv[i].w - mean) * rstd * lw[i].w + lb[i].w) << 16);
+      } else {
+        pk.x = (uint32_t)f2bf((xv[i].x - mean) * rstd) | ((uint32_t)f2bf((xv[i].y - mean) * rstd) << 16);
+        pk.y = (uint32_t)f2bf((xv[i].z - mean) * rstd) | ((uint32_t)f2bf((xv[i].w - mean) * rstd) << 16);
+      }
       *reinterpret_cast<uint2*>(hs + lr * ldh + 4 * c) = pk;
     }
     __syncthreads();
@@ -235,6 +245,7 @@ __global__ __launch_bounds__(64 * WAVES) void gemm_rows_kernel(RowsArgs g) {
   ZS_STAMP(6);
 }
 
+int g_rows_nt48 = 1;  // A/B knob (zs_tune_set "rows_nt48"): 48-column LN tiles
 int g_gemm_rows = 1;   // A/B knob (zs_tune_set "gemm_rows"): 0 = skinny split-K kernel for M <= 64
 
 // shape plan: waves (K split), k-steps per wave, column tile; waves < 0 when not covered
@@ -248,20 +259,23 @@ static RowsPlan rows_plan(int N, int K, bool ln) {
                                    : (S == 8 || S == 12 || S == 15 || S == 16));
   if (!ok) return {-1, 0, 0};
   const int per = ln ? 2 : 3;               // loads per k-step at NT = 32
+  // LN mode: 48-column tiles where N allows (c_fc 64 x 4 = 256 workgroups, c_attn 192: one per
+  // CU; at 32 columns c_fc's 384 put two on half the CUs, whose per-CU load bytes set the time)
+  if (ln && g_rows_nt48 && N % 48 == 0 && S * 3 <= RG_MAX_LOADS) return {waves, S, 48};
   if (S * per <= RG_MAX_LOADS && N >= 1536) return {waves, S, 32};
   return {waves, S, 16};
 }
 
-template <bool LN, int NT, int W, int S>
+template <int LNM, int NT, int W, int S>
 static void launch_rows_k(const RowsArgs& g, dim3 grid, size_t lds, hipStream_t st) {
-  if constexpr (S * (LN ? NT / 16 : NT / 16 + 1) <= RG_MAX_LOADS)   // rows_plan never asks more
-    hipLaunchKernelGGL((gemm_rows_kernel<NT, W, LN, S>), grid, dim3(64 * W), lds, st, g);
+  if constexpr (S * (LNM ? NT / 16 : NT / 16 + 1) <= RG_MAX_LOADS)   // rows_plan never asks more
+    hipLaunchKernelGGL((gemm_rows_kernel<NT, W, LNM, S>), grid, dim3(64 * W), lds, st, g);
 }
 
-template <bool LN, int NT, int W>
+template <int LNM, int NT, int W>
 static void launch_rows_s(const RowsArgs& g, int S, dim3 grid, size_t lds, hipStream_t st) {
-#define RL(S_) launch_rows_k<LN, NT, W, S_>(g, grid, lds, st)
-  if constexpr (LN) {
+#define RL(S_) launch_rows_k<LNM, NT, W, S_>(g, grid, lds, st)
+  if constexpr (LNM) {
     if (S == 6) RL(6); else RL(8);
   } else if constexpr (W == 4) {
     switch (S) { case 2: RL(2); break; case 4: RL(4); break; case 6: RL(6); break;
@@ -273,22 +287,24 @@ static void launch_rows_s(const RowsArgs& g, int S, dim3 grid, size_t lds, hipSt
 #undef RL
 }
 
-template <bool LN>
+template <int LNM>
 static int launch_rows(const RowsArgs& g0, RowsPlan p, hipStream_t st) {
+  constexpr bool LN = LNM != 0;
   RowsArgs g = g0;
   g.rgroups = cdiv(g.M, RG);
   g.ntiles = cdiv(g.N, p.nt);
   const dim3 grid(g.rgroups * g.ntiles);
   const size_t lds = (LN ? (size_t)RG * (g.K + 8) * 2 : 0) + (size_t)p.waves * RG * p.nt * 4;
   if constexpr (LN) {                       // rows_plan: LN at 4 waves only
-    if (p.nt == 32) launch_rows_s<LN, 32, 4>(g, p.steps, grid, lds, st);
-    else launch_rows_s<LN, 16, 4>(g, p.steps, grid, lds, st);
+    if (p.nt == 48) launch_rows_s<LNM, 48, 4>(g, p.steps, grid, lds, st);
+    else if (p.nt == 32) launch_rows_s<LNM, 32, 4>(g, p.steps, grid, lds, st);
+    else launch_rows_s<LNM, 16, 4>(g, p.steps, grid, lds, st);
   } else if (p.nt == 32) {
-    if (p.waves == 8) launch_rows_s<LN, 32, 8>(g, p.steps, grid, lds, st);
-    else launch_rows_s<LN, 32, 4>(g, p.steps, grid, lds, st);
+    if (p.waves == 8) launch_rows_s<0, 32, 8>(g, p.steps, grid, lds, st);
+    else launch_rows_s<0, 32, 4>(g, p.steps, grid, lds, st);
   } else {
-    if (p.waves == 8) launch_rows_s<LN, 16, 8>(g, p.steps, grid, lds, st);
-    else launch_rows_s<LN, 16, 4>(g, p.steps, grid, lds, st);
+    if (p.waves == 8) launch_rows_s<0, 16, 8>(g, p.steps, grid, lds, st);
+    else launch_rows_s<0, 16, 4>(g, p.steps, grid, lds, st);
   }
   ZS_LAUNCH_CHECK();
   return 0;
@@ -309,7 +325,7 @@ extern "C" __attribute__((visibility("hidden"))) int zs_gemm_rows_internal(
   g.M = M; g.N = N; g.K = K; g.A = (const bf16_t*)A; g.lda = lda; g.W = (const bf16_t*)W;
   g.ldw = ldw; g.bias = bias; g.residual = residual; g.ldr = ldr; g.out = out; g.ldo = ldo;
   g.out_dtype = out_dtype; g.act = act;
-  return launch_rows<false>(g, p, S(stream));
+  return launch_rows<0>(g, p, S(stream));
 }
 
 extern "C" int zs_gemm_ln(int M, int N, int K, const float* x, int ldx, const float* ln_w,
@@ -318,7 +334,8 @@ extern "C" int zs_gemm_ln(int M, int N, int K, const float* x, int ldx, const fl
                           int act, void* stream) {
   ZS_REQUIRE(M > 0 && M <= RG_MAX_M && N > 0 && K > 0, "zs_gemm_ln: M in 1..%d (got M=%d N=%d K=%d)",
              RG_MAX_M, M, N, K);
-  ZS_REQUIRE(x && ln_w && ln_b && W && out, "zs_gemm_ln: null pointer");
+  // ln_w == ln_b == nullptr: normalise only (the caller folded the LN affine into W and bias)
+  ZS_REQUIRE(x && W && out && (ln_w == nullptr) == (ln_b == nullptr), "zs_gemm_ln: null pointer");
   ZS_REQUIRE(ldx % 4 == 0 && ((uintptr_t)x & 15) == 0 && ((uintptr_t)ln_w & 15) == 0 &&
              ((uintptr_t)ln_b & 15) == 0, "zs_gemm_ln: x / LN params must be 16-byte aligned");
   ZS_REQUIRE(ldw % 8 == 0 && ((uintptr_t)W & 15) == 0, "zs_gemm_ln: W must be 16-byte aligned");
@@ -329,5 +346,5 @@ extern "C" int zs_gemm_ln(int M, int N, int K, const float* x, int ldx, const fl
   g.M = M; g.N = N; g.K = K; g.X = x; g.ldx = ldx; g.ln_w = ln_w; g.ln_b = ln_b; g.eps = eps;
   g.W = (const bf16_t*)W; g.ldw = ldw; g.bias = bias; g.residual = residual; g.ldr = ldr;
   g.out = out; g.ldo = ldo; g.out_dtype = out_dtype; g.act = act;
-  return launch_rows<true>(g, p, S(stream));
+  return ln_w ? launch_rows<1>(g, p, S(stream)) : launch_rows<2>(g, p, S(stream));
 }

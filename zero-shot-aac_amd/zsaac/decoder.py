@@ -166,15 +166,34 @@ class Gpt2Weights:
         self.wte_norm = _w(wn, device, dtype)          # predict_prompt.py:117-118
         self.V = self.wte.shape[0]
         self.layers = []
+        # bf16: the ln_1 / ln_2 affine is folded into c_attn / c_fc (W'[n,k] = W[n,k] * g[k],
+        # b'[n] = b[n] + sum_k W[n,k] * beta[k], in f32 before the bf16 rounding of W'), so the
+        # LayerNorm before them only normalises: zs_gemm_ln then skips the LN weight / bias loads
+        # its 16 row-threads each repeat (half the bytes its workgroups pull through L1 at decode
+        # shapes).  f32 parity mode keeps the reference's exact LN -> GEMM order.
+        self.folded = dtype == torch.bfloat16
+        one = torch.ones(D, device=device)
+        zero = torch.zeros(D, device=device)
         for i in range(NL):
             h = p + f"h.{i}."
             t = lambda k: _w(sd[h + k].t(), device, dtype)
+
+            def lin_ln(wk, bk, lnk):
+                W = sd[h + wk].float().t()
+                b = sd[h + bk].float()
+                g, beta = sd[h + lnk + ".weight"].float(), sd[h + lnk + ".bias"].float()
+                if not self.folded:
+                    return (_w(W, device, dtype), _f32(b, device),
+                            (_f32(g, device), _f32(beta, device)), (_f32(g, device), _f32(beta, device)))
+                Wf = W * g[None, :]
+                bf = (b.double() + W.double() @ beta.double()).float()
+                return _w(Wf, device, dtype), _f32(bf, device), (one, zero), (None, None)
+            aw, ab, ln1, ln1g = lin_ln("attn.c_attn.weight", "attn.c_attn.bias", "ln_1")
+            fw, fb, ln2, ln2g = lin_ln("mlp.c_fc.weight", "mlp.c_fc.bias", "ln_2")
             self.layers.append({
-                "ln1": (_f32(sd[h + "ln_1.weight"], device), _f32(sd[h + "ln_1.bias"], device)),
-                "attn_w": t("attn.c_attn.weight"), "attn_b": _f32(sd[h + "attn.c_attn.bias"], device),
+                "ln1": ln1, "ln1_gemm": ln1g, "attn_w": aw, "attn_b": ab,
                 "proj_w": t("attn.c_proj.weight"), "proj_b": _f32(sd[h + "attn.c_proj.bias"], device),
-                "ln2": (_f32(sd[h + "ln_2.weight"], device), _f32(sd[h + "ln_2.bias"], device)),
-                "fc_w": t("mlp.c_fc.weight"), "fc_b": _f32(sd[h + "mlp.c_fc.bias"], device),
+                "ln2": ln2, "ln2_gemm": ln2g, "fc_w": fw, "fc_b": fb,
                 "mproj_w": t("mlp.c_proj.weight"), "mproj_b": _f32(sd[h + "mlp.c_proj.bias"], device),
             })
         self.lnf = (_f32(sd[p + "ln_f.weight"], device), _f32(sd[p + "ln_f.bias"], device))
@@ -281,10 +300,10 @@ class Gpt2Decoder:
                 if qkv_attn_fn is not None:
                     qkv_attn_fn(l, ly, x, att)
                 else:
-                    ops.gemm_ln(x, *ly["ln1"], ly["attn_w"], qkv, bias=ly["attn_b"])
+                    ops.gemm_ln(x, *ly["ln1_gemm"], ly["attn_w"], qkv, bias=ly["attn_b"])
                     attn_fn(l, qkv, att)
                 ops.gemm(att, ly["proj_w"], x, bias=ly["proj_b"], residual=x, workspace=self.ws)
-                ops.gemm_ln(x, *ly["ln2"], ly["fc_w"], hid, bias=ly["fc_b"], act=ops.ACT_GELU_TANH)
+                ops.gemm_ln(x, *ly["ln2_gemm"], ly["fc_w"], hid, bias=ly["fc_b"], act=ops.ACT_GELU_TANH)
                 ops.gemm(hid, ly["mproj_w"], x, bias=ly["mproj_b"], residual=x, workspace=self.ws)
             return
         for l, ly in enumerate(self.w.layers):

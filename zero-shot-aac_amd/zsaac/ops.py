@@ -170,7 +170,7 @@ def gemm(a, w, out, bias=None, residual=None, act=ACT_NONE, split_k=0, workspace
 def gemm_ln(x, ln_w, ln_b, w, out, bias=None, residual=None, act=ACT_NONE, eps=1e-5):
     """out = act(LayerNorm(x) @ w.T + bias) + residual in one launch (zs_gemm_ln): x [M, K] f32
     rows (M <= 64), w [N, K] bf16.  The LN output is rounded to bf16 like the zs_layernorm ->
-    zs_gemm pair it replaces."""
+    zs_gemm pair it replaces.  ln_w = ln_b = None: normalise only (affine folded into w, bias)."""
     M, K = x.shape
     N = w.shape[0]
     _need(w.shape[1] == K and w.dtype == torch.bfloat16 and x.dtype == torch.float32,

@@ -310,3 +310,55 @@ def gpt2_vocab(label_names, n_vocab: int = 50257):
             vocab[f"<{k}>"] = i
             k += 1
     return vocab, merges
+
+
+# ----------------------------------------------------------------------------------- BERT (CLAP text)
+
+BERT_D = 768
+BERT_FF = 3072
+BERT_HEADS = 12
+BERT_NPOS = 512
+
+
+def bert_vocab() -> List[str]:
+    """A small WordPiece vocabulary (the bert-base-uncased vocab file is a name fetch, unavailable
+    offline): the special tokens at their BERT positions relative to each other, single
+    characters, '##' continuations and a few whole words, so that a WordPiece split of the
+    synthetic caption words (:class:`zsaac.tokenizer.WordTokenizer`) exercises greedy
+    longest-match-first, [UNK] and truncation."""
+    toks = ["[PAD]", "[UNK]", "[CLS]", "[SEP]", "[MASK]"]
+    chars = [chr(c) for c in range(97, 123)] + [str(d) for d in range(10)]
+    toks += [".", ",", "'", "-"] + chars + ["##" + c for c in chars]
+    toks += [f"w{i}" for i in range(40)] + [f"##{i}{j}" for i in range(3) for j in range(10)]
+    toks += ["there", "are", "in", "this", "audio", "sound", "dog", "bark", "##ing", "##s"]
+    return toks
+
+
+def bert_state_dict(seed: int = 13, vocab: int = None, layers: int = 12,
+                    prefix: str = "text_encoder.text_encoder.", proj_prefix: str = "text_proj.",
+                    embed_size: int = 1024, temp: float = 0.07):
+    """ASE's text tower: HF ``BertModel(add_pooling_layer=False)`` keys under
+    ``text_encoder.text_encoder.`` (retrieval/models/text_encoder.py:43-47), ``text_proj.{0,2}``
+    and ``temp`` (retrieval/models/ase_model.py:40-46).  bert-base geometry (768 / 12 heads /
+    3072), ``layers`` encoder layers (bert-base has 12)."""
+    g = _gen(seed)
+    vocab = vocab or len(bert_vocab())
+    sd = OrderedDict()
+    e = prefix + "embeddings."
+    sd[e + "word_embeddings.weight"] = _randn(g, (vocab, BERT_D), 0.5)
+    sd[e + "position_embeddings.weight"] = _randn(g, (BERT_NPOS, BERT_D), 0.2)
+    sd[e + "token_type_embeddings.weight"] = _randn(g, (2, BERT_D), 0.2)
+    _ln(sd, g, e + "LayerNorm", BERT_D)
+    for i in range(layers):
+        L = prefix + f"encoder.layer.{i}."
+        for n in ("query", "key", "value"):
+            _linear(sd, g, L + f"attention.self.{n}", BERT_D, BERT_D, gain=1.5)
+        _linear(sd, g, L + "attention.output.dense", BERT_D, BERT_D)
+        _ln(sd, g, L + "attention.output.LayerNorm", BERT_D)
+        _linear(sd, g, L + "intermediate.dense", BERT_FF, BERT_D, gain=1.5)
+        _linear(sd, g, L + "output.dense", BERT_D, BERT_FF)
+        _ln(sd, g, L + "output.LayerNorm", BERT_D)
+    _linear(sd, g, proj_prefix + "0", embed_size, BERT_D)
+    _linear(sd, g, proj_prefix + "2", embed_size, embed_size)
+    sd["temp"] = torch.tensor(float(temp))
+    return sd

@@ -110,3 +110,44 @@ def compose_prompt_text(labels: Iterable[str]) -> str:
     for e in labels:
         s += " " + e + ","
     return "There are" + s[:-1] + " in this audio."
+
+
+class WordTokenizer:
+    """A GPT-2-like decode for the CLAP-guided ("magic") decoding tests, where generated ids are
+    turned into TEXT and re-tokenised by the BERT text encoder (gpt2_prefix_eval.py:440-445,
+    582-586): ``decode`` concatenates one piece per id -- ' w<id>' starts a new word, 'q<id>'
+    (ids divisible by 5) continues the previous one, and the stop ids render as GPT-2 renders
+    them ('.' = 13, ' .' = 764, ',' = 11).  Every id has its own piece, so :meth:`parse` inverts
+    ``decode``.  ``encode('.')`` is [13] as in GPT-2."""
+
+    _RE = re.compile(r" w\d+|q\d+| \.|\.|,")
+
+    @staticmethod
+    def piece(i: int) -> str:
+        i = int(i)
+        if i == 13:
+            return "."
+        if i == 764:
+            return " ."
+        if i == 11:
+            return ","
+        return f"q{i}" if i % 5 == 0 else f" w{i}"
+
+    def encode(self, text: str) -> List[int]:
+        if text in TEMPLATE_IDS:
+            return list(TEMPLATE_IDS[text])
+        raise KeyError(text)
+
+    def decode(self, ids) -> str:
+        if hasattr(ids, "tolist"):
+            ids = ids.tolist()
+        if isinstance(ids, int):
+            ids = [ids]
+        return "".join(self.piece(i) for i in ids)
+
+    @classmethod
+    def parse(cls, text: str) -> List[int]:
+        out = []
+        for m in cls._RE.findall(text):
+            out.append({".": 13, " .": 764, ",": 11}.get(m) or int(m.lstrip(" wq")))
+        return out
