@@ -189,6 +189,68 @@ int zs_cross_attention(const void* q, int ldq, const void* k, const void* v, int
 int zs_label_topk(const float* emb, int B, int D, const float* labels, int L, int k, int* idx,
                   float* rows, void* stream);
 
+/* ------------------------------------------------------------------ CLAP-guided ("magic") decoding
+ * gpt2_prefix_eval.py:341-689 (magic_search, generate_beam_magic and their helpers) batched over C
+ * clips, b beams per clip (b = 1: magic_search), W candidates per beam.  Candidate c =
+ * (clip*b + beam)*W + w is also the physical row of the GPT-2 KV cache and of the context-hidden
+ * store ctx [rows][Lmax][768] that holds its position-pos entries; kvrow [beam][Lmax] names the
+ * row holding each position of a beam's history (enlarge/select_past_key_values,
+ * gpt2_prefix_eval.py:471-494, as index copies). */
+
+/* zs_bert_embed_ln: HF BertEmbeddings (input_ids, position ids 0..L-1, token type 0) +
+ * LayerNorm(eps) for rows = texts*L token rows (ids int32 [rows], row r = text*L + j): x f32
+ * [rows][768], and h (hdtype) the same values as the next GEMM's operand (may be NULL).
+ * Replaces BertModel's embedding layer under ASE.encode_text (text_encoder.py:64-68). */
+int zs_bert_embed_ln(const int* ids, int rows, int L, const float* word, const float* pos,
+                     const float* type0, const float* ln_w, const float* ln_b, float eps, float* x,
+                     void* h, int hdtype, void* stream);
+
+/* zs_layernorm_dual: LayerNorm of f32 rows y (ldy) into f32 x (ldx) and the operand copy h
+ * (hdtype, ldh; may be NULL) -- BERT's post-LN residual stream (BertSelfOutput / BertOutput).
+ * C must be 768. */
+int zs_layernorm_dual(const float* y, int rows, int C, int ldy, const float* ln_w,
+                      const float* ln_b, float eps, float* x, int ldx, void* h, int ldh,
+                      int hdtype, void* stream);
+
+/* zs_row_topk: per row of f32 logits [R][V] (row stride ld): the k largest (best first, ties to
+ * the lower index) as out_idx [R][k] int32 and out_val [R][k] = log(softmax) (mode 0,
+ * ComputeMagicScore gpt2_prefix_eval.py:560-562) or softmax probability (mode 1,
+ * PlugAndPlayContrastiveDecodingOneStepFast 411-413).  V <= 51200, k <= 64. */
+int zs_row_topk(const float* logits, int R, int V, long ld, int k, int mode, float* out_val,
+                int* out_idx, void* stream);
+
+/* zs_magic_expand: candidate c = beam*W + w inherits its beam's history: kvrow_c[c][t] =
+ * kvrow[beam][t] for t < pos[beam], pos_c[c] = pos[beam] (enlarge_past_key_values 471-480). */
+int zs_magic_expand(const int* kvrow, const int* pos, int nbeams, int W, int Lmax, int* kvrow_c,
+                    int* pos_c, void* stream);
+
+/* zs_magic_maxcos: maxcos[c] = max over t < pos[beam] of cos(ctx[kvrow[beam][t]][t], hid[c])
+ * (plug_and_play_fast_ranking 514-520, prefix_length 1), hid [ncand][768] = the candidates' ln_f
+ * rows (dtype); then stores hid[c] at ctx[c][pos[beam]]. */
+int zs_magic_maxcos(const void* hid, int ncand, int W, void* ctx, int Lmax, const int* kvrow,
+                    const int* pos, float* maxcos, int dtype, void* stream);
+
+/* zs_magic_score: per clip k, over its first nact*W candidates (nact = 1 at the first beam step):
+ * clap = log_softmax_c(cos(text[c], audio[k]) / temp) (gpt2_prefix_eval.py:541-547);
+ * score[c] = (1 - alpha) pval[c] - alpha maxcos[c] + beta clap[c] (plug_and_play_fast_ranking
+ * 530-531).  text [C*b*W][E], audio [C][E] f32.  b <= 8, W <= 64, nact*W <= 512. */
+int zs_magic_score(const float* pval, const float* maxcos, const float* text, const float* audio,
+                   int C, int E, int b, int W, int nact, float temp, float alpha, float beta,
+                   float* score, void* stream);
+
+/* zs_magic_step: one selection step per clip (one block each).  greedy = 0: generate_beam_magic
+ * 626-683 (first: topk(b) of beam 0's W scores; later: stopped beams keep candidate 0 at zero
+ * cost, length-normalised topk over b*W, scores = avg * seq_len); greedy = 1 (b = 1):
+ * magic_search's argmax 459-468.  Rewrites each beam's kvrow / token row from its source beam,
+ * kvrow[beam][pos] = chosen candidate row, pos += 1, tokens[beam][step] = chosen id, copies the
+ * candidate's ln_f row hid[c] to sel_h[beam] (the next LM-head input); a clip is frozen
+ * (cdone[k] = 1) once all its beams stopped or step + 1 >= max_steps[k]; ntok[k] = tokens
+ * emitted.  tokens [C*b][Smax], kvrow [C*b][Lmax] int32. */
+int zs_magic_step(const float* score, const int* cand, int C, int b, int W, int first, int greedy,
+                  int stop, int step, const int* max_steps, float* scores, float* seq_len,
+                  int* stopped, int* tokens, int Smax, int* kvrow, int Lmax, int* pos, int* cdone,
+                  int* ntok, const void* hid, void* sel_h, int dtype, void* stream);
+
 /* ------------------------------------------------------------------ GPT-2 decode
  * zs_gpt2_prefill_embed: clap_to_gpt (caption_model.py:315-329) + the caller's wte lookup
  * (predict_prompt.py:133) + GPT-2 input embedding:  row b, position p < P_b = hard_len[b]+n_soft:

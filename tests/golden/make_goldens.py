@@ -73,9 +73,12 @@ def _pad(rows, fill=-1):
     return out, np.array([len(r) for r in rows], dtype=np.int64)
 
 
-def _caption_model(mapping_type="mlp"):
+def _caption_model(mapping_type="mlp", stop_boost=None):
     from models.caption_model import ClapCaption_prompt
-    sd = S.gpt2_state_dict(**GPT2_KW)
+    kw = dict(GPT2_KW)
+    if stop_boost is not None:
+        kw["stop_boost"] = stop_boost
+    sd = S.gpt2_state_dict(**kw)
     if mapping_type == "mlp":
         sd.update(S.mlp_mapper_state_dict(1))
     else:
@@ -402,7 +405,8 @@ def gen_keys():
 
 
 MAGIC_BERT_LAYERS = 2
-MAGIC_CFGS = ((3, 25, 0.1, 0.2, 12), (2, 8, 0.3, 1.0, 10))   # beam, width, alpha, beta, entry_length
+# beam, width, alpha, beta, entry_length, GPT-2 stop_boost (3.0: some beams stop on '.')
+MAGIC_CFGS = ((3, 25, 0.1, 0.2, 12, 2.0), (2, 8, 0.3, 1.0, 10, 2.0), (3, 25, 0.1, 0.2, 16, 3.0))
 
 
 def _clap_ase(layers):
@@ -430,14 +434,18 @@ def gen_magic(n_clips=3):
     with torch.no_grad():
         text_emb = clap.encode_text(texts)
         bt = clap.text_encoder.tokenizer(texts, padding="longest", truncation=True, max_length=30)
-    model = _caption_model("mlp")
-    _refshim.legacy_cache(model.gpt)
+    models = {}
+    for boost in sorted({c[5] for c in MAGIC_CFGS}):
+        models[boost] = _caption_model("mlp", stop_boost=boost)
+        _refshim.legacy_cache(models[boost].gpt)
+    model = models[2.0]
     emb = S.synthetic_clap_embeddings(n_clips, seed=77)
     label_ids = S.label_token_table()
     hard_rows = [[1858, 389] + label_ids[3 * i] + [287, 428, 6597, 13] for i in range(n_clips)]
     hard, hard_len = _pad(hard_rows)
     out = {}
-    for c, (beam, width, alpha, beta, entry) in enumerate(MAGIC_CFGS):
+    for c, (beam, width, alpha, beta, entry, boost) in enumerate(MAGIC_CFGS):
+        model = models[boost]
         rows = []
         for i in range(n_clips):
             with torch.no_grad():
@@ -451,6 +459,7 @@ def gen_magic(n_clips=3):
         ids, lens = _pad([r for clip in rows for r in clip])
         out[f"beam_cfg{c}_ids"] = ids.reshape(n_clips, beam, -1)
         out[f"beam_cfg{c}_len"] = lens.reshape(n_clips, beam)
+    model = models[2.0]
     search = []
     for i in range(n_clips):
         with torch.no_grad():

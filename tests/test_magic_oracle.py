@@ -48,17 +48,20 @@ def test_encode_text_vs_reference(gold, sds):
     assert (got - torch.from_numpy(gold["text_emb"])).abs().max() < 1e-5
 
 
-def test_generate_beam_magic_vs_reference(gold, sds):
-    csd, bsd = sds
+@pytest.mark.parametrize("cfg,clip", [(1, 0), (2, 2)])
+def test_generate_beam_magic_vs_reference(gold, sds, cfg, clip):
+    bsd = sds[1]
+    beam, width, alpha, beta, entry, boost = gold["cfgs"][cfg]
+    csd = S.gpt2_state_dict(seed=0, std=0.1, emb_std=0.1, stop_boost=float(boost))
+    csd.update(S.mlp_mapper_state_dict(1))
     enc = OM.text_encoder(bert_tokenizer(), bsd, int(gold["bert_layers"]))
-    beam, width, alpha, beta, entry = gold["cfgs"][1]
-    pe, emb = _embed(gold, csd, 0)
+    pe, emb = _embed(gold, csd, clip)
     outs, _ = OM.generate_beam_magic(pe, csd, WordTokenizer().decode, enc, emb, float(bsd["temp"]),
                                      beam_size=int(beam), entry_length=int(entry),
                                      magic_width=int(width), alpha=alpha, beta=beta)
-    ref = gold["beam_cfg1_ids"][0]
+    ref = gold[f"beam_cfg{cfg}_ids"][clip]
     for b, o in enumerate(outs):
-        assert o == [t for t in ref[b][:gold["beam_cfg1_len"][0, b]]]
+        assert o == [t for t in ref[b][:gold[f"beam_cfg{cfg}_len"][clip, b]]]
 
 
 def test_magic_search_vs_reference(gold, sds):

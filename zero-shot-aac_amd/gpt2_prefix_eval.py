@@ -24,7 +24,8 @@ import torch.nn.functional as nnf
 from zsaac import ops
 from zsaac.modules import require_device
 
-__all__ = ["generate2", "generate_beam", "get_prefix_tokens"]
+__all__ = ["generate2", "generate_beam", "get_prefix_tokens", "generate_beam_magic", "magic_search",
+           "compute_audio_text_similarity_via_embeddings", "compute_audio_text_similarity_via_raw_text"]
 
 
 def _decoder(model, embed, entry_length, beam):
@@ -114,3 +115,86 @@ def get_prefix_tokens(prefix_embed, embeddings, tokenizer) -> str:
     prefix_tokens = [tokenizer.decode(int(t)) for t in idx.cpu()]
     prefix_sentence = "".join(prefix_tokens),
     return prefix_sentence
+
+
+# ------------------------------------------------------------------ CLAP-guided ("magic") decoding
+def compute_audio_text_similarity_via_embeddings(clap, audio_embeds, text_embeds):
+    """gpt2_prefix_eval.py:536-547: log(softmax(normalize(text) @ normalize(audio)^T / temp)^T)
+    -> [1, T] (one audio row, as the reference's ``.t()`` requires)."""
+    a = audio_embeds.reshape(1, -1).float()
+    a = a / a.norm(dim=-1, keepdim=True)
+    t = text_embeds / text_embeds.norm(dim=-1, keepdim=True)
+    return (torch.matmul(t, a.t()) / clap.temp).T.softmax(dim=1).log()
+
+
+def compute_audio_text_similarity_via_raw_text(clap, audio_embeds, text_list):
+    """gpt2_prefix_eval.py:549-551 (clap.encode_text on the HIP BERT engine)."""
+    return compute_audio_text_similarity_via_embeddings(clap, audio_embeds, clap.encode_text(text_list))
+
+
+def _magic_engine(model, clap, P, beam, width, steps):
+    from zsaac.magic import MagicDecoder
+    dev = next(model.parameters()).device
+    w = model.gpt.weights(dev)
+    bert = clap.text_engine()
+    key = (P, beam, width, steps, id(bert))
+    cache = w.__dict__.setdefault("_magic", {})
+    if key not in cache:
+        cache.clear()
+        cache[key] = MagicDecoder(w, bert, 1, P + 1, beam=beam, width=width, max_steps=steps)
+    return cache[key]
+
+
+def _magic_inputs(embed, audio_embeds):
+    require_device(embed, "magic decoding")
+    if embed.shape[0] != 1:
+        raise ValueError("the reference decodes one clip per call (batch 1); use "
+                         "zsaac.magic.MagicDecoder for batches")
+    dev = embed.device
+    zeros = torch.zeros(1, 1, dtype=torch.int32, device=dev)
+    hl = torch.zeros(1, dtype=torch.int32, device=dev)
+    # audio_embeds: [1, 1024] (the reference's .t() at line 543 needs 2-D; predict_prompt.py:140
+    # passes the collated [1, 1, 1024] prefix, which the reference itself cannot transpose)
+    audio = audio_embeds.reshape(1, -1).float().to(dev).contiguous()
+    return zeros, hl, embed.float().contiguous(), audio
+
+
+def generate_beam_magic(model, clap, tokenizer, audio_embeds, beam_size: int = 5, prompt=None,
+                        embed=None, entry_length=20, temperature=1., stop_token: str = '.',
+                        magic_width=25, alpha=0.1, beta=0.2) -> List[str]:
+    """CLAP-guided beam search (gpt2_prefix_eval.py:602-689): per step the top ``magic_width``
+    tokens of every beam are scored by (1-alpha) log p - alpha max-cos(context) + beta CLAP
+    log-softmax of the candidate text, then length-normalised beam selection; texts sorted best
+    first.  ``embed`` is required (with only a ``prompt`` the reference feeds the prompt ids into
+    the candidate texts and token rows, a path its own callers never take)."""
+    _check_temperature(temperature)
+    if embed is None:
+        raise NotImplementedError("generate_beam_magic needs embed= (predict_prompt.py:140)")
+    stop = tokenizer.encode(stop_token)[0]
+    hard, hl, soft, audio = _magic_inputs(embed, audio_embeds)
+    P = soft.shape[1]
+    eng = _magic_engine(model, clap, P, beam_size, magic_width, entry_length)
+    (toks, _), = eng.beam_magic(hard, hl, soft, P, audio, tokenizer, clap.text_encoder.tokenizer,
+                                beam_size, magic_width, entry_length, alpha, beta,
+                                float(clap.temp), stop)
+    return [tokenizer.decode(t) for t in toks]
+
+
+def magic_search(model, tokenizer, audio_embeds, clap, input_ids=None, prompt=None, embed=None,
+                 beam_width=15, alpha=0.1, decoding_len=35, beta=0.2, clip_text_max_len=60,
+                 stop_token='.') -> str:
+    """CLAP-guided greedy decoding (gpt2_prefix_eval.py:341-393 + 396-469): ``decoding_len -
+    prefix_len`` steps, each picking the argmax of (1-alpha) p - alpha max-cos + beta CLAP score
+    over the top ``beam_width`` tokens; stops after emitting ``stop_token``; returns the decoded
+    generated ids.  ``embed`` is required (the reference's prompt path raises NameError at 349)."""
+    if embed is None:
+        raise NotImplementedError("magic_search needs embed= (the reference's prompt path "
+                                  "references an unbound name, gpt2_prefix_eval.py:349)")
+    stop = tokenizer.encode(stop_token)[0]
+    hard, hl, soft, audio = _magic_inputs(embed, audio_embeds)
+    P = soft.shape[1]
+    steps = max(decoding_len - P, 1)
+    eng = _magic_engine(model, clap, P, 1, beam_width, steps)
+    ids, = eng.search(hard, hl, soft, P, audio, tokenizer, clap.text_encoder.tokenizer,
+                      beam_width, decoding_len, alpha, beta, float(clap.temp), stop)
+    return tokenizer.decode(ids)

@@ -68,6 +68,13 @@ SIGNATURES = {
     "zs_prefix_ids_assemble": [P, I, P, P, I, I, I, P, P],
     "zs_greedy_step": [P, P, I, I, P, I, I, I, P, P, P, P, P, P, P],
     "zs_beam_step": [P, P, P, I, I, I, I, I, I, P, I, P, P, P, P, P, P, P, I, P, P, P, P],
+    "zs_bert_embed_ln": [P, I, I, P, P, P, P, P, F, P, P, I, P],
+    "zs_layernorm_dual": [P, I, I, I, P, P, F, P, I, P, I, I, P],
+    "zs_row_topk": [P, I, I, L, I, I, P, P, P],
+    "zs_magic_expand": [P, P, I, I, I, P, P, P],
+    "zs_magic_maxcos": [P, I, I, P, I, P, P, P, I, P],
+    "zs_magic_score": [P, P, P, P, I, I, I, I, I, F, F, F, P, P],
+    "zs_magic_step": [P, P, I, I, I, I, I, I, I, P, P, P, P, P, I, P, I, P, P, P, P, P, I, P],
 }
 
 _lib = None

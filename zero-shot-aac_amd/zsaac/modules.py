@@ -255,14 +255,19 @@ class ZsGPT2LMHeadModel(nn.Module):
     def get_input_embeddings(self):
         return self.transformer.wte
 
-    def engine(self, max_rows: int, max_prompt: int, max_steps: int, device):
-        from .decoder import Gpt2Decoder, Gpt2Weights
+    def weights(self, device):
+        """The packed Gpt2Weights of these parameters (cached until they change)."""
+        from .decoder import Gpt2Weights
         dt = zs_dtype_of(self)
 
         def build():
             sd = {"gpt." + k: v for k, v in self.state_dict().items()}
             return Gpt2Weights(sd, device, dt)
-        w = self._cache.get(self, build, (dt, str(device)))
+        return self._cache.get(self, build, (dt, str(device)))
+
+    def engine(self, max_rows: int, max_prompt: int, max_steps: int, device):
+        from .decoder import Gpt2Decoder
+        w = self.weights(device)
         key = (max_rows, max_prompt, max_steps)
         decs = w.__dict__.setdefault("_decoders", {})
         if key not in decs:

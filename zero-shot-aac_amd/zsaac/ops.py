@@ -395,3 +395,60 @@ def beam_step(part_stat, part_val, part_idx, C, beam, nblk, topk, first, stop, s
          int(first), stop, _p(step_ctr), max_steps, _p(scores), _p(seq_len), _p(stopped),
          _p(tokens), _p(tokens_tmp), _p(kvrow), _p(kvrow_tmp), Lmax, _p(pos), _p(next_tok),
          _p(all_done), _s())
+
+
+# ---------------------------------------------------------------- CLAP text tower + magic decoding
+def bert_embed_ln(ids, L, word, pos, type0, ln_w, ln_b, x, h=None, eps=1e-12):
+    """ids [T*L] int32 -> x f32 [T*L, 768] (+ operand copy h): BertEmbeddings + LayerNorm."""
+    _i32(ids, "ids")
+    rows = ids.numel()
+    call("zs_bert_embed_ln", _p(ids), rows, L, _p(word), _p(pos), _p(type0), _p(ln_w), _p(ln_b),
+         float(eps), _p(x), _p(h), dt(h) if h is not None else ZS_F32, _s())
+    return x
+
+
+def layernorm_dual(y, ln_w, ln_b, x, h=None, eps=1e-12, M=None):
+    C = y.shape[-1]
+    M = M if M is not None else y.numel() // C
+    call("zs_layernorm_dual", _p(y), M, C, y.stride(0), _p(ln_w), _p(ln_b), float(eps), _p(x),
+         x.stride(0), _p(h), h.stride(0) if h is not None else C,
+         dt(h) if h is not None else ZS_F32, _s())
+    return x
+
+
+def row_topk(logits, k, out_val, out_idx, mode=0, R=None, V=None):
+    """top-k of each logits row with log(softmax) (mode 0) or softmax (mode 1) values."""
+    _need(logits.dtype == torch.float32, "row_topk: f32 logits")
+    _i32(out_idx, "out_idx")
+    R = R if R is not None else logits.shape[0]
+    V = V if V is not None else logits.shape[1]
+    call("zs_row_topk", _p(logits), R, V, logits.stride(0), k, mode, _p(out_val), _p(out_idx), _s())
+    return out_val, out_idx
+
+
+def magic_expand(kvrow, pos, nbeams, W, Lmax, kvrow_c, pos_c):
+    for t, n in ((kvrow, "kvrow"), (pos, "pos"), (kvrow_c, "kvrow_c"), (pos_c, "pos_c")):
+        _i32(t, n)
+    call("zs_magic_expand", _p(kvrow), _p(pos), nbeams, W, Lmax, _p(kvrow_c), _p(pos_c), _s())
+
+
+def magic_maxcos(hid, ncand, W, ctx, Lmax, kvrow, pos, maxcos):
+    _need(hid.dtype == ctx.dtype, "magic_maxcos: hid / ctx dtype")
+    call("zs_magic_maxcos", _p(hid), ncand, W, _p(ctx), Lmax, _p(kvrow), _p(pos), _p(maxcos),
+         dt(hid), _s())
+    return maxcos
+
+
+def magic_score(pval, maxcos, text, audio, C, b, W, nact, temp, alpha, beta, score):
+    E = audio.shape[-1]
+    call("zs_magic_score", _p(pval), _p(maxcos), _p(text), _p(audio), C, E, b, W, nact,
+         float(temp), float(alpha), float(beta), _p(score), _s())
+    return score
+
+
+def magic_step(score, cand, C, b, W, first, greedy, stop, step, max_steps, scores, seq_len,
+               stopped, tokens, kvrow, pos, cdone, ntok, hid, sel_h):
+    _need(hid.dtype == sel_h.dtype, "magic_step: hid / sel_h dtype")
+    call("zs_magic_step", _p(score), _p(cand), C, b, W, int(first), int(greedy), stop, step,
+         _p(max_steps), _p(scores), _p(seq_len), _p(stopped), _p(tokens), tokens.shape[1],
+         _p(kvrow), kvrow.shape[1], _p(pos), _p(cdone), _p(ntok), _p(hid), _p(sel_h), dt(hid), _s())
