@@ -114,6 +114,11 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--stages", action="store_true", help="also report per-stage ms (extra syncs)")
+    ap.add_argument("--magic", action="store_true",
+                    help="CLAP-guided beam decoding (generate_beam_magic: beam 3, width 25, "
+                         "entry 20, predict_prompt.py --magic) on bs=64 batches: a labelled "
+                         "secondary line, not the metric")
+    ap.add_argument("--magic-bert-layers", type=int, default=12)
     ap.add_argument("--embeddings-only", action="store_true",
                     help="C4: batched HTSAT/CNN14 encode_audio + one RCCL all-gather of the "
                          "[N,1024] embeddings (no caption decode)")
@@ -540,12 +545,72 @@ def main_embeddings(args, world, rank, device, pipe):
 
 
 # ------------------------------------------------------------------ main
+def main_magic(args, device):
+    """CLAP-guided decoding throughput (predict_prompt.py:121-140 with --magic): wav -> HTSAT ->
+    prompt + mapper -> generate_beam_magic(beam 3, width 25, alpha 0.1, beta 0.2, entry 20) with
+    a bert-base text tower (12 layers, synthetic WordPiece vocabulary), bs=64 batches, one
+    stream.  Host work per step (candidate texts + BERT tokenisation, as the reference) is
+    inside the timed region."""
+    from transformers import BertTokenizer
+    from zsaac import ops, synthetic as S
+    from zsaac.bert import BertTextEngine
+    from zsaac.magic import MagicDecoder
+    from zsaac.tokenizer import WordTokenizer
+    args.group = 1
+    pipe, _, _ = build(args, device, encoder_batch=args.batch)
+    vocab = S.bert_vocab()
+    bsd = S.bert_state_dict(layers=args.magic_bert_layers)
+    bert = BertTextEngine(bsd, device, pipe.cfg.dtype, max_texts=args.batch * 75)
+    tok = BertTokenizer(vocab={t: i for i, t in enumerate(vocab)}, do_lower_case=True)
+    beam, width, entry = 3, 25, 20
+    mag = MagicDecoder(pipe.gpt, bert, args.batch, pipe.Pmax, beam=beam, width=width,
+                       max_steps=entry)
+    n = args.steps or 2
+    wav = synthetic_clips(args.batch, 0, device)
+
+    def one():
+        emb = pipe.encode(wav)
+        B = emb.shape[0]
+        ops.prompt_assemble(emb, pipe.labels, pipe.cfg.sound_effect_num, pipe.label_tok,
+                            pipe.label_len, pipe.hard_ids[:B], pipe.hard_len[:B])
+        prefix = ops.l2norm(emb, out=pipe.prefix[:B])
+        soft = pipe.mapper(prefix)
+        return mag.beam_magic(pipe.hard_ids[:B], pipe.hard_len[:B], soft, 10, prefix,
+                              WordTokenizer(), tok, beam, width, entry, 0.1, 0.2, bert.temp,
+                              soft_ld=pipe.mapper.soft_ld)
+    for _ in range(max(1, args.warmup)):
+        one()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    toks = 0
+    for _ in range(n):
+        res = one()
+        toks += sum(len(r[0][0]) for r in res)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    clips = n * args.batch
+    print(json.dumps({
+        "metric": "audio clips/sec, CLAP-guided beam decoding (generate_beam_magic), bs=64",
+        "value": round(clips / dt, 3), "unit": "clips/s", "n_gpus": 1, "steps": n,
+        "warmup": args.warmup, "ms_per_step": round(dt / n * 1e3, 1), "higher_is_better": True,
+        "dtype": args.dtype, "data": DATA + "; bert-base text tower (synthetic weights/vocab)",
+        "config": {"workload": "wav -> HTSAT -> prompt + MLP mapper -> generate_beam_magic "
+                               "(beam 3, magic_width 25, entry_length 20, alpha 0.1, beta 0.2)",
+                   "batch": args.batch, "bert_layers": args.magic_bert_layers,
+                   "candidate_rows_per_step": args.batch * beam * width,
+                   "tokens_best_beam": toks},
+        "note": "secondary decode mode (predict_prompt.py --magic); not the headline metric"}),
+        flush=True)
+
+
 def main():
     args = parse()
     world, rank, local = dist_setup(args)
     device = torch.device("cuda", local)
     from zsaac import dist as zd
     pipe, csd, asd = build(args, device)
+    if args.magic:
+        return main_magic(args, torch.device("cuda", 0))
     if args.embeddings_only:
         return main_embeddings(args, world, rank, device, pipe)
     B = pipe.cfg.batch

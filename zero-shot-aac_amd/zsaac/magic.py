@@ -74,20 +74,20 @@ class MagicDecoder:
         self.ws = ops.skinny_workspace(dev, [(nb, gpt.V, D)])
 
     # ------------------------------------------------------------------ prefill
-    def _prefill(self, hard_ids, hard_len, soft, n_soft, C, b, W):
+    def _prefill(self, hard_ids, hard_len, soft, n_soft, C, b, W, soft_ld=None):
         """Prompt rows (clap_to_gpt: wte(hard) ; soft) through GPT-2: KV rows k*b*W, the ln_f
         rows of every prompt position into ctx[k*b*W], the last position's LM-head logits into
         beam row k*b."""
         dec = self.dec
         Pmax = int(hard_ids.shape[1]) + n_soft
-        ops.prefill_embed(hard_ids, hard_len, soft, soft.stride(0), n_soft, self.gpt.wte,
+        ops.prefill_embed(hard_ids, hard_len, soft, soft_ld or soft.stride(0), n_soft, self.gpt.wte,
                           self.gpt.wpe, C, Pmax, None, dec.x, dec.plen, dec.last_row)
         dec.prefill(C, Pmax, row_stride=b * W)
         M = C * Pmax
         hp = dec.h[:M]
         ops.layernorm(dec.x[:M], *self.gpt.lnf, out=hp)
         Lmax = dec.Lmax
-        self.ctx.view(-1, b * W, Lmax, D)[:C, 0, :Pmax].copy_(hp.view(C, Pmax, D))
+        self.ctx[:C * b * W].view(C, b * W, Lmax, D)[:, 0, :Pmax].copy_(hp.view(C, Pmax, D))
         nb = C * b
         self.logits[:nb].zero_()
         ops.gemm(dec.hf[:C], self.gpt.wte, self.logits[:nb].view(C, b * self.gpt.V)[:, :self.gpt.V],
@@ -150,8 +150,8 @@ class MagicDecoder:
     # ------------------------------------------------------------------ entry points
     def beam_magic(self, hard_ids, hard_len, soft, n_soft, audio, tokenizer, text_tokenizer,
                    beam: int, width: int, entry_length: int, alpha: float = 0.1,
-                   beta: float = 0.2, temp: Optional[float] = None,
-                   stop: int = 13) -> List[Tuple[List[List[int]], List[float]]]:
+                   beta: float = 0.2, temp: Optional[float] = None, stop: int = 13,
+                   soft_ld: Optional[int] = None) -> List[Tuple[List[List[int]], List[float]]]:
         """generate_beam_magic for every clip: per clip (token lists best-first, scores/len).
         hard_ids [C, H] int32 / hard_len [C] / soft [C, n_soft, 768] f32 (clap_to_gpt's rows),
         audio [C, 1024] f32 (the CLAP audio embeddings)."""
@@ -160,7 +160,7 @@ class MagicDecoder:
         if entry_length > self.max_steps:
             raise ValueError(f"entry_length {entry_length} > engine max_steps {self.max_steps}")
         temp = self.bert.temp if temp is None else temp
-        self._prefill(hard_ids, hard_len, soft, n_soft, C, beam, width)
+        self._prefill(hard_ids, hard_len, soft, n_soft, C, beam, width, soft_ld)
         self._init_state(C, beam, width, torch.full((C,), entry_length, dtype=torch.int32))
         self._run(C, beam, width, "beam", tokenizer, text_tokenizer, audio.float().contiguous(),
                   alpha, beta, temp, stop, entry_length)
