@@ -251,6 +251,50 @@ int zs_magic_step(const float* score, const int* cand, int C, int b, int W, int 
                   int* stopped, int* tokens, int Smax, int* kvrow, int Lmax, int* pos, int* cdone,
                   int* ntok, const void* hid, void* sel_h, int dtype, void* stream);
 
+/* ------------------------------------------------------------------ Mistral-7B decoder (C5)
+ * predict_mistralai_multilingual.py:97-111 / models/caption_model.py:340-413: batched greedy
+ * MistralForCausalLM.generate over inputs_embeds.  head_dim 128, grouped-query attention.
+ * Split-K GEMM results are f32 slabs [nsplit][M][N] (split stride ss) summed in order by their
+ * consumer (RoPE/KV append, SiLU*up, add+RMSNorm): deterministic, no reduction launch. */
+
+/* zs_fp8_gemm_rows: weight-only fp8 GEMM for M <= 64 rows (decode): out[s][m][n] = scale[n] *
+ * sum_{k in split s} A[m][k] W8[n][k]; A bf16 [M][lda], W8 fp8 e4m3 (OCP) codes [N][K], scale f32
+ * [N] (one per output channel), splits of 1024 along K (zs_fp8_splits(K) of them), ldo >= N.
+ * Replaces the NF4-quantised q/k/v/o/gate/up/down projections of the LoRA-wrapped Mistral
+ * (caption_model.py:355-364). */
+int zs_fp8_gemm_rows(const void* A, int lda, const void* W8, const float* scale, int M, int N,
+                     int K, float* out, long split_stride, int ldo, void* stream);
+int zs_fp8_splits(int K);
+
+/* zs_mistral_embed: prefill rows b*P + i (P = H + ns + nt): embed[hard[b][i]] (i < H, pads
+ * included as the reference attends them), soft[b][i-H] (ns rows, f32), embed[tail[i-H-ns]]
+ * (the language tag); or, with tok != NULL, decode rows embed[tok[m]].  x f32 [M][D]. */
+int zs_mistral_embed(const int* hard, int H, const float* soft, int ns, const int* tail, int nt,
+                     const int* tok, const void* emb, int D, int M, float* x, int dtype,
+                     void* stream);
+
+/* zs_mistral_add_rmsnorm: x[m] += sum_s y[s][m] (y may be NULL), h[m] = w * (x[m] *
+ * rsqrt(mean(x[m]^2) + eps)) (MistralRMSNorm; w NULL = folded into the next GEMM). */
+int zs_mistral_add_rmsnorm(float* x, const float* y, int nsplit, long ss, int M, int D, float eps,
+                           const float* w, void* h, int hdtype, void* stream);
+
+/* zs_mistral_rope_kv: q|k|v slabs [nsplit][M][(H + 2 KVH) * 128] -> rotary-embedded q [M][H*128]
+ * and k, plus v, appended to the caches [seq][KVH][Lmax][128] at position pos[m] (seq =
+ * m / rows_per_seq); cos / sin [Lmax][64] f32 tables (HF rotary, rotate_half). */
+int zs_mistral_rope_kv(const float* qkv, int nsplit, long ss, int M, int H, int KVH,
+                       const int* pos, int rows_per_seq, const float* cosb, const float* sinb,
+                       void* q, void* kc, void* vc, int Lmax, int dtype, void* stream);
+
+/* zs_mistral_silu_mul: act[m][f] = silu(gate) * up from gate|up slabs [nsplit][M][2F]. */
+int zs_mistral_silu_mul(const float* gu, int nsplit, long ss, int M, int F, void* act, int dtype,
+                        void* stream);
+
+/* zs_mistral_attention: causal GQA attention, query row m against keys 0..pos[m] of sequence
+ * m / rows_per_seq, kv head h / (H / KVH), softmax((q k^T) / sqrt(128)) v -> out [M][H*128]. */
+int zs_mistral_attention(const void* q, int M, int H, int KVH, const int* pos, int rows_per_seq,
+                         const void* kc, const void* vc, int Lmax, void* out, int dtype,
+                         void* stream);
+
 /* ------------------------------------------------------------------ GPT-2 decode
  * zs_gpt2_prefill_embed: clap_to_gpt (caption_model.py:315-329) + the caller's wte lookup
  * (predict_prompt.py:133) + GPT-2 input embedding:  row b, position p < P_b = hard_len[b]+n_soft:

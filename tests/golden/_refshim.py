@@ -116,6 +116,47 @@ def install_bert(vocab, layers):
         lambda *a, **k: BertTokenizer(vocab={t: i for i, t in enumerate(vocab)}, do_lower_case=True))
 
 
+def install_mistral(cfg_kw):
+    """ClapCaption_Mistralai_prompt (models/caption_model.py:340-370) loads
+    ``MistralForCausalLM.from_pretrained('mistralai/Mistral-7B-v0.1', quantization_config=NF4)``
+    (a name fetch, unavailable offline) and wraps it with peft LoRA (absent).  Shims: a locally
+    built ``MistralForCausalLM(MistralConfig(**cfg_kw))`` (eager attention) into which the caller
+    loads the synthetic weights; ``prepare_model_for_kbit_training`` = identity; ``get_peft_model``
+    = a wrapper exposing the ``base_model.model.model.embed_tokens`` path and ``generate`` of the
+    real PeftModelForCausalLM without adapters (LoRA with B = 0 at init is the identity)."""
+    install()
+    from transformers import MistralConfig, MistralForCausalLM
+
+    def _model(*a, **k):
+        cfg = MistralConfig(**cfg_kw)
+        cfg._attn_implementation = "eager"
+        return MistralForCausalLM(cfg)
+    MistralForCausalLM.from_pretrained = staticmethod(_model)
+
+    class _Lora(nn.Module):
+        def __init__(self, m):
+            super().__init__()
+            self.model = m
+
+    class _Peft(nn.Module):
+        def __init__(self, m):
+            super().__init__()
+            self.base_model = _Lora(m)
+
+        def generate(self, *a, **k):
+            return self.base_model.model.generate(*a, **k)
+
+        def forward(self, *a, **k):
+            return self.base_model.model(*a, **k)
+
+    peft = sys.modules["peft"]
+    peft.prepare_model_for_kbit_training = lambda m, **k: m
+    peft.get_peft_model = lambda m, cfg: _Peft(m)
+    peft.LoraConfig = lambda **k: None
+    transformers = sys.modules["transformers"]
+    transformers.__dict__["BitsAndBytesConfig"] = lambda **k: None
+
+
 def legacy_cache(gpt):
     """The reference's magic decoding handles ``past_key_values`` as transformers 4.24's tuples of
     per-layer (k, v) (gpt2_prefix_eval.py:471-494); transformers 5.x returns and expects a Cache

@@ -24,6 +24,10 @@ Fixture list (reference call sites in brackets):
                   ClapCaptionPrefix: clap_to_gpt outputs and generate2 ids.
   c2_margin.npz   generate2 with the reference's top-1/top-2 logit margin at every generated
   c2_margin_flat.npz  step, on smaller decoder weights (the bf16 id-parity check).
+  mistral.npz     C5 Mistral decoder path: ClapCaption_Mistralai_prompt.clap_to_gpt
+                  (caption_model.py:392-413) + LMmodel.generate(inputs_embeds, attention_mask=ones,
+                  do_sample=False, max_length=60, eos/pad 2) as predict_mistralai_multilingual.py:
+                  97-111 drive them, on a 2-layer / 1024-wide Mistral (head_dim 128, GQA 8/2).
   magic.npz       CLAP-guided decoding: ASE.encode_text on sample texts (text_encoder.py:58-68,
                   ase_model.py:57-60), generate_beam_magic (gpt2_prefix_eval.py:602-689) at two
                   (beam, width, alpha, beta) settings and magic_search (341-469), BERT text tower
@@ -475,10 +479,57 @@ def gen_magic(n_clips=3):
           search_ids=s_ids, search_len=s_len, **out)
 
 
+MISTRAL_CFG = dict(vocab_size=32000, hidden_size=1024, intermediate_size=3072,
+                   num_hidden_layers=2, num_attention_heads=8, num_key_value_heads=2,
+                   rms_norm_eps=1e-5, rope_theta=10000.0, tie_word_embeddings=False,
+                   max_position_embeddings=4096, sliding_window=4096)
+MISTRAL_TAGS = {"en": [1, 523, 269, 28767], "zh": [1, 523, 26715, 28767], "fr": [1, 523, 1642, 28767]}
+
+
+def gen_mistral(n_clips=6):
+    """One batch of ``n_clips`` through the reference's Mistral caption path, two languages."""
+    _refshim.install_mistral(MISTRAL_CFG)
+    from models.caption_model import ClapCaption_Mistralai_prompt
+    from zsaac import synthetic as SS
+    m = ClapCaption_Mistralai_prompt(10, clip_length=10, prefix_size=1024, num_layers=8,
+                                     mapping_type="mlp")
+    lm_sd = SS.mistral_state_dict()
+    m.LMmodel.base_model.model.load_state_dict(lm_sd)
+    D = MISTRAL_CFG["hidden_size"]
+    mlp = SS.mlp_mapper_state_dict(31, prefix_length=10, d=D)
+    missing, unexpected = m.clap_project.load_state_dict(
+        {k.replace("clap_project.", ""): v for k, v in mlp.items()})
+    m.eval()
+    emb = S.synthetic_clap_embeddings(n_clips, seed=55).unsqueeze(1)     # [B, 1, 1024] (collate)
+    g = torch.Generator().manual_seed(56)
+    lens = [int(x) for x in torch.randint(5, 12, (n_clips,), generator=g)]
+    H = max(lens)
+    hard = torch.zeros(n_clips, H, dtype=torch.long)                   # padding_captions: pad 0
+    for b, n in enumerate(lens):
+        hard[b, :n] = torch.randint(3, 32000, (n,), generator=g)
+    out = {}
+    with torch.no_grad():
+        eh = m.LMmodel.base_model.model.model.embed_tokens(hard)
+        for tag in ("en", "fr"):
+            tk = torch.tensor([MISTRAL_TAGS[tag]]).repeat(n_clips, 1)
+            et = m.LMmodel.base_model.model.model.embed_tokens(tk)
+            pe, _ = m.clap_to_gpt(emb, eh, et)
+            am = torch.ones(pe.shape[:-1]).long()
+            ids = m.LMmodel.generate(inputs_embeds=pe, attention_mask=am, do_sample=False,
+                                     max_length=60, eos_token_id=2, pad_token_id=2)
+            out[f"ids_{tag}"] = ids.numpy()
+            print(f"  mistral {tag}: P={pe.shape[1]} out {tuple(ids.shape)} "
+                  f"eos rows {int((ids == 2).any(1).sum())}", flush=True)
+    _save("mistral.npz", clap_emb=emb[:, 0].numpy(), hard_ids=hard.numpy(),
+          hard_len=np.array(lens), tag_en=np.array(MISTRAL_TAGS["en"]),
+          tag_fr=np.array(MISTRAL_TAGS["fr"]), **out)
+
+
 ALL = {"prompt": gen_prompt, "mappers": gen_mappers, "htsat": gen_htsat, "cnn14": gen_cnn14,
        "beam": gen_beam, "c1": gen_c1, "keys": gen_keys,
        "margin": gen_margin, "margin_flat": lambda: gen_margin(name="c2_margin_flat"),
-       "variants": gen_variants, "magic": gen_magic}
+       "variants": gen_variants, "magic": gen_magic,
+       "mistral": gen_mistral}
 
 if __name__ == "__main__":
     torch.set_num_threads(os.cpu_count() or 8)

@@ -1,0 +1,126 @@
+"""GPU: the C5 Mistral caption decoder (zsaac/mistral.py, csrc/mistral.hip) against the
+reference goldens (tests/golden/mistral.npz) and the pinned oracle (oracle/mistral.py).
+
+f32 parity mode: generated ids bit-exact for every clip and language.  fp8 perf mode (weight-only
+fp8 e4m3, bf16 activations): ids equal to the reference up to the first step whose reference
+top-2 logit margin is below 0.5 (the fp8/bf16 logit error is far below that; past such a step
+the two decodes may legitimately follow different branches).  Kernels: the fp8 row GEMM against
+torch on dequantised weights."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+H, KVH, EPS = 8, 2, 1e-5
+
+
+def _strip(row, eos=2):
+    row = [int(t) for t in row]
+    return row[:row.index(eos) + 1] if eos in row else row
+
+
+@pytest.fixture(scope="module")
+def setup(golden):
+    from oracle import mistral as OM
+    from zsaac import synthetic as S
+    g = golden("mistral.npz")
+    sd = S.mistral_state_dict()
+    mlp = S.mlp_mapper_state_dict(31, prefix_length=10, d=1024)
+    emb = torch.from_numpy(g["clap_emb"])[:, None]
+    hard = torch.from_numpy(g["hard_ids"])
+    pes = {t: OM.clap_to_gpt(emb, hard, torch.from_numpy(g[f"tag_{t}"]), sd, mlp) for t in ("en", "fr")}
+    return g, sd, pes
+
+
+def _run(cuda, g, sd, pes, mode):
+    from zsaac.mistral import MistralDecoder, MistralWeights
+    w = MistralWeights(sd, cuda, mode, n_heads=H, n_kv_heads=KVH, eps=EPS)
+    dec = MistralDecoder(w, max_batch=8, max_prompt=32, max_new=40)
+    hard = torch.from_numpy(g["hard_ids"]).to(torch.int32).to(cuda)
+    out = {}
+    for t, (pe, soft) in pes.items():
+        tag = torch.from_numpy(g[f"tag_{t}"]).to(torch.int32).to(cuda)
+        out[t] = dec.generate(hard, soft.contiguous().to(cuda), tag, max_length=60)
+    return out
+
+
+def test_mistral_f32_bit_exact(cuda, setup):
+    """f32: ids equal the reference's; a row may only part at a step where the reference's own
+    top-2 logits tie to f32 rounding (margin < 1e-4: 'fr' clip 4 has a 0.0 margin at step 12)."""
+    from oracle import mistral as OM
+    g, sd, pes = setup
+    out = _run(cuda, g, sd, pes, "f32")
+    exact = 0
+    for t in ("en", "fr"):
+        ref = g[f"ids_{t}"]
+        margins = []
+        OM.generate(pes[t][0], sd, H, KVH, EPS, margins=margins)
+        for b in range(ref.shape[0]):
+            r = _strip(ref[b])
+            n = next((i for i, m in enumerate(margins[b]) if m < 1e-4), len(r))
+            assert out[t][b][:n + 1] == r[:n + 1], (t, b, n)
+            exact += out[t][b] == r
+    print(f"f32 mistral: {exact}/12 rows exact end to end")
+    assert exact >= 11
+
+
+def test_mistral_fp8_ids_until_small_margin(cuda, setup):
+    from oracle import mistral as OM
+    g, sd, pes = setup
+    out = _run(cuda, g, sd, pes, "fp8")
+    agree = total = 0
+    for t in ("en", "fr"):
+        margins = []
+        ref = OM.generate(pes[t][0], sd, H, KVH, EPS, margins=margins)
+        for b in range(len(ref)):
+            n = next((i for i, m in enumerate(margins[b]) if m < 0.5), len(ref[b]))
+            assert out[t][b][:n] == ref[b][:n], (t, b, n)
+            agree += sum(int(x == y) for x, y in zip(out[t][b], ref[b]))
+            total += len(ref[b])
+    print(f"fp8 mistral: token agreement {agree}/{total}")
+
+
+@pytest.mark.parametrize("M,N,K", [(32, 6144, 4096), (7, 1000, 1024), (64, 256, 14336)])
+def test_fp8_gemm_rows(cuda, M, N, K):
+    from zsaac._lib import call
+    from zsaac.mistral import dequantize_fp8, quantize_fp8
+    g = torch.Generator().manual_seed(M + N)
+    w = torch.randn(N, K, generator=g) / K ** 0.5
+    a = torch.randn(M, K, generator=g).bfloat16()
+    q, s = quantize_fp8(w)
+    ref = a.float() @ dequantize_fp8(q, s).t()
+    ns = call("zs_fp8_splits", K)
+    out = torch.empty(ns, M, N, device=cuda)
+    ad, qd, sd = a.to(cuda), q.to(cuda), s.to(cuda)        # keep the device copies alive
+    call("zs_fp8_gemm_rows", ad.data_ptr(), K, qd.data_ptr(), sd.data_ptr(),
+         M, N, K, out.data_ptr(), M * N, N, torch.cuda.current_stream().cuda_stream)
+    got = out.sum(0).cpu()
+    assert float((got - ref).abs().max()) < 1e-3 * float(ref.abs().max()) + 1e-4
+
+
+def test_dropin_clap_caption_mistralai(cuda, golden):
+    """ClapCaption_Mistralai_prompt driven like predict_mistralai_multilingual.py:95-111 (peft
+    attribute path, clap_to_gpt with the language tag, LMmodel.generate), f32 parity mode."""
+    from models.caption_model import ClapCaption_Mistralai_prompt
+    from zsaac import synthetic as S
+    g = golden("mistral.npz")
+    cfg = dict(vocab_size=32000, hidden_size=1024, intermediate_size=3072, num_hidden_layers=2,
+               num_attention_heads=8, num_key_value_heads=2, rms_norm_eps=1e-5)
+    m = ClapCaption_Mistralai_prompt(10, clip_length=10, prefix_size=1024, num_layers=8,
+                                     mapping_type="mlp", mistral_config=cfg)
+    sd = {"LMmodel.base_model.model." + k: v for k, v in S.mistral_state_dict().items()}
+    sd.update(S.mlp_mapper_state_dict(31, prefix_length=10, d=1024))
+    m.load_state_dict(sd)
+    m = m.set_mode("f32").to(cuda).eval()
+    prefix = torch.from_numpy(g["clap_emb"])[:, None].to(cuda)
+    hard = torch.from_numpy(g["hard_ids"]).to(cuda)
+    with torch.no_grad():
+        eh = m.LMmodel.base_model.model.model.embed_tokens(hard)
+        tk = torch.from_numpy(g["tag_en"])[None].repeat(prefix.shape[0], 1).to(cuda)
+        et = m.LMmodel.base_model.model.model.embed_tokens(tk)
+        pe, _ = m.clap_to_gpt(prefix, eh, et)
+        am = torch.ones(pe.shape[:-1]).long().to(cuda)
+        ids = m.LMmodel.generate(inputs_embeds=pe, attention_mask=am, do_sample=False,
+                                 max_length=60, eos_token_id=2, pad_token_id=2)
+    assert torch.equal(ids.cpu(), torch.from_numpy(g["ids_en"]))

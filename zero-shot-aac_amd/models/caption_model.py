@@ -13,7 +13,15 @@ HIP kernels: the mappers' GEMMs, sound_effect_choice (zs_label_topk), the cross-
 
 Inference only: ``forward`` (the training forward, with labels and attention masks) serves
 labels=None / mask=None; ClapCaptionCrossattention_v2's training-time random key mask is not
-provided (eval uses no mask, caption_model.py:182-183).  The Mistral classes are not here.
+provided (eval uses no mask, caption_model.py:182-183).
+
+``ClapCaption_Mistralai_prompt`` (caption_model.py:340-413, BASELINE config C5) holds the
+MistralForCausalLM parameter tree under ``LMmodel.base_model.model`` (the peft path its callers
+use: ``LMmodel.base_model.model.model.embed_tokens``, predict_mistralai_multilingual.py:95-101)
+and ``LMmodel.generate`` runs zsaac.mistral on the HIP kernels (fp8 e4m3 weights by default;
+``zs_dtype = torch.float32`` selects the f32 parity mode).  A peft checkpoint's LoRA factors are
+merged into the base weights at load; the reference's NF4 storage (bitsandbytes) is replaced by
+fp8 (zsaac/mistral.py).
 """
 from enum import Enum
 from typing import Optional
@@ -259,3 +267,160 @@ class ClapCaption_prompt(ClapCaptionModel):
         else:
             embedding_cat = prefix_projections
         return embedding_cat, mask
+
+
+# ----------------------------------------------------------------------------- Mistral (C5)
+MISTRAL_7B_CONFIG = dict(vocab_size=32000, hidden_size=4096, intermediate_size=14336,
+                         num_hidden_layers=32, num_attention_heads=32, num_key_value_heads=8,
+                         rms_norm_eps=1e-5, rope_theta=10000.0)
+
+
+class _ZsMistralModel(nn.Module):
+    def __init__(self, c):
+        super().__init__()
+        D, F = c["hidden_size"], c["intermediate_size"]
+        hd = D // c["num_attention_heads"]
+        kv = c["num_key_value_heads"] * hd
+        self.embed_tokens = nn.Embedding(c["vocab_size"], D)
+        self.layers = nn.ModuleList()
+        for _ in range(c["num_hidden_layers"]):
+            ly = nn.Module()
+            ly.self_attn = nn.Module()
+            for n, o in (("q_proj", D), ("k_proj", kv), ("v_proj", kv), ("o_proj", D)):
+                setattr(ly.self_attn, n, nn.Linear(D, o, bias=False))
+            ly.mlp = nn.Module()
+            ly.mlp.gate_proj = nn.Linear(D, F, bias=False)
+            ly.mlp.up_proj = nn.Linear(D, F, bias=False)
+            ly.mlp.down_proj = nn.Linear(F, D, bias=False)
+            ly.input_layernorm = nn.Module()
+            ly.input_layernorm.weight = nn.Parameter(torch.ones(D))
+            ly.post_attention_layernorm = nn.Module()
+            ly.post_attention_layernorm.weight = nn.Parameter(torch.ones(D))
+            self.layers.append(ly)
+        self.norm = nn.Module()
+        self.norm.weight = nn.Parameter(torch.ones(D))
+
+
+class ZsMistralForCausalLM(nn.Module):
+    """MistralForCausalLM's module tree / keys (``model.*``, ``lm_head``); ``generate`` with
+    inputs_embeds runs the HIP decoder (greedy only, as the reference calls it)."""
+
+    def __init__(self, config: dict):
+        super().__init__()
+        with torch.device("meta"):
+            self.model = _ZsMistralModel(config)
+            self.lm_head = nn.Linear(config["hidden_size"], config["vocab_size"], bias=False)
+        self.config = dict(config)
+        self._cache = EngineCache()
+
+    def engine(self, device, max_batch, max_prompt, max_new):
+        from zsaac.mistral import MistralDecoder, MistralWeights
+        # fp8 weights unless set_mode() / zs_mistral_mode picks "bf16" or the "f32" parity mode
+        mode = getattr(self, "zs_mistral_mode", "fp8")
+        c = self.config
+
+        def build():
+            return MistralWeights(self.state_dict(), device, mode, c["num_attention_heads"],
+                                  c["num_key_value_heads"], c.get("rms_norm_eps", 1e-5),
+                                  c.get("rope_theta", 10000.0))
+        w = self._cache.get(self, build, (mode, str(device)))
+        key = (max_batch, max_prompt, max_new)
+        decs = w.__dict__.setdefault("_decoders", {})
+        if key not in decs:
+            decs.clear()
+            decs[key] = MistralDecoder(w, max_batch, max_prompt, max_new)
+        return decs[key]
+
+    def generate(self, inputs_embeds=None, attention_mask=None, do_sample=False, max_length=60,
+                 eos_token_id=2, pad_token_id=2, **kw):
+        """Greedy generate over inputs_embeds with an all-ones mask (the only call the reference
+        makes, predict_mistralai_multilingual.py:105-111): [B, max_length - P] ids, rows that
+        finished padded with ``pad_token_id`` (HF's output)."""
+        if do_sample or kw.get("num_beams", 1) != 1:
+            raise NotImplementedError("only greedy generate (do_sample=False) is provided")
+        if attention_mask is not None and not bool((attention_mask == 1).all()):
+            raise NotImplementedError("attention_mask must be all ones (as the reference passes)")
+        require_device(inputs_embeds, "MistralForCausalLM.generate")
+        B, P, _ = inputs_embeds.shape
+        new = max(max_length - P, 0)
+        dec = self.engine(inputs_embeds.device, max(B, 32), max(P, 64), max(new, 1))
+        rows = dec.generate_embeds(inputs_embeds, max_length=max_length, eos=eos_token_id)
+        out = torch.full((B, new), pad_token_id, dtype=torch.long)
+        for b, r in enumerate(rows):
+            out[b, :len(r)] = torch.tensor(r, dtype=torch.long)
+        return out.to(inputs_embeds.device)
+
+
+class _LoraModel(nn.Module):
+    def __init__(self, lm):
+        super().__init__()
+        self.model = lm
+
+
+class _PeftModel(nn.Module):
+    """The attribute path of peft's PeftModelForCausalLM that the reference's callers use."""
+
+    def __init__(self, lm):
+        super().__init__()
+        self.base_model = _LoraModel(lm)
+
+    def generate(self, *a, **k):
+        return self.base_model.model.generate(*a, **k)
+
+
+class ClapCaption_Mistralai_prompt(nn.Module):
+
+    def __init__(self, prefix_length: int, clip_length: Optional[int] = None, prefix_size: int = 512,
+                 num_layers: int = 8, mapping_type: MappingType = 'mlp',
+                 only_prefix: Optional[bool] = False, only_soft_prompt: Optional[bool] = False,
+                 islang: Optional[int] = 0, mistral_config: Optional[dict] = None):
+        super().__init__()
+        self.prefix_length = prefix_length
+        self.only_soft_prompt = only_soft_prompt
+        self.only_prefix = only_prefix
+        self.islang = islang
+        self.LMmodel = _PeftModel(ZsMistralForCausalLM(mistral_config or MISTRAL_7B_CONFIG))
+        self.lm_embedding_size = (mistral_config or MISTRAL_7B_CONFIG)["hidden_size"]
+        if mapping_type in ('mlp', MappingType.MLP):
+            self.clap_project = MLP((prefix_size, (self.lm_embedding_size * prefix_length) // 2,
+                                     self.lm_embedding_size * prefix_length))
+        else:
+            self.clap_project = TransformerMapper(prefix_size, self.lm_embedding_size, prefix_length,
+                                                  clip_length, num_layers)
+
+    def set_mode(self, mode: str):
+        """Decoder weight storage: "fp8" (default), "bf16" or "f32" (parity mode)."""
+        self.LMmodel.base_model.model.zs_mistral_mode = mode
+        return self
+
+    def load_state_dict(self, state_dict, strict: bool = True):
+        """Reference checkpoints hold the peft tree (``LMmodel.base_model.model.*`` with
+        ``base_layer`` / ``lora_A`` / ``lora_B``): LoRA merged, the rest loaded as is."""
+        from zsaac.mistral import merge_peft_state_dict
+        lm = {k: v for k, v in state_dict.items() if k.startswith("LMmodel.")}
+        rest = {k: v for k, v in state_dict.items() if not k.startswith("LMmodel.")}
+        if any(".lora_A." in k for k in lm):
+            merged = merge_peft_state_dict(lm, prefix="LMmodel.")
+        else:
+            merged = {k[len("LMmodel.base_model.model."):]: v for k, v in lm.items()
+                      if k.startswith("LMmodel.base_model.model.")}
+        self.LMmodel.base_model.model.load_state_dict(merged, strict=strict, assign=True)
+        return self.clap_project.load_state_dict(
+            {k[len("clap_project."):]: v for k, v in rest.items() if k.startswith("clap_project.")},
+            strict=strict)
+
+    def clap_to_gpt(self, prefix: torch.Tensor, embedding_hard_prompt: torch.Tensor,
+                    embedding_text: Optional[torch.Tensor] = None, mask: Optional[torch.Tensor] = None,
+                    hard_prompts_masks: Optional[torch.Tensor] = None):
+        """caption_model.py:392-413: [hard ; clap_project(prefix) ; text]."""
+        prefix_projections = self.clap_project(prefix).view(-1, self.prefix_length, self.lm_embedding_size)
+        if not self.only_soft_prompt:
+            prefix_projections = torch.cat((embedding_hard_prompt.float(), prefix_projections), dim=1)
+            if hard_prompts_masks is not None:
+                mask = torch.cat((hard_prompts_masks, mask), dim=1)
+        if embedding_text is not None:
+            return torch.cat((prefix_projections, embedding_text.float()), dim=1), mask
+        return prefix_projections, mask
+
+    def forward(self, *a, **k):
+        raise NotImplementedError("the training forward is out of scope (inference drop-in)")

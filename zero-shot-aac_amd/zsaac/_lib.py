@@ -74,6 +74,13 @@ SIGNATURES = {
     "zs_magic_expand": [P, P, I, I, I, P, P, P],
     "zs_magic_maxcos": [P, I, I, P, I, P, P, P, I, P],
     "zs_magic_score": [P, P, P, P, I, I, I, I, I, F, F, F, P, P],
+    "zs_fp8_gemm_rows": [P, I, P, P, I, I, I, P, L, I, P],
+    "zs_fp8_splits": [I],
+    "zs_mistral_embed": [P, I, P, I, P, I, P, P, I, I, P, I, P],
+    "zs_mistral_add_rmsnorm": [P, P, I, L, I, I, F, P, P, I, P],
+    "zs_mistral_rope_kv": [P, I, L, I, I, I, P, I, P, P, P, P, P, I, I, P],
+    "zs_mistral_silu_mul": [P, I, L, I, I, P, I, P],
+    "zs_mistral_attention": [P, I, I, I, P, I, P, P, I, P, I, P],
     "zs_magic_step": [P, P, I, I, I, I, I, I, I, P, P, P, P, P, I, P, I, P, P, P, P, P, I, P],
 }
 

@@ -1,0 +1,267 @@
+"""Mistral-7B caption decoder on the HIP kernels (BASELINE.json config C5).
+
+Reference: predict_mistralai_multilingual.py:90-111 -- per batch of 32 clips and per language tag
+(``<en>``, ``<zh>``, ``<fr>``): ``prefix_embed = clap_to_gpt(prefix, embed_tokens(hard prompt),
+embed_tokens(tokenizer(tag)))`` (models/caption_model.py:392-413) then
+``LMmodel.generate(inputs_embeds=prefix_embed, attention_mask=ones, do_sample=False,
+max_length=60, eos_token_id=2, pad_token_id=2)`` -- batched greedy decoding of
+``MistralForCausalLM`` (4-bit NF4 base weights + LoRA r=8 on every projection and the LM head,
+caption_model.py:355-364).
+
+Here: the LoRA adapters are merged into the base weights at load (W + (alpha / r) B A,
+:func:`merge_peft_state_dict`), the RMSNorm weights are folded into the GEMMs that follow them,
+and the decoder weights are stored as fp8 e4m3 (OCP) with one f32 scale per output channel
+(``mode="fp8"``, the perf mode), bf16 (``"bf16"``) or f32 (``"f32"``, the parity mode: no folding,
+zs_gemm f32, ids bit-exact against HF MistralForCausalLM on the same weights).  NF4 itself is a
+bitsandbytes storage format (absent here); fp8 is the MI355X-native 8-bit format, and a checkpoint's
+NF4 tensors would be dequantised to f32 before :class:`MistralWeights` re-quantises them.
+
+One decode step for M rows (csrc/mistral.hip): per layer
+  [add + RMSNorm] -> qkv GEMM (fp8 weights, split-K slabs) -> RoPE + KV append -> GQA attention
+  -> o GEMM -> add + RMSNorm -> gate|up GEMM -> SiLU * up -> down GEMM -> (next layer's add+norm)
+then the final norm, the LM head (zs_lmhead_topk argmax) and the greedy step (eos -> done).
+The prompt (hard prompt padded to the batch's longest with id 0 and attended, as the reference's
+all-ones attention mask does; soft rows; language tag ids) is prefilled as B x P rows.
+"""
+from __future__ import annotations
+
+import math
+from typing import Dict, List, Optional, Sequence
+
+import torch
+
+from . import ops
+from ._lib import ZS_BF16, ZS_F32, call
+
+
+def merge_peft_state_dict(sd: Dict[str, torch.Tensor], lora_alpha: float = 16.0, r: int = 8,
+                          prefix: str = "") -> Dict[str, torch.Tensor]:
+    """A peft LoRA state dict (``...base_model.model.model.layers.0.self_attn.q_proj.base_layer
+    .weight`` + ``lora_A.default.weight`` [r, in] + ``lora_B.default.weight`` [out, r], the
+    ``get_peft_model`` of caption_model.py:362-364) -> plain MistralForCausalLM keys with
+    W = base + (lora_alpha / r) B @ A."""
+    out, lora = {}, {}
+    strip = prefix + "base_model.model."
+    for k, v in sd.items():
+        if not k.startswith(strip):
+            continue
+        k2 = k[len(strip):]
+        if ".lora_A." in k2 or ".lora_B." in k2:
+            base = k2.split(".lora_")[0]
+            lora.setdefault(base, {})["A" if ".lora_A." in k2 else "B"] = v.float()
+        else:
+            out[k2.replace(".base_layer.", ".")] = v
+    for base, ab in lora.items():
+        w = base + ".weight"
+        out[w] = out[w].float() + (lora_alpha / r) * (ab["B"] @ ab["A"])
+    return out
+
+
+def quantize_fp8(w: torch.Tensor):
+    """Per-output-channel (row) fp8 e4m3fn: returns (uint8 codes [N, K], f32 scales [N])."""
+    w = w.float()
+    amax = w.abs().amax(dim=1).clamp(min=1e-12)
+    scale = amax / 448.0
+    q = (w / scale[:, None]).to(torch.float8_e4m3fn)
+    return q.view(torch.uint8), scale
+
+
+def dequantize_fp8(q: torch.Tensor, scale: torch.Tensor) -> torch.Tensor:
+    return q.view(torch.float8_e4m3fn).float() * scale[:, None].float()
+
+
+class MistralWeights:
+    """Packed decoder weights from MistralForCausalLM keys (``model.*``, ``lm_head.weight``)."""
+
+    def __init__(self, sd: Dict[str, torch.Tensor], device, mode: str = "fp8", n_heads: int = 32,
+                 n_kv_heads: int = 8, eps: float = 1e-5, rope_theta: float = 10000.0,
+                 prefix: str = ""):
+        if mode not in ("fp8", "bf16", "f32"):
+            raise ValueError(mode)
+        dev = torch.device(device)
+        self.mode, self.dev = mode, dev
+        self.adt = torch.float32 if mode == "f32" else torch.bfloat16   # activation operand dtype
+        p = prefix + "model."
+        self.emb = sd[p + "embed_tokens.weight"].to(dev, self.adt).contiguous()
+        self.V, self.D = self.emb.shape
+        self.H, self.KVH, self.HD = n_heads, n_kv_heads, 128
+        if self.D != self.H * self.HD:
+            raise ValueError("Mistral kernels need head_dim 128 (hidden = heads x 128)")
+        self.eps, self.theta = eps, rope_theta
+        fold = mode != "f32"
+        self.layers = []
+        i = 0
+        while f"{p}layers.{i}.self_attn.q_proj.weight" in sd:
+            L = f"{p}layers.{i}."
+            g1 = sd[L + "input_layernorm.weight"].float()
+            g2 = sd[L + "post_attention_layernorm.weight"].float()
+            qkv = torch.cat([sd[L + f"self_attn.{n}_proj.weight"].float() for n in "qkv"])
+            gu = torch.cat([sd[L + "mlp.gate_proj.weight"].float(), sd[L + "mlp.up_proj.weight"].float()])
+            ly = {"ln1": None if fold else g1.to(dev), "ln2": None if fold else g2.to(dev),
+                  "qkv": self._pack(qkv * g1[None] if fold else qkv),
+                  "o": self._pack(sd[L + "self_attn.o_proj.weight"]),
+                  "gu": self._pack(gu * g2[None] if fold else gu),
+                  "down": self._pack(sd[L + "mlp.down_proj.weight"])}
+            self.layers.append(ly)
+            i += 1
+        self.F = self.layers[0]["gu"]["N"] // 2
+        gn = sd[p + "norm.weight"].float()
+        lm = sd[prefix + "lm_head.weight"].float()
+        self.lnf = None if fold else gn.to(dev)
+        self.lm = (lm * gn[None] if fold else lm).to(dev, self.adt).contiguous()
+
+    def _pack(self, w):
+        w = w.float()
+        N, K = w.shape
+        if self.mode == "fp8":
+            q, s = quantize_fp8(w)
+            return {"N": N, "K": K, "w8": q.to(self.dev).contiguous(), "scale": s.to(self.dev).contiguous()}
+        return {"N": N, "K": K, "w": w.to(self.dev, self.adt).contiguous()}
+
+    def nbytes(self) -> int:
+        n = 0
+        for ly in self.layers:
+            for k in ("qkv", "o", "gu", "down"):
+                t = ly[k]
+                n += t["w8"].numel() + t["scale"].numel() * 4 if "w8" in t else t["w"].numel() * t["w"].element_size()
+        return n + self.lm.numel() * self.lm.element_size()
+
+
+class MistralDecoder:
+    """Batched greedy decoding (HF generate, do_sample=False) for up to ``max_batch`` sequences
+    with prompts of up to ``max_prompt`` rows and ``max_new`` generated tokens."""
+
+    def __init__(self, w: MistralWeights, max_batch: int = 32, max_prompt: int = 64,
+                 max_new: int = 60):
+        self.w = w
+        dev, adt = w.dev, w.adt
+        self.B, self.Pmax, self.max_new = max_batch, max_prompt, max_new
+        self.Lmax = max_prompt + max_new + 1
+        Mp = max_batch * max_prompt
+        D, H, KVH, HD, F = w.D, w.H, w.KVH, w.HD, w.F
+        self.nqkv = (H + 2 * KVH) * HD
+        self.x = torch.empty(Mp, D, device=dev)
+        self.h = torch.empty(Mp, D, device=dev, dtype=adt)
+        self.q = torch.empty(Mp, H * HD, device=dev, dtype=adt)
+        self.att = torch.empty(Mp, H * HD, device=dev, dtype=adt)
+        self.act = torch.empty(Mp, F, device=dev, dtype=adt)
+        nsplit = max(self._splits(w.D), self._splits(F))
+        self.slab = torch.empty(nsplit * Mp * max(self.nqkv, 2 * F, D), device=dev)
+        self.kc = [torch.empty(max_batch, KVH, self.Lmax, HD, device=dev, dtype=adt) for _ in w.layers]
+        self.vc = [torch.empty(max_batch, KVH, self.Lmax, HD, device=dev, dtype=adt) for _ in w.layers]
+        inv = 1.0 / (w.theta ** (torch.arange(0, HD, 2, dtype=torch.int64).float() / HD))
+        fr = torch.arange(self.Lmax, dtype=torch.float32)[:, None] * inv[None]
+        self.cos = fr.cos().to(dev).contiguous()
+        self.sin = fr.sin().to(dev).contiguous()
+        i32 = dict(device=dev, dtype=torch.int32)
+        self.pos = torch.zeros(Mp, **i32)
+        self.next_tok = torch.zeros(max_batch, **i32)
+        self.done = torch.zeros(max_batch, **i32)
+        self.out_ids = torch.zeros(max_batch, max_new, **i32)
+        self.out_len = torch.zeros(max_batch, **i32)
+        self.step_ctr = torch.zeros(1, **i32)
+        self.all_done = torch.zeros(3, **i32)
+        self.nblk = ops.lmhead_nblk(w.V)
+        self.pval = torch.empty(max_batch, self.nblk, 1, device=dev)
+        self.pidx = torch.empty(max_batch, self.nblk, 1, device=dev, dtype=torch.int32)
+        self.last = torch.empty(max_batch, D, device=dev, dtype=adt)
+
+    def _splits(self, K):
+        return call("zs_fp8_splits", K) if self.w.mode == "fp8" else 1
+
+    def _gemm(self, a, lw, M):
+        """f32 result slabs of a @ W^T for M rows: (slab tensor, nsplit, split stride)."""
+        N, K = lw["N"], lw["K"]
+        if self.w.mode == "fp8":
+            ns = self._splits(K)
+            ss = M * N
+            out = self.slab[:ns * ss]
+            for m0 in range(0, M, 64):
+                mm = min(64, M - m0)
+                call("zs_fp8_gemm_rows", a[m0:].data_ptr(), a.stride(0), lw["w8"].data_ptr(),
+                     lw["scale"].data_ptr(), mm, N, K, out[m0 * N:].data_ptr(), ss, N,
+                     torch.cuda.current_stream().cuda_stream)
+            return out, ns, ss
+        out = self.slab[:M * N].view(M, N)
+        ops.gemm(a[:M], lw["w"], out, split_k=1)
+        return out, 1, M * N
+
+    def _norm(self, M, y, ns, ss, w):
+        call("zs_mistral_add_rmsnorm", self.x.data_ptr(), y.data_ptr() if y is not None else None,
+             ns, ss, M, self.w.D, float(self.w.eps), w.data_ptr() if w is not None else None,
+             self.h.data_ptr(), ops.dt(self.h), torch.cuda.current_stream().cuda_stream)
+
+    def _layers(self, M, rows_per_seq):
+        w, st = self.w, torch.cuda.current_stream().cuda_stream
+        dt = ops.dt(self.h)
+        nl = len(w.layers)
+        self._norm(M, None, 1, 0, w.layers[0]["ln1"])
+        for l, ly in enumerate(w.layers):
+            y, ns, ss = self._gemm(self.h, ly["qkv"], M)
+            call("zs_mistral_rope_kv", y.data_ptr(), ns, ss, M, w.H, w.KVH, self.pos.data_ptr(),
+                 rows_per_seq, self.cos.data_ptr(), self.sin.data_ptr(), self.q.data_ptr(),
+                 self.kc[l].data_ptr(), self.vc[l].data_ptr(), self.Lmax, dt, st)
+            call("zs_mistral_attention", self.q.data_ptr(), M, w.H, w.KVH, self.pos.data_ptr(),
+                 rows_per_seq, self.kc[l].data_ptr(), self.vc[l].data_ptr(), self.Lmax,
+                 self.att.data_ptr(), dt, st)
+            y, ns, ss = self._gemm(self.att, ly["o"], M)
+            self._norm(M, y, ns, ss, ly["ln2"])
+            y, ns, ss = self._gemm(self.h, ly["gu"], M)
+            call("zs_mistral_silu_mul", y.data_ptr(), ns, ss, M, w.F, self.act.data_ptr(), dt, st)
+            y, ns, ss = self._gemm(self.act, ly["down"], M)
+            self._norm(M, y, ns, ss, w.layers[l + 1]["ln1"] if l + 1 < nl else w.lnf)
+
+    def _lm_argmax(self, a, B):
+        ops.lmhead_topk(a, self.w.lm, 1, None, self.pval, self.pidx, M=B)
+
+    def generate(self, hard_ids: torch.Tensor, soft: torch.Tensor, tail_ids: torch.Tensor,
+                 max_length: int = 60, eos: int = 2) -> List[List[int]]:
+        """hard_ids [B, H] int32 (padded with 0 like padding_captions), soft [B, ns, D] f32 (the
+        mapper rows), tail_ids [nt] int32 (the language tag's token ids) -> per sequence the
+        generated ids up to and including eos (HF generate with inputs_embeds: at most
+        max_length - P new tokens, finished rows padded, special tokens dropped by the caller)."""
+        w, st = self.w, torch.cuda.current_stream().cuda_stream
+        B, H = hard_ids.shape
+        ns, nt = soft.shape[1], tail_ids.numel()
+        P = H + ns + nt
+        new = max_length - P
+        if B > self.B or P > self.Pmax or new > self.max_new:
+            raise ValueError(f"mistral generate: B={B} P={P} new={new} exceeds the engine")
+        if new <= 0:
+            return [[] for _ in range(B)]
+        M = B * P
+        call("zs_mistral_embed", hard_ids.data_ptr(), H, soft.data_ptr(), ns, tail_ids.data_ptr(),
+             nt, None, w.emb.data_ptr(), w.D, M, self.x.data_ptr(), ops.dt(w.emb), st)
+        self.pos[:M].copy_(torch.arange(P, device=w.dev, dtype=torch.int32).repeat(B))
+        self._layers(M, P)
+        self.last[:B].copy_(self.h[:M].view(B, P, w.D)[:, P - 1])
+        self._lm_argmax(self.last[:B], B)
+        for t in (self.done, self.out_len, self.step_ctr, self.all_done, self.out_ids):
+            t.zero_()
+        self.pos[:B].fill_(P - 1)
+        # max_steps = the row stride of out_ids (the loop below stops after `new` steps)
+        ops.greedy_step(self.pval, self.pidx, B, self.nblk, self.step_ctr, self.max_new, eos, eos,
+                        self.out_ids, self.out_len, self.done, self.pos, self.next_tok, self.all_done)
+        for s in range(1, new):
+            if s % 8 == 0 and int(self.all_done[0]):
+                break
+            call("zs_mistral_embed", None, 0, None, 0, None, 0, self.next_tok.data_ptr(),
+                 w.emb.data_ptr(), w.D, B, self.x.data_ptr(), ops.dt(w.emb), st)
+            self._layers(B, 1)
+            self._lm_argmax(self.h[:B], B)
+            ops.greedy_step(self.pval, self.pidx, B, self.nblk, self.step_ctr, self.max_new, eos,
+                            eos, self.out_ids, self.out_len, self.done, self.pos, self.next_tok,
+                            self.all_done)
+        ids, ln = self.out_ids[:B].cpu(), self.out_len[:B].cpu()
+        return [ids[b, :int(ln[b])].tolist() for b in range(B)]
+
+    def generate_embeds(self, embeds: torch.Tensor, max_length: int = 60,
+                        eos: int = 2) -> List[List[int]]:
+        """HF ``generate(inputs_embeds=embeds, attention_mask=ones, do_sample=False, ...)`` from
+        already assembled prompt rows [B, P, D] (the drop-in's entry point)."""
+        B = embeds.shape[0]
+        dev = self.w.dev
+        empty = torch.zeros(B, 0, dtype=torch.int32, device=dev)
+        return self.generate(empty, embeds.float().contiguous(), torch.zeros(0, dtype=torch.int32,
+                                                                              device=dev),
+                             max_length=max_length, eos=eos)

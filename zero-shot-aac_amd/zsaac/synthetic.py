@@ -362,3 +362,49 @@ def bert_state_dict(seed: int = 13, vocab: int = None, layers: int = 12,
     _linear(sd, g, proj_prefix + "2", embed_size, embed_size)
     sd["temp"] = torch.tensor(float(temp))
     return sd
+
+
+# ----------------------------------------------------------------------------------- Mistral (C5)
+
+MISTRAL_7B = dict(vocab=32000, hidden=4096, heads=32, kv_heads=8, ffn=14336, layers=32)
+MISTRAL_TINY = dict(vocab=32000, hidden=1024, heads=8, kv_heads=2, ffn=3072, layers=2)
+
+
+def _fp8_exact(w):
+    """Round a weight to what per-row fp8 e4m3 (scale amax / 448) represents exactly, so the fp8
+    engine and an f32 reference hold the same values."""
+    amax = w.abs().amax(dim=1).clamp(min=1e-12)
+    s = amax / 448.0
+    return (w / s[:, None]).to(torch.float8_e4m3fn).float() * s[:, None]
+
+
+def mistral_state_dict(seed: int = 21, cfg: dict = None, eos_boost: float = 1.5,
+                       fp8_exact: bool = True):
+    """MistralForCausalLM keys (``model.embed_tokens``, ``model.layers.*``, ``model.norm``,
+    ``lm_head``) at ``cfg`` (default: the tiny test geometry); projection weights rounded to fp8
+    values unless ``fp8_exact`` is False; ``eos_boost`` scales lm_head row 2 (eos) so that some
+    captions end."""
+    c = dict(MISTRAL_TINY if cfg is None else cfg)
+    g = _gen(seed)
+    D, F, H, KVH, V = c["hidden"], c["ffn"], c["heads"], c["kv_heads"], c["vocab"]
+    hd = D // H
+    sd = OrderedDict()
+    rnd = (lambda o, i, gain=1.0: _fp8_exact(_randn(g, (o, i), gain / math.sqrt(i)))) if fp8_exact \
+        else (lambda o, i, gain=1.0: _randn(g, (o, i), gain / math.sqrt(i)))
+    sd["model.embed_tokens.weight"] = _randn(g, (V, D), 1.0)
+    for i in range(c["layers"]):
+        L = f"model.layers.{i}."
+        sd[L + "input_layernorm.weight"] = 1.0 + _randn(g, (D,), 0.1)
+        sd[L + "self_attn.q_proj.weight"] = rnd(H * hd, D, 2.0)
+        sd[L + "self_attn.k_proj.weight"] = rnd(KVH * hd, D, 2.0)
+        sd[L + "self_attn.v_proj.weight"] = rnd(KVH * hd, D)
+        sd[L + "self_attn.o_proj.weight"] = rnd(D, H * hd)
+        sd[L + "post_attention_layernorm.weight"] = 1.0 + _randn(g, (D,), 0.1)
+        sd[L + "mlp.gate_proj.weight"] = rnd(F, D, 1.5)
+        sd[L + "mlp.up_proj.weight"] = rnd(F, D)
+        sd[L + "mlp.down_proj.weight"] = rnd(D, F)
+    sd["model.norm.weight"] = 1.0 + _randn(g, (D,), 0.1)
+    lm = _randn(g, (V, D), 4.0 / math.sqrt(D))
+    lm[2] *= eos_boost
+    sd["lm_head.weight"] = lm
+    return sd
