@@ -119,6 +119,10 @@ def parse():
                          "entry 20, predict_prompt.py --magic) on bs=64 batches: a labelled "
                          "secondary line, not the metric")
     ap.add_argument("--magic-bert-layers", type=int, default=12)
+    ap.add_argument("--mistral", action="store_true",
+                    help="C5: wav -> HTSAT -> prompt + MLP mapper -> Mistral-7B (fp8 weights) "
+                         "greedy generate for the en / zh / fr tags, bs=32 (a labelled "
+                         "secondary line, not the metric)")
     ap.add_argument("--embeddings-only", action="store_true",
                     help="C4: batched HTSAT/CNN14 encode_audio + one RCCL all-gather of the "
                          "[N,1024] embeddings (no caption decode)")
@@ -603,6 +607,91 @@ def main_magic(args, device):
         flush=True)
 
 
+def main_mistral(args, device):
+    """C5 (predict_mistralai_multilingual.py:90-111): per batch of 32 clips, HTSAT encode ->
+    hard prompt (Mistral ids, padded to the batch's longest) -> MLP mapper (1024 -> 20480 ->
+    40960) -> for each language tag a batched greedy generate(max_length 60, eos 2) on a
+    Mistral-7B geometry decoder (32 layers, 4096, GQA 32/8, FFN 14336) with fp8 e4m3 weights.
+    Roofline: one decode step's bytes (fp8 weights + scales + bf16 LM head) / its time."""
+    from zsaac import ops, synthetic as S
+    from zsaac.decoder import MlpMapper
+    from zsaac.encoder import AudioEncoder
+    from zsaac.mistral import MistralDecoder, MistralWeights
+    B = 32
+    dt = torch.bfloat16
+    asd = S.htsat_state_dict(3)
+    asd.update(S.audio_proj_state_dict(5, audio_width=768))
+    enc = AudioEncoder(asd, "htsat", dt, B, device)
+    w = MistralWeights.synthetic(device, S.MISTRAL_7B, seed=1)
+    log(f"mistral-7B fp8 weights: {w.nbytes() / 1e9:.2f} GB on the device")
+    g = torch.Generator(device=device).manual_seed(2)
+    D = 4096
+    msd = {"clap_project.model.0.weight": torch.randn(D * 5, 1024, device=device, generator=g) / 32,
+           "clap_project.model.0.bias": torch.zeros(D * 5, device=device),
+           "clap_project.model.2.weight": torch.randn(D * 10, D * 5, device=device, generator=g) / (D * 5) ** 0.5,
+           "clap_project.model.2.bias": torch.zeros(D * 10, device=device)}
+    mapper = MlpMapper(msd, device, dt, B)
+    del msd
+    labels = S.label_table().to(device)
+    lt = torch.randint(3, 32000, (527, 3), generator=torch.Generator().manual_seed(3)).to(torch.int32)
+    label_tok, label_len = lt.to(device), torch.full((527,), 3, dtype=torch.int32, device=device)
+    Hc = 2 + 3 * 3 + 2 + 4
+    hard_ids = torch.zeros(B, Hc, dtype=torch.int32, device=device)
+    hard_len = torch.zeros(B, dtype=torch.int32, device=device)
+    tags = {"en": [1, 523, 269, 28767], "zh": [1, 523, 26715, 28767], "fr": [1, 523, 1642, 28767]}
+    tags = {k: torch.tensor(v, dtype=torch.int32, device=device) for k, v in tags.items()}
+    dec = MistralDecoder(w, max_batch=B, max_prompt=Hc + 10 + 4, max_new=60)
+    n = args.steps or 2
+    wav = synthetic_clips(B, 0, device)
+
+    def one():
+        emb = enc.encode(wav)
+        ops.prompt_assemble(emb, labels, 3, label_tok, label_len, hard_ids, hard_len)
+        H = int(hard_len.max())          # padding_captions pads to the batch's longest
+        soft = mapper(ops.l2norm(emb)).view(B, 10, D).float().contiguous()
+        hard = hard_ids[:, :H].contiguous()
+        return [dec.generate(hard, soft, tags[t], max_length=60) for t in ("en", "zh", "fr")]
+    for _ in range(max(1, args.warmup)):
+        one()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    ntok = 0
+    for _ in range(n):
+        res = one()
+        ntok += sum(len(r) for lang in res for r in lang)
+    torch.cuda.synchronize()
+    dt_s = time.perf_counter() - t0
+    # decode-step roofline: one 32-row step (M = 32, rows_per_seq 1) timed with HIP events
+    dec.next_tok.zero_()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    reps = 10
+    dec.pos[:B].fill_(30)
+    e0.record()
+    for _ in range(reps):
+        dec._layers(B, 1)
+        dec._lm_argmax(dec.h[:B], B)
+    e1.record()
+    e1.synchronize()
+    step_s = e0.elapsed_time(e1) / 1e3 / reps
+    byts = w.nbytes()
+    print(json.dumps({
+        "metric": "audio clips/sec, Mistral-7B caption decoder (en+zh+fr greedy generate), bs=32",
+        "value": round(n * B / dt_s, 3), "unit": "clips/s", "n_gpus": 1, "steps": n,
+        "warmup": args.warmup, "ms_per_step": round(dt_s / n * 1e3, 1), "higher_is_better": True,
+        "dtype": "fp8 weights (e4m3, per-channel scale) x bf16 activations, f32 accumulation",
+        "data": DATA + "; Mistral-7B geometry, synthetic fp8 weights",
+        "config": {"workload": "C5: wav -> HTSAT -> prompt + MLP mapper (1024->20480->40960) -> "
+                               "Mistral-7B greedy generate(max_length 60, eos 2) x 3 language tags",
+                   "batch": B, "generated_tokens": ntok},
+        "roofline": {"kernel": "one Mistral-7B decode step at 32 rows (32 layers: fp8 GEMMs + "
+                               "RoPE/attention/norms, bf16 LM head argmax)", "bound": "hbm",
+                     "achieved": round(byts / step_s / 1e9, 1), "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": round(byts / step_s / 1e9 / HBM_PEAK_GBS, 4),
+                     "step_us": round(step_s * 1e6, 1), "algo_bytes_per_step": int(byts)},
+        "note": "secondary config C5 (predict_mistralai_multilingual.py); not the headline metric"}),
+        flush=True)
+
+
 def main():
     args = parse()
     world, rank, local = dist_setup(args)
@@ -611,6 +700,8 @@ def main():
     pipe, csd, asd = build(args, device)
     if args.magic:
         return main_magic(args, torch.device("cuda", 0))
+    if args.mistral:
+        return main_mistral(args, torch.device("cuda", 0))
     if args.embeddings_only:
         return main_embeddings(args, world, rank, device, pipe)
     B = pipe.cfg.batch

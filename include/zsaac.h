@@ -259,7 +259,8 @@ int zs_magic_step(const float* score, const int* cand, int C, int b, int W, int 
 
 /* zs_fp8_gemm_rows: weight-only fp8 GEMM for M <= 64 rows (decode): out[s][m][n] = scale[n] *
  * sum_{k in split s} A[m][k] W8[n][k]; A bf16 [M][lda], W8 fp8 e4m3 (OCP) codes [N][K], scale f32
- * [N] (one per output channel), splits of 1024 along K (zs_fp8_splits(K) of them), ldo >= N.
+ * [N] (one per output channel), K % 1024 == 0, splits of 1024 along K (zs_fp8_splits(K) of
+ * them), ldo >= N.
  * Replaces the NF4-quantised q/k/v/o/gate/up/down projections of the LoRA-wrapped Mistral
  * (caption_model.py:355-364). */
 int zs_fp8_gemm_rows(const void* A, int lda, const void* W8, const float* scale, int M, int N,

@@ -657,10 +657,9 @@ __global__ __launch_bounds__(256) void decode_attn6_kernel(
   // wave-uniform (one (row, head) per wave): scalar branches for the phase loop and prefetch
   const int p = __builtin_amdgcn_readfirstlane(min(cpos ? p0 : pos[r], Lmax - 1));
   const long rh = ((long)r * heads + h) * Lmax;
-  if (grp == 0) {
-    *reinterpret_cast<uint4*>(kc + (rh + p) * HD + sub * EPC) = knu;
-    *reinterpret_cast<uint4*>(vc + (rh + p) * HD + sub * EPC) = vnu;
-  }
+  // the new token's K/V are stored at the END: the phases never read slot p (they take the new
+  // token from registers), and a store here would order every cache load after it -- the qkv
+  // load, the store and the cache loads became three dependent round trips instead of two
   float q[EPC];
   bf8_unpack(qu, q);
 #pragma unroll
@@ -761,6 +760,8 @@ __global__ __launch_bounds__(256) void decode_attn6_kernel(
 #pragma unroll
     for (int t = 0; t < EPC; ++t) of[t] = o[t] * inv;
     *reinterpret_cast<uint4*>(out + (long)c * D + h * HD + sub * EPC) = bf8_pack(of);
+    *reinterpret_cast<uint4*>(kc + (rh + p) * HD + sub * EPC) = knu;
+    *reinterpret_cast<uint4*>(vc + (rh + p) * HD + sub * EPC) = vnu;
   }
 }
 

@@ -21,64 +21,87 @@ namespace zs {
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8m_t;
 typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2m_t;
 typedef __attribute__((ext_vector_type(4))) float f32x4m_t;
+typedef __attribute__((ext_vector_type(4))) unsigned u32x4m_t;
 
-constexpr int F8_NT = 64;     // columns per workgroup (4 waves x 16)
+int g_fp8_tile = 0;   // zs_tune_set("fp8_tile", 1): 64-column tiles only (A/B knob)
+
 constexpr int F8_KC = 1024;   // k per workgroup (one split)
 constexpr int F8_MAXM = 64;
 
 // out[split][m][n] = scale[n] * sum_{k in split} A[m][k] * W8[n][k]   (M <= 64)
-// Lane l of a wave covers column n = l & 15 of the wave's 16; in each 64-deep k block lane group
-// g = l >> 4 loads the 16 consecutive fp8 at k = 64 j + 16 g (one 16-byte load) and feeds them as
-// two MFMA k-slices of 8; A is read from LDS with the same k assignment, so the products pair up
-// (the sum runs over a permuted k order).
-__global__ __launch_bounds__(256) void fp8_gemm_rows_kernel(const bf16_t* __restrict__ A, int lda,
-                                                            const uint8_t* __restrict__ W8,
-                                                            const float* __restrict__ scale, int M,
-                                                            int N, int K, float* __restrict__ out,
-                                                            long split_stride, int ldo) {
+// A workgroup of WAVES waves covers NT = 16 NB WAVES columns x one 1024-deep k split: lane l of a
+// wave covers column n = l & 15 of each of its NB 16-column blocks; in each 64-deep k block lane
+// group g = l >> 4 loads the 16 consecutive fp8 at k = 64 j + 16 g (one 16-byte load) and feeds
+// them as two MFMA k-slices of 8; A is staged once per workgroup in LDS and read with the same k
+// assignment, so the products pair up (the sum runs over a permuted k order).  Bytes per
+// workgroup: NT x 1024 weight + M x 1024 x 2 activation, so wide tiles (NT = 256 for gate|up)
+// keep the activation re-reads at a quarter of the weight stream.
+template <int NB, int WAVES>
+__global__ __launch_bounds__(64 * WAVES) void fp8_gemm_rows_kernel(
+    const bf16_t* __restrict__ A, int lda, const uint8_t* __restrict__ W8,
+    const float* __restrict__ scale, int M, int N, int K, float* __restrict__ out,
+    long split_stride, int ldo) {
+  constexpr int NT = 16 * NB * WAVES, NTHR = 64 * WAVES;
+  constexpr int JB = F8_KC / 64;                    // 64-deep k blocks per split
   extern __shared__ __attribute__((aligned(16))) char smem[];
   bf16_t* as = reinterpret_cast<bf16_t*>(smem);      // [M][F8_KC + 8]
   constexpr int LDA_S = F8_KC + 8;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int n0 = blockIdx.x * F8_NT + wid * 16;
+  const int n0 = blockIdx.x * NT + wid * 16 * NB;
   const int split = blockIdx.y, k0 = split * F8_KC;
-  const int kc = min(F8_KC, K - k0);                 // multiple of 64
+  constexpr int kc = F8_KC;     // K % 1024 == 0: every load unconditional (a runtime bound put
+                                // each weight load in its own branch, waited for there)
   const int fr = lane & 15, g = lane >> 4;
-  // weight loads first (independent of A): kc / 64 blocks of 16 bytes per lane
-  const int nrow = min(n0 + fr, N - 1);
-  const uint8_t* wr = W8 + (long)nrow * K + k0 + 16 * g;
-  uint4 wv[F8_KC / 64];
+  // the activation chunk's loads are issued FIRST (into registers), the weight stream after
+  // them: loads return in order, so the LDS stores below wait only for the A loads while the
+  // weight loads stay in flight (issued the other way round, every A load waited behind the
+  // whole weight stream and the A copy became a chain of round trips)
+  const int per_row = kc / 8;                        // 16-byte pieces per A row
+  constexpr int AMAX = F8_MAXM * (F8_KC / 8) / NTHR; // pieces per thread at M = 64
+  uint4 av[AMAX];
 #pragma unroll
-  for (int j = 0; j < F8_KC / 64; ++j)
-    if (64 * j < kc) wv[j] = *reinterpret_cast<const uint4*>(wr + 64 * j);
-  // A chunk -> LDS (16 bytes per thread per step)
-  const int per_row = kc / 8;
-  for (int i = threadIdx.x; i < M * per_row; i += 256) {
-    const int m = i / per_row, c = (i % per_row) * 8;
-    *reinterpret_cast<uint4*>(as + m * LDA_S + c) =
-        *reinterpret_cast<const uint4*>(A + (long)m * lda + k0 + c);
+  for (int t = 0; t < AMAX; ++t) {
+    const int i = threadIdx.x + t * NTHR;
+    const int m = min(i / per_row, M - 1), c = (i % per_row) * 8;
+    av[t] = *reinterpret_cast<const uint4*>(A + (long)m * lda + k0 + c);
+  }
+  u32x4m_t wv[NB][JB];   // weights are read once per decode step: non-temporal loads
+#pragma unroll
+  for (int nb = 0; nb < NB; ++nb) {
+    const uint8_t* wr = W8 + (long)min(n0 + 16 * nb + fr, N - 1) * K + k0 + 16 * g;
+#pragma unroll
+    for (int j = 0; j < JB; ++j)
+      wv[nb][j] = __builtin_nontemporal_load(reinterpret_cast<const u32x4m_t*>(wr + 64 * j));
+  }
+#pragma unroll
+  for (int t = 0; t < AMAX; ++t) {
+    const int i = threadIdx.x + t * NTHR;
+    if (i < M * per_row)
+      *reinterpret_cast<uint4*>(as + (i / per_row) * LDA_S + (i % per_row) * 8) = av[t];
   }
   __syncthreads();
   const int nrb = (M + 15) / 16;
-  f32x4m_t acc[F8_MAXM / 16];
+  f32x4m_t acc[NB][F8_MAXM / 16];
 #pragma unroll
-  for (int rb = 0; rb < F8_MAXM / 16; ++rb) acc[rb] = f32x4m_t{0.f, 0.f, 0.f, 0.f};
+  for (int nb = 0; nb < NB; ++nb)
 #pragma unroll
-  for (int j = 0; j < F8_KC / 64; ++j) {
-    if (64 * j >= kc) break;
-    const uint4 w = wv[j];
-    bf16x8m_t b0, b1;
-    {
+    for (int rb = 0; rb < F8_MAXM / 16; ++rb) acc[nb][rb] = f32x4m_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int j = 0; j < JB; ++j) {
+    bf16x8m_t b0[NB], b1[NB];
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb) {
+      const u32x4m_t w = wv[nb][j];
       const bf16x2m_t p0 = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(w.x, 1.0f, false);
       const bf16x2m_t p1 = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(w.x, 1.0f, true);
       const bf16x2m_t p2 = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(w.y, 1.0f, false);
       const bf16x2m_t p3 = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(w.y, 1.0f, true);
-      b0 = bf16x8m_t{p0[0], p0[1], p1[0], p1[1], p2[0], p2[1], p3[0], p3[1]};
+      b0[nb] = bf16x8m_t{p0[0], p0[1], p1[0], p1[1], p2[0], p2[1], p3[0], p3[1]};
       const bf16x2m_t q0 = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(w.z, 1.0f, false);
       const bf16x2m_t q1 = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(w.z, 1.0f, true);
       const bf16x2m_t q2 = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(w.w, 1.0f, false);
       const bf16x2m_t q3 = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(w.w, 1.0f, true);
-      b1 = bf16x8m_t{q0[0], q0[1], q1[0], q1[1], q2[0], q2[1], q3[0], q3[1]};
+      b1[nb] = bf16x8m_t{q0[0], q0[1], q1[0], q1[1], q2[0], q2[1], q3[0], q3[1]};
     }
     const int ka = 64 * j + 16 * g;
 #pragma unroll
@@ -87,22 +110,28 @@ __global__ __launch_bounds__(256) void fp8_gemm_rows_kernel(const bf16_t* __rest
       const int m = min(rb * 16 + fr, M - 1);
       const bf16x8m_t a0 = *reinterpret_cast<const bf16x8m_t*>(as + m * LDA_S + ka);
       const bf16x8m_t a1 = *reinterpret_cast<const bf16x8m_t*>(as + m * LDA_S + ka + 8);
-      acc[rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, b0, acc[rb], 0, 0, 0);
-      acc[rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, b1, acc[rb], 0, 0, 0);
+#pragma unroll
+      for (int nb = 0; nb < NB; ++nb) {
+        acc[nb][rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, b0[nb], acc[nb][rb], 0, 0, 0);
+        acc[nb][rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, b1[nb], acc[nb][rb], 0, 0, 0);
+      }
     }
   }
-  // C layout: lane -> column n0 + (lane & 15), rows 16 rb + 4 (lane >> 4) + i
-  const int n = n0 + fr;
-  if (n >= N) return;
-  const float s = scale[n];
+  // C layout: lane -> column (lane & 15) of each block, rows 16 rb + 4 (lane >> 4) + i
   float* o = out + split * split_stride;
 #pragma unroll
-  for (int rb = 0; rb < F8_MAXM / 16; ++rb) {
-    if (rb >= nrb) break;
+  for (int nb = 0; nb < NB; ++nb) {
+    const int n = n0 + 16 * nb + fr;
+    if (n >= N) continue;
+    const float s = scale[n];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int m = rb * 16 + 4 * g + i;
-      if (m < M) o[(long)m * ldo + n] = acc[rb][i] * s;
+    for (int rb = 0; rb < F8_MAXM / 16; ++rb) {
+      if (rb >= nrb) break;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int m = rb * 16 + 4 * g + i;
+        if (m < M) o[(long)m * ldo + n] = acc[nb][rb][i] * s;
+      }
     }
   }
 }
@@ -115,26 +144,53 @@ __device__ __forceinline__ float slab_sum(const float* __restrict__ p, int nspli
 }
 
 // x[m] += sum_s y[s][m]  (skipped when y == nullptr), then h[m] = w * (x[m] * rsqrt(mean(x^2) +
-// eps)) (MistralRMSNorm; w == nullptr: the weight is folded into the next GEMM), one block per row
+// eps)) (MistralRMSNorm; w == nullptr: the weight is folded into the next GEMM).  One 1024-thread
+// block per row, 4 columns per thread per pass (D <= 4096 in one pass), every split's load issued
+// before the adds (a row's slabs are one memory round trip, not one per split).
+__device__ __forceinline__ float4 slab_sum4(const float* __restrict__ p, int nsplit, long ss) {
+  float4 v = *reinterpret_cast<const float4*>(p);
+  int s = 1;
+  for (; s + 3 < nsplit; s += 4) {
+    const float4 a = *reinterpret_cast<const float4*>(p + s * ss);
+    const float4 b = *reinterpret_cast<const float4*>(p + (s + 1) * ss);
+    const float4 c = *reinterpret_cast<const float4*>(p + (s + 2) * ss);
+    const float4 d = *reinterpret_cast<const float4*>(p + (s + 3) * ss);
+    v.x += a.x; v.y += a.y; v.z += a.z; v.w += a.w;
+    v.x += b.x; v.y += b.y; v.z += b.z; v.w += b.w;
+    v.x += c.x; v.y += c.y; v.z += c.z; v.w += c.w;
+    v.x += d.x; v.y += d.y; v.z += d.z; v.w += d.w;
+  }
+  for (; s < nsplit; ++s) {
+    const float4 a = *reinterpret_cast<const float4*>(p + s * ss);
+    v.x += a.x; v.y += a.y; v.z += a.z; v.w += a.w;
+  }
+  return v;
+}
+
 template <typename T>
-__global__ __launch_bounds__(256) void mistral_add_rmsnorm_kernel(
+__global__ __launch_bounds__(1024) void mistral_add_rmsnorm_kernel(
     float* __restrict__ x, const float* __restrict__ y, int nsplit, long ss, int D, float eps,
     const float* __restrict__ w, T* __restrict__ h) {
-  __shared__ float red[4];
+  __shared__ float red[16];
   const int m = blockIdx.x;
   float* xr = x + (long)m * D;
   float q = 0.f;
-  for (int c = threadIdx.x; c < D; c += 256) {
-    float v = xr[c];
+  for (int c = 4 * threadIdx.x; c < D; c += 4 * 1024) {
+    float4 v = *reinterpret_cast<const float4*>(xr + c);
     if (y) {
-      v += slab_sum(y + (long)m * D + c, nsplit, ss);
-      xr[c] = v;
+      const float4 a = slab_sum4(y + (long)m * D + c, nsplit, ss);
+      v.x += a.x; v.y += a.y; v.z += a.z; v.w += a.w;
+      *reinterpret_cast<float4*>(xr + c) = v;
     }
-    q += v * v;
+    q += (v.x * v.x + v.y * v.y) + (v.z * v.z + v.w * v.w);
   }
   const float r = rsqrtf(block_sum(q, red) / D + eps);
-  for (int c = threadIdx.x; c < D; c += 256)
-    stf(h + (long)m * D + c, w ? w[c] * (xr[c] * r) : xr[c] * r);
+  for (int c = 4 * threadIdx.x; c < D; c += 4 * 1024) {
+    const float4 v = *reinterpret_cast<const float4*>(xr + c);
+    const float o[4] = {v.x * r, v.y * r, v.z * r, v.w * r};
+#pragma unroll
+    for (int t = 0; t < 4; ++t) stf(h + (long)m * D + c + t, w ? w[c + t] * o[t] : o[t]);
+  }
 }
 
 // prefill input rows (predict_mistralai_multilingual.py:97-107 clap_to_gpt): row b*P + i is
@@ -194,21 +250,27 @@ __global__ __launch_bounds__(128) void mistral_rope_kv_kernel(
   }
 }
 
-// act[m][f] = silu(gate) * up from the gate|up slabs [split][M][2F] (T out)
+// act[m][f] = silu(gate) * up from the gate|up slabs [split][M][2F] (T out), 4 columns per thread
 template <typename T>
 __global__ __launch_bounds__(256) void mistral_silu_mul_kernel(const float* __restrict__ gu,
                                                                int nsplit, long ss, int M, int F,
                                                                T* __restrict__ act) {
-  const long idx = (long)blockIdx.x * 256 + threadIdx.x;
+  const long idx = 4 * ((long)blockIdx.x * 256 + threadIdx.x);
   if (idx >= (long)M * F) return;
   const int m = idx / F, f = idx % F;
-  const float gt = slab_sum(gu + (long)m * 2 * F + f, nsplit, ss);
-  const float up = slab_sum(gu + (long)m * 2 * F + F + f, nsplit, ss);
-  stf(act + idx, gt / (1.0f + expf(-gt)) * up);     // F.silu(gate) * up
+  const float4 gt = slab_sum4(gu + (long)m * 2 * F + f, nsplit, ss);
+  const float4 up = slab_sum4(gu + (long)m * 2 * F + F + f, nsplit, ss);
+  const float g4[4] = {gt.x, gt.y, gt.z, gt.w}, u4[4] = {up.x, up.y, up.z, up.w};
+#pragma unroll
+  for (int t = 0; t < 4; ++t) stf(act + idx + t, g4[t] / (1.0f + expf(-g4[t])) * u4[t]);   // F.silu * up
 }
 
 // causal GQA attention, one wave per (query row m, q head h): keys 0..pos[m] of the sequence
-// m / rows_per_seq from kv head h / (H / KVH); softmax(q k^T / sqrt(128)) v, f32 math
+// m / rows_per_seq from kv head h / (H / KVH); softmax((q k^T) / sqrt(128)) v, f32 math.
+// Lane = (key group grp = lane >> 3, 16-dim slice sub = lane & 7): a wave step scores 8 keys
+// (3-shuffle group reductions), 4 steps (32 keys) of K / V loads are issued together, keys past
+// pos read a valid row and are masked by value; an online softmax carries across steps and the
+// 8 groups' partial outputs are combined at the end.
 template <typename T>
 __global__ __launch_bounds__(256) void mistral_attn_kernel(const T* __restrict__ q, int M, int H,
                                                            int KVH, const int* __restrict__ pos,
@@ -216,34 +278,67 @@ __global__ __launch_bounds__(256) void mistral_attn_kernel(const T* __restrict__
                                                            const T* __restrict__ kc,
                                                            const T* __restrict__ vc, int Lmax,
                                                            T* __restrict__ out) {
-  constexpr int HD = 128;
+  constexpr int HD = 128, DPL = 16, U = 4;
   const int lane = threadIdx.x & 63;
   const int w = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (w >= M * H) return;
+  const int grp = lane >> 3, sub = lane & 7;
   const int m = w / H, h = w % H, kvh = h / (H / KVH), seq = m / rows_per_seq;
-  const int p = pos[m];
-  const T* qr = q + (long)m * H * HD + h * HD;
+  const int p = __builtin_amdgcn_readfirstlane(pos[m]);
+  const T* qr = q + (long)m * H * HD + h * HD + sub * DPL;
+  float qv[DPL];
+#pragma unroll
+  for (int d = 0; d < DPL; ++d) qv[d] = ldf(qr + d);
   const float scale = 0.08838834764831845f;                      // 128^-0.5 (HF: (q k^T) * s)
-  const float q0 = ldf(qr + lane), q1 = ldf(qr + lane + 64);
   const long base = ((long)seq * KVH + kvh) * Lmax;
-  float mx = -INFINITY, l = 0.f, o0 = 0.f, o1 = 0.f;
-  for (int j = 0; j <= p; ++j) {
-    const T* kr = kc + (base + j) * HD;
-    const float s = wave_sum(q0 * ldf(kr + lane) + q1 * ldf(kr + lane + 64)) * scale;
-    const float mn = fmaxf(mx, s);
-    float corr, e;
-    if constexpr (sizeof(T) == 4) { corr = expf(mx - mn); e = expf(s - mn); }   // parity mode
-    else { corr = __expf(mx - mn); e = __expf(s - mn); }
-    const T* vr = vc + (base + j) * HD;
-    l = l * corr + e;
-    o0 = o0 * corr + e * ldf(vr + lane);
-    o1 = o1 * corr + e * ldf(vr + lane + 64);
-    mx = mn;
+  float mx = -INFINITY, l = 0.f, o[DPL];
+#pragma unroll
+  for (int d = 0; d < DPL; ++d) o[d] = 0.f;
+  for (int j0 = 0; j0 <= p; j0 += 8 * U) {
+    float kf[U][DPL], vf[U][DPL];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int j = min(j0 + 8 * u + grp, p);
+      const T* kr = kc + (base + j) * HD + sub * DPL;
+      const T* vr = vc + (base + j) * HD + sub * DPL;
+#pragma unroll
+      for (int d = 0; d < DPL; ++d) { kf[u][d] = ldf(kr + d); vf[u][d] = ldf(vr + d); }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      float sv = 0.f;
+#pragma unroll
+      for (int d = 0; d < DPL; ++d) sv += qv[d] * kf[u][d];
+      sv += __shfl_xor(sv, 1, 64);
+      sv += __shfl_xor(sv, 2, 64);
+      sv += __shfl_xor(sv, 4, 64);
+      sv = (j0 + 8 * u + grp <= p) ? sv * scale : -INFINITY;
+      float pm = fmaxf(sv, __shfl_xor(sv, 8, 64));
+      pm = fmaxf(pm, __shfl_xor(pm, 16, 64));
+      pm = fmaxf(pm, __shfl_xor(pm, 32, 64));
+      const float mn = fmaxf(mx, pm);
+      float corr, e;
+      if constexpr (sizeof(T) == 4) { corr = expf(mx - mn); e = expf(sv - mn); }   // parity mode
+      else { corr = __expf(mx - mn); e = __expf(sv - mn); }
+      l = l * corr + e;
+#pragma unroll
+      for (int d = 0; d < DPL; ++d) o[d] = o[d] * corr + e * vf[u][d];
+      mx = mn;
+    }
   }
-  const float inv = 1.0f / l;
-  T* orow = out + (long)m * H * HD + h * HD;
-  stf(orow + lane, o0 * inv);
-  stf(orow + lane + 64, o1 * inv);
+  // combine the 8 key groups (same running max in every group)
+#pragma unroll
+  for (int x = 8; x < 64; x <<= 1) {
+    l += __shfl_xor(l, x, 64);
+#pragma unroll
+    for (int d = 0; d < DPL; ++d) o[d] += __shfl_xor(o[d], x, 64);
+  }
+  if (grp == 0) {
+    const float inv = 1.0f / l;
+    T* orow = out + (long)m * H * HD + h * HD + sub * DPL;
+#pragma unroll
+    for (int d = 0; d < DPL; ++d) stf(orow + d, o[d] * inv);
+  }
 }
 
 }  // namespace zs
@@ -253,15 +348,24 @@ using namespace zs;
 extern "C" int zs_fp8_gemm_rows(const void* A, int lda, const void* W8, const float* scale, int M,
                                 int N, int K, float* out, long split_stride, int ldo,
                                 void* stream) {
-  ZS_REQUIRE(M > 0 && M <= F8_MAXM && N > 0 && K > 0 && K % 64 == 0,
-             "zs_fp8_gemm_rows: 1 <= M <= %d, K %% 64 == 0 (M=%d N=%d K=%d)", F8_MAXM, M, N, K);
+  ZS_REQUIRE(M > 0 && M <= F8_MAXM && N > 0 && K > 0 && K % F8_KC == 0,
+             "zs_fp8_gemm_rows: 1 <= M <= %d, K %% 1024 == 0 (M=%d N=%d K=%d)", F8_MAXM, M, N, K);
   ZS_REQUIRE(lda % 8 == 0 && ((uintptr_t)A & 15) == 0 && ((uintptr_t)W8 & 15) == 0 && K % 16 == 0,
              "zs_fp8_gemm_rows: 16-byte aligned A / W rows");
   ZS_REQUIRE(split_stride >= (long)(M - 1) * ldo + N && ldo >= N, "zs_fp8_gemm_rows: out layout");
-  const dim3 grid(cdiv(N, F8_NT), cdiv(K, F8_KC));
+  // tile: the widest whose grid still gives >= ~256 workgroups (activation re-reads per weight
+  // byte = 2 M / NT), else 64 columns
+  const int splits = cdiv(K, F8_KC);
   const size_t lds = (size_t)M * (F8_KC + 8) * 2;
-  hipLaunchKernelGGL(fp8_gemm_rows_kernel, grid, dim3(256), lds, S(stream), (const bf16_t*)A, lda,
-                     (const uint8_t*)W8, scale, M, N, K, out, split_stride, ldo);
+  hipStream_t st = S(stream);
+#define F8L(NB_, W_)                                                                            \
+  hipLaunchKernelGGL((fp8_gemm_rows_kernel<NB_, W_>), dim3(cdiv(N, 16 * NB_ * W_), splits),       \
+                     dim3(64 * W_), lds, st, (const bf16_t*)A, lda, (const uint8_t*)W8, scale, M,  \
+                     N, K, out, split_stride, ldo)
+  if ((long)cdiv(N, 256) * splits >= 256 && g_fp8_tile != 1) F8L(2, 8);
+  else if ((long)cdiv(N, 128) * splits >= 256 && g_fp8_tile != 1) F8L(1, 8);
+  else F8L(1, 4);
+#undef F8L
   ZS_LAUNCH_CHECK();
   return 0;
 }
@@ -288,12 +392,14 @@ extern "C" int zs_mistral_add_rmsnorm(float* x, const float* y, int nsplit, long
                                       void* stream) {
   ZS_REQUIRE(M > 0 && D > 0 && x && h && (y == nullptr || nsplit >= 1),
              "zs_mistral_add_rmsnorm: bad arguments");
+  ZS_REQUIRE(D % 4 == 0 && ss % 4 == 0 && ((uintptr_t)x & 15) == 0 && (!y || ((uintptr_t)y & 15) == 0),
+             "zs_mistral_add_rmsnorm: D, split stride multiples of 4, 16-byte aligned rows");
   if (hdtype == ZS_BF16)
-    hipLaunchKernelGGL(mistral_add_rmsnorm_kernel<bf16_t>, dim3(M), dim3(256), 0, S(stream), x, y,
-                       nsplit, ss, D, eps, w, (bf16_t*)h);
+    hipLaunchKernelGGL(mistral_add_rmsnorm_kernel<bf16_t>, dim3(M), dim3(1024), 0, S(stream), x,
+                       y, nsplit, ss, D, eps, w, (bf16_t*)h);
   else
-    hipLaunchKernelGGL(mistral_add_rmsnorm_kernel<float>, dim3(M), dim3(256), 0, S(stream), x, y,
-                       nsplit, ss, D, eps, w, (float*)h);
+    hipLaunchKernelGGL(mistral_add_rmsnorm_kernel<float>, dim3(M), dim3(1024), 0, S(stream), x,
+                       y, nsplit, ss, D, eps, w, (float*)h);
   ZS_LAUNCH_CHECK();
   return 0;
 }
@@ -320,7 +426,8 @@ extern "C" int zs_mistral_rope_kv(const float* qkv, int nsplit, long ss, int M, 
 extern "C" int zs_mistral_silu_mul(const float* gu, int nsplit, long ss, int M, int F, void* act,
                                    int dtype, void* stream) {
   ZS_REQUIRE(M > 0 && F > 0 && nsplit >= 1, "zs_mistral_silu_mul: bad shape");
-  const int nb = cdiv((long)M * F, 256);
+  ZS_REQUIRE(F % 4 == 0 && ss % 4 == 0, "zs_mistral_silu_mul: F and the split stride %% 4");
+  const int nb = cdiv((long)M * F / 4, 256);
   if (dtype == ZS_BF16)
     hipLaunchKernelGGL(mistral_silu_mul_kernel<bf16_t>, dim3(nb), dim3(256), 0, S(stream), gu,
                        nsplit, ss, M, F, (bf16_t*)act);

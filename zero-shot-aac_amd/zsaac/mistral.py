@@ -110,6 +110,37 @@ class MistralWeights:
         self.lnf = None if fold else gn.to(dev)
         self.lm = (lm * gn[None] if fold else lm).to(dev, self.adt).contiguous()
 
+    @classmethod
+    def synthetic(cls, device, cfg: dict, seed: int = 0, mode: str = "fp8", eos_boost: float = 1.5):
+        """Random-init weights at ``cfg`` (zsaac.synthetic.MISTRAL_7B geometry for the bench)
+        generated and quantised on the device, layer by layer (a 7B f32 state dict on the host
+        would take 29 GB)."""
+        dev = torch.device(device)
+        g = torch.Generator(device=dev).manual_seed(seed)
+        self = cls.__new__(cls)
+        self.mode, self.dev = mode, dev
+        self.adt = torch.float32 if mode == "f32" else torch.bfloat16
+        D, F, V = cfg["hidden"], cfg["ffn"], cfg["vocab"]
+        self.V, self.D, self.F = V, D, F
+        self.H, self.KVH, self.HD = cfg["heads"], cfg["kv_heads"], 128
+        self.eps, self.theta = 1e-5, 10000.0
+        rnd = lambda o, i, gain=1.0: torch.randn(o, i, device=dev, generator=g) * (gain / math.sqrt(i))
+        self.emb = torch.randn(V, D, device=dev, generator=g).to(self.adt)
+        self.layers = []
+        kv = self.KVH * 128
+        for _ in range(cfg["layers"]):
+            self.layers.append({
+                "ln1": None, "ln2": None,
+                "qkv": self._pack(torch.cat([rnd(D, D, 2.0), rnd(kv, D, 2.0), rnd(kv, D)])),
+                "o": self._pack(rnd(D, D)),
+                "gu": self._pack(torch.cat([rnd(F, D, 1.5), rnd(F, D)])),
+                "down": self._pack(rnd(D, F))})
+        self.lnf = None
+        lm = rnd(V, D, 4.0)
+        lm[2] *= eos_boost
+        self.lm = lm.to(self.adt).contiguous()
+        return self
+
     def _pack(self, w):
         w = w.float()
         N, K = w.shape
