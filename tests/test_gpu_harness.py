@@ -72,3 +72,38 @@ def test_predict_harness_matches_oracle(cuda, golden, tmp_path, isbeam):
             ref = OC.generate2(pe, sd, entry_length=67, use_cache=True)
         assert p["caption"] == tok.decode(ref).lower(), c["audio_id"]
         assert p["prefix"] == tok.decode(OC.prefix_tokens(pe, sd)), c["audio_id"]
+
+
+def test_predict_harness_magic(cuda, golden, tmp_path):
+    """--magic: the harness output equals the oracle's generate_beam_magic(beam 3, width 25) best
+    beam (f32), with the CLAP checkpoint and BERT vocabulary read from files like the reference."""
+    from oracle import caption as OC
+    from oracle import magic as OM
+    from transformers import BertTokenizer
+    from zsaac import bpe, predict
+    from zsaac import synthetic as S
+    from zsaac.tokenizer import compose_prompt_text
+    root = str(tmp_path)
+    sd, names, table, clips = _make_test_dir(root, golden)
+    bsd = S.bert_state_dict(layers=2)
+    torch.save({"model": dict(bsd)}, os.path.join(root, "clap.pt"))
+    vocab = S.bert_vocab()
+    with open(os.path.join(root, "vocab.txt"), "w") as f:
+        f.write("\n".join(vocab) + "\n")
+    argv = ["--test_dir", root, "--test_data", os.path.join(root, "test.pkl"), "--dtype", "f32",
+            "--batch", "4", "--magic", "--clap", os.path.join(root, "clap.pt"),
+            "--bert_vocab", os.path.join(root, "vocab.txt")]
+    assert predict.main(argv) == 0
+    out = json.load(open(os.path.join(root, "output.txt")))["predictions"]
+    tok = bpe.GPT2BPE.from_dir(os.path.join(root, "tokenizer"))
+    btok = BertTokenizer(vocab={t: i for i, t in enumerate(vocab)}, do_lower_case=True)
+    enc = OM.text_encoder(btok, bsd, 2)
+    for c, p in zip(clips[:2], out[:2]):
+        emb = c["audio_embedding"].float()
+        idx = OC.sound_effect_choice(emb, table, 3)[0].tolist()
+        hard = torch.tensor([tok.encode(compose_prompt_text([names[i].lower() for i in idx]))])
+        pref = torch.nn.functional.normalize(emb, dim=-1)
+        pe = OC.clap_to_gpt(pref[None], hard, sd)
+        outs, _ = OM.generate_beam_magic(pe, sd, tok.decode, enc, pref, float(bsd["temp"]),
+                                         beam_size=3, entry_length=20, magic_width=25)
+        assert p["caption"] == tok.decode(outs[0]).lower(), c["audio_id"]

@@ -245,7 +245,8 @@ __global__ __launch_bounds__(64 * WAVES) void gemm_rows_kernel(RowsArgs g) {
   ZS_STAMP(6);
 }
 
-int g_rows_nt48 = 1;  // A/B knob (zs_tune_set "rows_nt48"): 48-column LN tiles
+int g_rows_nt48 = 1;  // A/B knob (zs_tune_set "rows_nt48"): 48-column LN tiles (2: 64)
+int g_rows_wide = 0;  // A/B knob (zs_tune_set "rows_wide"): 32-column plain tiles at N < 1536
 int g_gemm_rows = 1;   // A/B knob (zs_tune_set "gemm_rows"): 0 = skinny split-K kernel for M <= 64
 
 // shape plan: waves (K split), k-steps per wave, column tile; waves < 0 when not covered
@@ -261,8 +262,13 @@ static RowsPlan rows_plan(int N, int K, bool ln) {
   const int per = ln ? 2 : 3;               // loads per k-step at NT = 32
   // LN mode: 48-column tiles where N allows (c_fc 64 x 4 = 256 workgroups, c_attn 192: one per
   // CU; at 32 columns c_fc's 384 put two on half the CUs, whose per-CU load bytes set the time)
+  // knobs for the concurrent bench (several batches co-running: the bytes each launch pulls
+  // through the CUs' load path matter more than its own latency): rows_nt48 = 2 -> 64-column
+  // LN tiles; rows_wide = 1 -> 32-column tiles for the N = 768 projections (half the
+  // activation re-reads of mproj's 3072-deep rows)
+  if (ln && g_rows_nt48 == 2 && N % 64 == 0 && S * 4 <= RG_MAX_LOADS) return {waves, S, 64};
   if (ln && g_rows_nt48 && N % 48 == 0 && S * 3 <= RG_MAX_LOADS) return {waves, S, 48};
-  if (S * per <= RG_MAX_LOADS && N >= 1536) return {waves, S, 32};
+  if (S * per <= RG_MAX_LOADS && (N >= 1536 || (!ln && g_rows_wide))) return {waves, S, 32};
   return {waves, S, 16};
 }
 
@@ -296,7 +302,8 @@ static int launch_rows(const RowsArgs& g0, RowsPlan p, hipStream_t st) {
   const dim3 grid(g.rgroups * g.ntiles);
   const size_t lds = (LN ? (size_t)RG * (g.K + 8) * 2 : 0) + (size_t)p.waves * RG * p.nt * 4;
   if constexpr (LN) {                       // rows_plan: LN at 4 waves only
-    if (p.nt == 48) launch_rows_s<LNM, 48, 4>(g, p.steps, grid, lds, st);
+    if (p.nt == 64) launch_rows_s<LNM, 64, 4>(g, p.steps, grid, lds, st);
+    else if (p.nt == 48) launch_rows_s<LNM, 48, 4>(g, p.steps, grid, lds, st);
     else if (p.nt == 32) launch_rows_s<LNM, 32, 4>(g, p.steps, grid, lds, st);
     else launch_rows_s<LNM, 16, 4>(g, p.steps, grid, lds, st);
   } else if (p.nt == 32) {

@@ -15,8 +15,11 @@ modes on the hot path (greedy ``generate2`` and ``generate_beam(beam_size=3)``):
   this image, and its SPICE/METEOR scorers need Java).
 
 The tokenizer is GPT-2 byte-level BPE from a local ``vocab.json`` + ``merges.txt``
-(``--tokenizer``; ``zsaac.bpe``).  CLAP-guided ``--magic`` decoding is not on the hot path
- and is refused.
+(``--tokenizer``; ``zsaac.bpe``).  ``--magic`` (predict_prompt.py:121-140) runs CLAP-guided
+beam decoding, ``generate_beam_magic(beam_size=3, magic_width, alpha 0.1, beta 0.2)`` with
+``audio_embeds = prefix``, batched on zsaac.magic.MagicDecoder; the CLAP checkpoint
+(``--clap``, the reference's HTSAT-BERT-ZS.pt: ``{"model": ASE state dict}``) supplies the BERT
+text tower and ``--bert_vocab`` its WordPiece vocabulary (bert-base-uncased's vocab.txt).
 """
 from __future__ import annotations
 
@@ -137,6 +140,39 @@ def make_preds(pipe: CaptionPipeline, tokenizer, all_data: List[Dict],
     return key2pred, key2pred_prefix, key2refs
 
 
+def make_preds_magic(pipe: CaptionPipeline, tokenizer, all_data: List[Dict], clap_sd, bert_tok,
+                     width: int = 25, alpha: float = 0.1, beta: float = 0.2, beam: int = 3,
+                     entry_length: int = 20):
+    """predict_prompt.py:121-140 with ``--magic``: per clip generate_beam_magic(model, clap,
+    tokenizer, audio_embeds=prefix, embed=prefix_embed, beam_size=3, alpha, beta, magic_width)[0]
+    (entry_length 20, the function's default), batched over ``pipe.cfg.batch`` clips."""
+    from . import ops
+    from .bert import BertTextEngine
+    from .magic import MagicDecoder
+    key2refs: Dict[str, List[str]] = {it["audio_id"]: post_processing(it.get("caption", []))
+                                      for it in all_data}
+    key2pred: Dict[str, List[str]] = {}
+    key2pred_prefix: Dict[str, List[str]] = {}
+    B = pipe.cfg.batch
+    bert = BertTextEngine(clap_sd, pipe.dev, pipe.cfg.dtype, max_texts=B * beam * width)
+    mag = MagicDecoder(pipe.gpt, bert, B, pipe.Pmax, beam=beam, width=width, max_steps=entry_length)
+    for c0 in range(0, len(all_data), B):
+        chunk = all_data[c0:c0 + B]
+        emb = safeload.stack_rows([it["audio_embedding"] for it in chunk]).to(pipe.dev)
+        n = emb.shape[0]
+        pipe.begin_emb(emb)                      # prompt, mapper, get_prefix_tokens (+ prefill)
+        prefs = pipe.result().prefix_token_lists()
+        prefix = pipe.prefix[:n]
+        soft = pipe.mapper(prefix)
+        res = mag.beam_magic(pipe.hard_ids[:n], pipe.hard_len[:n], soft, pipe.cfg.prefix_length,
+                             prefix, tokenizer, bert_tok, beam, width, entry_length, alpha, beta,
+                             soft_ld=pipe.mapper.soft_ld)
+        for it, (toks, _), pids in zip(chunk, res, prefs):
+            key2pred[it["audio_id"]] = [tokenizer.decode(toks[0]).lower()]
+            key2pred_prefix[it["audio_id"]] = [tokenizer.decode(pids)]
+    return key2pred, key2pred_prefix, key2refs
+
+
 def write_outputs(test_dir: str, key2pred, key2pred_prefix, key2refs) -> Optional[Dict]:
     """output.txt exactly as predict_prompt.py:172-181; scores.txt (:155-170) when the
     captioning metrics are importable."""
@@ -189,16 +225,31 @@ def main(argv: Optional[Sequence[str]] = None) -> int:
     ap.add_argument("--dtype", choices=["f32", "bf16"], default="f32")
     ap.add_argument("--batch", type=int, default=64)
     ap.add_argument("--device", type=str, default="cuda")
+    ap.add_argument("--clap", type=str, default=None,
+                    help="--magic: CLAP checkpoint ({'model': ASE state dict}, predict_prompt.py:125)")
+    ap.add_argument("--bert_vocab", type=str, default=None, help="--magic: BERT vocab.txt")
     args = ap.parse_args(argv)
-    if args.magic:
-        raise SystemExit("--magic (CLAP-guided decoding) is not implemented on this path")
+    if args.magic and not (args.clap and args.bert_vocab):
+        raise SystemExit("--magic needs --clap <checkpoint> and --bert_vocab <vocab.txt>")
     params = load_params(args.test_dir)
     tokenizer = GPT2BPE.from_dir(args.tokenizer or os.path.join(args.test_dir, "tokenizer"))
     dtype = torch.float32 if args.dtype == "f32" else torch.bfloat16
     pipe, _ = build_pipeline(args.test_dir, params, tokenizer, args.isbeam, dtype, args.batch,
                              args.device)
     all_data = safeload.load_pickle(args.test_data)
-    key2pred, key2pred_prefix, key2refs = make_preds(pipe, tokenizer, all_data)
+    if args.magic:
+        from transformers import BertTokenizer
+        ck = torch.load(args.clap, map_location="cpu", weights_only=True)
+        clap_sd = ck["model"] if "model" in ck else ck
+        with open(args.bert_vocab, encoding="utf-8") as f:
+            vocab = {t.rstrip("\n"): i for i, t in enumerate(f)}
+        bert_tok = BertTokenizer(vocab=vocab, do_lower_case=True)
+        # predict_prompt.py:19-22 (alpha 0.1, beta 0.2); magic_width from params.json (25 default)
+        key2pred, key2pred_prefix, key2refs = make_preds_magic(
+            pipe, tokenizer, all_data, clap_sd, bert_tok, width=int(params.get("magic_width", 25)),
+            alpha=float(params.get("alpha", 0.1)), beta=float(params.get("beta", 0.2)))
+    else:
+        key2pred, key2pred_prefix, key2refs = make_preds(pipe, tokenizer, all_data)
     write_outputs(args.test_dir, key2pred, key2pred_prefix, key2refs)
     return 0
 
