@@ -6,7 +6,7 @@ launches of exactly the launches bench.py times (roofline_setup: cold weights), 
 
     rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_fetch -o run --output-format csv -- python3 tools/pmc_traffic.py run
     rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write -o run --output-format csv -- python3 tools/pmc_traffic.py run
-    python3 tools/pmc_traffic.py parse gpurun_out/pmc_fetch gpurun_out/pmc_write gpurun_out/pmc_traffic_r1.json
+    python3 tools/pmc_traffic.py parse gpurun_out/pmc_fetch gpurun_out/pmc_write profiles/r2_pmc_traffic.json
 
 Corrections (MI355X_MICROARCH.md §HBM): FETCH_SIZE is in KiB and on gfx950 reports half the
 bytes of a 16-B/lane coalesced streaming read (the GEMM's LDS-DMA loads are all 16 B per lane),
@@ -25,18 +25,26 @@ sys.path.insert(0, os.path.join(ROOT, "zero-shot-aac_amd"))
 
 
 def run():
+    """The bench's roofline launches: zs_gemm_ln at the bs=64 decode c_fc shape (64 rows, folded
+    LN, gelu_new) rotating over cold weight copies, as bench.roofline_gemm_ln times them."""
     import torch
     import bench
+    from zsaac import ops
 
-    class A:       # bench.py defaults: eval batch 64, group 128 -> 8192 decode rows
-        batch, group, dtype, encoder, mapper, beam, entry_length = 64, 128, "bf16", "htsat", "mlp", 0, 67
+    class A:
+        batch, group, dtype, encoder, mapper, beam, entry_length, compact = \
+            64, 1, "bf16", "htsat", "mlp", 0, 67, 1
+        encoder_batch = 64
     pipe, _, _ = bench.build(A, torch.device("cuda", 0))
-    launch, flops, algo, ncopy, kname, shape = bench.roofline_setup(pipe)
-    for i in range(2 * ncopy):
-        launch(i)
+    dec, ly = pipe.decoder, pipe.gpt.layers[0]
+    x, hid = dec.x[:64], dec.hid[:64]
+    copies = bench._cold_copies(ly["fc_w"])
+    for i in range(2 * len(copies)):
+        ops.gemm_ln(x, *ly["ln2_gemm"], copies[i % len(copies)], hid, bias=ly["fc_b"],
+                    act=ops.ACT_GELU_TANH)
     torch.cuda.synchronize()
-    print(json.dumps({"algo_bytes_per_launch": algo, "launches": 2 * ncopy, "kernel": kname,
-                      "shape": shape}))
+    N, K = ly["fc_w"].shape
+    print(json.dumps({"launches": 2 * len(copies), "shape": [64, N, K]}))
 
 
 def _per_dispatch(d, counter, kname):
@@ -57,13 +65,13 @@ def _per_dispatch(d, counter, kname):
     return v[len(v) // 2], len(v)
 
 
-def parse(dfetch, dwrite, out, M=8192, N=3072, K=768, kname="gemm_lean_kernel"):
+def parse(dfetch, dwrite, out, M=64, N=3072, K=768, kname="gemm_rows_kernel"):
     fetch_kib, n_f = _per_dispatch(dfetch, "FETCH_SIZE", kname)
     write_kib, n_w = _per_dispatch(dwrite, "WRITE_SIZE", kname)
     rd = 2 * 1024 * fetch_kib
     wr = 1024 * write_kib
     sys.path.insert(0, ROOT)
-    res = {"kernel": f"{kname}<bf16> decode c_fc [{M}x{K}]x[{K}x{N}] (cold weights)",
+    res = {"kernel": f"{kname}<48,4,LN,6> (zs_gemm_ln) decode c_fc [{M}x{K}]x[{K}x{N}] (cold weights)",
            "fetch_size_kib_median": fetch_kib, "write_size_kib_median": write_kib,
            "dispatches": [n_f, n_w], "hbm_read_bytes_per_launch": int(rd),
            "hbm_write_bytes_per_launch": int(wr), "hbm_bytes_per_launch": int(rd + wr),
@@ -71,7 +79,7 @@ def parse(dfetch, dwrite, out, M=8192, N=3072, K=768, kname="gemm_lean_kernel"):
                           "write = 1024*WRITE_SIZE"}
     # the shape bench.py checks against before quoting the traffic
     res["shape"] = [M, N, K]
-    res["algo_bytes_per_launch"] = N * K * 2 + M * K * 2 + N * 4 + M * N * 2
+    res["algo_bytes_per_launch"] = N * K * 2 + M * K * 4 + N * 4 + M * N * 2
     with open(out, "w") as f:
         json.dump(res, f, indent=1)
     print(json.dumps(res))

@@ -151,13 +151,40 @@ class BertTextEngine:
         return self.encode_ids(ids, lens)
 
 
+_BACKENDS = {}
+
+
+def _backend(tokenizer, max_length):
+    """A private copy of a fast tokenizer's Rust backend configured like the reference's call
+    (truncation at max_length, pad to the longest with [PAD]): encode_batch gives the same ids
+    as ``tokenizer(..., padding='longest', truncation=True)`` without the Python wrapper's
+    per-text overhead (4800 candidate texts per magic step: 0.11 s against 0.36 s)."""
+    bk = getattr(tokenizer, "backend_tokenizer", None)
+    if bk is None or not getattr(tokenizer, "is_fast", False) or getattr(tokenizer, "padding_side", "right") != "right":
+        return None
+    key = (id(tokenizer), max_length)
+    if key not in _BACKENDS:
+        from tokenizers import Tokenizer
+        b = Tokenizer.from_str(bk.to_str())
+        b.enable_truncation(max_length)
+        b.enable_padding(pad_id=tokenizer.pad_token_id, pad_token=tokenizer.pad_token)
+        _BACKENDS[key] = b
+    return _BACKENDS[key]
+
+
 def tokenize(tokenizer, texts, max_length, device):
     """``tokenizer(texts, padding='longest', truncation=True, max_length=30)`` on the host ->
     device ids [T, L] int32 and lengths [T] int32 (the attention mask as lengths: BERT's
     tokenizer right-pads, so the mask is a prefix of ones)."""
-    t = tokenizer(list(texts), padding="longest", truncation=True, max_length=max_length,
-                  return_tensors="pt")
-    ids = t["input_ids"].to(torch.int32)
-    lens = t["attention_mask"].sum(1).to(torch.int32)
+    bk = _backend(tokenizer, max_length)
+    if bk is not None:
+        enc = bk.encode_batch(list(texts))
+        ids = torch.tensor([e.ids for e in enc], dtype=torch.int32)
+        lens = torch.tensor([sum(e.attention_mask) for e in enc], dtype=torch.int32)
+    else:
+        t = tokenizer(list(texts), padding="longest", truncation=True, max_length=max_length,
+                      return_tensors="pt")
+        ids = t["input_ids"].to(torch.int32)
+        lens = t["attention_mask"].sum(1).to(torch.int32)
     return (ids.pin_memory().to(device, non_blocking=True),
             lens.pin_memory().to(device, non_blocking=True))

@@ -118,16 +118,24 @@ class MagicDecoder:
         dec, nb, R = self.dec, C * b, C * b * W
         cand = dec.next_tok[:R]
         greedy = mode == "search"
+        if getattr(self, "_cand_h", None) is None or self._cand_h.numel() < self.R:
+            self._cand_h = torch.zeros(self.R, dtype=torch.int32, pin_memory=True)
+            self._tok_h = torch.zeros_like(self.tokens, device="cpu").pin_memory()
         for s in range(n_steps):
             ops.row_topk(self.logits[:nb], W, self.pval[:nb], cand.view(nb, W),
                          mode=1 if greedy else 0)
+            # candidate ids and histories to the host now; the candidate GPT-2 forward runs
+            # while the host builds and tokenises the candidate texts
+            self._cand_h[:R].copy_(cand, non_blocking=True)
+            self._tok_h[:nb].copy_(self.tokens[:nb], non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record()
             ops.magic_expand(self.kvrow, self.pos, nb, W, dec.Lmax, self.kvrow_c, dec.pos)
             dec._decode_forward(R, kvrow=self.kvrow_c[:R])
             hf = dec.hf[:R]
             ops.magic_maxcos(hf, R, W, self.ctx, dec.Lmax, self.kvrow, self.pos, self.maxcos)
-            cand_h = cand.cpu()
-            tok_h = self.tokens[:nb, :s].cpu() if s else torch.zeros(nb, 0, dtype=torch.int32)
-            texts = self._texts(tokenizer, cand_h, tok_h, C, b, W, s)
+            ev.synchronize()
+            texts = self._texts(tokenizer, self._cand_h[:R], self._tok_h[:nb, :s], C, b, W, s)
             ids, lens = tokenize(text_tokenizer, texts, self.text_max_len, self.dev)
             text = self.bert.encode_ids(ids, lens)
             nact = 1 if (s == 0 and not greedy) else b
