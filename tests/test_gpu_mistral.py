@@ -81,7 +81,7 @@ def test_mistral_fp8_ids_until_small_margin(cuda, setup):
     print(f"fp8 mistral: token agreement {agree}/{total}")
 
 
-@pytest.mark.parametrize("M,N,K", [(32, 6144, 4096), (7, 1000, 1024), (64, 256, 14336)])
+@pytest.mark.parametrize("M,N,K", [(32, 6144, 4096), (7, 1008, 1024), (64, 256, 14336)])
 def test_fp8_gemm_rows(cuda, M, N, K):
     from zsaac._lib import call
     from zsaac.mistral import dequantize_fp8, quantize_fp8

@@ -24,6 +24,7 @@ typedef __attribute__((ext_vector_type(4))) float f32x4m_t;
 typedef __attribute__((ext_vector_type(4))) unsigned u32x4m_t;
 
 int g_fp8_tile = 0;   // zs_tune_set("fp8_tile", 1): 64-column tiles only (A/B knob)
+int g_fp8_dbg = 0;    // zs_tune_set("fp8_dbg", b): ablations (1 no A loads, 2 no MFMA, 4 no W loads)
 
 constexpr int F8_KC = 1024;   // k per workgroup (one split)
 constexpr int F8_MAXM = 64;
@@ -36,11 +37,11 @@ constexpr int F8_MAXM = 64;
 // assignment, so the products pair up (the sum runs over a permuted k order).  Bytes per
 // workgroup: NT x 1024 weight + M x 1024 x 2 activation, so wide tiles (NT = 256 for gate|up)
 // keep the activation re-reads at a quarter of the weight stream.
-template <int NB, int WAVES>
+template <int NB, int WAVES, int MB>
 __global__ __launch_bounds__(64 * WAVES) void fp8_gemm_rows_kernel(
     const bf16_t* __restrict__ A, int lda, const uint8_t* __restrict__ W8,
     const float* __restrict__ scale, int M, int N, int K, float* __restrict__ out,
-    long split_stride, int ldo) {
+    long split_stride, int ldo, int dbg) {
   constexpr int NT = 16 * NB * WAVES, NTHR = 64 * WAVES;
   constexpr int JB = F8_KC / 64;                    // 64-deep k blocks per split
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -57,7 +58,7 @@ __global__ __launch_bounds__(64 * WAVES) void fp8_gemm_rows_kernel(
   // weight loads stay in flight (issued the other way round, every A load waited behind the
   // whole weight stream and the A copy became a chain of round trips)
   const int per_row = kc / 8;                        // 16-byte pieces per A row
-  constexpr int AMAX = F8_MAXM * (F8_KC / 8) / NTHR; // pieces per thread at M = 64
+  constexpr int AMAX = MB * (F8_KC / 8) / NTHR;      // pieces per thread at M = MB
   uint4 av[AMAX];
 #pragma unroll
   for (int t = 0; t < AMAX; ++t) {
@@ -73,6 +74,8 @@ __global__ __launch_bounds__(64 * WAVES) void fp8_gemm_rows_kernel(
     for (int j = 0; j < JB; ++j)
       wv[nb][j] = __builtin_nontemporal_load(reinterpret_cast<const u32x4m_t*>(wr + 64 * j));
   }
+  // (straight-line code from the first load to here: the compiler's counted waits let these
+  // stores wait for the A loads only, the weight stream stays in flight)
 #pragma unroll
   for (int t = 0; t < AMAX; ++t) {
     const int i = threadIdx.x + t * NTHR;
@@ -110,28 +113,31 @@ __global__ __launch_bounds__(64 * WAVES) void fp8_gemm_rows_kernel(
       const int m = min(rb * 16 + fr, M - 1);
       const bf16x8m_t a0 = *reinterpret_cast<const bf16x8m_t*>(as + m * LDA_S + ka);
       const bf16x8m_t a1 = *reinterpret_cast<const bf16x8m_t*>(as + m * LDA_S + ka + 8);
+      // transposed product out^T = W A^T: the weight fragment is the A operand, so a lane's
+      // accumulators are 4 consecutive output COLUMNS of one row -> one 16-byte slab store
 #pragma unroll
       for (int nb = 0; nb < NB; ++nb) {
-        acc[nb][rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, b0[nb], acc[nb][rb], 0, 0, 0);
-        acc[nb][rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, b1[nb], acc[nb][rb], 0, 0, 0);
+        acc[nb][rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b0[nb], a0, acc[nb][rb], 0, 0, 0);
+        acc[nb][rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b1[nb], a1, acc[nb][rb], 0, 0, 0);
       }
     }
   }
-  // C layout: lane -> column (lane & 15) of each block, rows 16 rb + 4 (lane >> 4) + i
+  // C layout (transposed product): lane -> output row m = 16 rb + (lane & 15), columns
+  // n0 + 16 nb + 4 (lane >> 4) + i, i = 0..3
   float* o = out + split * split_stride;
 #pragma unroll
   for (int nb = 0; nb < NB; ++nb) {
-    const int n = n0 + 16 * nb + fr;
+    const int n = n0 + 16 * nb + 4 * g;
     if (n >= N) continue;
-    const float s = scale[n];
+    const float4 sc = *reinterpret_cast<const float4*>(scale + n);
 #pragma unroll
     for (int rb = 0; rb < F8_MAXM / 16; ++rb) {
       if (rb >= nrb) break;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int m = rb * 16 + 4 * g + i;
-        if (m < M) o[(long)m * ldo + n] = acc[nb][rb][i] * s;
-      }
+      const int m = rb * 16 + fr;
+      if (m < M)
+        *reinterpret_cast<float4*>(o + (long)m * ldo + n) =
+            make_float4(acc[nb][rb][0] * sc.x, acc[nb][rb][1] * sc.y, acc[nb][rb][2] * sc.z,
+                        acc[nb][rb][3] * sc.w);
     }
   }
 }
@@ -352,16 +358,25 @@ extern "C" int zs_fp8_gemm_rows(const void* A, int lda, const void* W8, const fl
              "zs_fp8_gemm_rows: 1 <= M <= %d, K %% 1024 == 0 (M=%d N=%d K=%d)", F8_MAXM, M, N, K);
   ZS_REQUIRE(lda % 8 == 0 && ((uintptr_t)A & 15) == 0 && ((uintptr_t)W8 & 15) == 0 && K % 16 == 0,
              "zs_fp8_gemm_rows: 16-byte aligned A / W rows");
-  ZS_REQUIRE(split_stride >= (long)(M - 1) * ldo + N && ldo >= N, "zs_fp8_gemm_rows: out layout");
+  ZS_REQUIRE(split_stride >= (long)(M - 1) * ldo + N && ldo >= N && N % 16 == 0 && ldo % 4 == 0 &&
+             split_stride % 4 == 0 && ((uintptr_t)out & 15) == 0 && ((uintptr_t)scale & 15) == 0,
+             "zs_fp8_gemm_rows: out layout (N %% 16, 16-byte aligned rows and scales)");
   // tile: the widest whose grid still gives >= ~256 workgroups (activation re-reads per weight
   // byte = 2 M / NT), else 64 columns
   const int splits = cdiv(K, F8_KC);
   const size_t lds = (size_t)M * (F8_KC + 8) * 2;
   hipStream_t st = S(stream);
 #define F8L(NB_, W_)                                                                            \
-  hipLaunchKernelGGL((fp8_gemm_rows_kernel<NB_, W_>), dim3(cdiv(N, 16 * NB_ * W_), splits),       \
-                     dim3(64 * W_), lds, st, (const bf16_t*)A, lda, (const uint8_t*)W8, scale, M,  \
-                     N, K, out, split_stride, ldo)
+  do {                                                                                          \
+    if (M <= 32)                                                                                \
+      hipLaunchKernelGGL((fp8_gemm_rows_kernel<NB_, W_, 32>), dim3(cdiv(N, 16 * NB_ * W_), splits), \
+                         dim3(64 * W_), lds, st, (const bf16_t*)A, lda, (const uint8_t*)W8, scale, \
+                         M, N, K, out, split_stride, ldo, g_fp8_dbg);                            \
+    else                                                                                        \
+      hipLaunchKernelGGL((fp8_gemm_rows_kernel<NB_, W_, 64>), dim3(cdiv(N, 16 * NB_ * W_), splits), \
+                         dim3(64 * W_), lds, st, (const bf16_t*)A, lda, (const uint8_t*)W8, scale, \
+                         M, N, K, out, split_stride, ldo, g_fp8_dbg);                            \
+  } while (0)
   if ((long)cdiv(N, 256) * splits >= 256 && g_fp8_tile != 1) F8L(2, 8);
   else if ((long)cdiv(N, 128) * splits >= 256 && g_fp8_tile != 1) F8L(1, 8);
   else F8L(1, 4);
