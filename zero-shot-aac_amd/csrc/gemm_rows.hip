@@ -92,22 +92,8 @@ __global__ __launch_bounds__(64 * WAVES) void gemm_rows_kernel(RowsArgs g) {
   // their outputs are never stored
   const int am = min(m0 + fr, g.M - 1);
 
-  // weight fragments for every k-step of this wave, issued first (they do not depend on x)
-  bf16x8r_t b[S * NB];
-  bf16x8r_t a[LN ? 1 : S];
-  const bf16_t* wrow[NB];
-#pragma unroll
-  for (int nb = 0; nb < NB; ++nb) wrow[nb] = g.W + (long)min(n0 + 16 * nb + fr, g.N - 1) * g.ldw;
-#pragma unroll
-  for (int s = 0; s < S; ++s) {
-    const int k = kw + 32 * s + fk;
-#pragma unroll
-    for (int nb = 0; nb < NB; ++nb)
-      b[s * NB + nb] = *reinterpret_cast<const bf16x8r_t*>(wrow[nb] + k);
-    if constexpr (!LN) a[s] = *reinterpret_cast<const bf16x8r_t*>(g.A + (long)am * g.lda + k);
-  }
-  // epilogue operands (one column quad of one row per thread), fetched now so their latency
-  // hides under the operand loads; loads clamped in range, masked by value
+  // epilogue operands (one column quad of one row per thread), issued before the operand
+  // loads (the counted waits below then cover only the operands); loads clamped in range, masked by value
   constexpr int NQ = NT / 4;
   static_assert(RG * NQ <= NTHR, "one epilogue quad per thread");
   const bool epi = threadIdx.x < RG * NQ;
@@ -125,7 +111,9 @@ __global__ __launch_bounds__(64 * WAVES) void gemm_rows_kernel(RowsArgs g) {
       er.z = rr[min(en + 2, g.N - 1)]; er.w = rr[min(en + 3, g.N - 1)];
     }
   }
-  // LN operands: 16 rows, TPR threads per row, NV float4 per thread (column quads t, t+TPR, ..)
+  // LN operands FIRST (loads return in order: the LayerNorm below then waits only for x, and
+  // runs while the weight fragments are still in flight): 16 rows, TPR threads per row, NV
+  // float4 per thread (column quads t, t+TPR, ..)
   constexpr int TPR = NTHR / RG, NV = LN ? K / (4 * TPR) : 1;
   static_assert(!LN || K % (4 * TPR) == 0, "LN rows: K % (4 * threads per row)");
   const int lr = threadIdx.x / TPR, lt = threadIdx.x % TPR;
@@ -142,6 +130,21 @@ __global__ __launch_bounds__(64 * WAVES) void gemm_rows_kernel(RowsArgs g) {
         lb[i] = reinterpret_cast<const float4*>(g.ln_b)[lt + TPR * i];
       }
     }
+  }
+  // weight fragments for every k-step of this wave (straight-line code from here: the LN waits
+  // for x alone, the MFMA loop consumes the fragments as they land)
+  bf16x8r_t b[S * NB];
+  bf16x8r_t a[LN ? 1 : S];
+  const bf16_t* wrow[NB];
+#pragma unroll
+  for (int nb = 0; nb < NB; ++nb) wrow[nb] = g.W + (long)min(n0 + 16 * nb + fr, g.N - 1) * g.ldw;
+#pragma unroll
+  for (int s = 0; s < S; ++s) {
+    const int k = kw + 32 * s + fk;
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb)
+      b[s * NB + nb] = *reinterpret_cast<const bf16x8r_t*>(wrow[nb] + k);
+    if constexpr (!LN) a[s] = *reinterpret_cast<const bf16x8r_t*>(g.A + (long)am * g.lda + k);
   }
   // keep every load above in flight before any of them is used (the scheduler otherwise sinks
   // loads next to their MFMAs and waits on each group)
