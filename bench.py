@@ -697,11 +697,11 @@ def main():
     world, rank, local = dist_setup(args)
     device = torch.device("cuda", local)
     from zsaac import dist as zd
-    pipe, csd, asd = build(args, device)
     if args.magic:
         return main_magic(args, torch.device("cuda", 0))
     if args.mistral:
         return main_mistral(args, torch.device("cuda", 0))
+    pipe, csd, asd = build(args, device)
     if args.embeddings_only:
         return main_embeddings(args, world, rank, device, pipe)
     B = pipe.cfg.batch

@@ -399,6 +399,7 @@ __global__ __launch_bounds__(64 * RA_NW) void row_attn_mfma_kernel(
   }
 }
 
+int g_attn_split = 1;   // zs_tune_set("attn_split", 0): one wave per (row, head) at R <= 128
 int g_row_mfma = 1;   // zs_tune_set("row_mfma", 0): the scalar row_attn_kernel for bf16 too
 
 // ------------------------------------------------------------------ GPT-2 decode attention
@@ -632,16 +633,23 @@ __device__ __forceinline__ uint4 bf8_pack(const float (&f)[8]) {
                     (uint32_t)f2bf(f[6]) | ((uint32_t)f2bf(f[7]) << 16));
 }
 
-template <typename T, int KPP = 64, bool PF = false, bool DPP = false>   // KPP: keys per phase
+// SPLIT = 2: the keys of one (row, head) are split over two waves of the workgroup (slice s takes
+// phases s, s + 2, ...; 2 heads per workgroup), whose online-softmax states are merged through LDS
+// at the end: twice the waves for the bs=64 decode's 768 (row, head) pairs, each with half the
+// loads in flight (requires heads even, rows without rowmap; no early exit before the barrier).
+template <typename T, int KPP = 64, bool PF = false, bool DPP = false, int SPLIT = 1>
 __global__ __launch_bounds__(256) void decode_attn6_kernel(
     const T* __restrict__ qkv, int D, int heads, T* __restrict__ kc, T* __restrict__ vc, int Lmax,
     const int* __restrict__ pos, const int* __restrict__ kvrow, T* __restrict__ out,
     const int* __restrict__ rowmap, const int* __restrict__ cpos, int nphys) {
   static_assert(sizeof(T) == 2, "bf16 only");
+  static_assert(SPLIT == 1 || (SPLIT == 2 && !PF), "SPLIT 2 without prefetch");
   constexpr int HD = 64, EPC = 8, NG = KPP / 8;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int c = blockIdx.x, h = blockIdx.y * 4 + wid;
-  if (h >= heads) return;
+  const int slice = SPLIT == 1 ? 0 : (wid & 1);
+  const int c = blockIdx.x, h = blockIdx.y * (4 / SPLIT) + (SPLIT == 1 ? wid : wid >> 1);
+  __shared__ float merge[SPLIT == 1 ? 1 : 2][66];
+  if (SPLIT == 1 && h >= heads) return;
   const int grp = lane >> 3, sub = lane & 7;
   const int r = rowmap ? rowmap[c] : c;
   const int p0 = cpos ? cpos[c] : 0;
@@ -690,7 +698,7 @@ __global__ __launch_bounds__(256) void decode_attn6_kernel(
     }                                                                                          \
   } while (0)
   if (PF) ZS_LOAD_PHASE(0, kr, vr);
-  for (int base = 0; base <= p; base += KPP) {
+  for (int base = slice * KPP; base <= p; base += KPP * SPLIT) {
     if (PF) {
       if (base + KPP <= p) ZS_LOAD_PHASE(base + KPP, kx, vx);
     } else {
@@ -753,6 +761,23 @@ __global__ __launch_bounds__(256) void decode_attn6_kernel(
     sum += __shfl_xor(sum, d, 64);
 #pragma unroll
     for (int t = 0; t < EPC; ++t) o[t] += __shfl_xor(o[t], d, 64);
+  }
+  if constexpr (SPLIT == 2) {
+    // slice 1 publishes (max, sum, o) of its keys; slice 0 merges them into its own
+    float* mg = merge[wid >> 1];
+    if (slice == 1 && grp == 0) {
+#pragma unroll
+      for (int t = 0; t < EPC; ++t) mg[sub * EPC + t] = o[t];
+      if (sub == 0) { mg[64] = m; mg[65] = sum; }
+    }
+    __syncthreads();
+    if (slice == 1) return;
+    const float m1 = mg[64], s1 = mg[65];
+    const float mm = fmaxf(m, m1);
+    const float a0 = expf(m - mm), a1 = m1 == -INFINITY ? 0.f : expf(m1 - mm);
+    sum = sum * a0 + s1 * a1;
+#pragma unroll
+    for (int t = 0; t < EPC; ++t) o[t] = o[t] * a0 + mg[sub * EPC + t] * a1;
   }
   if (grp == 0) {
     const float inv = 1.0f / sum;
@@ -1019,6 +1044,16 @@ extern "C" int zs_decode_attention(const void* qkv, int R, int D, int heads, voi
              "zs_decode_attention: head_dim must be 64");
   ZS_REQUIRE(Lmax > 0 && Lmax <= 4096, "zs_decode_attention: Lmax");
   dim3 grid(R, heads);
+  if (dtype == ZS_BF16 && R <= 128 && g_small_attn && g_attn_split && heads % 2 == 0) {
+    // few waves (R x heads): each (row, head)'s keys over two waves, 64-key phases (all keys
+    // of L <= 128 in flight at once, half per wave)
+    hipLaunchKernelGGL((decode_attn6_kernel<bf16_t, 64, false, true, 2>), dim3(R, heads / 2),
+                       dim3(256), 0, S(stream), (const bf16_t*)qkv, D, heads, (bf16_t*)kc,
+                       (bf16_t*)vc, Lmax, pos, kvrow, (bf16_t*)out, (const int*)nullptr,
+                       (const int*)nullptr, R);
+    ZS_LAUNCH_CHECK();
+    return 0;
+  }
   if (dtype == ZS_BF16 && R <= 128 && g_small_attn) {
     // few waves (R x heads): nothing hides a phase's round trip, so take 128-key phases: every
     // key of a row in flight at once, one HBM round trip at L <= 128
