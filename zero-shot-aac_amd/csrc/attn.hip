@@ -238,8 +238,8 @@ __global__ __launch_bounds__(64 * WA_NW) void window_attn_mfma_kernel(
       const int d0 = 8 * g + 4 * h;
       if (d0 < hd) {
         uint2 u;
-        u.x = (uint32_t)f2bf(ot[qb][4 * g] * inv) | ((uint32_t)f2bf(ot[qb][4 * g + 1] * inv) << 16);
-        u.y = (uint32_t)f2bf(ot[qb][4 * g + 2] * inv) | ((uint32_t)f2bf(ot[qb][4 * g + 3] * inv) << 16);
+        u.x = pk2bf(ot[qb][4 * g] * inv, ot[qb][4 * g + 1] * inv);
+        u.y = pk2bf(ot[qb][4 * g + 2] * inv, ot[qb][4 * g + 3] * inv);
         *reinterpret_cast<uint2*>(orow + d0) = u;
       }
     }
@@ -391,8 +391,8 @@ __global__ __launch_bounds__(64 * RA_NW) void row_attn_mfma_kernel(
 #pragma unroll
       for (int g = 0; g < 4; ++g) {      // dims 8 g + 4 h .. +3 of this tile
         uint2 u;
-        u.x = (uint32_t)f2bf(ot[4 * g] * inv) | ((uint32_t)f2bf(ot[4 * g + 1] * inv) << 16);
-        u.y = (uint32_t)f2bf(ot[4 * g + 2] * inv) | ((uint32_t)f2bf(ot[4 * g + 3] * inv) << 16);
+        u.x = pk2bf(ot[4 * g] * inv, ot[4 * g + 1] * inv);
+        u.y = pk2bf(ot[4 * g + 2] * inv, ot[4 * g + 3] * inv);
         *reinterpret_cast<uint2*>(orow + 8 * g + 4 * h) = u;
       }
     }
@@ -627,10 +627,10 @@ __device__ __forceinline__ uint4 sel_u4(bool c, const uint4& a, const uint4& b) 
   return make_uint4(c ? a.x : b.x, c ? a.y : b.y, c ? a.z : b.z, c ? a.w : b.w);
 }
 __device__ __forceinline__ uint4 bf8_pack(const float (&f)[8]) {
-  return make_uint4((uint32_t)f2bf(f[0]) | ((uint32_t)f2bf(f[1]) << 16),
-                    (uint32_t)f2bf(f[2]) | ((uint32_t)f2bf(f[3]) << 16),
-                    (uint32_t)f2bf(f[4]) | ((uint32_t)f2bf(f[5]) << 16),
-                    (uint32_t)f2bf(f[6]) | ((uint32_t)f2bf(f[7]) << 16));
+  return make_uint4(pk2bf(f[0], f[1]),
+                    pk2bf(f[2], f[3]),
+                    pk2bf(f[4], f[5]),
+                    pk2bf(f[6], f[7]));
 }
 
 // SPLIT = 2: the keys of one (row, head) are split over two waves of the workgroup (slice s takes

@@ -42,6 +42,14 @@ __device__ __forceinline__ bf16_t f2bf(float f) {
   return *reinterpret_cast<bf16_t*>(&h);
 }
 
+// two floats -> one dword of two bf16 (low = a), round-to-nearest-even: ONE v_cvt_pk_bf16_f32
+// (two f2bf calls and an OR cost three instructions)
+typedef __attribute__((ext_vector_type(2))) float cvt_f32x2_t;
+typedef __attribute__((ext_vector_type(2))) __bf16 cvt_bf16x2_t;
+__device__ __forceinline__ uint32_t pk2bf(float a, float b) {
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector((cvt_f32x2_t){a, b}, cvt_bf16x2_t));
+}
+
 template <typename T> struct Cvt;
 template <> struct Cvt<float> {
   __device__ __forceinline__ static float to_f(float v) { return v; }

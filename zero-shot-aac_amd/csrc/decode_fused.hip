@@ -46,7 +46,7 @@ __device__ __forceinline__ void df_unpack8(const uint4& u, float (&f)[8]) {
   f[6] = __uint_as_float(u.w << 16); f[7] = __uint_as_float(u.w & 0xffff0000u);
 }
 __device__ __forceinline__ uint32_t df_pack2(float a, float b) {
-  return (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16);
+  return pk2bf(a, b);
 }
 __device__ __forceinline__ uint4 df_sel(bool c, const uint4& a, const uint4& b) {
   return make_uint4(c ? a.x : b.x, c ? a.y : b.y, c ? a.z : b.z, c ? a.w : b.w);

@@ -129,10 +129,10 @@ __device__ __forceinline__ void epi_slab(const GemmArgs& g, const float* slab, i
     if (full && vec_out) {
       if (g.out_dtype == ZS_BF16) {
         uint4 u;
-        u.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
-        u.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
-        u.z = (uint32_t)f2bf(v[4]) | ((uint32_t)f2bf(v[5]) << 16);
-        u.w = (uint32_t)f2bf(v[6]) | ((uint32_t)f2bf(v[7]) << 16);
+        u.x = pk2bf(v[0], v[1]);
+        u.y = pk2bf(v[2], v[3]);
+        u.z = pk2bf(v[4], v[5]);
+        u.w = pk2bf(v[6], v[7]);
         if (g.dbg != 6 || u.x == 0x7fc17fc1u)   // dbg 6 (experiment): no global stores
           *reinterpret_cast<uint4*>(reinterpret_cast<bf16_t*>(g.out) + o) = u;
       } else {

@@ -177,13 +177,13 @@ __global__ __launch_bounds__(64 * WAVES) void gemm_rows_kernel(RowsArgs g) {
       const int c = lt + TPR * i;
       uint2 pk;
       if constexpr (AFF) {
-        pk.x = (uint32_t)f2bf((xv[i].x - mean) * rstd * lw[i].x + lb[i].x) |
-               ((uint32_t)f2bf((xv[i].y - mean) * rstd * lw[i].y + lb[i].y) << 16);
-        pk.y = (uint32_t)f2bf((xv[i].z - mean) * rstd * lw[i].z + lb[i].z) |
-               ((uint32_t)f2bf((xv[i].w - mean) * rstd * lw[i].w + lb[i].w) << 16);
+        pk.x = pk2bf((xv[i].x - mean) * rstd * lw[i].x + lb[i].x,
+                     (xv[i].y - mean) * rstd * lw[i].y + lb[i].y);
+        pk.y = pk2bf((xv[i].z - mean) * rstd * lw[i].z + lb[i].z,
+                     (xv[i].w - mean) * rstd * lw[i].w + lb[i].w);
       } else {
-        pk.x = (uint32_t)f2bf((xv[i].x - mean) * rstd) | ((uint32_t)f2bf((xv[i].y - mean) * rstd) << 16);
-        pk.y = (uint32_t)f2bf((xv[i].z - mean) * rstd) | ((uint32_t)f2bf((xv[i].w - mean) * rstd) << 16);
+        pk.x = pk2bf((xv[i].x - mean) * rstd, (xv[i].y - mean) * rstd);
+        pk.y = pk2bf((xv[i].z - mean) * rstd, (xv[i].w - mean) * rstd);
       }
       *reinterpret_cast<uint2*>(hs + lr * ldh + 4 * c) = pk;
     }
@@ -231,8 +231,8 @@ __global__ __launch_bounds__(64 * WAVES) void gemm_rows_kernel(RowsArgs g) {
   if (en + 3 < g.N && (g.ldo & 3) == 0 && ((uintptr_t)g.out & 15) == 0) {
     if (bf) {
       uint2 pk;
-      pk.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
-      pk.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+      pk.x = pk2bf(v[0], v[1]);
+      pk.y = pk2bf(v[2], v[3]);
       *reinterpret_cast<uint2*>(reinterpret_cast<bf16_t*>(g.out) + (long)em * g.ldo + en) = pk;
     } else {
       *reinterpret_cast<float4*>(reinterpret_cast<float*>(g.out) + (long)em * g.ldo + en) =

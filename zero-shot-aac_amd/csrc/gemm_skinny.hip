@@ -244,6 +244,7 @@ extern int g_gemm_dbg;      // gemm.hip
 extern int g_fast_persist;  // gemm.hip
 extern int g_fast_xcd;      // gemm.hip
 extern int g_swin_dbg;      // swin.hip
+extern int g_swin_occ3;     // swin.hip
 extern int g_gemm_lean;     // gemm.hip
 extern int g_row_mfma;      // attn.hip
 extern int g_logmel_wave;   // frontend.hip
@@ -289,6 +290,7 @@ extern "C" int zs_tune_set(const char* key, int value) {
   if (!strcmp(key, "fast_persist")) { g_fast_persist = value; return 0; }
   if (!strcmp(key, "fast_xcd")) { g_fast_xcd = value; return 0; }
   if (!strcmp(key, "swin_dbg")) { g_swin_dbg = value; return 0; }
+  if (!strcmp(key, "swin_occ3")) { g_swin_occ3 = value; return 0; }
   if (!strcmp(key, "gemm_lean")) { g_gemm_lean = value; return 0; }
   if (!strcmp(key, "row_mfma")) { g_row_mfma = value; return 0; }
   if (!strcmp(key, "logmel_wave")) { g_logmel_wave = value; return 0; }

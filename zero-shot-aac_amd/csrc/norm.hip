@@ -72,8 +72,8 @@ __global__ __launch_bounds__(256) void layernorm_reg_kernel(const float* __restr
       // one 8-byte (bf16) / 16-byte (f32) store per lane: the caller guarantees the alignment
       if constexpr (sizeof(TO) == 2) {
         uint2 u;
-        u.x = (uint32_t)f2bf(o0) | ((uint32_t)f2bf(o1) << 16);
-        u.y = (uint32_t)f2bf(o2) | ((uint32_t)f2bf(o3) << 16);
+        u.x = pk2bf(o0, o1);
+        u.y = pk2bf(o2, o3);
         *reinterpret_cast<uint2*>(yr + 4 * c) = u;
       } else {
         *reinterpret_cast<float4*>(yr + 4 * c) = make_float4(o0, o1, o2, o3);

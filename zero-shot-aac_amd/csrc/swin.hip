@@ -62,6 +62,7 @@ struct SwinArgs {
 };
 
 int g_swin_dbg = 0;
+int g_swin_occ3 = 1;              // zs_tune_set "swin_occ3": C = 96 at 3 workgroups per CU
 
 __device__ __forceinline__ sw_bf16x8 as_bf8(uint4 u) { return __builtin_bit_cast(sw_bf16x8, u); }
 
@@ -128,20 +129,22 @@ __device__ __forceinline__ void win_gemm(const bf16_t* A, int lda, WPipe<NTW, D>
   }
 }
 
-template <int C>
+// OCC: workgroups per CU.  C = 96 runs 3 (53 KB of LDS, <= 168 VGPRs: two-deep weight pipes and
+// fc2 accumulated straight onto the residual registers), the wider blocks 2 (1 at C = 384).
+template <int C, int OCC = 2>
 struct SwinCfg {
-  static constexpr int NW = C >= 384 ? 8 : 4;  // waves per workgroup (2 per SIMD either way)
+  static constexpr int NW = C >= 384 ? 8 : 4;  // waves per workgroup
   static constexpr int G = NW / 2;           // heads per q/k/v group: one (head, 32 queries) per wave
   static constexpr int NH = C / 24;          // heads (head dim 24)
   static constexpr int NG = NH / G;          // head groups
-  static constexpr int LD = C + 16;          // H / ATT row stride (elements): conflict-free reads
+  static constexpr int LD = OCC >= 3 ? C + 8 : C + 16;   // H / ATT row stride (elements): conflict-free reads
   static constexpr int HC = 48 * NW;         // MLP hidden chunk (3 n-tiles per wave)
   static constexpr int LDH = HC + 16;
   static constexpr int NCH = 4 * C / HC;
   static constexpr int NTP = C / 16;         // n-tiles of proj / fc2
   static constexpr int NTW = (NTP + NW - 1) / NW;   // per wave (max)
-  static constexpr int DA = (C <= 96 || C >= 384) ? 3 : 2;   // weight pipe depth (k-steps): qkv / fc1
-  static constexpr int DB = (C <= 96 || C >= 384) ? 3 : 2;   // proj / fc2
+  static constexpr int DA = OCC >= 3 ? 2 : (C <= 96 || C >= 384) ? 3 : 2;   // weight pipe depth (k-steps): qkv / fc1
+  static constexpr int DB = OCC >= 3 ? 2 : (C <= 96 || C >= 384) ? 3 : 2;   // proj / fc2
   static constexpr int SZ_H = 64 * LD * 2;
   static constexpr int OFF_H = 0, OFF_ATT = SZ_H, OFF_QKV = 2 * SZ_H;
   static constexpr int SZ_QKV = 3 * G * 64 * 32 * 2;   // Qs[G][64][32], Ks[G][64][32], Vt[G][32][64]
@@ -152,13 +155,13 @@ struct SwinCfg {
   static_assert(64 * LDX * 4 <= LDS, "output staging fits");
   static_assert(64 * LDH * 2 <= SZ_H + SZ_QKV, "hidden chunk fits ATT + QKV");
   static_assert(2 * NW * 64 * 4 <= SZ_QKV, "LN2 reduction fits QKV");
-  static_assert(LDS <= 160 * 1024, "LDS");
+  static_assert(LDS * OCC <= 160 * 1024 || (OCC == 2 && LDS <= 160 * 1024), "LDS");
   static_assert(C % 96 == 0 && NH % G == 0 && (4 * C) % HC == 0 && C % (16 * NW / 4) == 0, "C");
 };
 
-template <int C, bool SH>   // SH: shifted windows (shift = ws / 2 = 4, odd blocks)
-__global__ __launch_bounds__(64 * SwinCfg<C>::NW, 2) void swin_block_kernel(SwinArgs g) {
-  using CF = SwinCfg<C>;
+template <int C, bool SH, int OCC>   // SH: shifted windows (shift = ws / 2 = 4, odd blocks)
+__global__ __launch_bounds__((64 * SwinCfg<C, OCC>::NW), OCC) void swin_block_kernel(SwinArgs g) {
+  using CF = SwinCfg<C, OCC>;
   constexpr int LD = CF::LD, NTW = CF::NTW, NTP = CF::NTP, KS = C / 32, NW = CF::NW, G = CF::G;
   constexpr int NT = 64 * NW, TPT = NW;      // threads; threads per token in the row passes
   __shared__ __attribute__((aligned(16))) char lds[CF::LDS];
@@ -216,10 +219,8 @@ __global__ __launch_bounds__(64 * SwinCfg<C>::NW, 2) void swin_block_kernel(Swin
       const float4 gw = *reinterpret_cast<const float4*>(g.ln1_w + c0);
       const float4 gb = *reinterpret_cast<const float4*>(g.ln1_b + c0);
       uint2 u;
-      u.x = (uint32_t)f2bf((v[j].x - mean) * rstd * gw.x + gb.x) |
-            ((uint32_t)f2bf((v[j].y - mean) * rstd * gw.y + gb.y) << 16);
-      u.y = (uint32_t)f2bf((v[j].z - mean) * rstd * gw.z + gb.z) |
-            ((uint32_t)f2bf((v[j].w - mean) * rstd * gw.w + gb.w) << 16);
+      u.x = pk2bf((v[j].x - mean) * rstd * gw.x + gb.x, (v[j].y - mean) * rstd * gw.y + gb.y);
+      u.y = pk2bf((v[j].z - mean) * rstd * gw.z + gb.z, (v[j].w - mean) * rstd * gw.w + gb.w);
       *reinterpret_cast<uint2*>(sH + t * LD + c0) = u;
     }
   }
@@ -253,8 +254,8 @@ __global__ __launch_bounds__(64 * SwinCfg<C>::NW, 2) void swin_block_kernel(Swin
         for (int mi = 0; mi < 4; ++mi) {
           const int t = 16 * mi + (l & 15);
           uint2 u;
-          u.x = (uint32_t)f2bf(acc[mi][j][0] + bias.x) | ((uint32_t)f2bf(acc[mi][j][1] + bias.y) << 16);
-          u.y = (uint32_t)f2bf(acc[mi][j][2] + bias.z) | ((uint32_t)f2bf(acc[mi][j][3] + bias.w) << 16);
+          u.x = pk2bf(acc[mi][j][0] + bias.x, acc[mi][j][1] + bias.y);
+          u.y = pk2bf(acc[mi][j][2] + bias.z, acc[mi][j][3] + bias.w);
           *reinterpret_cast<uint2*>(base + t * 32 + 8 * ((d0 >> 3) ^ ((t >> 2) & 3)) + (d0 & 7)) = u;
         }
       }
@@ -265,8 +266,8 @@ __global__ __launch_bounds__(64 * SwinCfg<C>::NW, 2) void swin_block_kernel(Swin
         for (int mi = 0; mi < 4; ++mi) {
           const int t0 = 16 * mi + 4 * (l >> 4);
           uint2 u;
-          u.x = (uint32_t)f2bf(acc[mi][2][0] + bias) | ((uint32_t)f2bf(acc[mi][2][1] + bias) << 16);
-          u.y = (uint32_t)f2bf(acc[mi][2][2] + bias) | ((uint32_t)f2bf(acc[mi][2][3] + bias) << 16);
+          u.x = pk2bf(acc[mi][2][0] + bias, acc[mi][2][1] + bias);
+          u.y = pk2bf(acc[mi][2][2] + bias, acc[mi][2][3] + bias);
           *reinterpret_cast<uint2*>(sVt + hh * 2048 + d * 64 + 4 * ((t0 >> 2) ^ (d & 15))) = u;
         }
       }
@@ -362,8 +363,8 @@ __global__ __launch_bounds__(64 * SwinCfg<C>::NW, 2) void swin_block_kernel(Swin
       for (int gq = 0; gq < 3; ++gq) {       // dims 8 gq + 4 h2 .. +3 (< 24)
         const int d0 = 8 * gq + 4 * h2;
         uint2 u;
-        u.x = (uint32_t)f2bf(ot[4 * gq] * inv) | ((uint32_t)f2bf(ot[4 * gq + 1] * inv) << 16);
-        u.y = (uint32_t)f2bf(ot[4 * gq + 2] * inv) | ((uint32_t)f2bf(ot[4 * gq + 3] * inv) << 16);
+        u.x = pk2bf(ot[4 * gq] * inv, ot[4 * gq + 1] * inv);
+        u.y = pk2bf(ot[4 * gq + 2] * inv, ot[4 * gq + 3] * inv);
         *reinterpret_cast<uint2*>(orow + d0) = u;
       }
     }
@@ -440,10 +441,10 @@ __global__ __launch_bounds__(64 * SwinCfg<C>::NW, 2) void swin_block_kernel(Swin
         for (int mi = 0; mi < 4; ++mi) {
           const int t = 16 * mi + (l & 15);
           uint2 u;
-          u.x = (uint32_t)f2bf((x1[mi][j][0] - mean[mi]) * rstd[mi] * gw.x + gb.x) |
-                ((uint32_t)f2bf((x1[mi][j][1] - mean[mi]) * rstd[mi] * gw.y + gb.y) << 16);
-          u.y = (uint32_t)f2bf((x1[mi][j][2] - mean[mi]) * rstd[mi] * gw.z + gb.z) |
-                ((uint32_t)f2bf((x1[mi][j][3] - mean[mi]) * rstd[mi] * gw.w + gb.w) << 16);
+          u.x = pk2bf((x1[mi][j][0] - mean[mi]) * rstd[mi] * gw.x + gb.x,
+                      (x1[mi][j][1] - mean[mi]) * rstd[mi] * gw.y + gb.y);
+          u.y = pk2bf((x1[mi][j][2] - mean[mi]) * rstd[mi] * gw.z + gb.z,
+                      (x1[mi][j][3] - mean[mi]) * rstd[mi] * gw.w + gb.w);
           *reinterpret_cast<uint2*>(sH + t * LD + c0) = u;
         }
       }
@@ -452,11 +453,19 @@ __global__ __launch_bounds__(64 * SwinCfg<C>::NW, 2) void swin_block_kernel(Swin
   __syncthreads();
 
   // ---- P5: MLP in hidden chunks of HC: fc1 + GELU(erf) -> HID (LDS) -> fc2 accumulates
-  sw_f32x4 acc2[4][NTW];
+  // fc2 accumulates onto x1 + b2 (the residual registers double as the accumulator)
+  sw_f32x4 (&acc2)[4][NTW] = x1;
 #pragma unroll
-  for (int mi = 0; mi < 4; ++mi)
+  for (int j = 0; j < NTW; ++j) {
+    if (NTP % NW == 0 || w + NW * j < NTP) {
+      const float4 bias = *reinterpret_cast<const float4*>(g.b2 + (w + NW * j) * 16 + 4 * (l >> 4));
 #pragma unroll
-    for (int j = 0; j < NTW; ++j) acc2[mi][j] = sw_f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int mi = 0; mi < 4; ++mi) {
+        acc2[mi][j][0] += bias.x; acc2[mi][j][1] += bias.y;
+        acc2[mi][j][2] += bias.z; acc2[mi][j][3] += bias.w;
+      }
+    }
+  }
   bf16_t* sHID = reinterpret_cast<bf16_t*>(lds + CF::OFF_ATT);
   for (int ch = 0; ch < ((g.dbg & 4) ? 0 : CF::NCH); ++ch) {
     {
@@ -481,8 +490,8 @@ __global__ __launch_bounds__(64 * SwinCfg<C>::NW, 2) void swin_block_kernel(Swin
             v2 = gelu_erf_fast(v2); v3 = gelu_erf_fast(v3);
           }
           uint2 u;
-          u.x = (uint32_t)f2bf(v0) | ((uint32_t)f2bf(v1) << 16);
-          u.y = (uint32_t)f2bf(v2) | ((uint32_t)f2bf(v3) << 16);
+          u.x = pk2bf(v0, v1);
+          u.y = pk2bf(v2, v3);
           *reinterpret_cast<uint2*>(sHID + t * CF::LDH + c0) = u;
         }
       }
@@ -500,13 +509,11 @@ __global__ __launch_bounds__(64 * SwinCfg<C>::NW, 2) void swin_block_kernel(Swin
   for (int j = 0; j < NTW; ++j) {
     if (NTP % NW == 0 || w + NW * j < NTP) {
       const int c0 = (w + NW * j) * 16 + 4 * (l >> 4);
-      const float4 bias = *reinterpret_cast<const float4*>(g.b2 + c0);
 #pragma unroll
       for (int mi = 0; mi < 4; ++mi) {
         const int t = 16 * mi + (l & 15);
         *reinterpret_cast<float4*>(sX + t * CF::LDX + c0) =
-            make_float4(acc2[mi][j][0] + bias.x + x1[mi][j][0], acc2[mi][j][1] + bias.y + x1[mi][j][1],
-                        acc2[mi][j][2] + bias.z + x1[mi][j][2], acc2[mi][j][3] + bias.w + x1[mi][j][3]);
+            make_float4(acc2[mi][j][0], acc2[mi][j][1], acc2[mi][j][2], acc2[mi][j][3]);
       }
     }
   }
@@ -541,11 +548,12 @@ extern "C" int zs_swin_block(float* x, int B, int H, int W, int C, int heads, in
              (const uint4*)w2_packed, b2, g_swin_dbg};
   dim3 grid(B * (H / 8) * (W / 8));
   hipStream_t st = S(stream);
-#define SWL(C_, SH_) \
-  hipLaunchKernelGGL((swin_block_kernel<C_, SH_>), grid, dim3(64 * SwinCfg<C_>::NW), 0, st, a)
-  if (C == 96) { if (shift) SWL(96, true); else SWL(96, false); }
-  else if (C == 192) { if (shift) SWL(192, true); else SWL(192, false); }
-  else { if (shift) SWL(384, true); else SWL(384, false); }
+#define SWL(C_, SH_, O_) \
+  hipLaunchKernelGGL((swin_block_kernel<C_, SH_, O_>), grid, dim3(64 * SwinCfg<C_, O_>::NW), 0, st, a)
+  if (C == 96 && g_swin_occ3) { if (shift) SWL(96, true, 3); else SWL(96, false, 3); }
+  else if (C == 96) { if (shift) SWL(96, true, 2); else SWL(96, false, 2); }
+  else if (C == 192) { if (shift) SWL(192, true, 2); else SWL(192, false, 2); }
+  else { if (shift) SWL(384, true, 2); else SWL(384, false, 2); }
 #undef SWL
   ZS_LAUNCH_CHECK();
   return 0;
