@@ -258,9 +258,11 @@ int zs_magic_step(const float* score, const int* cand, int C, int b, int W, int 
  * consumer (RoPE/KV append, SiLU*up, add+RMSNorm): deterministic, no reduction launch. */
 
 /* zs_fp8_gemm_rows: weight-only fp8 GEMM for M <= 64 rows (decode): out[s][m][n] = scale[n] *
- * sum_{k in split s} A[m][k] W8[n][k]; A bf16 [M][lda], W8 fp8 e4m3 (OCP) codes [N][K], scale f32
- * [N] (one per output channel), K % 1024 == 0, splits of 1024 along K (zs_fp8_splits(K) of
- * them), ldo >= N.
+ * sum_{k in split s} A[m][k] W[n][k]; A bf16 [M][lda], W8 the fp8 e4m3 (OCP) codes of W [N][K]
+ * TILE-PACKED [K/1024][ceil(N/128)][8][16][64][16 B] (zsaac/mistral.py fp8_pack_tiles: block
+ * (s, t, w, j), lane l = W[128 t + 16 w + (l & 15)][1024 s + 64 j + 16 (l >> 4) .. +16], rows past
+ * N zero), scale f32 [N] (one per output channel), K % 1024 == 0, splits of 1024 along K
+ * (zs_fp8_splits(K) of them), ldo >= N.
  * Replaces the NF4-quantised q/k/v/o/gate/up/down projections of the LoRA-wrapped Mistral
  * (caption_model.py:355-364). */
 int zs_fp8_gemm_rows(const void* A, int lda, const void* W8, const float* scale, int M, int N,

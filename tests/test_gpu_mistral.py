@@ -81,10 +81,14 @@ def test_mistral_fp8_ids_until_small_margin(cuda, setup):
     print(f"fp8 mistral: token agreement {agree}/{total}")
 
 
-@pytest.mark.parametrize("M,N,K", [(32, 6144, 4096), (7, 1008, 1024), (64, 256, 14336)])
+# one-shot tiles: the first three; the persistent stream kernel (M <= 32, more than one 128 x 1024
+# item per CU): the down shape (2 items per workgroup), gate-sized with 3 items per workgroup, a
+# column tail (16528 % 128 = 16) and a clamped last run, and 4 items at M = 7
+@pytest.mark.parametrize("M,N,K", [(32, 6144, 4096), (7, 1008, 1024), (64, 256, 14336),
+                                   (32, 4096, 14336), (20, 16528, 4096), (7, 28672, 4096)])
 def test_fp8_gemm_rows(cuda, M, N, K):
     from zsaac._lib import call
-    from zsaac.mistral import dequantize_fp8, quantize_fp8
+    from zsaac.mistral import dequantize_fp8, fp8_pack_tiles, quantize_fp8
     g = torch.Generator().manual_seed(M + N)
     w = torch.randn(N, K, generator=g) / K ** 0.5
     a = torch.randn(M, K, generator=g).bfloat16()
@@ -92,7 +96,7 @@ def test_fp8_gemm_rows(cuda, M, N, K):
     ref = a.float() @ dequantize_fp8(q, s).t()
     ns = call("zs_fp8_splits", K)
     out = torch.empty(ns, M, N, device=cuda)
-    ad, qd, sd = a.to(cuda), q.to(cuda), s.to(cuda)        # keep the device copies alive
+    ad, qd, sd = a.to(cuda), fp8_pack_tiles(q).to(cuda), s.to(cuda)   # keep the copies alive
     call("zs_fp8_gemm_rows", ad.data_ptr(), K, qd.data_ptr(), sd.data_ptr(),
          M, N, K, out.data_ptr(), M * N, N, torch.cuda.current_stream().cuda_stream)
     got = out.sum(0).cpu()

@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Microbenchmark of the weight-only fp8 row GEMM (csrc/mistral.hip) at the Mistral-7B decode
-shapes, M = 32, cold weights (launches rotate over > 512 MiB of weight copies); fp8_tile = 1
-forces 64-column tiles.  (Round-2 ablations, before the transposed product / straight-line load
+shapes, M = 32, cold weights (launches rotate over > 512 MiB of weight copies); fp8_tile = 0 is
+the default dispatch (persistent stream kernel for the long streams), 2 the one-shot kernel only,
+1 64-column one-shot tiles.  (Round-2 ablations, before the transposed product / straight-line load
 phase: no activation loads -47..-56 % time, no MFMA 0 %, no weight loads -44..-55 %, plain vs
 non-temporal weight loads 0 %.)
 
@@ -32,7 +33,7 @@ def main():
         ns = call("zs_fp8_splits", K)
         out = torch.empty(ns * M * N, device=dev)
         res = []
-        for knob, val in (("fp8_dbg", 0), ("fp8_tile", 1)):
+        for knob, val in (("fp8_tile", 0), ("fp8_tile", 2), ("fp8_tile", 1)):
             lib().zs_tune_set(knob.encode(), val)
 
             def launch(i):

@@ -23,16 +23,27 @@ typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2m_t;
 typedef __attribute__((ext_vector_type(4))) float f32x4m_t;
 typedef __attribute__((ext_vector_type(4))) unsigned u32x4m_t;
 
-int g_fp8_tile = 0;   // zs_tune_set("fp8_tile", 1): 64-column tiles only (A/B knob)
+int g_fp8_tile = 0;   // zs_tune_set("fp8_tile", v) A/B knob: 1 = 64-column one-shot tiles only,
+                      // 2 = one-shot kernel only (no persistent stream kernel)
 int g_fp8_dbg = 0;    // zs_tune_set("fp8_dbg", b): ablations (1 no A loads, 2 no MFMA, 4 no W loads)
 
 constexpr int F8_KC = 1024;   // k per workgroup (one split)
 constexpr int F8_MAXM = 64;
 
-// out[split][m][n] = scale[n] * sum_{k in split} A[m][k] * W8[n][k]   (M <= 64)
+// Tile-packed fp8 weights (zsaac/mistral.py fp8_pack_tiles): [K/1024][ntiles = ceil(N/128)][8]
+// [16][64 lanes][16 B].  The 1 KiB block of (k split s, 128-column tile t, 16-column group w,
+// 64-deep k block j) holds, in lane l, W[128 t + 16 w + (l & 15)][1024 s + 64 j + 16 (l >> 4) ..
+// +16] (rows past N zero): each wave-load is one contiguous KiB and an item (s, t) one
+// contiguous 128 KiB.  Returns lane l's address of block j = 0 of (s, group nb16 = 8 t + w).
+__device__ __forceinline__ const uint8_t* f8_frag(const uint8_t* W8, int ntiles, int split,
+                                                  int nb16, int lane) {
+  return W8 + ((((long)split * ntiles + (nb16 >> 3)) * 8 + (nb16 & 7)) * 16) * 1024 + lane * 16;
+}
+
+// out[split][m][n] = scale[n] * sum_{k in split} A[m][k] * W[n][k]   (M <= 64, W8 tile-packed)
 // A workgroup of WAVES waves covers NT = 16 NB WAVES columns x one 1024-deep k split: lane l of a
 // wave covers column n = l & 15 of each of its NB 16-column blocks; in each 64-deep k block lane
-// group g = l >> 4 loads the 16 consecutive fp8 at k = 64 j + 16 g (one 16-byte load) and feeds
+// group g = l >> 4 holds the 16 consecutive fp8 at k = 64 j + 16 g (one 16-byte load) and feeds
 // them as two MFMA k-slices of 8; A is staged once per workgroup in LDS and read with the same k
 // assignment, so the products pair up (the sum runs over a permuted k order).  Bytes per
 // workgroup: NT x 1024 weight + M x 1024 x 2 activation, so wide tiles (NT = 256 for gate|up)
@@ -67,12 +78,15 @@ __global__ __launch_bounds__(64 * WAVES) void fp8_gemm_rows_kernel(
     av[t] = *reinterpret_cast<const uint4*>(A + (long)m * lda + k0 + c);
   }
   u32x4m_t wv[NB][JB];   // weights are read once per decode step: non-temporal loads
+  const int ntiles = (N + 127) >> 7;
 #pragma unroll
   for (int nb = 0; nb < NB; ++nb) {
-    const uint8_t* wr = W8 + (long)min(n0 + 16 * nb + fr, N - 1) * K + k0 + 16 * g;
+    // groups past the last tile (a 256-column tile over an odd tile count) reread the last
+    // group; their columns are >= N and never stored
+    const uint8_t* wr = f8_frag(W8, ntiles, split, min((n0 >> 4) + nb, 8 * ntiles - 1), lane);
 #pragma unroll
     for (int j = 0; j < JB; ++j)
-      wv[nb][j] = __builtin_nontemporal_load(reinterpret_cast<const u32x4m_t*>(wr + 64 * j));
+      wv[nb][j] = __builtin_nontemporal_load(reinterpret_cast<const u32x4m_t*>(wr + 1024 * j));
   }
   // (straight-line code from the first load to here: the compiler's counted waits let these
   // stores wait for the A loads only, the weight stream stays in flight)
@@ -139,6 +153,141 @@ __global__ __launch_bounds__(64 * WAVES) void fp8_gemm_rows_kernel(
             make_float4(acc[nb][rb][0] * sc.x, acc[nb][rb][1] * sc.y, acc[nb][rb][2] * sc.z,
                         acc[nb][rb][3] * sc.w);
     }
+  }
+}
+
+// Persistent form of the same product for M <= 32 and the long weight streams (gate|up, down):
+// gridDim.x workgroups (one per CU) each walk a contiguous, equal-length run of (k split, column
+// tile) items in split-major order.  Item i+1's weight fragments are issued into the second
+// register buffer before item i's MFMAs, so a CU's weight stream never drains between items (the
+// one-shot kernel issues a workgroup's whole slice, waits, computes, stores and exits, and its
+// grid of 448 workgroups runs as 1.75 rounds); the LDS activation chunk is reloaded only when the
+// run crosses into the next split, before the next item's loads are issued (the counted waits
+// are in issue order).  Slab layout and the sum over k are the one-shot kernel's.
+template <int WAVES>
+struct F8Stream {
+  static constexpr int NT = 16 * WAVES, NTHR = 64 * WAVES, JB = F8_KC / 64, MB = 32;
+  static constexpr int LDA_S = F8_KC + 8;
+  static constexpr int AMAX = MB * (F8_KC / 8) / NTHR;
+};
+
+// one item's operands in flight: its weight fragments and the scales of the 4 output columns a
+// lane stores (loaded with the item, so the store never waits behind the next item's stream)
+struct F8Item {
+  u32x4m_t w[F8_KC / 64];
+  float4 sc;
+};
+
+template <int WAVES>
+__device__ __forceinline__ void f8s_issue(F8Item& b, const uint8_t* __restrict__ W8,
+                                          const float* __restrict__ scale, int N, int K,
+                                          int ntiles, int it) {
+  using P = F8Stream<WAVES>;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int split = it / ntiles, tile = it - split * ntiles;
+  const uint8_t* wr = f8_frag(W8, ntiles, split, tile * WAVES + wid, lane);
+#pragma unroll
+  for (int j = 0; j < P::JB; ++j)
+    b.w[j] = __builtin_nontemporal_load(reinterpret_cast<const u32x4m_t*>(wr + 1024 * j));
+  b.sc = *reinterpret_cast<const float4*>(scale + min(tile * P::NT + wid * 16 + 4 * (lane >> 4), N - 4));
+}
+
+template <int WAVES>
+__device__ __forceinline__ void f8s_load_a(bf16_t* as, const bf16_t* __restrict__ A, int lda,
+                                           int M, int split) {
+  using P = F8Stream<WAVES>;
+  constexpr int per_row = F8_KC / 8;
+  __syncthreads();                     // the previous split's readers are done with `as`
+  uint4 av[P::AMAX];
+#pragma unroll
+  for (int t = 0; t < P::AMAX; ++t) {
+    const int i = threadIdx.x + t * P::NTHR;
+    const int m = min(i / per_row, M - 1), c = (i % per_row) * 8;
+    av[t] = *reinterpret_cast<const uint4*>(A + (long)m * lda + split * F8_KC + c);
+  }
+#pragma unroll
+  for (int t = 0; t < P::AMAX; ++t) {
+    const int i = threadIdx.x + t * P::NTHR;
+    if (i < M * per_row)
+      *reinterpret_cast<uint4*>(as + (i / per_row) * P::LDA_S + (i % per_row) * 8) = av[t];
+  }
+  __syncthreads();
+}
+
+template <int WAVES>
+__device__ __forceinline__ void f8s_compute(const F8Item& b, const bf16_t* as, int M, int N,
+                                            float* __restrict__ out, long split_stride, int ldo,
+                                            int ntiles, int it) {
+  using P = F8Stream<WAVES>;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, fr = lane & 15, g = lane >> 4;
+  const int split = it / ntiles, tile = it - split * ntiles;
+  // both 16-row blocks always run (rows past M read row M - 1, their results are not stored):
+  // a data-dependent branch here would make the compiler wait for every load in flight,
+  // including the next item's
+  f32x4m_t acc[2] = {f32x4m_t{0.f, 0.f, 0.f, 0.f}, f32x4m_t{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+  for (int j = 0; j < P::JB; ++j) {
+    const u32x4m_t w = b.w[j];
+    const bf16x2m_t p0 = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(w.x, 1.0f, false);
+    const bf16x2m_t p1 = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(w.x, 1.0f, true);
+    const bf16x2m_t p2 = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(w.y, 1.0f, false);
+    const bf16x2m_t p3 = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(w.y, 1.0f, true);
+    const bf16x8m_t b0 = bf16x8m_t{p0[0], p0[1], p1[0], p1[1], p2[0], p2[1], p3[0], p3[1]};
+    const bf16x2m_t q0 = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(w.z, 1.0f, false);
+    const bf16x2m_t q1 = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(w.z, 1.0f, true);
+    const bf16x2m_t q2 = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(w.w, 1.0f, false);
+    const bf16x2m_t q3 = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(w.w, 1.0f, true);
+    const bf16x8m_t b1 = bf16x8m_t{q0[0], q0[1], q1[0], q1[1], q2[0], q2[1], q3[0], q3[1]};
+    const int ka = 64 * j + 16 * g;
+#pragma unroll
+    for (int rb = 0; rb < 2; ++rb) {
+      const int m = min(rb * 16 + fr, M - 1);
+      const bf16x8m_t a0 = *reinterpret_cast<const bf16x8m_t*>(as + m * P::LDA_S + ka);
+      const bf16x8m_t a1 = *reinterpret_cast<const bf16x8m_t*>(as + m * P::LDA_S + ka + 8);
+      acc[rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b0, a0, acc[rb], 0, 0, 0);
+      acc[rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b1, a1, acc[rb], 0, 0, 0);
+    }
+  }
+  const int n = tile * P::NT + wid * 16 + 4 * g;
+  if (n >= N) return;
+  const float4 sc = b.sc;
+  float* o = out + split * split_stride;
+#pragma unroll
+  for (int rb = 0; rb < 2; ++rb) {
+    const int m = rb * 16 + fr;
+    if (m < M)
+      *reinterpret_cast<float4*>(o + (long)m * ldo + n) =
+          make_float4(acc[rb][0] * sc.x, acc[rb][1] * sc.y, acc[rb][2] * sc.z, acc[rb][3] * sc.w);
+  }
+}
+
+// PER items per workgroup, a compile-time count: the loop unrolls and every next-item issue is
+// unconditional (a conditional issue makes the compiler's counted waits fall back to waiting for
+// every load in flight).  The last workgroup's run is clamped to the final item: it recomputes
+// and rewrites identical values.
+template <int WAVES, int PER>
+__global__ __launch_bounds__(64 * WAVES) void fp8_gemm_stream_kernel(
+    const bf16_t* __restrict__ A, int lda, const uint8_t* __restrict__ W8,
+    const float* __restrict__ scale, int M, int N, int K, float* __restrict__ out,
+    long split_stride, int ldo, int ntiles) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  bf16_t* as = reinterpret_cast<bf16_t*>(smem);
+  const int last = ntiles * (K / F8_KC) - 1;
+  const int i0 = blockIdx.x * PER;                 // grid = cdiv(items, PER)
+  F8Item buf[2];
+  int asplit = -1;
+  f8s_issue<WAVES>(buf[0], W8, scale, N, K, ntiles, min(i0, last));
+#pragma unroll
+  for (int t = 0; t < PER; ++t) {
+    const int it = min(i0 + t, last);
+    if (it / ntiles != asplit) { asplit = it / ntiles; f8s_load_a<WAVES>(as, A, lda, M, asplit); }
+    if (t + 1 < PER)
+      f8s_issue<WAVES>(buf[(t + 1) & 1], W8, scale, N, K, ntiles, min(i0 + t + 1, last));
+    // keep the next item's loads ahead of this item's MFMAs (the scheduler would otherwise sink
+    // them below the compute to save registers, and the stream would drain every item)
+    __builtin_amdgcn_sched_barrier(0);
+    f8s_compute<WAVES>(buf[t & 1], as, M, N, out, split_stride, ldo, ntiles, it);
+    __builtin_amdgcn_sched_barrier(0);
   }
 }
 
@@ -377,7 +526,29 @@ extern "C" int zs_fp8_gemm_rows(const void* A, int lda, const void* W8, const fl
                          dim3(64 * W_), lds, st, (const bf16_t*)A, lda, (const uint8_t*)W8, scale, \
                          M, N, K, out, split_stride, ldo, g_fp8_dbg);                            \
   } while (0)
-  if ((long)cdiv(N, 256) * splits >= 256 && g_fp8_tile != 1) F8L(2, 8);
+  // long streams at M <= 32 (more than one item of 128 columns x 1024 k per CU): persistent kernel
+  static int ncu = 0;
+  if (ncu == 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        ncu <= 0)
+      ncu = 256;
+  }
+  const long items = (long)cdiv(N, 128) * splits;
+  if (M <= 32 && g_fp8_tile == 0 && items > ncu && items <= 8L * ncu) {
+    const long per = (items + ncu - 1) / ncu;
+#define F8S(P_)                                                                                 \
+  hipLaunchKernelGGL((fp8_gemm_stream_kernel<8, P_>), dim3((unsigned)((items + P_ - 1) / P_)),  \
+                     dim3(512), (size_t)32 * (F8_KC + 8) * 2, st, (const bf16_t*)A, lda,        \
+                     (const uint8_t*)W8, scale, M, N, K, out, split_stride, ldo, cdiv(N, 128))
+    if (per <= 2) F8S(2);
+    else if (per <= 3) F8S(3);
+    else if (per <= 4) F8S(4);
+    else if (per <= 6) F8S(6);
+    else F8S(8);
+#undef F8S
+  } else if ((long)cdiv(N, 256) * splits >= 256 && g_fp8_tile != 1) F8L(2, 8);
   else if ((long)cdiv(N, 128) * splits >= 256 && g_fp8_tile != 1) F8L(1, 8);
   else F8L(1, 4);
 #undef F8L

@@ -70,6 +70,24 @@ def dequantize_fp8(q: torch.Tensor, scale: torch.Tensor) -> torch.Tensor:
     return q.view(torch.float8_e4m3fn).float() * scale[:, None].float()
 
 
+def fp8_pack_tiles(q: torch.Tensor) -> torch.Tensor:
+    """Row-major fp8 codes [N, K] (K % 1024 == 0) -> the tile-packed stream zs_fp8_gemm_rows reads
+    (csrc/mistral.hip): [K/1024][ceil(N/128)][8][16][64 lanes][16 B], i.e. the 1 KiB block of
+    (k split s, 128-column tile t, 16-column group w, 64-deep k block j) holds, in lane l,
+    W[128 t + 16 w + (l & 15)][1024 s + 64 j + 16 (l >> 4) .. +16]; rows past N are zero.  Every
+    wave-load of the GEMM is then one contiguous KiB and a workgroup's run of items one
+    contiguous stretch of HBM."""
+    N, K = q.shape
+    if K % 1024:
+        raise ValueError(f"fp8_pack_tiles: K={K} must be a multiple of 1024")
+    NT = -(-N // 128)
+    if NT * 128 != N:
+        q = torch.cat([q, q.new_zeros(NT * 128 - N, K)])
+    # [t, w, fr, s, j, g, 16] -> [s, t, w, j, g, fr, 16]
+    v = q.reshape(NT, 8, 16, K // 1024, 16, 4, 16).permute(3, 0, 1, 4, 5, 2, 6)
+    return v.contiguous().view(-1)
+
+
 class MistralWeights:
     """Packed decoder weights from MistralForCausalLM keys (``model.*``, ``lm_head.weight``)."""
 
@@ -146,7 +164,8 @@ class MistralWeights:
         N, K = w.shape
         if self.mode == "fp8":
             q, s = quantize_fp8(w)
-            return {"N": N, "K": K, "w8": q.to(self.dev).contiguous(), "scale": s.to(self.dev).contiguous()}
+            return {"N": N, "K": K, "w8": fp8_pack_tiles(q.to(self.dev)),
+                    "scale": s.to(self.dev).contiguous()}
         return {"N": N, "K": K, "w": w.to(self.dev, self.adt).contiguous()}
 
     def nbytes(self) -> int:
