@@ -641,6 +641,8 @@ def main_mistral(args, device):
     tags = {"en": [1, 523, 269, 28767], "zh": [1, 523, 26715, 28767], "fr": [1, 523, 1642, 28767]}
     tags = {k: torch.tensor(v, dtype=torch.int32, device=device) for k, v in tags.items()}
     dec = MistralDecoder(w, max_batch=B, max_prompt=Hc + 10 + 4, max_new=60)
+    dec.fused_decode_attn = os.environ.get("ZS_MISTRAL_FUSED_ATTN", "1") != "0"   # A/B knobs
+    dec.use_graph = os.environ.get("ZS_MISTRAL_GRAPH", "1") != "0"
     n = args.steps or 2
     wav = synthetic_clips(B, 0, device)
 
@@ -661,15 +663,18 @@ def main_mistral(args, device):
         ntok += sum(len(r) for lang in res for r in lang)
     torch.cuda.synchronize()
     dt_s = time.perf_counter() - t0
-    # decode-step roofline: one 32-row step (M = 32, rows_per_seq 1) timed with HIP events
+    # decode-step roofline: one 32-row greedy step (M = 32, rows_per_seq 1: embed, 32 layers,
+    # LM-head argmax, stop bookkeeping) as generate runs it (graph replay), timed with HIP events
     dec.next_tok.zero_()
+    for t in (dec.step_ctr, dec.done, dec.all_done):
+        t.zero_()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     reps = 10
     dec.pos[:B].fill_(30)
+    dec.decode_step(B)                              # captured already by generate
     e0.record()
     for _ in range(reps):
-        dec._layers(B, 1)
-        dec._lm_argmax(dec.h[:B], B)
+        dec.decode_step(B)
     e1.record()
     e1.synchronize()
     step_s = e0.elapsed_time(e1) / 1e3 / reps

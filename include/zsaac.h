@@ -298,6 +298,14 @@ int zs_mistral_attention(const void* q, int M, int H, int KVH, const int* pos, i
                          const void* kc, const void* vc, int Lmax, void* out, int dtype,
                          void* stream);
 
+/* zs_mistral_decode_attention: one decode step (row m = sequence m, new position pos[m]):
+ * zs_mistral_rope_kv + zs_mistral_attention (rows_per_seq 1) in one launch -- q / k / v summed
+ * from the slabs and rotated in registers, k / v row pos[m] appended to the caches, keys
+ * 0..pos[m]-1 read from them and key pos[m] from registers. */
+int zs_mistral_decode_attention(const float* qkv, int nsplit, long ss, int M, int H, int KVH,
+                                const int* pos, const float* cosb, const float* sinb, void* kc,
+                                void* vc, int Lmax, void* out, int dtype, void* stream);
+
 /* ------------------------------------------------------------------ GPT-2 decode
  * zs_gpt2_prefill_embed: clap_to_gpt (caption_model.py:315-329) + the caller's wte lookup
  * (predict_prompt.py:133) + GPT-2 input embedding:  row b, position p < P_b = hard_len[b]+n_soft:

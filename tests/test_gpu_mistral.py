@@ -128,3 +128,38 @@ def test_dropin_clap_caption_mistralai(cuda, golden):
         ids = m.LMmodel.generate(inputs_embeds=pe, attention_mask=am, do_sample=False,
                                  max_length=60, eos_token_id=2, pad_token_id=2)
     assert torch.equal(ids.cpu(), torch.from_numpy(g["ids_en"]))
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_decode_attention_fused_vs_unfused(cuda, dt):
+    """zs_mistral_decode_attention (RoPE + KV append + attention in one launch, the decode step)
+    against zs_mistral_rope_kv + zs_mistral_attention on the same slabs and caches: identical
+    cache rows, outputs within f32 reassociation (the key p term joins the softmax last)."""
+    from zsaac import ops
+    from zsaac._lib import call
+    M, H, KVH, Lmax, ns = 5, 8, 2, 40, 3
+    NQKV = (H + 2 * KVH) * 128
+    g = torch.Generator().manual_seed(1)
+    slab = torch.randn(ns, M, NQKV, generator=g).to(cuda)
+    pos = torch.tensor([0, 3, 17, 38, 39], dtype=torch.int32).to(cuda)
+    inv = 1.0 / (10000.0 ** (torch.arange(0, 128, 2).float() / 128))
+    fr = torch.arange(Lmax).float()[:, None] * inv[None]
+    cos, sin = fr.cos().to(cuda).contiguous(), fr.sin().to(cuda).contiguous()
+    kc = torch.randn(M, KVH, Lmax, 128, generator=g).to(cuda, dt)
+    vc = torch.randn(M, KVH, Lmax, 128, generator=g).to(cuda, dt)
+    kc2, vc2 = kc.clone(), vc.clone()
+    q = torch.empty(M, H * 128, device=cuda, dtype=dt)
+    a1, a2 = torch.empty_like(q), torch.empty_like(q)
+    st = torch.cuda.current_stream().cuda_stream
+    call("zs_mistral_rope_kv", slab.data_ptr(), ns, M * NQKV, M, H, KVH, pos.data_ptr(), 1,
+         cos.data_ptr(), sin.data_ptr(), q.data_ptr(), kc.data_ptr(), vc.data_ptr(), Lmax,
+         ops.dt(q), st)
+    call("zs_mistral_attention", q.data_ptr(), M, H, KVH, pos.data_ptr(), 1, kc.data_ptr(),
+         vc.data_ptr(), Lmax, a1.data_ptr(), ops.dt(q), st)
+    call("zs_mistral_decode_attention", slab.data_ptr(), ns, M * NQKV, M, H, KVH, pos.data_ptr(),
+         cos.data_ptr(), sin.data_ptr(), kc2.data_ptr(), vc2.data_ptr(), Lmax, a2.data_ptr(),
+         ops.dt(q), st)
+    torch.cuda.synchronize()
+    assert torch.equal(kc, kc2) and torch.equal(vc, vc2)
+    tol = 2e-5 if dt == torch.float32 else 2e-2
+    assert float((a1.float() - a2.float()).abs().max()) < tol

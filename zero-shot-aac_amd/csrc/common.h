@@ -61,6 +61,13 @@ template <> struct Cvt<bf16_t> {
 };
 template <typename T> __device__ __forceinline__ float ldf(const T* p) { return Cvt<T>::to_f(*p); }
 template <typename T> __device__ __forceinline__ void stf(T* p, float v) { *p = Cvt<T>::from_f(v); }
+// 4 consecutive values in one store (16 B f32 / 8 B bf16; p aligned to that)
+__device__ __forceinline__ void st4(float* p, float a, float b, float c, float d) {
+  *reinterpret_cast<float4*>(p) = make_float4(a, b, c, d);
+}
+__device__ __forceinline__ void st4(bf16_t* p, float a, float b, float c, float d) {
+  *reinterpret_cast<uint2*>(p) = make_uint2(pk2bf(a, b), pk2bf(c, d));
+}
 
 // ---------------------------------------------------------------- wave64 reductions
 __device__ __forceinline__ float wave_sum(float v) {

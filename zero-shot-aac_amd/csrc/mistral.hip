@@ -327,24 +327,34 @@ __global__ __launch_bounds__(1024) void mistral_add_rmsnorm_kernel(
     float* __restrict__ x, const float* __restrict__ y, int nsplit, long ss, int D, float eps,
     const float* __restrict__ w, T* __restrict__ h) {
   __shared__ float red[16];
+  constexpr int CMAX = 4;                              // D <= 4 x 4096 (host-checked)
   const int m = blockIdx.x;
   float* xr = x + (long)m * D;
   float q = 0.f;
-  for (int c = 4 * threadIdx.x; c < D; c += 4 * 1024) {
-    float4 v = *reinterpret_cast<const float4*>(xr + c);
+  float4 v[CMAX];                                      // the row stays in registers
+#pragma unroll
+  for (int u = 0; u < CMAX; ++u) {
+    const int c = 4 * threadIdx.x + 4096 * u;
+    if (c >= D) break;
+    v[u] = *reinterpret_cast<const float4*>(xr + c);
     if (y) {
       const float4 a = slab_sum4(y + (long)m * D + c, nsplit, ss);
-      v.x += a.x; v.y += a.y; v.z += a.z; v.w += a.w;
-      *reinterpret_cast<float4*>(xr + c) = v;
+      v[u].x += a.x; v[u].y += a.y; v[u].z += a.z; v[u].w += a.w;
+      *reinterpret_cast<float4*>(xr + c) = v[u];
     }
-    q += (v.x * v.x + v.y * v.y) + (v.z * v.z + v.w * v.w);
+    q += (v[u].x * v[u].x + v[u].y * v[u].y) + (v[u].z * v[u].z + v[u].w * v[u].w);
   }
   const float r = rsqrtf(block_sum(q, red) / D + eps);
-  for (int c = 4 * threadIdx.x; c < D; c += 4 * 1024) {
-    const float4 v = *reinterpret_cast<const float4*>(xr + c);
-    const float o[4] = {v.x * r, v.y * r, v.z * r, v.w * r};
 #pragma unroll
-    for (int t = 0; t < 4; ++t) stf(h + (long)m * D + c + t, w ? w[c + t] * o[t] : o[t]);
+  for (int u = 0; u < CMAX; ++u) {
+    const int c = 4 * threadIdx.x + 4096 * u;
+    if (c >= D) break;
+    float o[4] = {v[u].x * r, v[u].y * r, v[u].z * r, v[u].w * r};
+    if (w) {
+#pragma unroll
+      for (int t = 0; t < 4; ++t) o[t] *= w[c + t];
+    }
+    st4(h + (long)m * D + c, o[0], o[1], o[2], o[3]);
   }
 }
 
@@ -416,8 +426,10 @@ __global__ __launch_bounds__(256) void mistral_silu_mul_kernel(const float* __re
   const float4 gt = slab_sum4(gu + (long)m * 2 * F + f, nsplit, ss);
   const float4 up = slab_sum4(gu + (long)m * 2 * F + F + f, nsplit, ss);
   const float g4[4] = {gt.x, gt.y, gt.z, gt.w}, u4[4] = {up.x, up.y, up.z, up.w};
+  float o[4];
 #pragma unroll
-  for (int t = 0; t < 4; ++t) stf(act + idx + t, g4[t] / (1.0f + expf(-g4[t])) * u4[t]);   // F.silu * up
+  for (int t = 0; t < 4; ++t) o[t] = g4[t] / (1.0f + expf(-g4[t])) * u4[t];   // F.silu * up
+  st4(act + idx, o[0], o[1], o[2], o[3]);
 }
 
 // causal GQA attention, one wave per (query row m, q head h): keys 0..pos[m] of the sequence
@@ -493,6 +505,128 @@ __global__ __launch_bounds__(256) void mistral_attn_kernel(const T* __restrict__
     T* orow = out + (long)m * H * HD + h * HD + sub * DPL;
 #pragma unroll
     for (int d = 0; d < DPL; ++d) stf(orow + d, o[d] * inv);
+  }
+}
+
+// Decode step (one new position per sequence, rows_per_seq = 1): RoPE + KV append fused into the
+// attention.  Wave (row m, q head h) sums its q slice and its kv head's new k / v slices from the
+// qkv slabs, rotates q and k (the dims d and d + 64 of a pair sit in lanes sub and sub ^ 4), scores
+// keys 0..p-1 from the caches as mistral_attn_kernel does and key p = pos[m] from registers; the
+// first q head of each kv head (group 0 lanes) writes k / v row p to the caches for later steps.
+// Same sums, rotation and softmax arithmetic as mistral_rope_kv_kernel + mistral_attn_kernel.
+template <typename T>
+__global__ __launch_bounds__(256) void mistral_decode_attn_kernel(
+    const float* __restrict__ qkv, int nsplit, long ss, int M, int H, int KVH,
+    const int* __restrict__ pos, const float* __restrict__ cosb, const float* __restrict__ sinb,
+    T* __restrict__ kc, T* __restrict__ vc, int Lmax, T* __restrict__ out) {
+  constexpr int HD = 128, HALF = 64, DPL = 16, U = 4;
+  const int lane = threadIdx.x & 63;
+  const int w = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (w >= M * H) return;
+  const int grp = lane >> 3, sub = lane & 7;
+  const int m = w / H, h = w % H, kvh = h / (H / KVH);
+  const int p = __builtin_amdgcn_readfirstlane(pos[m]);
+  const long NQKV = (long)(H + 2 * KVH) * HD;
+  const float* src = qkv + m * NQKV + sub * DPL;
+  float qv[DPL], kn[DPL], vn[DPL];
+#pragma unroll
+  for (int d = 0; d < DPL; d += 4) {
+    const float4 a = slab_sum4(src + h * HD + d, nsplit, ss);
+    const float4 b = slab_sum4(src + (H + kvh) * HD + d, nsplit, ss);
+    const float4 c = slab_sum4(src + (H + KVH + kvh) * HD + d, nsplit, ss);
+    qv[d] = a.x; qv[d + 1] = a.y; qv[d + 2] = a.z; qv[d + 3] = a.w;
+    kn[d] = b.x; kn[d + 1] = b.y; kn[d + 2] = b.z; kn[d + 3] = b.w;
+    vn[d] = c.x; vn[d + 1] = c.y; vn[d + 2] = c.z; vn[d + 3] = c.w;
+  }
+  {
+    // rotary pair (i, i + 64): lo = a c - b s, hi = b c + a s with a = dim i, b = dim i + 64
+    const bool lo = sub < 4;
+    const float* cr = cosb + (long)p * HALF + (sub & 3) * DPL;
+    const float* sr = sinb + (long)p * HALF + (sub & 3) * DPL;
+#pragma unroll
+    for (int d = 0; d < DPL; ++d) {
+      const float c = cr[d], sn = sr[d];
+      const float qo = __shfl_xor(qv[d], 4, 64), ko = __shfl_xor(kn[d], 4, 64);
+      qv[d] = lo ? qv[d] * c - qo * sn : qv[d] * c + qo * sn;
+      kn[d] = lo ? kn[d] * c - ko * sn : kn[d] * c + ko * sn;
+    }
+  }
+  const long base = ((long)m * KVH + kvh) * Lmax;
+  if (h % (H / KVH) == 0 && grp == 0) {
+    T* kr = kc + (base + p) * HD + sub * DPL;
+    T* vr = vc + (base + p) * HD + sub * DPL;
+#pragma unroll
+    for (int d = 0; d < DPL; d += 4) {
+      st4(kr + d, kn[d], kn[d + 1], kn[d + 2], kn[d + 3]);
+      st4(vr + d, vn[d], vn[d + 1], vn[d + 2], vn[d + 3]);
+    }
+  }
+  // the cached operands are T: round q and the new k / v as the unfused path stores them
+#pragma unroll
+  for (int d = 0; d < DPL; ++d) {
+    qv[d] = Cvt<T>::to_f(Cvt<T>::from_f(qv[d]));
+    kn[d] = Cvt<T>::to_f(Cvt<T>::from_f(kn[d]));
+    vn[d] = Cvt<T>::to_f(Cvt<T>::from_f(vn[d]));
+  }
+  const float scale = 0.08838834764831845f;                      // 128^-0.5
+  float mx = -INFINITY, l = 0.f, o[DPL];
+#pragma unroll
+  for (int d = 0; d < DPL; ++d) o[d] = 0.f;
+  auto update = [&](float sv, const float* vf) {
+    float pm = fmaxf(sv, __shfl_xor(sv, 8, 64));
+    pm = fmaxf(pm, __shfl_xor(pm, 16, 64));
+    pm = fmaxf(pm, __shfl_xor(pm, 32, 64));
+    const float mn = fmaxf(mx, pm);
+    float corr, e;
+    if constexpr (sizeof(T) == 4) { corr = expf(mx - mn); e = expf(sv - mn); }   // parity mode
+    else { corr = __expf(mx - mn); e = __expf(sv - mn); }
+    l = l * corr + e;
+#pragma unroll
+    for (int d = 0; d < DPL; ++d) o[d] = o[d] * corr + e * vf[d];
+    mx = mn;
+  };
+  for (int j0 = 0; j0 < p; j0 += 8 * U) {
+    float kf[U][DPL], vf[U][DPL];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int j = min(j0 + 8 * u + grp, p - 1);
+      const T* kr = kc + (base + j) * HD + sub * DPL;
+      const T* vr = vc + (base + j) * HD + sub * DPL;
+#pragma unroll
+      for (int d = 0; d < DPL; ++d) { kf[u][d] = ldf(kr + d); vf[u][d] = ldf(vr + d); }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      float sv = 0.f;
+#pragma unroll
+      for (int d = 0; d < DPL; ++d) sv += qv[d] * kf[u][d];
+      sv += __shfl_xor(sv, 1, 64);
+      sv += __shfl_xor(sv, 2, 64);
+      sv += __shfl_xor(sv, 4, 64);
+      update((j0 + 8 * u + grp < p) ? sv * scale : -INFINITY, vf[u]);
+    }
+  }
+  {                                                              // key p (group 0 counts it)
+    float sv = 0.f;
+#pragma unroll
+    for (int d = 0; d < DPL; ++d) sv += qv[d] * kn[d];
+    sv += __shfl_xor(sv, 1, 64);
+    sv += __shfl_xor(sv, 2, 64);
+    sv += __shfl_xor(sv, 4, 64);
+    update(grp == 0 ? sv * scale : -INFINITY, vn);
+  }
+#pragma unroll
+  for (int x = 8; x < 64; x <<= 1) {
+    l += __shfl_xor(l, x, 64);
+#pragma unroll
+    for (int d = 0; d < DPL; ++d) o[d] += __shfl_xor(o[d], x, 64);
+  }
+  if (grp == 0) {
+    const float inv = 1.0f / l;
+    T* orow = out + (long)m * H * HD + h * HD + sub * DPL;
+#pragma unroll
+    for (int d = 0; d < DPL; d += 4)
+      st4(orow + d, o[d] * inv, o[d + 1] * inv, o[d + 2] * inv, o[d + 3] * inv);
   }
 }
 
@@ -578,8 +712,10 @@ extern "C" int zs_mistral_add_rmsnorm(float* x, const float* y, int nsplit, long
                                       void* stream) {
   ZS_REQUIRE(M > 0 && D > 0 && x && h && (y == nullptr || nsplit >= 1),
              "zs_mistral_add_rmsnorm: bad arguments");
-  ZS_REQUIRE(D % 4 == 0 && ss % 4 == 0 && ((uintptr_t)x & 15) == 0 && (!y || ((uintptr_t)y & 15) == 0),
-             "zs_mistral_add_rmsnorm: D, split stride multiples of 4, 16-byte aligned rows");
+  ZS_REQUIRE(D % 4 == 0 && D <= 16384 && ss % 4 == 0 && ((uintptr_t)x & 15) == 0 &&
+                 ((uintptr_t)h & 15) == 0 && (!y || ((uintptr_t)y & 15) == 0),
+             "zs_mistral_add_rmsnorm: D <= 16384, D and split stride multiples of 4, 16-byte "
+             "aligned rows");
   if (hdtype == ZS_BF16)
     hipLaunchKernelGGL(mistral_add_rmsnorm_kernel<bf16_t>, dim3(M), dim3(1024), 0, S(stream), x,
                        y, nsplit, ss, D, eps, w, (bf16_t*)h);
@@ -612,7 +748,8 @@ extern "C" int zs_mistral_rope_kv(const float* qkv, int nsplit, long ss, int M, 
 extern "C" int zs_mistral_silu_mul(const float* gu, int nsplit, long ss, int M, int F, void* act,
                                    int dtype, void* stream) {
   ZS_REQUIRE(M > 0 && F > 0 && nsplit >= 1, "zs_mistral_silu_mul: bad shape");
-  ZS_REQUIRE(F % 4 == 0 && ss % 4 == 0, "zs_mistral_silu_mul: F and the split stride %% 4");
+  ZS_REQUIRE(F % 4 == 0 && ss % 4 == 0 && ((uintptr_t)gu & 15) == 0 && ((uintptr_t)act & 15) == 0,
+             "zs_mistral_silu_mul: F and the split stride %% 4, 16-byte aligned buffers");
   const int nb = cdiv((long)M * F / 4, 256);
   if (dtype == ZS_BF16)
     hipLaunchKernelGGL(mistral_silu_mul_kernel<bf16_t>, dim3(nb), dim3(256), 0, S(stream), gu,
@@ -637,6 +774,28 @@ extern "C" int zs_mistral_attention(const void* q, int M, int H, int KVH, const 
   else
     hipLaunchKernelGGL(mistral_attn_kernel<float>, grid, dim3(256), 0, S(stream), (const float*)q,
                        M, H, KVH, pos, rows_per_seq, (const float*)kc, (const float*)vc, Lmax,
+                       (float*)out);
+  ZS_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int zs_mistral_decode_attention(const float* qkv, int nsplit, long ss, int M, int H,
+                                           int KVH, const int* pos, const float* cosb,
+                                           const float* sinb, void* kc, void* vc, int Lmax,
+                                           void* out, int dtype, void* stream) {
+  ZS_REQUIRE(M > 0 && H > 0 && KVH > 0 && H % KVH == 0 && nsplit >= 1 && Lmax > 0,
+             "zs_mistral_decode_attention: bad shape");
+  ZS_REQUIRE(ss % 4 == 0 && ((uintptr_t)qkv & 15) == 0 && ((uintptr_t)kc & 15) == 0 &&
+                 ((uintptr_t)vc & 15) == 0 && ((uintptr_t)out & 15) == 0,
+             "zs_mistral_decode_attention: 16-byte aligned buffers, split stride %% 4");
+  const dim3 grid(cdiv((long)M * H, 4));
+  if (dtype == ZS_BF16)
+    hipLaunchKernelGGL(mistral_decode_attn_kernel<bf16_t>, grid, dim3(256), 0, S(stream), qkv,
+                       nsplit, ss, M, H, KVH, pos, cosb, sinb, (bf16_t*)kc, (bf16_t*)vc, Lmax,
+                       (bf16_t*)out);
+  else
+    hipLaunchKernelGGL(mistral_decode_attn_kernel<float>, grid, dim3(256), 0, S(stream), qkv,
+                       nsplit, ss, M, H, KVH, pos, cosb, sinb, (float*)kc, (float*)vc, Lmax,
                        (float*)out);
   ZS_LAUNCH_CHECK();
   return 0;

@@ -81,6 +81,7 @@ SIGNATURES = {
     "zs_mistral_rope_kv": [P, I, L, I, I, I, P, I, P, P, P, P, P, I, I, P],
     "zs_mistral_silu_mul": [P, I, L, I, I, P, I, P],
     "zs_mistral_attention": [P, I, I, I, P, I, P, P, I, P, I, P],
+    "zs_mistral_decode_attention": [P, I, L, I, I, I, P, P, P, P, P, I, P, I, P],
     "zs_magic_step": [P, P, I, I, I, I, I, I, I, P, P, P, P, P, I, P, I, P, P, P, P, P, I, P],
 }
 

@@ -186,6 +186,9 @@ class MistralDecoder:
         self.w = w
         dev, adt = w.dev, w.adt
         self.B, self.Pmax, self.max_new = max_batch, max_prompt, max_new
+        self.fused_decode_attn = True     # False: decode through rope_kv + attention (A/B, tests)
+        self.use_graph = True             # decode steps replayed from hipGraphs (decode_step)
+        self.graphs = {}
         self.Lmax = max_prompt + max_new + 1
         Mp = max_batch * max_prompt
         D, H, KVH, HD, F = w.D, w.H, w.KVH, w.HD, w.F
@@ -248,12 +251,19 @@ class MistralDecoder:
         self._norm(M, None, 1, 0, w.layers[0]["ln1"])
         for l, ly in enumerate(w.layers):
             y, ns, ss = self._gemm(self.h, ly["qkv"], M)
-            call("zs_mistral_rope_kv", y.data_ptr(), ns, ss, M, w.H, w.KVH, self.pos.data_ptr(),
-                 rows_per_seq, self.cos.data_ptr(), self.sin.data_ptr(), self.q.data_ptr(),
-                 self.kc[l].data_ptr(), self.vc[l].data_ptr(), self.Lmax, dt, st)
-            call("zs_mistral_attention", self.q.data_ptr(), M, w.H, w.KVH, self.pos.data_ptr(),
-                 rows_per_seq, self.kc[l].data_ptr(), self.vc[l].data_ptr(), self.Lmax,
-                 self.att.data_ptr(), dt, st)
+            if rows_per_seq == 1 and self.fused_decode_attn:    # decode: RoPE + append + attention
+                call("zs_mistral_decode_attention", y.data_ptr(), ns, ss, M, w.H, w.KVH,
+                     self.pos.data_ptr(), self.cos.data_ptr(), self.sin.data_ptr(),
+                     self.kc[l].data_ptr(), self.vc[l].data_ptr(), self.Lmax,
+                     self.att.data_ptr(), dt, st)
+            else:                                                # prefill: P rows per sequence
+                call("zs_mistral_rope_kv", y.data_ptr(), ns, ss, M, w.H, w.KVH,
+                     self.pos.data_ptr(), rows_per_seq, self.cos.data_ptr(), self.sin.data_ptr(),
+                     self.q.data_ptr(), self.kc[l].data_ptr(), self.vc[l].data_ptr(), self.Lmax,
+                     dt, st)
+                call("zs_mistral_attention", self.q.data_ptr(), M, w.H, w.KVH,
+                     self.pos.data_ptr(), rows_per_seq, self.kc[l].data_ptr(),
+                     self.vc[l].data_ptr(), self.Lmax, self.att.data_ptr(), dt, st)
             y, ns, ss = self._gemm(self.att, ly["o"], M)
             self._norm(M, y, ns, ss, ly["ln2"])
             y, ns, ss = self._gemm(self.h, ly["gu"], M)
@@ -295,15 +305,35 @@ class MistralDecoder:
         for s in range(1, new):
             if s % 8 == 0 and int(self.all_done[0]):
                 break
-            call("zs_mistral_embed", None, 0, None, 0, None, 0, self.next_tok.data_ptr(),
-                 w.emb.data_ptr(), w.D, B, self.x.data_ptr(), ops.dt(w.emb), st)
-            self._layers(B, 1)
-            self._lm_argmax(self.h[:B], B)
-            ops.greedy_step(self.pval, self.pidx, B, self.nblk, self.step_ctr, self.max_new, eos,
-                            eos, self.out_ids, self.out_len, self.done, self.pos, self.next_tok,
-                            self.all_done)
+            self.decode_step(B, eos)
         ids, ln = self.out_ids[:B].cpu(), self.out_len[:B].cpu()
         return [ids[b, :int(ln[b])].tolist() for b in range(B)]
+
+    def _step_body(self, B, eos):
+        w, st = self.w, torch.cuda.current_stream().cuda_stream
+        call("zs_mistral_embed", None, 0, None, 0, None, 0, self.next_tok.data_ptr(),
+             w.emb.data_ptr(), w.D, B, self.x.data_ptr(), ops.dt(w.emb), st)
+        self._layers(B, 1)
+        self._lm_argmax(self.h[:B], B)
+        ops.greedy_step(self.pval, self.pidx, B, self.nblk, self.step_ctr, self.max_new, eos, eos,
+                        self.out_ids, self.out_len, self.done, self.pos, self.next_tok,
+                        self.all_done)
+
+    def decode_step(self, B: int, eos: int = 2):
+        """One greedy step of B sequences (every operand on the device: token ids, positions, KV
+        caches, stop flags), replayed from a hipGraph captured on first use per (B, eos): the
+        ~290 launches of a 32-layer step are one graph launch instead of ~290 host round trips
+        through the C-ABI."""
+        if not self.use_graph:
+            return self._step_body(B, eos)
+        key = (B, eos, self.fused_decode_attn)
+        g = self.graphs.get(key)
+        if g is None:
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):                 # capture only: nothing runs here
+                self._step_body(B, eos)
+            self.graphs[key] = g
+        g.replay()
 
     def generate_embeds(self, embeds: torch.Tensor, max_length: int = 60,
                         eos: int = 2) -> List[List[int]]:
