@@ -21,3 +21,11 @@ head -12 $O/dec64_kstats.txt
 timeout -s KILL 300 rocprofv3 --kernel-trace --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --output-format csv -d $O/pm -o run -- python3 tools/pmc_mfma.py run > $O/pmc.log 2>&1 || { tail $O/pmc.log; exit 1; }
 python3 tools/pmc_mfma.py parse $O/pm $O/pmc_mfma.json > $O/pmc_mfma.txt && rm -rf $O/pm
 head -8 $O/pmc_mfma.txt
+timeout -k 10 300 python bench.py --mistral > $O/mistral_bench.json 2> $O/mistral.err || { tail $O/mistral.err; exit 1; }
+cut -c1-200 $O/mistral_bench.json
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/mp -o run -- python3 bench.py --mistral > $O/mp.json 2> $O/mp.err || { tail $O/mp.err; exit 1; }
+cp $(find $O/mp -name "*kernel_stats.csv" | head -1) $O/mistral_kernel_stats.csv && rm -rf $O/mp
+timeout -k 10 120 python tools/fp8_mbench.py > $O/fp8_mbench.txt 2>&1 || { tail $O/fp8_mbench.txt; exit 1; }
+timeout -k 10 120 python tools/swin_bench.py 0,1 > $O/swin_bench.txt 2>&1 || { tail $O/swin_bench.txt; exit 1; }
+timeout -k 10 400 python bench.py --magic > $O/magic_bench.json 2> $O/magic.err || { tail $O/magic.err; exit 1; }
+cut -c1-200 $O/magic_bench.json
