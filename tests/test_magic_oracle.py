@@ -71,3 +71,33 @@ def test_magic_search_vs_reference(gold, sds):
     ids = OM.magic_search(pe, csd, WordTokenizer().decode, enc, emb, float(bsd["temp"]),
                           beam_width=15, decoding_len=pe.shape[1] + 10)
     assert ids == gold["search_ids"][1, :gold["search_len"][1]].tolist()
+
+
+def test_tokenize_pieces_equals_full_tokenization():
+    """The magic decoder's candidate-text tokenisation (prefix up to the head's last space + cached
+    rests, zsaac.bert.tokenize_pieces) gives exactly the ids / lengths of the reference's
+    ``tokenizer(texts, padding='longest', truncation=True, max_length=30)`` call on the full
+    texts, including word-continuing pieces ('q<id>'), punctuation, empty heads and truncation."""
+    import random
+    import torch
+    from transformers import BertTokenizer
+    from zsaac import synthetic as S
+    from zsaac.bert import tokenize, tokenize_pieces
+    from zsaac.magic import MagicDecoder
+    from zsaac.tokenizer import WordTokenizer
+    tok = BertTokenizer(vocab={t: i for i, t in enumerate(S.bert_vocab())}, do_lower_case=True)
+    wt = WordTokenizer()
+    rnd = random.Random(0)
+    C, b, W = 3, 2, 7
+    for s in (0, 1, 4, 19, 40):
+        tok_h = torch.tensor([[rnd.choice([rnd.randrange(50000), 13, 11, 764, 5 * rnd.randrange(9000)])
+                               for _ in range(s)] for _ in range(C * b)], dtype=torch.int32)
+        cand = torch.tensor([rnd.choice([rnd.randrange(50000), 13, 11, 764, 5 * rnd.randrange(9000)])
+                             for _ in range(C * b * W)], dtype=torch.int32)
+        pieces = MagicDecoder._texts(None, wt, cand, tok_h, C, b, W, s)
+        full = [wt.decode(tok_h[j // W, :s].tolist() + [int(cand[j])]) for j in range(C * b * W)]
+        assert [p + r for p, r in pieces] == full
+        for L in (30, 8):
+            i1, l1 = tokenize(tok, full, L, "cpu")
+            i2, l2 = tokenize_pieces(tok, pieces, L, "cpu")
+            assert torch.equal(i1, i2) and torch.equal(l1, l2), (s, L)

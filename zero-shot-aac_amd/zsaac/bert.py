@@ -172,6 +172,64 @@ def _backend(tokenizer, max_length):
     return _BACKENDS[key]
 
 
+_RAW = {}
+
+
+def _to_dev(t, device):
+    if torch.device(device).type == "cpu":
+        return t
+    return t.pin_memory().to(device, non_blocking=True)
+
+
+def _raw_backend(tokenizer):
+    """The fast tokenizer's Rust backend without truncation / padding (pieces are encoded without
+    special tokens and assembled by tokenize_pieces)."""
+    bk = getattr(tokenizer, "backend_tokenizer", None)
+    if bk is None or not getattr(tokenizer, "is_fast", False) or getattr(tokenizer, "padding_side", "right") != "right":
+        return None
+    key = id(tokenizer)
+    if key not in _RAW:
+        from tokenizers import Tokenizer
+        b = Tokenizer.from_str(bk.to_str())
+        b.no_truncation()
+        b.no_padding()
+        _RAW[key] = (b, {})
+    return _RAW[key]
+
+
+def tokenize_pieces(tokenizer, pieces, max_length, device):
+    """``tokenize`` of the texts ``prefix + rest`` for ``pieces = [(prefix, rest), ...]`` where every
+    ``rest`` is empty-prefixed or starts with ' ' (a BERT word boundary: the normalizer and the
+    whitespace / punctuation pre-tokenizer never act across it), so the WordPiece ids of the text
+    are those of the prefix followed by those of the rest.  The magic decoder's 4800 candidate
+    texts per step share one prefix per beam (the text up to the head's last space) and draw
+    their rests from a small set ('' + last word + candidate piece), so both are encoded once per
+    distinct string (the rests cached across steps) instead of 4800 full texts per step.  Ids
+    are [CLS] + (prefix ids + rest ids)[:max_length - 2] + [SEP], padded to the longest with
+    [PAD] -- exactly ``tokenizer(texts, padding='longest', truncation=True, max_length=...)``."""
+    raw = _raw_backend(tokenizer)
+    if raw is None:
+        return tokenize(tokenizer, [p + r for p, r in pieces], max_length, device)
+    bk, cache = raw
+    if len(cache) > 500_000:
+        cache.clear()
+    pre = {p for p, _ in pieces if p}
+    new = list({r for _, r in pieces if r not in cache} | {p for p in pre if p not in cache})
+    if new:
+        for t, e in zip(new, bk.encode_batch(new, add_special_tokens=False)):
+            cache[t] = e.ids
+    cls, sep, pad = tokenizer.cls_token_id, tokenizer.sep_token_id, tokenizer.pad_token_id
+    body = max_length - 2
+    rows = []
+    for p, r in pieces:
+        t = (cache[p] + cache[r]) if p else cache[r]
+        rows.append([cls] + t[:body] + [sep])
+    L = max(len(x) for x in rows)
+    lens = torch.tensor([len(x) for x in rows], dtype=torch.int32)
+    ids = torch.tensor([x + [pad] * (L - len(x)) for x in rows], dtype=torch.int32)
+    return _to_dev(ids, device), _to_dev(lens, device)
+
+
 def tokenize(tokenizer, texts, max_length, device):
     """``tokenizer(texts, padding='longest', truncation=True, max_length=30)`` on the host ->
     device ids [T, L] int32 and lengths [T] int32 (the attention mask as lengths: BERT's
@@ -186,5 +244,4 @@ def tokenize(tokenizer, texts, max_length, device):
                       return_tensors="pt")
         ids = t["input_ids"].to(torch.int32)
         lens = t["attention_mask"].sum(1).to(torch.int32)
-    return (ids.pin_memory().to(device, non_blocking=True),
-            lens.pin_memory().to(device, non_blocking=True))
+    return _to_dev(ids, device), _to_dev(lens, device)

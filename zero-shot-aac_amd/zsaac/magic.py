@@ -31,7 +31,7 @@ from typing import List, Optional, Sequence, Tuple
 import torch
 
 from . import ops
-from .bert import BertTextEngine, tokenize
+from .bert import BertTextEngine, tokenize_pieces
 from .decoder import D, Gpt2Decoder, Gpt2Weights
 
 
@@ -106,11 +106,30 @@ class MagicDecoder:
 
     # ------------------------------------------------------------------ one step
     def _texts(self, tokenizer, cand_h, tok_h, C, b, W, s):
+        """The candidate texts ``tokenizer.decode(tokens so far + candidate)`` (ref
+        gpt2_prefix_eval.py:582-586) as (prefix, rest) pieces for tokenize_pieces: the prefix is
+        the beam's decoded head up to its last space, when the candidate's text starts with it."""
         out = []
+        cand = cand_h.tolist()
+        # a tokenizer whose decode is a concatenation of per-id pieces (concat_decode) decodes a
+        # candidate text as head text + piece; any other decodes the whole id list each time
+        concat = getattr(tokenizer, "concat_decode", False)
+        pieces = {}
         for j in range(C * b):
             head = tok_h[j, :s].tolist()
+            ht = tokenizer.decode(head) if head else ""
+            i = ht.rfind(" ")
+            cut = ht[:i + 1] if i > 0 else None
             for w in range(W):
-                out.append(tokenizer.decode(head + [int(cand_h[j * W + w])]))
+                c = cand[j * W + w]
+                if concat:
+                    pc = pieces.get(c)
+                    if pc is None:
+                        pc = pieces[c] = tokenizer.decode([c])
+                    t = ht + pc
+                else:
+                    t = tokenizer.decode(head + [c])
+                out.append((t[:i], t[i:]) if cut is not None and t.startswith(cut) else ("", t))
         return out
 
     def _run(self, C, b, W, mode, tokenizer, text_tokenizer, audio, alpha, beta, temp, stop,
@@ -135,8 +154,8 @@ class MagicDecoder:
             hf = dec.hf[:R]
             ops.magic_maxcos(hf, R, W, self.ctx, dec.Lmax, self.kvrow, self.pos, self.maxcos)
             ev.synchronize()
-            texts = self._texts(tokenizer, self._cand_h[:R], self._tok_h[:nb, :s], C, b, W, s)
-            ids, lens = tokenize(text_tokenizer, texts, self.text_max_len, self.dev)
+            pieces = self._texts(tokenizer, self._cand_h[:R], self._tok_h[:nb, :s], C, b, W, s)
+            ids, lens = tokenize_pieces(text_tokenizer, pieces, self.text_max_len, self.dev)
             text = self.bert.encode_ids(ids, lens)
             nact = 1 if (s == 0 and not greedy) else b
             ops.magic_score(self.pval, self.maxcos, text, audio, C, b, W, nact, temp, alpha, beta,

@@ -121,6 +121,7 @@ class WordTokenizer:
     ``decode``.  ``encode('.')`` is [13] as in GPT-2."""
 
     _RE = re.compile(r" w\d+|q\d+| \.|\.|,")
+    concat_decode = True    # decode(ids) == "".join(decode([i]) for i in ids)
 
     @staticmethod
     def piece(i: int) -> str:
