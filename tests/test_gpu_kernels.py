@@ -355,22 +355,27 @@ def test_decode_attention_matches_prefill(cuda):
 
 
 @pytest.mark.parametrize("use_kvrow", [False, True])
-@pytest.mark.parametrize("variant", ["small", 6, 5, 4, 3, 2, 1, 0])
+@pytest.mark.parametrize("variant", ["small", "small_s0", "small_s1", "small_s4",
+                                     6, 5, 4, 3, 2, 1, 0])
 def test_decode_attention_bf16(cuda, use_kvrow, variant):
     """bf16 decode attention (register-resident decode_attn5, and the LDS-staged decode_attn4)
     vs an fp32 torch reference: ragged positions 0..Lmax-1 per row, optional beam kvrow
-    indirection, and the new token's k/v appended to the cache.  "small" = the R <= 128 kernel
-    (64-key phases, next phase prefetched) the bs=64 decode takes; the numbered variants are the
-    large-R knobs (small_attn off)."""
+    indirection, and the new token's k/v appended to the cache.  "small*" = the R <= 128 kernels
+    the bs=64 decode takes (attn_split: default 3 = two waves with 32-key phases; s0 one wave
+    with 128-key phases; s1 two waves with 64-key phases; s4 four waves with 32-key phases); the
+    numbered variants are the large-R knobs (small_attn off)."""
     from zsaac import ops
     from zsaac._lib import call
     R, D, H, Lmax = 40, 768, 12, 103
-    call("zs_tune_set", b"small_attn", 1 if variant == "small" else 0)
+    small = isinstance(variant, str)
+    call("zs_tune_set", b"small_attn", 1 if small else 0)
+    if small and variant != "small":
+        call("zs_tune_set", b"attn_split", int(variant[-1]))
     try:
-        _decode_attention_bf16_body(cuda, use_kvrow, 4 if variant == "small" else variant,
-                                    R, D, H, Lmax)
+        _decode_attention_bf16_body(cuda, use_kvrow, 4 if small else variant, R, D, H, Lmax)
     finally:
         call("zs_tune_set", b"small_attn", 1)
+        call("zs_tune_set", b"attn_split", 3)
 
 
 def _decode_attention_bf16_body(cuda, use_kvrow, variant, R, D, H, Lmax):

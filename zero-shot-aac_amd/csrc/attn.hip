@@ -399,7 +399,8 @@ __global__ __launch_bounds__(64 * RA_NW) void row_attn_mfma_kernel(
   }
 }
 
-int g_attn_split = 1;   // zs_tune_set("attn_split", 0): one wave per (row, head) at R <= 128
+int g_attn_split = 3;   // zs_tune_set("attn_split", v) at R <= 128: 0 one wave per (row, head),
+                        // 1 two waves (64-key phases), 3 two waves (32-key), 4 four waves (32-key)
 int g_row_mfma = 1;   // zs_tune_set("row_mfma", 0): the scalar row_attn_kernel for bf16 too
 
 // ------------------------------------------------------------------ GPT-2 decode attention
@@ -633,22 +634,23 @@ __device__ __forceinline__ uint4 bf8_pack(const float (&f)[8]) {
                     pk2bf(f[6], f[7]));
 }
 
-// SPLIT = 2: the keys of one (row, head) are split over two waves of the workgroup (slice s takes
-// phases s, s + 2, ...; 2 heads per workgroup), whose online-softmax states are merged through LDS
-// at the end: twice the waves for the bs=64 decode's 768 (row, head) pairs, each with half the
-// loads in flight (requires heads even, rows without rowmap; no early exit before the barrier).
+// SPLIT = 2 / 4: the keys of one (row, head) are split over SPLIT waves of the workgroup (slice s
+// takes phases s, s + SPLIT, ...; 4 / SPLIT heads per workgroup), whose online-softmax states are
+// merged through LDS at the end: SPLIT times the waves for the bs=64 decode's 768 (row, head)
+// pairs, each with a shorter chain of phases (requires heads % (4 / SPLIT) == 0, rows without
+// rowmap; no early exit before the barrier).
 template <typename T, int KPP = 64, bool PF = false, bool DPP = false, int SPLIT = 1>
 __global__ __launch_bounds__(256) void decode_attn6_kernel(
     const T* __restrict__ qkv, int D, int heads, T* __restrict__ kc, T* __restrict__ vc, int Lmax,
     const int* __restrict__ pos, const int* __restrict__ kvrow, T* __restrict__ out,
     const int* __restrict__ rowmap, const int* __restrict__ cpos, int nphys) {
   static_assert(sizeof(T) == 2, "bf16 only");
-  static_assert(SPLIT == 1 || (SPLIT == 2 && !PF), "SPLIT 2 without prefetch");
+  static_assert(SPLIT == 1 || ((SPLIT == 2 || SPLIT == 4) && !PF), "SPLIT 2 / 4 without prefetch");
   constexpr int HD = 64, EPC = 8, NG = KPP / 8;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int slice = SPLIT == 1 ? 0 : (wid & 1);
-  const int c = blockIdx.x, h = blockIdx.y * (4 / SPLIT) + (SPLIT == 1 ? wid : wid >> 1);
-  __shared__ float merge[SPLIT == 1 ? 1 : 2][66];
+  const int slice = wid % SPLIT;
+  const int c = blockIdx.x, h = blockIdx.y * (4 / SPLIT) + wid / SPLIT;
+  __shared__ float merge[SPLIT == 1 ? 1 : 4][66];
   if (SPLIT == 1 && h >= heads) return;
   const int grp = lane >> 3, sub = lane & 7;
   const int r = rowmap ? rowmap[c] : c;
@@ -762,22 +764,31 @@ __global__ __launch_bounds__(256) void decode_attn6_kernel(
 #pragma unroll
     for (int t = 0; t < EPC; ++t) o[t] += __shfl_xor(o[t], d, 64);
   }
-  if constexpr (SPLIT == 2) {
-    // slice 1 publishes (max, sum, o) of its keys; slice 0 merges them into its own
-    float* mg = merge[wid >> 1];
-    if (slice == 1 && grp == 0) {
+  if constexpr (SPLIT > 1) {
+    // slices 1.. publish (max, sum, o) of their keys; slice 0 merges them, in slice order, into
+    // its own (a slice without keys has max -inf and weight 0)
+    if (slice != 0 && grp == 0) {
 #pragma unroll
-      for (int t = 0; t < EPC; ++t) mg[sub * EPC + t] = o[t];
-      if (sub == 0) { mg[64] = m; mg[65] = sum; }
+      for (int t = 0; t < EPC; ++t) merge[wid][sub * EPC + t] = o[t];
+      if (sub == 0) { merge[wid][64] = m; merge[wid][65] = sum; }
     }
     __syncthreads();
-    if (slice == 1) return;
-    const float m1 = mg[64], s1 = mg[65];
-    const float mm = fmaxf(m, m1);
-    const float a0 = expf(m - mm), a1 = m1 == -INFINITY ? 0.f : expf(m1 - mm);
-    sum = sum * a0 + s1 * a1;
+    if (slice != 0) return;
+    float mm = m;
 #pragma unroll
-    for (int t = 0; t < EPC; ++t) o[t] = o[t] * a0 + mg[sub * EPC + t] * a1;
+    for (int u = 1; u < SPLIT; ++u) mm = fmaxf(mm, merge[wid + u][64]);
+    const float a0 = expf(m - mm);
+    sum *= a0;
+#pragma unroll
+    for (int t = 0; t < EPC; ++t) o[t] *= a0;
+#pragma unroll
+    for (int u = 1; u < SPLIT; ++u) {
+      const float mu = merge[wid + u][64];
+      const float au = mu == -INFINITY ? 0.f : expf(mu - mm);
+      sum += merge[wid + u][65] * au;
+#pragma unroll
+      for (int t = 0; t < EPC; ++t) o[t] += merge[wid + u][sub * EPC + t] * au;
+    }
   }
   if (grp == 0) {
     const float inv = 1.0f / sum;
@@ -1044,13 +1055,28 @@ extern "C" int zs_decode_attention(const void* qkv, int R, int D, int heads, voi
              "zs_decode_attention: head_dim must be 64");
   ZS_REQUIRE(Lmax > 0 && Lmax <= 4096, "zs_decode_attention: Lmax");
   dim3 grid(R, heads);
-  if (dtype == ZS_BF16 && R <= 128 && g_small_attn && g_attn_split && heads % 2 == 0) {
-    // few waves (R x heads): each (row, head)'s keys over two waves, 64-key phases (all keys
-    // of L <= 128 in flight at once, half per wave)
-    hipLaunchKernelGGL((decode_attn6_kernel<bf16_t, 64, false, true, 2>), dim3(R, heads / 2),
+  if (dtype == ZS_BF16 && R <= 128 && g_small_attn && g_attn_split == 4) {
+    // each (row, head)'s keys over four waves, 32-key phases (one phase per wave at L <= 128)
+    hipLaunchKernelGGL((decode_attn6_kernel<bf16_t, 32, false, true, 4>), dim3(R, heads),
                        dim3(256), 0, S(stream), (const bf16_t*)qkv, D, heads, (bf16_t*)kc,
                        (bf16_t*)vc, Lmax, pos, kvrow, (bf16_t*)out, (const int*)nullptr,
                        (const int*)nullptr, R);
+    ZS_LAUNCH_CHECK();
+    return 0;
+  }
+  if (dtype == ZS_BF16 && R <= 128 && g_small_attn && g_attn_split && heads % 2 == 0) {
+    // few waves (R x heads): each (row, head)'s keys over two waves, KPP-key phases (64: all
+    // keys of L <= 128 in flight at once, half per wave; 32 (attn_split 3): two phases a wave)
+    if (g_attn_split == 3)
+      hipLaunchKernelGGL((decode_attn6_kernel<bf16_t, 32, false, true, 2>), dim3(R, heads / 2),
+                         dim3(256), 0, S(stream), (const bf16_t*)qkv, D, heads, (bf16_t*)kc,
+                         (bf16_t*)vc, Lmax, pos, kvrow, (bf16_t*)out, (const int*)nullptr,
+                         (const int*)nullptr, R);
+    else
+      hipLaunchKernelGGL((decode_attn6_kernel<bf16_t, 64, false, true, 2>), dim3(R, heads / 2),
+                         dim3(256), 0, S(stream), (const bf16_t*)qkv, D, heads, (bf16_t*)kc,
+                         (bf16_t*)vc, Lmax, pos, kvrow, (bf16_t*)out, (const int*)nullptr,
+                         (const int*)nullptr, R);
     ZS_LAUNCH_CHECK();
     return 0;
   }
