@@ -350,7 +350,7 @@ def roofline_attention(pipe, L_mean=None):
     avg = _graph_time(launch, 50)
     es = qkv.element_size()
     byts = R * H * (2 * L * 64 * es) + R * 3 * D * es + R * D * es
-    return _hbm_entry(f"decode_attn6_kernel<bf16,{128 if R <= 128 else 16}> R={R} heads=12 keys={L}",
+    return _hbm_entry(f"decode_attn6_kernel<bf16,{'32,SPLIT=2' if R <= 128 else 16}> R={R} heads=12 keys={L}",
                       byts, avg)
 
 
