@@ -671,6 +671,7 @@ def main_mistral(args, device):
     dec = MistralDecoder(w, max_batch=B, max_prompt=Hc + 10 + 4, max_new=60)
     dec.fused_decode_attn = os.environ.get("ZS_MISTRAL_FUSED_ATTN", "1") != "0"   # A/B knobs
     dec.use_graph = os.environ.get("ZS_MISTRAL_GRAPH", "1") != "0"
+    dec.prefill_unpack = os.environ.get("ZS_MISTRAL_UNPACK", "1") != "0"
     n = args.steps or 2
     wav = synthetic_clips(B, 0, device)
 

@@ -288,6 +288,13 @@ int zs_mistral_rope_kv(const float* qkv, int nsplit, long ss, int M, int H, int 
                        const int* pos, int rows_per_seq, const float* cosb, const float* sinb,
                        void* q, void* kc, void* vc, int Lmax, int dtype, void* stream);
 
+/* zs_fp8_unpack_bf16: the tile-packed fp8 codes of W [N][K] (see zs_fp8_gemm_rows) -> row-major
+ * bf16 W-codes [N][K] (exact; the per-channel scale is not applied).  zs_scale_cols:
+ * x[m][n] *= scale[n] for an f32 [M][ld] matrix.  Together with zs_gemm they run a prefill's
+ * M > 64 rows as one tiled MFMA GEMM (weights read once, not once per 64 rows). */
+int zs_fp8_unpack_bf16(const void* W8, int N, int K, void* out, void* stream);
+int zs_scale_cols(float* x, int M, int N, int ld, const float* scale, void* stream);
+
 /* zs_mistral_silu_mul: act[m][f] = silu(gate) * up from gate|up slabs [nsplit][M][2F]. */
 int zs_mistral_silu_mul(const float* gu, int nsplit, long ss, int M, int F, void* act, int dtype,
                         void* stream);

@@ -163,3 +163,27 @@ def test_decode_attention_fused_vs_unfused(cuda, dt):
     assert torch.equal(kc, kc2) and torch.equal(vc, vc2)
     tol = 2e-5 if dt == torch.float32 else 2e-2
     assert float((a1.float() - a2.float()).abs().max()) < tol
+
+
+@pytest.mark.parametrize("M,N,K", [(200, 1008, 2048), (928, 6144, 4096)])
+def test_fp8_prefill_unpack_gemm(cuda, M, N, K):
+    """The prefill form of the fp8 GEMM (M > 64): zs_fp8_unpack_bf16 (tile-packed codes -> bf16,
+    exact) + the tiled bf16 GEMM + zs_scale_cols against the dequantised reference."""
+    from zsaac import ops
+    from zsaac._lib import call
+    from zsaac.mistral import dequantize_fp8, fp8_pack_tiles, quantize_fp8
+    g = torch.Generator().manual_seed(M + N)
+    w = torch.randn(N, K, generator=g) / K ** 0.5
+    a = torch.randn(M, K, generator=g).bfloat16()
+    q, s = quantize_fp8(w)
+    ref = a.float() @ dequantize_fp8(q, s).t()
+    ad, qd, sd = a.to(cuda), fp8_pack_tiles(q).to(cuda), s.to(cuda)
+    wb = torch.empty(N, K, device=cuda, dtype=torch.bfloat16)
+    st = torch.cuda.current_stream().cuda_stream
+    call("zs_fp8_unpack_bf16", qd.data_ptr(), N, K, wb.data_ptr(), st)
+    assert torch.equal(wb.cpu().float(), q.view(torch.float8_e4m3fn).float())
+    out = torch.empty(M, N, device=cuda)
+    ops.gemm(ad, wb, out, split_k=1)
+    call("zs_scale_cols", out.data_ptr(), M, N, N, sd.data_ptr(), st)
+    got = out.cpu()
+    assert float((got - ref).abs().max()) < 1e-3 * float(ref.abs().max()) + 1e-4

@@ -291,6 +291,56 @@ __global__ __launch_bounds__(64 * WAVES) void fp8_gemm_stream_kernel(
   }
 }
 
+// Prefill (M > 64 rows) helpers: the tile-packed fp8 codes of one weight matrix unpacked to
+// row-major bf16 [N][K] (exact: e4m3 -> bf16 is lossless, the scale is NOT applied) for the
+// tiled bf16 MFMA GEMM, whose f32 result columns are then scaled (out[m][n] *= scale[n]).  The
+// products and the scaling are the fp8 row kernel's (sum_k a q, then x scale), only the order
+// of the k sum differs.  One thread per 16-byte code chunk (16 k of one row).
+__global__ __launch_bounds__(256) void fp8_unpack_bf16_kernel(const uint8_t* __restrict__ W8,
+                                                              int N, int K,
+                                                              bf16_t* __restrict__ out) {
+  const long idx = (long)blockIdx.x * 256 + threadIdx.x;   // packed chunk index
+  const int ntiles = (N + 127) >> 7;
+  const long nchunks = (long)ntiles * 128 * (K / 16);
+  if (idx >= nchunks) return;
+  // packed order: [split][tile][w][j][lane]
+  const int lane = idx & 63;
+  long r = idx >> 6;
+  const int j = r & 15; r >>= 4;
+  const int w = r & 7; r >>= 3;
+  const int t = r % ntiles;
+  const int split = r / ntiles;
+  const int n = t * 128 + w * 16 + (lane & 15);
+  if (n >= N) return;
+  const int k = split * F8_KC + 64 * j + 16 * (lane >> 4);
+  const u32x4m_t c = *reinterpret_cast<const u32x4m_t*>(W8 + idx * 16);
+  u32x4m_t lo, hi;
+  const unsigned cw[4] = {c.x, c.y, c.z, c.w};
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const bf16x2m_t a = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(cw[q], 1.0f, false);
+    const bf16x2m_t b = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(cw[q], 1.0f, true);
+    const unsigned ua = __builtin_bit_cast(unsigned, a), ub = __builtin_bit_cast(unsigned, b);
+    if (q < 2) { lo[2 * q] = ua; lo[2 * q + 1] = ub; }
+    else { hi[2 * (q - 2)] = ua; hi[2 * (q - 2) + 1] = ub; }
+  }
+  u32x4m_t* o = reinterpret_cast<u32x4m_t*>(out + (long)n * K + k);
+  o[0] = lo;
+  o[1] = hi;
+}
+
+__global__ __launch_bounds__(256) void scale_cols_kernel(float* __restrict__ x, int M, int N,
+                                                         int ld, const float* __restrict__ scale) {
+  const long idx = 4 * ((long)blockIdx.x * 256 + threadIdx.x);
+  if (idx >= (long)M * N) return;
+  const int m = idx / N, n = idx % N;
+  float4* p = reinterpret_cast<float4*>(x + (long)m * ld + n);
+  const float4 s = *reinterpret_cast<const float4*>(scale + n);
+  float4 v = *p;
+  v.x *= s.x; v.y *= s.y; v.z *= s.z; v.w *= s.w;
+  *p = v;
+}
+
 // ---------------------------------------------------------------- consumers of the slabs
 __device__ __forceinline__ float slab_sum(const float* __restrict__ p, int nsplit, long ss) {
   float v = p[0];
@@ -691,6 +741,27 @@ extern "C" int zs_fp8_gemm_rows(const void* A, int lda, const void* W8, const fl
 }
 
 extern "C" int zs_fp8_splits(int K) { return K > 0 ? cdiv(K, F8_KC) : 0; }
+
+extern "C" int zs_fp8_unpack_bf16(const void* W8, int N, int K, void* out, void* stream) {
+  ZS_REQUIRE(N > 0 && K > 0 && K % F8_KC == 0 && ((uintptr_t)W8 & 15) == 0 &&
+                 ((uintptr_t)out & 15) == 0,
+             "zs_fp8_unpack_bf16: K %% 1024, 16-byte aligned buffers");
+  const long nchunks = (long)cdiv(N, 128) * 128 * (K / 16);
+  hipLaunchKernelGGL(fp8_unpack_bf16_kernel, dim3((unsigned)cdiv(nchunks, 256)), dim3(256), 0,
+                     S(stream), (const uint8_t*)W8, N, K, (bf16_t*)out);
+  ZS_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int zs_scale_cols(float* x, int M, int N, int ld, const float* scale, void* stream) {
+  ZS_REQUIRE(M > 0 && N > 0 && N % 4 == 0 && ld % 4 == 0 && ld >= N && ((uintptr_t)x & 15) == 0 &&
+                 ((uintptr_t)scale & 15) == 0,
+             "zs_scale_cols: N, ld multiples of 4, 16-byte aligned");
+  hipLaunchKernelGGL(scale_cols_kernel, dim3((unsigned)cdiv((long)M * N / 4, 256)), dim3(256), 0,
+                     S(stream), x, M, N, ld, scale);
+  ZS_LAUNCH_CHECK();
+  return 0;
+}
 
 extern "C" int zs_mistral_embed(const int* hard, int H, const float* soft, int ns, const int* tail,
                                 int nt, const int* tok, const void* emb, int D, int M, float* x,

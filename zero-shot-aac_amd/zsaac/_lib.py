@@ -76,6 +76,8 @@ SIGNATURES = {
     "zs_magic_score": [P, P, P, P, I, I, I, I, I, F, F, F, P, P],
     "zs_fp8_gemm_rows": [P, I, P, P, I, I, I, P, L, I, P],
     "zs_fp8_splits": [I],
+    "zs_fp8_unpack_bf16": [P, I, I, P, P],
+    "zs_scale_cols": [P, I, I, I, P, P],
     "zs_mistral_embed": [P, I, P, I, P, I, P, P, I, I, P, I, P],
     "zs_mistral_add_rmsnorm": [P, P, I, L, I, I, F, P, P, I, P],
     "zs_mistral_rope_kv": [P, I, L, I, I, I, P, I, P, P, P, P, P, I, I, P],

@@ -189,6 +189,10 @@ class MistralDecoder:
         self.fused_decode_attn = True     # False: decode through rope_kv + attention (A/B, tests)
         self.use_graph = True             # decode steps replayed from hipGraphs (decode_step)
         self.graphs = {}
+        self.prefill_unpack = True        # fp8 prefill as unpack + tiled GEMM (A/B knob)
+        self._wb = None
+        ly0 = w.layers[0]
+        self._wb_need = max(ly0[k]["N"] * ly0[k]["K"] for k in ("qkv", "o", "gu", "down"))
         self.Lmax = max_prompt + max_new + 1
         Mp = max_batch * max_prompt
         D, H, KVH, HD, F = w.D, w.H, w.KVH, w.HD, w.F
@@ -219,12 +223,29 @@ class MistralDecoder:
         self.pidx = torch.empty(max_batch, self.nblk, 1, device=dev, dtype=torch.int32)
         self.last = torch.empty(max_batch, D, device=dev, dtype=adt)
 
+    def _wscratch(self, N, K):
+        """bf16 [N][K] scratch for one unpacked weight matrix (the largest: gate|up)."""
+        if self._wb is None or self._wb.numel() < N * K:
+            self._wb = torch.empty(max(N * K, self._wb_need), device=self.w.dev,
+                                   dtype=torch.bfloat16)
+        return self._wb[:N * K].view(N, K)
+
     def _splits(self, K):
         return call("zs_fp8_splits", K) if self.w.mode == "fp8" else 1
 
     def _gemm(self, a, lw, M):
         """f32 result slabs of a @ W^T for M rows: (slab tensor, nsplit, split stride)."""
         N, K = lw["N"], lw["K"]
+        if self.w.mode == "fp8" and M > 64 and self.prefill_unpack:
+            # prefill: codes -> bf16 once per matrix, one tiled MFMA GEMM over all M rows, then
+            # the per-channel scales (the row kernel would re-stream the weights per 64 rows)
+            st = torch.cuda.current_stream().cuda_stream
+            wb = self._wscratch(N, K)
+            call("zs_fp8_unpack_bf16", lw["w8"].data_ptr(), N, K, wb.data_ptr(), st)
+            out = self.slab[:M * N].view(M, N)
+            ops.gemm(a[:M], wb, out, split_k=1)
+            call("zs_scale_cols", out.data_ptr(), M, N, N, lw["scale"].data_ptr(), st)
+            return out, 1, M * N
         if self.w.mode == "fp8":
             ns = self._splits(K)
             ss = M * N
