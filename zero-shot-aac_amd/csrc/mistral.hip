@@ -24,7 +24,8 @@ typedef __attribute__((ext_vector_type(4))) float f32x4m_t;
 typedef __attribute__((ext_vector_type(4))) unsigned u32x4m_t;
 
 int g_fp8_tile = 0;   // zs_tune_set("fp8_tile", v) A/B knob: 1 = 64-column one-shot tiles only,
-                      // 2 = one-shot kernel only (no persistent stream kernel)
+                      // 2 = one-shot kernel only (no persistent stream kernel), 3 = 128-column
+                      // one-shot tiles where the stream kernel does not apply
 int g_fp8_dbg = 0;    // zs_tune_set("fp8_dbg", b): ablations (1 no A loads, 2 no MFMA, 4 no W loads)
 int g_mis_attn_split = 1;   // zs_tune_set("mis_attn_split", 2): keys over two waves (A/B: 3.28 vs 3.21 ms)
 
@@ -767,7 +768,7 @@ extern "C" int zs_fp8_gemm_rows(const void* A, int lda, const void* W8, const fl
     else F8S(8);
 #undef F8S
   } else if ((long)cdiv(N, 256) * splits >= 256 && g_fp8_tile != 1) F8L(2, 8);
-  else if ((long)cdiv(N, 128) * splits >= 256 && g_fp8_tile != 1) F8L(1, 8);
+  else if (((long)cdiv(N, 128) * splits >= 256 && g_fp8_tile != 1) || g_fp8_tile == 3) F8L(1, 8);
   else F8L(1, 4);
 #undef F8L
   ZS_LAUNCH_CHECK();
