@@ -16,6 +16,7 @@ CLS rows only.  bf16 operands with f32 accumulation and an f32 residual stream (
 throughout (parity mode)."""
 from __future__ import annotations
 
+import weakref
 from typing import Dict, Optional
 
 import torch
@@ -151,7 +152,9 @@ class BertTextEngine:
         return self.encode_ids(ids, lens)
 
 
-_BACKENDS = {}
+# per-tokenizer caches, keyed weakly by the tokenizer object (an id() key could be reused by a
+# later tokenizer with another vocabulary)
+_BACKENDS = weakref.WeakKeyDictionary()
 
 
 def _backend(tokenizer, max_length):
@@ -162,17 +165,17 @@ def _backend(tokenizer, max_length):
     bk = getattr(tokenizer, "backend_tokenizer", None)
     if bk is None or not getattr(tokenizer, "is_fast", False) or getattr(tokenizer, "padding_side", "right") != "right":
         return None
-    key = (id(tokenizer), max_length)
-    if key not in _BACKENDS:
+    per = _BACKENDS.setdefault(tokenizer, {})
+    if max_length not in per:
         from tokenizers import Tokenizer
         b = Tokenizer.from_str(bk.to_str())
         b.enable_truncation(max_length)
         b.enable_padding(pad_id=tokenizer.pad_token_id, pad_token=tokenizer.pad_token)
-        _BACKENDS[key] = b
-    return _BACKENDS[key]
+        per[max_length] = b
+    return per[max_length]
 
 
-_RAW = {}
+_RAW = weakref.WeakKeyDictionary()
 
 
 def _to_dev(t, device):
@@ -187,14 +190,13 @@ def _raw_backend(tokenizer):
     bk = getattr(tokenizer, "backend_tokenizer", None)
     if bk is None or not getattr(tokenizer, "is_fast", False) or getattr(tokenizer, "padding_side", "right") != "right":
         return None
-    key = id(tokenizer)
-    if key not in _RAW:
+    if tokenizer not in _RAW:
         from tokenizers import Tokenizer
         b = Tokenizer.from_str(bk.to_str())
         b.no_truncation()
         b.no_padding()
-        _RAW[key] = (b, {})
-    return _RAW[key]
+        _RAW[tokenizer] = (b, {})
+    return _RAW[tokenizer]
 
 
 def tokenize_pieces(tokenizer, pieces, max_length, device):
