@@ -9,8 +9,8 @@ tail -1 $O/t.log
 for arm in "fp8_tile=0" "fp8_tile=4" "fp8_tile=0" "fp8_tile=4"; do
   ZSAAC_TUNE=$arm timeout -k 10 300 python bench.py --mistral > $O/m.json 2> $O/m.err || { tail $O/m.err; exit 1; }
   python -c "import json;d=json.load(open('$O/m.json'));print('$arm', d['value'], d['ms_per_step'], d['roofline']['step_us'], d['config']['generated_tokens'])"
+  [ "$arm" = "fp8_tile=0" ] && cp $O/m.json $O/mistral_bench.json
 done
-cp $O/m.json $O/mistral_bench.json
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" && timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python bench.py --mistral > $O/mp.json 2> $O/mp.err || { tail $O/mp.err; exit 1; }
 f=$(ls $O/prof/*/run_kernel_stats.csv 2>/dev/null | head -1); [ -n "$f" ] || f=$(find $O/prof -name '*kernel_stats.csv' | head -1)
 cp "$f" $O/mistral_kernel_stats.csv && rm -rf $O/prof
