@@ -87,6 +87,21 @@ def test_mistral_fp8_ids_until_small_margin(cuda, setup):
 @pytest.mark.parametrize("M,N,K", [(32, 6144, 4096), (7, 1008, 1024), (64, 256, 14336),
                                    (32, 4096, 14336), (20, 16528, 4096), (7, 28672, 4096)])
 def test_fp8_gemm_rows(cuda, M, N, K):
+    _fp8_gemm_rows_check(cuda, M, N, K)
+
+
+@pytest.mark.parametrize("M,N,K", [(32, 4096, 14336), (20, 16512, 4096), (7, 28672, 4096)])
+def test_fp8_gemm_rows_stream_w4(cuda, M, N, K):
+    """The 4-wave (64-column item, 2 workgroups per CU) stream kernel variant (knob)."""
+    from zsaac._lib import call
+    call("zs_tune_set", b"fp8_stream_w4", 1)
+    try:
+        _fp8_gemm_rows_check(cuda, M, N, K)
+    finally:
+        call("zs_tune_set", b"fp8_stream_w4", 0)
+
+
+def _fp8_gemm_rows_check(cuda, M, N, K):
     from zsaac._lib import call
     from zsaac.mistral import dequantize_fp8, fp8_pack_tiles, quantize_fp8
     g = torch.Generator().manual_seed(M + N)

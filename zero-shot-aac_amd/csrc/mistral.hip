@@ -28,6 +28,8 @@ int g_fp8_tile = 0;   // zs_tune_set("fp8_tile", v) A/B knob: 1 = 64-column one-
                       // one-shot tiles where the stream kernel does not apply, 4 = 64-column
                       // one-shot tiles below 256 workgroups at M <= 32 (the earlier rule)
 int g_fp8_dbg = 0;    // zs_tune_set("fp8_dbg", b): ablations (1 no A loads, 2 no MFMA, 4 no W loads)
+int g_fp8_stream_w4 = 0;    // zs_tune_set("fp8_stream_w4", 1): 4-wave stream workgroups, 2 per
+                            // CU (A/B: gate|up 28.2 vs 27.7 us, step 3.16 vs 3.07 ms -- off)
 int g_mis_attn_split = 1;   // zs_tune_set("mis_attn_split", 2): keys over two waves (A/B: 3.28 vs 3.21 ms)
 
 constexpr int F8_KC = 1024;   // k per workgroup (one split)
@@ -187,8 +189,8 @@ __device__ __forceinline__ void f8s_issue(F8Item& b, const uint8_t* __restrict__
                                           int ntiles, int it) {
   using P = F8Stream<WAVES>;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int split = it / ntiles, tile = it - split * ntiles;
-  const uint8_t* wr = f8_frag(W8, ntiles, split, tile * WAVES + wid, lane);
+  const int split = it / ntiles, tile = it - split * ntiles;     // NT-column item tiles
+  const uint8_t* wr = f8_frag(W8, (N + 127) >> 7, split, tile * WAVES + wid, lane);
 #pragma unroll
   for (int j = 0; j < P::JB; ++j)
     b.w[j] = __builtin_nontemporal_load(reinterpret_cast<const u32x4m_t*>(wr + 1024 * j));
@@ -269,7 +271,7 @@ __device__ __forceinline__ void f8s_compute(const F8Item& b, const bf16_t* as, i
 // every load in flight).  The last workgroup's run is clamped to the final item: it recomputes
 // and rewrites identical values.
 template <int WAVES, int PER>
-__global__ __launch_bounds__(64 * WAVES) void fp8_gemm_stream_kernel(
+__global__ __launch_bounds__(64 * WAVES, WAVES == 4 ? 2 : 1) void fp8_gemm_stream_kernel(
     const bf16_t* __restrict__ A, int lda, const uint8_t* __restrict__ W8,
     const float* __restrict__ scale, int M, int N, int K, float* __restrict__ out,
     long split_stride, int ldo, int ntiles) {
@@ -757,16 +759,27 @@ extern "C" int zs_fp8_gemm_rows(const void* A, int lda, const void* W8, const fl
   }
   const long items = (long)cdiv(N, 128) * splits;
   if (M <= 32 && (g_fp8_tile == 0 || g_fp8_tile == 4) && items > ncu && items <= 8L * ncu) {
-    const long per = (items + ncu - 1) / ncu;
-#define F8S(P_)                                                                                 \
-  hipLaunchKernelGGL((fp8_gemm_stream_kernel<8, P_>), dim3((unsigned)((items + P_ - 1) / P_)),  \
-                     dim3(512), (size_t)32 * (F8_KC + 8) * 2, st, (const bf16_t*)A, lda,        \
-                     (const uint8_t*)W8, scale, M, N, K, out, split_stride, ldo, cdiv(N, 128))
-    if (per <= 2) F8S(2);
-    else if (per <= 3) F8S(3);
-    else if (per <= 4) F8S(4);
-    else if (per <= 6) F8S(6);
-    else F8S(8);
+    const bool w4 = g_fp8_stream_w4 && N % 64 == 0;   // 64-column items, 2 workgroups per CU
+    const long its = w4 ? (long)(N / 64) * splits : items, slots = w4 ? 2L * ncu : ncu;
+    const long per = (its + slots - 1) / slots;
+#define F8S(W_, P_)                                                                             \
+  hipLaunchKernelGGL((fp8_gemm_stream_kernel<W_, P_>), dim3((unsigned)((its + P_ - 1) / P_)),   \
+                     dim3(64 * W_), (size_t)32 * (F8_KC + 8) * 2, st, (const bf16_t*)A, lda,   \
+                     (const uint8_t*)W8, scale, M, N, K, out, split_stride, ldo,               \
+                     W_ == 8 ? cdiv(N, 128) : N / 64)
+    if (w4) {
+      if (per <= 2) F8S(4, 2);
+      else if (per <= 3) F8S(4, 3);
+      else if (per <= 4) F8S(4, 4);
+      else if (per <= 6) F8S(4, 6);
+      else F8S(4, 8);
+    } else {
+      if (per <= 2) F8S(8, 2);
+      else if (per <= 3) F8S(8, 3);
+      else if (per <= 4) F8S(8, 4);
+      else if (per <= 6) F8S(8, 6);
+      else F8S(8, 8);
+    }
 #undef F8S
   } else if ((long)cdiv(N, 256) * splits >= 256 && g_fp8_tile != 1) F8L(2, 8);
   // 128-column tiles also at M <= 32 with >= 128 workgroups (q|k|v at 192: 11.1 -> 9.8 us)
