@@ -237,6 +237,11 @@ int zs_magic_maxcos(const void* hid, int ncand, int W, void* ctx, int Lmax, cons
 int zs_magic_score(const float* pval, const float* maxcos, const float* text, const float* audio,
                    int C, int E, int b, int W, int nact, float temp, float alpha, float beta,
                    float* score, void* stream);
+/* zs_magic_score_t: zs_magic_score with the score divided by score_temp (> 0):
+ * generate_beam_magic's `temperature` (gpt2_prefix_eval.py:629). */
+int zs_magic_score_t(const float* pval, const float* maxcos, const float* text, const float* audio,
+                     int C, int E, int b, int W, int nact, float temp, float alpha, float beta,
+                     float score_temp, float* score, void* stream);
 
 /* zs_magic_step: one selection step per clip (one block each).  greedy = 0: generate_beam_magic
  * 626-683 (first: topk(b) of beam 0's W scores; later: stopped beams keep candidate 0 at zero
@@ -385,6 +390,11 @@ int zs_compact_rows(const int* done, int nrows, int* rowmap, int* n_active, void
 int zs_lmhead_topk(int M, int K, int V, int dtype, const void* A, int lda, const void* W,
                    int topk, int row_norm, float* part_stat, float* part_val, int* part_idx,
                    void* stream);
+/* zs_lmhead_topk_t: zs_lmhead_topk on logits / temperature (temperature > 0; row_norm needs 1):
+ * generate2 / generate_beam's `temperature` (gpt2_prefix_eval.py:121, 196). */
+int zs_lmhead_topk_t(int M, int K, int V, int dtype, const void* A, int lda, const void* W,
+                     int topk, int row_norm, float temperature, float* part_stat, float* part_val,
+                     int* part_idx, void* stream);
 int zs_lmhead_nblk(int V);
 
 /* zs_argmax_finalize: merge zs_lmhead_topk partials (topk 1) into idx[M] (lower index on ties). */
@@ -417,6 +427,39 @@ int zs_greedy_step_map(const float* part_val, const int* part_idx, int R, const 
                        int nphys, int nblk, int* step_ctr, int max_steps, int stop0, int stop1,
                        int* out_ids, int* out_len, int* done, int* pos, int* next_tok,
                        int* all_done, void* stream);
+
+/* zs_gpt2_decode_persist: every remaining step of generate2 (gpt2_prefix_eval.py:161-222: the
+ * 67-step loop of model.gpt(inputs_embeds=...) -> argmax -> stop check) for ONE batch of R <= 64
+ * rows (the reference's eval batch), bf16, as one persistent launch of
+ * zs_decode_persist_grid() workgroups (one per CU; the caller keeps the concurrent launches'
+ * grids within the CU count): per step the 12 GPT2Blocks (ln_1 affine folded into c_attn and
+ * ln_2's into c_fc, as zs_gemm_ln), ln_f, the tied LM head with its argmax (ties -> lower id)
+ * and zs_greedy_step's bookkeeping, until every row stopped or max_steps.  Starts from the state
+ * zs_greedy_step left after step 0 (next_tok, pos, done, out_ids, out_len, *step_ctr,
+ * all_done[0]); leaves it as the per-step path would.  layer_w: 12 x 8 device pointers
+ * {c_attn W [2304][768] bf16, its bias f32, attn.c_proj W [768][768], bias, c_fc W [3072][768],
+ * bias, mlp.c_proj W [768][3072], bias} (W = Conv1D weight transposed); wte_packed: the tied
+ * LM head in MFMA B-fragment order, [ceil(V/16)][24][64][8] bf16 (zs layout of block j, k-step s,
+ * lane l = W[16 j + l % 16][32 s + 8 (l / 16) .. + 8], rows past V zero); temperature > 0 divides
+ * the logits before the argmax (gpt2_prefix_eval.py:196); kv: 24 pointers
+ * {kc[0..11], vc[0..11]}, each [R][12][Lmax][64] bf16 (zs_kv_write layout).  ws: scratch of
+ * zs_decode_persist_workspace_bytes() bytes, 256-byte aligned, private to one launch in flight.
+ * A grid that cannot become co-resident gives up after a bounded wait: then
+ * zs_decode_persist_status reports timed_out != 0 and the outputs are invalid. */
+int zs_decode_persist_workspace_bytes(void);
+int zs_decode_persist_grid(void);
+int zs_gpt2_decode_persist(int R, int Lmax, int max_steps, int stop0, int stop1, int V,
+                           const void* wte, const void* wpe, const void* wte_packed,
+                           float temperature, const void* const* layer_w,
+                           const float* lnf_w, const float* lnf_b, void* const* kv, int* pos,
+                           int* next_tok, int* done, int* out_ids, int* out_len, int* step_ctr,
+                           int* all_done, void* ws, long ws_bytes, void* stream);
+int zs_decode_persist_status(const void* ws, int* timed_out);
+/* zs_decode_persist_set_stamps: diagnostic phase timing (tools/persist_stamps.py): with buf !=
+ * NULL ([grid][128] u64), thread 0 of every workgroup of later launches writes s_memrealtime
+ * (100 MHz) at each barrier arrive (slot 2i) / wait end (2i + 1) of decode step `step`, and at
+ * that step's start (127) / end (126).  NULL turns it off. */
+int zs_decode_persist_set_stamps(void* buf, int step);
 
 /* zs_beam_step: generate_beam's per-step update (gpt2_prefix_eval.py:119-151) for C clips x
  * `beam` rows, from zs_lmhead_topk partials (topk >= beam) with log(softmax) semantics.

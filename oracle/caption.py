@@ -133,9 +133,10 @@ def gpt2_logits(embeds, sd, past=None, pos0=0):
 
 
 def generate2(embed: torch.Tensor, sd, entry_length=67, use_cache=False,
-              margins: Optional[list] = None) -> List[int]:
-    """generate2 (gpt2_prefix_eval.py:161-222), batch 1, temperature 1.  The top-p filter never
-    removes the sorted-first token (lines 197-206), so the pick is the argmax of the raw logits.
+              margins: Optional[list] = None, temperature=1.0) -> List[int]:
+    """generate2 (gpt2_prefix_eval.py:161-222), batch 1.  Logits are divided by ``temperature``
+    (line 196: ``temperature if temperature > 0 else 1.0``); the top-p filter never removes the
+    sorted-first token (lines 197-206), so the pick is the argmax of the scaled logits.
     Stops after appending 13 ('.') or 764 (' .').  ``use_cache`` swaps the reference's full
     recompute for a KV cache (same math, ~1e-6 different rounding)."""
     generated = embed
@@ -150,7 +151,7 @@ def generate2(embed: torch.Tensor, sd, entry_length=67, use_cache=False,
                 pos = generated.shape[1]
             else:
                 logits, _ = gpt2_logits(generated, sd)
-            last = logits[0, -1]
+            last = logits[0, -1] / (temperature if temperature > 0 else 1.0)
             nxt = int(torch.argmax(last))
             if margins is not None:
                 top2 = last.topk(2).values
@@ -163,8 +164,9 @@ def generate2(embed: torch.Tensor, sd, entry_length=67, use_cache=False,
 
 
 def generate_beam(embed: torch.Tensor, sd, beam_size=5, entry_length=67,
-                  use_cache=False) -> Tuple[List[List[int]], List[float]]:
-    """generate_beam (gpt2_prefix_eval.py:99-158), temperature 1: log(softmax) scores, stopped
+                  use_cache=False, temperature=1.0) -> Tuple[List[List[int]], List[float]]:
+    """generate_beam (gpt2_prefix_eval.py:99-158): logits / temperature (line 121, ``temperature
+    if temperature > 0 else 1.0``), log(softmax) scores, stopped
     beams only extend with id 0 at zero cost, length-normalised top-k over beam x vocab, stop when
     every beam has emitted 13.  Returns (token lists ordered best-first, their final scores)."""
     wte = sd["gpt.transformer.wte.weight"]
@@ -182,7 +184,7 @@ def generate_beam(embed: torch.Tensor, sd, beam_size=5, entry_length=67,
                 pos = generated.shape[1]
             else:
                 logits, _ = gpt2_logits(generated, sd)
-            logits = logits[:, -1, :].softmax(-1).log()
+            logits = (logits[:, -1, :] / (temperature if temperature > 0 else 1.0)).softmax(-1).log()
             if scores is None:
                 scores, next_tokens = logits.topk(beam_size, -1)
                 generated = generated.expand(beam_size, *generated.shape[1:])

@@ -308,6 +308,43 @@ def gen_beam(n_clips=4, entry_length=67):
           entry_length=np.int64(entry_length), **out)
 
 
+def gen_temperature(n_clips=4, entry_length=24):
+    """generate_beam (beam 3, temperature 0.7 and 1.6) and generate2 (temperature 0.7) on the
+    beam.npz clips: the reference divides the logits by temperature before softmax().log()
+    (gpt2_prefix_eval.py:121-122) / the top-p sort (196)."""
+    import gpt2_prefix_eval as G
+    model = _caption_model("mlp")
+    emb = S.synthetic_clap_embeddings(n_clips, seed=99)
+    label_ids = S.label_token_table()
+    hard_rows = [[1858, 389] + label_ids[i] + [11] + label_ids[2 * i + 1] + [287, 428, 6597, 13]
+                 for i in range(n_clips)]
+    hard, hard_len = _pad(hard_rows)
+    out = {}
+    for tag, T in (("t07", 0.7), ("t16", 1.6)):
+        rows = []
+        for i in range(n_clips):
+            h = torch.tensor([hard_rows[i]])
+            with torch.no_grad():
+                pe, _ = model.clap_to_gpt(emb[i:i + 1].unsqueeze(0), model.gpt.transformer.wte(h))
+                texts = G.generate_beam(model, IdTokenizer(), beam_size=3, embed=pe,
+                                        entry_length=entry_length, temperature=T)
+            rows.append([[int(t) for t in s.split()] for s in texts])
+        ids, lens = _pad([r for clip in rows for r in clip])
+        out[f"beam3_{tag}_ids"] = ids.reshape(n_clips, 3, -1)
+        out[f"beam3_{tag}_len"] = lens.reshape(n_clips, 3)
+        print(f"  beam3 T={T}: lens {lens.tolist()}", flush=True)
+    g = []
+    for i in range(n_clips):
+        h = torch.tensor([hard_rows[i]])
+        with torch.no_grad():
+            pe, _ = model.clap_to_gpt(emb[i:i + 1].unsqueeze(0), model.gpt.transformer.wte(h))
+            g.append([int(t) for t in G.generate2(model, IdTokenizer(), embed=pe,
+                                                  entry_length=entry_length, temperature=0.7).split()])
+    gi, gl = _pad(g)
+    _save("temperature.npz", clap_emb=emb.numpy(), hard_ids=hard, hard_len=hard_len,
+          entry_length=np.int64(entry_length), greedy_t07_ids=gi, greedy_t07_len=gl, **out)
+
+
 def gen_mappers():
     from models.mapper import MLP, TransformerMapper
     x = S.synthetic_clap_embeddings(3, seed=11).unsqueeze(1)  # [3,1,1024] as in make_preds
@@ -528,7 +565,7 @@ def gen_mistral(n_clips=6):
 ALL = {"prompt": gen_prompt, "mappers": gen_mappers, "htsat": gen_htsat, "cnn14": gen_cnn14,
        "beam": gen_beam, "c1": gen_c1, "keys": gen_keys,
        "margin": gen_margin, "margin_flat": lambda: gen_margin(name="c2_margin_flat"),
-       "variants": gen_variants, "magic": gen_magic,
+       "variants": gen_variants, "magic": gen_magic, "temperature": gen_temperature,
        "mistral": gen_mistral}
 
 if __name__ == "__main__":

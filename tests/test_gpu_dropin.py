@@ -67,6 +67,29 @@ def test_generate_beam_dropin(cuda, golden, model):
     assert [[int(t) for t in s.split()] for s in texts] == ref
 
 
+@pytest.mark.parametrize("tag,T", [("t07", 0.7), ("t16", 1.6)])
+def test_generate_temperature_dropin(cuda, golden, model, tag, T):
+    """generate_beam / generate2 with temperature != 1 (the LM head divides the logits before the
+    top-k and the softmax statistics) against the reference's own outputs (temperature.npz)."""
+    import gpt2_prefix_eval as G
+    from zsaac.tokenizer import IdTokenizer
+    g = golden("temperature.npz")
+    E = int(g["entry_length"])
+    for c in range(g["clap_emb"].shape[0]):
+        n = int(g["hard_len"][c])
+        hard = torch.from_numpy(g["hard_ids"][c:c + 1, :n]).to(cuda)
+        with torch.no_grad():
+            pe, _ = model.clap_to_gpt(torch.from_numpy(g["clap_emb"][c:c + 1])[None].to(cuda),
+                                      model.gpt.transformer.wte(hard))
+        texts = G.generate_beam(model, IdTokenizer(), beam_size=3, embed=pe, entry_length=E,
+                                temperature=T)
+        ref = [g[f"beam3_{tag}_ids"][c, i, :g[f"beam3_{tag}_len"][c, i]].tolist() for i in range(3)]
+        assert [[int(t) for t in s.split()] for s in texts] == ref, (tag, c)
+        if tag == "t07":
+            out = G.generate2(model, IdTokenizer(), embed=pe, entry_length=E, temperature=0.7)
+            assert [int(t) for t in out.split()] == g["greedy_t07_ids"][c, :g["greedy_t07_len"][c]].tolist()
+
+
 def test_gpt_full_logits(cuda, golden, model):
     from oracle import caption as OC
     from zsaac import synthetic as S

@@ -105,3 +105,22 @@ def test_beam_kv_oracle(golden, csd, beam):
     outs, _ = C.generate_beam(pe, csd, beam_size=beam, use_cache=True)
     ref = [g[f"beam{beam}_ids"][c, i, :g[f"beam{beam}_len"][c, i]].tolist() for i in range(beam)]
     assert outs == ref
+
+
+@pytest.mark.parametrize("tag,T", [("t07", 0.7), ("t16", 1.6)])
+def test_beam_temperature_oracle(golden, csd, tag, T):
+    """generate_beam with temperature != 1 (logits / T before softmax().log(),
+    gpt2_prefix_eval.py:121-122): the oracle against the reference's own output."""
+    from oracle import caption as C
+    g = golden("temperature.npz")
+    c = 1
+    n = int(g["hard_len"][c])
+    hard = torch.from_numpy(g["hard_ids"][c:c + 1, :n])
+    with torch.no_grad():
+        pe = C.clap_to_gpt(torch.from_numpy(g["clap_emb"][c:c + 1])[None], hard, csd)
+    outs, _ = C.generate_beam(pe, csd, beam_size=3, entry_length=int(g["entry_length"]),
+                              use_cache=True, temperature=T)
+    ref = [g[f"beam3_{tag}_ids"][c, i, :g[f"beam3_{tag}_len"][c, i]].tolist() for i in range(3)]
+    assert outs == ref
+    ids = C.generate2(pe, csd, entry_length=int(g["entry_length"]), use_cache=True, temperature=0.7)
+    assert ids == g["greedy_t07_ids"][c, :g["greedy_t07_len"][c]].tolist()

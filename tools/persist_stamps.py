@@ -1,0 +1,79 @@
+#!/usr/bin/env python3
+"""Phase timing inside the persistent decode (zs_decode_persist_set_stamps): per barrier of one
+decode step, the median over workgroups of the compute before it (previous wait end -> arrive),
+the wait (arrive -> wait end) and the arrival skew (last - first arrive), in microseconds.
+
+    python tools/persist_stamps.py [step=3]
+"""
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "zero-shot-aac_amd"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import bench  # noqa: E402
+
+
+def main():
+    step = int(sys.argv[1]) if len(sys.argv) > 1 else 3
+    from zsaac import ops
+    from zsaac._lib import call
+
+    class A:
+        batch, dtype, encoder, mapper, beam, entry_length, group, compact = \
+            64, "bf16", "htsat", "mlp", 0, 67, 1, 1
+        encoder_batch = 64
+    dev = torch.device("cuda", 0)
+    pipe, _, _ = bench.build(A, dev)
+    wav = bench.synthetic_clips(64, 0, dev)
+    pipe.caption_wav(wav)
+    G = ops.decode_persist_grid()
+    buf = torch.zeros(G, 128, dtype=torch.int64, device=dev)
+    call("zs_decode_persist_set_stamps", buf.data_ptr(), step)
+    dec = pipe.decoder
+    for _ in range(3):
+        dec.greedy_begin(64)
+        torch.cuda.synchronize()
+    call("zs_decode_persist_set_stamps", None, 0)
+    t = buf.cpu().numpy().astype(np.float64) / 100.0     # us (100 MHz)
+    start, end = t[:, 127], t[:, 126]
+    names = []
+    for l in range(12):
+        names += [f"L{l}.A qkv", f"L{l}.B attn", f"L{l}.C proj", f"L{l}.D fc", f"L{l}.E mproj"]
+    names.append("F lmhead")
+    t0 = np.median(start)
+    prev = start.copy()
+    rows, comp, wait = [], [], []
+    for i, nm in enumerate(names):
+        arr, wt = t[:, 2 * i], t[:, 2 * i + 1]
+        c, w = arr - prev, wt - arr
+        rows.append({"phase": nm, "compute_med": round(float(np.median(c)), 2),
+                     "compute_max": round(float(np.max(c)), 2),
+                     "wait_med": round(float(np.median(w)), 2),
+                     "arrive_skew": round(float(arr.max() - arr.min()), 2),
+                     "end_at": round(float(np.median(wt) - t0), 1)})
+        comp.append(c)
+        wait.append(w)
+        prev = wt
+    g_phase = end - prev
+    for r in rows[:5] + rows[-6:]:
+        print(json.dumps(r))
+    kinds = {"A": [], "B": [], "C": [], "D": [], "E": []}
+    for r in rows[:-1]:
+        kinds[r["phase"].split(".")[1][0]].append((r["compute_med"], r["wait_med"], r["compute_max"]))
+    summ = {k: {"compute_med": round(float(np.mean([a for a, _, _ in v])), 2),
+                "compute_max": round(float(np.mean([c for _, _, c in v])), 2),
+                "wait_med": round(float(np.mean([b for _, b, _ in v])), 2)} for k, v in kinds.items()}
+    summ["F"] = {"compute_med": rows[-1]["compute_med"], "wait_med": rows[-1]["wait_med"]}
+    summ["G"] = round(float(np.median(g_phase)), 2)
+    summ["step_us"] = round(float(np.median(end - start)), 1)
+    print(json.dumps({"per_phase_kind_mean_us": summ}))
+
+
+if __name__ == "__main__":
+    main()

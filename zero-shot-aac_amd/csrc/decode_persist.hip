@@ -1,0 +1,966 @@
+// GPT-2 greedy decode of ONE eval batch (R <= 64 rows, the reference's bs = 64) as ONE persistent
+// launch: every remaining step of generate2 (gpt2_prefix_eval.py:161-222 over transformers'
+// GPT2LMHeadModel with a KV cache) -- 12 blocks, ln_f, the LM head with its argmax and the stop /
+// length bookkeeping -- runs inside the kernel, from the step after the prefill to the last one.
+//
+// Why: at 64 rows a decode step is ~390 MB of weight + KV-cache reads spread over ~63 dependent
+// launches of 1-5 MB each; each launch spends most of its 5-9 us on the kernel boundary and on
+// issuing its first weight loads.  Here a fixed set of G workgroups (one per CU)
+// owns a fixed slice of every GEMM's columns and of the (row, head) attention units for the whole
+// decode.  A phase's inputs arrive through a grid barrier, and the weights of the NEXT phase
+// (activation independent) are issued into registers BEFORE the workgroup waits on that barrier,
+// so the weight stream overlaps the hand-off instead of following a kernel boundary.
+//
+// The launch uses G of the chip's 256 CUs, so several eval batches decode at once on disjoint CUs
+// (ConcurrentRunner streams): the chip is filled by independent bs = 64 batches, never by merging
+// their rows into one GEMM.
+//
+// Phases of one step (WG w of G = 48, 8 waves; "sc1" = write-through stores / L1-bypassing loads,
+// MI355X_MICROARCH.md § Workgroup dispatch, Valid forms row 1):
+//   A  ln_1 + c_attn: x [64][768] f32 -> LN (affine folded into W, as the bf16 zs_gemm_ln path)
+//      -> bf16 rows in LDS -> qkv[:, 48w .. 48w+48) (bf16); layer 0 embeds wte[tok] + wpe[pos].
+//   B  attention: units (row, head) 16w .. 16w+16 (two per wave), keys 0..pos from the cache plus
+//      the new k / v from qkv, appended to the cache; out att [64][768] bf16.
+//   C  attn.c_proj + residual: x[:, 16w .. 16w+16) += att W^T + b.
+//   D  ln_2 + mlp.c_fc + gelu_new: hid[:, 64w .. 64w+64) (bf16).
+//   E  mlp.c_proj + residual: x[:, 16w .. 16w+16) += hid W^T + b.
+//   F  (after the 12 blocks) ln_f + LM head over vocab rows [wV/G, (w+1)V/G): per row the best
+//      (logit, id) of the slice.
+//   G  every WG merges the G slices per row (ties -> lower id, torch.argmax) and applies
+//      greedy_step's bookkeeping to its LDS copy of (token, position, done); WG 0 writes the
+//      state / ids.  Rows past R compute garbage that is never stored.
+// Barriers: 5 per block + 1 after F = 61 per step (one monotonic agent-scope counter).
+#include "common.h"
+
+namespace zs {
+namespace dpk {
+
+constexpr int D = 768, NH = 12, HD = 64, DFF = 3072, NLY = 12, RM = 64, QKVN = 3 * D;
+constexpr int G = 48;                  // workgroups per batch, one per CU
+constexpr int NW = 8, NT = 64 * NW;    // 8 waves
+constexpr int HLD = D + 8;             // bf16 row stride of the normalised rows in LDS
+constexpr unsigned SPIN_MAX = 1u << 22;
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8_t;
+typedef __attribute__((ext_vector_type(4))) float f32x4_t;
+typedef __attribute__((ext_vector_type(4))) unsigned u32x4_t;
+typedef __attribute__((ext_vector_type(2))) unsigned u32x2_t;
+typedef __attribute__((address_space(1))) unsigned gu32;
+typedef __attribute__((address_space(1))) unsigned long long gu64;
+
+// workspace (bytes): the sync block first, zeroed by the launcher before every launch:
+//   [0] barrier counter, [4] timeout word, [256..1280) per-row LM-head argmax keys, two step parities
+// att and hid are stored in MFMA A-fragment order ([4 row blocks][K/32 k-steps][64 lanes][8]), so
+// every A-fragment load of the consuming projection is one contiguous KiB per wave-instruction
+constexpr int WS_SYNC = 0;
+constexpr int WS_LMKEY = 256;                      // u64  [2][64]
+constexpr int WS_SYNC_BYTES = 1280;
+constexpr int WS_X = WS_SYNC_BYTES;                // f32  [64][768]
+constexpr int WS_QKV = WS_X + RM * D * 4;          // bf16 [64][2304]
+constexpr int WS_ATT = WS_QKV + RM * QKVN * 2;     // bf16 fragment-packed [4][24][64][8]
+constexpr int WS_HID = WS_ATT + RM * D * 2;        // bf16 fragment-packed [4][96][64][8]
+constexpr int WS_BYTES = WS_HID + RM * DFF * 2;
+
+struct Args {
+  int R, Lmax, max_steps, stop0, stop1, V;
+  const bf16_t* wte; const bf16_t* wpe;
+  const bf16_t* wqkv[NLY]; const float* bqkv[NLY];
+  const bf16_t* wproj[NLY]; const float* bproj[NLY];
+  const bf16_t* wfc[NLY]; const float* bfc[NLY];
+  const bf16_t* wmp[NLY]; const float* bmp[NLY];
+  const float* lnf_w; const float* lnf_b;
+  const bf16_t* wtep;   // wte in B-fragment order [ceil(V/16)][24][64][8] (rows past V zero)
+  float temp;           // generate2's temperature (logits / temp before the argmax; 1 = none)
+  bf16_t* kc[NLY]; bf16_t* vc[NLY];
+  int* pos; int* next_tok; int* done; int* out_ids; int* out_len; int* step_ctr; int* all_done;
+  char* ws;
+};
+
+// LDS: normalised rows [64][HLD] bf16, aliased by the GEMM partial slabs (<= 98,304 B); argmax
+// merge; per-row decode state
+constexpr int SM_HS = RM * HLD * 2;
+constexpr int SM_AM = 2 * NW * RM * 4;
+constexpr int SM_ST = 4 * RM * 4 + 64;
+constexpr int SM_LNF = 2 * D * 4;                 // ln_f weight / bias
+constexpr int SM_TOTAL = SM_HS + SM_AM + SM_ST + SM_LNF;
+static_assert(NW * RM * 48 * 4 <= SM_HS, "QKV partial slabs fit the aliased row buffer");
+
+// ------------------------------------------------------------------ memory helpers
+struct Rs {
+  __amdgpu_buffer_rsrc_t x, qkv, att, hid;
+};
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t mk(char* p, int bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(p, (short)0, bytes, 0x00020000);
+}
+// aux 16 = sc1: stores write through (no release fence needed), loads bypass this CU's L1
+__device__ __forceinline__ u32x4_t ld16(__amdgpu_buffer_rsrc_t r, int off) {
+  return __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 16);
+}
+__device__ __forceinline__ unsigned ld4(__amdgpu_buffer_rsrc_t r, int off) {
+  return __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 16);
+}
+__device__ __forceinline__ void st16(__amdgpu_buffer_rsrc_t r, int off, u32x4_t v) {
+  __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, 16);
+}
+__device__ __forceinline__ void st8(__amdgpu_buffer_rsrc_t r, int off, u32x2_t v) {
+  __builtin_amdgcn_raw_buffer_store_b64(v, r, off, 0, 16);
+}
+__device__ __forceinline__ void st4(__amdgpu_buffer_rsrc_t r, int off, unsigned v) {
+  __builtin_amdgcn_raw_buffer_store_b32(v, r, off, 0, 16);
+}
+__device__ __forceinline__ float4 u2f4(u32x4_t u) {
+  return make_float4(__uint_as_float(u.x), __uint_as_float(u.y), __uint_as_float(u.z),
+                     __uint_as_float(u.w));
+}
+__device__ __forceinline__ u32x4_t f42u(float a, float b, float c, float d) {
+  return u32x4_t{__float_as_uint(a), __float_as_uint(b), __float_as_uint(c), __float_as_uint(d)};
+}
+__device__ __forceinline__ bf16x8_t bf8(u32x4_t u) { return __builtin_bit_cast(bf16x8_t, u); }
+__device__ __forceinline__ f32x4_t mfma(bf16x8_t a, bf16x8_t b, f32x4_t c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+// threadIdx.x through an empty asm: per-phase lane arithmetic is recomputed in the phase
+// instead of being hoisted out of the decode loop by LICM (and spilled: ~200 VGPRs of addresses)
+__device__ __forceinline__ int otid() {
+  int t = threadIdx.x;
+  asm volatile("" : "+v"(t));
+  return t;
+}
+// in-wave exchanges without LDS: DPP within rows of 16, v_permlane16/32_swap across them
+template <int CTRL>
+__device__ __forceinline__ float dppf(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xf, 0xf, false));
+}
+// sum over the 8 lanes of each 8-lane group (quad_perm [1,0,3,2], [2,3,0,1], row_half_mirror)
+__device__ __forceinline__ float sum8(float s) {
+  s += dppf<0xB1>(s);
+  s += dppf<0x4E>(s);
+  return s + dppf<0x141>(s);
+}
+__device__ __forceinline__ float xor8(float v) { return dppf<0x128>(v); }   // row_ror:8
+// v + partner (lane ^ 16 / lane ^ 32), summed in the same order on both lanes
+__device__ __forceinline__ float add16(float v) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+__device__ __forceinline__ float add32(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+__device__ __forceinline__ float max16(float v) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float max32(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+
+// workgroup barrier for LDS hand-offs; waits for nothing in flight in vector memory
+__device__ __forceinline__ void lds_sync() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+// weight fragments of NB 16-column blocks x S k-steps (MFMA B operand, W [N][K] row-major)
+template <int NB, int S>
+__device__ __forceinline__ void load_w(const bf16_t* W, int K, int n0, int N, int kbase,
+                                       bf16x8_t (&b)[NB * S]) {
+  const int lane = otid() & 63, fr = lane & 15, fk = 8 * (lane >> 4);
+#pragma unroll
+  for (int nb = 0; nb < NB; ++nb) {
+    const bf16_t* row = W + (long)min(n0 + 16 * nb + fr, N - 1) * K + kbase + fk;
+#pragma unroll
+    for (int s = 0; s < S; ++s) b[nb * S + s] = *reinterpret_cast<const bf16x8_t*>(row + 32 * s);
+  }
+}
+
+// ------------------------------------------------------------------ diagnostic stamps
+// zs_decode_persist_set_stamps(buf): thread 0 of every workgroup writes s_memrealtime (100 MHz)
+// after each barrier arrive and wait of decode step `stamp_step` into buf[w][2 * barrier + {0,1}]
+// (tools/persist_stamps.py).  The kernel never reads the buffer; NULL (default) = off.
+__device__ unsigned long long* dp_stamp_buf;
+__device__ int dp_stamp_step;
+#define DP_NB 64                       // stamp slots per (workgroup, step): 61 barriers + spare
+__device__ __forceinline__ void stamp(unsigned long long* sb, int slot) {
+  if (sb != nullptr && threadIdx.x == 0) {
+    unsigned long long t;
+    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    ((gu64*)sb)[slot] = t;     // a global (not flat) store
+  }
+}
+
+// ------------------------------------------------------------------ grid barrier
+// Producer side (R1): every storing wave drains its sc1 stores, the workgroup meets, ONE lane adds
+// to the counter.  Consumer side: ONE lane polls the counter (relaxed sc1 loads), the workgroup
+// meets, then every load of handed-off bytes is an sc1 load.  arrive() and wait() are split so a
+// workgroup issues its next phase's weight loads in between.
+struct Bar {
+  gu32* cnt;
+  gu32* tmo;
+  unsigned n;
+  unsigned long long* sb;   // this workgroup's stamp row of the traced step (or NULL)
+  unsigned n0;              // barrier count at the start of the traced step
+};
+__device__ __forceinline__ void bar_arrive(Bar& b) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  if (threadIdx.x == 0)
+    __hip_atomic_fetch_add(b.cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  stamp(b.sb, 2 * (b.n - b.n0));
+  ++b.n;
+}
+typedef __attribute__((address_space(3))) int lds_int_t;
+__device__ __forceinline__ bool bar_wait(Bar& b, volatile lds_int_t* s_ok) {
+  if (threadIdx.x == 0) {
+    const unsigned target = b.n * G;
+    unsigned spins = 0;
+    int ok = 1;
+    while (__hip_atomic_load(b.cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+      ++spins;
+      // bounded spin: give up (and tell every other workgroup) after ~2^22 polls, so a grid that
+      // is not co-resident drains instead of hanging
+      if ((spins & 255) == 0 &&
+          (spins > SPIN_MAX || __hip_atomic_load(b.tmo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
+        __hip_atomic_store(b.tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        ok = 0;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    *s_ok = ok;
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  stamp(b.sb, 2 * (b.n - b.n0) - 1);
+  return *s_ok != 0;
+}
+
+// ------------------------------------------------------------------ LayerNorm rows -> LDS
+// 8 threads per row (row = tid / 8), column quads q + 8i.  MODE 0: x from the workspace;
+// 1: the token embedding wte[tok] + wpe[pos] (layer 0; WG w also stores rows r % G == w of x);
+// 2: x with the ln_f affine.  The LN affine of ln_1 / ln_2 is folded into c_attn / c_fc.
+template <int MODE>
+__device__ __forceinline__ void ln_rows(const Args& a, const Rs& rs, bf16_t* hs, const int* s_tok,
+                                        const int* s_pos, int w, const float* s_lnf = nullptr) {
+  const int tid = otid(), r = tid >> 3, q = tid & 7;
+  const int rr = min(r, a.R - 1);
+  float4 xv[24];
+  if constexpr (MODE == 1) {
+    const bf16_t* te = a.wte + (long)s_tok[r] * D;
+    const bf16_t* pe = a.wpe + (long)s_pos[r] * D;
+    // two halves of 12 quads (the bf16 pairs of a half are converted before the next is issued)
+#pragma unroll
+    for (int hf = 0; hf < 2; ++hf) {
+      uint2 tu[12], pu[12];
+#pragma unroll
+      for (int i = 0; i < 12; ++i) {
+        tu[i] = *reinterpret_cast<const uint2*>(te + 4 * (q + 8 * (12 * hf + i)));
+        pu[i] = *reinterpret_cast<const uint2*>(pe + 4 * (q + 8 * (12 * hf + i)));
+      }
+#pragma unroll
+      for (int i = 0; i < 12; ++i)
+        xv[12 * hf + i] = make_float4(
+            __uint_as_float(tu[i].x << 16) + __uint_as_float(pu[i].x << 16),
+            __uint_as_float(tu[i].x & 0xffff0000u) + __uint_as_float(pu[i].x & 0xffff0000u),
+            __uint_as_float(tu[i].y << 16) + __uint_as_float(pu[i].y << 16),
+            __uint_as_float(tu[i].y & 0xffff0000u) + __uint_as_float(pu[i].y & 0xffff0000u));
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if (r < a.R && r % G == w) {
+#pragma unroll
+      for (int i = 0; i < 24; ++i)
+        st16(rs.x, (r * D + 4 * (q + 8 * i)) * 4, f42u(xv[i].x, xv[i].y, xv[i].z, xv[i].w));
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < 24; ++i) xv[i] = u2f4(ld16(rs.x, (rr * D + 4 * (q + 8 * i)) * 4));
+  }
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < 24; ++i) s += (xv[i].x + xv[i].y) + (xv[i].z + xv[i].w);
+  s += __shfl_xor(s, 1, 64);
+  s += __shfl_xor(s, 2, 64);
+  s += __shfl_xor(s, 4, 64);
+  const float mean = s * (1.0f / D);
+  float qq = 0.f;
+#pragma unroll
+  for (int i = 0; i < 24; ++i) {
+    const float d0 = xv[i].x - mean, d1 = xv[i].y - mean, d2 = xv[i].z - mean, d3 = xv[i].w - mean;
+    qq += (d0 * d0 + d1 * d1) + (d2 * d2 + d3 * d3);
+  }
+  qq += __shfl_xor(qq, 1, 64);
+  qq += __shfl_xor(qq, 2, 64);
+  qq += __shfl_xor(qq, 4, 64);
+  const float rstd = rsqrtf(qq * (1.0f / D) + 1e-5f);
+#pragma unroll
+  for (int i = 0; i < 24; ++i) {
+    const int c = 4 * (q + 8 * i);
+    float y0 = (xv[i].x - mean) * rstd, y1 = (xv[i].y - mean) * rstd;
+    float y2 = (xv[i].z - mean) * rstd, y3 = (xv[i].w - mean) * rstd;
+    if constexpr (MODE == 2) {   // ln_f params staged in LDS at kernel start (s_lnf)
+      const float4 g = *reinterpret_cast<const float4*>(s_lnf + c);
+      const float4 bb = *reinterpret_cast<const float4*>(s_lnf + D + c);
+      y0 = y0 * g.x + bb.x; y1 = y1 * g.y + bb.y; y2 = y2 * g.z + bb.z; y3 = y3 * g.w + bb.w;
+    }
+    *reinterpret_cast<uint2*>(hs + r * HLD + c) = make_uint2(pk2bf(y0, y1), pk2bf(y2, y3));
+  }
+}
+
+// A fragments from the LDS rows, all 4 row blocks, S k-steps from kbase, NB column blocks
+template <int NB, int S>
+__device__ __forceinline__ void mma_lds(const bf16_t* hs, int kbase, const bf16x8_t (&b)[NB * S],
+                                        f32x4_t (&acc)[4][NB]) {
+  const int lane = otid() & 63, fr = lane & 15, fk = 8 * (lane >> 4);
+#pragma unroll
+  for (int rb = 0; rb < 4; ++rb)
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb) acc[rb][nb] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int s = 0; s < S; ++s)
+#pragma unroll
+    for (int rb = 0; rb < 4; ++rb) {
+      const bf16x8_t af = *reinterpret_cast<const bf16x8_t*>(hs + (16 * rb + fr) * HLD + kbase + 32 * s + fk);
+#pragma unroll
+      for (int nb = 0; nb < NB; ++nb) acc[rb][nb] = mfma(af, b[nb * S + s], acc[rb][nb]);
+    }
+}
+
+// partial slab [slab][64][NC] f32: lane's accumulators of NB column blocks from column col0
+template <int NB, int NC>
+__device__ __forceinline__ void put_partial(float* red, int slab, int col0, const f32x4_t (&acc)[4][NB]) {
+  const int lane = otid() & 63, fr = lane & 15, r4 = 4 * (lane >> 4);
+#pragma unroll
+  for (int rb = 0; rb < 4; ++rb)
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        red[(slab * RM + 16 * rb + r4 + i) * NC + col0 + 16 * nb + fr] = acc[rb][nb][i];
+}
+
+// ------------------------------------------------------------------ phase A: ln_1 + c_attn
+__device__ __forceinline__ void phase_qkv(const Args& a, const Rs& rs, int l, char* smem,
+                                          const int* s_tok, const int* s_pos, int w,
+                                          const bf16x8_t (&wq)[9]) {
+  bf16_t* hs = reinterpret_cast<bf16_t*>(smem);
+  float* red = reinterpret_cast<float*>(smem);
+  const int tid = otid(), v = tid >> 6;
+  // epilogue quads (issued first): 64 rows x 12 column quads, quads tid and tid + 512
+  const int c0 = 4 * (tid % 12), c1 = 4 * ((tid + 512) % 12);
+  const float4 b0 = *reinterpret_cast<const float4*>(a.bqkv[l] + 48 * w + c0);
+  const float4 b1 = *reinterpret_cast<const float4*>(a.bqkv[l] + 48 * w + c1);
+  if (l == 0) ln_rows<1>(a, rs, hs, s_tok, s_pos, w);
+  else ln_rows<0>(a, rs, hs, s_tok, s_pos, w);
+  lds_sync();
+  f32x4_t acc[4][3];
+  mma_lds<3, 3>(hs, 96 * v, wq, acc);
+  lds_sync();
+  put_partial<3, 48>(red, v, 0, acc);
+  lds_sync();
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int qd = tid + 512 * h;
+    if (qd >= RM * 12) break;
+    const int row = qd / 12, c = h ? c1 : c0;
+    const float4 bb = h ? b1 : b0;
+    float4 s = *reinterpret_cast<const float4*>(red + row * 48 + c);
+#pragma unroll
+    for (int k = 1; k < NW; ++k) {
+      const float4 p = *reinterpret_cast<const float4*>(red + (k * RM + row) * 48 + c);
+      s.x += p.x; s.y += p.y; s.z += p.z; s.w += p.w;
+    }
+    if (row < a.R)
+      st8(rs.qkv, (row * QKVN + 48 * w + c) * 2,
+          u32x2_t{pk2bf(s.x + bb.x, s.y + bb.y), pk2bf(s.z + bb.z, s.w + bb.w)});
+  }
+}
+
+// ------------------------------------------------------------------ phase B: attention
+__device__ __forceinline__ void bf8_unpack(const uint4& u, float (&f)[8]) {
+  f[0] = __uint_as_float(u.x << 16); f[1] = __uint_as_float(u.x & 0xffff0000u);
+  f[2] = __uint_as_float(u.y << 16); f[3] = __uint_as_float(u.y & 0xffff0000u);
+  f[4] = __uint_as_float(u.z << 16); f[5] = __uint_as_float(u.z & 0xffff0000u);
+  f[6] = __uint_as_float(u.w << 16); f[7] = __uint_as_float(u.w & 0xffff0000u);
+}
+__device__ __forceinline__ uint4 sel4(bool c, const uint4& x, const uint4& y) {
+  return make_uint4(c ? x.x : y.x, c ? x.y : y.y, c ? x.z : y.z, c ? x.w : y.w);
+}
+__device__ __forceinline__ uint4 tou4(u32x4_t u) { return make_uint4(u.x, u.y, u.z, u.w); }
+
+// one wave per two (row, head) units (16 w + 2 v + k); keys in 64-key chunks, 8 lanes per key
+// (lane sub holds dims 8 sub .. 8 sub + 8), online softmax in f32 (decode_attn6 arithmetic).
+// The cached keys of the first chunk do not depend on this step's activations: attn_load issues
+// them BEFORE the workgroup waits on the c_attn barrier (kr / vr held across it).
+__device__ __forceinline__ void attn_unit(const Args& a, const int* s_pos, int w, int v, int k,
+                                          int& row, int& hh, int& p, long& base) {
+  const int u = 16 * w + 2 * v + k;
+  row = u / NH;
+  hh = u % NH;
+  const int rr = min(row, a.R - 1);
+  p = min(s_pos[rr], a.Lmax - 1);
+  base = ((long)(rr * NH + hh) * a.Lmax) * HD + 8 * ((otid() & 63) & 7);
+}
+__device__ __forceinline__ void attn_load(const Args& a, int l, const int* s_pos, int w, int cb,
+                                          uint4 (&kr)[2][8], uint4 (&vr)[2][8]) {
+  const int tid = otid(), v = tid >> 6, grp = (tid & 63) >> 3;
+  const bf16_t* kc = a.kc[l];
+  const bf16_t* vc = a.vc[l];
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    int row, hh, p;
+    long base;
+    attn_unit(a, s_pos, w, v, k, row, hh, p, base);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int jc = max(min(cb + 8 * i + grp, p - 1), 0);
+      kr[k][i] = *reinterpret_cast<const uint4*>(kc + base + (long)jc * HD);
+      vr[k][i] = *reinterpret_cast<const uint4*>(vc + base + (long)jc * HD);
+    }
+  }
+}
+// The new token (key pos, from qkv) is folded in after the cached keys 0..pos-1 (one more
+// online-softmax update with its score and v), so the cached chunks need no per-key selects.
+__device__ __forceinline__ void phase_attn(const Args& a, const Rs& rs, int l, const int* s_pos, int w,
+                                           uint4 (&kr)[2][8], uint4 (&vr)[2][8]) {
+  const int tid = otid(), lane = tid & 63, v = tid >> 6, grp = lane >> 3, sub = lane & 7;
+  float q[2][8], o[2][8], m[2], sum[2];
+  uint4 knu[2], vnu[2];
+  int p[2], row[2], hh[2];
+  long base[2];
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    attn_unit(a, s_pos, w, v, k, row[k], hh[k], p[k], base[k]);
+    const int off = (min(row[k], a.R - 1) * QKVN + hh[k] * HD + 8 * sub) * 2;
+    const uint4 qu = tou4(ld16(rs.qkv, off));
+    knu[k] = tou4(ld16(rs.qkv, off + 2 * D));
+    vnu[k] = tou4(ld16(rs.qkv, off + 4 * D));
+    bf8_unpack(qu, q[k]);
+#pragma unroll
+    for (int t = 0; t < 8; ++t) { q[k][t] *= 0.125f; o[k][t] = 0.f; }
+    m[k] = -INFINITY;
+    sum[k] = 0.f;
+  }
+  const int pmax = max(p[0], p[1]);
+  for (int cb = 0; cb < pmax; cb += 64) {       // cached keys 0 .. p - 1
+    if (cb > 0) attn_load(a, l, s_pos, w, cb, kr, vr);
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      if (cb >= p[k]) continue;                   // wave-uniform
+      float sc[8];
+      float pm = -INFINITY;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        float kf[8];
+        bf8_unpack(kr[k][i], kf);
+        float sv = 0.f;
+#pragma unroll
+        for (int t = 0; t < 8; ++t) sv += q[k][t] * kf[t];
+        sv = sum8(sv);
+        sc[i] = cb + 8 * i + grp < p[k] ? sv : -INFINITY;
+        pm = fmaxf(pm, sc[i]);
+      }
+      pm = fmaxf(pm, xor8(pm));       // group-uniform values: row_ror 8 == lane ^ 8
+      pm = max16(pm);
+      pm = max32(pm);
+      const float mn = fmaxf(m[k], pm);
+      const float scale = __expf(m[k] - mn);   // 0 on the first chunk (m = -inf)
+      sum[k] *= scale;
+#pragma unroll
+      for (int t = 0; t < 8; ++t) o[k][t] *= scale;
+      m[k] = mn;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const float e = __expf(sc[i] - mn);     // masked keys: exp(-inf) = 0
+        sum[k] += e;
+        float vf[8];
+        bf8_unpack(vr[k][i], vf);
+#pragma unroll
+        for (int t = 0; t < 8; ++t) o[k][t] += e * vf[t];
+      }
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    // over the 8 key groups (lanes sub, sub + 8, ..): same additions on every lane
+    sum[k] = add32(add16(sum[k] + xor8(sum[k])));
+#pragma unroll
+    for (int t = 0; t < 8; ++t) o[k][t] = add32(add16(o[k][t] + xor8(o[k][t])));
+    // the new token, key pos: its score from registers
+    float kf[8], vf[8];
+    bf8_unpack(knu[k], kf);
+    bf8_unpack(vnu[k], vf);
+    float sn = 0.f;
+#pragma unroll
+    for (int t = 0; t < 8; ++t) sn += q[k][t] * kf[t];
+    sn = sum8(sn);
+    const float mn = fmaxf(m[k], sn);
+    const float sc = __expf(m[k] - mn), en = __expf(sn - mn);
+    const float inv = 1.0f / (sum[k] * sc + en);
+    float of[8];
+#pragma unroll
+    for (int t = 0; t < 8; ++t) of[t] = (o[k][t] * sc + en * vf[t]) * inv;
+    if (grp == 0 && row[k] < a.R) {
+      u32x4_t pk{pk2bf(of[0], of[1]), pk2bf(of[2], of[3]), pk2bf(of[4], of[5]), pk2bf(of[6], of[7])};
+      // att in A-fragment order: row r, dims 64 h + 8 sub .. + 8 = k-step 2 h + sub / 4,
+      // lane (r & 15) + 16 (sub & 3)
+      const int r = row[k];
+      const int fo = (((r >> 4) * (D / 32) + 2 * hh[k] + (sub >> 2)) * 64 + (r & 15) + 16 * (sub & 3)) * 16;
+      st16(rs.att, fo, pk);
+      // the new token's K / V (read again only by this workgroup, at later steps)
+      *reinterpret_cast<uint4*>(a.kc[l] + base[k] + (long)p[k] * HD) = knu[k];
+      *reinterpret_cast<uint4*>(a.vc[l] + base[k] + (long)p[k] * HD) = vnu[k];
+    }
+  }
+}
+
+// ------------------------------------------------------------------ phases C / E: projections
+// x[:, 16w .. 16w + 16) += A W^T + b, A = att (K 768) or hid (K 3072) from the workspace in
+// A-fragment order; wave v takes k-steps [v S, (v+1) S), its A fragments in chunks of 4 k-steps
+// (two chunks in flight), each fragment load one contiguous KiB
+template <int S>
+__device__ __forceinline__ void phase_proj(const Args& a, const Rs& rs, __amdgpu_buffer_rsrc_t ra,
+                                           int K, const float* bias, char* smem, int w,
+                                           const bf16x8_t (&wb)[S]) {
+  float* red = reinterpret_cast<float*>(smem);
+  const int tid = otid(), lane = tid & 63, v = tid >> 6, fr = lane & 15, fk = 8 * (lane >> 4);
+  // epilogue operands first: 64 rows x 4 quads on threads 0..255
+  const int erow = (tid >> 2) & 63, ec = 16 * w + 4 * (tid & 3);
+  float4 eb = make_float4(0.f, 0.f, 0.f, 0.f), ex = eb;
+  if (tid < 256) {
+    eb = *reinterpret_cast<const float4*>(bias + ec);
+    ex = u2f4(ld16(rs.x, (min(erow, a.R - 1) * D + ec) * 4));
+  }
+  // fragment (rb, k-step s) of this lane at ((rb * K/32 + s) * 64 + lane) * 16 bytes
+  int aoff[4];
+#pragma unroll
+  for (int rb = 0; rb < 4; ++rb) aoff[rb] = ((rb * (K / 32) + v * S) * 64 + lane) * 16;
+  f32x4_t acc[4];
+#pragma unroll
+  for (int rb = 0; rb < 4; ++rb) acc[rb] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  constexpr int CH = 4;                      // k-steps per chunk
+  constexpr int NCH = (S + CH - 1) / CH;
+  u32x4_t af[NCH][4 * CH];
+#pragma unroll
+  for (int c = 0; c < NCH && c < 2; ++c)
+#pragma unroll
+    for (int s = 0; s < CH; ++s)
+#pragma unroll
+      for (int rb = 0; rb < 4; ++rb)
+        if (c * CH + s < S) af[c][s * 4 + rb] = ld16(ra, aoff[rb] + 1024 * (c * CH + s));
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+#pragma unroll
+    for (int s = 0; s < CH; ++s)
+#pragma unroll
+      for (int rb = 0; rb < 4; ++rb)
+        if (c * CH + s < S) acc[rb] = mfma(bf8(af[c][s * 4 + rb]), wb[c * CH + s], acc[rb]);
+    if (c + 2 < NCH) {
+#pragma unroll
+      for (int s = 0; s < CH; ++s)
+#pragma unroll
+        for (int rb = 0; rb < 4; ++rb)
+          if ((c + 2) * CH + s < S) af[c + 2][s * 4 + rb] = ld16(ra, aoff[rb] + 1024 * ((c + 2) * CH + s));
+    }
+  }
+  put_partial<1, 16>(red, v, 0, reinterpret_cast<const f32x4_t(&)[4][1]>(acc));
+  lds_sync();
+  if (tid < 256) {
+    float4 s = *reinterpret_cast<const float4*>(red + erow * 16 + 4 * (tid & 3));
+#pragma unroll
+    for (int k = 1; k < NW; ++k) {
+      const float4 p = *reinterpret_cast<const float4*>(red + (k * RM + erow) * 16 + 4 * (tid & 3));
+      s.x += p.x; s.y += p.y; s.z += p.z; s.w += p.w;
+    }
+    if (erow < a.R)
+      st16(rs.x, (erow * D + ec) * 4,
+           f42u(s.x + eb.x + ex.x, s.y + eb.y + ex.y, s.z + eb.z + ex.z, s.w + eb.w + ex.w));
+  }
+}
+
+// ------------------------------------------------------------------ phase D: ln_2 + c_fc + gelu
+__device__ __forceinline__ float gelu_new_fast(float x) {
+  const float u2 = -1.5957691216057308f * (x + 0.044715f * x * x * x);
+  return x * __builtin_amdgcn_rcpf(1.0f + __expf(u2));
+}
+__device__ __forceinline__ void phase_fc(const Args& a, const Rs& rs, int l, char* smem,
+                                         const int* s_tok, const int* s_pos, int w,
+                                         const bf16x8_t (&wf)[12]) {
+  bf16_t* hs = reinterpret_cast<bf16_t*>(smem);
+  float* red = reinterpret_cast<float*>(smem);
+  const int tid = otid(), v = tid >> 6, cg = v >> 2, kq = v & 3;
+  // epilogue: 64 rows x 16 quads, quads tid and tid + 512 (same column quad)
+  const int c = 4 * (tid & 15);
+  const float4 bb = *reinterpret_cast<const float4*>(a.bfc[l] + 64 * w + c);
+  ln_rows<0>(a, rs, hs, s_tok, s_pos, w);
+  lds_sync();
+  f32x4_t acc[4][2];
+  mma_lds<2, 6>(hs, 192 * kq, wf, acc);
+  lds_sync();
+  put_partial<2, 64>(red, kq, 32 * cg, acc);
+  lds_sync();
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int row = (tid >> 4) + 32 * h;
+    float4 s = *reinterpret_cast<const float4*>(red + row * 64 + c);
+#pragma unroll
+    for (int k = 1; k < 4; ++k) {
+      const float4 p = *reinterpret_cast<const float4*>(red + (k * RM + row) * 64 + c);
+      s.x += p.x; s.y += p.y; s.z += p.z; s.w += p.w;
+    }
+    // hid in A-fragment order: column k = 64 w + c -> k-step k / 32, lane (row & 15) + 16 ((k / 8) & 3)
+    const int k = 64 * w + c;
+    if (row < a.R)
+      st8(rs.hid, ((((row >> 4) * (DFF / 32) + (k >> 5)) * 64 + (row & 15) + 16 * ((k >> 3) & 3)) * 8 + (k & 7)) * 2,
+          u32x2_t{pk2bf(gelu_new_fast(s.x + bb.x), gelu_new_fast(s.y + bb.y)),
+                  pk2bf(gelu_new_fast(s.z + bb.z), gelu_new_fast(s.w + bb.w))});
+  }
+}
+
+// ------------------------------------------------------------------ phase F: ln_f + LM head
+// vocab blocks of 16 rows [w nvb / G, (w+1) nvb / G) of this WG, taken in PAIRS (one A fragment
+// read from LDS feeds the MFMAs of both blocks: half the LDS traffic per MFMA); wave v takes
+// pairs v, v + 8, ..  A pair's weights (wtep: 24 KiB contiguous per block, one KiB per k-step in
+// B-fragment order) arrive as six 4-k-step pieces (both blocks) through a 3-slot register ring:
+// two pieces in flight while one is consumed.  Per lane a running (logit, id) best for each of
+// its 16 rows.  The WG's best per row goes to a 64-bit agent-scope atomic max of
+// key = (order-preserving logit bits, ~id): larger logit wins, then the lower id (torch.argmax),
+// whatever order the workgroups arrive in.
+__device__ __forceinline__ void lm_piece(const bf16_t* Wp, int b0, int b1, int c, bf16x8_t (&b)[8]) {
+  const int lane = otid() & 63;
+  const bf16_t* p0 = Wp + ((long)(b0 * (D / 32) + 4 * c) * 64 + lane) * 8;
+  const bf16_t* p1 = Wp + ((long)(b1 * (D / 32) + 4 * c) * 64 + lane) * 8;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    b[i] = *reinterpret_cast<const bf16x8_t*>(p0 + 512 * i);
+    b[4 + i] = *reinterpret_cast<const bf16x8_t*>(p1 + 512 * i);
+  }
+}
+__device__ __forceinline__ void lm_consume(const bf16_t* hs, int c, const bf16x8_t (&b)[8],
+                                           f32x4_t (&acc)[2][4]) {
+  const int lane = otid() & 63, fr = lane & 15, fk = 8 * (lane >> 4);
+  // A fragments one k-step ahead of the MFMAs (two register sets)
+  const bf16_t* hrow = hs + fr * HLD + 128 * c + fk;
+  bf16x8_t af[2][4];
+#pragma unroll
+  for (int rb = 0; rb < 4; ++rb) af[0][rb] = *reinterpret_cast<const bf16x8_t*>(hrow + 16 * rb * HLD);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    if (i + 1 < 4) {
+#pragma unroll
+      for (int rb = 0; rb < 4; ++rb)
+        af[(i + 1) & 1][rb] = *reinterpret_cast<const bf16x8_t*>(hrow + 16 * rb * HLD + 32 * (i + 1));
+    }
+    // 4 LDS reads, then the 8 MFMAs of the previous reads (sched_group_barrier: DS read 0x100,
+    // MFMA 0x008)
+    __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
+    __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);
+#pragma unroll
+    for (int rb = 0; rb < 4; ++rb) {
+      acc[0][rb] = mfma(af[i & 1][rb], b[i], acc[0][rb]);
+      acc[1][rb] = mfma(af[i & 1][rb], b[4 + i], acc[1][rb]);
+    }
+  }
+}
+__device__ __forceinline__ void phase_lm(const Args& a, const Rs& rs, char* smem, const int* s_tok,
+                                         const int* s_pos, float* am_v, int* am_i, int w,
+                                         gu64* keys, const float* s_lnf) {
+  bf16_t* hs = reinterpret_cast<bf16_t*>(smem);
+  const int tid = otid(), lane = tid & 63, v = tid >> 6, fr = lane & 15, r4 = 4 * (lane >> 4);
+  ln_rows<2>(a, rs, hs, s_tok, s_pos, w, s_lnf);
+  lds_sync();
+  const int nvb = (a.V + 15) / 16;
+  const int b_lo = (int)((long)w * nvb / G), b_hi = (int)((long)(w + 1) * nvb / G);
+  const int npair = (b_hi - b_lo + 1) / 2;              // the last pair may hold one block
+  const int npw = (npair - v + NW - 1) / NW;            // pairs of this wave (>= 1)
+  float bv[16];
+  int bi[16];
+#pragma unroll
+  for (int e = 0; e < 16; ++e) { bv[e] = -INFINITY; bi[e] = 0x7fffffff; }
+  // blocks of pair m of this wave (clamped into the WG's range: loads past it re-read its last
+  // block; their columns are masked below)
+  auto blk = [&](int m, int h) { return min(b_lo + 2 * (v + NW * min(m, npw - 1)) + h, b_hi - 1); };
+  const bool tmp = a.temp != 1.0f;
+  bf16x8_t P0[8], P1[8], P2[8];
+  lm_piece(a.wtep, blk(0, 0), blk(0, 1), 0, P0);
+  lm_piece(a.wtep, blk(0, 0), blk(0, 1), 1, P1);
+  for (int m = 0; m < npw; ++m) {
+    const int b0 = blk(m, 0), b1 = blk(m, 1), n0 = blk(m + 1, 0), n1 = blk(m + 1, 1);
+    f32x4_t acc[2][4];
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int rb = 0; rb < 4; ++rb) acc[h][rb] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    lm_piece(a.wtep, b0, b1, 2, P2);
+    lm_consume(hs, 0, P0, acc);
+    lm_piece(a.wtep, b0, b1, 3, P0);
+    lm_consume(hs, 1, P1, acc);
+    lm_piece(a.wtep, b0, b1, 4, P1);
+    lm_consume(hs, 2, P2, acc);
+    lm_piece(a.wtep, b0, b1, 5, P2);
+    lm_consume(hs, 3, P0, acc);
+    lm_piece(a.wtep, n0, n1, 0, P0);
+    lm_consume(hs, 4, P1, acc);
+    lm_piece(a.wtep, n0, n1, 1, P1);
+    lm_consume(hs, 5, P2, acc);
+    // blocks in increasing id order within the lane: strict > keeps the lower id on ties
+    const int p0 = b_lo + 2 * (v + NW * m);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int col = 16 * (p0 + h) + fr;
+      if (p0 + h < b_hi && col < a.V) {
+#pragma unroll
+        for (int rb = 0; rb < 4; ++rb)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const float val = tmp ? acc[h][rb][i] / a.temp : acc[h][rb][i];
+            if (val > bv[4 * rb + i]) { bv[4 * rb + i] = val; bi[4 * rb + i] = col; }
+          }
+      }
+    }
+  }
+  // over the 16 lanes of each row group (columns), ties -> lower id
+#pragma unroll
+  for (int o = 1; o < 16; o <<= 1)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const float ov = __shfl_xor(bv[e], o, 64);
+      const int oi = __shfl_xor(bi[e], o, 64);
+      if (ov > bv[e] || (ov == bv[e] && oi < bi[e])) { bv[e] = ov; bi[e] = oi; }
+    }
+  if (fr == 0) {
+#pragma unroll
+    for (int rb = 0; rb < 4; ++rb)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int row = 16 * rb + r4 + i;
+        am_v[v * RM + row] = bv[4 * rb + i];
+        am_i[v * RM + row] = bi[4 * rb + i];
+      }
+  }
+  lds_sync();
+  if (tid < RM) {
+    float best = am_v[tid];
+    int bidx = am_i[tid];
+#pragma unroll
+    for (int k = 1; k < NW; ++k) {
+      const float cv = am_v[k * RM + tid];
+      const int ci = am_i[k * RM + tid];
+      if (cv > best || (cv == best && ci < bidx)) { best = cv; bidx = ci; }
+    }
+    const unsigned long long key = ((unsigned long long)f2key(best) << 32) | (unsigned)(~bidx);
+    __hip_atomic_fetch_max(keys + tid, key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+// a workgroup that gave up waiting (grid not co-resident): all_done = {1, -1} tells the host
+__device__ __forceinline__ void gave_up(const Args& a) {
+  if (threadIdx.x == 0) {
+    __hip_atomic_store(&a.all_done[1], -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&a.all_done[0], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+// ------------------------------------------------------------------ the kernel
+__global__ __launch_bounds__(NT) void decode_persist_kernel(Args a) {
+  __shared__ __attribute__((aligned(16))) char smem[SM_TOTAL];
+  float* am_v = reinterpret_cast<float*>(smem + SM_HS);
+  int* am_i = reinterpret_cast<int*>(smem + SM_HS) + NW * RM;
+  int* s_tok = reinterpret_cast<int*>(smem + SM_HS + SM_AM);
+  int* s_pos = s_tok + RM;
+  int* s_done = s_pos + RM;
+  int* s_misc = s_done + RM;     // [0] rows still decoding, [8] barrier ok flag
+  const int w = blockIdx.x;
+  Rs rs;
+  rs.x = mk(a.ws + WS_X, RM * D * 4);
+  rs.qkv = mk(a.ws + WS_QKV, RM * QKVN * 2);
+  rs.att = mk(a.ws + WS_ATT, RM * D * 2);
+  rs.hid = mk(a.ws + WS_HID, RM * DFF * 2);
+  Bar bar{(gu32*)(a.ws + WS_SYNC), (gu32*)(a.ws + WS_SYNC + 4), 0, nullptr, 0};
+  gu64* const lmkey = (gu64*)(a.ws + WS_LMKEY);
+  unsigned long long* const stamps = dp_stamp_buf;
+  const int stamp_step = dp_stamp_step;
+  // the barrier's ok word, through an LDS-typed pointer (a generic volatile pointer became flat
+  // accesses, whose wait is vmcnt(0): every wave then waited for its weight prefetch at each barrier)
+  typedef __attribute__((address_space(3))) int lds_int;
+  volatile lds_int* s_ok = (volatile lds_int*)(s_misc + 8);
+  float* s_lnf = reinterpret_cast<float*>(smem + SM_HS + SM_AM + SM_ST);
+  for (int i = otid(); i < D; i += NT) { s_lnf[i] = a.lnf_w[i]; s_lnf[D + i] = a.lnf_b[i]; }
+
+  if (a.all_done[0]) return;                 // every row stopped at step 0 (uniform)
+  int step = *a.step_ctr;
+  if (step >= a.max_steps) return;
+  if (otid() < RM) {
+    const int tid = otid();
+    const bool in = tid < a.R;
+    s_tok[tid] = in ? a.next_tok[tid] : 0;
+    s_pos[tid] = in ? a.pos[tid] : 0;
+    s_done[tid] = in ? a.done[tid] : 1;
+  }
+  __syncthreads();
+
+  bf16x8_t wq[9], wp[3], wf[12], wm[12];
+#define V_ (otid() >> 6)
+  load_w<3, 3>(a.wqkv[0], D, 48 * w, QKVN, 96 * V_, wq);
+  for (;;) {
+    bar.sb = (stamps != nullptr && step == stamp_step) ? stamps + (long)w * 2 * DP_NB : nullptr;
+    bar.n0 = bar.n;
+    stamp(bar.sb, 2 * DP_NB - 1);   // step start
+    for (int l = 0; l < NLY; ++l) {
+      phase_qkv(a, rs, l, smem, s_tok, s_pos, w, wq);
+      bar_arrive(bar);
+      uint4 kr[2][8], vr[2][8];
+      attn_load(a, l, s_pos, w, 0, kr, vr);
+      if (!bar_wait(bar, s_ok)) return gave_up(a);
+      if (l == 0 && w == 0 && otid() < RM)   // the previous step's argmax keys: every WG has read them
+        __hip_atomic_store(lmkey + ((step + 1) & 1) * RM + otid(), 0ull, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+
+      phase_attn(a, rs, l, s_pos, w, kr, vr);
+      bar_arrive(bar);
+      load_w<1, 3>(a.wproj[l], D, 16 * w, D, 96 * V_, wp);
+      load_w<2, 6>(a.wfc[l], D, 64 * w + 32 * (V_ >> 2), DFF, 192 * (V_ & 3), wf);
+      if (!bar_wait(bar, s_ok)) return gave_up(a);
+
+      phase_proj<3>(a, rs, rs.att, D, a.bproj[l], smem, w, wp);
+      bar_arrive(bar);
+      if (!bar_wait(bar, s_ok)) return gave_up(a);
+
+      phase_fc(a, rs, l, smem, s_tok, s_pos, w, wf);
+      bar_arrive(bar);
+      load_w<1, 12>(a.wmp[l], DFF, 16 * w, D, 384 * V_, wm);
+      if (!bar_wait(bar, s_ok)) return gave_up(a);
+
+      phase_proj<12>(a, rs, rs.hid, DFF, a.bmp[l], smem, w, wm);
+      bar_arrive(bar);
+      // next block's c_attn (after block 11: block 0 of the next step, held through ln_f / LM head)
+      load_w<3, 3>(a.wqkv[l + 1 < NLY ? l + 1 : 0], D, 48 * w, QKVN, 96 * V_, wq);
+      if (!bar_wait(bar, s_ok)) return gave_up(a);
+    }
+    phase_lm(a, rs, smem, s_tok, s_pos, am_v, am_i, w, lmkey + (step & 1) * RM, s_lnf);
+    bar_arrive(bar);
+    if (!bar_wait(bar, s_ok)) return gave_up(a);
+
+    // ---- G: every WG reads the per-row argmax (one agent-scope key per row) and applies
+    // generate2's bookkeeping (greedy_step_kernel, gpt2.hip) to its copy of the row state
+    {
+      const int tid = otid();
+      int alive = 0;
+      if (tid < RM) {
+        const unsigned long long key =
+            __hip_atomic_load(lmkey + (step & 1) * RM + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int t = (int)~(unsigned)key;
+        if (tid < a.R) {
+          int d = s_done[tid];
+          if (!d) {
+            if (w == 0) {
+              a.out_ids[(long)tid * a.max_steps + step] = t;
+              a.out_len[tid] = step + 1;
+            }
+            if (t == a.stop0 || t == a.stop1) d = 1;
+          }
+          alive = !d;
+          s_done[tid] = d;
+          s_tok[tid] = t;
+          s_pos[tid] += 1;
+        }
+      }
+      // rows 0..63 are the lanes of wave 0: one ballot counts the rows still decoding
+      const unsigned long long bal = __ballot(alive);
+      if (tid == 0) s_misc[0] = (int)__popcll(bal);
+    }
+    __syncthreads();
+    stamp(bar.sb, 2 * DP_NB - 2);   // step end
+    const int total = s_misc[0];
+    const bool fin = total == 0 || step + 1 >= a.max_steps;
+    if (fin) {
+      const int tid = otid();
+      if (w == 0) {
+        if (tid < a.R) {
+          a.done[tid] = s_done[tid];
+          a.pos[tid] = s_pos[tid];
+          a.next_tok[tid] = s_tok[tid];
+        }
+        if (tid == 0) {
+          *a.step_ctr = step + 1;
+          a.all_done[0] = 1;
+          a.all_done[2] = total;
+        }
+      }
+      return;
+    }
+    ++step;
+    __syncthreads();     // s_misc is rewritten next step
+  }
+}
+
+}  // namespace dpk
+}  // namespace zs
+
+using namespace zs;
+
+extern "C" int zs_decode_persist_workspace_bytes(void) { return dpk::WS_BYTES; }
+extern "C" int zs_decode_persist_grid(void) { return dpk::G; }
+
+extern "C" int zs_gpt2_decode_persist(int R, int Lmax, int max_steps, int stop0, int stop1, int V,
+                                      const void* wte, const void* wpe, const void* wte_packed,
+                                      float temperature, const void* const* layer_w,
+                                      const float* lnf_w, const float* lnf_b, void* const* kv,
+                                      int* pos, int* next_tok, int* done, int* out_ids,
+                                      int* out_len, int* step_ctr, int* all_done, void* ws,
+                                      long ws_bytes, void* stream) {
+  using namespace dpk;
+  ZS_REQUIRE(R >= 1 && R <= RM, "zs_gpt2_decode_persist: R in 1..%d (got %d)", RM, R);
+  ZS_REQUIRE(V >= 16 * NW * G && V <= 1 << 24, "zs_gpt2_decode_persist: vocab %d", V);
+  ZS_REQUIRE(Lmax >= 2 && max_steps >= 1, "zs_gpt2_decode_persist: Lmax %d max_steps %d", Lmax, max_steps);
+  ZS_REQUIRE(ws && ws_bytes >= WS_BYTES && ((uintptr_t)ws & 255) == 0,
+             "zs_gpt2_decode_persist: workspace of %d bytes, 256-byte aligned", WS_BYTES);
+  ZS_REQUIRE(temperature > 0.f, "zs_gpt2_decode_persist: temperature %g (> 0)", temperature);
+  ZS_REQUIRE(wte_packed && ((uintptr_t)wte_packed & 15) == 0,
+             "zs_gpt2_decode_persist: wte_packed null or not 16-byte aligned");
+  ZS_REQUIRE(wte && wpe && layer_w && lnf_w && lnf_b && kv && pos && next_tok && done && out_ids &&
+             out_len && step_ctr && all_done, "zs_gpt2_decode_persist: null pointer");
+  Args a{};
+  a.R = R; a.Lmax = Lmax; a.max_steps = max_steps; a.stop0 = stop0; a.stop1 = stop1; a.V = V;
+  a.wte = (const bf16_t*)wte; a.wpe = (const bf16_t*)wpe;
+  for (int l = 0; l < NLY; ++l) {
+    const void* const* p = layer_w + 8 * l;
+    for (int k = 0; k < 8; ++k)
+      ZS_REQUIRE(p[k] && ((uintptr_t)p[k] & 15) == 0,
+                 "zs_gpt2_decode_persist: layer %d pointer %d null or not 16-byte aligned", l, k);
+    a.wqkv[l] = (const bf16_t*)p[0]; a.bqkv[l] = (const float*)p[1];
+    a.wproj[l] = (const bf16_t*)p[2]; a.bproj[l] = (const float*)p[3];
+    a.wfc[l] = (const bf16_t*)p[4]; a.bfc[l] = (const float*)p[5];
+    a.wmp[l] = (const bf16_t*)p[6]; a.bmp[l] = (const float*)p[7];
+    ZS_REQUIRE(kv[l] && kv[NLY + l], "zs_gpt2_decode_persist: KV cache pointer");
+    a.kc[l] = (bf16_t*)kv[l];
+    a.vc[l] = (bf16_t*)kv[NLY + l];
+  }
+  a.lnf_w = lnf_w; a.lnf_b = lnf_b; a.wtep = (const bf16_t*)wte_packed; a.temp = temperature;
+  a.pos = pos; a.next_tok = next_tok; a.done = done; a.out_ids = out_ids; a.out_len = out_len;
+  a.step_ctr = step_ctr; a.all_done = all_done; a.ws = (char*)ws;
+  // the barrier counter and timeout word: zeroed before every launch (a memset node under capture)
+  ZS_CHECK_HIP(hipMemsetAsync(ws, 0, WS_SYNC_BYTES, S(stream)));
+  hipLaunchKernelGGL(decode_persist_kernel, dim3(G), dim3(NT), 0, S(stream), a);
+  ZS_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int zs_decode_persist_set_stamps(void* buf, int step) {
+  ZS_CHECK_HIP(hipMemcpyToSymbol(HIP_SYMBOL(dpk::dp_stamp_buf), &buf, sizeof(buf)));
+  ZS_CHECK_HIP(hipMemcpyToSymbol(HIP_SYMBOL(dpk::dp_stamp_step), &step, sizeof(step)));
+  return 0;
+}
+
+// timeout word of the last launch on this workspace (non-zero: the grid was not co-resident and
+// the launch gave up; the outputs are invalid).  Host-side read, after a synchronisation.
+extern "C" int zs_decode_persist_status(const void* ws, int* timed_out) {
+  ZS_REQUIRE(ws && timed_out, "zs_decode_persist_status: null pointer");
+  unsigned t = 0;
+  ZS_CHECK_HIP(hipMemcpy(&t, (const char*)ws + 4, 4, hipMemcpyDeviceToHost));
+  *timed_out = (int)t;
+  return 0;
+}

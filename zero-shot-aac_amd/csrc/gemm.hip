@@ -525,7 +525,10 @@ template <typename T, int BM, int KMAX>
 __global__ __launch_bounds__(256) void lmhead_kernel(int xcd_order, int M, int K, int V, const T* A, int lda,
                                                      const T* W, int topk, int row_norm,
                                                      float* part_stat, float* part_val,
-                                                     int* part_idx) {
+                                                     int* part_idx, float temp) {
+  // temp != 1: logits / temp before the top-k and the softmax statistics (generate2 /
+  // generate_beam's `temperature`, gpt2_prefix_eval.py:121, 196); a true division, as the reference
+  const bool tdiv = temp != 1.0f;
   constexpr int LDW = BK + GemmTraits<T>::PAD;
   constexpr int TM = BM / 64, TN = LM_BN / 64;
   constexpr int SM_MAIN = 2 * (BM + LM_BN) * LDW * (int)sizeof(T);
@@ -631,6 +634,7 @@ __global__ __launch_bounds__(256) void lmhead_kernel(int xcd_order, int M, int K
         for (int e = 0; e < 16; ++e) {
           const int n = n0 + wr0 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5);
           float cv = n < V ? acct[i][j][e] * sc : -INFINITY;
+          if (tdiv) cv = cv / temp;
           int ci = n;
           // n increases with (i, e): strict > keeps the lower index first among equals
           if (cv > tv[KMAX - 1]) {
@@ -673,7 +677,7 @@ __global__ __launch_bounds__(256) void lmhead_kernel(int xcd_order, int M, int K
 #pragma unroll
           for (int e = 0; e < 16; ++e) {
             const int n = n0 + wr0 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5);
-            if (n < V) se += __expf(acct[i][j][e] * sc - bv);
+            if (n < V) se += __expf((tdiv ? acct[i][j][e] * sc / temp : acct[i][j][e] * sc) - bv);
           }
         se += __shfl_xor(se, 32, 64);
       }
@@ -744,7 +748,8 @@ __global__ __launch_bounds__(256) void lmhead_kernel(int xcd_order, int M, int K
   for (int c = sub * CPT; c < sub * CPT + CPT; ++c) {
     const int n = n0 + c;
     if (n >= V) break;
-    const float v = tile[r * (LM_BN + 1) + c] * scale;
+    float v = tile[r * (LM_BN + 1) + c] * scale;
+    if (tdiv) v = v / temp;
     mx = fmaxf(mx, v);
     // insertion into the descending top-k list (strict > keeps the lower index on ties)
     if (KMAX == 1) {
@@ -772,7 +777,7 @@ __global__ __launch_bounds__(256) void lmhead_kernel(int xcd_order, int M, int K
   for (int c = sub * CPT; part_stat != nullptr && c < sub * CPT + CPT; ++c) {
     const int n = n0 + c;
     if (n >= V) break;
-    se += expf(tile[r * (LM_BN + 1) + c] * scale - gmx);
+    se += expf((tdiv ? tile[r * (LM_BN + 1) + c] * scale / temp : tile[r * (LM_BN + 1) + c] * scale) - gmx);
   }
 #pragma unroll
   for (int o = 1; o < TPR; o <<= 1) se += __shfl_xor(se, o, 64);
@@ -876,6 +881,15 @@ extern "C" int zs_lmhead_nblk(int V) { return cdiv(V, LM_BN); }
 extern "C" int zs_lmhead_topk(int M, int K, int V, int dtype, const void* A, int lda,
                               const void* W, int topk, int row_norm, float* part_stat,
                               float* part_val, int* part_idx, void* stream) {
+  return zs_lmhead_topk_t(M, K, V, dtype, A, lda, W, topk, row_norm, 1.0f, part_stat, part_val,
+                          part_idx, stream);
+}
+
+extern "C" int zs_lmhead_topk_t(int M, int K, int V, int dtype, const void* A, int lda,
+                                const void* W, int topk, int row_norm, float temperature,
+                                float* part_stat, float* part_val, int* part_idx, void* stream) {
+  ZS_REQUIRE(temperature > 0.f, "zs_lmhead_topk_t: temperature %g (> 0)", temperature);
+  ZS_REQUIRE(!row_norm || temperature == 1.0f, "zs_lmhead_topk_t: row_norm with temperature");
   ZS_REQUIRE(M > 0 && K > 0 && V > 0, "zs_lmhead_topk: bad shape");
   ZS_REQUIRE(K % BK == 0 && lda % 8 == 0, "zs_lmhead_topk: K %% 32, lda %% 8");
   ZS_REQUIRE(((uintptr_t)A & 15) == 0 && ((uintptr_t)W & 15) == 0,
@@ -887,7 +901,7 @@ extern "C" int zs_lmhead_topk(int M, int K, int V, int dtype, const void* A, int
   hipLaunchKernelGGL((lmhead_kernel<T, BM_, KM_>), dim3(nblk * cdiv(M, BM_)), dim3(256), 0, st, \
                      (g_fast_xcd ? 1 : 0) | (g_lm_prio ? 2 : 0), M, K, V, (const T*)A, lda,       \
                      (const T*)W, topk, row_norm, part_stat,                                      \
-                     part_val, part_idx)
+                     part_val, part_idx, temperature)
 #define LMH_K(T, BM_) do { if (topk == 1) LMH(T, BM_, 1); else LMH(T, BM_, 8); } while (0)
   if (M <= 64) {
     if (dtype == ZS_BF16) LMH_K(bf16_t, 64); else LMH_K(float, 64);

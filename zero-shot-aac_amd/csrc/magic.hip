@@ -216,7 +216,7 @@ __global__ __launch_bounds__(256) void magic_maxcos_kernel(const T* __restrict__
 __global__ __launch_bounds__(256) void magic_score_kernel(
     const float* __restrict__ pval, const float* __restrict__ maxcos,
     const float* __restrict__ text, const float* __restrict__ audio, int E, int b, int W,
-    int nact, float inv_temp, float alpha, float beta, float* __restrict__ score) {
+    int nact, float inv_temp, float alpha, float beta, float* __restrict__ score, float stemp) {
   __shared__ float cl[8 * 64];
   const int k = blockIdx.x, lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int n = nact * W;
@@ -242,7 +242,9 @@ __global__ __launch_bounds__(256) void magic_score_kernel(
     const float lse = mx + __logf(wave_sum(s));
     for (int i = lane; i < n; i += 64) {
       const long c = (long)k * b * W + i;
-      score[c] = (1.0f - alpha) * pval[c] - alpha * maxcos[c] + beta * (cl[i] - lse);
+      const float sc = (1.0f - alpha) * pval[c] - alpha * maxcos[c] + beta * (cl[i] - lse);
+      // generate_beam_magic's `temperature` divides the ranking score (gpt2_prefix_eval.py:629)
+      score[c] = stemp != 1.0f ? sc / stemp : sc;
     }
   }
 }
@@ -417,11 +419,20 @@ extern "C" int zs_magic_maxcos(const void* hid, int ncand, int W, void* ctx, int
 extern "C" int zs_magic_score(const float* pval, const float* maxcos, const float* text,
                               const float* audio, int C, int E, int b, int W, int nact, float temp,
                               float alpha, float beta, float* score, void* stream) {
+  return zs_magic_score_t(pval, maxcos, text, audio, C, E, b, W, nact, temp, alpha, beta, 1.0f,
+                          score, stream);
+}
+
+extern "C" int zs_magic_score_t(const float* pval, const float* maxcos, const float* text,
+                                const float* audio, int C, int E, int b, int W, int nact,
+                                float temp, float alpha, float beta, float score_temp,
+                                float* score, void* stream) {
+  ZS_REQUIRE(score_temp > 0.f, "zs_magic_score_t: temperature %g (> 0)", score_temp);
   ZS_REQUIRE(C > 0 && E > 0 && b >= 1 && b <= MAGIC_MAXB && W >= 1 && W <= MAGIC_MAXW &&
              nact >= 1 && nact <= b && nact * W <= 8 * 64 && temp > 0.f,
              "zs_magic_score: 1 <= beams <= %d, 1 <= width <= %d", MAGIC_MAXB, MAGIC_MAXW);
   hipLaunchKernelGGL(magic_score_kernel, dim3(C), dim3(256), 0, S(stream), pval, maxcos, text,
-                     audio, E, b, W, nact, 1.0f / temp, alpha, beta, score);
+                     audio, E, b, W, nact, 1.0f / temp, alpha, beta, score, score_temp);
   ZS_LAUNCH_CHECK();
   return 0;
 }

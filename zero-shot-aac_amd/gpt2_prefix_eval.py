@@ -12,9 +12,12 @@ runs on the MI355X kernels with a KV cache (the reference recomputes the whole s
 step; identical math).  For throughput use the batched zsaac.pipeline.CaptionPipeline: these
 functions keep the reference's one-clip-per-call signature.
 
-Deviations (documented): temperature must be 1 (the reference's only value on this
-path); a stop token emitted as the very first token returns that one-token caption (the reference
-crashes there: ``tokens.squeeze()`` is 0-d, gpt2_prefix_eval.py:218).
+``temperature`` divides the logits as the reference does (``temperature if temperature > 0 else
+1.0``, lines 121, 196, 629): in the LM-head kernel's top-k / softmax statistics (zs_lmhead_topk_t,
+zs_gpt2_decode_persist) and in the magic ranking score (zs_magic_score_t).
+
+Deviation (documented): a stop token emitted as the very first token returns that
+one-token caption (the reference crashes there: ``tokens.squeeze()`` is 0-d, line 218).
 """
 from typing import List
 
@@ -44,9 +47,9 @@ def _decoder(model, embed, entry_length, beam):
     return dec, P
 
 
-def _check_temperature(temperature):
-    if temperature != 1.0:
-        raise NotImplementedError("temperature != 1 is not supported on the HIP decode path")
+def _temperature(temperature) -> float:
+    """The reference's divisor: ``temperature if temperature > 0 else 1.0``."""
+    return float(temperature) if temperature > 0 else 1.0
 
 
 def generate2(model, tokenizer, tokens=None, prompt=None, embed=None, entry_count=1, entry_length=67,
@@ -55,7 +58,6 @@ def generate2(model, tokenizer, tokens=None, prompt=None, embed=None, entry_coun
     argmax (gpt2_prefix_eval.py:194-212); stop after appending ``stop_token`` or 764 (' .').
     Like the reference, the returned text starts with the prompt tokens (``tokens`` or the
     encoded ``prompt``) when no ``embed`` is given (lines 182-184, 209-210, 218)."""
-    _check_temperature(temperature)
     if embed is None:
         if tokens is None:
             tokens = torch.tensor(tokenizer.encode(prompt)).unsqueeze(0)
@@ -66,6 +68,7 @@ def generate2(model, tokenizer, tokens=None, prompt=None, embed=None, entry_coun
     dec, P = _decoder(model, embed, entry_length, 1)
     dec.prefill(1, P)
     dec.stop0 = stop
+    dec.temperature = _temperature(temperature)
     ids, ln = dec.greedy(1, P)
     out = head + ids[0, :int(ln[0])].tolist()
     return tokenizer.decode(out)
@@ -78,7 +81,6 @@ def generate_beam(model, tokenizer, beam_size: int = 5, prompt=None, embed=None,
     ``prompt`` and no ``embed`` each beam's token row starts with the prompt ids and is cut at
     ``seq_length`` (which counts generated tokens only), as the reference does (lines 112-130,
     154-155)."""
-    _check_temperature(temperature)
     head = []
     if embed is None:
         tokens = torch.tensor(tokenizer.encode(prompt)).unsqueeze(0)
@@ -89,6 +91,7 @@ def generate_beam(model, tokenizer, beam_size: int = 5, prompt=None, embed=None,
     dec, P = _decoder(model, embed, entry_length, beam_size)
     dec.prefill(1, P, row_stride=beam_size)
     dec.stop0 = stop
+    dec.temperature = _temperature(temperature)
     ids, ln, sc = dec.beam(1, beam_size, P)
     ids, ln, sc = ids[0].cpu(), ln[0].cpu(), sc[0].cpu()
     texts = [tokenizer.decode((head + ids[i].tolist())[:int(ln[i])]) for i in range(beam_size)]
@@ -167,7 +170,6 @@ def generate_beam_magic(model, clap, tokenizer, audio_embeds, beam_size: int = 5
     log-softmax of the candidate text, then length-normalised beam selection; texts sorted best
     first.  ``embed`` is required (with only a ``prompt`` the reference feeds the prompt ids into
     the candidate texts and token rows, a path its own callers never take)."""
-    _check_temperature(temperature)
     if embed is None:
         raise NotImplementedError("generate_beam_magic needs embed= (predict_prompt.py:140)")
     stop = tokenizer.encode(stop_token)[0]
@@ -176,7 +178,7 @@ def generate_beam_magic(model, clap, tokenizer, audio_embeds, beam_size: int = 5
     eng = _magic_engine(model, clap, P, beam_size, magic_width, entry_length)
     (toks, _), = eng.beam_magic(hard, hl, soft, P, audio, tokenizer, clap.text_encoder.tokenizer,
                                 beam_size, magic_width, entry_length, alpha, beta,
-                                float(clap.temp), stop)
+                                float(clap.temp), stop, temperature=_temperature(temperature))
     return [tokenizer.decode(t) for t in toks]
 
 

@@ -63,10 +63,16 @@ SIGNATURES = {
     "zs_compact_rows": [P, I, P, P, P],
     "zs_greedy_step_map": [P, P, I, P, I, I, P, I, I, I, P, P, P, P, P, P, P],
     "zs_lmhead_topk": [I, I, I, I, P, I, P, I, I, P, P, P, P],
+    "zs_lmhead_topk_t": [I, I, I, I, P, I, P, I, I, F, P, P, P, P],
     "zs_lmhead_nblk": [I],
     "zs_argmax_finalize": [P, P, I, I, P, P],
     "zs_prefix_ids_assemble": [P, I, P, P, I, I, I, P, P],
     "zs_greedy_step": [P, P, I, I, P, I, I, I, P, P, P, P, P, P, P],
+    "zs_decode_persist_workspace_bytes": [],
+    "zs_decode_persist_grid": [],
+    "zs_gpt2_decode_persist": [I, I, I, I, I, I, P, P, P, F, P, P, P, P, P, P, P, P, P, P, P, P, L, P],
+    "zs_decode_persist_status": [P, P],
+    "zs_decode_persist_set_stamps": [P, I],
     "zs_beam_step": [P, P, P, I, I, I, I, I, I, P, I, P, P, P, P, P, P, P, I, P, P, P, P],
     "zs_bert_embed_ln": [P, I, I, P, P, P, P, P, F, P, P, I, P],
     "zs_layernorm_dual": [P, I, I, I, P, P, F, P, I, P, I, I, P],
@@ -84,6 +90,7 @@ SIGNATURES = {
     "zs_mistral_silu_mul": [P, I, L, I, I, P, I, P],
     "zs_mistral_attention": [P, I, I, I, P, I, P, P, I, P, I, P],
     "zs_mistral_decode_attention": [P, I, L, I, I, I, P, P, P, P, P, I, P, I, P],
+    "zs_magic_score_t": [P, P, P, P, I, I, I, I, I, F, F, F, F, P, P],
     "zs_magic_step": [P, P, I, I, I, I, I, I, I, P, P, P, P, P, I, P, I, P, P, P, P, P, I, P],
 }
 

@@ -17,6 +17,7 @@ from __future__ import annotations
 
 import copy
 import math
+import os
 from typing import Dict, List, Optional, Tuple
 
 import torch
@@ -197,6 +198,23 @@ class Gpt2Weights:
                 "mproj_w": t("mlp.c_proj.weight"), "mproj_b": _f32(sd[h + "mlp.c_proj.bias"], device),
             })
         self.lnf = (_f32(sd[p + "ln_f.weight"], device), _f32(sd[p + "ln_f.bias"], device))
+        self._layer_ptrs = None
+
+    def layer_ptrs(self):
+        """The 12 x 8 device pointers zs_gpt2_decode_persist takes (c_attn W, b, attn.c_proj W, b,
+        c_fc W, b, mlp.c_proj W, b per block; bf16 with the LN affine folded)."""
+        if self._layer_ptrs is None:
+            import ctypes
+            keys = ("attn_w", "attn_b", "proj_w", "proj_b", "fc_w", "fc_b", "mproj_w", "mproj_b")
+            self._layer_ptrs = (ctypes.c_void_p * (8 * NL))(
+                *[ly[k].data_ptr() for ly in self.layers for k in keys])
+        return self._layer_ptrs
+
+    def wte_packed(self):
+        """The tied LM head in MFMA B-fragment order (zs_gpt2_decode_persist), built once."""
+        if getattr(self, "_wte_packed", None) is None:
+            self._wte_packed = ops.pack_b_fragments(self.wte)
+        return self._wte_packed
 
     def nbytes(self) -> int:
         n = self.wte.numel() + self.wpe.numel()
@@ -213,7 +231,8 @@ class Gpt2Decoder:
 
     def __init__(self, w: Gpt2Weights, max_rows: int, max_prompt: int, max_steps: int = 67,
                  max_prefill_rows: Optional[int] = None, topk: int = 8, chunk: int = 0,
-                 use_graph: bool = True, compact: Optional[bool] = None):
+                 use_graph: bool = True, compact: Optional[bool] = None,
+                 persist: Optional[bool] = None):
         if chunk <= 0:   # a divisor of the steps after step 0, near 6 (no wasted tail steps)
             n = max(max_steps - 1, 1)
             cands = [c for c in range(4, 13) if n % c == 0]
@@ -232,6 +251,7 @@ class Gpt2Decoder:
         self.max_steps = max_steps
         self.topk, self.chunk, self.use_graph = topk, chunk, use_graph
         self.stop0, self.stop1 = STOP_DOT, STOP_SPACE_DOT   # generate2 stops on '.' and ' .'
+        self.temperature = 1.0      # logits / temperature (gpt2_prefix_eval.py:121, 196)
         # + chunk: a replayed graph chunk may run a few steps past entry_length (no-ops)
         self.Lmax = max_prompt + max_steps + chunk + 1
         dt = self.dtype
@@ -270,6 +290,16 @@ class Gpt2Decoder:
             compact = dt == torch.bfloat16
         self.compact = (compact and dt == torch.bfloat16 and self.Lmax <= 128
                         and self.R >= self.min_bucket)
+        # greedy bf16 decode of one eval batch (<= 64 rows): all steps after step 0 in one
+        # persistent launch (zs_gpt2_decode_persist) instead of graph-replayed per-step chains
+        if persist is None:
+            persist = os.environ.get("ZSAAC_PERSIST", "1") != "0"
+        self.persist = bool(persist) and dt == torch.bfloat16 and w.folded and self.R <= 64
+        if self.persist:
+            import ctypes
+            self.persist_ws = ops.decode_persist_workspace(dev)
+            self._kv_ptrs = (ctypes.c_void_p * (2 * NL))(
+                *[t.data_ptr() for t in self.kc], *[t.data_ptr() for t in self.vc])
         self.rowmap = torch.zeros(self.R, **i32)
         self.cpos = torch.zeros(self.R, **i32)      # this step's positions in compact order
         self.n_act = torch.zeros(1, **i32)
@@ -359,7 +389,8 @@ class Gpt2Decoder:
 
     def _greedy_step_body_c(self, R, Rb):
         self._decode_forward_c(R, Rb)
-        ops.lmhead_topk(self.hf[:Rb], self.w.wte, 1, None, self.pval1, self.pidx1)
+        ops.lmhead_topk(self.hf[:Rb], self.w.wte, 1, None, self.pval1, self.pidx1,
+                        temperature=self.temperature)
         ops.greedy_step_map(self.pval1, self.pidx1, Rb, self.rowmap, R, self.nblk, self.step_ctr,
                             self.max_steps, self.stop0, self.stop1, self.out_ids, self.out_len,
                             self.done, self.pos, self.next_tok, self.all_done)
@@ -377,7 +408,7 @@ class Gpt2Decoder:
             return key, body, None
         R = self._cgreedy
         Rb = self._bucket_rows(R, alive)
-        return (("greedy_c", R, Rb, self.stop0, self.stop1),
+        return (("greedy_c", R, Rb, self.stop0, self.stop1, self.temperature),
                 lambda: self._greedy_step_body_c(R, Rb),
                 lambda: ops.compact_rows(self.done, R, self.rowmap, self.n_act))
 
@@ -396,7 +427,8 @@ class Gpt2Decoder:
 
     def _greedy_step_body(self, R):
         self._decode_forward(R)
-        ops.lmhead_topk(self.hf[:R], self.w.wte, 1, None, self.pval1, self.pidx1)
+        ops.lmhead_topk(self.hf[:R], self.w.wte, 1, None, self.pval1, self.pidx1,
+                        temperature=self.temperature)
         ops.greedy_step(self.pval1, self.pidx1, R, self.nblk, self.step_ctr, self.max_steps,
                         self.stop0, self.stop1, self.out_ids, self.out_len, self.done, self.pos,
                         self.next_tok, self.all_done)
@@ -451,11 +483,15 @@ class Gpt2Decoder:
                 body()
 
     def finished_async(self):
-        """Enqueue a copy of all_done to pinned host memory; returns (event, host tensor):
-        [0] = finished flag, [2] = rows still decoding."""
+        """Enqueue a copy of all_done + step_ctr to pinned host memory; returns (event, host
+        tensor): [0] = finished flag, [1] < 0 = a persistent launch gave up, [2] = rows still
+        decoding, [3] = decode steps done."""
         if not hasattr(self, "_flag_host"):
-            self._flag_host = torch.zeros(3, dtype=torch.int32, pin_memory=True)
-        self._flag_host.copy_(self.all_done, non_blocking=True)
+            self._flag_host = torch.zeros(4, dtype=torch.int32, pin_memory=True)
+            self._flag_dev = torch.zeros(4, dtype=torch.int32, device=self.dev)
+        self._flag_dev[:3].copy_(self.all_done)
+        self._flag_dev[3:].copy_(self.step_ctr)
+        self._flag_host.copy_(self._flag_dev, non_blocking=True)
         ev = torch.cuda.Event()
         ev.record()
         return ev, self._flag_host
@@ -463,7 +499,10 @@ class Gpt2Decoder:
     def run_to_completion(self):
         """Synchronous loop: replay chunks until every row stopped or entry_length reached."""
         for _ in range(self.n_chunks):
-            flag, _, alive = self.all_done.tolist()
+            flag, arr, alive = self.all_done.tolist()
+            if arr < 0:
+                raise RuntimeError("zs_gpt2_decode_persist: the persistent grid was not co-resident "
+                                   "(gave up waiting); too many launches in flight for the CUs")
             if flag:
                 break
             self.step_chunk(alive)
@@ -477,15 +516,25 @@ class Gpt2Decoder:
         """Enqueue step 0 of generate2 from the prefill rows (no host sync); afterwards
         :meth:`step_chunk` advances ``chunk`` steps at a time."""
         R = B
-        ops.lmhead_topk(self.hf[:R], self.w.wte, 1, None, self.pval1, self.pidx1)
+        ops.lmhead_topk(self.hf[:R], self.w.wte, 1, None, self.pval1, self.pidx1,
+                        temperature=self.temperature)
         self.pos[:R].copy_(self.plen[:R] - 1)
         for t in (self.done, self.out_len, self.step_ctr, self.all_done, self.out_ids):
             t.zero_()
         ops.greedy_step(self.pval1, self.pidx1, R, self.nblk, self.step_ctr, self.max_steps,
                         self.stop0, self.stop1, self.out_ids, self.out_len, self.done, self.pos,
                         self.next_tok, self.all_done)
-        self._active = (("greedy", R, self.stop0, self.stop1), lambda: self._greedy_step_body(R))
+        self._active = (("greedy", R, self.stop0, self.stop1, self.temperature),
+                        lambda: self._greedy_step_body(R))
         self._cgreedy = R if (self.compact and R >= self.min_bucket) else None
+        if self.persist and R <= 64:
+            w = self.w
+            ops.gpt2_decode_persist(R, self.Lmax, self.max_steps, self.stop0, self.stop1, w.V, w.wte,
+                                    w.wpe, w.wte_packed(), self.temperature, w.layer_ptrs(),
+                                    w.lnf[0], w.lnf[1], self._kv_ptrs,
+                                    self.pos, self.next_tok, self.done, self.out_ids, self.out_len,
+                                    self.step_ctr, self.all_done, self.persist_ws)
+            self.rows_stepped += R * (self.max_steps - 1)   # upper bound (rows that stop early end it)
 
     def greedy(self, B: int, Pmax: int):
         """After :meth:`prefill` (row_stride 1): generate2 for all B rows.
@@ -498,7 +547,8 @@ class Gpt2Decoder:
     def _beam_step_body(self, C, beam):
         R = C * beam
         self._decode_forward(R, kvrow=self.kvrow[:R])
-        ops.lmhead_topk(self.hf[:R], self.w.wte, self.topk, self.pstat, self.pval, self.pidx)
+        ops.lmhead_topk(self.hf[:R], self.w.wte, self.topk, self.pstat, self.pval, self.pidx,
+                        temperature=self.temperature)
         ops.beam_step(self.pstat, self.pval, self.pidx, C, beam, self.nblk, self.topk, False,
                       self.stop0, self.step_ctr, self.max_steps, self.scores, self.seq_len,
                       self.done, self.out_ids, self.tok_tmp, self.kvrow, self.kvrow_tmp, self.Lmax,
@@ -517,7 +567,8 @@ class Gpt2Decoder:
     def beam_begin(self, C: int, beam: int):
         assert beam <= self.topk and C * beam <= self.R
         R = C * beam
-        ops.lmhead_topk(self.hf[:C], self.w.wte, self.topk, self.pstat, self.pval, self.pidx)
+        ops.lmhead_topk(self.hf[:C], self.w.wte, self.topk, self.pstat, self.pval, self.pidx,
+                        temperature=self.temperature)
         for t in (self.done, self.step_ctr, self.all_done, self.out_ids, self.scores):
             t.zero_()
         self.seq_len.fill_(1.0)
@@ -526,7 +577,8 @@ class Gpt2Decoder:
                       self.stop0, self.step_ctr, self.max_steps, self.scores, self.seq_len,
                       self.done, self.out_ids, self.tok_tmp, self.kvrow, self.kvrow_tmp, self.Lmax,
                       self.pos, self.next_tok, self.all_done)
-        self._active = (("beam", C, beam, self.stop0), lambda: self._beam_step_body(C, beam))
+        self._active = (("beam", C, beam, self.stop0, self.temperature),
+                        lambda: self._beam_step_body(C, beam))
         self._cgreedy = None
 
     # ---------------------------------------------------------------- get_prefix_tokens

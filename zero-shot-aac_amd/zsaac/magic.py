@@ -133,7 +133,7 @@ class MagicDecoder:
         return out
 
     def _run(self, C, b, W, mode, tokenizer, text_tokenizer, audio, alpha, beta, temp, stop,
-             n_steps):
+             n_steps, score_temp=1.0):
         dec, nb, R = self.dec, C * b, C * b * W
         cand = dec.next_tok[:R]
         greedy = mode == "search"
@@ -159,7 +159,7 @@ class MagicDecoder:
             text = self.bert.encode_ids(ids, lens)
             nact = 1 if (s == 0 and not greedy) else b
             ops.magic_score(self.pval, self.maxcos, text, audio, C, b, W, nact, temp, alpha, beta,
-                            self.score)
+                            self.score, score_temp=score_temp)
             ops.magic_step(self.score, cand, C, b, W, s == 0, greedy, stop, s, self.step_limit,
                            self.scores, self.seq_len, self.stopped, self.tokens, self.kvrow,
                            self.pos, self.cdone, self.ntok, hf, self.sel_h)
@@ -178,10 +178,12 @@ class MagicDecoder:
     def beam_magic(self, hard_ids, hard_len, soft, n_soft, audio, tokenizer, text_tokenizer,
                    beam: int, width: int, entry_length: int, alpha: float = 0.1,
                    beta: float = 0.2, temp: Optional[float] = None, stop: int = 13,
-                   soft_ld: Optional[int] = None) -> List[Tuple[List[List[int]], List[float]]]:
+                   soft_ld: Optional[int] = None,
+                   temperature: float = 1.0) -> List[Tuple[List[List[int]], List[float]]]:
         """generate_beam_magic for every clip: per clip (token lists best-first, scores/len).
         hard_ids [C, H] int32 / hard_len [C] / soft [C, n_soft, 768] f32 (clap_to_gpt's rows),
-        audio [C, 1024] f32 (the CLAP audio embeddings)."""
+        audio [C, 1024] f32 (the CLAP audio embeddings).  ``temp`` is CLAP's logit temperature,
+        ``temperature`` generate_beam_magic's (divides the ranking scores, line 629)."""
         C = int(hard_len.shape[0])
         self._check(C, beam, width, int(hard_ids.shape[1]) + n_soft)
         if entry_length > self.max_steps:
@@ -190,7 +192,8 @@ class MagicDecoder:
         self._prefill(hard_ids, hard_len, soft, n_soft, C, beam, width, soft_ld)
         self._init_state(C, beam, width, torch.full((C,), entry_length, dtype=torch.int32))
         self._run(C, beam, width, "beam", tokenizer, text_tokenizer, audio.float().contiguous(),
-                  alpha, beta, temp, stop, entry_length)
+                  alpha, beta, temp, stop, entry_length,
+                  score_temp=temperature if temperature > 0 else 1.0)
         toks = self.tokens[:C * beam].cpu().view(C, beam, -1)
         ln = self.seq_len[:C * beam].cpu().view(C, beam)
         sc = (self.scores[:C * beam].cpu() / self.seq_len[:C * beam].cpu()).view(C, beam)

@@ -355,12 +355,15 @@ def lmhead_nblk(V: int) -> int:
     return call("zs_lmhead_nblk", V)
 
 
-def lmhead_topk(a, w, topk, part_stat, part_val, part_idx, row_norm=False, M=None):
+def lmhead_topk(a, w, topk, part_stat, part_val, part_idx, row_norm=False, M=None,
+                temperature=1.0):
     K = a.shape[-1]
     M = M if M is not None else a.numel() // K
     _need(a.dtype == w.dtype and w.shape[1] == K, "lmhead: dtype/shape mismatch")
-    call("zs_lmhead_topk", M, K, w.shape[0], dt(a), _p(a), a.stride(-2) if a.dim() > 1 else K,
-         _p(w), topk, int(row_norm), _p(part_stat), _p(part_val), _p(part_idx), _s())
+    _need(temperature > 0, "lmhead: temperature > 0")
+    call("zs_lmhead_topk_t", M, K, w.shape[0], dt(a), _p(a), a.stride(-2) if a.dim() > 1 else K,
+         _p(w), topk, int(row_norm), float(temperature), _p(part_stat), _p(part_val),
+         _p(part_idx), _s())
 
 
 def argmax_finalize(part_val, part_idx, M, nblk, idx):
@@ -439,10 +442,11 @@ def magic_maxcos(hid, ncand, W, ctx, Lmax, kvrow, pos, maxcos):
     return maxcos
 
 
-def magic_score(pval, maxcos, text, audio, C, b, W, nact, temp, alpha, beta, score):
+def magic_score(pval, maxcos, text, audio, C, b, W, nact, temp, alpha, beta, score,
+                score_temp=1.0):
     E = audio.shape[-1]
-    call("zs_magic_score", _p(pval), _p(maxcos), _p(text), _p(audio), C, E, b, W, nact,
-         float(temp), float(alpha), float(beta), _p(score), _s())
+    call("zs_magic_score_t", _p(pval), _p(maxcos), _p(text), _p(audio), C, E, b, W, nact,
+         float(temp), float(alpha), float(beta), float(score_temp), _p(score), _s())
     return score
 
 
@@ -452,3 +456,45 @@ def magic_step(score, cand, C, b, W, first, greedy, stop, step, max_steps, score
     call("zs_magic_step", _p(score), _p(cand), C, b, W, int(first), int(greedy), stop, step,
          _p(max_steps), _p(scores), _p(seq_len), _p(stopped), _p(tokens), tokens.shape[1],
          _p(kvrow), kvrow.shape[1], _p(pos), _p(cdone), _p(ntok), _p(hid), _p(sel_h), dt(hid), _s())
+
+
+# ---------------------------------------------------------------- persistent greedy decode
+def decode_persist_workspace(device) -> torch.Tensor:
+    n = call("zs_decode_persist_workspace_bytes")
+    return torch.zeros(n + 256, dtype=torch.uint8, device=device)
+
+
+def decode_persist_grid() -> int:
+    return call("zs_decode_persist_grid")
+
+
+def pack_b_fragments(W: torch.Tensor) -> torch.Tensor:
+    """W [N][K] (bf16, K % 32 == 0) -> MFMA 16x16x32 B-fragment order [ceil(N/16)][K/32][64][8]:
+    block j, k-step s, lane l holds W[16 j + l % 16][32 s + 8 (l // 16) .. + 8]; rows past N are
+    zero.  One KiB per (block, k-step): each wave-load of a fragment is contiguous."""
+    N, K = W.shape
+    _need(K % 32 == 0, "pack_b_fragments: K % 32")
+    Np = -(-N // 16) * 16
+    Wp = torch.zeros(Np, K, dtype=W.dtype, device=W.device)
+    Wp[:N] = W
+    return (Wp.view(Np // 16, 16, K // 32, 4, 8).permute(0, 2, 3, 1, 4).contiguous()
+            .view(Np // 16, K // 32, 64, 8))
+
+
+def gpt2_decode_persist(R, Lmax, max_steps, stop0, stop1, V, wte, wpe, wte_packed, temperature,
+                        layer_ptrs, lnf_w, lnf_b, kv_ptrs, pos, next_tok, done, out_ids, out_len,
+                        step_ctr, all_done, ws):
+    """The remaining greedy steps of one bs <= 64 batch in one persistent launch
+    (zs_gpt2_decode_persist).  layer_ptrs / kv_ptrs: ctypes arrays of 96 / 24 device pointers."""
+    _need(1 <= R <= 64, "gpt2_decode_persist: 1 <= R <= 64")
+    _need(wte.dtype == torch.bfloat16 and wpe.dtype == torch.bfloat16, "gpt2_decode_persist: bf16")
+    for t, n in ((pos, "pos"), (next_tok, "next_tok"), (done, "done"), (out_ids, "out_ids"),
+                 (out_len, "out_len"), (step_ctr, "step_ctr"), (all_done, "all_done")):
+        _i32(t, n)
+    _need(out_ids.shape[-1] == max_steps, "gpt2_decode_persist: out_ids [R, max_steps]")
+    base = ws.data_ptr()
+    off = (-base) % 256
+    _need(temperature > 0, "gpt2_decode_persist: temperature > 0")
+    call("zs_gpt2_decode_persist", R, Lmax, max_steps, stop0, stop1, V, _p(wte), _p(wpe),
+         _p(wte_packed), float(temperature), layer_ptrs, _p(lnf_w), _p(lnf_b), kv_ptrs, _p(pos), _p(next_tok), _p(done), _p(out_ids),
+         _p(out_len), _p(step_ctr), _p(all_done), base + off, ws.numel() - off, _s())

@@ -40,6 +40,8 @@ class CaptionConfig:
     compact_decode: bool = True       # greedy bf16: decode only the rows that have not stopped
     clip_length: int = 10             # TransformerMapper clip_length (params.json prefix_length_clip)
     mapper_layers: int = 8            # TransformerMapper num_layers (params.json num_layers)
+    persist_decode: Optional[bool] = None   # greedy bf16 at <= 64 rows: the persistent decode
+                                      # launch (zs_gpt2_decode_persist); None = env ZSAAC_PERSIST (on)
     encoder_batch: int = 64           # clips per encoder pass (the reference's eval batch size);
                                       # a larger ``batch`` is encoded in chunks of this size and
                                       # decoded together (clip results do not depend on it)
@@ -123,7 +125,7 @@ class CaptionPipeline:
         beam = max(cfg.beam, 1)
         self.decoder = Gpt2Decoder(self.gpt, B * beam, self.Pmax, cfg.entry_length,
                                    max_prefill_rows=B, use_graph=cfg.use_graph,
-                                   compact=cfg.compact_decode)
+                                   compact=cfg.compact_decode, persist=cfg.persist_decode)
         i32 = dict(device=dev, dtype=torch.int32)
         self.hard_ids = torch.zeros(B, self.h_cap, **i32)
         self.hard_len = torch.zeros(B, **i32)
@@ -232,6 +234,11 @@ class ConcurrentRunner:
     Results are copied out on the pipeline's stream before it takes the next batch."""
 
     def __init__(self, pipe: CaptionPipeline, n_inflight: int = 2):
+        if pipe.decoder.persist:
+            # persistent decode grids must be co-resident: at most CUs // grid launches in flight
+            cus = torch.cuda.get_device_properties(pipe.dev).multi_processor_count
+            n_inflight = max(1, min(n_inflight, cus // ops.decode_persist_grid()))
+        self.n_inflight = n_inflight
         self.pipes = [pipe] + [pipe.twin() for _ in range(n_inflight - 1)]
         # dedicated streams on distinct hardware queues: pooled torch streams take their queue at
         # first use and can end up sharing one, which serializes the batches
@@ -285,8 +292,10 @@ class ConcurrentRunner:
                 if not ev.query():
                     continue
                 progressed = True
+                if int(flag[1]) < 0:
+                    raise RuntimeError("persistent decode gave up: grid not co-resident")
                 if int(flag[0]) or n >= p.decoder.n_chunks:
-                    self.decode_steps[bi] = 1 + n * p.decoder.chunk
+                    self.decode_steps[bi] = int(flag[3]) if not p.cfg.beam else 1 + n * p.decoder.chunk
                     with torch.cuda.stream(s):
                         r = p.result()
                         results[bi] = _copy_batch(r, caller)
