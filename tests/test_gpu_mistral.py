@@ -206,3 +206,45 @@ def test_fp8_prefill_unpack_gemm(cuda, M, N, K):
     call("zs_scale_cols", out.data_ptr(), M, N, N, sd.data_ptr(), st)
     got = out.cpu()
     assert float((got - ref).abs().max()) < 1e-3 * float(ref.abs().max()) + 1e-4
+
+
+def test_dropin_generate_trims_and_reuses_engine(cuda, golden):
+    """HF generate's output width is the longest generated row (every row emitted eos earlier
+    than max_length - P -> fewer columns), not max_length - P; one decoder is reused across
+    calls whose prompt length changes (en / fr tags) and rebuilt only when the capacity grows."""
+    from models.caption_model import ClapCaption_Mistralai_prompt
+    from oracle import mistral as OM
+    from zsaac import synthetic as S
+    g = golden("mistral.npz")
+    cfg = dict(vocab_size=32000, hidden_size=1024, intermediate_size=3072, num_hidden_layers=2,
+               num_attention_heads=8, num_key_value_heads=2, rms_norm_eps=1e-5)
+    msd = S.mistral_state_dict(eos_boost=6.0)
+    mlp = S.mlp_mapper_state_dict(31, prefix_length=10, d=1024)
+    m = ClapCaption_Mistralai_prompt(10, clip_length=10, prefix_size=1024, num_layers=8,
+                                     mapping_type="mlp", mistral_config=cfg)
+    sd = {"LMmodel.base_model.model." + k: v for k, v in msd.items()}
+    sd.update(mlp)
+    m.load_state_dict(sd)
+    m = m.set_mode("f32").to(cuda).eval()
+    lm = m.LMmodel.base_model.model
+    emb = torch.from_numpy(g["clap_emb"])[:, None]
+    hard = torch.from_numpy(g["hard_ids"])
+    decs = []
+    for t in ("en", "fr", "en"):
+        pe, _ = OM.clap_to_gpt(emb, hard, torch.from_numpy(g[f"tag_{t}"]), msd, mlp)
+        ref = OM.generate(pe, msd, H, KVH, EPS, max_length=60)
+        with torch.no_grad():
+            ids = m.LMmodel.generate(inputs_embeds=pe.to(cuda), attention_mask=None,
+                                     do_sample=False, max_length=60, eos_token_id=2,
+                                     pad_token_id=2).cpu()
+        width = max(len(r) for r in ref)
+        assert width < 60 - pe.shape[1], "eos boost too weak for the trim check"
+        assert ids.shape == (len(ref), width), (t, ids.shape, width)
+        for b, r in enumerate(ref):
+            assert ids[b, :len(r)].tolist() == r, (t, b)
+            assert bool((ids[b, len(r):] == 2).all())
+        decs.append(lm.engine(cuda, 32, 64, 60))
+    assert decs[0] is decs[1] is decs[2]
+    big = lm.engine(cuda, 64, 64, 60)
+    assert big is not decs[0] and big.B >= 64
+    assert lm.engine(cuda, 8, 16, 10) is big

@@ -112,3 +112,12 @@ def test_output_format(tmp_path):
     assert out == {"predictions": [{"filename": "b.wav", "caption": "a dog barks.", "prefix": "There are x"},
                                    {"filename": "a.wav", "caption": "rain.", "prefix": "There are y"}]}
     assert predict.post_processing([{"caption": "A Dog"}, {"caption": "b."}]) == ["a dog.", "b."]
+
+
+def test_magic_settings_follow_reference_params():
+    """predict_prompt.py applies its module-level {'beta': 0.2, 'alpha': 0.1} after params.json
+    (lines 19-22, 196-197): a params.json alpha / beta never reaches generate_beam_magic, its
+    magic_width does (line 140)."""
+    from zsaac.predict import magic_settings
+    assert magic_settings({"alpha": 0.5, "beta": 0.9, "magic_width": 30}) == (30, 0.1, 0.2)
+    assert magic_settings({}) == (25, 0.1, 0.2)

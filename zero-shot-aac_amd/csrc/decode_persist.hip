@@ -836,12 +836,15 @@ __global__ __launch_bounds__(NT) void decode_persist_kernel(Args a) {
 
       phase_proj<12>(a, rs, rs.hid, DFF, a.bmp[l], smem, w, wm);
       bar_arrive(bar);
-      // next block's c_attn (after block 11: block 0 of the next step, held through ln_f / LM head)
+      // next block's c_attn.  Unconditional (a conditional load keeps the old wq live through
+      // the whole block for the path that skips it); after block 11 the value is dead and wq is
+      // reloaded after the LM head, which needs the VGPRs
       load_w<3, 3>(a.wqkv[l + 1 < NLY ? l + 1 : 0], D, 48 * w, QKVN, 96 * V_, wq);
       if (!bar_wait(bar, s_ok)) return gave_up(a);
     }
     phase_lm(a, rs, smem, s_tok, s_pos, am_v, am_i, w, lmkey + (step & 1) * RM, s_lnf);
     bar_arrive(bar);
+    load_w<3, 3>(a.wqkv[0], D, 48 * w, QKVN, 96 * V_, wq);
     if (!bar_wait(bar, s_ok)) return gave_up(a);
 
     // ---- G: every WG reads the per-row argmax (one agent-scope key per row) and applies

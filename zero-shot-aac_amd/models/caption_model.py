@@ -324,12 +324,18 @@ class ZsMistralForCausalLM(nn.Module):
                                   c["num_key_value_heads"], c.get("rms_norm_eps", 1e-5),
                                   c.get("rope_theta", 10000.0))
         w = self._cache.get(self, build, (mode, str(device)))
-        key = (max_batch, max_prompt, max_new)
-        decs = w.__dict__.setdefault("_decoders", {})
-        if key not in decs:
-            decs.clear()
-            decs[key] = MistralDecoder(w, max_batch, max_prompt, max_new)
-        return decs[key]
+        # one decoder per weights, reused while its capacity covers the call (the reference pads
+        # each batch's hard prompt to its longest and appends a per-language tag, so P changes
+        # from call to call; rebuilding per (B, P, new) re-allocated the KV caches and slabs and
+        # re-captured the decode graph every time); grown to the max of old and new bounds
+        dec = w.__dict__.get("_decoder")
+        if dec is None or dec.B < max_batch or dec.Pmax < max_prompt or dec.max_new < max_new:
+            if dec is not None:
+                max_batch, max_prompt = max(max_batch, dec.B), max(max_prompt, dec.Pmax)
+                max_new = max(max_new, dec.max_new)
+            w.__dict__["_decoder"] = None
+            dec = w.__dict__["_decoder"] = MistralDecoder(w, max_batch, max_prompt, max_new)
+        return dec
 
     def generate(self, inputs_embeds=None, attention_mask=None, do_sample=False, max_length=60,
                  eos_token_id=2, pad_token_id=2, **kw):
@@ -343,9 +349,13 @@ class ZsMistralForCausalLM(nn.Module):
         require_device(inputs_embeds, "MistralForCausalLM.generate")
         B, P, _ = inputs_embeds.shape
         new = max(max_length - P, 0)
-        dec = self.engine(inputs_embeds.device, max(B, 32), max(P, 64), max(new, 1))
+        # capacity by the call's upper bounds: any prompt up to 64 rows (or P), any new <= max_length
+        dec = self.engine(inputs_embeds.device, max(B, 32), max(P, 64), max(max_length, 1))
         rows = dec.generate_embeds(inputs_embeds, max_length=max_length, eos=eos_token_id)
-        out = torch.full((B, new), pad_token_id, dtype=torch.long)
+        # HF generate returns only as many columns as were generated: until every row emitted eos
+        # (finished rows padded with pad_token_id) or max_length - P
+        width = min(new, max([len(r) for r in rows] + [0]))
+        out = torch.full((B, width), pad_token_id, dtype=torch.long)
         for b, r in enumerate(rows):
             out[b, :len(r)] = torch.tensor(r, dtype=torch.long)
         return out.to(inputs_embeds.device)
@@ -395,11 +405,12 @@ class ClapCaption_Mistralai_prompt(nn.Module):
 
     def load_state_dict(self, state_dict, strict: bool = True):
         """Reference checkpoints hold the peft tree (``LMmodel.base_model.model.*`` with
-        ``base_layer`` / ``lora_A`` / ``lora_B``): LoRA merged, the rest loaded as is."""
+        ``base_layer`` / ``lora_A`` / ``lora_B``, 4-bit bitsandbytes base weights): NF4 dequantized,
+        LoRA merged, the rest loaded as is."""
         from zsaac.mistral import merge_peft_state_dict
         lm = {k: v for k, v in state_dict.items() if k.startswith("LMmodel.")}
         rest = {k: v for k, v in state_dict.items() if not k.startswith("LMmodel.")}
-        if any(".lora_A." in k for k in lm):
+        if any(".lora_A." in k or ".quant_state.bitsandbytes__" in k for k in lm):
             merged = merge_peft_state_dict(lm, prefix="LMmodel.")
         else:
             merged = {k[len("LMmodel.base_model.model."):]: v for k, v in lm.items()

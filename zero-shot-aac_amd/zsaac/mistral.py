@@ -13,8 +13,9 @@ Here: the LoRA adapters are merged into the base weights at load (W + (alpha / r
 and the decoder weights are stored as fp8 e4m3 (OCP) with one f32 scale per output channel
 (``mode="fp8"``, the perf mode), bf16 (``"bf16"``) or f32 (``"f32"``, the parity mode: no folding,
 zs_gemm f32, ids bit-exact against HF MistralForCausalLM on the same weights).  NF4 itself is a
-bitsandbytes storage format (absent here); fp8 is the MI355X-native 8-bit format, and a checkpoint's
-NF4 tensors would be dequantised to f32 before :class:`MistralWeights` re-quantises them.
+bitsandbytes storage format (the library is absent here); fp8 is the MI355X-native 8-bit format:
+a checkpoint's NF4 tensors are dequantised to f32 on load (:func:`dequantize_bnb_4bit`, in torch on
+the host, from the saved quant_state) and :class:`MistralWeights` re-quantises them.
 
 One decode step for M rows (csrc/mistral.hip): per layer
   [add + RMSNorm] -> qkv GEMM (fp8 weights, split-K slabs) -> RoPE + KV append -> GQA attention
@@ -34,12 +35,81 @@ from . import ops
 from ._lib import ZS_BF16, ZS_F32, call
 
 
+# bitsandbytes 4-bit checkpoints (caption_model.py:355-364 loads the base model with
+# BitsAndBytesConfig(load_in_4bit, bnb_4bit_quant_type="nf4", bnb_4bit_use_double_quant=True)):
+# a quantized Linear's state dict holds ``weight`` (packed uint8, two 4-bit codes per byte, the
+# first element in the HIGH nibble), ``weight.absmax`` (one scale per block of `blocksize`
+# elements; uint8 codes when double-quantized), ``weight.quant_map`` (the 16-entry NF4 code),
+# ``weight.nested_absmax`` / ``weight.nested_quant_map`` (the double quantization of absmax:
+# blocks of `nested_blocksize`, a 256-entry dynamic code, plus `nested_offset`) and
+# ``weight.quant_state.bitsandbytes__nf4`` (the remaining fields as JSON bytes in a uint8 tensor:
+# shape, dtype, blocksize, quant_type, nested_*).  Read with json (nothing executed).
+_BNB_STATE = ".quant_state.bitsandbytes__"
+
+
+def _bnb_state(sd: Dict[str, torch.Tensor], wkey: str) -> Optional[dict]:
+    import json
+    for qt in ("nf4", "fp4"):
+        k = wkey + _BNB_STATE + qt
+        if k in sd:
+            return json.loads(bytes(sd[k].to(torch.uint8).flatten().tolist()).decode("utf-8"))
+    return None
+
+
+def dequantize_bnb_4bit(sd: Dict[str, torch.Tensor], wkey: str) -> torch.Tensor:
+    """The f32 weight of a bitsandbytes 4-bit (NF4 / FP4) Linear saved under ``wkey``
+    (bitsandbytes dequantize_4bit: code[nibble] * absmax[i // blocksize], absmax itself
+    dequantized as nested_code[q] * nested_absmax[j // nested_blocksize] + nested_offset when
+    double-quantized)."""
+    st = _bnb_state(sd, wkey)
+    if st is None:
+        raise ValueError(f"{wkey}: no bitsandbytes quant_state")
+    shape = [int(v) for v in st["shape"]]
+    n = 1
+    for v in shape:
+        n *= v
+    bs = int(st["blocksize"])
+    packed = sd[wkey].to(torch.uint8).flatten()
+    codes = torch.empty(packed.numel() * 2, dtype=torch.long)
+    codes[0::2] = (packed >> 4).long()
+    codes[1::2] = (packed & 0xF).long()
+    codes = codes[:n]
+    qmap = sd[wkey + ".quant_map"].float().flatten()
+    absmax = sd[wkey + ".absmax"]
+    if wkey + ".nested_absmax" in sd:
+        nbs = int(st.get("nested_blocksize", 256))
+        nq = sd[wkey + ".nested_quant_map"].float().flatten()
+        na = sd[wkey + ".nested_absmax"].float().flatten()
+        aq = absmax.to(torch.uint8).flatten().long()
+        idx = torch.arange(aq.numel()) // nbs
+        absmax = nq[aq] * na[idx] + float(st.get("nested_offset", 0.0))
+    absmax = absmax.float().flatten()
+    vals = qmap[codes] * absmax[torch.arange(n) // bs]
+    return vals.view(shape)
+
+
+def dequantize_bnb_state_dict(sd: Dict[str, torch.Tensor]) -> Dict[str, torch.Tensor]:
+    """A state dict with bitsandbytes 4-bit Linear weights -> plain f32 weights under the same
+    keys (the absmax / quant_map / nested_* / quant_state entries dropped); other entries as is."""
+    qkeys = {k.split(_BNB_STATE)[0] for k in sd if _BNB_STATE in k}
+    aux = (".absmax", ".quant_map", ".nested_absmax", ".nested_quant_map")
+    out = {}
+    for k, v in sd.items():
+        if _BNB_STATE in k or any(k.endswith(a) and k[:-len(a)] in qkeys for a in aux):
+            continue
+        out[k] = dequantize_bnb_4bit(sd, k) if k in qkeys else v
+    return out
+
+
 def merge_peft_state_dict(sd: Dict[str, torch.Tensor], lora_alpha: float = 16.0, r: int = 8,
                           prefix: str = "") -> Dict[str, torch.Tensor]:
     """A peft LoRA state dict (``...base_model.model.model.layers.0.self_attn.q_proj.base_layer
     .weight`` + ``lora_A.default.weight`` [r, in] + ``lora_B.default.weight`` [out, r], the
     ``get_peft_model`` of caption_model.py:362-364) -> plain MistralForCausalLM keys with
-    W = base + (lora_alpha / r) B @ A."""
+    W = base + (lora_alpha / r) B @ A.  bitsandbytes 4-bit base weights (the reference's NF4
+    checkpoint) are dequantized first (:func:`dequantize_bnb_state_dict`)."""
+    if any(_BNB_STATE in k for k in sd):
+        sd = dequantize_bnb_state_dict(sd)
     out, lora = {}, {}
     strip = prefix + "base_model.model."
     for k, v in sd.items():
@@ -202,8 +272,13 @@ class MistralDecoder:
         self.q = torch.empty(Mp, H * HD, device=dev, dtype=adt)
         self.att = torch.empty(Mp, H * HD, device=dev, dtype=adt)
         self.act = torch.empty(Mp, F, device=dev, dtype=adt)
-        nsplit = max(self._splits(w.D), self._splits(F))
-        self.slab = torch.empty(nsplit * Mp * max(self.nqkv, 2 * F, D), device=dev)
+        # f32 result slabs: decode (M = B <= 64 rows) writes nsplit split-K slabs of B rows; the
+        # fp8 prefill (unpack + one tiled GEMM, prefill_unpack) writes one slab of M = B P rows;
+        # only the 64-row-chunk fp8 prefill (prefill_unpack False, an A/B knob) needs nsplit x Mp
+        # rows, and _gemm grows the slab for it on demand (at 7B: 14 x 2048 x 28672 f32 = 3.3 GB)
+        self.nsplit = max(self._splits(w.D), self._splits(F))
+        self.slab_ncol = max(self.nqkv, 2 * F, D)
+        self.slab = torch.empty(max(self.nsplit * max_batch, Mp) * self.slab_ncol, device=dev)
         self.kc = [torch.empty(max_batch, KVH, self.Lmax, HD, device=dev, dtype=adt) for _ in w.layers]
         self.vc = [torch.empty(max_batch, KVH, self.Lmax, HD, device=dev, dtype=adt) for _ in w.layers]
         inv = 1.0 / (w.theta ** (torch.arange(0, HD, 2, dtype=torch.int64).float() / HD))
@@ -249,6 +324,9 @@ class MistralDecoder:
         if self.w.mode == "fp8":
             ns = self._splits(K)
             ss = M * N
+            if self.slab.numel() < ns * ss:      # (captured decode graphs point at the old slab)
+                self.slab = torch.empty(ns * ss, device=self.w.dev)
+                self.graphs.clear()
             out = self.slab[:ns * ss]
             for m0 in range(0, M, 64):
                 mm = min(64, M - m0)

@@ -36,6 +36,15 @@ from .bpe import GPT2BPE
 from .pipeline import CaptionConfig, CaptionPipeline
 from .tokenizer import TEMPLATE_IDS
 
+# predict_prompt.py:19-22: applied over params.json (args.__dict__.update(params), line 197)
+MAGIC_PARAMS = {"beta": 0.2, "alpha": 0.1}
+
+
+def magic_settings(params: dict):
+    """(magic_width, alpha, beta) as predict_prompt.py --magic uses them: magic_width from
+    params.json (line 140), alpha / beta from the module-level params that overwrite it (197)."""
+    return int(params.get("magic_width", 25)), MAGIC_PARAMS["alpha"], MAGIC_PARAMS["beta"]
+
 
 def post_processing(captions) -> List[str]:
     """predict_prompt.py:83-92: append '.' when missing, lower-case."""
@@ -244,10 +253,13 @@ def main(argv: Optional[Sequence[str]] = None) -> int:
         with open(args.bert_vocab, encoding="utf-8") as f:
             vocab = {t.rstrip("\n"): i for i, t in enumerate(f)}
         bert_tok = BertTokenizer(vocab=vocab, do_lower_case=True)
-        # predict_prompt.py:19-22 (alpha 0.1, beta 0.2); magic_width from params.json (25 default)
+        # the reference applies its module-level params {'beta': 0.2, 'alpha': 0.1} AFTER
+        # params.json (predict_prompt.py:19-22, 196-197), so magic decoding always runs with
+        # alpha 0.1 / beta 0.2 whatever the checkpoint's params.json says; magic_width does come
+        # from params.json (line 140: args.magic_width)
+        width, alpha, beta = magic_settings(params)
         key2pred, key2pred_prefix, key2refs = make_preds_magic(
-            pipe, tokenizer, all_data, clap_sd, bert_tok, width=int(params.get("magic_width", 25)),
-            alpha=float(params.get("alpha", 0.1)), beta=float(params.get("beta", 0.2)))
+            pipe, tokenizer, all_data, clap_sd, bert_tok, width=width, alpha=alpha, beta=beta)
     else:
         key2pred, key2pred_prefix, key2refs = make_preds(pipe, tokenizer, all_data)
     write_outputs(args.test_dir, key2pred, key2pred_prefix, key2refs)
