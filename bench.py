@@ -9,7 +9,7 @@ eval batches of 64 clips exactly as the reference evaluates them: STFT/log-mel +
 audio_proj + L2 -> sound-effect hard prompt -> MLP mapper -> GPT-2 small prefill +
 get_prefix_tokens + greedy generate2 (entry_length 67, stop ids 13 / 764), bf16 operands / f32
 accumulation.  Every decode GEMM of a batch is a 64-row GEMM.  One "step" = one eval batch of
-64 clips (the last batch of the 1045 holds 21).  --inflight independent batches (default 4) are
+64 clips (the last batch of the 1045 holds 21).  --inflight independent batches (default 5) are
 in flight per GPU, each on its own HIP stream (pipeline twins sharing the weights,
 zsaac/pipeline.py ConcurrentRunner); GPU_MAX_HW_QUEUES is raised to --hw-queues (default 8, the
 runtime allows up to 32) so those streams get hardware queues of their own.  With N ranks the
@@ -22,18 +22,27 @@ clips are sharded (zsaac/dist.py shard_range) and ONE RCCL all-gather of the gen
     torchrun --nproc-per-node N bench.py --gpus N    # one process per GPU, RCCL
 
 Rank 0 prints ONE JSON line.  Besides the contract fields (value = whole-job clips/s) it holds
-  roofline:          the dominant kernel of the bs-64 decode (the row-group GEMM with fused
-                     LayerNorm at the c_fc shape [64 x 768] x [768 x 3072]), HBM-bound:
-                     algorithmic bytes per launch / its average duration (HIP events on its
-                     stream, weights cold: the launches rotate over > 256 MiB of weight copies);
-  roofline_*:        the other decode kernels and the whole decode step, same method;
+  roofline:          the dominant kernel, decode_persist_kernel (zs_gpt2_decode_persist: every
+                     decode step after step 0 of one eval batch in one launch), HBM-bound:
+                     algorithmic bytes per launch (weights per step + every row's K/V reads and
+                     appends, persist_launch_bytes) / its average duration over the timed region's
+                     launches (HIP events on each launch's stream); traffic from the committed
+                     PMC passes (profiles/r3_pmc_persist.json);
+  roofline_decode_step: one decode step of one batch on one stream (nothing else running);
+  stages:            per-stage ms on one stream with each stage's roofline fraction (front end
+                     HBM, encoder MFMA, prompt+mapper HBM, prefill MFMA, decode HBM);
+  roofline_stepwise_*, roofline_decode_attention: the per-step path's kernels (beam, f32, > 64
+                     rows) at the bs-64 shapes, cold weights / cold K/V;
+  strong_scaling_proxy: T(1045 clips) / T(one rank's 131-clip shard) on this GPU = the predicted
+                     1 -> 8 GPU speed-up;
   throughput_mode:   the same path with 128 eval batches decoded per step (8192-row GEMMs) —
                      a different configuration, NOT the metric;
   f32_parity_mode:   the bs-64 headline in f32 (the mode whose greedy ids are bit-exact);
   id_agreement:      greedy ids against the reference goldens (bf16 and f32), first divergence
                      and the reference's own top-2 logit margin there (tools/idparity.py);
   cpu_baseline:      the oracle (reference semantics: batch 1, full recompute, fp32) on bounded
-                     samples of C2 and C1 on this host's CPU (rank 0, N=1 only).
+                     samples of C2, C1 and C3 (beam 5) on this host's CPU (rank 0, N=1 only);
+                     --cpu-baseline-full times BASELINE.md §3's 64 / 50 / 64 clips.
 """
 from __future__ import annotations
 
@@ -67,6 +76,7 @@ import torch  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0           # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 MFMA_BF16_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense bf16 MFMA (no sparsity)
+MFMA_F32_PEAK_TFLOPS = 157.3    # MI355X_MICROARCH.md: dense f32 MFMA
 GPT2_KW = dict(seed=0, std=0.1, emb_std=0.1, stop_boost=2.0)
 CLOTHO_EVAL_CLIPS = 1045
 METRIC = "audio clips/sec end-to-end (encode+mapper+GPT-2 decode), Clotho-eval bs=64"
@@ -102,7 +112,7 @@ def parse():
     ap.add_argument("--group", type=int, default=1,
                     help="eval batches decoded together in one decode step (1 = the metric's "
                          "bs=64; > 1 is the labelled throughput mode)")
-    ap.add_argument("--inflight", type=int, default=4,
+    ap.add_argument("--inflight", type=int, default=5,
                     help="independent batches in flight per GPU, each on its own HIP stream")
     ap.add_argument("--hw-queues", type=int, default=8,
                     help="GPU_MAX_HW_QUEUES for this process (read before HIP initialises)")
@@ -110,7 +120,11 @@ def parse():
                     help="greedy bf16 at >= 512 rows: decode only the rows that have not stopped")
     ap.add_argument("--extras", type=int, default=1,
                     help="N=1: also measure the throughput mode, the f32 mode and id agreement")
-    ap.add_argument("--cpu-baseline-clips", type=int, default=16)
+    ap.add_argument("--cpu-baseline-clips", type=int, default=8,
+                    help="C2 clips timed on the CPU oracle (C1 takes 2x, C3 beam 5 takes 1/2)")
+    ap.add_argument("--cpu-baseline-full", action="store_true",
+                    help="the BASELINE.md §3 plan: 64 C2 clips, all 50 C1 clips, 64 C3 clips")
+    ap.add_argument("--no-scaling-proxy", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--stages", action="store_true", help="also report per-stage ms (extra syncs)")
@@ -176,16 +190,37 @@ def synthetic_clips(n, first, device):
 
 
 # ------------------------------------------------------------------ caption runs
-def run_captions(args, world, rank, device, pipe, n_local, first, counts, inflight, warmup):
+def split_batches(n, B, parts=0):
+    """[start, end) ranges of n clips in eval batches of at most B: consecutive full batches (the
+    reference's DataLoader), or with ``parts`` > 0 at least that many near-equal batches (a small
+    shard spread over every in-flight stream; each batch still <= B rows)."""
+    k = -(-n // B)
+    if parts:
+        k = max(k, min(parts, n))
+    if not parts:
+        return [(i, min(n, i + B)) for i in range(0, n, B)]
+    base, rem = divmod(n, k)
+    out, a = [], 0
+    for j in range(k):
+        b = a + base + (1 if j < rem else 0)
+        out.append((a, b))
+        a = b
+    return out
+
+
+def run_captions(args, world, rank, device, pipe, n_local, first, counts, inflight, warmup,
+                 parts=0):
     """Times the captioning of this rank's n_local clips (clip ids first..) in batches of
-    pipe.cfg.batch on `inflight` streams, then the all-gather; returns (seconds max over ranks,
-    outs, runner, info)."""
+    pipe.cfg.batch (split_batches) on `inflight` streams, then the all-gather; returns (seconds
+    max over ranks, outs, runner, info)."""
     from zsaac.pipeline import ConcurrentRunner
-    from zsaac import dist as zd
+    from zsaac import decoder as zdec, dist as zd
     B = pipe.cfg.batch
     pool = synthetic_clips(n_local, first, device)
-    batches = [pool[i:i + B] for i in range(0, n_local, B)]
+    batches = [pool[a:b] for a, b in split_batches(n_local, B, parts)]
     log(f"{n_local} clips in {len(batches)} batches of <= {B}, {inflight} in flight: capturing")
+    if len(batches) == 0:
+        raise ValueError("no clips on this rank")
     runner = ConcurrentRunner(pipe, max(1, inflight))
     for size in sorted({b.shape[0] for b in batches}, reverse=True):   # captures every graph
         runner.warmup(next(b for b in batches if b.shape[0] == size))
@@ -199,6 +234,7 @@ def run_captions(args, world, rank, device, pipe, n_local, first, counts, inflig
     torch.cuda.synchronize()
     cap0 = sum(p.decoder.n_captures for p in runner.pipes)
     rows0 = sum(p.decoder.rows_stepped for p in runner.pipes)
+    log0 = len(zdec.PERSIST_LOG) if zdec.PERSIST_LOG is not None else 0
     t0 = time.perf_counter()
     outs = runner.run(batches)
     if world > 1:
@@ -213,6 +249,7 @@ def run_captions(args, world, rank, device, pipe, n_local, first, counts, inflig
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         dt = float(t)
     log(f"timed: {n_local} clips in {dt:.3f} s")
+    runner.timed_log = zdec.PERSIST_LOG[log0:] if zdec.PERSIST_LOG is not None else []
     info = {"graph_captures_timed": sum(p.decoder.n_captures for p in runner.pipes) - cap0,
             "decode_rows_stepped_per_clip": round(
                 (sum(p.decoder.rows_stepped for p in runner.pipes) - rows0) / max(1, n_local), 2),
@@ -332,49 +369,142 @@ def roofline_rows_gemm(pipe, which):
                       f"(cold W)", byts, avg)
 
 
-def roofline_attention(pipe, L_mean=None):
+def roofline_attention(pipe, L_mean=None, cold_bytes=320 << 20):
     """decode attention at the bench's decode rows, every row at the mean key count of a 67-step
-    greedy decode (prompt Pmax + 34): bytes = K and V of every key once + q/k/v + output."""
+    greedy decode (prompt Pmax + 34): bytes = K and V of every key once + q/k/v + output.  Cold:
+    the launches rotate over copies of the layer's K/V caches totalling > 256 MiB (more than the
+    8 x 4 MiB L2s and the 256 MiB Infinity Cache), as the GEMM rooflines rotate weight copies."""
     from zsaac import ops
     dec = pipe.decoder
     R = pipe.cfg.batch * max(1, pipe.cfg.beam)
     D, H, Lmax = 768, 12, dec.Lmax
     L = L_mean or min(Lmax - 1, pipe.Pmax + 34)
     kc, vc = dec.kc[0], dec.vc[0]
+    n = max(1, -(-cold_bytes // (kc.nbytes + vc.nbytes)))
+    caches = [(kc, vc)] + [(kc.clone(), vc.clone()) for _ in range(n - 1)]
     qkv = dec.qkv[:R]
     pos = torch.full((R,), L - 1, device=pipe.dev, dtype=torch.int32)
     out = torch.empty(R, D, device=pipe.dev, dtype=qkv.dtype)
 
     def launch(i):
-        ops.decode_attention(qkv, R, D, H, kc, vc, Lmax, pos, out)
-    avg = _graph_time(launch, 50)
+        k, v = caches[i % n]
+        ops.decode_attention(qkv, R, D, H, k, v, Lmax, pos, out)
+    avg = _graph_time(launch, 2 * n)
     es = qkv.element_size()
     byts = R * H * (2 * L * 64 * es) + R * 3 * D * es + R * D * es
-    return _hbm_entry(f"decode_attn6_kernel<bf16,{'32,SPLIT=2' if R <= 128 else 16}> R={R} heads=12 keys={L}",
-                      byts, avg)
+    r = _hbm_entry(f"decode_attn6_kernel<bf16,{'32,SPLIT=2' if R <= 128 else 16}> R={R} heads=12 "
+                   f"keys={L} (cold K/V: {n} cache copies, {n * (kc.nbytes + vc.nbytes) >> 20} MiB)",
+                   byts, avg)
+    del caches
+    return r
 
 
-def decode_step_roofline(pipe, agg_steps_per_s=None):
-    """One greedy decode step of one batch (graph replay of a chunk, single stream): HBM bytes
-    a step must move (GPT-2 weights incl. the tied LM head + every row's KV at the mean key
-    count) / its time; with the concurrent run's aggregate steps/s when given."""
-    dec = pipe.decoder
-    R = pipe.cfg.batch
-    dec.done.zero_()
-    gr = dec._graph(*dec._chunk_plan(None))
-    torch.cuda.synchronize()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    reps = 10
-    e0.record()
-    for _ in range(reps):
-        gr.replay()
-    e1.record()
-    e1.synchronize()
-    step_s = e0.elapsed_time(e1) / 1e3 / reps / dec.chunk
-    L = min(dec.Lmax - 1, pipe.Pmax + 34)
-    byts = pipe.gpt.nbytes() + R * L * 12 * 2 * 768 * 2
-    r = _hbm_entry(f"one greedy decode step, {R} rows (12 blocks + ln_f + LM head + greedy step), "
-                   f"single stream", byts, step_s, {"avg_step_us": round(step_s * 1e6, 1)})
+# ------------------------------------------------------------------ persistent decode roofline
+def gpt2_step_weight_bytes(pipe):
+    """Bytes of weights one greedy decode step reads: the 12 blocks' bf16 c_attn / attn.c_proj /
+    c_fc / mlp.c_proj matrices and f32 biases, the tied LM head (bf16 wte) and ln_f."""
+    D, F = 768, 3072
+    es = pipe.gpt.wte.element_size()
+    per_layer = (3 * D * D + D * D + D * F + F * D) * es + (3 * D + D + F + D) * 4
+    return len(pipe.gpt.layers) * per_layer + pipe.gpt.V * D * es + 2 * D * 4
+
+
+def persist_launch_bytes(w_step, plen, steps, kv_row=12 * 2 * 768 * 2):
+    """Algorithmic HBM bytes of one persistent launch (decode steps 1 .. steps-1 of a batch whose
+    rows have prompt lengths ``plen``): per step the weights once, and per row its cached K/V
+    (keys 0 .. pos-1 of all 12 layers, pos = plen - 1 + t at step t) read plus the new K/V row
+    written.  Every row is counted every step (the kernel computes rows that already stopped)."""
+    n = steps - 1
+    if n <= 0:
+        return 0
+    keys = sum(n * (p - 1) + n * (n + 1) // 2 for p in plen)
+    return n * w_step + kv_row * (keys + len(plen) * n)
+
+
+PMC_PERSIST_FILE = os.path.join(ROOT, "profiles", "r3_pmc_persist.json")
+
+
+def persist_roofline(pipe, runner, outs, dt, log):
+    """roofline of the dominant kernel, decode_persist_kernel: the timed region's launches (HIP
+    events recorded on each launch's own stream around it, zsaac.decoder.PERSIST_LOG), algorithmic
+    bytes of each launch from its batch's prompt lengths and step count / its duration."""
+    from zsaac import ops
+    w_step = gpt2_step_weight_bytes(pipe)
+    by_dec = {}
+    for e0, e1, tag in log:
+        by_dec.setdefault(tag, []).append((e0, e1))
+    durs, byts = [], []
+    for i, b in runner.assign:
+        e0, e1 = by_dec[id(runner.pipes[i].decoder)].pop(0)
+        durs.append(e0.elapsed_time(e1) / 1e3)
+        byts.append(persist_launch_bytes(w_step, outs[b].plen.tolist(), runner.decode_steps[b]))
+    n = len(durs)
+    avg_s, avg_b = sum(durs) / n, sum(byts) / n
+    traffic, tsrc = None, None
+    if os.path.exists(PMC_PERSIST_FILE):     # rocprofv3 --pmc passes (tools/pmc_traffic.py persist)
+        with open(PMC_PERSIST_FILE) as f:
+            pmc = json.load(f)
+        if pmc.get("kernel", "").startswith("decode_persist_kernel"):
+            traffic, tsrc = pmc["hbm_bytes_per_launch"], os.path.relpath(PMC_PERSIST_FILE, ROOT)
+    steps = sum(runner.decode_steps) / max(1, len(runner.decode_steps))
+    return _hbm_entry(
+        f"decode_persist_kernel (zs_gpt2_decode_persist): decode steps 1..{steps - 1:.0f} of one "
+        f"bs-64 eval batch in one launch (G={ops.decode_persist_grid()} workgroups), the {n} launches of "
+        f"the timed region, {runner.n_inflight} batches in flight", avg_b, avg_s,
+        {"launches": n, "avg_launch_ms": round(avg_s * 1e3, 3),
+         "weight_bytes_per_step": int(w_step), "steps_per_launch_mean": round(steps - 1, 2),
+         "traffic": traffic, "traffic_source": tsrc,
+         "traffic_note": "PMC FETCH_SIZE*2*1024 + WRITE_SIZE*1024 per launch, single-stream "
+                         "launches of the same workload (tools/pmc_traffic.py persist)",
+         "concurrent_aggregate": {"algo_GBps": round(sum(byts) / dt / 1e9, 1),
+                                  "frac": round(sum(byts) / dt / 1e9 / HBM_PEAK_GBS, 4),
+                                  "note": "all launches' algorithmic bytes / the timed wall"}})
+
+
+def persist_all_launches(log):
+    """Average duration of every persistent launch of this process (warmup, timed region and the
+    single-stream roofline runs): the number rocprofv3 --kernel-trace --stats reports."""
+    d = [e0.elapsed_time(e1) for e0, e1, _ in log]
+    return {"launches": len(d), "avg_ms": round(sum(d) / max(1, len(d)), 3)}
+
+
+def decode_step_roofline(pipe, wav, agg_steps_per_s=None, reps=3):
+    """One greedy decode step of one batch on ONE stream (nothing else running): the persistent
+    launch (all steps after step 0) timed with HIP events / its steps, or, on the per-step path,
+    a graph-replayed chunk / its steps.  Bytes = persist_launch_bytes per step."""
+    from zsaac import decoder as zdec
+    dec, B = pipe.decoder, wav.shape[0]
+    w_step = gpt2_step_weight_bytes(pipe)
+    if dec.persist:
+        per = []
+        for _ in range(reps):
+            pipe.begin_wav(wav)
+            dec.run_to_completion()
+            torch.cuda.synchronize()
+            e0, e1, _ = zdec.PERSIST_LOG[-1]
+            steps = int(dec.step_ctr.item())
+            per.append((e0.elapsed_time(e1) / 1e3, steps))
+        dur, steps = sorted(per)[len(per) // 2]
+        byts = persist_launch_bytes(w_step, dec.plen[:B].tolist(), steps) / (steps - 1)
+        step_s = dur / (steps - 1)
+        what = "decode_persist_kernel launch / its steps"
+    else:
+        pipe.begin_wav(wav)
+        dec.done.zero_()
+        gr = dec._graph(*dec._chunk_plan(None))
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(10):
+            gr.replay()
+        e1.record()
+        e1.synchronize()
+        step_s = e0.elapsed_time(e1) / 1e3 / 10 / dec.chunk
+        L = min(dec.Lmax - 1, pipe.Pmax + 34)
+        byts = w_step + B * L * 12 * 2 * 768 * 2
+        what = "graph-replayed chunk / its steps"
+    r = _hbm_entry(f"one greedy decode step, {B} rows (12 blocks + ln_f + LM head + greedy step), "
+                   f"single stream ({what})", byts, step_s, {"avg_step_us": round(step_s * 1e6, 1)})
     r.pop("avg_launch_us")
     if agg_steps_per_s:
         agg = byts * agg_steps_per_s / 1e9
@@ -384,35 +514,98 @@ def decode_step_roofline(pipe, agg_steps_per_s=None):
     return r
 
 
+def htsat_flops(B):
+    """Multiply-add flops x 2 of HTSAT forward_features for B clips (patch embed, every Swin
+    block's qkv / window attention (64-token windows) / proj / MLP, the patch merges)."""
+    from zsaac.encoder import DEPTHS, EMBED, WIN
+    M, C = B * 4096, EMBED
+    f = 2 * M * C * 16                                   # 4 x 4 patch embed, 1 channel
+    for i, depth in enumerate(DEPTHS):
+        blk = 2 * M * C * 3 * C + 2 * 2 * M * WIN * WIN * C + 2 * M * C * C + 2 * 2 * M * C * 4 * C
+        f += depth * blk
+        if i < len(DEPTHS) - 1:
+            f += 2 * (M // 4) * 4 * C * 2 * C
+            M, C = M // 4, 2 * C
+    return f
+
+
+def cnn14_flops(B, frames):
+    from zsaac.encoder import CNN14_CH
+    H, W, ci, f = frames, 64, 1, 0
+    for co in CNN14_CH:
+        f += 2 * B * H * W * 9 * (ci * co + co * co)
+        H, W, ci = H // 2, W // 2, co
+    return f
+
+
 def stage_times(pipe, wav, reps=3):
-    """Per-stage device time of one batch (events between stages; extra syncs, so outside the
-    timed region): front end + encoder + proj, prompt + mapper + prefill + prefix tokens, decode."""
+    """Per-stage device time of one batch on one stream (events between stages, outside the timed
+    region) and each stage's roofline fraction: front end (STFT/log-mel, HBM), encoder (HTSAT /
+    CNN14 + audio_proj, MFMA), prompt + mapper (HBM: the mapper's weights), prefill (GPT-2 over
+    B x Pmax rows + get_prefix_tokens, MFMA) and decode (HBM, persist_launch_bytes + step 0)."""
     from zsaac import ops
-    dec, cfg = pipe.decoder, pipe.cfg
+    dec, cfg, enc = pipe.decoder, pipe.cfg, pipe.encoder
     B, Pmax = wav.shape[0], pipe.Pmax
-    out = {"encode": [], "prompt_mapper_prefill": [], "decode": []}
+    names = ("front_end", "encoder", "prompt_mapper", "prefill", "decode")
+    out = {k: [] for k in names}
     for _ in range(reps):
-        ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(6)]
         ev[0].record()
-        emb = pipe.encode(wav)
+        ops.logmel(wav, enc.tables, bn=enc.w.bn0, out=enc.logmel[:B])
         ev[1].record()
+        emb = enc.encode_logmel(None, B)
+        ev[2].record()
         ops.prompt_assemble(emb, pipe.labels, cfg.sound_effect_num, pipe.label_tok, pipe.label_len,
                             pipe.hard_ids[:B], pipe.hard_len[:B])
         soft = pipe.mapper(ops.l2norm(emb, out=pipe.prefix[:B]))
+        ev[3].record()
         ops.prefill_embed(pipe.hard_ids[:B], pipe.hard_len[:B], soft, pipe.mapper.soft_ld,
                           cfg.prefix_length, pipe.gpt.wte, pipe.gpt.wpe, B, Pmax,
                           pipe.embed[:B * Pmax], dec.x, dec.plen, dec.last_row)
         pipe.prefix_tokens(B, soft)
         dec.prefill(B, Pmax)
-        ev[2].record()
-        dec.greedy(B, Pmax)
-        ev[3].record()
+        ev[4].record()
+        dec.greedy_begin(B)
+        dec.run_to_completion()
+        ev[5].record()
         torch.cuda.synchronize()
-        for i, k in enumerate(out):
+        for i, k in enumerate(names):
             out[k].append(ev[i].elapsed_time(ev[i + 1]))
-    res = {k: round(sorted(v)[len(v) // 2], 3) for k, v in out.items()}
-    res["decode_steps"] = int(dec.step_ctr.item())
-    return res
+    ms = {k: sorted(v)[len(v) // 2] for k, v in out.items()}
+    steps = int(dec.step_ctr.item())
+    es = 2 if cfg.dtype == torch.bfloat16 else 4
+    peak_mfma = MFMA_BF16_PEAK_TFLOPS if es == 2 else MFMA_F32_PEAK_TFLOPS
+    frames = enc.n_frames
+    mp = pipe.mapper
+    if hasattr(mp, "w0"):
+        map_bytes = (mp.w0.numel() + mp.w2.numel()) * mp.w0.element_size()
+    else:
+        map_bytes = sum(t.numel() * t.element_size() for ly in mp.layers for t in ly.values()
+                        if torch.is_tensor(t))
+    n_gpt = sum(ly[k].numel() for ly in pipe.gpt.layers for k in ("attn_w", "proj_w", "fc_w", "mproj_w"))
+    rows = B * Pmax
+    prefill_flops = (2 * rows * n_gpt + 2 * 2 * B * 12 * Pmax * Pmax * 64 // 2
+                     + 2 * B * cfg.prefix_length * pipe.gpt.V * 768)
+    enc_flops = htsat_flops(B) if cfg.encoder == "htsat" else cnn14_flops(B, frames)
+    dec_bytes = (persist_launch_bytes(gpt2_step_weight_bytes(pipe), dec.plen[:B].tolist(), steps)
+                 + pipe.gpt.V * 768 * es)
+    fe_bytes = wav.numel() * 4 + B * frames * 64 * 4
+
+    def hbm(b, k):
+        gbs = b / (ms[k] / 1e3) / 1e9
+        return {"ms": round(ms[k], 3), "bound": "hbm", "algo_bytes": int(b), "achieved_GBps": round(gbs, 1),
+                "frac": round(gbs / HBM_PEAK_GBS, 4)}
+
+    def mfma(f, k):
+        tf = f / (ms[k] / 1e3) / 1e12
+        return {"ms": round(ms[k], 3), "bound": "mfma", "flops": int(f), "achieved_TFLOPs": round(tf, 1),
+                "frac": round(tf / peak_mfma, 4)}
+    return {"clips": B, "single_stream": True, "decode_steps": steps,
+            "front_end": hbm(fe_bytes, "front_end"),
+            "encoder": mfma(enc_flops, "encoder"),
+            "prompt_mapper": hbm(map_bytes, "prompt_mapper"),
+            "prefill": mfma(prefill_flops, "prefill"),
+            "decode": hbm(dec_bytes, "decode")}
 
 
 # ------------------------------------------------------------------ CPU baseline
@@ -427,11 +620,13 @@ def _cpu_model():
     return None
 
 
-def cpu_baseline(args, csd, asd, n_c2, n_c1):
+def cpu_baseline(args, csd, asd, n_c2, n_c1, n_c3):
     """Oracle = reference semantics (batch 1 per clip, full-sequence recompute every step, fp32)
-    on bounded samples: n_c2 clips of the C2 workload (wav -> HTSAT -> MLP -> greedy) and n_c1
-    clips of C1 (the reference goldens' CLAP embeddings -> MLP -> greedy), on the CPUs this
-    process may use (sched affinity; os.cpu_count() may count the whole machine)."""
+    on the BASELINE.md §3 configs, bounded by default: n_c2 clips of the C2 workload (wav ->
+    HTSAT -> MLP -> greedy), n_c1 of C1's 50 reference-golden CLAP embeddings (-> MLP -> greedy)
+    and n_c3 clips of C3 (wav -> HTSAT -> MLP -> beam 5); --cpu-baseline-full times the plan's
+    64 / 50 / 64.  On the CPUs this process may use (sched affinity; os.cpu_count() may count the
+    whole machine)."""
     import numpy as np
     from oracle import audio as A, caption as OC, frontend as OF
     from zsaac import synthetic as S
@@ -444,27 +639,31 @@ def cpu_baseline(args, csd, asd, n_c2, n_c1):
     torch.set_num_threads(threads)
     table, lt = S.label_table(), S.label_token_table()
 
-    def caption(emb, ntok):
+    def caption(emb, ntok, beam=0):
         idx = OC.sound_effect_choice(emb, table, 3)[0].tolist()
         hard = torch.tensor([OC.prompt_ids(idx, lt)])
         pe = OC.clap_to_gpt(torch.nn.functional.normalize(emb, dim=-1)[None], hard, csd, args.mapper)
         OC.prefix_tokens(pe, csd)
-        if args.beam:
-            OC.generate_beam(pe, csd, beam_size=args.beam, entry_length=args.entry_length)
+        if beam:
+            lists, _ = OC.generate_beam(pe, csd, beam_size=beam, entry_length=args.entry_length)
+            ntok[0] += len(lists[0])
         else:
             ntok[0] += len(OC.generate2(pe, csd, entry_length=args.entry_length))
 
-    log(f"cpu baseline: C2 {n_c2} clips, C1 {n_c1} clips, {threads} threads")
-    wav = synthetic_clips(n_c2, 777, torch.device("cpu"))
-    ntok = [0]
-    t0 = time.perf_counter()
-    with torch.no_grad():
-        for i in range(n_c2):
-            lm = OF.logmel(wav[i:i + 1])
-            feat = A.htsat_embedding(lm, asd) if args.encoder == "htsat" else A.cnn14_embedding(lm, asd)
-            caption(A.audio_project(feat, asd), ntok)
-            log(f"cpu baseline C2 clip {i + 1}/{n_c2}")
-    dt2 = time.perf_counter() - t0
+    def wav_clips(n, first, beam, label):
+        wav = synthetic_clips(n, first, torch.device("cpu"))
+        ntok = [0]
+        t0 = time.perf_counter()
+        with torch.no_grad():
+            for i in range(n):
+                lm = OF.logmel(wav[i:i + 1])
+                feat = A.htsat_embedding(lm, asd) if args.encoder == "htsat" else A.cnn14_embedding(lm, asd)
+                caption(A.audio_project(feat, asd), ntok, beam)
+                log(f"cpu baseline {label} clip {i + 1}/{n}")
+        return time.perf_counter() - t0, ntok[0]
+
+    log(f"cpu baseline: C2 {n_c2} clips, C1 {n_c1} clips, C3 {n_c3} clips, {threads} threads")
+    dt2, tok2 = wav_clips(n_c2, 777, 0, "C2")
     c1 = np.load(os.path.join(ROOT, "tests", "golden", "c1_greedy.npz"))
     emb = torch.from_numpy(c1["clap_emb"][:n_c1])
     ntok1 = [0]
@@ -475,21 +674,32 @@ def cpu_baseline(args, csd, asd, n_c2, n_c1):
             if i % 4 == 3:
                 log(f"cpu baseline C1 clip {i + 1}/{n_c1}")
     dt1 = time.perf_counter() - t0
-    return {"value": round(n_c2 / dt2, 4), "unit": "clips/s", "cores": threads, "kind": "port",
-            "threads": threads, "cpus_visible": visible, "cpus_available": avail,
-            "omp_num_threads_env": share or None,
-            "cpu_model": _cpu_model(),
-            "sample": f"C2: {n_c2} clips of the headline workload (wav -> log-mel -> "
-                      f"{args.encoder.upper()} -> audio_proj -> prompt -> {args.mapper} mapper -> "
-                      f"get_prefix_tokens -> greedy, {ntok[0]} tokens) in {dt2:.1f} s; batch 1, "
-                      f"full-sequence recompute per step (reference semantics), fp32, "
-                      f"{threads} threads.  A bounded sample (the full 1045 clips would take "
-                      f"~{CLOTHO_EVAL_CLIPS / max(n_c2 / dt2, 1e-9) / 60:.0f} min)",
-            "c1_plumbing": {"value": round(n_c1 / dt1, 4), "unit": "clips/s", "clips": n_c1,
-                            "tokens": ntok1[0], "seconds": round(dt1, 1),
-                            "sample": "C1: the first clips of the 50 reference-golden CLAP "
-                                      "embeddings -> MLP -> greedy (of 50: bounded to keep the "
-                                      "default run within minutes)"}}
+    res = {"value": round(n_c2 / dt2, 4), "unit": "clips/s", "cores": threads, "kind": "port",
+           "threads": threads, "cpus_visible": visible, "cpus_available": avail,
+           "omp_num_threads_env": share or None,
+           "cpu_model": _cpu_model(),
+           "sample": f"C2: {n_c2} clips of the headline workload (wav -> log-mel -> "
+                     f"{args.encoder.upper()} -> audio_proj -> prompt -> {args.mapper} mapper -> "
+                     f"get_prefix_tokens -> greedy, {tok2} tokens) in {dt2:.1f} s; batch 1, "
+                     f"full-sequence recompute per step (reference semantics), fp32, "
+                     f"{threads} threads.  " + ("The BASELINE.md §3 slice (64 clips)" if n_c2 >= 64 else
+                     f"A bounded sample (BASELINE.md §3 plans 64 clips; the full 1045 would take "
+                     f"~{CLOTHO_EVAL_CLIPS / max(n_c2 / dt2, 1e-9) / 60:.0f} min; "
+                     f"bench.py --cpu-baseline-full times the plan)"),
+           "c1_plumbing": {"value": round(n_c1 / dt1, 4), "unit": "clips/s", "clips": n_c1,
+                           "tokens": ntok1[0], "seconds": round(dt1, 1),
+                           "sample": f"C1: {n_c1} of the 50 reference-golden CLAP embeddings -> "
+                                     f"MLP -> greedy" + ("" if n_c1 >= 50 else
+                                     " (bounded; --cpu-baseline-full times all 50)")}}
+    if n_c3 > 0:
+        dt3, _ = wav_clips(n_c3, 5555, 5, "C3")
+        res["c3_beam5"] = {"value": round(n_c3 / dt3, 4), "unit": "clips/s", "clips": n_c3,
+                           "seconds": round(dt3, 1),
+                           "sample": f"C3: {n_c3} clips wav -> {args.encoder.upper()} -> MLP -> "
+                                     f"generate_beam (beam 5, softmax().log() scores, entry_length "
+                                     f"{args.entry_length}), batch 1" + ("" if n_c3 >= 64 else
+                                     " (bounded; BASELINE.md §3 plans 64, --cpu-baseline-full)")}
+    return res
 
 
 # ------------------------------------------------------------------ C4
@@ -726,6 +936,31 @@ def main_mistral(args, device):
         flush=True)
 
 
+def strong_scaling_proxy(args, device, pipe, t_full, n_full, n_ranks=8):
+    """Predicted 1 -> 8 GPU strong-scaling speed-up on Clotho-eval from ONE GPU: one rank's
+    1/8 shard (shard_range: 131 clips) timed alone, T(1045) / T(131).  Two batchings of the
+    shard: the reference's consecutive bs-64 batches (64 + 64 + 3) and near-equal batches over
+    every in-flight stream (split_batches parts=inflight); the faster is what a rank runs."""
+    from zsaac import dist as zd
+    lo, hi = zd.shard_range(n_full, 0, n_ranks)
+    n = hi - lo
+    out = {"clips_full": n_full, "seconds_full": round(t_full, 4), "ranks": n_ranks,
+           "clips_per_rank": n}
+    best = None
+    for name, parts in (("bs64_batches", 0), ("balanced_batches", args.inflight)):
+        dt, outs, runner, _ = run_captions(args, 1, 0, device, pipe, n, lo, [n], args.inflight,
+                                           0, parts=parts)
+        sizes = [int(o.ids.shape[0]) for o in outs]
+        out[name] = {"seconds": round(dt, 4), "batches": sizes,
+                     "predicted_speedup": round(t_full / dt, 2)}
+        best = max(best or 0.0, t_full / dt)
+        del outs, runner
+    out["predicted_speedup"] = round(best, 2)
+    out["note"] = ("one GPU, one rank's shard alone; the 8-rank run adds one RCCL all-gather of "
+                   "token ids (zsaac/dist.py collect_captions)")
+    return out
+
+
 def main():
     args = parse()
     world, rank, local = dist_setup(args)
@@ -735,6 +970,9 @@ def main():
         return main_magic(args, torch.device("cuda", 0))
     if args.mistral:
         return main_mistral(args, torch.device("cuda", 0))
+    if not args.no_roofline:
+        from zsaac import decoder as zdec
+        zdec.PERSIST_LOG = []         # HIP events around every persistent decode launch
     pipe, csd, asd = build(args, device)
     if args.embeddings_only:
         return main_embeddings(args, world, rank, device, pipe)
@@ -776,17 +1014,31 @@ def main():
                    "parallelism": f"dp{world} (clip-sharded, RCCL all-gather of token ids)",
                    **info},
     }
-    if rank == 0 and args.stages:
-        res["stages_ms"] = stage_times(pipe, synthetic_clips(B, 0, device))
-    if rank == 0 and not args.no_roofline and args.group == 1 and B <= 64 and not args.beam \
-            and args.dtype == "bf16":
+    headline_cfg = rank == 0 and args.group == 1 and B <= 64 and not args.beam
+    if rank == 0 and not args.no_roofline and headline_cfg and args.dtype == "bf16":
         log("rooflines")
-        res["roofline"] = roofline_gemm_ln(pipe)
-        res["roofline_mproj"] = roofline_rows_gemm(pipe, "mproj")
-        res["roofline_proj"] = roofline_rows_gemm(pipe, "proj")
-        res["roofline_decode_attention"] = roofline_attention(pipe)
+        from zsaac import decoder as zdec
+        if pipe.decoder.persist:
+            res["roofline"] = persist_roofline(pipe, runner, outs, dt, runner.timed_log)
+        else:
+            res["roofline"] = roofline_gemm_ln(pipe)
+        wav = synthetic_clips(B, 0, device)
         agg = info["decode_steps_mean"] * steps / dt if world == 1 else None
-        res["roofline_decode_step"] = decode_step_roofline(pipe, agg)
+        res["roofline_decode_step"] = decode_step_roofline(pipe, wav, agg)
+        res["stages"] = stage_times(pipe, wav)
+        # the per-step-path kernels (configs the persistent launch does not take: beam, f32,
+        # > 64 rows), at the bs-64 decode shapes, cold weights / K/V
+        res["roofline_stepwise_c_fc"] = roofline_gemm_ln(pipe)
+        res["roofline_stepwise_mproj"] = roofline_rows_gemm(pipe, "mproj")
+        res["roofline_stepwise_proj"] = roofline_rows_gemm(pipe, "proj")
+        res["roofline_decode_attention"] = roofline_attention(pipe)
+        res["persist_launches_all"] = persist_all_launches(zdec.PERSIST_LOG or [])
+        del wav
+    elif rank == 0 and args.stages:
+        res["stages"] = stage_times(pipe, synthetic_clips(B, 0, device))
+    if (rank == 0 and world == 1 and headline_cfg and not args.clips and not args.steps
+            and not args.no_scaling_proxy):
+        res["strong_scaling_proxy"] = strong_scaling_proxy(args, device, pipe, dt, n_total)
     del runner, outs
     if rank == 0 and world == 1 and args.extras and args.group == 1 and not args.beam:
         del pipe
@@ -805,8 +1057,10 @@ def main():
         res["id_agreement"] = {"bf16": idparity.summary(torch.bfloat16, device),
                                "f32": idparity.summary(torch.float32, device)}
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.cpu_baseline_clips > 0:
-        res["cpu_baseline"] = cpu_baseline(args, csd, asd, args.cpu_baseline_clips,
-                                           max(1, args.cpu_baseline_clips // 2))
+        n2, n1, n3 = ((64, 50, 64) if args.cpu_baseline_full else
+                      (args.cpu_baseline_clips, min(50, 2 * args.cpu_baseline_clips),
+                       max(1, args.cpu_baseline_clips // 2)))
+        res["cpu_baseline"] = cpu_baseline(args, csd, asd, n2, n1, n3)
     if rank == 0:
         print(json.dumps(res), flush=True)
     if world > 1:

@@ -8,6 +8,14 @@ launches of exactly the launches bench.py times (roofline_setup: cold weights), 
     rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_write -o run --output-format csv -- python3 tools/pmc_traffic.py run
     python3 tools/pmc_traffic.py parse gpurun_out/pmc_fetch gpurun_out/pmc_write profiles/r2_pmc_traffic.json
 
+The persistent decode kernel (bench.py's roofline since round 3): ``run_persist`` decodes the
+bench's first eval batch (64 synthetic clips, 67 greedy steps) three times on one stream, and
+``parse_persist`` writes profiles/r3_pmc_persist.json (per-launch bytes, median launch):
+
+    rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_pf -o run --output-format csv -- python3 tools/pmc_traffic.py run_persist
+    rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_pw -o run --output-format csv -- python3 tools/pmc_traffic.py run_persist
+    python3 tools/pmc_traffic.py parse_persist gpurun_out/pmc_pf gpurun_out/pmc_pw profiles/r3_pmc_persist.json
+
 Corrections (MI355X_MICROARCH.md §HBM): FETCH_SIZE is in KiB and on gfx950 reports half the
 bytes of a 16-B/lane coalesced streaming read (the GEMM's LDS-DMA loads are all 16 B per lane),
 so read bytes = 2 * 1024 * FETCH_SIZE; WRITE_SIZE (KiB) is exact for 16-B/lane stores (the
@@ -85,8 +93,62 @@ def parse(dfetch, dwrite, out, M=64, N=3072, K=768, kname="gemm_rows_kernel"):
     print(json.dumps(res))
 
 
+def _bench_pipe():
+    import torch
+    import bench
+
+    class A:
+        batch, group, dtype, encoder, mapper, beam, entry_length, compact = \
+            64, 1, "bf16", "htsat", "mlp", 0, 67, 1
+        encoder_batch = 64
+    pipe, _, _ = bench.build(A, torch.device("cuda", 0))
+    return bench, pipe
+
+
+def run_persist(reps=3):
+    import torch
+    bench, pipe = _bench_pipe()
+    assert pipe.decoder.persist, "the persistent decode path is off"
+    wav = bench.synthetic_clips(64, 0, torch.device("cuda", 0))
+    info = []
+    for _ in range(reps):
+        pipe.begin_wav(wav)
+        pipe.decoder.run_to_completion()
+        torch.cuda.synchronize()
+        info.append(int(pipe.decoder.step_ctr.item()))
+    plen = pipe.decoder.plen[:64].tolist()
+    algo = bench.persist_launch_bytes(bench.gpt2_step_weight_bytes(pipe), plen, info[-1])
+    with open(os.path.join(ROOT, "gpurun_out", "pmc_persist_run.json"), "w") as f:
+        json.dump({"steps": info, "plen": plen, "algo_bytes_per_launch": algo}, f)
+    print(json.dumps({"launches": reps, "steps": info, "algo_bytes_per_launch": algo}))
+
+
+def parse_persist(dfetch, dwrite, out, kname="decode_persist_kernel"):
+    fetch_kib, n_f = _per_dispatch(dfetch, "FETCH_SIZE", kname)
+    write_kib, n_w = _per_dispatch(dwrite, "WRITE_SIZE", kname)
+    rd, wr = 2 * 1024 * fetch_kib, 1024 * write_kib
+    with open(os.path.join(ROOT, "gpurun_out", "pmc_persist_run.json")) as f:
+        run_info = json.load(f)
+    res = {"kernel": f"{kname} (zs_gpt2_decode_persist): one bs-64 eval batch of the bench "
+                     f"(64 synthetic clips), decode steps 1..{run_info['steps'][-1] - 1}, one stream",
+           "fetch_size_kib_median": fetch_kib, "write_size_kib_median": write_kib,
+           "dispatches": [n_f, n_w], "hbm_read_bytes_per_launch": int(rd),
+           "hbm_write_bytes_per_launch": int(wr), "hbm_bytes_per_launch": int(rd + wr),
+           "algo_bytes_per_launch": run_info["algo_bytes_per_launch"],
+           "traffic_over_algo": round((rd + wr) / run_info["algo_bytes_per_launch"], 3),
+           "corrections": "read = 2*1024*FETCH_SIZE (gfx950 16B/lane streaming reads; FETCH_SIZE "
+                          "counts L2 misses incl. Infinity-Cache hits); write = 1024*WRITE_SIZE"}
+    with open(out, "w") as f:
+        json.dump(res, f, indent=1)
+    print(json.dumps(res))
+
+
 if __name__ == "__main__":
     if sys.argv[1] == "run":
         run()
+    elif sys.argv[1] == "run_persist":
+        run_persist()
+    elif sys.argv[1] == "parse_persist":
+        parse_persist(*sys.argv[2:5])
     else:
         parse(*sys.argv[2:5])

@@ -318,6 +318,9 @@ class ZsMistralForCausalLM(nn.Module):
         # fp8 weights unless set_mode() / zs_mistral_mode picks "bf16" or the "f32" parity mode
         mode = getattr(self, "zs_mistral_mode", "fp8")
         c = self.config
+        device = torch.device(device)
+        if device.type == "cuda" and device.index is None:        # "cuda" and "cuda:0" are one key
+            device = torch.device("cuda", torch.cuda.current_device())
 
         def build():
             return MistralWeights(self.state_dict(), device, mode, c["num_attention_heads"],

@@ -24,6 +24,10 @@ import torch
 
 from . import ops
 
+# bench.py sets a list here: every persistent decode launch then appends (start event, end event,
+# id(decoder)), recorded on the launching stream around the launch (the roofline's live timing)
+PERSIST_LOG: Optional[list] = None
+
 D, NH, HD, NL = 768, 12, 64, 12
 STOP_DOT, STOP_SPACE_DOT = 13, 764
 
@@ -529,11 +533,18 @@ class Gpt2Decoder:
         self._cgreedy = R if (self.compact and R >= self.min_bucket) else None
         if self.persist and R <= 64:
             w = self.w
+            ev = PERSIST_LOG
+            if ev is not None:          # bench.py's roofline: HIP events around each launch
+                ev.append((torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True),
+                           id(self)))
+                ev[-1][0].record()
             ops.gpt2_decode_persist(R, self.Lmax, self.max_steps, self.stop0, self.stop1, w.V, w.wte,
                                     w.wpe, w.wte_packed(), self.temperature, w.layer_ptrs(),
                                     w.lnf[0], w.lnf[1], self._kv_ptrs,
                                     self.pos, self.next_tok, self.done, self.out_ids, self.out_len,
                                     self.step_ctr, self.all_done, self.persist_ws)
+            if ev is not None:
+                ev[-1][1].record()
             self.rows_stepped += R * (self.max_steps - 1)   # upper bound (rows that stop early end it)
 
     def greedy(self, B: int, Pmax: int):

@@ -275,6 +275,7 @@ class ConcurrentRunner:
         active = {}
         nxt = 0
         self.decode_steps = [0] * len(batches)     # per batch: decode steps actually enqueued
+        self.assign = []                           # (pipeline index, batch index), in begin order
         while nxt < len(batches) or active:
             progressed = False
             for i, (p, s) in enumerate(zip(self.pipes, self.streams)):
@@ -285,6 +286,7 @@ class ConcurrentRunner:
                             (p.begin_wav if inputs == "wav" else p.begin_emb)(batches[nxt])
                             ev, flag = p.decoder.finished_async()
                         active[i] = (nxt, 0, ev, flag)
+                        self.assign.append((i, nxt))
                         nxt += 1
                         progressed = True
                     continue
