@@ -13,6 +13,8 @@ import numpy as np
 import pytest
 import torch
 
+TAU = 0.2      # the floor of tests/test_gpu_idparity.py's margin rule
+
 pytestmark = pytest.mark.gpu
 
 GPT2_KW = dict(seed=0, std=0.1, emb_std=0.1, stop_boost=2.0)   # the bench's decoder weights
@@ -99,12 +101,33 @@ def test_c2_bf16_wav_batch64(cuda, sds):
     print(f"C2 bf16 B=64: encoder cos min {float(cos.min()):.5f}; first-step logit max err / std "
           f"{float(rel.max()):.3f}; first token {first_ok}/{B}; leading tokens agreeing "
           f"{sum(lead)}/{tot}; exact captions {sum(c16[b] == c32[b] for b in range(B))}/{B}")
-    # floors (the bench's std-0.1 synthetic decoder is chaotic, DESIGN.md §5: bf16 moves
-    # first-step logits by up to ~0.4 std and ids part after a few tokens; the margin-gated
-    # bit-exactness check on reference goldens is tests/test_gpu_idparity.py): the first token on
-    # >= 3/4 of the clips, >= 5 % of the tokens in agreeing leading runs
-    assert first_ok >= B * 3 // 4
-    assert sum(lead) >= 0.05 * tot
+    # the margin rule of tests/test_gpu_idparity.py on this workload: along the f32 path's own
+    # greedy trajectory, the f32 oracle's top-1 / top-2 logit margin at every step (teacher-forced
+    # full recompute on the host); bf16 ids must equal the f32 ids up to the first step whose
+    # margin is below tau = max(TAU, 2 x the measured bf16 first-step logit error), and a clip
+    # whose margins all clear tau must be exact end to end
+    tau = max(TAU, 2.0 * float((l16 - l32).abs().max()))
+    wte = csd["gpt.transformer.wte.weight"]
+    exact_needed = checked = 0
+    with torch.no_grad():
+        for b in range(B):
+            hard = hi[b, :hl[b]].tolist()
+            pe = OC.clap_to_gpt(torch.nn.functional.normalize(e[b:b + 1].cpu(), dim=-1)[None],
+                                torch.tensor([hard]), csd)
+            toks = c32[b]
+            seq = torch.cat([pe, wte[toks[:-1]][None]], 1) if len(toks) > 1 else pe
+            lg, _ = OC.gpt2_logits(seq, csd)
+            top2 = lg[0, pe.shape[1] - 1:].topk(2, dim=-1).values
+            margin = (top2[:, 0] - top2[:, 1]).tolist()
+            amb = next((i for i, m in enumerate(margin) if m < tau), None)
+            n = len(toks) if amb is None else amb
+            assert c16[b][:n] == toks[:n], (b, n, tau, c16[b][:n + 1], toks[:n + 1])
+            if amb is None:
+                exact_needed += 1
+                assert c16[b] == toks, (b, tau)
+            checked += n
+    print(f"C2 bf16 margin rule: tau {tau:.3f}; {checked}/{tot} tokens before the first ambiguous "
+          f"step must agree (they do); clips with every margin >= tau: {exact_needed}")
 
 
 def _beam_caps(csd, dtype, emb, beam):

@@ -61,6 +61,7 @@ struct RowsArgs {
   const float* residual; int ldr;
   void* out; int ldo; int out_dtype; int act;
   int rgroups, ntiles;
+  const float* Af; const float* Wf;         // f32 operands (gemm_rows_f32_kernel)
 };
 
 template <int NT, int WAVES, int LNM, int S>
@@ -248,6 +249,177 @@ __global__ __launch_bounds__(64 * WAVES) void gemm_rows_kernel(RowsArgs g) {
   ZS_STAMP(6);
 }
 
+// ------------------------------------------------------------------ f32 operands
+// The f32 parity mode's decode GEMMs (exact f32 products, f32 accumulation: v_mfma_f32_16x16x4_f32,
+// MI355X_MICROARCH.md: bitwise an fmaf chain).  Same structure as gemm_rows_kernel (row groups of
+// 16, full K per workgroup split over its waves, every weight load issued up front, LN prologue
+// from the f32 residual stream with the LN affine applied in f32, wave partials summed in LDS).
+// A k-step covers 16 k: lane l (fr = l & 15, g = l >> 4) loads 16 bytes of its A row and of its
+// weight row at k + 4 g .. + 4; MFMA j (j = 0..3) takes element j of both, i.e. the MFMA's k index
+// g stands for k + 4 g + j, so the four MFMAs of a k-step cover its 16 k.
+typedef __attribute__((ext_vector_type(4))) float f32x4v_t;
+
+template <int NT, int WAVES, int LNM, int S>
+__global__ __launch_bounds__(64 * WAVES) void gemm_rows_f32_kernel(RowsArgs g) {
+  constexpr bool LN = LNM != 0;
+  constexpr int NB = NT / 16;
+  constexpr int NTHR = 64 * WAVES;
+  constexpr int K = 16 * WAVES * S, KW = K / WAVES;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int nwg = gridDim.x, id = blockIdx.x, xcd = id & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int u = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (id >> 3);
+  const int rg = u % g.rgroups, tile = u / g.rgroups;
+  const int m0 = rg * RG, n0 = tile * NT;
+  const int kw = wid * KW;
+  constexpr int ldh = K + 4;                // padded f32 LDS row
+  float* hs = reinterpret_cast<float*>(smem);
+  float* red = reinterpret_cast<float*>(smem + (LN ? RG * ldh * 4 : 0));
+  const int fr = lane & 15, fk = 4 * (lane >> 4);
+  const int am = min(m0 + fr, g.M - 1);
+
+  constexpr int NQ = NT / 4;
+  static_assert(RG * NQ <= NTHR, "one epilogue quad per thread");
+  const bool epi = threadIdx.x < RG * NQ;
+  const int erow = threadIdx.x / NQ, ecq = threadIdx.x % NQ;
+  const int em = m0 + erow, en = n0 + 4 * ecq;
+  float4 eb = make_float4(0.f, 0.f, 0.f, 0.f), er = eb;
+  if (epi) {
+    if (g.bias) {
+      eb.x = g.bias[min(en, g.N - 1)];     eb.y = g.bias[min(en + 1, g.N - 1)];
+      eb.z = g.bias[min(en + 2, g.N - 1)]; eb.w = g.bias[min(en + 3, g.N - 1)];
+    }
+    if (g.residual) {
+      const float* rr = g.residual + (long)min(em, g.M - 1) * g.ldr;
+      er.x = rr[min(en, g.N - 1)];     er.y = rr[min(en + 1, g.N - 1)];
+      er.z = rr[min(en + 2, g.N - 1)]; er.w = rr[min(en + 3, g.N - 1)];
+    }
+  }
+  constexpr int TPR = NTHR / RG, NV = LN ? K / (4 * TPR) : 1;
+  static_assert(!LN || K % (4 * TPR) == 0, "LN rows: K % (4 * threads per row)");
+  const int lr = threadIdx.x / TPR, lt = threadIdx.x % TPR;
+  float4 xv[NV];
+  if constexpr (LN) {
+    const float4* xr = reinterpret_cast<const float4*>(g.X + (long)min(m0 + lr, g.M - 1) * g.ldx);
+#pragma unroll
+    for (int i = 0; i < NV; ++i) xv[i] = xr[lt + TPR * i];
+  }
+  f32x4v_t b[S * NB];
+  f32x4v_t a[LN ? 1 : S];
+  const float* wrow[NB];
+#pragma unroll
+  for (int nb = 0; nb < NB; ++nb) wrow[nb] = g.Wf + (long)min(n0 + 16 * nb + fr, g.N - 1) * g.ldw;
+#pragma unroll
+  for (int s = 0; s < S; ++s) {
+    const int k = kw + 16 * s + fk;
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb) b[s * NB + nb] = *reinterpret_cast<const f32x4v_t*>(wrow[nb] + k);
+    if constexpr (!LN) a[s] = *reinterpret_cast<const f32x4v_t*>(g.Af + (long)am * g.lda + k);
+  }
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+
+  if constexpr (LN) {
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) s += (xv[i].x + xv[i].y) + (xv[i].z + xv[i].w);
+#pragma unroll
+    for (int o = TPR / 2; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+    const float mean = s * (1.0f / K);
+    float q = 0.f;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const float a0 = xv[i].x - mean, a1 = xv[i].y - mean, a2 = xv[i].z - mean, a3 = xv[i].w - mean;
+      q += (a0 * a0 + a1 * a1) + (a2 * a2 + a3 * a3);
+    }
+#pragma unroll
+    for (int o = TPR / 2; o > 0; o >>= 1) q += __shfl_xor(q, o, 64);
+    const float rstd = rsqrtf(q * (1.0f / K) + g.eps);
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int c = lt + TPR * i;
+      const float4 lw = reinterpret_cast<const float4*>(g.ln_w)[c];
+      const float4 lb = reinterpret_cast<const float4*>(g.ln_b)[c];
+      *reinterpret_cast<float4*>(hs + lr * ldh + 4 * c) =
+          make_float4((xv[i].x - mean) * rstd * lw.x + lb.x, (xv[i].y - mean) * rstd * lw.y + lb.y,
+                      (xv[i].z - mean) * rstd * lw.z + lb.z, (xv[i].w - mean) * rstd * lw.w + lb.w);
+    }
+    __syncthreads();
+  }
+
+  f32x4r_t acc[NB];
+#pragma unroll
+  for (int nb = 0; nb < NB; ++nb) acc[nb] = f32x4r_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int s = 0; s < S; ++s) {
+    f32x4v_t af;
+    if constexpr (LN)
+      af = *reinterpret_cast<const f32x4v_t*>(hs + fr * ldh + kw + 16 * s + fk);
+    else
+      af = a[s];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int nb = 0; nb < NB; ++nb)
+        acc[nb] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[j], b[s * NB + nb][j], acc[nb], 0, 0, 0);
+  }
+  float* mine = red + wid * RG * NT;
+#pragma unroll
+  for (int nb = 0; nb < NB; ++nb)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) mine[(4 * (lane >> 4) + i) * NT + 16 * nb + fr] = acc[nb][i];
+  __syncthreads();
+  if (!epi) return;
+  float4 sum = *reinterpret_cast<const float4*>(red + erow * NT + 4 * ecq);
+#pragma unroll
+  for (int w = 1; w < WAVES; ++w) {
+    const float4 p = *reinterpret_cast<const float4*>(red + (w * RG + erow) * NT + 4 * ecq);
+    sum.x += p.x; sum.y += p.y; sum.z += p.z; sum.w += p.w;
+  }
+  if (em >= g.M) return;
+  float v[4] = {sum.x + eb.x, sum.y + eb.y, sum.z + eb.z, sum.w + eb.w};
+#pragma unroll
+  for (int j = 0; j < 4; ++j) v[j] = act_apply(v[j], g.act);
+  v[0] += er.x; v[1] += er.y; v[2] += er.z; v[3] += er.w;
+  float* o = reinterpret_cast<float*>(g.out) + (long)em * g.ldo + en;
+  if (en + 3 < g.N && (g.ldo & 3) == 0 && ((uintptr_t)g.out & 15) == 0) {
+    *reinterpret_cast<float4*>(o) = make_float4(v[0], v[1], v[2], v[3]);
+  } else {
+    for (int j = 0; j < 4; ++j)
+      if (en + j < g.N) o[j] = v[j];
+  }
+}
+
+// f32 plan: 8 waves; LN (K 768 / 1024): 32-column tiles; plain: 16-column tiles, K 768 .. 4096
+static int launch_rows_f32(const RowsArgs& g0, bool ln, hipStream_t st) {
+  constexpr int W = 8;
+  RowsArgs g = g0;
+  const int K = g.K;
+  if (K % (16 * W)) return 1;
+  const int S = K / (16 * W);
+  const int nt = ln ? 32 : 16;
+  g.rgroups = cdiv(g.M, RG);
+  g.ntiles = cdiv(g.N, nt);
+  const dim3 grid(g.rgroups * g.ntiles);
+  const size_t lds = (ln ? (size_t)RG * (K + 4) * 4 : 0) + (size_t)W * RG * nt * 4;
+#define RF(LNM_, NT_, S_) hipLaunchKernelGGL((gemm_rows_f32_kernel<NT_, W, LNM_, S_>), grid, dim3(64 * W), lds, st, g)
+  if (ln) {
+    if (S == 6) RF(1, 32, 6);
+    else if (S == 8) RF(1, 32, 8);
+    else return 1;
+  } else {
+    switch (S) {
+      case 6: RF(0, 16, 6); break;
+      case 8: RF(0, 16, 8); break;
+      case 24: RF(0, 16, 24); break;
+      default: return 1;
+    }
+  }
+#undef RF
+  ZS_LAUNCH_CHECK();
+  return 0;
+}
+
 int g_rows_nt48 = 1;  // A/B knob (zs_tune_set "rows_nt48"): 48-column LN tiles (2: 64)
 int g_rows_wide = 0;  // A/B knob (zs_tune_set "rows_wide"): 32-column plain tiles at N < 1536
 int g_gemm_rows = 1;   // A/B knob (zs_tune_set "gemm_rows"): 0 = skinny split-K kernel for M <= 64
@@ -357,4 +529,34 @@ extern "C" int zs_gemm_ln(int M, int N, int K, const float* x, int ldx, const fl
   g.W = (const bf16_t*)W; g.ldw = ldw; g.bias = bias; g.residual = residual; g.ldr = ldr;
   g.out = out; g.ldo = ldo; g.out_dtype = out_dtype; g.act = act;
   return ln_w ? launch_rows<1>(g, p, S(stream)) : launch_rows<2>(g, p, S(stream));
+}
+
+// f32 operands, M <= 64 (zs_gemm auto mode); returns 1 when the shape is not covered
+extern "C" __attribute__((visibility("hidden"))) int zs_gemm_rows_f32_internal(
+    int M, int N, int K, const void* A, int lda, const void* W, int ldw, const float* bias,
+    const float* residual, int ldr, void* out, int ldo, int out_dtype, int act, void* stream) {
+  if (!g_gemm_rows || M > RG_MAX_M || out_dtype != ZS_F32 || (lda & 3) || (ldw & 3)) return 1;
+  RowsArgs g{};
+  g.M = M; g.N = N; g.K = K; g.Af = (const float*)A; g.lda = lda; g.Wf = (const float*)W;
+  g.ldw = ldw; g.bias = bias; g.residual = residual; g.ldr = ldr; g.out = out; g.ldo = ldo;
+  g.out_dtype = out_dtype; g.act = act;
+  return launch_rows_f32(g, false, S(stream));
+}
+
+extern "C" int zs_gemm_ln_f32(int M, int N, int K, const float* x, int ldx, const float* ln_w,
+                              const float* ln_b, float eps, const float* W, int ldw,
+                              const float* bias, const float* residual, int ldr, float* out,
+                              int ldo, int act, void* stream) {
+  ZS_REQUIRE(M > 0 && M <= RG_MAX_M && N > 0 && K > 0,
+             "zs_gemm_ln_f32: M in 1..%d (got M=%d N=%d K=%d)", RG_MAX_M, M, N, K);
+  ZS_REQUIRE(x && W && out && ln_w && ln_b, "zs_gemm_ln_f32: null pointer");
+  ZS_REQUIRE(ldx % 4 == 0 && ldw % 4 == 0 && ((uintptr_t)x & 15) == 0 && ((uintptr_t)W & 15) == 0 &&
+             ((uintptr_t)ln_w & 15) == 0 && ((uintptr_t)ln_b & 15) == 0,
+             "zs_gemm_ln_f32: x / W / LN params must be 16-byte aligned, ldx / ldw multiples of 4");
+  ZS_REQUIRE(K == 768 || K == 1024, "zs_gemm_ln_f32: unsupported K=%d (768 or 1024)", K);
+  RowsArgs g{};
+  g.M = M; g.N = N; g.K = K; g.X = x; g.ldx = ldx; g.ln_w = ln_w; g.ln_b = ln_b; g.eps = eps;
+  g.Wf = W; g.ldw = ldw; g.bias = bias; g.residual = residual; g.ldr = ldr;
+  g.out = out; g.ldo = ldo; g.out_dtype = ZS_F32; g.act = act;
+  return launch_rows_f32(g, true, S(stream));
 }

@@ -40,6 +40,7 @@ SIGNATURES = {
     "zs_gemm": [I, I, I, I, P, I, P, I, P, P, I, P, I, I, I, I, P, P],
     "zs_gemm_workspace_floats": [I, I, I],
     "zs_gemm_ln": [I, I, I, P, I, P, P, F, P, I, P, P, I, P, I, I, I, P],
+    "zs_gemm_ln_f32": [I, I, I, P, I, P, P, F, P, I, P, P, I, P, I, I, P],
     "zs_l2norm_rows": [P, I, I, F, P, P],
     "zs_window_attention": [P, I, I, I, I, I, I, I, P, P, I, P],
     "zs_swin_block": [P, I, I, I, I, I, I, P, P, P, P, P, P, P, P, P, P, P, P, P, P],

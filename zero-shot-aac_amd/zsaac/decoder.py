@@ -247,6 +247,8 @@ class Gpt2Decoder:
         # its 48 workgroups each stream a head's 295 KB of weights plus 16 rows of KV cache, and
         # one CU moves far less than the 288 + 192 workgroups of the pair)
         self.fused_qkv_attn = False
+        # f32 decode on the f32 row-group kernels (zs_gemm_ln_f32); 0 = layernorm + skinny GEMMs
+        self.rows_f32 = os.environ.get("ZSAAC_ROWS_F32", "1") != "0"
         dev = w.wte.device
         self.dev = dev
         self.R = max_rows
@@ -339,6 +341,18 @@ class Gpt2Decoder:
                 ops.gemm(att, ly["proj_w"], x, bias=ly["proj_b"], residual=x, workspace=self.ws)
                 ops.gemm_ln(x, *ly["ln2_gemm"], ly["fc_w"], hid, bias=ly["fc_b"], act=ops.ACT_GELU_TANH)
                 ops.gemm(hid, ly["mproj_w"], x, bias=ly["mproj_b"], residual=x, workspace=self.ws)
+            return
+        if self.dtype == torch.float32 and M <= 64 and self.rows_f32:
+            # the f32 parity mode's decode: ln_1 / ln_2 fused into f32 row-group GEMMs
+            # (zs_gemm_ln_f32; the affine applied in f32, exact f32 products), f32 row-group
+            # kernels for the projections (zs_gemm auto mode)
+            for l, ly in enumerate(self.w.layers):
+                qkv, att, hid = self.qkv[:M], self.att[:M], self.hid[:M]
+                ops.gemm_ln_f32(x, *ly["ln1"], ly["attn_w"], qkv, bias=ly["attn_b"])
+                attn_fn(l, qkv, att)
+                ops.gemm(att, ly["proj_w"], x, bias=ly["proj_b"], residual=x)
+                ops.gemm_ln_f32(x, *ly["ln2"], ly["fc_w"], hid, bias=ly["fc_b"], act=ops.ACT_GELU_TANH)
+                ops.gemm(hid, ly["mproj_w"], x, bias=ly["mproj_b"], residual=x)
             return
         for l, ly in enumerate(self.w.layers):
             h, qkv, att, hid = self.h[:M], self.qkv[:M], self.att[:M], self.hid[:M]
