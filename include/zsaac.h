@@ -352,16 +352,6 @@ int zs_kv_write(const void* qkv, int R, int n, int D, int heads, const int* pos0
 int zs_decode_attention(const void* qkv, int R, int D, int heads, void* kc, void* vc, int Lmax,
                         const int* pos, const int* kvrow, void* out, int dtype, void* stream);
 
-/* zs_decode_qkv_attention: the attention half of one GPT-2 decode step for R <= 64 rows (bf16),
- * fused: ln_1 (eps) of the f32 rows x [R][768] -> c_attn (w_qkv bf16 [2304][768] out x in, rows
- * q | k | v; b_qkv f32) -> each row's new k, v appended to the caches kc / vc
- * [R][12][Lmax][64] at pos[r] -> attention of q over keys 0..pos[r] -> out [R][768] bf16.
- * Replaces zs_gemm_ln (c_attn) + zs_decode_attention of transformers' GPT2Block with a KV cache
- * (GPT2Attention, scale 1/8); same bf16 roundings of q, k, v.  No kvrow (greedy decode). */
-int zs_decode_qkv_attention(int R, const float* x, const float* ln_w, const float* ln_b, float eps,
-                            const void* w_qkv, const float* b_qkv, void* kc, void* vc, int Lmax,
-                            const int* pos, void* out, void* stream);
-
 /* zs_decode_attention_map: zs_decode_attention over a compacted row set (bf16, no kvrow):
  * qkv/out rows are compact slots c in [0, R); the physical decode row of slot c is rowmap[c]
  * (the cache is indexed physically).  The position of slot c is cpos[c] when cpos != NULL (as

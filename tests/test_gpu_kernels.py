@@ -414,57 +414,6 @@ def _decode_attention_bf16_body(cuda, use_kvrow, variant, R, D, H, Lmax):
         assert torch.equal(vc[r, :, p], qkv[r, 2 * D:].view(H, 64))
 
 
-@pytest.mark.parametrize("R", [1, 20, 64])
-def test_decode_qkv_attention(cuda, R):
-    """zs_decode_qkv_attention (ln_1 + c_attn + KV append + attention in one launch) against a
-    torch fp32 reference of the same bf16 roundings, and against the unfused zs_gemm_ln ->
-    zs_decode_attention pair: ragged positions, position 0 and Lmax - 1 included."""
-    from zsaac import ops
-    D, H, Lmax = 768, 12, 103
-    g = torch.Generator(device="cuda").manual_seed(R + 5)
-    x = torch.randn(R, D, device=cuda, generator=g) * 2 + 0.3
-    x[:, 7] += 30.0
-    lw = torch.randn(D, device=cuda, generator=g) * 0.2 + 1
-    lb = torch.randn(D, device=cuda, generator=g) * 0.1
-    w = torch.randn(3 * D, D, device=cuda, generator=g).div(math.sqrt(D)).bfloat16()
-    b = torch.randn(3 * D, device=cuda, generator=g) * 0.1
-    kc0 = torch.randn(R, H, Lmax, 64, device=cuda, generator=g).bfloat16()
-    vc0 = torch.randn(R, H, Lmax, 64, device=cuda, generator=g).bfloat16()
-    pos = torch.randint(0, Lmax, (R,), device=cuda, generator=g, dtype=torch.int32)
-    pos[0] = 0
-    if R > 1:
-        pos[1] = Lmax - 1
-    kc, vc = kc0.clone(), vc0.clone()
-    out = torch.empty(R, D, device=cuda, dtype=torch.bfloat16)
-    ops.decode_qkv_attention(x, lw, lb, w, b, kc, vc, Lmax, pos, out)
-    # unfused pair
-    kc2, vc2 = kc0.clone(), vc0.clone()
-    qkv = torch.empty(R, 3 * D, device=cuda, dtype=torch.bfloat16)
-    ops.gemm_ln(x, lw, lb, w, qkv, bias=b)
-    out2 = torch.empty_like(out)
-    ops.decode_attention(qkv, R, D, H, kc2, vc2, Lmax, pos, out2)
-    assert _rel(out, out2) < 2e-2
-    # fp32 reference of the same roundings
-    h = torch.nn.functional.layer_norm(x, (D,), lw, lb, 1e-5).bfloat16().float()
-    qf = (h @ w.float().t() + b).bfloat16().float()
-    for r in range(R):
-        p = int(pos[r])
-        for hh in range(H):
-            sl = slice(64 * hh, 64 * hh + 64)
-            K = torch.cat([kc0[r, hh, :p].float(), qf[r, D:][sl][None]])
-            V = torch.cat([vc0[r, hh, :p].float(), qf[r, 2 * D:][sl][None]])
-            att = torch.softmax(K @ (qf[r, sl] * 0.125), 0) @ V
-            got = out[r, sl].float()
-            assert float((got - att).abs().max()) < 2e-2 * float(att.abs().max()) + 1e-2, (r, hh, p)
-        # the new token's k / v landed at pos (bf16 of the same f32 value, up to summation order)
-        assert float((kc[r, :, p].float() - qf[r, D:2 * D].view(H, 64)).abs().max()) <= \
-            2 ** -7 * float(qf[r, D:2 * D].abs().max())
-        assert float((vc[r, :, p].float() - qf[r, 2 * D:].view(H, 64)).abs().max()) <= \
-            2 ** -7 * float(qf[r, 2 * D:].abs().max())
-        keep = torch.ones(Lmax, dtype=torch.bool, device=cuda)
-        keep[p] = False
-        assert torch.equal(kc[r][:, keep], kc0[r][:, keep]) and torch.equal(vc[r][:, keep], vc0[r][:, keep])
-
 
 def test_decode_attention_dpp_bitwise(cuda):
     """Variant 6 (DPP in-group reductions) performs the same additions in the same order as

@@ -33,7 +33,7 @@ def main():
         ns = call("zs_fp8_splits", K)
         out = torch.empty(ns * M * N, device=dev)
         res = []
-        for knob, val in (("fp8_tile", 0), ("fp8_stream_w4", 1), ("fp8_tile", 2), ("fp8_tile", 3)):
+        for knob, val in (("fp8_tile", 0), ("fp8_tile", 2), ("fp8_tile", 3)):
             lib().zs_tune_set(knob.encode(), val)
 
             def launch(i):

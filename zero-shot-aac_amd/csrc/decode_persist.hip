@@ -526,7 +526,7 @@ __device__ __forceinline__ void phase_proj(const Args& a, const Rs& rs, __amdgpu
                                            int K, const float* bias, char* smem, int w,
                                            const bf16x8_t (&wb)[S]) {
   float* red = reinterpret_cast<float*>(smem);
-  const int tid = otid(), lane = tid & 63, v = tid >> 6, fr = lane & 15, fk = 8 * (lane >> 4);
+  const int tid = otid(), lane = tid & 63, v = tid >> 6;
   // epilogue operands first: 64 rows x 4 quads on threads 0..255
   const int erow = (tid >> 2) & 63, ec = 16 * w + 4 * (tid & 3);
   float4 eb = make_float4(0.f, 0.f, 0.f, 0.f), ex = eb;

@@ -256,8 +256,6 @@ extern int g_rows_nt48;     // gemm_rows.hip
 extern int g_fp8_tile;      // mistral.hip
 extern int g_rows_wide;     // gemm_rows.hip
 extern int g_fp8_dbg;       // mistral.hip
-extern int g_mis_attn_split;  // mistral.hip
-extern int g_fp8_stream_w4;   // mistral.hip
 extern int g_attn_split;    // attn.hip
 extern int g_small_attn;    // attn.hip
 
@@ -304,8 +302,6 @@ extern "C" int zs_tune_set(const char* key, int value) {
   if (!strcmp(key, "fp8_tile")) { g_fp8_tile = value; return 0; }
   if (!strcmp(key, "rows_wide")) { g_rows_wide = value; return 0; }
   if (!strcmp(key, "fp8_dbg")) { g_fp8_dbg = value; return 0; }
-  if (!strcmp(key, "mis_attn_split")) { g_mis_attn_split = value; return 0; }
-  if (!strcmp(key, "fp8_stream_w4")) { g_fp8_stream_w4 = value; return 0; }
   if (!strcmp(key, "attn_split")) { g_attn_split = value; return 0; }
   if (!strcmp(key, "small_attn")) { g_small_attn = value; return 0; }
   return fail(ZS_ERR_ARG, "zs_tune_set: unknown key %s", key);

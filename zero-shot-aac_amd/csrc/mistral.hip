@@ -28,9 +28,6 @@ int g_fp8_tile = 0;   // zs_tune_set("fp8_tile", v) A/B knob: 1 = 64-column one-
                       // one-shot tiles where the stream kernel does not apply, 4 = 64-column
                       // one-shot tiles below 256 workgroups at M <= 32 (the earlier rule)
 int g_fp8_dbg = 0;    // zs_tune_set("fp8_dbg", b): ablations (1 no A loads, 2 no MFMA, 4 no W loads)
-int g_fp8_stream_w4 = 0;    // zs_tune_set("fp8_stream_w4", 1): 4-wave stream workgroups, 2 per
-                            // CU (A/B: gate|up 28.2 vs 27.7 us, step 3.16 vs 3.07 ms -- off)
-int g_mis_attn_split = 1;   // zs_tune_set("mis_attn_split", 2): keys over two waves (A/B: 3.28 vs 3.21 ms)
 
 constexpr int F8_KC = 1024;   // k per workgroup (one split)
 constexpr int F8_MAXM = 64;
@@ -271,7 +268,7 @@ __device__ __forceinline__ void f8s_compute(const F8Item& b, const bf16_t* as, i
 // every load in flight).  The last workgroup's run is clamped to the final item: it recomputes
 // and rewrites identical values.
 template <int WAVES, int PER>
-__global__ __launch_bounds__(64 * WAVES, WAVES == 4 ? 2 : 1) void fp8_gemm_stream_kernel(
+__global__ __launch_bounds__(64 * WAVES) void fp8_gemm_stream_kernel(
     const bf16_t* __restrict__ A, int lda, const uint8_t* __restrict__ W8,
     const float* __restrict__ scale, int M, int N, int K, float* __restrict__ out,
     long split_stride, int ldo, int ntiles) {
@@ -569,18 +566,15 @@ __global__ __launch_bounds__(256) void mistral_attn_kernel(const T* __restrict__
 // keys 0..p-1 from the caches as mistral_attn_kernel does and key p = pos[m] from registers; the
 // first q head of each kv head (group 0 lanes) writes k / v row p to the caches for later steps.
 // Same sums, rotation and softmax arithmetic as mistral_rope_kv_kernel + mistral_attn_kernel.
-// SPLIT = 2: each (row, head)'s cached keys over two waves (32-key steps s, s + 2, ...), merged
-// through LDS in slice order (needs M H SPLIT % 4 == 0: no wave leaves before the barrier).
-template <typename T, int SPLIT = 1>
+template <typename T>
 __global__ __launch_bounds__(256) void mistral_decode_attn_kernel(
     const float* __restrict__ qkv, int nsplit, long ss, int M, int H, int KVH,
     const int* __restrict__ pos, const float* __restrict__ cosb, const float* __restrict__ sinb,
     T* __restrict__ kc, T* __restrict__ vc, int Lmax, T* __restrict__ out) {
   constexpr int HD = 128, HALF = 64, DPL = 16, U = 4;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int w = (blockIdx.x * 4 + wid) / SPLIT, slice = wid % SPLIT;
-  __shared__ float merge[SPLIT == 1 ? 1 : 4][HD + 2];
-  if (SPLIT == 1 && w >= M * H) return;
+  const int w = blockIdx.x * 4 + wid;
+  if (w >= M * H) return;
   const int grp = lane >> 3, sub = lane & 7;
   const int m = w / H, h = w % H, kvh = h / (H / KVH);
   const int p = __builtin_amdgcn_readfirstlane(pos[m]);
@@ -610,7 +604,7 @@ __global__ __launch_bounds__(256) void mistral_decode_attn_kernel(
     }
   }
   const long base = ((long)m * KVH + kvh) * Lmax;
-  if (h % (H / KVH) == 0 && grp == 0 && slice == 0) {
+  if (h % (H / KVH) == 0 && grp == 0) {
     T* kr = kc + (base + p) * HD + sub * DPL;
     T* vr = vc + (base + p) * HD + sub * DPL;
 #pragma unroll
@@ -643,7 +637,7 @@ __global__ __launch_bounds__(256) void mistral_decode_attn_kernel(
     for (int d = 0; d < DPL; ++d) o[d] = o[d] * corr + e * vf[d];
     mx = mn;
   };
-  for (int j0 = slice * 8 * U; j0 < p; j0 += 8 * U * SPLIT) {
+  for (int j0 = 0; j0 < p; j0 += 8 * U) {
     float kf[U][DPL], vf[U][DPL];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -664,7 +658,7 @@ __global__ __launch_bounds__(256) void mistral_decode_attn_kernel(
       update((j0 + 8 * u + grp < p) ? sv * scale : -INFINITY, vf[u]);
     }
   }
-  if (slice == 0) {                                              // key p (group 0 counts it)
+  {                                                              // key p (group 0 counts it)
     float sv = 0.f;
 #pragma unroll
     for (int d = 0; d < DPL; ++d) sv += qv[d] * kn[d];
@@ -678,36 +672,6 @@ __global__ __launch_bounds__(256) void mistral_decode_attn_kernel(
     l += __shfl_xor(l, x, 64);
 #pragma unroll
     for (int d = 0; d < DPL; ++d) o[d] += __shfl_xor(o[d], x, 64);
-  }
-  if constexpr (SPLIT > 1) {
-    if (slice != 0 && grp == 0) {
-#pragma unroll
-      for (int d = 0; d < DPL; ++d) merge[wid][sub * DPL + d] = o[d];
-      if (sub == 0) { merge[wid][HD] = mx; merge[wid][HD + 1] = l; }
-    }
-    __syncthreads();
-    if (slice != 0) return;
-    float mm = mx;
-#pragma unroll
-    for (int u = 1; u < SPLIT; ++u) mm = fmaxf(mm, merge[wid + u][HD]);
-    float a0;
-    if constexpr (sizeof(T) == 4) a0 = expf(mx - mm);
-    else a0 = __expf(mx - mm);
-    l *= a0;
-#pragma unroll
-    for (int d = 0; d < DPL; ++d) o[d] *= a0;
-#pragma unroll
-    for (int u = 1; u < SPLIT; ++u) {
-      const float mu = merge[wid + u][HD];
-      float au = 0.f;
-      if (mu != -INFINITY) {
-        if constexpr (sizeof(T) == 4) au = expf(mu - mm);
-        else au = __expf(mu - mm);
-      }
-      l += merge[wid + u][HD + 1] * au;
-#pragma unroll
-      for (int d = 0; d < DPL; ++d) o[d] += merge[wid + u][sub * DPL + d] * au;
-    }
   }
   if (grp == 0) {
     const float inv = 1.0f / l;
@@ -759,27 +723,18 @@ extern "C" int zs_fp8_gemm_rows(const void* A, int lda, const void* W8, const fl
   }
   const long items = (long)cdiv(N, 128) * splits;
   if (M <= 32 && (g_fp8_tile == 0 || g_fp8_tile == 4) && items > ncu && items <= 8L * ncu) {
-    const bool w4 = g_fp8_stream_w4 && N % 64 == 0;   // 64-column items, 2 workgroups per CU
-    const long its = w4 ? (long)(N / 64) * splits : items, slots = w4 ? 2L * ncu : ncu;
+    const long its = items, slots = ncu;
     const long per = (its + slots - 1) / slots;
 #define F8S(W_, P_)                                                                             \
   hipLaunchKernelGGL((fp8_gemm_stream_kernel<W_, P_>), dim3((unsigned)((its + P_ - 1) / P_)),   \
                      dim3(64 * W_), (size_t)32 * (F8_KC + 8) * 2, st, (const bf16_t*)A, lda,   \
                      (const uint8_t*)W8, scale, M, N, K, out, split_stride, ldo,               \
-                     W_ == 8 ? cdiv(N, 128) : N / 64)
-    if (w4) {
-      if (per <= 2) F8S(4, 2);
-      else if (per <= 3) F8S(4, 3);
-      else if (per <= 4) F8S(4, 4);
-      else if (per <= 6) F8S(4, 6);
-      else F8S(4, 8);
-    } else {
-      if (per <= 2) F8S(8, 2);
-      else if (per <= 3) F8S(8, 3);
-      else if (per <= 4) F8S(8, 4);
-      else if (per <= 6) F8S(8, 6);
-      else F8S(8, 8);
-    }
+                     cdiv(N, 128))
+    if (per <= 2) F8S(8, 2);
+    else if (per <= 3) F8S(8, 3);
+    else if (per <= 4) F8S(8, 4);
+    else if (per <= 6) F8S(8, 6);
+    else F8S(8, 8);
 #undef F8S
   } else if ((long)cdiv(N, 256) * splits >= 256 && g_fp8_tile != 1) F8L(2, 8);
   // 128-column tiles also at M <= 32 with >= 128 workgroups (q|k|v at 192: 11.1 -> 9.8 us)
@@ -913,11 +868,7 @@ extern "C" int zs_mistral_decode_attention(const float* qkv, int nsplit, long ss
                  ((uintptr_t)vc & 15) == 0 && ((uintptr_t)out & 15) == 0,
              "zs_mistral_decode_attention: 16-byte aligned buffers, split stride %% 4");
   const dim3 grid(cdiv((long)M * H, 4));
-  if (dtype == ZS_BF16 && g_mis_attn_split == 2 && ((long)M * H * 2) % 4 == 0)
-    hipLaunchKernelGGL((mistral_decode_attn_kernel<bf16_t, 2>), dim3(cdiv((long)M * H * 2, 4)),
-                       dim3(256), 0, S(stream), qkv, nsplit, ss, M, H, KVH, pos, cosb, sinb,
-                       (bf16_t*)kc, (bf16_t*)vc, Lmax, (bf16_t*)out);
-  else if (dtype == ZS_BF16)
+  if (dtype == ZS_BF16)
     hipLaunchKernelGGL(mistral_decode_attn_kernel<bf16_t>, grid, dim3(256), 0, S(stream), qkv,
                        nsplit, ss, M, H, KVH, pos, cosb, sinb, (bf16_t*)kc, (bf16_t*)vc, Lmax,
                        (bf16_t*)out);

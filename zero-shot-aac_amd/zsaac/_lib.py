@@ -57,7 +57,6 @@ SIGNATURES = {
     "zs_gpt2_prefill_embed": [P, P, I, P, I, I, P, P, I, I, I, P, P, P, P, I, P],
     "zs_kv_write": [P, I, I, I, I, P, I, P, P, I, I, P],
     "zs_decode_attention": [P, I, I, I, P, P, I, P, P, P, I, P],
-    "zs_decode_qkv_attention": [I, P, P, P, F, P, P, P, P, I, P, P, P],
     "zs_embed_tokens": [P, P, P, P, I, I, P, I, P],
     "zs_embed_tokens_map": [P, P, P, I, P, P, I, I, P, P, I, P],
     "zs_decode_attention_map": [P, I, P, I, I, I, P, P, I, P, P, P, I, P],

@@ -242,11 +242,6 @@ class Gpt2Decoder:
             cands = [c for c in range(4, 13) if n % c == 0]
             chunk = min(cands, key=lambda c: abs(c - 6)) if cands else 6
         self.w, self.dtype = w, w.dtype
-        # greedy bf16 decode at <= 64 rows through zs_decode_qkv_attention: off (measured 23.5 us
-        # per launch against 9.1 + 8.0 us for the zs_gemm_ln + decode attention pair it fuses:
-        # its 48 workgroups each stream a head's 295 KB of weights plus 16 rows of KV cache, and
-        # one CU moves far less than the 288 + 192 workgroups of the pair)
-        self.fused_qkv_attn = False
         # f32 decode on the f32 row-group kernels (zs_gemm_ln_f32); 0 = layernorm + skinny GEMMs
         self.rows_f32 = os.environ.get("ZSAAC_ROWS_F32", "1") != "0"
         dev = w.wte.device
@@ -325,19 +320,15 @@ class Gpt2Decoder:
                                              for N, K in ((3 * D, D), (D, D), (4 * D, D), (D, 4 * D))])
 
     # ---------------------------------------------------------------- blocks
-    def _layers(self, M, attn_fn, qkv_attn_fn=None):
+    def _layers(self, M, attn_fn):
         x = self.x[:M]
         if self.dtype == torch.bfloat16 and M <= 64:
             # decode at the reference's eval batch: LayerNorm fused into the c_attn / c_fc
-            # launches (zs_gemm_ln), row-group GEMMs for the projections (5 launches per block);
-            # greedy decode fuses ln_1 + c_attn + KV append + attention (qkv_attn_fn: 4 launches)
+            # launches (zs_gemm_ln), row-group GEMMs for the projections (5 launches per block)
             for l, ly in enumerate(self.w.layers):
                 qkv, att, hid = self.qkv[:M], self.att[:M], self.hid[:M]
-                if qkv_attn_fn is not None:
-                    qkv_attn_fn(l, ly, x, att)
-                else:
-                    ops.gemm_ln(x, *ly["ln1_gemm"], ly["attn_w"], qkv, bias=ly["attn_b"])
-                    attn_fn(l, qkv, att)
+                ops.gemm_ln(x, *ly["ln1_gemm"], ly["attn_w"], qkv, bias=ly["attn_b"])
+                attn_fn(l, qkv, att)
                 ops.gemm(att, ly["proj_w"], x, bias=ly["proj_b"], residual=x, workspace=self.ws)
                 ops.gemm_ln(x, *ly["ln2_gemm"], ly["fc_w"], hid, bias=ly["fc_b"], act=ops.ACT_GELU_TANH)
                 ops.gemm(hid, ly["mproj_w"], x, bias=ly["mproj_b"], residual=x, workspace=self.ws)
@@ -385,12 +376,7 @@ class Gpt2Decoder:
             ops.decode_attention(qkv, R, D, NH, self.kc[l], self.vc[l], self.Lmax, self.pos[:R],
                                  att, kvrow=kvrow)
 
-        def qkv_attn(l, ly, x, att):
-            ops.decode_qkv_attention(x, *ly["ln1"], ly["attn_w"], ly["attn_b"], self.kc[l],
-                                     self.vc[l], self.Lmax, self.pos[:R], att)
-
-        fused = kvrow is None and self.fused_qkv_attn
-        self._layers(R, attn, qkv_attn if fused else None)
+        self._layers(R, attn)
         ops.layernorm(self.x[:R], *self.w.lnf, out=self.hf[:R])
 
     def _decode_forward_c(self, R, Rb):

@@ -316,18 +316,6 @@ def label_topk(emb, labels, k, rows, idx=None):
     return rows
 
 
-def decode_qkv_attention(x, ln_w, ln_b, w_qkv, b_qkv, kc, vc, Lmax, pos, out, eps=1e-5):
-    """ln_1 -> c_attn -> KV append -> decode attention for R <= 64 rows in one launch
-    (zs_decode_qkv_attention): x [R, 768] f32, w_qkv [2304, 768] bf16, caches [R, 12, Lmax, 64]
-    bf16, out [R, 768] bf16."""
-    R = x.shape[0]
-    _need(x.dtype == torch.float32 and w_qkv.dtype == torch.bfloat16 and kc.dtype == torch.bfloat16,
-          "decode_qkv_attention: dtypes")
-    call("zs_decode_qkv_attention", R, _p(x), _p(ln_w), _p(ln_b), float(eps), _p(w_qkv), _p(b_qkv),
-         _p(kc), _p(vc), Lmax, _p(pos), _p(out), _s())
-    return out
-
-
 def dedicated_streams(n: int, device) -> list:
     """n new HIP streams bound to distinct hardware queues (zs_stream_create), as torch streams.
     torch's pooled streams get their hardware queue at first use, so concurrent batch streams
