@@ -415,6 +415,41 @@ def _decode_attention_bf16_body(cuda, use_kvrow, variant, R, D, H, Lmax):
 
 
 
+@pytest.mark.parametrize("use_kvrow", [False, True])
+def test_decode_attention_f32(cuda, use_kvrow):
+    """f32 decode attention (the f32 parity mode's two-wave decode_attn6<float> at R <= 128) vs
+    a float64 torch reference: ragged positions 0..Lmax-1, optional beam kvrow indirection, the
+    new token's k/v appended; |err| <= 1e-5 * max|ref| + 1e-6."""
+    from zsaac import ops
+    R, D, H, Lmax = 40, 768, 12, 103
+    g = torch.Generator(device="cuda").manual_seed(12)
+    kc = torch.randn(R, H, Lmax, 64, device=cuda, generator=g)
+    vc = torch.randn(R, H, Lmax, 64, device=cuda, generator=g)
+    if use_kvrow:
+        pos = torch.full((R,), 57, device=cuda, dtype=torch.int32)
+        kvrow = torch.randint(0, R, (R, Lmax), device=cuda, generator=g, dtype=torch.int32)
+    else:
+        pos = torch.randint(0, Lmax, (R,), device=cuda, generator=g, dtype=torch.int32)
+        pos[0], pos[1] = 0, Lmax - 1
+        kvrow = None
+    qkv = torch.randn(R, 3 * D, device=cuda, generator=g)
+    k0, v0 = kc.double().clone(), vc.double().clone()
+    out = torch.empty(R, D, device=cuda)
+    ops.decode_attention(qkv, R, D, H, kc, vc, Lmax, pos, out, kvrow=kvrow)
+    qf = qkv.double()
+    for r in range(R):
+        p = int(pos[r])
+        src = kvrow[r, :p].long() if use_kvrow else torch.full((p,), r, device=cuda, dtype=torch.long)
+        for h in range(H):
+            K = torch.cat([k0[src, h, torch.arange(p, device=cuda)], qf[r, D + 64 * h:D + 64 * h + 64][None]])
+            V = torch.cat([v0[src, h, torch.arange(p, device=cuda)], qf[r, 2 * D + 64 * h:2 * D + 64 * h + 64][None]])
+            ref = torch.softmax(K @ (qf[r, 64 * h:64 * h + 64] * 0.125), 0) @ V
+            got = out[r, 64 * h:64 * h + 64].double()
+            assert float((got - ref).abs().max()) <= 1e-5 * float(ref.abs().max()) + 1e-6, (r, h, p)
+        assert torch.equal(kc[r, :, p], qkv[r, D:2 * D].view(H, 64))
+        assert torch.equal(vc[r, :, p], qkv[r, 2 * D:].view(H, 64))
+
+
 def test_decode_attention_dpp_bitwise(cuda):
     """Variant 6 (DPP in-group reductions) performs the same additions in the same order as
     variant 4 (ds_bpermute shuffles): outputs are bitwise equal."""

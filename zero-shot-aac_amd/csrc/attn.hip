@@ -634,6 +634,45 @@ __device__ __forceinline__ uint4 bf8_pack(const float (&f)[8]) {
                     pk2bf(f[6], f[7]));
 }
 
+// 8 consecutive elements of a head row as one register packet: one uint4 of bf16, or two of f32
+// (the f32 parity mode), with the same unpack / select / pack interface
+template <typename T> struct Pk8;
+template <> struct Pk8<bf16_t> {
+  uint4 u;
+  __device__ static Pk8 ld(const bf16_t* p) { return {*reinterpret_cast<const uint4*>(p)}; }
+  __device__ void st(bf16_t* p) const { *reinterpret_cast<uint4*>(p) = u; }
+  __device__ void unpack(float (&f)[8]) const { bf8_unpack(u, f); }
+  __device__ static Pk8 sel(bool c, const Pk8& a, const Pk8& b) { return {sel_u4(c, a.u, b.u)}; }
+  __device__ static Pk8 zero() { return {make_uint4(0, 0, 0, 0)}; }
+  __device__ static Pk8 pack(const float (&f)[8]) { return {bf8_pack(f)}; }
+};
+template <> struct Pk8<float> {
+  uint4 lo, hi;
+  __device__ static Pk8 ld(const float* p) {
+    return {*reinterpret_cast<const uint4*>(p), *reinterpret_cast<const uint4*>(p + 4)};
+  }
+  __device__ void st(float* p) const {
+    *reinterpret_cast<uint4*>(p) = lo;
+    *reinterpret_cast<uint4*>(p + 4) = hi;
+  }
+  __device__ void unpack(float (&f)[8]) const {
+    f[0] = __uint_as_float(lo.x); f[1] = __uint_as_float(lo.y);
+    f[2] = __uint_as_float(lo.z); f[3] = __uint_as_float(lo.w);
+    f[4] = __uint_as_float(hi.x); f[5] = __uint_as_float(hi.y);
+    f[6] = __uint_as_float(hi.z); f[7] = __uint_as_float(hi.w);
+  }
+  __device__ static Pk8 sel(bool c, const Pk8& a, const Pk8& b) {
+    return {sel_u4(c, a.lo, b.lo), sel_u4(c, a.hi, b.hi)};
+  }
+  __device__ static Pk8 zero() { return {make_uint4(0, 0, 0, 0), make_uint4(0, 0, 0, 0)}; }
+  __device__ static Pk8 pack(const float (&f)[8]) {
+    return {make_uint4(__float_as_uint(f[0]), __float_as_uint(f[1]), __float_as_uint(f[2]),
+                       __float_as_uint(f[3])),
+            make_uint4(__float_as_uint(f[4]), __float_as_uint(f[5]), __float_as_uint(f[6]),
+                       __float_as_uint(f[7]))};
+  }
+};
+
 // SPLIT = 2 / 4: the keys of one (row, head) are split over SPLIT waves of the workgroup (slice s
 // takes phases s, s + SPLIT, ...; 4 / SPLIT heads per workgroup), whose online-softmax states are
 // merged through LDS at the end: SPLIT times the waves for the bs=64 decode's 768 (row, head)
@@ -644,7 +683,7 @@ __global__ __launch_bounds__(256) void decode_attn6_kernel(
     const T* __restrict__ qkv, int D, int heads, T* __restrict__ kc, T* __restrict__ vc, int Lmax,
     const int* __restrict__ pos, const int* __restrict__ kvrow, T* __restrict__ out,
     const int* __restrict__ rowmap, const int* __restrict__ cpos, int nphys) {
-  static_assert(sizeof(T) == 2, "bf16 only");
+  using V8 = Pk8<T>;
   static_assert(SPLIT == 1 || ((SPLIT == 2 || SPLIT == 4) && !PF), "SPLIT 2 / 4 without prefetch");
   constexpr int HD = 64, EPC = 8, NG = KPP / 8;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -656,12 +695,11 @@ __global__ __launch_bounds__(256) void decode_attn6_kernel(
   const int r = rowmap ? rowmap[c] : c;
   const int p0 = cpos ? cpos[c] : 0;
   const T* row = qkv + (long)c * 3 * D + h * HD + sub * EPC;
-  const uint4 qu = *reinterpret_cast<const uint4*>(row);
-  const uint4 knu = *reinterpret_cast<const uint4*>(row + D);
-  const uint4 vnu = *reinterpret_cast<const uint4*>(row + 2 * D);
+  const V8 qu = V8::ld(row);
+  const V8 knu = V8::ld(row + D);
+  const V8 vnu = V8::ld(row + 2 * D);
   if (r >= nphys) {
-    if (grp == 0)
-      *reinterpret_cast<uint4*>(out + (long)c * D + h * HD + sub * EPC) = make_uint4(0, 0, 0, 0);
+    if (grp == 0) V8::zero().st(out + (long)c * D + h * HD + sub * EPC);
     return;
   }
   // wave-uniform (one (row, head) per wave): scalar branches for the phase loop and prefetch
@@ -671,7 +709,7 @@ __global__ __launch_bounds__(256) void decode_attn6_kernel(
   // token from registers), and a store here would order every cache load after it -- the qkv
   // load, the store and the cache loads became three dependent round trips instead of two
   float q[EPC];
-  bf8_unpack(qu, q);
+  qu.unpack(q);
 #pragma unroll
   for (int t = 0; t < EPC; ++t) q[t] *= 0.125f;
   float m = -INFINITY, sum = 0.f, o[EPC];
@@ -681,7 +719,7 @@ __global__ __launch_bounds__(256) void decode_attn6_kernel(
   // min(j, p - 1), or slot 0 at p == 0) and the key is then chosen by value: cached for j < p,
   // the new token for j == p, zero past it.  (Loads under a divergent `if` were each waited
   // for inside their branch: one round trip per key group instead of one per phase.)
-  uint4 kr[NG], vr[NG], kx[NG], vx[NG];
+  V8 kr[NG], vr[NG], kx[NG], vx[NG];
   // (beam: the kvrow source rows of the whole phase are loaded first, under one uniform branch)
 #define ZS_LOAD_PHASE(BASE, KA, VA)                                                            \
   do {                                                                                         \
@@ -695,8 +733,8 @@ __global__ __launch_bounds__(256) void decode_attn6_kernel(
     }                                                                                          \
     _Pragma("unroll") for (int i = 0; i < NG; ++i) {                                           \
       const long src = ((long)srow[i] * heads + h) * Lmax + jc[i];                             \
-      KA[i] = *reinterpret_cast<const uint4*>(kc + src * HD + sub * EPC);                      \
-      VA[i] = *reinterpret_cast<const uint4*>(vc + src * HD + sub * EPC);                      \
+      KA[i] = V8::ld(kc + src * HD + sub * EPC);                                               \
+      VA[i] = V8::ld(vc + src * HD + sub * EPC);                                               \
     }                                                                                          \
   } while (0)
   if (PF) ZS_LOAD_PHASE(0, kr, vr);
@@ -711,16 +749,16 @@ __global__ __launch_bounds__(256) void decode_attn6_kernel(
 #pragma unroll
     for (int i = 0; i < NG; ++i) {
       const int j = base + i * 8 + grp;
-      const uint4 z = make_uint4(0, 0, 0, 0);
-      kr[i] = sel_u4(j < p, kr[i], sel_u4(j == p, knu, z));
-      vr[i] = sel_u4(j < p, vr[i], sel_u4(j == p, vnu, z));
+      const V8 z = V8::zero();
+      kr[i] = V8::sel(j < p, kr[i], V8::sel(j == p, knu, z));
+      vr[i] = V8::sel(j < p, vr[i], V8::sel(j == p, vnu, z));
     }
     float sc[NG];
     float pm = -INFINITY;
 #pragma unroll
     for (int i = 0; i < NG; ++i) {
       float kf[EPC];
-      bf8_unpack(kr[i], kf);
+      kr[i].unpack(kf);
       float sv = 0.f;
 #pragma unroll
       for (int t = 0; t < EPC; ++t) sv += q[t] * kf[t];
@@ -748,7 +786,7 @@ __global__ __launch_bounds__(256) void decode_attn6_kernel(
       const float e = (base + i * 8 + grp <= p) ? expf(sc[i] - m) : 0.f;
       sum += e;
       float vf[EPC];
-      bf8_unpack(vr[i], vf);
+      vr[i].unpack(vf);
 #pragma unroll
       for (int t = 0; t < EPC; ++t) o[t] += e * vf[t];
     }
@@ -795,9 +833,9 @@ __global__ __launch_bounds__(256) void decode_attn6_kernel(
     float of[EPC];
 #pragma unroll
     for (int t = 0; t < EPC; ++t) of[t] = o[t] * inv;
-    *reinterpret_cast<uint4*>(out + (long)c * D + h * HD + sub * EPC) = bf8_pack(of);
-    *reinterpret_cast<uint4*>(kc + (rh + p) * HD + sub * EPC) = knu;
-    *reinterpret_cast<uint4*>(vc + (rh + p) * HD + sub * EPC) = vnu;
+    V8::pack(of).st(out + (long)c * D + h * HD + sub * EPC);
+    knu.st(kc + (rh + p) * HD + sub * EPC);
+    vnu.st(vc + (rh + p) * HD + sub * EPC);
   }
 }
 
@@ -1055,6 +1093,15 @@ extern "C" int zs_decode_attention(const void* qkv, int R, int D, int heads, voi
              "zs_decode_attention: head_dim must be 64");
   ZS_REQUIRE(Lmax > 0 && Lmax <= 4096, "zs_decode_attention: Lmax");
   dim3 grid(R, heads);
+  if (dtype == ZS_F32 && R <= 128 && g_small_attn && g_attn_split && heads % 2 == 0) {
+    // the f32 parity mode's decode: the bf16 path's two-wave split with 32-key phases
+    hipLaunchKernelGGL((decode_attn6_kernel<float, 32, false, true, 2>), dim3(R, heads / 2),
+                       dim3(256), 0, S(stream), (const float*)qkv, D, heads, (float*)kc,
+                       (float*)vc, Lmax, pos, kvrow, (float*)out, (const int*)nullptr,
+                       (const int*)nullptr, R);
+    ZS_LAUNCH_CHECK();
+    return 0;
+  }
   if (dtype == ZS_BF16 && R <= 128 && g_small_attn && g_attn_split == 4) {
     // each (row, head)'s keys over four waves, 32-key phases (one phase per wave at L <= 128)
     hipLaunchKernelGGL((decode_attn6_kernel<bf16_t, 32, false, true, 4>), dim3(R, heads),
