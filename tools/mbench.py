@@ -350,6 +350,42 @@ def bench_attn():
     print(f"layernorm {R}x768: {t:7.2f}us ({R * 768 * 6 / t / 1e3:5.0f} GB/s)")
 
 
+def bench_attn_beam():
+    """Beam decode attention (C3: 256 clips x beam 5 = 1280 rows, kvrow indirection as
+    generate_beam's reordered caches): the R > 128 variants (decode_attn5 knob) and the small-R
+    kernels with their row cap lifted (small_rmax), GB/s of the K/V bytes read."""
+    from zsaac import ops
+    from zsaac._lib import call
+    dev = torch.device("cuda", 0)
+    R, D, H, Lmax, beam = int(os.environ.get("ZS_M", 1280)), 768, 12, 102, 5
+    kc = torch.randn(R, H, Lmax, 64, device=dev).bfloat16()
+    vc = torch.randn_like(kc)
+    qkv = torch.randn(R, 3 * D, device=dev).bfloat16()
+    out = torch.empty(R, D, device=dev, dtype=torch.bfloat16)
+    # kvrow: each row's keys come from the rows of its own clip (a clip's 5 beams)
+    clip = torch.arange(R, device=dev) // beam
+    kvrow = (clip[:, None] * beam + torch.randint(0, beam, (R, Lmax), device=dev)).int().contiguous()
+    arms = [("v4", {"decode_attn5": 4}), ("v3", {"decode_attn5": 3}), ("v2", {"decode_attn5": 2}),
+            ("v5", {"decode_attn5": 5}), ("v6", {"decode_attn5": 6}),
+            ("small128", {"small_rmax": 4096, "attn_split": 0}),
+            ("small_s1", {"small_rmax": 4096, "attn_split": 1}),
+            ("small_s3", {"small_rmax": 4096, "attn_split": 3})]
+    for L in (30, 60, 90):
+        pos = torch.full((R,), L - 1, device=dev, dtype=torch.int32)
+        byts = R * H * L * 64 * 2 * 2
+        r = {}
+        for name, knobs in arms:
+            for k, v in knobs.items():
+                call("zs_tune_set", k.encode(), v)
+            r[name] = timeit(lambda: ops.decode_attention(qkv, R, D, H, kc, vc, Lmax, pos, out,
+                                                          kvrow=kvrow), reps=20)
+            call("zs_tune_set", b"decode_attn5", 4)
+            call("zs_tune_set", b"small_rmax", 128)
+            call("zs_tune_set", b"attn_split", 3)
+        print(f"beam attn R={R} L={L}: " + "  ".join(
+            f"{n}={t:7.2f}us ({byts / t / 1e3:5.0f} GB/s)" for n, t in r.items()), flush=True)
+
+
 def bench_inflight():
     """End-to-end clips/s vs the number of concurrently decoded bs=64 batches."""
     sys.path.insert(0, ROOT)
@@ -481,4 +517,4 @@ if __name__ == "__main__":
             call("zs_tune_set", k.encode(), int(v))
     which = sys.argv[1:] or ["gemm", "attn"]
     for wname in which:
-        {"gemm": bench_gemm, "rows": bench_rows, "gemm_m": bench_gemm_m, "gemm_htsat": bench_gemm_htsat, "gemm_dbg": bench_gemm_dbg, "lmhead": bench_lmhead, "overhead": bench_overhead, "front": bench_front, "window": bench_window, "decode_gemm": bench_decode_gemm, "attn": bench_attn, "inflight": bench_inflight, "buckets": bench_buckets, "compact_ab": bench_compact_ab, "host": bench_host}[wname]()
+        {"gemm": bench_gemm, "rows": bench_rows, "gemm_m": bench_gemm_m, "gemm_htsat": bench_gemm_htsat, "gemm_dbg": bench_gemm_dbg, "lmhead": bench_lmhead, "overhead": bench_overhead, "front": bench_front, "window": bench_window, "decode_gemm": bench_decode_gemm, "attn": bench_attn, "attn_beam": bench_attn_beam, "inflight": bench_inflight, "buckets": bench_buckets, "compact_ab": bench_compact_ab, "host": bench_host}[wname]()

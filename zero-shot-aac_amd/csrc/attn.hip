@@ -10,6 +10,8 @@
 namespace zs {
 
 int g_small_attn = 1;     // R <= 128: decode_attn6 with 128-key phases
+int g_small_rmax = 128;   // zs_tune_set("small_rmax", r): the row count up to which the small-R
+                          // decode attention kernels are taken
 int g_decode_attn5 = 4;   // 5: decode_attn6 16-key phases + next-phase prefetch; 4/3/2: decode_attn6 (phases of 16/32/64 keys), 1: decode_attn5, 0: LDS
 int g_window_mfma = 1;    // zs_tune_set("window_mfma", 0): VALU window attention for bf16   // zs_tune_set("decode_attn5", 0): LDS-staged decode_attn4 for bf16
 
@@ -1093,7 +1095,7 @@ extern "C" int zs_decode_attention(const void* qkv, int R, int D, int heads, voi
              "zs_decode_attention: head_dim must be 64");
   ZS_REQUIRE(Lmax > 0 && Lmax <= 4096, "zs_decode_attention: Lmax");
   dim3 grid(R, heads);
-  if (dtype == ZS_F32 && R <= 128 && g_small_attn && g_attn_split && heads % 2 == 0) {
+  if (dtype == ZS_F32 && R <= g_small_rmax && g_small_attn && g_attn_split && heads % 2 == 0) {
     // the f32 parity mode's decode: the bf16 path's two-wave split with 32-key phases
     hipLaunchKernelGGL((decode_attn6_kernel<float, 32, false, true, 2>), dim3(R, heads / 2),
                        dim3(256), 0, S(stream), (const float*)qkv, D, heads, (float*)kc,
@@ -1102,7 +1104,7 @@ extern "C" int zs_decode_attention(const void* qkv, int R, int D, int heads, voi
     ZS_LAUNCH_CHECK();
     return 0;
   }
-  if (dtype == ZS_BF16 && R <= 128 && g_small_attn && g_attn_split == 4) {
+  if (dtype == ZS_BF16 && R <= g_small_rmax && g_small_attn && g_attn_split == 4) {
     // each (row, head)'s keys over four waves, 32-key phases (one phase per wave at L <= 128)
     hipLaunchKernelGGL((decode_attn6_kernel<bf16_t, 32, false, true, 4>), dim3(R, heads),
                        dim3(256), 0, S(stream), (const bf16_t*)qkv, D, heads, (bf16_t*)kc,
@@ -1111,7 +1113,7 @@ extern "C" int zs_decode_attention(const void* qkv, int R, int D, int heads, voi
     ZS_LAUNCH_CHECK();
     return 0;
   }
-  if (dtype == ZS_BF16 && R <= 128 && g_small_attn && g_attn_split && heads % 2 == 0) {
+  if (dtype == ZS_BF16 && R <= g_small_rmax && g_small_attn && g_attn_split && heads % 2 == 0) {
     // few waves (R x heads): each (row, head)'s keys over two waves, KPP-key phases (64: all
     // keys of L <= 128 in flight at once, half per wave; 32 (attn_split 3): two phases a wave)
     if (g_attn_split == 3)
@@ -1127,7 +1129,7 @@ extern "C" int zs_decode_attention(const void* qkv, int R, int D, int heads, voi
     ZS_LAUNCH_CHECK();
     return 0;
   }
-  if (dtype == ZS_BF16 && R <= 128 && g_small_attn) {
+  if (dtype == ZS_BF16 && R <= g_small_rmax && g_small_attn) {
     // few waves (R x heads): nothing hides a phase's round trip, so take 128-key phases: every
     // key of a row in flight at once, one HBM round trip at L <= 128
     hipLaunchKernelGGL((decode_attn6_kernel<bf16_t, 128, false, true>), dim3(R, cdiv(heads, 4)),

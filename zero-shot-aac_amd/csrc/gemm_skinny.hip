@@ -258,6 +258,7 @@ extern int g_rows_wide;     // gemm_rows.hip
 extern int g_fp8_dbg;       // mistral.hip
 extern int g_attn_split;    // attn.hip
 extern int g_small_attn;    // attn.hip
+extern int g_small_rmax;    // attn.hip
 
 // choose K per workgroup: a multiple of 64 dividing K, each wave <= 128 deep, ~256-320 WGs
 static int skinny_splits(int N, int K) {
@@ -304,6 +305,7 @@ extern "C" int zs_tune_set(const char* key, int value) {
   if (!strcmp(key, "fp8_dbg")) { g_fp8_dbg = value; return 0; }
   if (!strcmp(key, "attn_split")) { g_attn_split = value; return 0; }
   if (!strcmp(key, "small_attn")) { g_small_attn = value; return 0; }
+  if (!strcmp(key, "small_rmax")) { g_small_rmax = value; return 0; }
   return fail(ZS_ERR_ARG, "zs_tune_set: unknown key %s", key);
 }
 

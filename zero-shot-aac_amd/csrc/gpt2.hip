@@ -307,20 +307,44 @@ __global__ __launch_bounds__(256) void beam_step_kernel(
       Ssum += pstat[((long)prow * nblk + k) * 2 + 1] * expf(bm - M);
     }
     Ssum = wave_sum(Ssum);
-    // top-beam over all blocks' lists: `beam` rounds of wave argmax over list heads
+    // top-beam over all blocks' lists: each lane first keeps the best MB of its own blocks'
+    // candidates in registers (one pass of independent loads, insertion in (value desc, index
+    // asc) order), then `beam` rounds of wave argmax over those lane lists (the rounds no longer
+    // re-read the candidates from memory)
+    float lv[MB];
+    int li[MB];
+#pragma unroll
+    for (int t = 0; t < MB; ++t) { lv[t] = -INFINITY; li[t] = 0x7fffffff; }
+    for (int k = lane; k < nblk; k += 64) {
+      const long base = ((long)prow * nblk + k) * topk;
+      for (int t = 0; t < topk; ++t) {
+        float v = pv[base + t];
+        int ix = pi[base + t];
+#pragma unroll
+        for (int u = 0; u < MB; ++u) {      // bubble (v, ix) into the sorted lane list
+          const bool better = v > lv[u] || (v == lv[u] && ix < li[u]);
+          const float tv = better ? lv[u] : v;
+          const int ti = better ? li[u] : ix;
+          lv[u] = better ? v : lv[u];
+          li[u] = better ? ix : li[u];
+          v = tv;
+          ix = ti;
+        }
+      }
+    }
     float lastv = INFINITY;
     int lasti = -1;
     for (int q = 0; q < beam; ++q) {
       float bv = -INFINITY;
       int bi = 0x7fffffff;
-      for (int k = lane; k < nblk; k += 64)
-        for (int t = 0; t < topk; ++t) {
-          const float v = pv[((long)prow * nblk + k) * topk + t];
-          const int ix = pi[((long)prow * nblk + k) * topk + t];
-          // strictly after the previous pick in (value desc, index asc) order
-          const bool after = v < lastv || (v == lastv && ix > lasti);
-          if (after && (v > bv || (v == bv && ix < bi))) { bv = v; bi = ix; }
-        }
+#pragma unroll
+      for (int t = 0; t < MB; ++t) {
+        const float v = lv[t];
+        const int ix = li[t];
+        // strictly after the previous pick in (value desc, index asc) order
+        const bool after = v < lastv || (v == lastv && ix > lasti);
+        if (after && (v > bv || (v == bv && ix < bi))) { bv = v; bi = ix; }
+      }
       wave_argmax(bv, bi);
       lastv = bv;
       lasti = bi;
