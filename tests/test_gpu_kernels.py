@@ -75,6 +75,37 @@ def test_gemm_lean_tiles(cuda, tile):
         call("zs_tune_set", b"fast_tile", 0)
 
 
+@pytest.mark.parametrize("M,N,K", [(1000, 2304, 768), (333, 770, 3072), (520, 770, 64),
+                                   (300, 260, 128), (2048, 3072, 768), (1280, 768, 3072)])
+def test_gemm_big_tile(cuda, M, N, K):
+    """The 256 x 256 multi-phase LDS-DMA tile (gemm_big_kernel, forced by fast_tile 18) at ragged
+    shapes and K-tile counts 1, 2, 12, 48 (the prologue-only, tail-wait and steady-state counted
+    waits), with bias + gelu and with a residual; five repeats bitwise equal (a staging race shows
+    as run-to-run differences)."""
+    from zsaac import ops
+    from zsaac._lib import call
+    call("zs_tune_set", b"fast_tile", 18)
+    try:
+        g = torch.Generator(device="cuda").manual_seed(M + N + K)
+        a = torch.randn(M, K, device=cuda, generator=g).bfloat16()
+        w = torch.randn(N, K, device=cuda, generator=g).div(math.sqrt(K)).bfloat16()
+        bias = torch.randn(N, device=cuda, generator=g)
+        res = torch.randn(M, N, device=cuda, generator=g)
+        ref = a.float() @ w.float().t() + bias
+        outs = []
+        for _ in range(5):
+            out = torch.empty(M, N, device=cuda, dtype=torch.bfloat16)
+            ops.gemm(a, w, out, bias=bias, act=ops.ACT_GELU_ERF, split_k=1)
+            outs.append(out)
+        assert _rel(outs[0], torch.nn.functional.gelu(ref)) < 1e-2, (M, N, K)
+        assert all(torch.equal(outs[0], o) for o in outs[1:])
+        out = res.clone()
+        ops.gemm(a, w, out, bias=bias, residual=out, split_k=1)
+        assert _rel(out, ref + res) < 1e-2, (M, N, K)
+    finally:
+        call("zs_tune_set", b"fast_tile", 0)
+
+
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("M,N,K", [(64, 2304, 768), (64, 768, 768), (64, 3072, 768), (64, 768, 3072),
                                    (50, 7680, 3840), (3, 1024, 768), (64, 100, 64),

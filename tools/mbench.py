@@ -350,6 +350,35 @@ def bench_attn():
     print(f"layernorm {R}x768: {t:7.2f}us ({R * 768 * 6 / t / 1e3:5.0f} GB/s)")
 
 
+def bench_gemm_big():
+    """bf16 GEMMs of >= 1k rows: the 256 x 256 multi-phase tile (gemm_big) against the lean
+    128 x 128 / 8-wave tiles (gemm_big=0) and torch (hipBLASLt); TFLOP/s."""
+    from zsaac import ops
+    from zsaac._lib import call
+    dev = torch.device("cuda", 0)
+    shapes = [(1600, 2304, 768, "prefill qkv"), (1600, 3072, 768, "prefill fc"),
+              (1280, 3072, 768, "c3 fc"), (1280, 768, 3072, "c3 mproj"),
+              (8192, 3072, 768, "tput fc"), (8192, 768, 3072, "tput mproj"),
+              (8192, 2304, 768, "tput qkv"), (4096, 4096, 4096, "4k"), (8192, 8192, 8192, "8k"),
+              (2048, 3072, 768, "bert fc-ish")]
+    for M, N, K, name in shapes:
+        a = torch.randn(M, K, device=dev).bfloat16()
+        w = (torch.randn(N, K, device=dev) * 0.02).bfloat16()
+        b = torch.randn(N, device=dev)
+        out = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+        fl = 2.0 * M * N * K
+        res = {}
+        for arm, knobs in (("big", {"fast_tile": 18}), ("auto", {}), ("lean", {"gemm_big": 0})):
+            for k, v in knobs.items():
+                call("zs_tune_set", k.encode(), v)
+            res[arm] = timeit(lambda: ops.gemm(a, w, out, bias=b, split_k=1), reps=10)
+            call("zs_tune_set", b"fast_tile", 0)
+            call("zs_tune_set", b"gemm_big", 1)
+        res["torch"] = timeit(lambda: torch.nn.functional.linear(a, w, b.bfloat16()), reps=10)
+        print(f"{name:12s} {M}x{N}x{K}: " + "  ".join(
+            f"{k}={v:8.1f}us ({fl / v / 1e6:6.0f} TF)" for k, v in res.items()), flush=True)
+
+
 def bench_attn_beam():
     """Beam decode attention (C3: 256 clips x beam 5 = 1280 rows, kvrow indirection as
     generate_beam's reordered caches): the R > 128 variants (decode_attn5 knob) and the small-R
@@ -517,4 +546,4 @@ if __name__ == "__main__":
             call("zs_tune_set", k.encode(), int(v))
     which = sys.argv[1:] or ["gemm", "attn"]
     for wname in which:
-        {"gemm": bench_gemm, "rows": bench_rows, "gemm_m": bench_gemm_m, "gemm_htsat": bench_gemm_htsat, "gemm_dbg": bench_gemm_dbg, "lmhead": bench_lmhead, "overhead": bench_overhead, "front": bench_front, "window": bench_window, "decode_gemm": bench_decode_gemm, "attn": bench_attn, "attn_beam": bench_attn_beam, "inflight": bench_inflight, "buckets": bench_buckets, "compact_ab": bench_compact_ab, "host": bench_host}[wname]()
+        {"gemm": bench_gemm, "rows": bench_rows, "gemm_m": bench_gemm_m, "gemm_htsat": bench_gemm_htsat, "gemm_dbg": bench_gemm_dbg, "lmhead": bench_lmhead, "overhead": bench_overhead, "front": bench_front, "window": bench_window, "decode_gemm": bench_decode_gemm, "attn": bench_attn, "attn_beam": bench_attn_beam, "gemm_big": bench_gemm_big, "inflight": bench_inflight, "buckets": bench_buckets, "compact_ab": bench_compact_ab, "host": bench_host}[wname]()

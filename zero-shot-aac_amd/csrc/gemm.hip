@@ -392,6 +392,247 @@ __global__ __launch_bounds__(64 * WGM * WGN, WGM * WGN == 4 ? 2 : 1) void gemm_l
   }
 }
 
+// ------------------------------------------------------------------ 256 x 256 multi-phase tile
+// For GEMMs with >= ~1k rows (prefill, the throughput mode, the beam decode at 1280 rows, the
+// BERT tower, HTSAT stage 4, the Mistral prefill).  One 512-thread workgroup (8 waves as 2 (M) x
+// 4 (N)) per CU owns a 256 x 256 output tile; each wave a 128 x 64 sub-tile as 8 x 4 fragments
+// of v_mfma_f32_16x16x32_bf16 (128 accumulator registers).  K in 64-deep tiles, two LDS buffers
+// of [256 A rows][256 W rows] x 128 B (128 KiB), staged by LDS-DMA (global_load_lds_dwordx4) with
+// the bank swizzle on the source address (FastTile's involution, conflict-free 16-lane reads).
+//
+// A K-tile is computed in FOUR phases, one output quadrant of every wave each (16 MFMAs):
+//   p0 (m0, n0): reads the wave's A rows m0 (4 fragments x 2 k-steps) and W rows n0
+//   p1 (m0, n1): reads W rows n1
+//   p2 (m1, n1): reads A rows m1
+//   p3 (m1, n0): no reads (n0 still in registers)
+// so the LDS rows of a K-tile free up in four SETS as their readers finish (A-m0 + W-n0 after p0,
+// W-n1 after p1, A-m1 after p2), and each set of K-tile t+2 is staged into the same buffer as
+// soon as it is free (p1: A-m0 + W-n0, p2: W-n1, p3: A-m1) — seven phases before it is read.
+// Every phase: counted `s_waitcnt vmcnt` retiring this wave's DMAs of the set(s) read in it
+// (never vmcnt(0) in steady state), ONE raw s_barrier (RAW: every wave's DMAs of the set landed;
+// WAR: every wave's reads of the sets restaged in this phase done — each wave's reads complete
+// before its MFMAs of the previous phase), the phase's reads, the restaging DMAs, the MFMAs at
+// raised priority (cdna_hip_programming.md §5 "Pipelining across barriers", the 256² template).
+namespace big {
+constexpr int BM = 256, BN = 256, BKB = 64, RB = 128, BUF = (BM + BN) * RB;
+__device__ __forceinline__ int swz(int row) { return (row >> 1) & 7; }
+// LDS DMA instruction index (8 rows of 128 B each) of instruction j (0..15) of row set `set`:
+// 0 = A rows m0 of both wave rows, 1 = A rows m1, 2 = W rows n0 of the 4 wave columns, 3 = n1
+__device__ __forceinline__ int set_instr(int set, int j) {
+  if (set < 2) return ((j >> 3) * 128 + set * 64) / 8 + (j & 7);
+  return (BM + (j >> 2) * 64 + (set - 2) * 32) / 8 + (j & 3);
+}
+}  // namespace big
+
+typedef __attribute__((ext_vector_type(4))) float f32x4_t;
+// the wave's 128 x 64 accumulators as 4 slabs of 32 rows ([32][64] f32, 8 KiB of LDS each)
+template <int ACT>
+__device__ __forceinline__ void big_epilogue(const GemmArgs& g, float* slab, int mrw, int nc0,
+                                             bool vec_out, bool vec_res, const float (&bb)[8],
+                                             const f32x4_t (&acc)[8][4]) {
+  const int lane = threadIdx.x & 63, fr = lane & 15, fq = lane >> 4;
+#pragma unroll
+  for (int sl = 0; sl < 4; ++sl) {
+    const int mr0 = mrw + 32 * sl;
+    float4 res[4][2];
+    epi_res_load<64>(g, mr0, nc0, vec_res, res);
+#pragma unroll
+    for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          slab[(16 * ii + 4 * fq + e) * 64 + 16 * j + fr] = acc[2 * sl + ii][j][e];
+    epi_slab<ACT, 64>(g, slab, mr0, nc0, 0, vec_out, vec_res, bb, res);
+  }
+}
+
+__global__ __launch_bounds__(512) void gemm_big_kernel(GemmArgs g) {
+  using namespace big;
+  __shared__ __attribute__((aligned(16))) char lds[2 * BUF];
+  const int ntn = cdiv(g.N, BN), ntm = cdiv(g.M, BM), ntiles = ntn * ntm;
+  int m0, n0;
+  {  // XCD-local grouped tile order (as gemm_lean_kernel)
+    const int b = blockIdx.x, x = b & 7, q8 = ntiles >> 3, r8 = ntiles & 7;
+    const int u = (x < r8 ? x * (q8 + 1) : r8 * (q8 + 1) + (x - r8) * q8) + (b >> 3);
+    const int conc = max(1, min(q8, 32));
+    int gm = (int)(sqrtf((float)conc) + 0.5f);
+    gm = max(1, min(gm, ntm));
+    const int per = gm * ntn, grp = u / per, fm = grp * gm;
+    const int gs = min(ntm - fm, gm), r = u - grp * per;
+    m0 = (fm + r % gs) * BM;
+    n0 = (r / gs) * BN;
+  }
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, wr = wid >> 2, wc = wid & 3;
+  const bf16_t* A = (const bf16_t*)g.A;
+  const bf16_t* W = (const bf16_t*)g.W;
+  // per lane: the source of its 2 DMA instructions in each of the 4 sets, as element offsets
+  // from A / W (rows clamped into the matrices; clamped rows feed only outputs the store guard
+  // drops)
+  int src[4][2];
+#pragma unroll
+  for (int set = 0; set < 4; ++set)
+#pragma unroll
+    for (int jj = 0; jj < 2; ++jj) {
+      const int idx = set_instr(set, wid + 8 * jj);
+      const int row = 8 * idx + (lane >> 3);
+      const int c = 8 * ((lane & 7) ^ swz(row));
+      src[set][jj] = set < 2 ? min(m0 + row, g.M - 1) * g.lda + c
+                             : min(n0 + row - BM, g.N - 1) * g.ldw + c;
+    }
+  auto issue = [&](int set, char* bufp, int k0) {
+#pragma unroll
+    for (int jj = 0; jj < 2; ++jj)
+      __builtin_amdgcn_global_load_lds((gptr_t)((set < 2 ? A : W) + src[set][jj] + k0),
+                                       (lds_ptr_t)(bufp + set_instr(set, wid + 8 * jj) * 1024),
+                                       16, 0, 0);
+  };
+  auto tile_issue = [&](char* bufp, int k0) {  // the steady-state order: A-m0, W-n0, W-n1, A-m1
+    issue(0, bufp, k0); issue(2, bufp, k0); issue(3, bufp, k0); issue(1, bufp, k0);
+  };
+  f32x4_t acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  const int nk = g.K / BKB;
+  tile_issue(lds, 0);
+  if (nk > 1) tile_issue(lds + BUF, BKB);
+  const int fr = lane & 15, fq = lane >> 4;
+  // fragment rows step by 16 (a multiple of the swizzle period 2 x 8 rows): one swizzle per
+  // lane, so a fragment is base + 2048 * i (+ the k-step's chunk), an immediate offset
+  const int arow = wr * 128 + fr, brow = BM + wc * 64 + fr;
+  int aoff[2], boff[2];
+#pragma unroll
+  for (int s2 = 0; s2 < 2; ++s2) {
+    aoff[s2] = arow * RB + 16 * ((4 * s2 + fq) ^ swz(arow));
+    boff[s2] = brow * RB + 16 * ((4 * s2 + fq) ^ swz(brow));
+  }
+  bf16x8_t a[4][2], b0[2][2], b1[2][2];
+#pragma unroll 1
+  for (int t = 0; t < nk; ++t) {
+    char* bufp = lds + (t & 1) * BUF;
+    const bool pf = t + 2 < nk;                  // this K-tile restages its sets with t + 2
+    const int kn = (t + 2) * BKB;
+    // ---- p0 (m0, n0)
+    if (pf || t + 2 == nk) wait_vm<12>(); else wait_vm<4>();
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+        a[i][s2] = *reinterpret_cast<const bf16x8_t*>(bufp + aoff[s2] + 2048 * i);
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+        b0[j][s2] = *reinterpret_cast<const bf16x8_t*>(bufp + boff[s2] + 2048 * j);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][s2], b0[j][s2], acc[i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    // ---- p1 (m0, n1)
+    if (pf || t + 2 == nk) wait_vm<10>(); else wait_vm<2>();
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+        b1[j][s2] = *reinterpret_cast<const bf16x8_t*>(bufp + boff[s2] + 2048 * (2 + j));
+    if (pf) { issue(0, bufp, kn); issue(2, bufp, kn); }
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[i][2 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][s2], b1[j][s2], acc[i][2 + j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    // ---- p2 (m1, n1)
+    if (pf) wait_vm<12>(); else if (t + 2 == nk) wait_vm<8>(); else wait_vm<0>();
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2)
+        a[i][s2] = *reinterpret_cast<const bf16x8_t*>(bufp + aoff[s2] + 2048 * (4 + i));
+    if (pf) issue(3, bufp, kn);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[4 + i][2 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][s2], b1[j][s2], acc[4 + i][2 + j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    // ---- p3 (m1, n0): no reads; restage A-m1 (read in p2)
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (pf) issue(1, bufp, kn);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][s2], b0[j][s2], acc[4 + i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  }
+  wait_vm<0>();
+  __syncthreads();   // the LDS becomes the epilogue's slabs
+  // epilogue: 4 slabs of 32 rows per wave ([32][64] f32, 8 KiB), as gemm_lean_kernel
+  const bool vec_out = g.ldo % 8 == 0 && ((uintptr_t)g.out & 15) == 0;
+  const bool vec_res = g.residual == nullptr || (g.ldr % 4 == 0 && ((uintptr_t)g.residual & 15) == 0);
+  const int nc0 = n0 + wc * 64;
+  float bb[8];
+  {
+    const int n = nc0 + (lane % 8) * 8, nv = min(8, g.N - n);
+    if (g.bias && nv == 8 && ((uintptr_t)(g.bias + n) & 15) == 0) {
+      const float4 c0 = reinterpret_cast<const float4*>(g.bias + n)[0];
+      const float4 c1 = reinterpret_cast<const float4*>(g.bias + n)[1];
+      bb[0] = c0.x; bb[1] = c0.y; bb[2] = c0.z; bb[3] = c0.w;
+      bb[4] = c1.x; bb[5] = c1.y; bb[6] = c1.z; bb[7] = c1.w;
+    } else {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) bb[q] = (g.bias && q < nv) ? g.bias[n + q] : 0.f;
+    }
+  }
+  float* slab = reinterpret_cast<float*>(lds) + wid * 32 * 64;
+  const int mrw = m0 + wr * 128;
+  switch (g.act) {
+    case ACT_GELU_ERF: big_epilogue<ACT_GELU_ERF>(g, slab, mrw, nc0, vec_out, vec_res, bb, acc); break;
+    case ACT_GELU_TANH: big_epilogue<ACT_GELU_TANH>(g, slab, mrw, nc0, vec_out, vec_res, bb, acc); break;
+    case ACT_RELU: big_epilogue<ACT_RELU>(g, slab, mrw, nc0, vec_out, vec_res, bb, acc); break;
+    case ACT_TANH: big_epilogue<ACT_TANH>(g, slab, mrw, nc0, vec_out, vec_res, bb, acc); break;
+    default: big_epilogue<ACT_NONE>(g, slab, mrw, nc0, vec_out, vec_res, bb, acc); break;
+  }
+}
+
+// measured (tools/mbench.py gemm_big, random operands): 1096 TF at 4096^3 and 1252 TF at 8192^3
+// against 909 / 968 for the lean 128 x 128 tiles; at K = 768 (every GPT-2 / HTSAT / BERT shape)
+// and at grids of < 256 tiles the tile's prologue, 128 KiB epilogue and second-round tail cost
+// more than its MFMA efficiency saves (8192 x 3072 x 768: 60 vs 56 us; 1280-1600 rows: 2-4x
+// slower), so it is taken only for long K on a full grid
+int g_gemm_big = 1;    // zs_tune_set("gemm_big", 0): no 256 x 256 multi-phase tiles
+int g_big_min = 256;   // zs_tune_set("big_min", n): 256 x 256 tiles from n tiles up (K >= 2048)
+
+static int launch_big(GemmArgs& g, hipStream_t st) {
+  hipLaunchKernelGGL(gemm_big_kernel, dim3(cdiv(g.N, 256) * cdiv(g.M, 256)), dim3(512), 0, st, g);
+  ZS_LAUNCH_CHECK();
+  return 0;
+}
+
 int g_gemm_lean = 1;   // zs_tune_set("gemm_lean", 0): decode-shaped GEMMs on gemm_fast_kernel
 int g_lean96 = 0;      // zs_tune_set("lean96", 1): 128x96 tiles for the N = 768 projections
                        // (faster alone, but -2 % end to end with the decode groups co-running)
@@ -449,6 +690,9 @@ static int dispatch_fast(GemmArgs& g, hipStream_t st) {
     case 17: return launch_fast<64, 64, 2, 2, 2, 128>(g, st);
     default: break;
   }
+  if ((g_fast_tile == 18 || (g_gemm_big && g.K >= 2048 && nblocks(g, 256, 256) >= g_big_min)) &&
+      g.split_k == 1 && g.K % 64 == 0 && g.lda % 8 == 0 && g.ldw % 8 == 0)
+    return launch_big(g, st);
   if (g_gemm_lean && g.split_k == 1 && g.K % 64 == 0) {
     // measured (tools/mbench.py decode_gemm / gemm_dbg; M = 1024..98304 x the GPT-2 and HTSAT
     // shapes): 128x128 for big grids and while it makes 1-2 tiles per 2-block CU slot, 128x64
