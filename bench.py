@@ -35,6 +35,7 @@ Rank 0 prints ONE JSON line.  Besides the contract fields (value = whole-job cli
                      rows) at the bs-64 shapes, cold weights / cold K/V;
   strong_scaling_proxy: T(1045 clips) / T(one rank's 131-clip shard) on this GPU = the predicted
                      1 -> 8 GPU speed-up;
+  c3_beam5:          BASELINE configs[2] (beam 5, batch 256) with its LM head's MFMA roofline;
   throughput_mode:   the same path with 128 eval batches decoded per step (8192-row GEMMs) —
                      a different configuration, NOT the metric;
   f32_parity_mode:   the bs-64 headline in f32 (the mode whose greedy ids are bit-exact);
@@ -936,6 +937,53 @@ def main_mistral(args, device):
         flush=True)
 
 
+def roofline_lmhead_beam(pipe, reps=20):
+    """The C3 beam decode's dominant GEMM: the LM head over all C x beam rows (1280 at B = 256,
+    beam 5) against the tied wte [50257 x 768] bf16, with its fused per-row max / sum-exp /
+    top-k epilogue (zs_lmhead_topk, the call _beam_step_body makes), MFMA-bound: 2 M V K flops
+    per launch / its average duration (HIP events, back-to-back launches in one graph)."""
+    from zsaac import ops
+    dec = pipe.decoder
+    R = pipe.cfg.batch * pipe.cfg.beam
+    V, K = pipe.gpt.wte.shape
+    a = dec.hf[:R]
+
+    def launch(i):
+        ops.lmhead_topk(a, pipe.gpt.wte, dec.topk, dec.pstat, dec.pval, dec.pidx)
+    avg = _graph_time(launch, reps)
+    fl = 2.0 * R * V * K
+    tf = fl / avg / 1e12
+    return {"kernel": f"lmhead_kernel<bf16,128,8> (zs_lmhead_topk) M={R} V={V} K={K}, top-{dec.topk} "
+                      f"+ softmax statistics per 128-token block", "bound": "mfma",
+            "achieved": round(tf, 1), "peak": MFMA_BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
+            "frac": round(tf / MFMA_BF16_PEAK_TFLOPS, 4), "avg_launch_us": round(avg * 1e6, 2),
+            "flops_per_launch": int(fl)}
+
+
+def c3_beam5(args, device, n_clips=1024, inflight=2):
+    """C3 (BASELINE.json configs[2]): the same wav -> HTSAT -> MLP -> GPT-2 path with
+    generate_beam (beam 5) on eval batches of 256 clips (1280 decode rows), 1024 synthetic clips,
+    `inflight` batches in flight; plus the MFMA roofline of its dominant GEMM (the LM head)."""
+    import copy
+    a3 = copy.copy(args)
+    a3.beam, a3.batch, a3.group, a3.encoder_batch = 5, 256, 1, 0
+    pipe, _, _ = build(a3, device, dtype=torch.bfloat16, group=1)
+    dt, outs, runner, info = run_captions(a3, 1, 0, device, pipe, n_clips, 3 * 10 ** 6, [n_clips],
+                                          inflight, 1)
+    res = {"metric": "audio clips/sec end-to-end (encode+mapper+GPT-2 decode), AudioCaps-eval "
+                     "beam 5 bs=256", "value": round(n_clips / dt, 2), "unit": "clips/s",
+           "clips": n_clips, "ms_per_step": round(dt / math.ceil(n_clips / 256) * 1e3, 3),
+           "dtype": "bf16", "config": {"workload": "C3: HTSAT + MLP mapper + GPT-2 generate_beam, "
+                                                   "beam 5, entry_length 67", "eval_batch": 256,
+                                       "decode_rows_per_gemm": 1280,
+                                       "steps_in_flight_per_gpu": inflight, **info},
+           "roofline": roofline_lmhead_beam(pipe)}
+    del runner, outs, pipe
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    return res
+
+
 def strong_scaling_proxy(args, device, pipe, t_full, n_full, n_ranks=8):
     """Predicted 1 -> 8 GPU strong-scaling speed-up on Clotho-eval from ONE GPU: one rank's
     1/8 shard (shard_range: 131 clips) timed alone, T(1045) / T(131).  Two batchings of the
@@ -1049,6 +1097,8 @@ def main():
                                          encoder_batch=256)
         res["throughput_mode"]["note"] = ("128 eval batches decoded together (8192-row decode "
                                           "GEMMs), 3 in flight: NOT the metric's bs=64")
+        log("C3 beam 5")
+        res["c3_beam5"] = c3_beam5(args, device)
         log("f32 parity mode")
         res["f32_parity_mode"] = sub_run(args, device, torch.float32, 1, args.inflight, 6 * 64, 1)
         res["f32_parity_mode"]["note"] = "bs=64 in f32: the mode whose greedy ids are bit-exact"

@@ -199,39 +199,52 @@ class MistralWeights:
         self.lm = (lm * gn[None] if fold else lm).to(dev, self.adt).contiguous()
 
     @classmethod
-    def synthetic(cls, device, cfg: dict, seed: int = 0, mode: str = "fp8", eos_boost: float = 1.5):
+    def synthetic(cls, device, cfg: dict, seed: int = 0, mode: str = "fp8", eos_boost: float = 1.5,
+                  shared_values: bool = False, resid_init: bool = False):
         """Random-init weights at ``cfg`` (zsaac.synthetic.MISTRAL_7B geometry for the bench)
         generated and quantised on the device, layer by layer (a 7B f32 state dict on the host
-        would take 29 GB)."""
+        would take 29 GB).  ``shared_values``: every mode holds the SAME values for one seed --
+        the matrices rounded to what per-row fp8 e4m3 represents, the embedding and LM head to
+        bf16 -- so an "f32" engine is the exact-arithmetic reference of the "fp8" one.
+        ``resid_init``: the residual-branch outputs (o_proj, down_proj) scaled by 1 / sqrt(2 L) and
+        unit gains elsewhere (the GPT-2 / Megatron initialisation): a residual stream whose
+        per-layer perturbations stay small, as in a trained model, instead of the bench's
+        high-gain init, whose 32-layer stack amplifies bf16 rounding ~0.7 % per layer."""
         dev = torch.device(device)
         g = torch.Generator(device=dev).manual_seed(seed)
         self = cls.__new__(cls)
         self.mode, self.dev = mode, dev
+        self._shared = shared_values
         self.adt = torch.float32 if mode == "f32" else torch.bfloat16
         D, F, V = cfg["hidden"], cfg["ffn"], cfg["vocab"]
         self.V, self.D, self.F = V, D, F
         self.H, self.KVH, self.HD = cfg["heads"], cfg["kv_heads"], 128
         self.eps, self.theta = 1e-5, 10000.0
         rnd = lambda o, i, gain=1.0: torch.randn(o, i, device=dev, generator=g) * (gain / math.sqrt(i))
-        self.emb = torch.randn(V, D, device=dev, generator=g).to(self.adt)
+        emb = torch.randn(V, D, device=dev, generator=g)
+        self.emb = (emb.bfloat16() if shared_values else emb).to(self.adt)
         self.layers = []
         kv = self.KVH * 128
+        ro = 1.0 / math.sqrt(2 * cfg["layers"]) if resid_init else 1.0
+        gq, gg = (1.0, 1.0) if resid_init else (2.0, 1.5)
         for _ in range(cfg["layers"]):
             self.layers.append({
                 "ln1": None, "ln2": None,
-                "qkv": self._pack(torch.cat([rnd(D, D, 2.0), rnd(kv, D, 2.0), rnd(kv, D)])),
-                "o": self._pack(rnd(D, D)),
-                "gu": self._pack(torch.cat([rnd(F, D, 1.5), rnd(F, D)])),
-                "down": self._pack(rnd(D, F))})
+                "qkv": self._pack(torch.cat([rnd(D, D, gq), rnd(kv, D, gq), rnd(kv, D)])),
+                "o": self._pack(rnd(D, D, ro)),
+                "gu": self._pack(torch.cat([rnd(F, D, gg), rnd(F, D)])),
+                "down": self._pack(rnd(D, F, ro))})
         self.lnf = None
         lm = rnd(V, D, 4.0)
         lm[2] *= eos_boost
-        self.lm = lm.to(self.adt).contiguous()
+        self.lm = (lm.bfloat16() if shared_values else lm).to(self.adt).contiguous()
         return self
 
     def _pack(self, w):
         w = w.float()
         N, K = w.shape
+        if self.mode != "fp8" and getattr(self, "_shared", False):
+            w = dequantize_fp8(*quantize_fp8(w))        # the fp8 engine's exact values
         if self.mode == "fp8":
             q, s = quantize_fp8(w)
             return {"N": N, "K": K, "w8": fp8_pack_tiles(q.to(self.dev)),
@@ -433,6 +446,22 @@ class MistralDecoder:
                 self._step_body(B, eos)
             self.graphs[key] = g
         g.replay()
+
+    def hidden_states(self, embeds: torch.Tensor) -> torch.Tensor:
+        """The final-norm hidden states of every row of ``embeds`` [B, P, D] (causal, positions
+        0..P-1, the prefill of :meth:`generate`) as f32 [B, P, D]: the logits are ``h @ lm^T``
+        (tests: logits and top-1 / top-2 margins along a sequence)."""
+        w, st = self.w, torch.cuda.current_stream().cuda_stream
+        B, P, _ = embeds.shape
+        if B > self.B or P > self.Pmax:
+            raise ValueError(f"mistral hidden_states: B={B} P={P} exceeds the engine")
+        M = B * P
+        x = embeds.float().contiguous()
+        call("zs_mistral_embed", None, 0, x.data_ptr(), P, None, 0, None, w.emb.data_ptr(), w.D,
+             M, self.x.data_ptr(), ops.dt(w.emb), st)
+        self.pos[:M].copy_(torch.arange(P, device=w.dev, dtype=torch.int32).repeat(B))
+        self._layers(M, P)
+        return self.h[:M].float().view(B, P, w.D).clone()
 
     def generate_embeds(self, embeds: torch.Tensor, max_length: int = 60,
                         eos: int = 2) -> List[List[int]]:
