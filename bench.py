@@ -210,7 +210,7 @@ def split_batches(n, B, parts=0):
 
 
 def run_captions(args, world, rank, device, pipe, n_local, first, counts, inflight, warmup,
-                 parts=0):
+                 parts=0, log_pass=False):
     """Times the captioning of this rank's n_local clips (clip ids first..) in batches of
     pipe.cfg.batch (split_batches) on `inflight` streams, then the all-gather; returns (seconds
     max over ranks, outs, runner, info)."""
@@ -235,7 +235,6 @@ def run_captions(args, world, rank, device, pipe, n_local, first, counts, inflig
     torch.cuda.synchronize()
     cap0 = sum(p.decoder.n_captures for p in runner.pipes)
     rows0 = sum(p.decoder.rows_stepped for p in runner.pipes)
-    log0 = len(zdec.PERSIST_LOG) if zdec.PERSIST_LOG is not None else 0
     t0 = time.perf_counter()
     outs = runner.run(batches)
     if world > 1:
@@ -250,7 +249,14 @@ def run_captions(args, world, rank, device, pipe, n_local, first, counts, inflig
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         dt = float(t)
     log(f"timed: {n_local} clips in {dt:.3f} s")
-    runner.timed_log = zdec.PERSIST_LOG[log0:] if zdec.PERSIST_LOG is not None else []
+    runner.timed_log, runner.log_outs = [], None
+    if log_pass and pipe.decoder.persist:
+        # the roofline's live launch timing: the same batches once more, untimed, with HIP events
+        # around every persistent launch (events recorded inside the timed region cost it 3-5 %)
+        zdec.PERSIST_LOG = []
+        runner.log_outs = runner.run(batches)
+        torch.cuda.synchronize()
+        runner.timed_log = list(zdec.PERSIST_LOG)
     info = {"graph_captures_timed": sum(p.decoder.n_captures for p in runner.pipes) - cap0,
             "decode_rows_stepped_per_clip": round(
                 (sum(p.decoder.rows_stepped for p in runner.pipes) - rows0) / max(1, n_local), 2),
@@ -426,9 +432,11 @@ PMC_PERSIST_FILE = os.path.join(ROOT, "profiles", "r3_pmc_persist.json")
 
 
 def persist_roofline(pipe, runner, outs, dt, log):
-    """roofline of the dominant kernel, decode_persist_kernel: the timed region's launches (HIP
-    events recorded on each launch's own stream around it, zsaac.decoder.PERSIST_LOG), algorithmic
-    bytes of each launch from its batch's prompt lengths and step count / its duration."""
+    """roofline of the dominant kernel, decode_persist_kernel: every launch of a repeat of the
+    timed region (same batches, same streams and concurrency, untimed: HIP events recorded on each
+    launch's own stream around it, zsaac.decoder.PERSIST_LOG -- recorded inside the timed region
+    they cost it 3-5 %), algorithmic bytes of each launch from its batch's prompt lengths and step
+    count / its duration."""
     from zsaac import ops
     w_step = gpt2_step_weight_bytes(pipe)
     by_dec = {}
@@ -451,7 +459,7 @@ def persist_roofline(pipe, runner, outs, dt, log):
     return _hbm_entry(
         f"decode_persist_kernel (zs_gpt2_decode_persist): decode steps 1..{steps - 1:.0f} of one "
         f"bs-64 eval batch in one launch (G={ops.decode_persist_grid()} workgroups), the {n} launches of "
-        f"the timed region, {runner.n_inflight} batches in flight", avg_b, avg_s,
+        f"a repeat of the timed region, {runner.n_inflight} batches in flight", avg_b, avg_s,
         {"launches": n, "avg_launch_ms": round(avg_s * 1e3, 3),
          "weight_bytes_per_step": int(w_step), "steps_per_launch_mean": round(steps - 1, 2),
          "traffic": traffic, "traffic_source": tsrc,
@@ -459,7 +467,7 @@ def persist_roofline(pipe, runner, outs, dt, log):
                          "launches of the same workload (tools/pmc_traffic.py persist)",
          "concurrent_aggregate": {"algo_GBps": round(sum(byts) / dt / 1e9, 1),
                                   "frac": round(sum(byts) / dt / 1e9 / HBM_PEAK_GBS, 4),
-                                  "note": "all launches' algorithmic bytes / the timed wall"}})
+                                  "note": "all launches' algorithmic bytes / the headline's timed wall"}})
 
 
 def persist_all_launches(log):
@@ -1018,9 +1026,6 @@ def main():
         return main_magic(args, torch.device("cuda", 0))
     if args.mistral:
         return main_mistral(args, torch.device("cuda", 0))
-    if not args.no_roofline:
-        from zsaac import decoder as zdec
-        zdec.PERSIST_LOG = []         # HIP events around every persistent decode launch
     pipe, csd, asd = build(args, device)
     if args.embeddings_only:
         return main_embeddings(args, world, rank, device, pipe)
@@ -1036,8 +1041,10 @@ def main():
         counts = [per] * world
     n_local = hi - lo
     steps = -(-n_local // B)
+    want_roof = (rank == 0 and not args.no_roofline and args.group == 1 and B <= 64
+                 and not args.beam and args.dtype == "bf16")
     dt, outs, runner, info = run_captions(args, world, rank, device, pipe, n_local, lo, counts,
-                                          args.inflight, args.warmup)
+                                          args.inflight, args.warmup, log_pass=want_roof)
     workload = (("C3 AudioCaps-eval" if args.beam else "C2 Clotho-eval")
                 + (" (1045 clips per rank)" if not (args.steps or args.clips) else "")
                 + ": STFT/log-mel + " + args.encoder.upper() + " + " + args.mapper
@@ -1067,7 +1074,7 @@ def main():
         log("rooflines")
         from zsaac import decoder as zdec
         if pipe.decoder.persist:
-            res["roofline"] = persist_roofline(pipe, runner, outs, dt, runner.timed_log)
+            res["roofline"] = persist_roofline(pipe, runner, runner.log_outs, dt, runner.timed_log)
         else:
             res["roofline"] = roofline_gemm_ln(pipe)
         wav = synthetic_clips(B, 0, device)
