@@ -1153,7 +1153,13 @@ extern "C" int zs_lmhead_topk_t(int M, int K, int V, int dtype, const void* A, i
                      (g_fast_xcd ? 1 : 0) | (g_lm_prio ? 2 : 0), M, K, V, (const T*)A, lda,       \
                      (const T*)W, topk, row_norm, part_stat,                                      \
                      part_val, part_idx, temperature)
-#define LMH_K(T, BM_) do { if (topk == 1) LMH(T, BM_, 1); else LMH(T, BM_, 8); } while (0)
+  // top-k lists of 1 (argmax), 5 (beam <= 5: generate_beam's default) or 8 entries per block
+#define LMH_K(T, BM_)                                                                          \
+  do {                                                                                         \
+    if (topk == 1) LMH(T, BM_, 1);                                                             \
+    else if (topk <= 5) LMH(T, BM_, 5);                                                        \
+    else LMH(T, BM_, 8);                                                                       \
+  } while (0)
   if (M <= 64) {
     if (dtype == ZS_BF16) LMH_K(bf16_t, 64); else LMH_K(float, 64);
   } else {

@@ -123,8 +123,11 @@ class CaptionPipeline:
     def _alloc(self):
         cfg, dev, B = self.cfg, self.dev, self.cfg.batch
         beam = max(cfg.beam, 1)
+        # beam: per-block top-`beam` lists suffice for the global top-beam (fewer candidates to
+        # sort in the LM head's epilogue and to merge in beam_step)
         self.decoder = Gpt2Decoder(self.gpt, B * beam, self.Pmax, cfg.entry_length,
                                    max_prefill_rows=B, use_graph=cfg.use_graph,
+                                   topk=cfg.beam if cfg.beam else 8,
                                    compact=cfg.compact_decode, persist=cfg.persist_decode)
         i32 = dict(device=dev, dtype=torch.int32)
         self.hard_ids = torch.zeros(B, self.h_cap, **i32)
