@@ -106,8 +106,10 @@ int zs_gemm_ln(int M, int N, int K, const float* x, int ldx, const float* ln_w, 
 /* zs_gemm_ln_f32: zs_gemm_ln with f32 W [N][ldw] and f32 out (the f32 parity mode's decode
  *   step): LayerNorm of the f32 rows x with the affine (ln_w, ln_b) applied in f32, exact f32
  *   products and f32 accumulation (v_mfma_f32_16x16x4_f32).  M <= 64, K 768 or 1024; x, W and
- *   the LN params 16-byte aligned.  zs_gemm routes f32 M <= 64 GEMMs to the same row-group
- *   kernel (no LayerNorm).  Replaces GPT2Block's ln_1 -> c_attn / ln_2 -> c_fc pairs. */
+ *   the LN params 16-byte aligned.  Replaces GPT2Block's ln_1 -> c_attn / ln_2 -> c_fc pairs.
+ *   ln_w == ln_b == NULL: no LayerNorm (out = act(x W^T + b) + residual, K up to 3072: the
+ *   attn.c_proj / mlp.c_proj of the same step).  zs_gemm keeps its own f32 kernels, so a row's
+ *   zs_gemm result stays independent of how many rows share the launch. */
 int zs_gemm_ln_f32(int M, int N, int K, const float* x, int ldx, const float* ln_w,
                    const float* ln_b, float eps, const float* W, int ldw, const float* bias,
                    const float* residual, int ldr, float* out, int ldo, int act, void* stream);

@@ -1,6 +1,6 @@
 """GPU: the f32 row-group decode GEMMs (csrc/gemm_rows.hip gemm_rows_f32_kernel) against a
 torch fp32 reference of the same op -- zs_gemm_ln_f32 (LayerNorm with its affine in f32, then
-the product, bias, gelu_new / residual) and zs_gemm's f32 M <= 64 route -- at the GPT-2 decode
+the product, bias, gelu_new / residual) and its no-LayerNorm form (the projections) -- at the GPT-2 decode
 shapes and ragged row counts.  Tolerance: exact f32 products with a different summation order
 than torch's, |err| <= 2e-5 * max|ref| + 1e-5."""
 import pytest
@@ -41,5 +41,5 @@ def test_gemm_rows_f32_residual(cuda, M, N, K):
     b = torch.randn(N, generator=g).to(cuda)
     x = torch.randn(M, N, generator=g).to(cuda)
     ref = a.double() @ w.double().t() + b.double() + x.double()
-    ops.gemm(a, w, x, bias=b, residual=x)
+    ops.gemm_ln_f32(a, None, None, w, x, bias=b, residual=x)
     assert float((x.double() - ref).abs().max()) <= _tol(ref)

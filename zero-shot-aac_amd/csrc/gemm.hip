@@ -1072,10 +1072,6 @@ extern "C" __attribute__((visibility("hidden"))) int zs_gemm_rows_internal(
     int M, int N, int K, const void* A, int lda, const void* W, int ldw, const float* bias,
     const float* residual, int ldr, void* out, int ldo, int out_dtype, int act, void* stream);
 
-extern "C" __attribute__((visibility("hidden"))) int zs_gemm_rows_f32_internal(
-    int M, int N, int K, const void* A, int lda, const void* W, int ldw, const float* bias,
-    const float* residual, int ldr, void* out, int ldo, int out_dtype, int act, void* stream);
-
 extern "C" int zs_gemm(int M, int N, int K, int dtype, const void* A, int lda, const void* W,
                        int ldw, const float* bias, const float* residual, int ldr, void* out,
                        int ldo, int out_dtype, int act, int split_k, float* workspace,
@@ -1089,12 +1085,9 @@ extern "C" int zs_gemm(int M, int N, int K, int dtype, const void* A, int lda, c
   ZS_REQUIRE(split_k >= 0, "zs_gemm: split_k >= 0");
   ZS_REQUIRE(dtype == ZS_F32 || dtype == ZS_BF16, "zs_gemm: dtype");
   if (M == 0) return 0;
-  if (split_k == 0 && M <= 64) {   // decode-sized: row-group kernel (bf16 or f32 operands)
-    const int rc = dtype == ZS_BF16
-        ? zs_gemm_rows_internal(M, N, K, A, lda, W, ldw, bias, residual, ldr, out, ldo, out_dtype,
-                                act, stream)
-        : zs_gemm_rows_f32_internal(M, N, K, A, lda, W, ldw, bias, residual, ldr, out, ldo,
-                                    out_dtype, act, stream);
+  if (split_k == 0 && dtype == ZS_BF16 && M <= 64) {   // decode-sized: row-group kernel
+    const int rc = zs_gemm_rows_internal(M, N, K, A, lda, W, ldw, bias, residual, ldr, out, ldo,
+                                         out_dtype, act, stream);
     if (rc <= 0) return rc;                             // 1 = shape not covered
   }
   if (split_k == 0) {   // auto: weight-streaming skinny kernel for decode-sized M

@@ -531,32 +531,25 @@ extern "C" int zs_gemm_ln(int M, int N, int K, const float* x, int ldx, const fl
   return ln_w ? launch_rows<1>(g, p, S(stream)) : launch_rows<2>(g, p, S(stream));
 }
 
-// f32 operands, M <= 64 (zs_gemm auto mode); returns 1 when the shape is not covered
-extern "C" __attribute__((visibility("hidden"))) int zs_gemm_rows_f32_internal(
-    int M, int N, int K, const void* A, int lda, const void* W, int ldw, const float* bias,
-    const float* residual, int ldr, void* out, int ldo, int out_dtype, int act, void* stream) {
-  if (!g_gemm_rows || M > RG_MAX_M || out_dtype != ZS_F32 || (lda & 3) || (ldw & 3)) return 1;
-  RowsArgs g{};
-  g.M = M; g.N = N; g.K = K; g.Af = (const float*)A; g.lda = lda; g.Wf = (const float*)W;
-  g.ldw = ldw; g.bias = bias; g.residual = residual; g.ldr = ldr; g.out = out; g.ldo = ldo;
-  g.out_dtype = out_dtype; g.act = act;
-  return launch_rows_f32(g, false, S(stream));
-}
-
 extern "C" int zs_gemm_ln_f32(int M, int N, int K, const float* x, int ldx, const float* ln_w,
                               const float* ln_b, float eps, const float* W, int ldw,
                               const float* bias, const float* residual, int ldr, float* out,
                               int ldo, int act, void* stream) {
   ZS_REQUIRE(M > 0 && M <= RG_MAX_M && N > 0 && K > 0,
              "zs_gemm_ln_f32: M in 1..%d (got M=%d N=%d K=%d)", RG_MAX_M, M, N, K);
-  ZS_REQUIRE(x && W && out && ln_w && ln_b, "zs_gemm_ln_f32: null pointer");
+  // ln_w == ln_b == nullptr: no LayerNorm, out = act(x W^T + b) + residual (the f32 decode's
+  // attn.c_proj / mlp.c_proj; K up to 3072)
+  ZS_REQUIRE(x && W && out && (ln_w == nullptr) == (ln_b == nullptr), "zs_gemm_ln_f32: null pointer");
   ZS_REQUIRE(ldx % 4 == 0 && ldw % 4 == 0 && ((uintptr_t)x & 15) == 0 && ((uintptr_t)W & 15) == 0 &&
              ((uintptr_t)ln_w & 15) == 0 && ((uintptr_t)ln_b & 15) == 0,
              "zs_gemm_ln_f32: x / W / LN params must be 16-byte aligned, ldx / ldw multiples of 4");
-  ZS_REQUIRE(K == 768 || K == 1024, "zs_gemm_ln_f32: unsupported K=%d (768 or 1024)", K);
+  const bool ln = ln_w != nullptr;
+  ZS_REQUIRE(ln ? (K == 768 || K == 1024) : (K == 768 || K == 1024 || K == 3072),
+             "zs_gemm_ln_f32: unsupported K=%d (768 / 1024, or 3072 without LayerNorm)", K);
   RowsArgs g{};
   g.M = M; g.N = N; g.K = K; g.X = x; g.ldx = ldx; g.ln_w = ln_w; g.ln_b = ln_b; g.eps = eps;
+  g.Af = x; g.lda = ldx;
   g.Wf = W; g.ldw = ldw; g.bias = bias; g.residual = residual; g.ldr = ldr;
   g.out = out; g.ldo = ldo; g.out_dtype = ZS_F32; g.act = act;
-  return launch_rows_f32(g, true, S(stream));
+  return launch_rows_f32(g, ln, S(stream));
 }

@@ -335,15 +335,15 @@ class Gpt2Decoder:
             return
         if self.dtype == torch.float32 and M <= 64 and self.rows_f32:
             # the f32 parity mode's decode: ln_1 / ln_2 fused into f32 row-group GEMMs
-            # (zs_gemm_ln_f32; the affine applied in f32, exact f32 products), f32 row-group
-            # kernels for the projections (zs_gemm auto mode)
+            # (zs_gemm_ln_f32; the affine applied in f32, exact f32 products), the same kernels
+            # without LayerNorm for the projections
             for l, ly in enumerate(self.w.layers):
                 qkv, att, hid = self.qkv[:M], self.att[:M], self.hid[:M]
                 ops.gemm_ln_f32(x, *ly["ln1"], ly["attn_w"], qkv, bias=ly["attn_b"])
                 attn_fn(l, qkv, att)
-                ops.gemm(att, ly["proj_w"], x, bias=ly["proj_b"], residual=x)
+                ops.gemm_ln_f32(att, None, None, ly["proj_w"], x, bias=ly["proj_b"], residual=x)
                 ops.gemm_ln_f32(x, *ly["ln2"], ly["fc_w"], hid, bias=ly["fc_b"], act=ops.ACT_GELU_TANH)
-                ops.gemm(hid, ly["mproj_w"], x, bias=ly["mproj_b"], residual=x)
+                ops.gemm_ln_f32(hid, None, None, ly["mproj_w"], x, bias=ly["mproj_b"], residual=x)
             return
         for l, ly in enumerate(self.w.layers):
             h, qkv, att, hid = self.h[:M], self.qkv[:M], self.att[:M], self.hid[:M]

@@ -153,9 +153,9 @@ def gemm(a, w, out, bias=None, residual=None, act=ACT_NONE, split_k=0, workspace
             # larger M simply takes the tiled kernel
             _need(M > 64, f"gemm: workspace {workspace.numel()} < {need} floats")
             workspace = None
-        # M <= 64 keeps auto mode without a workspace: zs_gemm takes the row-group kernel (bf16
-        # or f32, no workspace), and the tiled kernel for shapes that kernel does not cover
-        if workspace is None and not M <= 64:
+        # bf16 M <= 64 keeps auto mode without a workspace: zs_gemm takes the row-group kernel
+        # (no workspace), and the tiled kernel for shapes that kernel does not cover
+        if workspace is None and not (a.dtype == torch.bfloat16 and M <= 64):
             split_k = 1
     lda = a.stride(-2) if a.dim() > 1 else K
     ldo = out.stride(-2) if out.dim() > 1 else N
@@ -185,12 +185,13 @@ def gemm_ln(x, ln_w, ln_b, w, out, bias=None, residual=None, act=ACT_NONE, eps=1
 
 def gemm_ln_f32(x, ln_w, ln_b, w, out, bias=None, residual=None, act=ACT_NONE, eps=1e-5):
     """out = act(LayerNorm(x) @ w.T + bias) + residual, all f32 (zs_gemm_ln_f32): x [M, K]
-    (M <= 64), w [N, K] f32; the LN affine applied in f32 before the product."""
+    (M <= 64), w [N, K] f32; the LN affine applied in f32 before the product.  ln_w = ln_b =
+    None: no LayerNorm (the decode step's projections, K up to 3072)."""
     M, K = x.shape
     N = w.shape[0]
     _need(w.shape[1] == K and w.dtype == torch.float32 and x.dtype == torch.float32
           and out.dtype == torch.float32, f"gemm_ln_f32: x{tuple(x.shape)} w{tuple(w.shape)} {w.dtype}")
-    _need(ln_w is not None and ln_b is not None, "gemm_ln_f32: LN weight and bias")
+    _need((ln_w is None) == (ln_b is None), "gemm_ln_f32: LN weight and bias together")
     _need(bias is None or bias.dtype == torch.float32, "gemm_ln_f32: bias must be f32")
     ldr = residual.stride(0) if residual is not None else 0
     call("zs_gemm_ln_f32", M, N, K, _p(x), x.stride(0), _p(ln_w), _p(ln_b), float(eps), _p(w),
