@@ -461,6 +461,7 @@ def persist_roofline(pipe, runner, outs, dt, log):
         f"bs-64 eval batch in one launch (G={ops.decode_persist_grid()} workgroups), the {n} launches of "
         f"a repeat of the timed region, {runner.n_inflight} batches in flight", avg_b, avg_s,
         {"launches": n, "avg_launch_ms": round(avg_s * 1e3, 3),
+         "row_split2_launches": sum(1 for r in getattr(runner, "row_split", []) if r == 2),
          "weight_bytes_per_step": int(w_step), "steps_per_launch_mean": round(steps - 1, 2),
          "traffic": traffic, "traffic_source": tsrc,
          "traffic_note": "PMC FETCH_SIZE*2*1024 + WRITE_SIZE*1024 per launch, single-stream "
@@ -891,6 +892,10 @@ def main_mistral(args, device):
     dec.fused_decode_attn = os.environ.get("ZS_MISTRAL_FUSED_ATTN", "1") != "0"   # A/B knobs
     dec.use_graph = os.environ.get("ZS_MISTRAL_GRAPH", "1") != "0"
     dec.prefill_unpack = os.environ.get("ZS_MISTRAL_UNPACK", "1") != "0"
+    dec.fused_glu = os.environ.get("ZS_MISTRAL_RUN", "1") != "0"
+    for kv in filter(None, os.environ.get("ZS_MISTRAL_RUN_CFG", "").split(",")):   # e.g. down=2x2
+        k, v = kv.split("=")
+        dec.run_cfg[k] = tuple(int(t) for t in v.split("x"))
     n = args.steps or 2
     wav = synthetic_clips(B, 0, device)
 
@@ -1008,6 +1013,7 @@ def strong_scaling_proxy(args, device, pipe, t_full, n_full, n_ranks=8):
                                            0, parts=parts)
         sizes = [int(o.ids.shape[0]) for o in outs]
         out[name] = {"seconds": round(dt, 4), "batches": sizes,
+                     "row_split": list(getattr(runner, "row_split", [])),
                      "predicted_speedup": round(t_full / dt, 2)}
         best = max(best or 0.0, t_full / dt)
         del outs, runner

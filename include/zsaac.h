@@ -285,6 +285,26 @@ int zs_fp8_gemm_rows(const void* A, int lda, const void* W8, const float* scale,
                      int K, float* out, long split_stride, int ldo, void* stream);
 int zs_fp8_splits(int K);
 
+/* zs_fp8_gemm_run: the same product for M <= 32 with one workgroup per (128-column tile, run of
+ * ks consecutive splits, k half of kh), the run summed in registers: out gets
+ * zs_fp8_splits(K) / ks * kh slabs (slab (run, half) at index run * kh + half; kh 2 halves each
+ * split between two workgroups, for short streams).
+ * act != NULL (GLU; ks == zs_fp8_splits(K)): W is the gate|up matrix with rows glu-interleaved
+ * (zsaac/mistral.py glu_interleave) and act[m][f] = silu(gate_f) * up_f is written directly as
+ * bf16 [M][ld_act] (N / 2 columns; out unused) -- MistralMLP's act_fn(gate_proj(x)) * up_proj(x)
+ * (transformers MistralMLP, called from caption_model.py:355-364's generate). */
+int zs_fp8_gemm_run(const void* A, int lda, const void* W8, const float* scale, int M, int N,
+                    int K, int ks, int kh, float* out, long split_stride, int ldo, void* act,
+                    int ld_act, const float* rss, int nch, float eps, void* stream);
+
+/* zs_mistral_add_ss: the decode form of zs_mistral_add_rmsnorm when the next GEMM applies the
+ * norm (zs_fp8_gemm_run with rss; MistralRMSNorm's weight folded into that GEMM): x[m] +=
+ * sum_s y[s][m] (y may be NULL), xb[m] = bf16(x[m]) and rss[c][m] (row stride 32) = sum of x^2 over
+ * columns 512 c .. 512 c + 511; M <= 32, D % 512 == 0.  zs_fp8_gemm_run(..., rss, D / 512 <= 8, eps)
+ * then scales output row m by rsqrt(sum_c rss[c][m] / K + eps). */
+int zs_mistral_add_ss(float* x, const float* y, int nsplit, long ss, int M, int D, void* xb,
+                      float* rss, void* stream);
+
 /* zs_mistral_embed: prefill rows b*P + i (P = H + ns + nt): embed[hard[b][i]] (i < H, pads
  * included as the reference attends them), soft[b][i-H] (ns rows, f32), embed[tail[i-H-ns]]
  * (the language tag); or, with tok != NULL, decode rows embed[tok[m]].  x f32 [M][D]. */
@@ -311,7 +331,8 @@ int zs_mistral_rope_kv(const float* qkv, int nsplit, long ss, int M, int H, int 
 int zs_fp8_unpack_bf16(const void* W8, int N, int K, void* out, void* stream);
 int zs_scale_cols(float* x, int M, int N, int ld, const float* scale, void* stream);
 
-/* zs_mistral_silu_mul: act[m][f] = silu(gate) * up from gate|up slabs [nsplit][M][2F]. */
+/* zs_mistral_silu_mul: act[m][f] = silu(gate) * up from gate|up slabs [nsplit][M][2F] whose
+ * columns are glu-interleaved: gate f at 16 (f / 8) + 8 (f / 4 % 2) + f % 4, up f at that + 4. */
 int zs_mistral_silu_mul(const float* gu, int nsplit, long ss, int M, int F, void* act, int dtype,
                         void* stream);
 
@@ -445,6 +466,9 @@ int zs_greedy_step_map(const float* part_val, const int* part_idx, int R, const 
  * the logits before the argmax (gpt2_prefix_eval.py:196); kv: 24 pointers
  * {kc[0..11], vc[0..11]}, each [R][12][Lmax][64] bf16 (zs_kv_write layout).  ws: scratch of
  * zs_decode_persist_workspace_bytes() bytes, 256-byte aligned, private to one launch in flight.
+ * row_split 1: zs_decode_persist_grid() workgroups each own a column slice of every GEMM for all
+ * rows; 2: twice as many, each the same slice for half of the rows (half the per-workgroup
+ * activation reads, a shorter step; for few batches in flight).
  * A grid that cannot become co-resident gives up after a bounded wait: then
  * zs_decode_persist_status reports timed_out != 0 and the outputs are invalid. */
 int zs_decode_persist_workspace_bytes(void);
@@ -454,7 +478,7 @@ int zs_gpt2_decode_persist(int R, int Lmax, int max_steps, int stop0, int stop1,
                            float temperature, const void* const* layer_w,
                            const float* lnf_w, const float* lnf_b, void* const* kv, int* pos,
                            int* next_tok, int* done, int* out_ids, int* out_len, int* step_ctr,
-                           int* all_done, void* ws, long ws_bytes, void* stream);
+                           int* all_done, void* ws, long ws_bytes, int row_split, void* stream);
 int zs_decode_persist_status(const void* ws, int* timed_out);
 /* zs_decode_persist_set_stamps: diagnostic phase timing (tools/persist_stamps.py): with buf !=
  * NULL ([grid][128] u64), thread 0 of every workgroup of later launches writes s_memrealtime

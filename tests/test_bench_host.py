@@ -22,3 +22,27 @@ def test_persist_launch_bytes():
     got = bench.persist_launch_bytes(1000, [10, 12], 3)
     assert got == 2 * 1000 + row * ((10 + 11) + (12 + 13) + 2 * 2)
     assert bench.persist_launch_bytes(1000, [10], 1) == 0
+
+
+def test_choose_row_split_keeps_grids_coresident():
+    """ConcurrentRunner's row_split choice (zsaac.pipeline.choose_row_split): simulated begins and
+    finishes in random order, 5 pipelines, G = 48 on 256 CUs -- the workgroups in flight never
+    exceed the CUs, and a shard of two or three batches runs its first ones at row_split 2."""
+    import random
+    from zsaac.pipeline import choose_row_split
+    G, CUS, P = 48, 256, 5
+    rng = random.Random(0)
+    for n in list(range(1, 24)) * 20:
+        active, nxt, chosen = {}, 0, []
+        while nxt < n or active:
+            free = [i for i in range(P) if i not in active]
+            if nxt < n and free and rng.random() < 0.7:
+                rs = choose_row_split(sum(active.values()), n - nxt, G, CUS)
+                active[free[0]] = rs * G
+                chosen.append(rs)
+                nxt += 1
+                assert sum(active.values()) <= CUS, (n, chosen)
+            elif active:
+                del active[rng.choice(list(active))]
+    assert choose_row_split(0, 2, G, CUS) == 2 and choose_row_split(0, 3, G, CUS) == 2
+    assert choose_row_split(96, 2, G, CUS) == 2 and choose_row_split(0, 5, G, CUS) == 1

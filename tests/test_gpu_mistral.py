@@ -107,6 +107,101 @@ def _fp8_gemm_rows_check(cuda, M, N, K):
     assert float((got - ref).abs().max()) < 1e-3 * float(ref.abs().max()) + 1e-4
 
 
+@pytest.mark.parametrize("M,N,K,ks,kh", [(32, 4096, 14336, 2, 1), (7, 1008, 2048, 2, 1),
+                                         (32, 2048, 4096, 4, 1), (20, 4096, 4096, 1, 1),
+                                         (32, 4096, 4096, 1, 2), (9, 1040, 4096, 2, 2),
+                                         (1, 6144, 4096, 4, 2)])
+def test_fp8_gemm_run(cuda, M, N, K, ks, kh):
+    """zs_fp8_gemm_run's slabs (runs of ks splits, 1 / kh of each, summed in registers) sum to
+    the product."""
+    from zsaac._lib import call
+    from zsaac.mistral import dequantize_fp8, fp8_pack_tiles, quantize_fp8
+    g = torch.Generator().manual_seed(M + N + ks)
+    w = torch.randn(N, K, generator=g) / K ** 0.5
+    a = torch.randn(M, K, generator=g).bfloat16()
+    q, s = quantize_fp8(w)
+    ref = a.float() @ dequantize_fp8(q, s).t()
+    ns = call("zs_fp8_splits", K) // ks * kh
+    out = torch.full((ns, M, N), float("nan"), device=cuda)
+    ad, qd, sd = a.to(cuda), fp8_pack_tiles(q).to(cuda), s.to(cuda)
+    call("zs_fp8_gemm_run", ad.data_ptr(), K, qd.data_ptr(), sd.data_ptr(), M, N, K, ks, kh,
+         out.data_ptr(), M * N, N, None, 0, None, 0, 0.0, torch.cuda.current_stream().cuda_stream)
+    got = out.sum(0).cpu()
+    assert float((got - ref).abs().max()) < 1e-3 * float(ref.abs().max()) + 1e-4
+
+
+@pytest.mark.parametrize("M,F,K", [(32, 14336, 4096), (5, 1024, 2048), (17, 1032, 1024)])
+def test_fp8_gemm_run_glu(cuda, M, F, K):
+    """GLU epilogue: act = silu(gate) * up straight from the glu-interleaved gate|up matrix, and
+    the prefill consumer (zs_mistral_silu_mul over slabs of the same matrix) agrees."""
+    from zsaac._lib import ZS_BF16, call
+    from zsaac.mistral import dequantize_fp8, fp8_pack_tiles, glu_interleave, quantize_fp8
+    g = torch.Generator().manual_seed(M + F)
+    gate, up = torch.randn(F, K, generator=g) / K ** 0.5, torch.randn(F, K, generator=g) / K ** 0.5
+    a = torch.randn(M, K, generator=g).bfloat16()
+    q, s = quantize_fp8(glu_interleave(torch.cat([gate, up])))
+    wd = dequantize_fp8(q, s)
+    # the interleave is a row permutation: undo it on the dequantised matrix for the reference
+    r = torch.arange(2 * F)
+    c = r % 16
+    j = 8 * (r // 16) + 4 * (c // 8) + c % 4
+    src = torch.where((c // 4) % 2 == 0, j, F + j)
+    wcat = torch.empty_like(wd)
+    wcat[src] = wd
+    y = a.float() @ wcat.t()
+    ref = torch.nn.functional.silu(y[:, :F]) * y[:, F:]
+    st = torch.cuda.current_stream().cuda_stream
+    ad, qd, sd = a.to(cuda), fp8_pack_tiles(q).to(cuda), s.to(cuda)
+    act = torch.full((M, F + 8), float("nan"), device=cuda, dtype=torch.bfloat16)
+    call("zs_fp8_gemm_run", ad.data_ptr(), K, qd.data_ptr(), sd.data_ptr(), M, 2 * F, K,
+         call("zs_fp8_splits", K), 1, None, 0, 0, act.data_ptr(), F + 8, None, 0, 0.0, st)
+    got = act[:, :F].float().cpu()
+    tol = 1e-2 * float(ref.abs().max()) + 1e-3
+    assert float((got - ref).abs().max()) < tol
+    assert torch.isnan(act[:, F:].float()).all()              # nothing past F columns written
+    ns = call("zs_fp8_splits", K)
+    slab = torch.empty(ns, M, 2 * F, device=cuda)
+    call("zs_fp8_gemm_rows", ad.data_ptr(), K, qd.data_ptr(), sd.data_ptr(), M, 2 * F, K,
+         slab.data_ptr(), M * 2 * F, 2 * F, st)
+    act2 = torch.empty(M, F, device=cuda, dtype=torch.bfloat16)
+    call("zs_mistral_silu_mul", slab.data_ptr(), ns, M * 2 * F, M, F, act2.data_ptr(), ZS_BF16, st)
+    assert float((act2.float().cpu() - ref).abs().max()) < tol
+
+
+@pytest.mark.parametrize("M,D,N,ns", [(32, 4096, 6144, 4), (6, 1024, 1040, 3), (17, 2048, 512, 0)])
+def test_add_ss_then_normed_gemm(cuda, M, D, N, ns):
+    """zs_mistral_add_ss (x += slab sum, bf16 copy, partial sums of squares) + zs_fp8_gemm_run
+    with rss (the RMSNorm row factor applied after the product) == RMSNorm(x + y) @ W^T."""
+    from zsaac._lib import call
+    from zsaac.mistral import dequantize_fp8, fp8_pack_tiles, quantize_fp8
+    g = torch.Generator().manual_seed(M + D)
+    x = torch.randn(M, D, generator=g) * 3
+    y = torch.randn(max(ns, 1), M, D, generator=g)
+    w = torch.randn(N, D, generator=g) / D ** 0.5
+    q, s = quantize_fp8(w)
+    xs = x + (y.sum(0) if ns else 0)
+    hn = xs * torch.rsqrt(xs.pow(2).mean(1, keepdim=True) + 1e-5)
+    ref = hn @ dequantize_fp8(q, s).t()
+    st = torch.cuda.current_stream().cuda_stream
+    xd, yd = x.to(cuda), y.to(cuda)
+    xb = torch.empty(M, D, device=cuda, dtype=torch.bfloat16)
+    rss = torch.full((8 * 32,), float("nan"), device=cuda)
+    call("zs_mistral_add_ss", xd.data_ptr(), yd.data_ptr() if ns else None, ns, M * D, M, D,
+         xb.data_ptr(), rss.data_ptr(), st)
+    assert torch.allclose(xd.cpu(), xs, atol=1e-5)
+    assert torch.equal(xb.cpu(), xs.bfloat16())
+    nch = D // 512
+    ss_ref = xs.pow(2).view(M, nch, 512).sum(2).t()
+    assert torch.allclose(rss.view(8, 32)[:nch, :M].cpu(), ss_ref, rtol=1e-5)
+    qd, sd = fp8_pack_tiles(q).to(cuda), s.to(cuda)
+    nsl = call("zs_fp8_splits", D)
+    out = torch.empty(nsl, M, N, device=cuda)
+    call("zs_fp8_gemm_run", xb.data_ptr(), D, qd.data_ptr(), sd.data_ptr(), M, N, D, 1, 1,
+         out.data_ptr(), M * N, N, None, 0, rss.data_ptr(), nch, 1e-5, st)
+    got = out.sum(0).cpu()
+    assert float((got - ref).abs().max()) < 1e-2 * float(ref.abs().max())
+
+
 def test_dropin_clap_caption_mistralai(cuda, golden):
     """ClapCaption_Mistralai_prompt driven like predict_mistralai_multilingual.py:95-111 (peft
     attribute path, clap_to_gpt with the language tag, LMmodel.generate), f32 parity mode."""

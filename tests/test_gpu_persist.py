@@ -118,3 +118,21 @@ def test_persist_temperature(cuda, flat):
         p.decoder.temperature = 0.7
         res.append(p.caption_emb(emb).captions())
     assert res[0] == res[1]
+
+
+@pytest.mark.parametrize("B", [32, 7])
+def test_persist_row_split(cuda, flat, B):
+    """The row-split grid (row_split 2: twice the workgroups, each a column slice for half of the
+    rows) gives the ids and decode state of the default grid and the reference's ids."""
+    from tools import idparity
+    emb = torch.from_numpy(flat["clap_emb"][:B]).to(cuda)
+    res = []
+    for rs in (1, 2):
+        p = _pipe(flat, cuda, True, batch=B)
+        p.decoder.persist_row_split = rs
+        out = p.caption_emb(emb)
+        res.append((out.captions(), _state(p, B), p.decoder.step_ctr.item()))
+    assert res[0][0] == res[1][0]
+    for k in res[0][1]:
+        assert np.array_equal(res[0][1][k], res[1][1][k]), k
+    assert res[0][2] == res[1][2]

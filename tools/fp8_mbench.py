@@ -31,17 +31,30 @@ def main():
         sc = torch.full((N,), 1e-3, device=dev)
         a = torch.randn(M, K, device=dev).bfloat16()
         ns = call("zs_fp8_splits", K)
-        out = torch.empty(ns * M * N, device=dev)
+        out = torch.empty(2 * ns * M * N, device=dev)
+        act = torch.empty(M, N // 2 + 8, device=dev, dtype=torch.bfloat16)
         res = []
-        for knob, val in (("fp8_tile", 0), ("fp8_tile", 2), ("fp8_tile", 3)):
-            lib().zs_tune_set(knob.encode(), val)
+        st = lambda: torch.cuda.current_stream().cuda_stream
+        variants = [("fp8_tile=0", 0, None), ("fp8_tile=2", 2, None)]
+        variants += [(f"run ks={k} kh={h}", None, (k, h)) for k in (1, 2, 4) for h in (1, 2)
+                     if ns % k == 0]
+        if name == "gate|up":
+            variants.append(("run glu", None, (-ns, 1)))
+        for label, tile, ks in variants:
+            if ks is None:
+                lib().zs_tune_set(b"fp8_tile", tile)
 
-            def launch(i):
-                call("zs_fp8_gemm_rows", a.data_ptr(), K, ws[i % ncopy].data_ptr(), sc.data_ptr(),
-                     M, N, K, out.data_ptr(), M * N, N, torch.cuda.current_stream().cuda_stream)
+                def launch(i):
+                    call("zs_fp8_gemm_rows", a.data_ptr(), K, ws[i % ncopy].data_ptr(),
+                         sc.data_ptr(), M, N, K, out.data_ptr(), M * N, N, st())
+            else:
+                def launch(i, ks=ks[0], kh=ks[1]):
+                    call("zs_fp8_gemm_run", a.data_ptr(), K, ws[i % ncopy].data_ptr(),
+                         sc.data_ptr(), M, N, K, abs(ks), kh, out.data_ptr(), M * N, N,
+                         act.data_ptr() if ks < 0 else None, N // 2 + 8, None, 0, 0.0, st())
             t = bench._graph_time(launch, 2 * ncopy)
-            lib().zs_tune_set(knob.encode(), 0)
-            res.append(f"{knob}={val}: {t * 1e6:7.1f}us {N * K / t / 1e9:6.0f}GB/s")
+            lib().zs_tune_set(b"fp8_tile", 0)
+            res.append(f"{label}: {t * 1e6:6.1f}us {N * K / t / 1e9:5.0f}GB/s")
         print(f"{name:8s} N={N} K={K}: " + " | ".join(res), flush=True)
         del ws
 

@@ -202,6 +202,7 @@ struct Bar {
   unsigned n;
   unsigned long long* sb;   // this workgroup's stamp row of the traced step (or NULL)
   unsigned n0;              // barrier count at the start of the traced step
+  unsigned g;               // workgroups in the grid
 };
 __device__ __forceinline__ void bar_arrive(Bar& b) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -215,7 +216,7 @@ __device__ __forceinline__ void bar_arrive(Bar& b) {
 typedef __attribute__((address_space(3))) int lds_int_t;
 __device__ __forceinline__ bool bar_wait(Bar& b, volatile lds_int_t* s_ok) {
   if (threadIdx.x == 0) {
-    const unsigned target = b.n * G;
+    const unsigned target = b.n * b.g;
     unsigned spins = 0;
     int ok = 1;
     while (__hip_atomic_load(b.cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
@@ -243,62 +244,65 @@ __device__ __forceinline__ bool bar_wait(Bar& b, volatile lds_int_t* s_ok) {
 // 8 threads per row (row = tid / 8), column quads q + 8i.  MODE 0: x from the workspace;
 // 1: the token embedding wte[tok] + wpe[pos] (layer 0; WG w also stores rows r % G == w of x);
 // 2: x with the ln_f affine.  The LN affine of ln_1 / ln_2 is folded into c_attn / c_fc.
-template <int MODE>
+// NR rows (64, or 32 for a row-split grid) from row r0, TPR = 512 / NR threads per row, NQ column
+// quads per thread; rows land at LDS row r - r0.  MODE 1 stores x rows r % 48 == w of its range.
+template <int MODE, int NR = RM>
 __device__ __forceinline__ void ln_rows(const Args& a, const Rs& rs, bf16_t* hs, const int* s_tok,
-                                        const int* s_pos, int w, const float* s_lnf = nullptr) {
-  const int tid = otid(), r = tid >> 3, q = tid & 7;
+                                        const int* s_pos, int w, const float* s_lnf = nullptr,
+                                        int r0 = 0) {
+  constexpr int TPR = NT / NR, NQ = D / 4 / TPR;
+  const int tid = otid(), rl = tid / TPR, q = tid % TPR, r = r0 + rl;
   const int rr = min(r, a.R - 1);
-  float4 xv[24];
+  float4 xv[NQ];
   if constexpr (MODE == 1) {
     const bf16_t* te = a.wte + (long)s_tok[r] * D;
     const bf16_t* pe = a.wpe + (long)s_pos[r] * D;
-    // two halves of 12 quads (the bf16 pairs of a half are converted before the next is issued)
+    // halves of NQ / 2 quads (the bf16 pairs of a half are converted before the next is issued)
+    constexpr int HQ = NQ / 2;
 #pragma unroll
     for (int hf = 0; hf < 2; ++hf) {
-      uint2 tu[12], pu[12];
+      uint2 tu[HQ], pu[HQ];
 #pragma unroll
-      for (int i = 0; i < 12; ++i) {
-        tu[i] = *reinterpret_cast<const uint2*>(te + 4 * (q + 8 * (12 * hf + i)));
-        pu[i] = *reinterpret_cast<const uint2*>(pe + 4 * (q + 8 * (12 * hf + i)));
+      for (int i = 0; i < HQ; ++i) {
+        tu[i] = *reinterpret_cast<const uint2*>(te + 4 * (q + TPR * (HQ * hf + i)));
+        pu[i] = *reinterpret_cast<const uint2*>(pe + 4 * (q + TPR * (HQ * hf + i)));
       }
 #pragma unroll
-      for (int i = 0; i < 12; ++i)
-        xv[12 * hf + i] = make_float4(
+      for (int i = 0; i < HQ; ++i)
+        xv[HQ * hf + i] = make_float4(
             __uint_as_float(tu[i].x << 16) + __uint_as_float(pu[i].x << 16),
             __uint_as_float(tu[i].x & 0xffff0000u) + __uint_as_float(pu[i].x & 0xffff0000u),
             __uint_as_float(tu[i].y << 16) + __uint_as_float(pu[i].y << 16),
             __uint_as_float(tu[i].y & 0xffff0000u) + __uint_as_float(pu[i].y & 0xffff0000u));
       __builtin_amdgcn_sched_barrier(0);
     }
-    if (r < a.R && r % G == w) {
+    if (r < a.R && r % 48 == w) {
 #pragma unroll
-      for (int i = 0; i < 24; ++i)
-        st16(rs.x, (r * D + 4 * (q + 8 * i)) * 4, f42u(xv[i].x, xv[i].y, xv[i].z, xv[i].w));
+      for (int i = 0; i < NQ; ++i)
+        st16(rs.x, (r * D + 4 * (q + TPR * i)) * 4, f42u(xv[i].x, xv[i].y, xv[i].z, xv[i].w));
     }
   } else {
 #pragma unroll
-    for (int i = 0; i < 24; ++i) xv[i] = u2f4(ld16(rs.x, (rr * D + 4 * (q + 8 * i)) * 4));
+    for (int i = 0; i < NQ; ++i) xv[i] = u2f4(ld16(rs.x, (rr * D + 4 * (q + TPR * i)) * 4));
   }
   float s = 0.f;
 #pragma unroll
-  for (int i = 0; i < 24; ++i) s += (xv[i].x + xv[i].y) + (xv[i].z + xv[i].w);
-  s += __shfl_xor(s, 1, 64);
-  s += __shfl_xor(s, 2, 64);
-  s += __shfl_xor(s, 4, 64);
+  for (int i = 0; i < NQ; ++i) s += (xv[i].x + xv[i].y) + (xv[i].z + xv[i].w);
+#pragma unroll
+  for (int o = 1; o < TPR; o <<= 1) s += __shfl_xor(s, o, 64);
   const float mean = s * (1.0f / D);
   float qq = 0.f;
 #pragma unroll
-  for (int i = 0; i < 24; ++i) {
+  for (int i = 0; i < NQ; ++i) {
     const float d0 = xv[i].x - mean, d1 = xv[i].y - mean, d2 = xv[i].z - mean, d3 = xv[i].w - mean;
     qq += (d0 * d0 + d1 * d1) + (d2 * d2 + d3 * d3);
   }
-  qq += __shfl_xor(qq, 1, 64);
-  qq += __shfl_xor(qq, 2, 64);
-  qq += __shfl_xor(qq, 4, 64);
+#pragma unroll
+  for (int o = 1; o < TPR; o <<= 1) qq += __shfl_xor(qq, o, 64);
   const float rstd = rsqrtf(qq * (1.0f / D) + 1e-5f);
 #pragma unroll
-  for (int i = 0; i < 24; ++i) {
-    const int c = 4 * (q + 8 * i);
+  for (int i = 0; i < NQ; ++i) {
+    const int c = 4 * (q + TPR * i);
     float y0 = (xv[i].x - mean) * rstd, y1 = (xv[i].y - mean) * rstd;
     float y2 = (xv[i].z - mean) * rstd, y3 = (xv[i].w - mean) * rstd;
     if constexpr (MODE == 2) {   // ln_f params staged in LDS at kernel start (s_lnf)
@@ -306,76 +310,79 @@ __device__ __forceinline__ void ln_rows(const Args& a, const Rs& rs, bf16_t* hs,
       const float4 bb = *reinterpret_cast<const float4*>(s_lnf + D + c);
       y0 = y0 * g.x + bb.x; y1 = y1 * g.y + bb.y; y2 = y2 * g.z + bb.z; y3 = y3 * g.w + bb.w;
     }
-    *reinterpret_cast<uint2*>(hs + r * HLD + c) = make_uint2(pk2bf(y0, y1), pk2bf(y2, y3));
+    *reinterpret_cast<uint2*>(hs + rl * HLD + c) = make_uint2(pk2bf(y0, y1), pk2bf(y2, y3));
   }
 }
 
 // A fragments from the LDS rows, all 4 row blocks, S k-steps from kbase, NB column blocks
-template <int NB, int S>
+template <int NB, int S, int NRB = 4>
 __device__ __forceinline__ void mma_lds(const bf16_t* hs, int kbase, const bf16x8_t (&b)[NB * S],
-                                        f32x4_t (&acc)[4][NB]) {
+                                        f32x4_t (&acc)[NRB][NB]) {
   const int lane = otid() & 63, fr = lane & 15, fk = 8 * (lane >> 4);
 #pragma unroll
-  for (int rb = 0; rb < 4; ++rb)
+  for (int rb = 0; rb < NRB; ++rb)
 #pragma unroll
     for (int nb = 0; nb < NB; ++nb) acc[rb][nb] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int s = 0; s < S; ++s)
 #pragma unroll
-    for (int rb = 0; rb < 4; ++rb) {
+    for (int rb = 0; rb < NRB; ++rb) {
       const bf16x8_t af = *reinterpret_cast<const bf16x8_t*>(hs + (16 * rb + fr) * HLD + kbase + 32 * s + fk);
 #pragma unroll
       for (int nb = 0; nb < NB; ++nb) acc[rb][nb] = mfma(af, b[nb * S + s], acc[rb][nb]);
     }
 }
 
-// partial slab [slab][64][NC] f32: lane's accumulators of NB column blocks from column col0
-template <int NB, int NC>
-__device__ __forceinline__ void put_partial(float* red, int slab, int col0, const f32x4_t (&acc)[4][NB]) {
+// partial slab [slab][16 NRB][NC] f32: lane's accumulators of NB column blocks from column col0
+template <int NB, int NC, int NRB = 4>
+__device__ __forceinline__ void put_partial(float* red, int slab, int col0, const f32x4_t (&acc)[NRB][NB]) {
   const int lane = otid() & 63, fr = lane & 15, r4 = 4 * (lane >> 4);
 #pragma unroll
-  for (int rb = 0; rb < 4; ++rb)
+  for (int rb = 0; rb < NRB; ++rb)
 #pragma unroll
     for (int nb = 0; nb < NB; ++nb)
 #pragma unroll
       for (int i = 0; i < 4; ++i)
-        red[(slab * RM + 16 * rb + r4 + i) * NC + col0 + 16 * nb + fr] = acc[rb][nb][i];
+        red[(slab * 16 * NRB + 16 * rb + r4 + i) * NC + col0 + 16 * nb + fr] = acc[rb][nb][i];
 }
 
 // ------------------------------------------------------------------ phase A: ln_1 + c_attn
+// RH = 1: all 64 rows; RH = 2: the 32 rows of half h (row-split grid)
+template <int RH>
 __device__ __forceinline__ void phase_qkv(const Args& a, const Rs& rs, int l, char* smem,
-                                          const int* s_tok, const int* s_pos, int w,
+                                          const int* s_tok, const int* s_pos, int w, int h,
                                           const bf16x8_t (&wq)[9]) {
+  constexpr int NR = RM / RH, NRB = NR / 16;
   bf16_t* hs = reinterpret_cast<bf16_t*>(smem);
   float* red = reinterpret_cast<float*>(smem);
-  const int tid = otid(), v = tid >> 6;
-  // epilogue quads (issued first): 64 rows x 12 column quads, quads tid and tid + 512
+  const int tid = otid(), v = tid >> 6, r0 = h * NR;
+  // epilogue quads (issued first): NR rows x 12 column quads, quads tid and tid + 512
   const int c0 = 4 * (tid % 12), c1 = 4 * ((tid + 512) % 12);
   const float4 b0 = *reinterpret_cast<const float4*>(a.bqkv[l] + 48 * w + c0);
   const float4 b1 = *reinterpret_cast<const float4*>(a.bqkv[l] + 48 * w + c1);
-  if (l == 0) ln_rows<1>(a, rs, hs, s_tok, s_pos, w);
-  else ln_rows<0>(a, rs, hs, s_tok, s_pos, w);
+  if (l == 0) ln_rows<1, NR>(a, rs, hs, s_tok, s_pos, w, nullptr, r0);
+  else ln_rows<0, NR>(a, rs, hs, s_tok, s_pos, w, nullptr, r0);
   lds_sync();
-  f32x4_t acc[4][3];
-  mma_lds<3, 3>(hs, 96 * v, wq, acc);
+  f32x4_t acc[NRB][3];
+  mma_lds<3, 3, NRB>(hs, 96 * v, wq, acc);
   lds_sync();
-  put_partial<3, 48>(red, v, 0, acc);
+  put_partial<3, 48, NRB>(red, v, 0, acc);
   lds_sync();
 #pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    const int qd = tid + 512 * h;
-    if (qd >= RM * 12) break;
-    const int row = qd / 12, c = h ? c1 : c0;
-    const float4 bb = h ? b1 : b0;
-    float4 s = *reinterpret_cast<const float4*>(red + row * 48 + c);
+  for (int hq = 0; hq < 2; ++hq) {
+    const int qd = tid + 512 * hq;
+    if (qd >= NR * 12) break;
+    const int rl = qd / 12, c = hq ? c1 : c0, row = r0 + rl;
+    const float4 bb = hq ? b1 : b0;
+    float4 sm = *reinterpret_cast<const float4*>(red + rl * 48 + c);
 #pragma unroll
     for (int k = 1; k < NW; ++k) {
-      const float4 p = *reinterpret_cast<const float4*>(red + (k * RM + row) * 48 + c);
-      s.x += p.x; s.y += p.y; s.z += p.z; s.w += p.w;
+      const float4 p = *reinterpret_cast<const float4*>(red + (k * NR + rl) * 48 + c);
+      sm.x += p.x; sm.y += p.y; sm.z += p.z; sm.w += p.w;
     }
     if (row < a.R)
       st8(rs.qkv, (row * QKVN + 48 * w + c) * 2,
-          u32x2_t{pk2bf(s.x + bb.x, s.y + bb.y), pk2bf(s.z + bb.z, s.w + bb.w)});
+          u32x2_t{pk2bf(sm.x + bb.x, sm.y + bb.y), pk2bf(sm.z + bb.z, sm.w + bb.w)});
   }
 }
 
@@ -395,25 +402,28 @@ __device__ __forceinline__ uint4 tou4(u32x4_t u) { return make_uint4(u.x, u.y, u
 // (lane sub holds dims 8 sub .. 8 sub + 8), online softmax in f32 (decode_attn6 arithmetic).
 // The cached keys of the first chunk do not depend on this step's activations: attn_load issues
 // them BEFORE the workgroup waits on the c_attn barrier (kr / vr held across it).
-__device__ __forceinline__ void attn_unit(const Args& a, const int* s_pos, int w, int v, int k,
+// unit u = (row u / 12, head u % 12); wave v of a workgroup whose first unit is ub takes units
+// ub + KU v .. + KU (KU = 2: 16 units per workgroup of a 48-grid; 1: 8 per workgroup of a row
+// half, 96-grid)
+__device__ __forceinline__ void attn_unit(const Args& a, const int* s_pos, int u,
                                           int& row, int& hh, int& p, long& base) {
-  const int u = 16 * w + 2 * v + k;
   row = u / NH;
   hh = u % NH;
   const int rr = min(row, a.R - 1);
   p = min(s_pos[rr], a.Lmax - 1);
   base = ((long)(rr * NH + hh) * a.Lmax) * HD + 8 * ((otid() & 63) & 7);
 }
-__device__ __forceinline__ void attn_load(const Args& a, int l, const int* s_pos, int w, int cb,
-                                          uint4 (&kr)[2][8], uint4 (&vr)[2][8]) {
+template <int KU>
+__device__ __forceinline__ void attn_load(const Args& a, int l, const int* s_pos, int ub, int cb,
+                                          uint4 (&kr)[KU][8], uint4 (&vr)[KU][8]) {
   const int tid = otid(), v = tid >> 6, grp = (tid & 63) >> 3;
   const bf16_t* kc = a.kc[l];
   const bf16_t* vc = a.vc[l];
 #pragma unroll
-  for (int k = 0; k < 2; ++k) {
+  for (int k = 0; k < KU; ++k) {
     int row, hh, p;
     long base;
-    attn_unit(a, s_pos, w, v, k, row, hh, p, base);
+    attn_unit(a, s_pos, ub + KU * v + k, row, hh, p, base);
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       const int jc = max(min(cb + 8 * i + grp, p - 1), 0);
@@ -424,16 +434,17 @@ __device__ __forceinline__ void attn_load(const Args& a, int l, const int* s_pos
 }
 // The new token (key pos, from qkv) is folded in after the cached keys 0..pos-1 (one more
 // online-softmax update with its score and v), so the cached chunks need no per-key selects.
-__device__ __forceinline__ void phase_attn(const Args& a, const Rs& rs, int l, const int* s_pos, int w,
-                                           uint4 (&kr)[2][8], uint4 (&vr)[2][8]) {
+template <int KU>
+__device__ __forceinline__ void phase_attn(const Args& a, const Rs& rs, int l, const int* s_pos, int ub,
+                                           uint4 (&kr)[KU][8], uint4 (&vr)[KU][8]) {
   const int tid = otid(), lane = tid & 63, v = tid >> 6, grp = lane >> 3, sub = lane & 7;
-  float q[2][8], o[2][8], m[2], sum[2];
-  uint4 knu[2], vnu[2];
-  int p[2], row[2], hh[2];
-  long base[2];
+  float q[KU][8], o[KU][8], m[KU], sum[KU];
+  uint4 knu[KU], vnu[KU];
+  int p[KU], row[KU], hh[KU];
+  long base[KU];
 #pragma unroll
-  for (int k = 0; k < 2; ++k) {
-    attn_unit(a, s_pos, w, v, k, row[k], hh[k], p[k], base[k]);
+  for (int k = 0; k < KU; ++k) {
+    attn_unit(a, s_pos, ub + KU * v + k, row[k], hh[k], p[k], base[k]);
     const int off = (min(row[k], a.R - 1) * QKVN + hh[k] * HD + 8 * sub) * 2;
     const uint4 qu = tou4(ld16(rs.qkv, off));
     knu[k] = tou4(ld16(rs.qkv, off + 2 * D));
@@ -444,11 +455,13 @@ __device__ __forceinline__ void phase_attn(const Args& a, const Rs& rs, int l, c
     m[k] = -INFINITY;
     sum[k] = 0.f;
   }
-  const int pmax = max(p[0], p[1]);
-  for (int cb = 0; cb < pmax; cb += 64) {       // cached keys 0 .. p - 1
-    if (cb > 0) attn_load(a, l, s_pos, w, cb, kr, vr);
+  int pmax = p[0];
 #pragma unroll
-    for (int k = 0; k < 2; ++k) {
+  for (int k = 1; k < KU; ++k) pmax = max(pmax, p[k]);
+  for (int cb = 0; cb < pmax; cb += 64) {       // cached keys 0 .. p - 1
+    if (cb > 0) attn_load<KU>(a, l, s_pos, ub, cb, kr, vr);
+#pragma unroll
+    for (int k = 0; k < KU; ++k) {
       if (cb >= p[k]) continue;                   // wave-uniform
       float sc[8];
       float pm = -INFINITY;
@@ -484,7 +497,7 @@ __device__ __forceinline__ void phase_attn(const Args& a, const Rs& rs, int l, c
     }
   }
 #pragma unroll
-  for (int k = 0; k < 2; ++k) {
+  for (int k = 0; k < KU; ++k) {
     // over the 8 key groups (lanes sub, sub + 8, ..): same additions on every lane
     sum[k] = add32(add16(sum[k] + xor8(sum[k])));
 #pragma unroll
@@ -521,63 +534,65 @@ __device__ __forceinline__ void phase_attn(const Args& a, const Rs& rs, int l, c
 // x[:, 16w .. 16w + 16) += A W^T + b, A = att (K 768) or hid (K 3072) from the workspace in
 // A-fragment order; wave v takes k-steps [v S, (v+1) S), its A fragments in chunks of 4 k-steps
 // (two chunks in flight), each fragment load one contiguous KiB
-template <int S>
+template <int S, int RH = 1>
 __device__ __forceinline__ void phase_proj(const Args& a, const Rs& rs, __amdgpu_buffer_rsrc_t ra,
-                                           int K, const float* bias, char* smem, int w,
+                                           int K, const float* bias, char* smem, int w, int h,
                                            const bf16x8_t (&wb)[S]) {
+  constexpr int NR = RM / RH, NRB = NR / 16;
   float* red = reinterpret_cast<float*>(smem);
-  const int tid = otid(), lane = tid & 63, v = tid >> 6;
-  // epilogue operands first: 64 rows x 4 quads on threads 0..255
-  const int erow = (tid >> 2) & 63, ec = 16 * w + 4 * (tid & 3);
+  const int tid = otid(), lane = tid & 63, v = tid >> 6, r0 = h * NR;
+  // epilogue operands first: NR rows x 4 quads on threads 0 .. 4 NR - 1
+  const int erl = (tid >> 2) & (NR - 1), erow = r0 + erl, ec = 16 * w + 4 * (tid & 3);
   float4 eb = make_float4(0.f, 0.f, 0.f, 0.f), ex = eb;
-  if (tid < 256) {
+  if (tid < 4 * NR) {
     eb = *reinterpret_cast<const float4*>(bias + ec);
     ex = u2f4(ld16(rs.x, (min(erow, a.R - 1) * D + ec) * 4));
   }
-  // fragment (rb, k-step s) of this lane at ((rb * K/32 + s) * 64 + lane) * 16 bytes
-  int aoff[4];
+  // fragment (row block rb of the workgroup's rows, k-step s) of this lane at
+  // (((r0 / 16 + rb) * K/32 + s) * 64 + lane) * 16 bytes
+  int aoff[NRB];
 #pragma unroll
-  for (int rb = 0; rb < 4; ++rb) aoff[rb] = ((rb * (K / 32) + v * S) * 64 + lane) * 16;
-  f32x4_t acc[4];
+  for (int rb = 0; rb < NRB; ++rb) aoff[rb] = (((r0 / 16 + rb) * (K / 32) + v * S) * 64 + lane) * 16;
+  f32x4_t acc[NRB];
 #pragma unroll
-  for (int rb = 0; rb < 4; ++rb) acc[rb] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  for (int rb = 0; rb < NRB; ++rb) acc[rb] = f32x4_t{0.f, 0.f, 0.f, 0.f};
   constexpr int CH = 4;                      // k-steps per chunk
   constexpr int NCH = (S + CH - 1) / CH;
-  u32x4_t af[NCH][4 * CH];
+  u32x4_t af[NCH][NRB * CH];
 #pragma unroll
   for (int c = 0; c < NCH && c < 2; ++c)
 #pragma unroll
     for (int s = 0; s < CH; ++s)
 #pragma unroll
-      for (int rb = 0; rb < 4; ++rb)
-        if (c * CH + s < S) af[c][s * 4 + rb] = ld16(ra, aoff[rb] + 1024 * (c * CH + s));
+      for (int rb = 0; rb < NRB; ++rb)
+        if (c * CH + s < S) af[c][s * NRB + rb] = ld16(ra, aoff[rb] + 1024 * (c * CH + s));
 #pragma unroll
   for (int c = 0; c < NCH; ++c) {
 #pragma unroll
     for (int s = 0; s < CH; ++s)
 #pragma unroll
-      for (int rb = 0; rb < 4; ++rb)
-        if (c * CH + s < S) acc[rb] = mfma(bf8(af[c][s * 4 + rb]), wb[c * CH + s], acc[rb]);
+      for (int rb = 0; rb < NRB; ++rb)
+        if (c * CH + s < S) acc[rb] = mfma(bf8(af[c][s * NRB + rb]), wb[c * CH + s], acc[rb]);
     if (c + 2 < NCH) {
 #pragma unroll
       for (int s = 0; s < CH; ++s)
 #pragma unroll
-        for (int rb = 0; rb < 4; ++rb)
-          if ((c + 2) * CH + s < S) af[c + 2][s * 4 + rb] = ld16(ra, aoff[rb] + 1024 * ((c + 2) * CH + s));
+        for (int rb = 0; rb < NRB; ++rb)
+          if ((c + 2) * CH + s < S) af[c + 2][s * NRB + rb] = ld16(ra, aoff[rb] + 1024 * ((c + 2) * CH + s));
     }
   }
-  put_partial<1, 16>(red, v, 0, reinterpret_cast<const f32x4_t(&)[4][1]>(acc));
+  put_partial<1, 16, NRB>(red, v, 0, reinterpret_cast<const f32x4_t(&)[NRB][1]>(acc));
   lds_sync();
-  if (tid < 256) {
-    float4 s = *reinterpret_cast<const float4*>(red + erow * 16 + 4 * (tid & 3));
+  if (tid < 4 * NR) {
+    float4 sm = *reinterpret_cast<const float4*>(red + erl * 16 + 4 * (tid & 3));
 #pragma unroll
     for (int k = 1; k < NW; ++k) {
-      const float4 p = *reinterpret_cast<const float4*>(red + (k * RM + erow) * 16 + 4 * (tid & 3));
-      s.x += p.x; s.y += p.y; s.z += p.z; s.w += p.w;
+      const float4 p = *reinterpret_cast<const float4*>(red + (k * NR + erl) * 16 + 4 * (tid & 3));
+      sm.x += p.x; sm.y += p.y; sm.z += p.z; sm.w += p.w;
     }
     if (erow < a.R)
       st16(rs.x, (erow * D + ec) * 4,
-           f42u(s.x + eb.x + ex.x, s.y + eb.y + ex.y, s.z + eb.z + ex.z, s.w + eb.w + ex.w));
+           f42u(sm.x + eb.x + ex.x, sm.y + eb.y + ex.y, sm.z + eb.z + ex.z, sm.w + eb.w + ex.w));
   }
 }
 
@@ -586,42 +601,44 @@ __device__ __forceinline__ float gelu_new_fast(float x) {
   const float u2 = -1.5957691216057308f * (x + 0.044715f * x * x * x);
   return x * __builtin_amdgcn_rcpf(1.0f + __expf(u2));
 }
+template <int RH = 1>
 __device__ __forceinline__ void phase_fc(const Args& a, const Rs& rs, int l, char* smem,
-                                         const int* s_tok, const int* s_pos, int w,
+                                         const int* s_tok, const int* s_pos, int w, int h,
                                          const bf16x8_t (&wf)[12]) {
+  constexpr int NR = RM / RH, NRB = NR / 16;
   bf16_t* hs = reinterpret_cast<bf16_t*>(smem);
   float* red = reinterpret_cast<float*>(smem);
-  const int tid = otid(), v = tid >> 6, cg = v >> 2, kq = v & 3;
-  // epilogue: 64 rows x 16 quads, quads tid and tid + 512 (same column quad)
+  const int tid = otid(), v = tid >> 6, cg = v >> 2, kq = v & 3, r0 = h * NR;
+  // epilogue: NR rows x 16 quads, quads tid and tid + 512 (same column quad)
   const int c = 4 * (tid & 15);
   const float4 bb = *reinterpret_cast<const float4*>(a.bfc[l] + 64 * w + c);
-  ln_rows<0>(a, rs, hs, s_tok, s_pos, w);
+  ln_rows<0, NR>(a, rs, hs, s_tok, s_pos, w, nullptr, r0);
   lds_sync();
-  f32x4_t acc[4][2];
-  mma_lds<2, 6>(hs, 192 * kq, wf, acc);
+  f32x4_t acc[NRB][2];
+  mma_lds<2, 6, NRB>(hs, 192 * kq, wf, acc);
   lds_sync();
-  put_partial<2, 64>(red, kq, 32 * cg, acc);
+  put_partial<2, 64, NRB>(red, kq, 32 * cg, acc);
   lds_sync();
 #pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    const int row = (tid >> 4) + 32 * h;
-    float4 s = *reinterpret_cast<const float4*>(red + row * 64 + c);
+  for (int hq = 0; hq < NR / 32; ++hq) {
+    const int rl = (tid >> 4) + 32 * hq, row = r0 + rl;
+    float4 sm = *reinterpret_cast<const float4*>(red + rl * 64 + c);
 #pragma unroll
     for (int k = 1; k < 4; ++k) {
-      const float4 p = *reinterpret_cast<const float4*>(red + (k * RM + row) * 64 + c);
-      s.x += p.x; s.y += p.y; s.z += p.z; s.w += p.w;
+      const float4 p = *reinterpret_cast<const float4*>(red + (k * NR + rl) * 64 + c);
+      sm.x += p.x; sm.y += p.y; sm.z += p.z; sm.w += p.w;
     }
     // hid in A-fragment order: column k = 64 w + c -> k-step k / 32, lane (row & 15) + 16 ((k / 8) & 3)
     const int k = 64 * w + c;
     if (row < a.R)
       st8(rs.hid, ((((row >> 4) * (DFF / 32) + (k >> 5)) * 64 + (row & 15) + 16 * ((k >> 3) & 3)) * 8 + (k & 7)) * 2,
-          u32x2_t{pk2bf(gelu_new_fast(s.x + bb.x), gelu_new_fast(s.y + bb.y)),
-                  pk2bf(gelu_new_fast(s.z + bb.z), gelu_new_fast(s.w + bb.w))});
+          u32x2_t{pk2bf(gelu_new_fast(sm.x + bb.x), gelu_new_fast(sm.y + bb.y)),
+                  pk2bf(gelu_new_fast(sm.z + bb.z), gelu_new_fast(sm.w + bb.w))});
   }
 }
 
 // ------------------------------------------------------------------ phase F: ln_f + LM head
-// vocab blocks of 16 rows [w nvb / G, (w+1) nvb / G) of this WG, taken in PAIRS (one A fragment
+// vocab blocks of 16 rows [wg nvb / gg, (wg+1) nvb / gg) of this WG (gg = the grid), taken in PAIRS (one A fragment
 // read from LDS feeds the MFMAs of both blocks: half the LDS traffic per MFMA); wave v takes
 // pairs v, v + 8, ..  A pair's weights (wtep: 24 KiB contiguous per block, one KiB per k-step in
 // B-fragment order) arrive as six 4-k-step pieces (both blocks) through a 3-slot register ring:
@@ -666,14 +683,14 @@ __device__ __forceinline__ void lm_consume(const bf16_t* hs, int c, const bf16x8
   }
 }
 __device__ __forceinline__ void phase_lm(const Args& a, const Rs& rs, char* smem, const int* s_tok,
-                                         const int* s_pos, float* am_v, int* am_i, int w,
+                                         const int* s_pos, float* am_v, int* am_i, int wg, int gg,
                                          gu64* keys, const float* s_lnf) {
   bf16_t* hs = reinterpret_cast<bf16_t*>(smem);
   const int tid = otid(), lane = tid & 63, v = tid >> 6, fr = lane & 15, r4 = 4 * (lane >> 4);
-  ln_rows<2>(a, rs, hs, s_tok, s_pos, w, s_lnf);
+  ln_rows<2>(a, rs, hs, s_tok, s_pos, wg, s_lnf);
   lds_sync();
   const int nvb = (a.V + 15) / 16;
-  const int b_lo = (int)((long)w * nvb / G), b_hi = (int)((long)(w + 1) * nvb / G);
+  const int b_lo = (int)((long)wg * nvb / gg), b_hi = (int)((long)(wg + 1) * nvb / gg);
   const int npair = (b_hi - b_lo + 1) / 2;              // the last pair may hold one block
   const int npw = (npair - v + NW - 1) / NW;            // pairs of this wave (>= 1)
   float bv[16];
@@ -765,6 +782,12 @@ __device__ __forceinline__ void gave_up(const Args& a) {
 }
 
 // ------------------------------------------------------------------ the kernel
+// RH = 1: G = 48 workgroups, each owns a column slice of every GEMM for all 64 rows; RH = 2 (the
+// row-split grid, 96 workgroups): workgroup (w, h) = the same column slice for rows 32 h .. + 32
+// (half the handed-off activation bytes per workgroup, the same weights: blocks b and b + 8 --
+// one XCD under round-robin dispatch, speed only -- hold the two halves of a slice), the attention
+// units of its rows, and 1/96 of the LM head's vocabulary for all rows.
+template <int RH>
 __global__ __launch_bounds__(NT) void decode_persist_kernel(Args a) {
   __shared__ __attribute__((aligned(16))) char smem[SM_TOTAL];
   float* am_v = reinterpret_cast<float*>(smem + SM_HS);
@@ -773,13 +796,16 @@ __global__ __launch_bounds__(NT) void decode_persist_kernel(Args a) {
   int* s_pos = s_tok + RM;
   int* s_done = s_pos + RM;
   int* s_misc = s_done + RM;     // [0] rows still decoding, [8] barrier ok flag
-  const int w = blockIdx.x;
+  constexpr int GG = G * RH;
+  const int wg = blockIdx.x;
+  const int w = RH == 1 ? wg : (wg & 7) + 8 * (wg >> 4), h = RH == 1 ? 0 : (wg >> 3) & 1;
+  const int ub = RH == 1 ? 16 * w : 384 * h + 8 * w;    // first attention unit of this workgroup
   Rs rs;
   rs.x = mk(a.ws + WS_X, RM * D * 4);
   rs.qkv = mk(a.ws + WS_QKV, RM * QKVN * 2);
   rs.att = mk(a.ws + WS_ATT, RM * D * 2);
   rs.hid = mk(a.ws + WS_HID, RM * DFF * 2);
-  Bar bar{(gu32*)(a.ws + WS_SYNC), (gu32*)(a.ws + WS_SYNC + 4), 0, nullptr, 0};
+  Bar bar{(gu32*)(a.ws + WS_SYNC), (gu32*)(a.ws + WS_SYNC + 4), 0, nullptr, 0, GG};
   gu64* const lmkey = (gu64*)(a.ws + WS_LMKEY);
   unsigned long long* const stamps = dp_stamp_buf;
   const int stamp_step = dp_stamp_step;
@@ -806,35 +832,35 @@ __global__ __launch_bounds__(NT) void decode_persist_kernel(Args a) {
 #define V_ (otid() >> 6)
   load_w<3, 3>(a.wqkv[0], D, 48 * w, QKVN, 96 * V_, wq);
   for (;;) {
-    bar.sb = (stamps != nullptr && step == stamp_step) ? stamps + (long)w * 2 * DP_NB : nullptr;
+    bar.sb = (stamps != nullptr && step == stamp_step) ? stamps + (long)wg * 2 * DP_NB : nullptr;
     bar.n0 = bar.n;
     stamp(bar.sb, 2 * DP_NB - 1);   // step start
     for (int l = 0; l < NLY; ++l) {
-      phase_qkv(a, rs, l, smem, s_tok, s_pos, w, wq);
+      phase_qkv<RH>(a, rs, l, smem, s_tok, s_pos, w, h, wq);
       bar_arrive(bar);
-      uint4 kr[2][8], vr[2][8];
-      attn_load(a, l, s_pos, w, 0, kr, vr);
+      uint4 kr[2 / RH][8], vr[2 / RH][8];
+      attn_load<2 / RH>(a, l, s_pos, ub, 0, kr, vr);
       if (!bar_wait(bar, s_ok)) return gave_up(a);
-      if (l == 0 && w == 0 && otid() < RM)   // the previous step's argmax keys: every WG has read them
+      if (l == 0 && wg == 0 && otid() < RM)  // the previous step's argmax keys: every WG has read them
         __hip_atomic_store(lmkey + ((step + 1) & 1) * RM + otid(), 0ull, __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
 
-      phase_attn(a, rs, l, s_pos, w, kr, vr);
+      phase_attn<2 / RH>(a, rs, l, s_pos, ub, kr, vr);
       bar_arrive(bar);
       load_w<1, 3>(a.wproj[l], D, 16 * w, D, 96 * V_, wp);
       load_w<2, 6>(a.wfc[l], D, 64 * w + 32 * (V_ >> 2), DFF, 192 * (V_ & 3), wf);
       if (!bar_wait(bar, s_ok)) return gave_up(a);
 
-      phase_proj<3>(a, rs, rs.att, D, a.bproj[l], smem, w, wp);
+      phase_proj<3, RH>(a, rs, rs.att, D, a.bproj[l], smem, w, h, wp);
       bar_arrive(bar);
       if (!bar_wait(bar, s_ok)) return gave_up(a);
 
-      phase_fc(a, rs, l, smem, s_tok, s_pos, w, wf);
+      phase_fc<RH>(a, rs, l, smem, s_tok, s_pos, w, h, wf);
       bar_arrive(bar);
       load_w<1, 12>(a.wmp[l], DFF, 16 * w, D, 384 * V_, wm);
       if (!bar_wait(bar, s_ok)) return gave_up(a);
 
-      phase_proj<12>(a, rs, rs.hid, DFF, a.bmp[l], smem, w, wm);
+      phase_proj<12, RH>(a, rs, rs.hid, DFF, a.bmp[l], smem, w, h, wm);
       bar_arrive(bar);
       // next block's c_attn.  Unconditional (a conditional load keeps the old wq live through
       // the whole block for the path that skips it); after block 11 the value is dead and wq is
@@ -842,7 +868,7 @@ __global__ __launch_bounds__(NT) void decode_persist_kernel(Args a) {
       load_w<3, 3>(a.wqkv[l + 1 < NLY ? l + 1 : 0], D, 48 * w, QKVN, 96 * V_, wq);
       if (!bar_wait(bar, s_ok)) return gave_up(a);
     }
-    phase_lm(a, rs, smem, s_tok, s_pos, am_v, am_i, w, lmkey + (step & 1) * RM, s_lnf);
+    phase_lm(a, rs, smem, s_tok, s_pos, am_v, am_i, wg, GG, lmkey + (step & 1) * RM, s_lnf);
     bar_arrive(bar);
     load_w<3, 3>(a.wqkv[0], D, 48 * w, QKVN, 96 * V_, wq);
     if (!bar_wait(bar, s_ok)) return gave_up(a);
@@ -859,7 +885,7 @@ __global__ __launch_bounds__(NT) void decode_persist_kernel(Args a) {
         if (tid < a.R) {
           int d = s_done[tid];
           if (!d) {
-            if (w == 0) {
+            if (wg == 0) {
               a.out_ids[(long)tid * a.max_steps + step] = t;
               a.out_len[tid] = step + 1;
             }
@@ -881,7 +907,7 @@ __global__ __launch_bounds__(NT) void decode_persist_kernel(Args a) {
     const bool fin = total == 0 || step + 1 >= a.max_steps;
     if (fin) {
       const int tid = otid();
-      if (w == 0) {
+      if (wg == 0) {
         if (tid < a.R) {
           a.done[tid] = s_done[tid];
           a.pos[tid] = s_pos[tid];
@@ -914,10 +940,12 @@ extern "C" int zs_gpt2_decode_persist(int R, int Lmax, int max_steps, int stop0,
                                       const float* lnf_w, const float* lnf_b, void* const* kv,
                                       int* pos, int* next_tok, int* done, int* out_ids,
                                       int* out_len, int* step_ctr, int* all_done, void* ws,
-                                      long ws_bytes, void* stream) {
+                                      long ws_bytes, int row_split, void* stream) {
   using namespace dpk;
+  ZS_REQUIRE(row_split == 1 || row_split == 2, "zs_gpt2_decode_persist: row_split 1 or 2 (got %d)",
+             row_split);
   ZS_REQUIRE(R >= 1 && R <= RM, "zs_gpt2_decode_persist: R in 1..%d (got %d)", RM, R);
-  ZS_REQUIRE(V >= 16 * NW * G && V <= 1 << 24, "zs_gpt2_decode_persist: vocab %d", V);
+  ZS_REQUIRE(V >= 32 * NW * G * row_split && V <= 1 << 24, "zs_gpt2_decode_persist: vocab %d", V);
   ZS_REQUIRE(Lmax >= 2 && max_steps >= 1, "zs_gpt2_decode_persist: Lmax %d max_steps %d", Lmax, max_steps);
   ZS_REQUIRE(ws && ws_bytes >= WS_BYTES && ((uintptr_t)ws & 255) == 0,
              "zs_gpt2_decode_persist: workspace of %d bytes, 256-byte aligned", WS_BYTES);
@@ -947,7 +975,10 @@ extern "C" int zs_gpt2_decode_persist(int R, int Lmax, int max_steps, int stop0,
   a.step_ctr = step_ctr; a.all_done = all_done; a.ws = (char*)ws;
   // the barrier counter and timeout word: zeroed before every launch (a memset node under capture)
   ZS_CHECK_HIP(hipMemsetAsync(ws, 0, WS_SYNC_BYTES, S(stream)));
-  hipLaunchKernelGGL(decode_persist_kernel, dim3(G), dim3(NT), 0, S(stream), a);
+  if (row_split == 2)
+    hipLaunchKernelGGL(decode_persist_kernel<2>, dim3(2 * G), dim3(NT), 0, S(stream), a);
+  else
+    hipLaunchKernelGGL(decode_persist_kernel<1>, dim3(G), dim3(NT), 0, S(stream), a);
   ZS_LAUNCH_CHECK();
   return 0;
 }

@@ -293,6 +293,164 @@ __global__ __launch_bounds__(64 * WAVES) void fp8_gemm_stream_kernel(
   }
 }
 
+// Run kernel (decode, M <= 32): one workgroup per (128-column tile, run of KS consecutive 1024-deep
+// k splits), the run's products summed in registers, so a GEMM writes nsplit / KS partial slabs
+// instead of nsplit.  Per split the activation chunk is loaded into registers first and the
+// split's weight fragments after it (loads return in order), both one split AHEAD of the MFMAs:
+// the chunk lands in one of two LDS buffers while the previous split computes from the other, and
+// the weight stream of a run never drains.  GLU (KS = nsplit: each workgroup holds complete sums):
+// the gate|up matrix is packed with gate and up columns interleaved by 4 (zsaac/mistral.py
+// glu_interleave: in every 16-column group, lanes of column quad g = 0 / 2 hold gate columns
+// 8 grp + 0..3 / 4..7 and quads 1 / 3 the matching up columns), so lane l's partner is lane l ^ 16
+// and the epilogue writes act = silu(gate) * up (bf16, F = N / 2 columns) itself -- no slab, no
+// consumer launch (predict_mistralai_multilingual.py's MistralMLP: down(silu(gate(x)) * up(x))).
+template <int KH>
+struct F8Run {
+  static constexpr int WAVES = 8, NTHR = 512, KC = F8_KC / KH, JB = KC / 64, LDA_S = KC + 8;
+  static constexpr int PER_ROW = KC / 8, AMAX = 32 * PER_ROW / NTHR;   // M <= 32
+  static constexpr int LDS_BYTES = 2 * 32 * LDA_S * 2;
+};
+
+template <int KH>
+__device__ __forceinline__ void f8r_load_a(uint4 (&av)[F8Run<KH>::AMAX],
+                                           const bf16_t* __restrict__ A, int lda, int M, int k0) {
+  using P = F8Run<KH>;
+#pragma unroll
+  for (int t = 0; t < P::AMAX; ++t) {
+    const int i = threadIdx.x + t * P::NTHR;
+    const int m = min(i / P::PER_ROW, M - 1), c = (i % P::PER_ROW) * 8;
+    av[t] = *reinterpret_cast<const uint4*>(A + (long)m * lda + k0 + c);
+  }
+}
+
+// KH = 2: each workgroup takes one half (512 k) of every split of its run -- twice the workgroups
+// and slabs for the short streams (o: 32 tiles x 4 splits = 128 workgroups -> 256)
+// rss != NULL: A holds the un-normalised rows x (bf16) of an RMSNorm whose weight is folded into
+// W, and rss [nch][32] their partial sums of squares (zs_mistral_add_ss); each output row is
+// scaled by rsqrt(sum / K + eps) in the epilogue (the norm's per-row factor moved past the GEMM).
+template <int KS, int KH, bool GLU, bool RS>
+__global__ __launch_bounds__(512) void fp8_gemm_run_kernel(
+    const bf16_t* __restrict__ A, int lda, const uint8_t* __restrict__ W8,
+    const float* __restrict__ scale, int M, int N, int K, float* __restrict__ out,
+    long split_stride, int ldo, bf16_t* __restrict__ act, int ld_act, int ntiles,
+    const float* __restrict__ rss, int nch, float eps) {
+  using P = F8Run<KH>;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  bf16_t* as = reinterpret_cast<bf16_t*>(smem);                 // [2][32][LDA_S]
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, fr = lane & 15, g = lane >> 4;
+  const int tile = blockIdx.x % ntiles, rh = blockIdx.x / ntiles;
+  const int run = rh / KH, hf = rh % KH, s0 = run * KS;
+  const uint8_t* wr0 = f8_frag(W8, ntiles, s0, tile * P::WAVES + wid, lane) + 1024 * P::JB * hf;
+  const long split_bytes = (long)ntiles * 128 * 1024;           // one split of every tile
+  const int n = tile * 128 + wid * 16 + 4 * g;
+  uint4 av[P::AMAX];
+  u32x4m_t wv[2][P::JB];
+  f8r_load_a<KH>(av, A, lda, M, s0 * F8_KC + hf * P::KC);
+#pragma unroll
+  for (int j = 0; j < P::JB; ++j)
+    wv[0][j] = __builtin_nontemporal_load(reinterpret_cast<const u32x4m_t*>(wr0 + 1024 * j));
+  const float4 sc = *reinterpret_cast<const float4*>(scale + min(n, N - 4));
+  // the norm's partial sums of squares of the lane's two rows (issued behind split 0's weights,
+  // waited for in the epilogue only); chunks past nch read chunk nch - 1 and are not summed
+  float rq[2][8];
+  if constexpr (RS) {
+#pragma unroll
+    for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+      for (int c = 0; c < 8; ++c) rq[rb][c] = rss[min(c, nch - 1) * 32 + min(rb * 16 + fr, M - 1)];
+  }
+  f32x4m_t acc[2] = {f32x4m_t{0.f, 0.f, 0.f, 0.f}, f32x4m_t{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+  for (int t = 0; t < KS; ++t) {
+    bf16_t* ab = as + (t & 1) * 32 * P::LDA_S;
+    // chunk t -> LDS (the compiler's counted wait covers the chunk's loads only: split t's
+    // weights and anything issued after stay in flight)
+#pragma unroll
+    for (int u = 0; u < P::AMAX; ++u) {
+      const int i = threadIdx.x + u * P::NTHR;
+      *reinterpret_cast<uint4*>(ab + (i / P::PER_ROW) * P::LDA_S + (i % P::PER_ROW) * 8) = av[u];
+    }
+    if (t + 1 < KS) {                                            // split t + 1 in flight
+      f8r_load_a<KH>(av, A, lda, M, (s0 + t + 1) * F8_KC + hf * P::KC);
+      const uint8_t* wr = wr0 + (t + 1) * split_bytes;
+#pragma unroll
+      for (int j = 0; j < P::JB; ++j)
+        wv[(t + 1) & 1][j] = __builtin_nontemporal_load(reinterpret_cast<const u32x4m_t*>(wr + 1024 * j));
+    }
+    // LDS hand-off without waiting on vector memory (a __syncthreads would drain split t + 1)
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int j = 0; j < P::JB; ++j) {
+      const u32x4m_t w = wv[t & 1][j];
+      const bf16x2m_t p0 = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(w.x, 1.0f, false);
+      const bf16x2m_t p1 = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(w.x, 1.0f, true);
+      const bf16x2m_t p2 = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(w.y, 1.0f, false);
+      const bf16x2m_t p3 = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(w.y, 1.0f, true);
+      const bf16x8m_t b0 = bf16x8m_t{p0[0], p0[1], p1[0], p1[1], p2[0], p2[1], p3[0], p3[1]};
+      const bf16x2m_t q0 = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(w.z, 1.0f, false);
+      const bf16x2m_t q1 = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(w.z, 1.0f, true);
+      const bf16x2m_t q2 = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(w.w, 1.0f, false);
+      const bf16x2m_t q3 = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(w.w, 1.0f, true);
+      const bf16x8m_t b1 = bf16x8m_t{q0[0], q0[1], q1[0], q1[1], q2[0], q2[1], q3[0], q3[1]};
+      const int ka = 64 * j + 16 * g;
+#pragma unroll
+      for (int rb = 0; rb < 2; ++rb) {
+        const int m = rb * 16 + fr;             // LDS rows past M hold row M - 1 (clamped loads)
+        const bf16x8m_t a0 = *reinterpret_cast<const bf16x8m_t*>(ab + m * P::LDA_S + ka);
+        const bf16x8m_t a1 = *reinterpret_cast<const bf16x8m_t*>(ab + m * P::LDA_S + ka + 8);
+        acc[rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b0, a0, acc[rb], 0, 0, 0);
+        acc[rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b1, a1, acc[rb], 0, 0, 0);
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  // lane -> row m = 16 rb + fr, columns n .. n + 3 (transposed product, as the one-shot kernel)
+  if constexpr (RS) {
+#pragma unroll
+    for (int rb = 0; rb < 2; ++rb) {
+      float q = 0.f;
+#pragma unroll
+      for (int c = 0; c < 8; ++c) q += c < nch ? rq[rb][c] : 0.f;
+      const float r = rsqrtf(q / K + eps);
+      acc[rb][0] *= r; acc[rb][1] *= r; acc[rb][2] *= r; acc[rb][3] *= r;
+    }
+  }
+  if constexpr (GLU) {
+#pragma unroll
+    for (int rb = 0; rb < 2; ++rb) {
+      float gv[4], uv[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float mine = acc[rb][i] * (i == 0 ? sc.x : i == 1 ? sc.y : i == 2 ? sc.z : sc.w);
+        const float other = __shfl_xor(mine, 16, 64);
+        gv[i] = (g & 1) ? other : mine;
+        uv[i] = (g & 1) ? mine : other;
+      }
+      const int m = rb * 16 + fr;
+      if (!(g & 1) && m < M && n < N) {
+        const int f = 8 * (tile * P::WAVES + wid) + 4 * (g >> 1);
+        float o[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) o[i] = gv[i] / (1.0f + expf(-gv[i])) * uv[i];   // F.silu * up
+        st4(act + (long)m * ld_act + f, o[0], o[1], o[2], o[3]);
+      }
+    }
+  } else {
+    if (n >= N) return;
+    float* o = out + rh * split_stride;
+#pragma unroll
+    for (int rb = 0; rb < 2; ++rb) {
+      const int m = rb * 16 + fr;
+      if (m < M)
+        *reinterpret_cast<float4*>(o + (long)m * ldo + n) =
+            make_float4(acc[rb][0] * sc.x, acc[rb][1] * sc.y, acc[rb][2] * sc.z, acc[rb][3] * sc.w);
+    }
+  }
+}
+
 // Prefill (M > 64 rows) helpers: the tile-packed fp8 codes of one weight matrix unpacked to
 // row-major bf16 [N][K] (exact: e4m3 -> bf16 is lossless, the scale is NOT applied) for the
 // tiled bf16 MFMA GEMM, whose f32 result columns are then scaled (out[m][n] *= scale[n]).  The
@@ -410,6 +568,31 @@ __global__ __launch_bounds__(1024) void mistral_add_rmsnorm_kernel(
   }
 }
 
+// Decode form of the residual add + RMSNorm when its consumer is zs_fp8_gemm_run with rss: x[m] +=
+// sum_s y[s][m] (y may be NULL), xb[m] = bf16(x[m]) and rss[chunk][m] = the chunk's sum of x^2
+// (512 columns per chunk, one 128-thread block per (row, chunk): 256 blocks at 32 rows x 4096,
+// where the one-block-per-row norm spreads a step's slab reads over 32 CUs).
+__global__ __launch_bounds__(128) void mistral_add_ss_kernel(float* __restrict__ x,
+                                                             const float* __restrict__ y,
+                                                             int nsplit, long ss, int D,
+                                                             bf16_t* __restrict__ xb,
+                                                             float* __restrict__ rss) {
+  __shared__ float red[2];
+  const int m = blockIdx.x, ch = blockIdx.y, c = ch * 512 + 4 * threadIdx.x;
+  float* xr = x + (long)m * D + c;
+  float4 v = *reinterpret_cast<const float4*>(xr);
+  if (y) {
+    const float4 a = slab_sum4(y + (long)m * D + c, nsplit, ss);
+    v.x += a.x; v.y += a.y; v.z += a.z; v.w += a.w;
+    *reinterpret_cast<float4*>(xr) = v;
+  }
+  st4(xb + (long)m * D + c, v.x, v.y, v.z, v.w);
+  float q = wave_sum((v.x * v.x + v.y * v.y) + (v.z * v.z + v.w * v.w));
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = q;
+  __syncthreads();
+  if (threadIdx.x == 0) rss[ch * 32 + m] = red[0] + red[1];
+}
+
 // prefill input rows (predict_mistralai_multilingual.py:97-107 clap_to_gpt): row b*P + i is
 // embed[hard[b][i]] for i < H (pads included: the reference attends to them), soft[b][i-H] for
 // the next ns rows, embed[tail[i-H-ns]] (the language tag's ids) after; decode rows embed[tok[m]]
@@ -467,7 +650,9 @@ __global__ __launch_bounds__(128) void mistral_rope_kv_kernel(
   }
 }
 
-// act[m][f] = silu(gate) * up from the gate|up slabs [split][M][2F] (T out), 4 columns per thread
+// act[m][f] = silu(gate) * up from the gate|up slabs [split][M][2F] (T out), 4 columns per thread;
+// the columns are glu-interleaved (fp8_gemm_run_kernel): gate f at 16 (f / 8) + 8 (f / 4 % 2) +
+// f % 4, up f four columns after it
 template <typename T>
 __global__ __launch_bounds__(256) void mistral_silu_mul_kernel(const float* __restrict__ gu,
                                                                int nsplit, long ss, int M, int F,
@@ -475,8 +660,9 @@ __global__ __launch_bounds__(256) void mistral_silu_mul_kernel(const float* __re
   const long idx = 4 * ((long)blockIdx.x * 256 + threadIdx.x);
   if (idx >= (long)M * F) return;
   const int m = idx / F, f = idx % F;
-  const float4 gt = slab_sum4(gu + (long)m * 2 * F + f, nsplit, ss);
-  const float4 up = slab_sum4(gu + (long)m * 2 * F + F + f, nsplit, ss);
+  const long pg = (long)m * 2 * F + 16 * (f >> 3) + 8 * ((f >> 2) & 1);
+  const float4 gt = slab_sum4(gu + pg, nsplit, ss);
+  const float4 up = slab_sum4(gu + pg + 4, nsplit, ss);
   const float g4[4] = {gt.x, gt.y, gt.z, gt.w}, u4[4] = {up.x, up.y, up.z, up.w};
   float o[4];
 #pragma unroll
@@ -750,6 +936,63 @@ extern "C" int zs_fp8_gemm_rows(const void* A, int lda, const void* W8, const fl
 
 extern "C" int zs_fp8_splits(int K) { return K > 0 ? cdiv(K, F8_KC) : 0; }
 
+extern "C" int zs_fp8_gemm_run(const void* A, int lda, const void* W8, const float* scale, int M,
+                               int N, int K, int ks, int kh, float* out, long split_stride,
+                               int ldo, void* act, int ld_act, const float* rss, int nch,
+                               float eps, void* stream) {
+  ZS_REQUIRE(!rss || (nch >= 1 && nch <= 8), "zs_fp8_gemm_run: rss needs 1 <= nch <= 8");
+  ZS_REQUIRE(M > 0 && M <= 32 && N > 0 && N % 16 == 0 && K > 0 && K % F8_KC == 0,
+             "zs_fp8_gemm_run: 1 <= M <= 32, N %% 16, K %% 1024 (M=%d N=%d K=%d)", M, N, K);
+  const int nsplit = K / F8_KC;
+  ZS_REQUIRE(ks >= 1 && nsplit % ks == 0 && (ks == 1 || ks == 2 || ks == 4) && (kh == 1 || kh == 2),
+             "zs_fp8_gemm_run: ks in {1, 2, 4} dividing the %d splits, kh 1 or 2 (got %d, %d)",
+             nsplit, ks, kh);
+  ZS_REQUIRE(lda % 8 == 0 && ((uintptr_t)A & 15) == 0 && ((uintptr_t)W8 & 15) == 0 &&
+                 ((uintptr_t)scale & 15) == 0,
+             "zs_fp8_gemm_run: 16-byte aligned A rows, weights and scales");
+  if (act) {
+    ZS_REQUIRE(ks == nsplit && kh == 1 && ld_act % 4 == 0 && ld_act >= N / 2 &&
+                   ((uintptr_t)act & 7) == 0,
+               "zs_fp8_gemm_run: glu needs ks == splits (%d), kh 1, an 8-byte aligned act", nsplit);
+  } else {
+    ZS_REQUIRE(out && split_stride >= (long)(M - 1) * ldo + N && ldo >= N && ldo % 4 == 0 &&
+                   split_stride % 4 == 0 && ((uintptr_t)out & 15) == 0,
+               "zs_fp8_gemm_run: out layout (16-byte aligned rows, split stride)");
+  }
+  const int ntiles = cdiv(N, 128);
+  const dim3 grid((unsigned)(ntiles * (nsplit / ks) * kh));
+  hipStream_t st = S(stream);
+#define F8R(KS_, KH_, GLU_)                                                                     \
+  do {                                                                                          \
+    if (rss)                                                                                    \
+      hipLaunchKernelGGL((fp8_gemm_run_kernel<KS_, KH_, GLU_, true>), grid, dim3(512),          \
+                         (size_t)F8Run<KH_>::LDS_BYTES, st, (const bf16_t*)A, lda,              \
+                         (const uint8_t*)W8, scale, M, N, K, out, split_stride, ldo,            \
+                         (bf16_t*)act, ld_act, ntiles, rss, nch, eps);                          \
+    else                                                                                        \
+      hipLaunchKernelGGL((fp8_gemm_run_kernel<KS_, KH_, GLU_, false>), grid, dim3(512),         \
+                         (size_t)F8Run<KH_>::LDS_BYTES, st, (const bf16_t*)A, lda,              \
+                         (const uint8_t*)W8, scale, M, N, K, out, split_stride, ldo,            \
+                         (bf16_t*)act, ld_act, ntiles, rss, nch, eps);                          \
+  } while (0)
+  if (act) {
+    if (ks == 4) F8R(4, 1, true);
+    else if (ks == 2) F8R(2, 1, true);
+    else F8R(1, 1, true);
+  } else if (kh == 2) {
+    if (ks == 4) F8R(4, 2, false);
+    else if (ks == 2) F8R(2, 2, false);
+    else F8R(1, 2, false);
+  } else {
+    if (ks == 4) F8R(4, 1, false);
+    else if (ks == 2) F8R(2, 1, false);
+    else F8R(1, 1, false);
+  }
+#undef F8R
+  ZS_LAUNCH_CHECK();
+  return 0;
+}
+
 extern "C" int zs_fp8_unpack_bf16(const void* W8, int N, int K, void* out, void* stream) {
   ZS_REQUIRE(N > 0 && K > 0 && K % F8_KC == 0 && ((uintptr_t)W8 & 15) == 0 &&
                  ((uintptr_t)out & 15) == 0,
@@ -805,6 +1048,18 @@ extern "C" int zs_mistral_add_rmsnorm(float* x, const float* y, int nsplit, long
   return 0;
 }
 
+extern "C" int zs_mistral_add_ss(float* x, const float* y, int nsplit, long ss, int M, int D,
+                                 void* xb, float* rss, void* stream) {
+  ZS_REQUIRE(M > 0 && M <= 32 && D > 0 && D % 512 == 0 && D <= 64 * 512 && x && xb && rss &&
+                 (y == nullptr || (nsplit >= 1 && ss % 4 == 0 && ((uintptr_t)y & 15) == 0)) &&
+                 ((uintptr_t)x & 15) == 0 && ((uintptr_t)xb & 7) == 0,
+             "zs_mistral_add_ss: M <= 32, D %% 512 (<= 32768), aligned buffers (M=%d D=%d)", M, D);
+  hipLaunchKernelGGL(mistral_add_ss_kernel, dim3(M, D / 512), dim3(128), 0, S(stream), x, y, nsplit,
+                     ss, D, (bf16_t*)xb, rss);
+  ZS_LAUNCH_CHECK();
+  return 0;
+}
+
 extern "C" int zs_mistral_rope_kv(const float* qkv, int nsplit, long ss, int M, int H, int KVH,
                                   const int* pos, int rows_per_seq, const float* cosb,
                                   const float* sinb, void* q, void* kc, void* vc, int Lmax,
@@ -827,8 +1082,8 @@ extern "C" int zs_mistral_rope_kv(const float* qkv, int nsplit, long ss, int M, 
 extern "C" int zs_mistral_silu_mul(const float* gu, int nsplit, long ss, int M, int F, void* act,
                                    int dtype, void* stream) {
   ZS_REQUIRE(M > 0 && F > 0 && nsplit >= 1, "zs_mistral_silu_mul: bad shape");
-  ZS_REQUIRE(F % 4 == 0 && ss % 4 == 0 && ((uintptr_t)gu & 15) == 0 && ((uintptr_t)act & 15) == 0,
-             "zs_mistral_silu_mul: F and the split stride %% 4, 16-byte aligned buffers");
+  ZS_REQUIRE(F % 8 == 0 && ss % 4 == 0 && ((uintptr_t)gu & 15) == 0 && ((uintptr_t)act & 15) == 0,
+             "zs_mistral_silu_mul: F %% 8, the split stride %% 4, 16-byte aligned buffers");
   const int nb = cdiv((long)M * F / 4, 256);
   if (dtype == ZS_BF16)
     hipLaunchKernelGGL(mistral_silu_mul_kernel<bf16_t>, dim3(nb), dim3(256), 0, S(stream), gu,

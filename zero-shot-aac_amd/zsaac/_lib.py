@@ -70,7 +70,7 @@ SIGNATURES = {
     "zs_greedy_step": [P, P, I, I, P, I, I, I, P, P, P, P, P, P, P],
     "zs_decode_persist_workspace_bytes": [],
     "zs_decode_persist_grid": [],
-    "zs_gpt2_decode_persist": [I, I, I, I, I, I, P, P, P, F, P, P, P, P, P, P, P, P, P, P, P, P, L, P],
+    "zs_gpt2_decode_persist": [I, I, I, I, I, I, P, P, P, F, P, P, P, P, P, P, P, P, P, P, P, P, L, I, P],
     "zs_decode_persist_status": [P, P],
     "zs_decode_persist_set_stamps": [P, I],
     "zs_beam_step": [P, P, P, I, I, I, I, I, I, P, I, P, P, P, P, P, P, P, I, P, P, P, P],
@@ -82,6 +82,8 @@ SIGNATURES = {
     "zs_magic_score": [P, P, P, P, I, I, I, I, I, F, F, F, P, P],
     "zs_fp8_gemm_rows": [P, I, P, P, I, I, I, P, L, I, P],
     "zs_fp8_splits": [I],
+    "zs_fp8_gemm_run": [P, I, P, P, I, I, I, I, I, P, L, I, P, I, P, I, F, P],
+    "zs_mistral_add_ss": [P, P, I, L, I, I, P, P, P],
     "zs_fp8_unpack_bf16": [P, I, I, P, P],
     "zs_scale_cols": [P, I, I, I, P, P],
     "zs_mistral_embed": [P, I, P, I, P, I, P, P, I, I, P, I, P],

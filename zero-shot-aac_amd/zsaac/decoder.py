@@ -296,6 +296,9 @@ class Gpt2Decoder:
         if persist is None:
             persist = os.environ.get("ZSAAC_PERSIST", "1") != "0"
         self.persist = bool(persist) and dt == torch.bfloat16 and w.folded and self.R <= 64
+        # 2: the row-split grid (2 x decode_persist_grid() workgroups, a shorter step) -- chosen
+        # by the caller when few batches are in flight (pipeline.ConcurrentRunner)
+        self.persist_row_split = int(os.environ.get("ZSAAC_PERSIST_RS", "1"))
         if self.persist:
             import ctypes
             self.persist_ws = ops.decode_persist_workspace(dev)
@@ -542,7 +545,8 @@ class Gpt2Decoder:
                                     w.wpe, w.wte_packed(), self.temperature, w.layer_ptrs(),
                                     w.lnf[0], w.lnf[1], self._kv_ptrs,
                                     self.pos, self.next_tok, self.done, self.out_ids, self.out_len,
-                                    self.step_ctr, self.all_done, self.persist_ws)
+                                    self.step_ctr, self.all_done, self.persist_ws,
+                                    row_split=self.persist_row_split)
             if ev is not None:
                 ev[-1][1].record()
             self.rows_stepped += R * (self.max_steps - 1)   # upper bound (rows that stop early end it)

@@ -140,6 +140,20 @@ def dequantize_fp8(q: torch.Tensor, scale: torch.Tensor) -> torch.Tensor:
     return q.view(torch.float8_e4m3fn).float() * scale[:, None].float()
 
 
+def glu_interleave(gu: torch.Tensor) -> torch.Tensor:
+    """[gate; up] rows [2F, K] -> the glu-interleaved order the decode GEMM's fused SiLU * up
+    epilogue reads (csrc/mistral.hip fp8_gemm_run_kernel, zs_mistral_silu_mul): in every group of
+    16 rows, rows 0-3 / 8-11 are gate rows 8 grp + 0..3 / 4..7 and rows 4-7 / 12-15 the matching
+    up rows.  F % 8 == 0."""
+    F = gu.shape[0] // 2
+    if gu.shape[0] != 2 * F or F % 8:
+        raise ValueError(f"glu_interleave: {tuple(gu.shape)} is not [2F, K] with F % 8 == 0")
+    r = torch.arange(2 * F, device=gu.device)
+    c = r % 16
+    j = 8 * (r // 16) + 4 * (c // 8) + c % 4
+    return gu[torch.where((c // 4) % 2 == 0, j, F + j)]
+
+
 def fp8_pack_tiles(q: torch.Tensor) -> torch.Tensor:
     """Row-major fp8 codes [N, K] (K % 1024 == 0) -> the tile-packed stream zs_fp8_gemm_rows reads
     (csrc/mistral.hip): [K/1024][ceil(N/128)][8][16][64 lanes][16 B], i.e. the 1 KiB block of
@@ -188,7 +202,7 @@ class MistralWeights:
             ly = {"ln1": None if fold else g1.to(dev), "ln2": None if fold else g2.to(dev),
                   "qkv": self._pack(qkv * g1[None] if fold else qkv),
                   "o": self._pack(sd[L + "self_attn.o_proj.weight"]),
-                  "gu": self._pack(gu * g2[None] if fold else gu),
+                  "gu": self._pack(glu_interleave(gu * g2[None] if fold else gu)),
                   "down": self._pack(sd[L + "mlp.down_proj.weight"])}
             self.layers.append(ly)
             i += 1
@@ -232,7 +246,7 @@ class MistralWeights:
                 "ln1": None, "ln2": None,
                 "qkv": self._pack(torch.cat([rnd(D, D, gq), rnd(kv, D, gq), rnd(kv, D)])),
                 "o": self._pack(rnd(D, D, ro)),
-                "gu": self._pack(torch.cat([rnd(F, D, gg), rnd(F, D)])),
+                "gu": self._pack(glu_interleave(torch.cat([rnd(F, D, gg), rnd(F, D)]))),
                 "down": self._pack(rnd(D, F, ro))})
         self.lnf = None
         lm = rnd(V, D, 4.0)
@@ -273,6 +287,11 @@ class MistralDecoder:
         self.use_graph = True             # decode steps replayed from hipGraphs (decode_step)
         self.graphs = {}
         self.prefill_unpack = True        # fp8 prefill as unpack + tiled GEMM (A/B knob)
+        # fp8 decode (M <= 32) through zs_fp8_gemm_run: gate|up with the SiLU * up epilogue in one
+        # launch (GLU), the other projections as (ks splits, 1 / kh of a split) per workgroup
+        # (A/B knobs; False: zs_fp8_gemm_rows + zs_mistral_silu_mul)
+        self.fused_glu = True
+        self.run_cfg = {"qkv": (1, 1), "o": (1, 2), "down": (2, 1)}
         self._wb = None
         ly0 = w.layers[0]
         self._wb_need = max(ly0[k]["N"] * ly0[k]["K"] for k in ("qkv", "o", "gu", "down"))
@@ -310,6 +329,10 @@ class MistralDecoder:
         self.pval = torch.empty(max_batch, self.nblk, 1, device=dev)
         self.pidx = torch.empty(max_batch, self.nblk, 1, device=dev, dtype=torch.int32)
         self.last = torch.empty(max_batch, D, device=dev, dtype=adt)
+        # decode rows before an RMSNorm folded into the next GEMM (zs_mistral_add_ss): bf16 x and
+        # the per-512-column partial sums of squares [8][32]
+        self.xb = torch.empty(max_batch, D, device=dev, dtype=torch.bfloat16)
+        self.rss = torch.empty(8 * 32, device=dev)
 
     def _wscratch(self, N, K):
         """bf16 [N][K] scratch for one unpacked weight matrix (the largest: gate|up)."""
@@ -351,6 +374,28 @@ class MistralDecoder:
         ops.gemm(a[:M], lw["w"], out, split_k=1)
         return out, 1, M * N
 
+    def _gemm_run(self, a, lw, M, name, normed=False, act=None):
+        """Decode GEMM through zs_fp8_gemm_run (fp8, M <= 32): (slab tensor, nslab, stride).
+        normed: ``a`` is xb and the RMSNorm factor comes from rss (zs_mistral_add_ss); act: the
+        GLU form writing silu(gate) * up there."""
+        N, K = lw["N"], lw["K"]
+        ks, kh = (self._splits(K), 1) if act is not None else self.run_cfg[name]
+        if self._splits(K) % ks:
+            ks = 1
+        ns, ss = self._splits(K) // ks * kh, M * N
+        y = self.slab[:ns * ss]
+        call("zs_fp8_gemm_run", a.data_ptr(), a.stride(0), lw["w8"].data_ptr(),
+             lw["scale"].data_ptr(), M, N, K, ks, kh, None if act is not None else y.data_ptr(),
+             ss, N, act.data_ptr() if act is not None else None,
+             act.stride(0) if act is not None else 0, self.rss.data_ptr() if normed else None,
+             self.w.D // 512, float(self.w.eps), torch.cuda.current_stream().cuda_stream)
+        return y, ns, ss
+
+    def _add_ss(self, M, y, ns, ss):
+        call("zs_mistral_add_ss", self.x.data_ptr(), y.data_ptr() if y is not None else None, ns,
+             ss, M, self.w.D, self.xb.data_ptr(), self.rss.data_ptr(),
+             torch.cuda.current_stream().cuda_stream)
+
     def _norm(self, M, y, ns, ss, w):
         call("zs_mistral_add_rmsnorm", self.x.data_ptr(), y.data_ptr() if y is not None else None,
              ns, ss, M, self.w.D, float(self.w.eps), w.data_ptr() if w is not None else None,
@@ -360,9 +405,17 @@ class MistralDecoder:
         w, st = self.w, torch.cuda.current_stream().cuda_stream
         dt = ops.dt(self.h)
         nl = len(w.layers)
-        self._norm(M, None, 1, 0, w.layers[0]["ln1"])
+        # decode through zs_fp8_gemm_run: every RMSNorm but the last as zs_mistral_add_ss + the
+        # consuming GEMM's row factor; the last one (the LM head's input h) as before
+        run = (self.fused_glu and w.mode == "fp8" and rows_per_seq == 1 and M <= 32
+               and w.D % 512 == 0 and w.D <= 4096)
+        if run:
+            self._add_ss(M, None, 1, 0)
+        else:
+            self._norm(M, None, 1, 0, w.layers[0]["ln1"])
         for l, ly in enumerate(w.layers):
-            y, ns, ss = self._gemm(self.h, ly["qkv"], M)
+            y, ns, ss = (self._gemm_run(self.xb, ly["qkv"], M, "qkv", normed=True) if run else
+                         self._gemm(self.h, ly["qkv"], M))
             if rows_per_seq == 1 and self.fused_decode_attn:    # decode: RoPE + append + attention
                 call("zs_mistral_decode_attention", y.data_ptr(), ns, ss, M, w.H, w.KVH,
                      self.pos.data_ptr(), self.cos.data_ptr(), self.sin.data_ptr(),
@@ -376,11 +429,21 @@ class MistralDecoder:
                 call("zs_mistral_attention", self.q.data_ptr(), M, w.H, w.KVH,
                      self.pos.data_ptr(), rows_per_seq, self.kc[l].data_ptr(),
                      self.vc[l].data_ptr(), self.Lmax, self.att.data_ptr(), dt, st)
-            y, ns, ss = self._gemm(self.att, ly["o"], M)
-            self._norm(M, y, ns, ss, ly["ln2"])
-            y, ns, ss = self._gemm(self.h, ly["gu"], M)
-            call("zs_mistral_silu_mul", y.data_ptr(), ns, ss, M, w.F, self.act.data_ptr(), dt, st)
-            y, ns, ss = self._gemm(self.act, ly["down"], M)
+            if run:
+                y, ns, ss = self._gemm_run(self.att, ly["o"], M, "o")
+                self._add_ss(M, y, ns, ss)
+                self._gemm_run(self.xb, ly["gu"], M, "gu", normed=True, act=self.act)
+                y, ns, ss = self._gemm_run(self.act, ly["down"], M, "down")
+                if l + 1 < nl:
+                    self._add_ss(M, y, ns, ss)
+                    continue
+            else:
+                y, ns, ss = self._gemm(self.att, ly["o"], M)
+                self._norm(M, y, ns, ss, ly["ln2"])
+                y, ns, ss = self._gemm(self.h, ly["gu"], M)
+                call("zs_mistral_silu_mul", y.data_ptr(), ns, ss, M, w.F, self.act.data_ptr(), dt,
+                     st)
+                y, ns, ss = self._gemm(self.act, ly["down"], M)
             self._norm(M, y, ns, ss, w.layers[l + 1]["ln1"] if l + 1 < nl else w.lnf)
 
     def _lm_argmax(self, a, B):
@@ -438,7 +501,7 @@ class MistralDecoder:
         through the C-ABI."""
         if not self.use_graph:
             return self._step_body(B, eos)
-        key = (B, eos, self.fused_decode_attn)
+        key = (B, eos, self.fused_decode_attn, self.fused_glu, tuple(sorted(self.run_cfg.items())))
         g = self.graphs.get(key)
         if g is None:
             g = torch.cuda.CUDAGraph()
