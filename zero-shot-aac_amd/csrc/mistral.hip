@@ -670,6 +670,36 @@ __global__ __launch_bounds__(256) void mistral_silu_mul_kernel(const float* __re
   st4(act + idx, o[0], o[1], o[2], o[3]);
 }
 
+// in-wave reductions of the attention kernels without LDS round trips (DPP within rows of 16,
+// v_permlane16/32_swap across them), the same butterfly order as __shfl_xor 1, 2, 4 / 8, 16, 32
+template <int CTRL>
+__device__ __forceinline__ float m_dpp(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xf, 0xf, false));
+}
+__device__ __forceinline__ float m_sum8(float s) {          // over lane & 7
+  s += m_dpp<0xB1>(s);                                        // quad_perm [1,0,3,2]
+  s += m_dpp<0x4E>(s);                                        // quad_perm [2,3,0,1]
+  return s + m_dpp<0x141>(s);                                 // row_half_mirror
+}
+__device__ __forceinline__ float m_pair16(float v) {        // v + lane ^ 16's v
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+__device__ __forceinline__ float m_pair32(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+__device__ __forceinline__ float m_max_grp(float v) {       // over lane >> 3
+  v = fmaxf(v, m_dpp<0x128>(v));                              // row_ror:8 = lane ^ 8
+  auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+  r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float m_add_grp(float v) {
+  return m_pair32(m_pair16(v + m_dpp<0x128>(v)));
+}
+
 // causal GQA attention, one wave per (query row m, q head h): keys 0..pos[m] of the sequence
 // m / rows_per_seq from kv head h / (H / KVH); softmax((q k^T) / sqrt(128)) v, f32 math.
 // Lane = (key group grp = lane >> 3, 16-dim slice sub = lane & 7): a wave step scores 8 keys
@@ -714,13 +744,9 @@ __global__ __launch_bounds__(256) void mistral_attn_kernel(const T* __restrict__
       float sv = 0.f;
 #pragma unroll
       for (int d = 0; d < DPL; ++d) sv += qv[d] * kf[u][d];
-      sv += __shfl_xor(sv, 1, 64);
-      sv += __shfl_xor(sv, 2, 64);
-      sv += __shfl_xor(sv, 4, 64);
+      sv = m_sum8(sv);
       sv = (j0 + 8 * u + grp <= p) ? sv * scale : -INFINITY;
-      float pm = fmaxf(sv, __shfl_xor(sv, 8, 64));
-      pm = fmaxf(pm, __shfl_xor(pm, 16, 64));
-      pm = fmaxf(pm, __shfl_xor(pm, 32, 64));
+      float pm = m_max_grp(sv);
       const float mn = fmaxf(mx, pm);
       float corr, e;
       if constexpr (sizeof(T) == 4) { corr = expf(mx - mn); e = expf(sv - mn); }   // parity mode
@@ -732,12 +758,9 @@ __global__ __launch_bounds__(256) void mistral_attn_kernel(const T* __restrict__
     }
   }
   // combine the 8 key groups (same running max in every group)
+  l = m_add_grp(l);
 #pragma unroll
-  for (int x = 8; x < 64; x <<= 1) {
-    l += __shfl_xor(l, x, 64);
-#pragma unroll
-    for (int d = 0; d < DPL; ++d) o[d] += __shfl_xor(o[d], x, 64);
-  }
+  for (int d = 0; d < DPL; ++d) o[d] = m_add_grp(o[d]);
   if (grp == 0) {
     const float inv = 1.0f / l;
     T* orow = out + (long)m * H * HD + h * HD + sub * DPL;
@@ -766,6 +789,21 @@ __global__ __launch_bounds__(256) void mistral_decode_attn_kernel(
   const int p = __builtin_amdgcn_readfirstlane(pos[m]);
   const long NQKV = (long)(H + 2 * KVH) * HD;
   const float* src = qkv + m * NQKV + sub * DPL;
+  const long base = ((long)m * KVH + kvh) * Lmax;
+  // the first 8 U cached keys do not depend on this step's q / k / v: their loads are issued
+  // before the slab sums (one memory round trip for both at the usual p <= 8 U... prompt + steps)
+  float kf[U][DPL], vf[U][DPL];
+  auto load_keys = [&](int j0) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int j = max(min(j0 + 8 * u + grp, p - 1), 0);
+      const T* kr = kc + (base + j) * HD + sub * DPL;
+      const T* vr = vc + (base + j) * HD + sub * DPL;
+#pragma unroll
+      for (int d = 0; d < DPL; ++d) { kf[u][d] = ldf(kr + d); vf[u][d] = ldf(vr + d); }
+    }
+  };
+  load_keys(0);
   float qv[DPL], kn[DPL], vn[DPL];
 #pragma unroll
   for (int d = 0; d < DPL; d += 4) {
@@ -789,7 +827,6 @@ __global__ __launch_bounds__(256) void mistral_decode_attn_kernel(
       kn[d] = lo ? kn[d] * c - ko * sn : kn[d] * c + ko * sn;
     }
   }
-  const long base = ((long)m * KVH + kvh) * Lmax;
   if (h % (H / KVH) == 0 && grp == 0) {
     T* kr = kc + (base + p) * HD + sub * DPL;
     T* vr = vc + (base + p) * HD + sub * DPL;
@@ -811,9 +848,7 @@ __global__ __launch_bounds__(256) void mistral_decode_attn_kernel(
 #pragma unroll
   for (int d = 0; d < DPL; ++d) o[d] = 0.f;
   auto update = [&](float sv, const float* vf) {
-    float pm = fmaxf(sv, __shfl_xor(sv, 8, 64));
-    pm = fmaxf(pm, __shfl_xor(pm, 16, 64));
-    pm = fmaxf(pm, __shfl_xor(pm, 32, 64));
+    float pm = m_max_grp(sv);
     const float mn = fmaxf(mx, pm);
     float corr, e;
     if constexpr (sizeof(T) == 4) { corr = expf(mx - mn); e = expf(sv - mn); }   // parity mode
@@ -824,23 +859,13 @@ __global__ __launch_bounds__(256) void mistral_decode_attn_kernel(
     mx = mn;
   };
   for (int j0 = 0; j0 < p; j0 += 8 * U) {
-    float kf[U][DPL], vf[U][DPL];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int j = min(j0 + 8 * u + grp, p - 1);
-      const T* kr = kc + (base + j) * HD + sub * DPL;
-      const T* vr = vc + (base + j) * HD + sub * DPL;
-#pragma unroll
-      for (int d = 0; d < DPL; ++d) { kf[u][d] = ldf(kr + d); vf[u][d] = ldf(vr + d); }
-    }
+    if (j0 > 0) load_keys(j0);
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       float sv = 0.f;
 #pragma unroll
       for (int d = 0; d < DPL; ++d) sv += qv[d] * kf[u][d];
-      sv += __shfl_xor(sv, 1, 64);
-      sv += __shfl_xor(sv, 2, 64);
-      sv += __shfl_xor(sv, 4, 64);
+      sv = m_sum8(sv);
       update((j0 + 8 * u + grp < p) ? sv * scale : -INFINITY, vf[u]);
     }
   }
@@ -848,17 +873,12 @@ __global__ __launch_bounds__(256) void mistral_decode_attn_kernel(
     float sv = 0.f;
 #pragma unroll
     for (int d = 0; d < DPL; ++d) sv += qv[d] * kn[d];
-    sv += __shfl_xor(sv, 1, 64);
-    sv += __shfl_xor(sv, 2, 64);
-    sv += __shfl_xor(sv, 4, 64);
+    sv = m_sum8(sv);
     update(grp == 0 ? sv * scale : -INFINITY, vn);
   }
+  l = m_add_grp(l);
 #pragma unroll
-  for (int x = 8; x < 64; x <<= 1) {
-    l += __shfl_xor(l, x, 64);
-#pragma unroll
-    for (int d = 0; d < DPL; ++d) o[d] += __shfl_xor(o[d], x, 64);
-  }
+  for (int d = 0; d < DPL; ++d) o[d] = m_add_grp(o[d]);
   if (grp == 0) {
     const float inv = 1.0f / l;
     T* orow = out + (long)m * H * HD + h * HD + sub * DPL;
