@@ -33,6 +33,7 @@
 #include "common.h"
 
 namespace zs {
+int g_dp_xb = 1;   // zs_tune_set("dp_xb", 0): LayerNorm inputs from the f32 x (A/B)
 namespace dpk {
 
 constexpr int D = 768, NH = 12, HD = 64, DFF = 3072, NLY = 12, RM = 64, QKVN = 3 * D;
@@ -59,7 +60,8 @@ constexpr int WS_X = WS_SYNC_BYTES;                // f32  [64][768]
 constexpr int WS_QKV = WS_X + RM * D * 4;          // bf16 [64][2304]
 constexpr int WS_ATT = WS_QKV + RM * QKVN * 2;     // bf16 fragment-packed [4][24][64][8]
 constexpr int WS_HID = WS_ATT + RM * D * 2;        // bf16 fragment-packed [4][96][64][8]
-constexpr int WS_BYTES = WS_HID + RM * DFF * 2;
+constexpr int WS_XB = WS_HID + RM * DFF * 2;       // bf16 [64][768]: x for the LayerNorms
+constexpr int WS_BYTES = WS_XB + RM * D * 2;
 
 struct Args {
   int R, Lmax, max_steps, stop0, stop1, V;
@@ -87,7 +89,7 @@ static_assert(NW * RM * 48 * 4 <= SM_HS, "QKV partial slabs fit the aliased row 
 
 // ------------------------------------------------------------------ memory helpers
 struct Rs {
-  __amdgpu_buffer_rsrc_t x, qkv, att, hid;
+  __amdgpu_buffer_rsrc_t x, qkv, att, hid, xb;
 };
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t mk(char* p, int bytes) {
   return __builtin_amdgcn_make_buffer_rsrc(p, (short)0, bytes, 0x00020000);
@@ -246,13 +248,59 @@ __device__ __forceinline__ bool bar_wait(Bar& b, volatile lds_int_t* s_ok) {
 // 2: x with the ln_f affine.  The LN affine of ln_1 / ln_2 is folded into c_attn / c_fc.
 // NR rows (64, or 32 for a row-split grid) from row r0, TPR = 512 / NR threads per row, NQ column
 // quads per thread; rows land at LDS row r - r0.  MODE 1 stores x rows r % 48 == w of its range.
-template <int MODE, int NR = RM>
+template <int MODE, int NR = RM, bool XB = false>
 __device__ __forceinline__ void ln_rows(const Args& a, const Rs& rs, bf16_t* hs, const int* s_tok,
                                         const int* s_pos, int w, const float* s_lnf = nullptr,
                                         int r0 = 0) {
   constexpr int TPR = NT / NR, NQ = D / 4 / TPR;
   const int tid = otid(), rl = tid / TPR, q = tid % TPR, r = r0 + rl;
   const int rr = min(r, a.R - 1);
+  if constexpr (XB && MODE != 1) {
+    // x handed off in bf16 (the producers' copy, rs.xb): half the bytes of the f32 rows, 16-byte
+    // sc1 loads of 8 columns (octets q + TPR i); statistics in f32 over the bf16 values
+    constexpr int NO = NQ / 2;
+    float xv[NO][8];
+#pragma unroll
+    for (int i = 0; i < NO; ++i) {
+      const u32x4_t u = ld16(rs.xb, (rr * D + 8 * (q + TPR * i)) * 2);
+      xv[i][0] = __uint_as_float(u.x << 16); xv[i][1] = __uint_as_float(u.x & 0xffff0000u);
+      xv[i][2] = __uint_as_float(u.y << 16); xv[i][3] = __uint_as_float(u.y & 0xffff0000u);
+      xv[i][4] = __uint_as_float(u.z << 16); xv[i][5] = __uint_as_float(u.z & 0xffff0000u);
+      xv[i][6] = __uint_as_float(u.w << 16); xv[i][7] = __uint_as_float(u.w & 0xffff0000u);
+    }
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < NO; ++i)
+      s += ((xv[i][0] + xv[i][1]) + (xv[i][2] + xv[i][3])) + ((xv[i][4] + xv[i][5]) + (xv[i][6] + xv[i][7]));
+#pragma unroll
+    for (int o = 1; o < TPR; o <<= 1) s += __shfl_xor(s, o, 64);
+    const float mean = s * (1.0f / D);
+    float qq = 0.f;
+#pragma unroll
+    for (int i = 0; i < NO; ++i)
+#pragma unroll
+      for (int t = 0; t < 8; ++t) {
+        const float d0 = xv[i][t] - mean;
+        qq += d0 * d0;
+      }
+#pragma unroll
+    for (int o = 1; o < TPR; o <<= 1) qq += __shfl_xor(qq, o, 64);
+    const float rstd = rsqrtf(qq * (1.0f / D) + 1e-5f);
+#pragma unroll
+    for (int i = 0; i < NO; ++i) {
+      const int c = 8 * (q + TPR * i);
+      float y[8];
+#pragma unroll
+      for (int t = 0; t < 8; ++t) y[t] = (xv[i][t] - mean) * rstd;
+      if constexpr (MODE == 2) {
+#pragma unroll
+        for (int t = 0; t < 8; ++t) y[t] = y[t] * s_lnf[c + t] + s_lnf[D + c + t];
+      }
+      *reinterpret_cast<uint4*>(hs + rl * HLD + c) =
+          make_uint4(pk2bf(y[0], y[1]), pk2bf(y[2], y[3]), pk2bf(y[4], y[5]), pk2bf(y[6], y[7]));
+    }
+    return;
+  }
   float4 xv[NQ];
   if constexpr (MODE == 1) {
     const bf16_t* te = a.wte + (long)s_tok[r] * D;
@@ -348,7 +396,7 @@ __device__ __forceinline__ void put_partial(float* red, int slab, int col0, cons
 
 // ------------------------------------------------------------------ phase A: ln_1 + c_attn
 // RH = 1: all 64 rows; RH = 2: the 32 rows of half h (row-split grid)
-template <int RH>
+template <int RH, bool XB>
 __device__ __forceinline__ void phase_qkv(const Args& a, const Rs& rs, int l, char* smem,
                                           const int* s_tok, const int* s_pos, int w, int h,
                                           const bf16x8_t (&wq)[9]) {
@@ -361,7 +409,7 @@ __device__ __forceinline__ void phase_qkv(const Args& a, const Rs& rs, int l, ch
   const float4 b0 = *reinterpret_cast<const float4*>(a.bqkv[l] + 48 * w + c0);
   const float4 b1 = *reinterpret_cast<const float4*>(a.bqkv[l] + 48 * w + c1);
   if (l == 0) ln_rows<1, NR>(a, rs, hs, s_tok, s_pos, w, nullptr, r0);
-  else ln_rows<0, NR>(a, rs, hs, s_tok, s_pos, w, nullptr, r0);
+  else ln_rows<0, NR, XB>(a, rs, hs, s_tok, s_pos, w, nullptr, r0);
   lds_sync();
   f32x4_t acc[NRB][3];
   mma_lds<3, 3, NRB>(hs, 96 * v, wq, acc);
@@ -534,14 +582,15 @@ __device__ __forceinline__ void phase_attn(const Args& a, const Rs& rs, int l, c
 // x[:, 16w .. 16w + 16) += A W^T + b, A = att (K 768) or hid (K 3072) from the workspace in
 // A-fragment order; wave v takes k-steps [v S, (v+1) S), its A fragments in chunks of 4 k-steps
 // (two chunks in flight), each fragment load one contiguous KiB
-template <int S, int RH = 1>
+template <int S, int RH, bool XB>
 __device__ __forceinline__ void phase_proj(const Args& a, const Rs& rs, __amdgpu_buffer_rsrc_t ra,
                                            int K, const float* bias, char* smem, int w, int h,
                                            const bf16x8_t (&wb)[S]) {
   constexpr int NR = RM / RH, NRB = NR / 16;
   float* red = reinterpret_cast<float*>(smem);
   const int tid = otid(), lane = tid & 63, v = tid >> 6, r0 = h * NR;
-  // epilogue operands first: NR rows x 4 quads on threads 0 .. 4 NR - 1
+  // epilogue operands first: NR rows x 4 quads on threads 0 .. 4 NR - 1 (two threads per
+  // 16-byte bf16 copy were tried: the longer per-thread epilogue cost more than the 8-byte stores)
   const int erl = (tid >> 2) & (NR - 1), erow = r0 + erl, ec = 16 * w + 4 * (tid & 3);
   float4 eb = make_float4(0.f, 0.f, 0.f, 0.f), ex = eb;
   if (tid < 4 * NR) {
@@ -590,9 +639,12 @@ __device__ __forceinline__ void phase_proj(const Args& a, const Rs& rs, __amdgpu
       const float4 p = *reinterpret_cast<const float4*>(red + (k * NR + erl) * 16 + 4 * (tid & 3));
       sm.x += p.x; sm.y += p.y; sm.z += p.z; sm.w += p.w;
     }
-    if (erow < a.R)
-      st16(rs.x, (erow * D + ec) * 4,
-           f42u(sm.x + eb.x + ex.x, sm.y + eb.y + ex.y, sm.z + eb.z + ex.z, sm.w + eb.w + ex.w));
+    if (erow < a.R) {
+      const float4 o = make_float4(sm.x + eb.x + ex.x, sm.y + eb.y + ex.y, sm.z + eb.z + ex.z,
+                                   sm.w + eb.w + ex.w);
+      st16(rs.x, (erow * D + ec) * 4, f42u(o.x, o.y, o.z, o.w));
+      if constexpr (XB) st8(rs.xb, (erow * D + ec) * 2, u32x2_t{pk2bf(o.x, o.y), pk2bf(o.z, o.w)});
+    }
   }
 }
 
@@ -601,7 +653,7 @@ __device__ __forceinline__ float gelu_new_fast(float x) {
   const float u2 = -1.5957691216057308f * (x + 0.044715f * x * x * x);
   return x * __builtin_amdgcn_rcpf(1.0f + __expf(u2));
 }
-template <int RH = 1>
+template <int RH, bool XB>
 __device__ __forceinline__ void phase_fc(const Args& a, const Rs& rs, int l, char* smem,
                                          const int* s_tok, const int* s_pos, int w, int h,
                                          const bf16x8_t (&wf)[12]) {
@@ -612,7 +664,7 @@ __device__ __forceinline__ void phase_fc(const Args& a, const Rs& rs, int l, cha
   // epilogue: NR rows x 16 quads, quads tid and tid + 512 (same column quad)
   const int c = 4 * (tid & 15);
   const float4 bb = *reinterpret_cast<const float4*>(a.bfc[l] + 64 * w + c);
-  ln_rows<0, NR>(a, rs, hs, s_tok, s_pos, w, nullptr, r0);
+  ln_rows<0, NR, XB>(a, rs, hs, s_tok, s_pos, w, nullptr, r0);
   lds_sync();
   f32x4_t acc[NRB][2];
   mma_lds<2, 6, NRB>(hs, 192 * kq, wf, acc);
@@ -682,12 +734,13 @@ __device__ __forceinline__ void lm_consume(const bf16_t* hs, int c, const bf16x8
     }
   }
 }
+template <bool XB>
 __device__ __forceinline__ void phase_lm(const Args& a, const Rs& rs, char* smem, const int* s_tok,
                                          const int* s_pos, float* am_v, int* am_i, int wg, int gg,
                                          gu64* keys, const float* s_lnf) {
   bf16_t* hs = reinterpret_cast<bf16_t*>(smem);
   const int tid = otid(), lane = tid & 63, v = tid >> 6, fr = lane & 15, r4 = 4 * (lane >> 4);
-  ln_rows<2>(a, rs, hs, s_tok, s_pos, wg, s_lnf);
+  ln_rows<2, RM, XB>(a, rs, hs, s_tok, s_pos, wg, s_lnf);
   lds_sync();
   const int nvb = (a.V + 15) / 16;
   const int b_lo = (int)((long)wg * nvb / gg), b_hi = (int)((long)(wg + 1) * nvb / gg);
@@ -787,7 +840,9 @@ __device__ __forceinline__ void gave_up(const Args& a) {
 // (half the handed-off activation bytes per workgroup, the same weights: blocks b and b + 8 --
 // one XCD under round-robin dispatch, speed only -- hold the two halves of a slice), the attention
 // units of its rows, and 1/96 of the LM head's vocabulary for all rows.
-template <int RH>
+// XB: the LayerNorm inputs are handed off as a bf16 copy of x (written by phases C / E beside
+// the f32 residual stream), halving the bytes every workgroup reads in phases A, D and F.
+template <int RH, bool XB>
 __global__ __launch_bounds__(NT) void decode_persist_kernel(Args a) {
   __shared__ __attribute__((aligned(16))) char smem[SM_TOTAL];
   float* am_v = reinterpret_cast<float*>(smem + SM_HS);
@@ -805,6 +860,7 @@ __global__ __launch_bounds__(NT) void decode_persist_kernel(Args a) {
   rs.qkv = mk(a.ws + WS_QKV, RM * QKVN * 2);
   rs.att = mk(a.ws + WS_ATT, RM * D * 2);
   rs.hid = mk(a.ws + WS_HID, RM * DFF * 2);
+  rs.xb = mk(a.ws + WS_XB, RM * D * 2);
   Bar bar{(gu32*)(a.ws + WS_SYNC), (gu32*)(a.ws + WS_SYNC + 4), 0, nullptr, 0, GG};
   gu64* const lmkey = (gu64*)(a.ws + WS_LMKEY);
   unsigned long long* const stamps = dp_stamp_buf;
@@ -836,7 +892,7 @@ __global__ __launch_bounds__(NT) void decode_persist_kernel(Args a) {
     bar.n0 = bar.n;
     stamp(bar.sb, 2 * DP_NB - 1);   // step start
     for (int l = 0; l < NLY; ++l) {
-      phase_qkv<RH>(a, rs, l, smem, s_tok, s_pos, w, h, wq);
+      phase_qkv<RH, XB>(a, rs, l, smem, s_tok, s_pos, w, h, wq);
       bar_arrive(bar);
       uint4 kr[2 / RH][8], vr[2 / RH][8];
       attn_load<2 / RH>(a, l, s_pos, ub, 0, kr, vr);
@@ -851,16 +907,16 @@ __global__ __launch_bounds__(NT) void decode_persist_kernel(Args a) {
       load_w<2, 6>(a.wfc[l], D, 64 * w + 32 * (V_ >> 2), DFF, 192 * (V_ & 3), wf);
       if (!bar_wait(bar, s_ok)) return gave_up(a);
 
-      phase_proj<3, RH>(a, rs, rs.att, D, a.bproj[l], smem, w, h, wp);
+      phase_proj<3, RH, XB>(a, rs, rs.att, D, a.bproj[l], smem, w, h, wp);
       bar_arrive(bar);
       if (!bar_wait(bar, s_ok)) return gave_up(a);
 
-      phase_fc<RH>(a, rs, l, smem, s_tok, s_pos, w, h, wf);
+      phase_fc<RH, XB>(a, rs, l, smem, s_tok, s_pos, w, h, wf);
       bar_arrive(bar);
       load_w<1, 12>(a.wmp[l], DFF, 16 * w, D, 384 * V_, wm);
       if (!bar_wait(bar, s_ok)) return gave_up(a);
 
-      phase_proj<12, RH>(a, rs, rs.hid, DFF, a.bmp[l], smem, w, h, wm);
+      phase_proj<12, RH, XB>(a, rs, rs.hid, DFF, a.bmp[l], smem, w, h, wm);
       bar_arrive(bar);
       // next block's c_attn.  Unconditional (a conditional load keeps the old wq live through
       // the whole block for the path that skips it); after block 11 the value is dead and wq is
@@ -868,7 +924,7 @@ __global__ __launch_bounds__(NT) void decode_persist_kernel(Args a) {
       load_w<3, 3>(a.wqkv[l + 1 < NLY ? l + 1 : 0], D, 48 * w, QKVN, 96 * V_, wq);
       if (!bar_wait(bar, s_ok)) return gave_up(a);
     }
-    phase_lm(a, rs, smem, s_tok, s_pos, am_v, am_i, wg, GG, lmkey + (step & 1) * RM, s_lnf);
+    phase_lm<XB>(a, rs, smem, s_tok, s_pos, am_v, am_i, wg, GG, lmkey + (step & 1) * RM, s_lnf);
     bar_arrive(bar);
     load_w<3, 3>(a.wqkv[0], D, 48 * w, QKVN, 96 * V_, wq);
     if (!bar_wait(bar, s_ok)) return gave_up(a);
@@ -975,10 +1031,13 @@ extern "C" int zs_gpt2_decode_persist(int R, int Lmax, int max_steps, int stop0,
   a.step_ctr = step_ctr; a.all_done = all_done; a.ws = (char*)ws;
   // the barrier counter and timeout word: zeroed before every launch (a memset node under capture)
   ZS_CHECK_HIP(hipMemsetAsync(ws, 0, WS_SYNC_BYTES, S(stream)));
-  if (row_split == 2)
-    hipLaunchKernelGGL(decode_persist_kernel<2>, dim3(2 * G), dim3(NT), 0, S(stream), a);
-  else
-    hipLaunchKernelGGL(decode_persist_kernel<1>, dim3(G), dim3(NT), 0, S(stream), a);
+  if (row_split == 2) {
+    if (g_dp_xb) hipLaunchKernelGGL((decode_persist_kernel<2, true>), dim3(2 * G), dim3(NT), 0, S(stream), a);
+    else hipLaunchKernelGGL((decode_persist_kernel<2, false>), dim3(2 * G), dim3(NT), 0, S(stream), a);
+  } else {
+    if (g_dp_xb) hipLaunchKernelGGL((decode_persist_kernel<1, true>), dim3(G), dim3(NT), 0, S(stream), a);
+    else hipLaunchKernelGGL((decode_persist_kernel<1, false>), dim3(G), dim3(NT), 0, S(stream), a);
+  }
   ZS_LAUNCH_CHECK();
   return 0;
 }
