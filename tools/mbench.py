@@ -201,7 +201,7 @@ def bench_lmhead():
     V, K = 50257, 768
     w = (torch.randn(V, K, device=dev) * 0.05).bfloat16()
     nblk = ops.lmhead_nblk(V)
-    for M in (64, 256, 1024, 2048, 8192):
+    for M in (64, 256, 1280, 2048, 8192):
         a = torch.randn(M, K, device=dev).bfloat16()
         ps = torch.empty(M, nblk, 2, device=dev)
         res = {}
@@ -209,6 +209,9 @@ def bench_lmhead():
             pv = torch.empty(M, nblk, k, device=dev)
             pi = torch.empty(M, nblk, k, device=dev, dtype=torch.int32)
             res[f"topk{k}"] = timeit(lambda: ops.lmhead_topk(a, w, k, ps, pv, pi), reps=20)
+            res[f"topk{k}_nostat"] = timeit(lambda: ops.lmhead_topk(a, w, k, None, pv, pi), reps=20)
+        lo = torch.empty(M, V, device=dev, dtype=torch.bfloat16)
+        res["zs_gemm_bf16out"] = timeit(lambda: ops.gemm(a, w, lo), reps=20)
         pv = torch.empty(M, nblk, 1, device=dev)
         pi = torch.empty(M, nblk, 1, device=dev, dtype=torch.int32)
         res["rownorm"] = timeit(lambda: ops.lmhead_topk(a, w, 1, ps, pv, pi, row_norm=True), reps=20)

@@ -880,11 +880,20 @@ __global__ __launch_bounds__(256) void lmhead_kernel(int xcd_order, int M, int K
           float cv = n < V ? acct[i][j][e] * sc : -INFINITY;
           if (tdiv) cv = cv / temp;
           int ci = n;
-          // n increases with (i, e): strict > keeps the lower index first among equals
+          // n increases with (i, e): strict > keeps the lower index first among equals.  The
+          // bubble insertion is select-only (per-element branches became ~500 divergent
+          // exec-mask branches per kernel); the outer test skips a value no lane keeps
           if (cv > tv[KMAX - 1]) {
 #pragma unroll
-            for (int q = 0; q < KMAX; ++q)
-              if (cv > tv[q]) { const float t = tv[q]; const int u = ti[q]; tv[q] = cv; ti[q] = ci; cv = t; ci = u; }
+            for (int q = 0; q < KMAX; ++q) {
+              const bool c = cv > tv[q];
+              const float t = tv[q];
+              const int u = ti[q];
+              tv[q] = c ? cv : t;
+              ti[q] = c ? ci : u;
+              cv = c ? t : cv;
+              ci = c ? u : ci;
+            }
           }
         }
       // merge with the partner lane's list (both lanes end with the same top-KMAX)
@@ -892,24 +901,28 @@ __global__ __launch_bounds__(256) void lmhead_kernel(int xcd_order, int M, int K
       int pi[KMAX];
 #pragma unroll
       for (int q = 0; q < KMAX; ++q) { pv[q] = __shfl_xor(tv[q], 32, 64); pi[q] = __shfl_xor(ti[q], 32, 64); }
-      {
-        float mv[KMAX];
-        int mi[KMAX];
-        int a = 0, b = 0;
+      if constexpr (KMAX > 1) {
+        // merge of two descending lists, select-only: the partner's entries bubble into this
+        // lane's list like new values (the same order as a merge: value desc, then index asc)
 #pragma unroll
-        for (int q = 0; q < KMAX; ++q) {
-          float av = -INFINITY, bv2 = -INFINITY;
-          int ai = 0x7fffffff, bi2 = 0x7fffffff;
+        for (int p = 0; p < KMAX; ++p) {
+          float cv = pv[p];
+          int ci = pi[p];
 #pragma unroll
-          for (int t = 0; t < KMAX; ++t) {
-            if (t == a) { av = tv[t]; ai = ti[t]; }
-            if (t == b) { bv2 = pv[t]; bi2 = pi[t]; }
+          for (int q = 0; q < KMAX; ++q) {
+            const bool c = better(cv, ci, tv[q], ti[q]);
+            const float t = tv[q];
+            const int u = ti[q];
+            tv[q] = c ? cv : t;
+            ti[q] = c ? ci : u;
+            cv = c ? t : cv;
+            ci = c ? u : ci;
           }
-          if (better(av, ai, bv2, bi2)) { mv[q] = av; mi[q] = ai; ++a; }
-          else { mv[q] = bv2; mi[q] = bi2; ++b; }
         }
-#pragma unroll
-        for (int q = 0; q < KMAX; ++q) { tv[q] = mv[q]; ti[q] = mi[q]; }
+      } else {
+        const bool c = better(pv[0], pi[0], tv[0], ti[0]);
+        tv[0] = c ? pv[0] : tv[0];
+        ti[0] = c ? pi[0] : ti[0];
       }
       const float bv = tv[0];
       float se = 0.f;
@@ -1003,13 +1016,14 @@ __global__ __launch_bounds__(256) void lmhead_kernel(int xcd_order, int M, int K
       float cv = v;
       int ci = n;
 #pragma unroll
-      for (int q = 0; q < KMAX; ++q) {
-        if (cv > tv[q]) {
-          const float t = tv[q];
-          const int u = ti[q];
-          tv[q] = cv; ti[q] = ci;
-          cv = t; ci = u;
-        }
+      for (int q = 0; q < KMAX; ++q) {   // select-only, as the transposed path above
+        const bool c = cv > tv[q];
+        const float t = tv[q];
+        const int u = ti[q];
+        tv[q] = c ? cv : t;
+        ti[q] = c ? ci : u;
+        cv = c ? t : cv;
+        ci = c ? u : ci;
       }
     }
   }
