@@ -269,8 +269,10 @@ __global__ __launch_bounds__(256) void greedy_step_kernel(
 }
 
 // ------------------------------------------------------------------ beam search step
-// one block per clip; beam <= 8, topk (partials per block) >= beam
-__global__ __launch_bounds__(256) void beam_step_kernel(
+// one block per clip, one wave per source row (64 beam threads); beam <= LMB <= 8, topk
+// (partials per block) >= beam; LMB = the lane candidate list length
+template <int LMB>
+__global__ __launch_bounds__(512) void beam_step_kernel(
     const float* __restrict__ pstat, const float* __restrict__ pv, const int* __restrict__ pi,
     int beam, int nblk, int topk, int first, int stop, const int* __restrict__ step_ctr,
     int max_steps, float* __restrict__ scores, float* __restrict__ seq_len,
@@ -285,6 +287,7 @@ __global__ __launch_bounds__(256) void beam_step_kernel(
   __shared__ float sel_avg[MB];
   __shared__ int s_skip;
   const int c = blockIdx.x, lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int nwv = blockDim.x >> 6, nthr = blockDim.x;
   const int step = *step_ctr;
   const int r0 = c * beam;
   if (threadIdx.x == 0) {
@@ -296,7 +299,7 @@ __global__ __launch_bounds__(256) void beam_step_kernel(
   if (s_skip) return;   // finished clip: the reference has left its loop; state is frozen
   const int nsrc = first ? 1 : beam;
   // per source row: lse pieces and its top-`beam` logits (merging the per-block sorted lists)
-  for (int i = wid; i < nsrc; i += 4) {
+  for (int i = wid; i < nsrc; i += nwv) {
     const int prow = first ? c : r0 + i;   // partial row (prefill rows are per clip)
     float M = -INFINITY;
     for (int k = lane; k < nblk; k += 64) M = fmaxf(M, pstat[((long)prow * nblk + k) * 2]);
@@ -311,17 +314,17 @@ __global__ __launch_bounds__(256) void beam_step_kernel(
     // candidates in registers (one pass of independent loads, insertion in (value desc, index
     // asc) order), then `beam` rounds of wave argmax over those lane lists (the rounds no longer
     // re-read the candidates from memory)
-    float lv[MB];
-    int li[MB];
+    float lv[LMB];
+    int li[LMB];
 #pragma unroll
-    for (int t = 0; t < MB; ++t) { lv[t] = -INFINITY; li[t] = 0x7fffffff; }
+    for (int t = 0; t < LMB; ++t) { lv[t] = -INFINITY; li[t] = 0x7fffffff; }
     for (int k = lane; k < nblk; k += 64) {
       const long base = ((long)prow * nblk + k) * topk;
-      for (int t = 0; t < topk; ++t) {
+      for (int t = 0; t < beam; ++t) {   // only a block's first `beam` can reach the top-beam
         float v = pv[base + t];
         int ix = pi[base + t];
 #pragma unroll
-        for (int u = 0; u < MB; ++u) {      // bubble (v, ix) into the sorted lane list
+        for (int u = 0; u < LMB; ++u) {     // bubble (v, ix) into the sorted lane list
           const bool better = v > lv[u] || (v == lv[u] && ix < li[u]);
           const float tv = better ? lv[u] : v;
           const int ti = better ? li[u] : ix;
@@ -338,7 +341,7 @@ __global__ __launch_bounds__(256) void beam_step_kernel(
       float bv = -INFINITY;
       int bi = 0x7fffffff;
 #pragma unroll
-      for (int t = 0; t < MB; ++t) {
+      for (int t = 0; t < LMB; ++t) {
         const float v = lv[t];
         const int ix = li[t];
         // strictly after the previous pick in (value desc, index asc) order
@@ -403,9 +406,9 @@ __global__ __launch_bounds__(256) void beam_step_kernel(
   for (int q = 0; q < beam; ++q) {
     const int src = first ? r0 : r0 + sel_src[q];
     const int dst = r0 + q;
-    for (int s = threadIdx.x; s < step; s += 256)
+    for (int s = threadIdx.x; s < step; s += nthr)
       tokens_tmp[(long)dst * max_steps + s] = tokens[(long)src * max_steps + s];
-    for (int s = threadIdx.x; s < Lmax; s += 256) {
+    for (int s = threadIdx.x; s < Lmax; s += nthr) {
       int v;
       if (first) v = s < P ? r0 : -1;                       // prompt lives in clip row r0
       else v = s < P ? kvrow[(long)src * Lmax + s] : (s == P ? src : -1);
@@ -415,9 +418,9 @@ __global__ __launch_bounds__(256) void beam_step_kernel(
   __syncthreads();
   for (int q = 0; q < beam; ++q) {
     const int dst = r0 + q;
-    for (int s = threadIdx.x; s < step; s += 256)
+    for (int s = threadIdx.x; s < step; s += nthr)
       tokens[(long)dst * max_steps + s] = tokens_tmp[(long)dst * max_steps + s];
-    for (int s = threadIdx.x; s < Lmax; s += 256)
+    for (int s = threadIdx.x; s < Lmax; s += nthr)
       kvrow[(long)dst * Lmax + s] = kvrow_tmp[(long)dst * Lmax + s];
   }
   __syncthreads();
@@ -615,9 +618,16 @@ extern "C" int zs_beam_step(const float* part_stat, const float* part_val, const
                             void* stream) {
   ZS_REQUIRE(C > 0 && beam >= 1 && beam <= 8 && topk >= beam && nblk > 0,
              "zs_beam_step: 1 <= beam <= 8, topk >= beam");
-  hipLaunchKernelGGL(beam_step_kernel, dim3(C), dim3(256), 0, S(stream), part_stat, part_val,
-                     part_idx, beam, nblk, topk, first, stop, step_ctr, max_steps, scores, seq_len,
-                     stopped, tokens, tokens_tmp, kvrow, kvrow_tmp, Lmax, pos, next_tok);
+  // one wave per source row (at least 4 waves for the history gathers)
+  const dim3 blk(64 * (beam < 4 ? 4 : beam));
+  if (beam <= 5)
+    hipLaunchKernelGGL(beam_step_kernel<5>, dim3(C), blk, 0, S(stream), part_stat, part_val,
+                       part_idx, beam, nblk, topk, first, stop, step_ctr, max_steps, scores,
+                       seq_len, stopped, tokens, tokens_tmp, kvrow, kvrow_tmp, Lmax, pos, next_tok);
+  else
+    hipLaunchKernelGGL(beam_step_kernel<8>, dim3(C), blk, 0, S(stream), part_stat, part_val,
+                       part_idx, beam, nblk, topk, first, stop, step_ctr, max_steps, scores,
+                       seq_len, stopped, tokens, tokens_tmp, kvrow, kvrow_tmp, Lmax, pos, next_tok);
   ZS_LAUNCH_CHECK();
   hipLaunchKernelGGL(beam_advance_kernel, dim3(1), dim3(1024), 0, S(stream), stopped, C * beam,
                      step_ctr, max_steps, all_done);
