@@ -429,7 +429,7 @@ def _decode_attention_bf16_body(cuda, use_kvrow, variant, R, D, H, Lmax):
     try:
         ops.decode_attention(qkv, R, D, H, kc, vc, Lmax, pos, out, kvrow=kvrow)
     finally:
-        call("zs_tune_set", b"decode_attn5", 3)
+        call("zs_tune_set", b"decode_attn5", 6)
     qf = qkv.float()
     for r in range(R):
         p = int(pos[r])
@@ -501,9 +501,39 @@ def test_decode_attention_dpp_bitwise(cuda):
         try:
             ops.decode_attention(qkv, R, D, H, kc, vc, Lmax, pos, out)
         finally:
-            call("zs_tune_set", b"decode_attn5", 4)
+            call("zs_tune_set", b"decode_attn5", 6)
         outs.append(out)
     assert torch.equal(outs[0], outs[1])
+
+
+@pytest.mark.parametrize("R", [80, 400])
+def test_decode_attention_beam_xcd_groups(cuda, R):
+    """Beam rows grouped per XCD (beam_xcd: rows 5 g .. 5 g + 4 on one XCD) only reorders the
+    workgroups: outputs and cache appends equal the ungrouped launch bit for bit."""
+    from zsaac import ops
+    from zsaac._lib import call
+    g = torch.Generator(device=cuda).manual_seed(R)
+    H, Lmax = 12, 70
+    D = 64 * H
+    kc0 = torch.randn(R, H, Lmax, 64, device=cuda, generator=g).bfloat16()
+    vc0 = torch.randn(R, H, Lmax, 64, device=cuda, generator=g).bfloat16()
+    qkv = torch.randn(R, 3 * D, device=cuda, generator=g).bfloat16()
+    # a clip's beams share one position (the new token's slot is never a key of this step)
+    clip = torch.arange(R, device=cuda) // 5
+    pos = torch.randint(1, Lmax, (R // 5,), device=cuda, generator=g, dtype=torch.int32)[clip]
+    kvrow = (clip[:, None] * 5 + torch.randint(0, 5, (R, Lmax), device=cuda, generator=g)).int()
+    res = []
+    for grp in (5, 1):
+        kc, vc = kc0.clone(), vc0.clone()
+        out = torch.empty(R, D, device=cuda, dtype=torch.bfloat16)
+        call("zs_tune_set", b"beam_xcd", grp)
+        try:
+            ops.decode_attention(qkv, R, D, H, kc, vc, Lmax, pos, out, kvrow=kvrow)
+        finally:
+            call("zs_tune_set", b"beam_xcd", 5)
+        res.append((out, kc, vc))
+    for a, b in zip(res[0], res[1]):
+        assert torch.equal(a, b)
 
 
 @pytest.mark.parametrize("nrows", [1, 700, 2500])

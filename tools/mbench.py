@@ -397,7 +397,8 @@ def bench_attn_beam():
     # kvrow: each row's keys come from the rows of its own clip (a clip's 5 beams)
     clip = torch.arange(R, device=dev) // beam
     kvrow = (clip[:, None] * beam + torch.randint(0, beam, (R, Lmax), device=dev)).int().contiguous()
-    arms = [("v4", {"decode_attn5": 4}), ("v3", {"decode_attn5": 3}), ("v2", {"decode_attn5": 2}),
+    arms = [("v4", {"decode_attn5": 4}), ("v4_noxcd", {"decode_attn5": 4, "beam_xcd": 1}),
+            ("v3", {"decode_attn5": 3}), ("v2", {"decode_attn5": 2}),
             ("v5", {"decode_attn5": 5}), ("v6", {"decode_attn5": 6}),
             ("small128", {"small_rmax": 4096, "attn_split": 0}),
             ("small_s1", {"small_rmax": 4096, "attn_split": 1}),
@@ -411,9 +412,10 @@ def bench_attn_beam():
                 call("zs_tune_set", k.encode(), v)
             r[name] = timeit(lambda: ops.decode_attention(qkv, R, D, H, kc, vc, Lmax, pos, out,
                                                           kvrow=kvrow), reps=20)
-            call("zs_tune_set", b"decode_attn5", 4)
+            call("zs_tune_set", b"decode_attn5", 6)
             call("zs_tune_set", b"small_rmax", 128)
             call("zs_tune_set", b"attn_split", 3)
+            call("zs_tune_set", b"beam_xcd", 5)
         print(f"beam attn R={R} L={L}: " + "  ".join(
             f"{n}={t:7.2f}us ({byts / t / 1e3:5.0f} GB/s)" for n, t in r.items()), flush=True)
 

@@ -12,7 +12,8 @@ namespace zs {
 int g_small_attn = 1;     // R <= 128: decode_attn6 with 128-key phases
 int g_small_rmax = 128;   // zs_tune_set("small_rmax", r): the row count up to which the small-R
                           // decode attention kernels are taken
-int g_decode_attn5 = 4;   // 5: decode_attn6 16-key phases + next-phase prefetch; 4/3/2: decode_attn6 (phases of 16/32/64 keys), 1: decode_attn5, 0: LDS
+int g_beam_xcd = 5;       // zs_tune_set("beam_xcd", g): beam-row groups per XCD (1 = off)
+int g_decode_attn5 = 6;   // 6: decode_attn6 16-key phases, DPP reductions; 5: + next-phase prefetch; 4/3/2: decode_attn6 (phases of 16/32/64 keys), 1: decode_attn5, 0: LDS
 int g_window_mfma = 1;    // zs_tune_set("window_mfma", 0): VALU window attention for bf16   // zs_tune_set("decode_attn5", 0): LDS-staged decode_attn4 for bf16
 
 // ------------------------------------------------------------------ HTSAT window attention
@@ -684,13 +685,20 @@ template <typename T, int KPP = 64, bool PF = false, bool DPP = false, int SPLIT
 __global__ __launch_bounds__(256) void decode_attn6_kernel(
     const T* __restrict__ qkv, int D, int heads, T* __restrict__ kc, T* __restrict__ vc, int Lmax,
     const int* __restrict__ pos, const int* __restrict__ kvrow, T* __restrict__ out,
-    const int* __restrict__ rowmap, const int* __restrict__ cpos, int nphys) {
+    const int* __restrict__ rowmap, const int* __restrict__ cpos, int nphys, int rgrp) {
   using V8 = Pk8<T>;
   static_assert(SPLIT == 1 || ((SPLIT == 2 || SPLIT == 4) && !PF), "SPLIT 2 / 4 without prefetch");
   constexpr int HD = 64, EPC = 8, NG = KPP / 8;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int slice = wid % SPLIT;
-  const int c = blockIdx.x, h = blockIdx.y * (4 / SPLIT) + wid / SPLIT;
+  // rgrp > 1 (beam search, gridDim.x % (8 rgrp) == 0): rows in groups of rgrp consecutive rows
+  // (one clip's beams, whose cached prompt and shared history are the same cache rows through
+  // kvrow) go to one XCD at about the same time (workgroups are dealt round-robin over the 8 XCDs:
+  // b and b + 8 share one), so a group's shared keys are read from HBM once and from L2 after
+  const int c = rgrp > 1 ? ((blockIdx.x & 7) + 8 * ((blockIdx.x >> 3) / rgrp)) * rgrp +
+                               (blockIdx.x >> 3) % rgrp
+                         : blockIdx.x;
+  const int h = blockIdx.y * (4 / SPLIT) + wid / SPLIT;
   __shared__ float merge[SPLIT == 1 ? 1 : 4][66];
   if (SPLIT == 1 && h >= heads) return;
   const int grp = lane >> 3, sub = lane & 7;
@@ -1048,24 +1056,24 @@ extern "C" int zs_decode_attention_map(const void* qkv, int R, const int* rowmap
   } else if (g_decode_attn5 == 2) {
     hipLaunchKernelGGL((decode_attn6_kernel<bf16_t, 64>), dim3(R, cdiv(heads, 4)), dim3(256), 0,
                        S(stream), (const bf16_t*)qkv, D, heads, (bf16_t*)kc, (bf16_t*)vc, Lmax,
-                       pos, (const int*)nullptr, (bf16_t*)out, rowmap, cpos, nphys);
+                       pos, (const int*)nullptr, (bf16_t*)out, rowmap, cpos, nphys, 1);
   } else if (g_decode_attn5 == 4) {
     hipLaunchKernelGGL((decode_attn6_kernel<bf16_t, 16>), dim3(R, cdiv(heads, 4)), dim3(256), 0,
                        S(stream), (const bf16_t*)qkv, D, heads, (bf16_t*)kc, (bf16_t*)vc, Lmax,
-                       pos, (const int*)nullptr, (bf16_t*)out, rowmap, cpos, nphys);
+                       pos, (const int*)nullptr, (bf16_t*)out, rowmap, cpos, nphys, 1);
   } else if (g_decode_attn5 == 5) {
     hipLaunchKernelGGL((decode_attn6_kernel<bf16_t, 16, true>), dim3(R, cdiv(heads, 4)), dim3(256),
                        0, S(stream), (const bf16_t*)qkv, D, heads, (bf16_t*)kc, (bf16_t*)vc, Lmax,
-                       pos, (const int*)nullptr, (bf16_t*)out, rowmap, cpos, nphys);
+                       pos, (const int*)nullptr, (bf16_t*)out, rowmap, cpos, nphys, 1);
   } else if (g_decode_attn5 == 6) {
     hipLaunchKernelGGL((decode_attn6_kernel<bf16_t, 16, false, true>), dim3(R, cdiv(heads, 4)),
                        dim3(256), 0, S(stream), (const bf16_t*)qkv, D, heads, (bf16_t*)kc,
                        (bf16_t*)vc, Lmax, pos, (const int*)nullptr, (bf16_t*)out, rowmap, cpos,
-                       nphys);
+                       nphys, 1);
   } else {
     hipLaunchKernelGGL((decode_attn6_kernel<bf16_t, 32>), dim3(R, cdiv(heads, 4)), dim3(256), 0,
                        S(stream), (const bf16_t*)qkv, D, heads, (bf16_t*)kc, (bf16_t*)vc, Lmax,
-                       pos, (const int*)nullptr, (bf16_t*)out, rowmap, cpos, nphys);
+                       pos, (const int*)nullptr, (bf16_t*)out, rowmap, cpos, nphys, 1);
   }
   ZS_LAUNCH_CHECK();
   return 0;
@@ -1095,12 +1103,14 @@ extern "C" int zs_decode_attention(const void* qkv, int R, int D, int heads, voi
              "zs_decode_attention: head_dim must be 64");
   ZS_REQUIRE(Lmax > 0 && Lmax <= 4096, "zs_decode_attention: Lmax");
   dim3 grid(R, heads);
+  // beam rows (kvrow != NULL): groups of g_beam_xcd consecutive rows per XCD (decode_attn6_kernel)
+  const int rg = (kvrow && g_beam_xcd > 1 && R % (8 * g_beam_xcd) == 0) ? g_beam_xcd : 1;
   if (dtype == ZS_F32 && R <= g_small_rmax && g_small_attn && g_attn_split && heads % 2 == 0) {
     // the f32 parity mode's decode: the bf16 path's two-wave split with 32-key phases
     hipLaunchKernelGGL((decode_attn6_kernel<float, 32, false, true, 2>), dim3(R, heads / 2),
                        dim3(256), 0, S(stream), (const float*)qkv, D, heads, (float*)kc,
                        (float*)vc, Lmax, pos, kvrow, (float*)out, (const int*)nullptr,
-                       (const int*)nullptr, R);
+                       (const int*)nullptr, R, rg);
     ZS_LAUNCH_CHECK();
     return 0;
   }
@@ -1109,7 +1119,7 @@ extern "C" int zs_decode_attention(const void* qkv, int R, int D, int heads, voi
     hipLaunchKernelGGL((decode_attn6_kernel<bf16_t, 32, false, true, 4>), dim3(R, heads),
                        dim3(256), 0, S(stream), (const bf16_t*)qkv, D, heads, (bf16_t*)kc,
                        (bf16_t*)vc, Lmax, pos, kvrow, (bf16_t*)out, (const int*)nullptr,
-                       (const int*)nullptr, R);
+                       (const int*)nullptr, R, rg);
     ZS_LAUNCH_CHECK();
     return 0;
   }
@@ -1120,12 +1130,12 @@ extern "C" int zs_decode_attention(const void* qkv, int R, int D, int heads, voi
       hipLaunchKernelGGL((decode_attn6_kernel<bf16_t, 32, false, true, 2>), dim3(R, heads / 2),
                          dim3(256), 0, S(stream), (const bf16_t*)qkv, D, heads, (bf16_t*)kc,
                          (bf16_t*)vc, Lmax, pos, kvrow, (bf16_t*)out, (const int*)nullptr,
-                         (const int*)nullptr, R);
+                         (const int*)nullptr, R, rg);
     else
       hipLaunchKernelGGL((decode_attn6_kernel<bf16_t, 64, false, true, 2>), dim3(R, heads / 2),
                          dim3(256), 0, S(stream), (const bf16_t*)qkv, D, heads, (bf16_t*)kc,
                          (bf16_t*)vc, Lmax, pos, kvrow, (bf16_t*)out, (const int*)nullptr,
-                         (const int*)nullptr, R);
+                         (const int*)nullptr, R, rg);
     ZS_LAUNCH_CHECK();
     return 0;
   }
@@ -1135,14 +1145,14 @@ extern "C" int zs_decode_attention(const void* qkv, int R, int D, int heads, voi
     hipLaunchKernelGGL((decode_attn6_kernel<bf16_t, 128, false, true>), dim3(R, cdiv(heads, 4)),
                        dim3(256), 0, S(stream), (const bf16_t*)qkv, D, heads, (bf16_t*)kc,
                        (bf16_t*)vc, Lmax, pos, kvrow, (bf16_t*)out, (const int*)nullptr,
-                       (const int*)nullptr, R);
+                       (const int*)nullptr, R, rg);
     ZS_LAUNCH_CHECK();
     return 0;
   }
   if (dtype == ZS_BF16 && g_decode_attn5 == 4) {
     hipLaunchKernelGGL((decode_attn6_kernel<bf16_t, 16>), dim3(R, cdiv(heads, 4)), dim3(256), 0,
                        S(stream), (const bf16_t*)qkv, D, heads, (bf16_t*)kc, (bf16_t*)vc, Lmax,
-                       pos, kvrow, (bf16_t*)out, (const int*)nullptr, (const int*)nullptr, R);
+                       pos, kvrow, (bf16_t*)out, (const int*)nullptr, (const int*)nullptr, R, rg);
     ZS_LAUNCH_CHECK();
     return 0;
   }
@@ -1150,28 +1160,28 @@ extern "C" int zs_decode_attention(const void* qkv, int R, int D, int heads, voi
     hipLaunchKernelGGL((decode_attn6_kernel<bf16_t, 16, false, true>), dim3(R, cdiv(heads, 4)),
                        dim3(256), 0, S(stream), (const bf16_t*)qkv, D, heads, (bf16_t*)kc,
                        (bf16_t*)vc, Lmax, pos, kvrow, (bf16_t*)out, (const int*)nullptr,
-                       (const int*)nullptr, R);
+                       (const int*)nullptr, R, rg);
     ZS_LAUNCH_CHECK();
     return 0;
   }
   if (dtype == ZS_BF16 && g_decode_attn5 == 5) {
     hipLaunchKernelGGL((decode_attn6_kernel<bf16_t, 16, true>), dim3(R, cdiv(heads, 4)), dim3(256),
                        0, S(stream), (const bf16_t*)qkv, D, heads, (bf16_t*)kc, (bf16_t*)vc, Lmax,
-                       pos, kvrow, (bf16_t*)out, (const int*)nullptr, (const int*)nullptr, R);
+                       pos, kvrow, (bf16_t*)out, (const int*)nullptr, (const int*)nullptr, R, rg);
     ZS_LAUNCH_CHECK();
     return 0;
   }
   if (dtype == ZS_BF16 && g_decode_attn5 == 3) {
     hipLaunchKernelGGL((decode_attn6_kernel<bf16_t, 32>), dim3(R, cdiv(heads, 4)), dim3(256), 0,
                        S(stream), (const bf16_t*)qkv, D, heads, (bf16_t*)kc, (bf16_t*)vc, Lmax,
-                       pos, kvrow, (bf16_t*)out, (const int*)nullptr, (const int*)nullptr, R);
+                       pos, kvrow, (bf16_t*)out, (const int*)nullptr, (const int*)nullptr, R, rg);
     ZS_LAUNCH_CHECK();
     return 0;
   }
   if (dtype == ZS_BF16 && g_decode_attn5 == 2) {
     hipLaunchKernelGGL(decode_attn6_kernel<bf16_t>, dim3(R, cdiv(heads, 4)), dim3(256), 0,
                        S(stream), (const bf16_t*)qkv, D, heads, (bf16_t*)kc, (bf16_t*)vc, Lmax,
-                       pos, kvrow, (bf16_t*)out, (const int*)nullptr, (const int*)nullptr, R);
+                       pos, kvrow, (bf16_t*)out, (const int*)nullptr, (const int*)nullptr, R, rg);
     ZS_LAUNCH_CHECK();
     return 0;
   }
