@@ -88,6 +88,31 @@ def bench_gemm_m():
                   flush=True)
 
 
+def bench_gemm_c3():
+    """The C3 beam decode's GEMMs (M = 1280 rows) under each lean tile the dispatch can force
+    (fast_tile 100 + lt) against the default pick, TF/s."""
+    from zsaac import ops
+    from zsaac._lib import call
+    dev = torch.device("cuda", 0)
+    M = int(os.environ.get("ZS_M", 1280))
+    for N, K, name in ((2304, 768, "qkv"), (768, 768, "proj"), (3072, 768, "fc"), (768, 3072, "mproj")):
+        a = torch.randn(M, K, device=dev).bfloat16()
+        w = (torch.randn(N, K, device=dev) * 0.02).bfloat16()
+        b = torch.randn(N, device=dev)
+        out = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+        res = {"default": timeit(lambda: ops.gemm(a, w, out, bias=b, split_k=1))}
+        for lt in (1, 2, 3, 5, 6, 8, 9, 10, 11, 12, 13):
+            call("zs_tune_set", b"fast_tile", 100 + lt)
+            try:
+                res[f"lt{lt}"] = timeit(lambda: ops.gemm(a, w, out, bias=b, split_k=1))
+            except Exception:
+                pass
+            call("zs_tune_set", b"fast_tile", 0)
+        fl = 2 * M * N * K
+        print(f"M{M} {name:6s} N{N} K{K}  " + "  ".join(f"{k}={v:6.2f}us/{fl / v / 1e6:4.0f}"
+                                                   for k, v in res.items()), flush=True)
+
+
 def bench_gemm_htsat():
     """HTSAT encoder GEMM shapes for one 64-clip batch: tokens 4096/1024/256/64 per clip."""
     from zsaac import ops
@@ -551,4 +576,4 @@ if __name__ == "__main__":
             call("zs_tune_set", k.encode(), int(v))
     which = sys.argv[1:] or ["gemm", "attn"]
     for wname in which:
-        {"gemm": bench_gemm, "rows": bench_rows, "gemm_m": bench_gemm_m, "gemm_htsat": bench_gemm_htsat, "gemm_dbg": bench_gemm_dbg, "lmhead": bench_lmhead, "overhead": bench_overhead, "front": bench_front, "window": bench_window, "decode_gemm": bench_decode_gemm, "attn": bench_attn, "attn_beam": bench_attn_beam, "gemm_big": bench_gemm_big, "inflight": bench_inflight, "buckets": bench_buckets, "compact_ab": bench_compact_ab, "host": bench_host}[wname]()
+        {"gemm": bench_gemm, "rows": bench_rows, "gemm_m": bench_gemm_m, "gemm_c3": bench_gemm_c3, "gemm_htsat": bench_gemm_htsat, "gemm_dbg": bench_gemm_dbg, "lmhead": bench_lmhead, "overhead": bench_overhead, "front": bench_front, "window": bench_window, "decode_gemm": bench_decode_gemm, "attn": bench_attn, "attn_beam": bench_attn_beam, "gemm_big": bench_gemm_big, "inflight": bench_inflight, "buckets": bench_buckets, "compact_ab": bench_compact_ab, "host": bench_host}[wname]()

@@ -715,7 +715,11 @@ static int dispatch_fast(GemmArgs& g, hipStream_t st) {
     if (!lt && n128 >= 128) return launch_lean<128, 128, 4, 64, 2, 4>(g, st);
     if (lt == 2 || (!lt && nblocks(g, 128, 64) >= 256))
       return g.M >= g.N ? launch_lean<128, 64, 3, 64>(g, st) : launch_lean<64, 128, 3, 64>(g, st);
-    if (lt == 3 && g.K % 128 == 0) return launch_lean<64, 64, 2, 128>(g, st);
+    // 64x64 with 128-deep k-steps when a 64x64 grid is still under one tile per CU at >= 512
+    // rows (the C3 beam decode's N = 768 projections at 1280 rows: proj 7.1 -> 6.5 us, mproj
+    // 19.2 -> 17.7 us, tools/mbench.py gemm_c3)
+    if ((lt == 3 || (!lt && g.M >= 512 && nblocks(g, 64, 64) < 256)) && g.K % 128 == 0)
+      return launch_lean<64, 64, 2, 128>(g, st);
     // 8-wave tiles at one block per CU (experiments)
     if (lt == 5) return launch_lean<256, 128, 2, 64, 4, 2>(g, st);
     if (lt == 6) return launch_lean<128, 256, 2, 64, 2, 4>(g, st);
