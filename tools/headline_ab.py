@@ -1,0 +1,79 @@
+#!/usr/bin/env python3
+"""Headline A/B in ONE process: the bench's C2 timed region (1045 clips, bs 64, persistent
+decode) repeated for several arms, interleaved, so box-to-box and run-to-run spread cancel.
+
+An arm is "name:inflight:knob=v,knob=v" (zs_tune_set knobs, reset to the baseline values given
+with --base between arms); every arm runs on the first arm's streams, so list the arm with the
+most batches in flight first.
+
+    python tools/headline_ab.py --reps 6 "base:5:" "l64:5:lean_min128=64"
+"""
+import argparse
+import os
+import statistics
+import sys
+import time
+from types import SimpleNamespace
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "zero-shot-aac_amd"))
+
+import torch  # noqa: E402
+
+import bench  # noqa: E402
+from zsaac import _lib  # noqa: E402
+from zsaac.pipeline import ConcurrentRunner  # noqa: E402
+
+
+def knobs(spec):
+    out = {}
+    for kv in filter(None, spec.split(",")):
+        k, v = kv.split("=")
+        out[k.strip()] = int(v)
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--clips", type=int, default=1045)
+    ap.add_argument("--base", default="lean_min128=256", help="knob values restored between arms")
+    ap.add_argument("arms", nargs="+")
+    a = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    args = SimpleNamespace(dtype="bf16", group=1, encoder="htsat", mapper="mlp", batch=64,
+                           encoder_batch=0, beam=0, entry_length=67, compact=1)
+    pipe, _, _ = bench.build(args, dev)
+    pool = bench.synthetic_clips(a.clips, 0, dev)
+    batches = [pool[x:y] for x, y in bench.split_batches(a.clips, 64)]
+    base = knobs(a.base)
+    arms = []
+    streams = None       # one set of dedicated streams for every arm (distinct hardware queues)
+    for spec in a.arms:
+        name, inflight, kn = spec.split(":")
+        r = ConcurrentRunner(pipe, int(inflight), streams=streams)
+        streams = streams or r.streams
+        for size in sorted({b.shape[0] for b in batches}, reverse=True):
+            r.warmup(next(b for b in batches if b.shape[0] == size))
+        arms.append((name, r, knobs(kn)))
+    res = {n: [] for n, _, _ in arms}
+    for rep in range(a.reps + 1):
+        for name, r, kn in arms:
+            for k, v in {**base, **kn}.items():
+                _lib.call("zs_tune_set", k.encode(), v)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            r.run(batches)
+            torch.cuda.synchronize()
+            dt = time.perf_counter() - t0
+            if rep:                     # rep 0 warms every arm's kernels up
+                res[name].append(a.clips / dt)
+        if rep:
+            print(f"rep {rep}: " + "  ".join(f"{n} {res[n][-1]:.0f}" for n in res), flush=True)
+    for n, v in res.items():
+        print(f"{n:12s} median {statistics.median(v):8.1f} clips/s  min {min(v):8.1f}  max {max(v):8.1f}")
+
+
+if __name__ == "__main__":
+    main()

@@ -667,6 +667,7 @@ static long nblocks(const GemmArgs& g, int bm, int bn) {
 
 int g_fast_ns = 2;     // zs_tune_set("fast_ns", n): stages of the 128x128 tile (experiment knob)
 int g_fast_tile = 0;   // zs_tune_set("fast_tile", t): force a tile (see dispatch_fast)
+int g_lean_min128 = 256;  // zs_tune_set("lean_min128", n): 128x128 2-stage tiles from n tiles up
 
 // largest tile that still puts >= 1 block on every CU, else the smallest
 static int dispatch_fast(GemmArgs& g, hipStream_t st) {
@@ -711,7 +712,7 @@ static int dispatch_fast(GemmArgs& g, hipStream_t st) {
     // 8 column tiles, 2 blocks per CU (8192x768x3072 56.4 vs 59.2 us, 6144x768x3072 50.2 vs 53.7)
     if (!lt && g_lean96 && g.N % 96 == 0 && g.N <= 1536 && nblocks(g, 128, 96) >= 384)
       return launch_lean<128, 96, 2, 64, 4, 1>(g, st);
-    if (lt == 1 || (!lt && n128 >= 256)) return launch_lean<128, 128, 2, 64>(g, st);
+    if (lt == 1 || (!lt && n128 >= g_lean_min128)) return launch_lean<128, 128, 2, 64>(g, st);
     if (!lt && n128 >= 128) return launch_lean<128, 128, 4, 64, 2, 4>(g, st);
     if (lt == 2 || (!lt && nblocks(g, 128, 64) >= 256))
       return g.M >= g.N ? launch_lean<128, 64, 3, 64>(g, st) : launch_lean<64, 128, 3, 64>(g, st);

@@ -247,7 +247,7 @@ class ConcurrentRunner:
 
     Results are copied out on the pipeline's stream before it takes the next batch."""
 
-    def __init__(self, pipe: CaptionPipeline, n_inflight: int = 2):
+    def __init__(self, pipe: CaptionPipeline, n_inflight: int = 2, streams: Optional[list] = None):
         if pipe.decoder.persist:
             # persistent decode grids must be co-resident: at most CUs // grid launches in flight
             cus = torch.cuda.get_device_properties(pipe.dev).multi_processor_count
@@ -256,7 +256,10 @@ class ConcurrentRunner:
         self.pipes = [pipe] + [pipe.twin() for _ in range(n_inflight - 1)]
         # dedicated streams on distinct hardware queues: pooled torch streams take their queue at
         # first use and can end up sharing one, which serializes the batches
-        self.streams = ops.dedicated_streams(len(self.pipes), pipe.dev)
+        # (``streams``: reuse another runner's, at least as many -- tools/headline_ab.py)
+        self.streams = (list(streams[:len(self.pipes)]) if streams is not None
+                        else ops.dedicated_streams(len(self.pipes), pipe.dev))
+        assert len(self.streams) == len(self.pipes), "ConcurrentRunner: too few streams given"
         # persistent grid per launch: decode_persist_grid() workgroups (row_split 1) or twice that
         # (row_split 2, a ~25% shorter step for ~50% more CU time); see run()
         self.cus = torch.cuda.get_device_properties(pipe.dev).multi_processor_count
