@@ -34,6 +34,8 @@
 
 namespace zs {
 int g_dp_xb = 1;   // zs_tune_set("dp_xb", 0): LayerNorm inputs from the f32 x (A/B)
+int g_dp_nt = 2;   // zs_tune_set("dp_nt", m): non-temporal loads, bit 0 weights + LM head (slower:
+                   // the concurrent grids share them through L2 / MALL), bit 1 cached K/V (default)
 namespace dpk {
 
 constexpr int D = 768, NH = 12, HD = 64, DFF = 3072, NLY = 12, RM = 64, QKVN = 3 * D;
@@ -165,8 +167,15 @@ __device__ __forceinline__ void lds_sync() {
   asm volatile("" ::: "memory");
 }
 
+// a 16-byte global load, non-temporal (nt: streamed once, evict-first in L2) when NTL
+template <bool NTL, typename T>
+__device__ __forceinline__ T ldg(const T* p) {
+  if constexpr (NTL) return __builtin_nontemporal_load(p);
+  else return *p;
+}
+
 // weight fragments of NB 16-column blocks x S k-steps (MFMA B operand, W [N][K] row-major)
-template <int NB, int S>
+template <int NB, int S, bool NTL = false>
 __device__ __forceinline__ void load_w(const bf16_t* W, int K, int n0, int N, int kbase,
                                        bf16x8_t (&b)[NB * S]) {
   const int lane = otid() & 63, fr = lane & 15, fk = 8 * (lane >> 4);
@@ -174,7 +183,8 @@ __device__ __forceinline__ void load_w(const bf16_t* W, int K, int n0, int N, in
   for (int nb = 0; nb < NB; ++nb) {
     const bf16_t* row = W + (long)min(n0 + 16 * nb + fr, N - 1) * K + kbase + fk;
 #pragma unroll
-    for (int s = 0; s < S; ++s) b[nb * S + s] = *reinterpret_cast<const bf16x8_t*>(row + 32 * s);
+    for (int s = 0; s < S; ++s)
+      b[nb * S + s] = ldg<NTL>(reinterpret_cast<const bf16x8_t*>(row + 32 * s));
   }
 }
 
@@ -404,15 +414,17 @@ __device__ __forceinline__ void phase_qkv(const Args& a, const Rs& rs, int l, ch
   bf16_t* hs = reinterpret_cast<bf16_t*>(smem);
   float* red = reinterpret_cast<float*>(smem);
   const int tid = otid(), v = tid >> 6, r0 = h * NR;
-  // epilogue quads (issued first): NR rows x 12 column quads, quads tid and tid + 512
+  // epilogue quads: NR rows x 12 column quads, quads tid and tid + 512.  The bias quads are
+  // issued after the MFMAs (issued before the LayerNorm they were spilled, and the spill store
+  // waited for the load at the top of the phase)
   const int c0 = 4 * (tid % 12), c1 = 4 * ((tid + 512) % 12);
-  const float4 b0 = *reinterpret_cast<const float4*>(a.bqkv[l] + 48 * w + c0);
-  const float4 b1 = *reinterpret_cast<const float4*>(a.bqkv[l] + 48 * w + c1);
   if (l == 0) ln_rows<1, NR>(a, rs, hs, s_tok, s_pos, w, nullptr, r0);
   else ln_rows<0, NR, XB>(a, rs, hs, s_tok, s_pos, w, nullptr, r0);
   lds_sync();
   f32x4_t acc[NRB][3];
   mma_lds<3, 3, NRB>(hs, 96 * v, wq, acc);
+  const float4 b0 = *reinterpret_cast<const float4*>(a.bqkv[l] + 48 * w + c0);
+  const float4 b1 = *reinterpret_cast<const float4*>(a.bqkv[l] + 48 * w + c1);
   lds_sync();
   put_partial<3, 48, NRB>(red, v, 0, acc);
   lds_sync();
@@ -461,7 +473,7 @@ __device__ __forceinline__ void attn_unit(const Args& a, const int* s_pos, int u
   p = min(s_pos[rr], a.Lmax - 1);
   base = ((long)(rr * NH + hh) * a.Lmax) * HD + 8 * ((otid() & 63) & 7);
 }
-template <int KU>
+template <int KU, bool NTL = false>
 __device__ __forceinline__ void attn_load(const Args& a, int l, const int* s_pos, int ub, int cb,
                                           uint4 (&kr)[KU][8], uint4 (&vr)[KU][8]) {
   const int tid = otid(), v = tid >> 6, grp = (tid & 63) >> 3;
@@ -475,14 +487,14 @@ __device__ __forceinline__ void attn_load(const Args& a, int l, const int* s_pos
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       const int jc = max(min(cb + 8 * i + grp, p - 1), 0);
-      kr[k][i] = *reinterpret_cast<const uint4*>(kc + base + (long)jc * HD);
-      vr[k][i] = *reinterpret_cast<const uint4*>(vc + base + (long)jc * HD);
+      kr[k][i] = __builtin_bit_cast(uint4, ldg<NTL>(reinterpret_cast<const u32x4_t*>(kc + base + (long)jc * HD)));
+      vr[k][i] = __builtin_bit_cast(uint4, ldg<NTL>(reinterpret_cast<const u32x4_t*>(vc + base + (long)jc * HD)));
     }
   }
 }
 // The new token (key pos, from qkv) is folded in after the cached keys 0..pos-1 (one more
 // online-softmax update with its score and v), so the cached chunks need no per-key selects.
-template <int KU>
+template <int KU, bool NTL = false>
 __device__ __forceinline__ void phase_attn(const Args& a, const Rs& rs, int l, const int* s_pos, int ub,
                                            uint4 (&kr)[KU][8], uint4 (&vr)[KU][8]) {
   const int tid = otid(), lane = tid & 63, v = tid >> 6, grp = lane >> 3, sub = lane & 7;
@@ -507,7 +519,7 @@ __device__ __forceinline__ void phase_attn(const Args& a, const Rs& rs, int l, c
 #pragma unroll
   for (int k = 1; k < KU; ++k) pmax = max(pmax, p[k]);
   for (int cb = 0; cb < pmax; cb += 64) {       // cached keys 0 .. p - 1
-    if (cb > 0) attn_load<KU>(a, l, s_pos, ub, cb, kr, vr);
+    if (cb > 0) attn_load<KU, NTL>(a, l, s_pos, ub, cb, kr, vr);
 #pragma unroll
     for (int k = 0; k < KU; ++k) {
       if (cb >= p[k]) continue;                   // wave-uniform
@@ -698,14 +710,15 @@ __device__ __forceinline__ void phase_fc(const Args& a, const Rs& rs, int l, cha
 // its 16 rows.  The WG's best per row goes to a 64-bit agent-scope atomic max of
 // key = (order-preserving logit bits, ~id): larger logit wins, then the lower id (torch.argmax),
 // whatever order the workgroups arrive in.
+template <bool NTL>
 __device__ __forceinline__ void lm_piece(const bf16_t* Wp, int b0, int b1, int c, bf16x8_t (&b)[8]) {
   const int lane = otid() & 63;
   const bf16_t* p0 = Wp + ((long)(b0 * (D / 32) + 4 * c) * 64 + lane) * 8;
   const bf16_t* p1 = Wp + ((long)(b1 * (D / 32) + 4 * c) * 64 + lane) * 8;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    b[i] = *reinterpret_cast<const bf16x8_t*>(p0 + 512 * i);
-    b[4 + i] = *reinterpret_cast<const bf16x8_t*>(p1 + 512 * i);
+    b[i] = ldg<NTL>(reinterpret_cast<const bf16x8_t*>(p0 + 512 * i));
+    b[4 + i] = ldg<NTL>(reinterpret_cast<const bf16x8_t*>(p1 + 512 * i));
   }
 }
 __device__ __forceinline__ void lm_consume(const bf16_t* hs, int c, const bf16x8_t (&b)[8],
@@ -734,7 +747,7 @@ __device__ __forceinline__ void lm_consume(const bf16_t* hs, int c, const bf16x8
     }
   }
 }
-template <bool XB>
+template <bool XB, bool NTL>
 __device__ __forceinline__ void phase_lm(const Args& a, const Rs& rs, char* smem, const int* s_tok,
                                          const int* s_pos, float* am_v, int* am_i, int wg, int gg,
                                          gu64* keys, const float* s_lnf) {
@@ -755,8 +768,8 @@ __device__ __forceinline__ void phase_lm(const Args& a, const Rs& rs, char* smem
   auto blk = [&](int m, int h) { return min(b_lo + 2 * (v + NW * min(m, npw - 1)) + h, b_hi - 1); };
   const bool tmp = a.temp != 1.0f;
   bf16x8_t P0[8], P1[8], P2[8];
-  lm_piece(a.wtep, blk(0, 0), blk(0, 1), 0, P0);
-  lm_piece(a.wtep, blk(0, 0), blk(0, 1), 1, P1);
+  lm_piece<NTL>(a.wtep, blk(0, 0), blk(0, 1), 0, P0);
+  lm_piece<NTL>(a.wtep, blk(0, 0), blk(0, 1), 1, P1);
   for (int m = 0; m < npw; ++m) {
     const int b0 = blk(m, 0), b1 = blk(m, 1), n0 = blk(m + 1, 0), n1 = blk(m + 1, 1);
     f32x4_t acc[2][4];
@@ -764,17 +777,17 @@ __device__ __forceinline__ void phase_lm(const Args& a, const Rs& rs, char* smem
     for (int h = 0; h < 2; ++h)
 #pragma unroll
       for (int rb = 0; rb < 4; ++rb) acc[h][rb] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-    lm_piece(a.wtep, b0, b1, 2, P2);
+    lm_piece<NTL>(a.wtep, b0, b1, 2, P2);
     lm_consume(hs, 0, P0, acc);
-    lm_piece(a.wtep, b0, b1, 3, P0);
+    lm_piece<NTL>(a.wtep, b0, b1, 3, P0);
     lm_consume(hs, 1, P1, acc);
-    lm_piece(a.wtep, b0, b1, 4, P1);
+    lm_piece<NTL>(a.wtep, b0, b1, 4, P1);
     lm_consume(hs, 2, P2, acc);
-    lm_piece(a.wtep, b0, b1, 5, P2);
+    lm_piece<NTL>(a.wtep, b0, b1, 5, P2);
     lm_consume(hs, 3, P0, acc);
-    lm_piece(a.wtep, n0, n1, 0, P0);
+    lm_piece<NTL>(a.wtep, n0, n1, 0, P0);
     lm_consume(hs, 4, P1, acc);
-    lm_piece(a.wtep, n0, n1, 1, P1);
+    lm_piece<NTL>(a.wtep, n0, n1, 1, P1);
     lm_consume(hs, 5, P2, acc);
     // blocks in increasing id order within the lane: strict > keeps the lower id on ties
     const int p0 = b_lo + 2 * (v + NW * m);
@@ -842,8 +855,10 @@ __device__ __forceinline__ void gave_up(const Args& a) {
 // units of its rows, and 1/96 of the LM head's vocabulary for all rows.
 // XB: the LayerNorm inputs are handed off as a bf16 copy of x (written by phases C / E beside
 // the f32 residual stream), halving the bytes every workgroup reads in phases A, D and F.
-template <int RH, bool XB>
+// NTM: non-temporal loads, bit 0 the weight / LM-head streams, bit 1 the cached K/V
+template <int RH, bool XB, int NTM = 0>
 __global__ __launch_bounds__(NT) void decode_persist_kernel(Args a) {
+  constexpr bool NTW = NTM & 1, NTK = (NTM >> 1) & 1;
   __shared__ __attribute__((aligned(16))) char smem[SM_TOTAL];
   float* am_v = reinterpret_cast<float*>(smem + SM_HS);
   int* am_i = reinterpret_cast<int*>(smem + SM_HS) + NW * RM;
@@ -886,7 +901,7 @@ __global__ __launch_bounds__(NT) void decode_persist_kernel(Args a) {
 
   bf16x8_t wq[9], wp[3], wf[12], wm[12];
 #define V_ (otid() >> 6)
-  load_w<3, 3>(a.wqkv[0], D, 48 * w, QKVN, 96 * V_, wq);
+  load_w<3, 3, NTW>(a.wqkv[0], D, 48 * w, QKVN, 96 * V_, wq);
   for (;;) {
     bar.sb = (stamps != nullptr && step == stamp_step) ? stamps + (long)wg * 2 * DP_NB : nullptr;
     bar.n0 = bar.n;
@@ -895,16 +910,16 @@ __global__ __launch_bounds__(NT) void decode_persist_kernel(Args a) {
       phase_qkv<RH, XB>(a, rs, l, smem, s_tok, s_pos, w, h, wq);
       bar_arrive(bar);
       uint4 kr[2 / RH][8], vr[2 / RH][8];
-      attn_load<2 / RH>(a, l, s_pos, ub, 0, kr, vr);
+      attn_load<2 / RH, NTK>(a, l, s_pos, ub, 0, kr, vr);
       if (!bar_wait(bar, s_ok)) return gave_up(a);
       if (l == 0 && wg == 0 && otid() < RM)  // the previous step's argmax keys: every WG has read them
         __hip_atomic_store(lmkey + ((step + 1) & 1) * RM + otid(), 0ull, __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
 
-      phase_attn<2 / RH>(a, rs, l, s_pos, ub, kr, vr);
+      phase_attn<2 / RH, NTK>(a, rs, l, s_pos, ub, kr, vr);
       bar_arrive(bar);
-      load_w<1, 3>(a.wproj[l], D, 16 * w, D, 96 * V_, wp);
-      load_w<2, 6>(a.wfc[l], D, 64 * w + 32 * (V_ >> 2), DFF, 192 * (V_ & 3), wf);
+      load_w<1, 3, NTW>(a.wproj[l], D, 16 * w, D, 96 * V_, wp);
+      load_w<2, 6, NTW>(a.wfc[l], D, 64 * w + 32 * (V_ >> 2), DFF, 192 * (V_ & 3), wf);
       if (!bar_wait(bar, s_ok)) return gave_up(a);
 
       phase_proj<3, RH, XB>(a, rs, rs.att, D, a.bproj[l], smem, w, h, wp);
@@ -913,7 +928,7 @@ __global__ __launch_bounds__(NT) void decode_persist_kernel(Args a) {
 
       phase_fc<RH, XB>(a, rs, l, smem, s_tok, s_pos, w, h, wf);
       bar_arrive(bar);
-      load_w<1, 12>(a.wmp[l], DFF, 16 * w, D, 384 * V_, wm);
+      load_w<1, 12, NTW>(a.wmp[l], DFF, 16 * w, D, 384 * V_, wm);
       if (!bar_wait(bar, s_ok)) return gave_up(a);
 
       phase_proj<12, RH, XB>(a, rs, rs.hid, DFF, a.bmp[l], smem, w, h, wm);
@@ -921,12 +936,12 @@ __global__ __launch_bounds__(NT) void decode_persist_kernel(Args a) {
       // next block's c_attn.  Unconditional (a conditional load keeps the old wq live through
       // the whole block for the path that skips it); after block 11 the value is dead and wq is
       // reloaded after the LM head, which needs the VGPRs
-      load_w<3, 3>(a.wqkv[l + 1 < NLY ? l + 1 : 0], D, 48 * w, QKVN, 96 * V_, wq);
+      load_w<3, 3, NTW>(a.wqkv[l + 1 < NLY ? l + 1 : 0], D, 48 * w, QKVN, 96 * V_, wq);
       if (!bar_wait(bar, s_ok)) return gave_up(a);
     }
-    phase_lm<XB>(a, rs, smem, s_tok, s_pos, am_v, am_i, wg, GG, lmkey + (step & 1) * RM, s_lnf);
+    phase_lm<XB, NTW>(a, rs, smem, s_tok, s_pos, am_v, am_i, wg, GG, lmkey + (step & 1) * RM, s_lnf);
     bar_arrive(bar);
-    load_w<3, 3>(a.wqkv[0], D, 48 * w, QKVN, 96 * V_, wq);
+    load_w<3, 3, NTW>(a.wqkv[0], D, 48 * w, QKVN, 96 * V_, wq);
     if (!bar_wait(bar, s_ok)) return gave_up(a);
 
     // ---- G: every WG reads the per-row argmax (one agent-scope key per row) and applies
@@ -1031,13 +1046,22 @@ extern "C" int zs_gpt2_decode_persist(int R, int Lmax, int max_steps, int stop0,
   a.step_ctr = step_ctr; a.all_done = all_done; a.ws = (char*)ws;
   // the barrier counter and timeout word: zeroed before every launch (a memset node under capture)
   ZS_CHECK_HIP(hipMemsetAsync(ws, 0, WS_SYNC_BYTES, S(stream)));
+#define DP_LAUNCH(RH_, XB_, NTM_) \
+  hipLaunchKernelGGL((decode_persist_kernel<RH_, XB_, NTM_>), dim3(RH_ * G), dim3(NT), 0, S(stream), a)
   if (row_split == 2) {
-    if (g_dp_xb) hipLaunchKernelGGL((decode_persist_kernel<2, true>), dim3(2 * G), dim3(NT), 0, S(stream), a);
-    else hipLaunchKernelGGL((decode_persist_kernel<2, false>), dim3(2 * G), dim3(NT), 0, S(stream), a);
+    if (!g_dp_xb) DP_LAUNCH(2, false, 0);
+    else if (g_dp_nt == 1) DP_LAUNCH(2, true, 1);
+    else if (g_dp_nt == 2) DP_LAUNCH(2, true, 2);
+    else if (g_dp_nt == 3) DP_LAUNCH(2, true, 3);
+    else DP_LAUNCH(2, true, 0);
   } else {
-    if (g_dp_xb) hipLaunchKernelGGL((decode_persist_kernel<1, true>), dim3(G), dim3(NT), 0, S(stream), a);
-    else hipLaunchKernelGGL((decode_persist_kernel<1, false>), dim3(G), dim3(NT), 0, S(stream), a);
+    if (!g_dp_xb) DP_LAUNCH(1, false, 0);
+    else if (g_dp_nt == 1) DP_LAUNCH(1, true, 1);
+    else if (g_dp_nt == 2) DP_LAUNCH(1, true, 2);
+    else if (g_dp_nt == 3) DP_LAUNCH(1, true, 3);
+    else DP_LAUNCH(1, true, 0);
   }
+#undef DP_LAUNCH
   ZS_LAUNCH_CHECK();
   return 0;
 }
