@@ -10,16 +10,18 @@
 namespace zs {
 
 // ------------------------------------------------------------------ prompt
+constexpr int PB = 1024;   // threads per prompt / label-top-k block (4x the label rows in flight of 256)
 // sound_effect_choice (utils.py:131-137 / caption_model.py:15-20): the k labels of highest
 // similarity emb . label (softmax is monotone, so top-k of the raw similarities), best first,
-// ties to the lower label index; one 256-thread block per row, result in sel[0..k).
+// ties to the lower label index; one block per row (PB threads: one label row per thread, so
+// the block keeps PB rows streaming at once), result in sel[0..k).
 __device__ __forceinline__ void label_select(const float* __restrict__ emb, int D,
                                              const float* __restrict__ labels, int L, int k,
                                              float* e, float* sim, int* sel, float* rv, int* ri) {
   const int b = blockIdx.x;
-  for (int d = threadIdx.x; d < D; d += 256) e[d] = emb[(long)b * D + d];
+  for (int d = threadIdx.x; d < D; d += PB) e[d] = emb[(long)b * D + d];
   __syncthreads();
-  for (int l = threadIdx.x; l < L; l += 256) {
+  for (int l = threadIdx.x; l < L; l += PB) {
     const float* lr = labels + (long)l * D;
     float s = 0.f;
     for (int d = 0; d < D; ++d) s += e[d] * lr[d];
@@ -30,7 +32,7 @@ __device__ __forceinline__ void label_select(const float* __restrict__ emb, int 
   for (int q = 0; q < k; ++q) {
     float bv = -INFINITY;
     int bi = 0x7fffffff;
-    for (int l = threadIdx.x; l < L; l += 256) {
+    for (int l = threadIdx.x; l < L; l += PB) {
       bool taken = false;
       for (int p = 0; p < q; ++p) taken |= (sel[p] == l);
       if (!taken && (sim[l] > bv || (sim[l] == bv && l < bi))) { bv = sim[l]; bi = l; }
@@ -46,7 +48,7 @@ __device__ __forceinline__ void label_select(const float* __restrict__ emb, int 
     if (threadIdx.x == 0) {
       float v = rv[0];
       int i = ri[0];
-      for (int w = 1; w < 4; ++w)
+      for (int w = 1; w < PB / 64; ++w)
         if (rv[w] > v || (rv[w] == v && ri[w] < i)) { v = rv[w]; i = ri[w]; }
       sel[q] = i;
     }
@@ -54,7 +56,7 @@ __device__ __forceinline__ void label_select(const float* __restrict__ emb, int 
   }
 }
 
-__global__ __launch_bounds__(256) void prompt_kernel(const float* __restrict__ emb, int D,
+__global__ __launch_bounds__(PB) void prompt_kernel(const float* __restrict__ emb, int D,
                                                      const float* __restrict__ labels, int L,
                                                      int k, const int* __restrict__ ltok,
                                                      const int* __restrict__ llen, int max_tok,
@@ -63,8 +65,8 @@ __global__ __launch_bounds__(256) void prompt_kernel(const float* __restrict__ e
                                                      int* __restrict__ chosen) {
   extern __shared__ float sm[];
   __shared__ int sel[16];
-  __shared__ float rv[4];
-  __shared__ int ri[4];
+  __shared__ float rv[PB / 64];
+  __shared__ int ri[PB / 64];
   const int b = blockIdx.x;
   label_select(emb, D, labels, L, k, sm, sm + D, sel, rv, ri);
   if (threadIdx.x == 0) {
@@ -90,19 +92,19 @@ __global__ __launch_bounds__(256) void prompt_kernel(const float* __restrict__ e
 
 // the chosen labels' rows gathered: rows[b][q][:] = labels[sel[q]][:] (caption_model.py:15-20,
 // sound_effect_embeddings[index].squeeze(1)), and their indices
-__global__ __launch_bounds__(256) void label_topk_kernel(const float* __restrict__ emb, int D,
+__global__ __launch_bounds__(PB) void label_topk_kernel(const float* __restrict__ emb, int D,
                                                          const float* __restrict__ labels, int L,
                                                          int k, int* __restrict__ idx,
                                                          float* __restrict__ rows) {
   extern __shared__ float sm[];
   __shared__ int sel[16];
-  __shared__ float rv[4];
-  __shared__ int ri[4];
+  __shared__ float rv[PB / 64];
+  __shared__ int ri[PB / 64];
   const int b = blockIdx.x;
   label_select(emb, D, labels, L, k, sm, sm + D, sel, rv, ri);
   if (idx && threadIdx.x < k) idx[(long)b * k + threadIdx.x] = sel[threadIdx.x];
   for (int q = 0; q < k; ++q)
-    for (int d = threadIdx.x; d < D; d += 256)
+    for (int d = threadIdx.x; d < D; d += PB)
       rows[((long)b * k + q) * D + d] = labels[(long)sel[q] * D + d];
 }
 
@@ -479,7 +481,7 @@ extern "C" int zs_prompt_assemble(const float* emb, int B, int D, const float* l
   ZS_REQUIRE(B > 0 && D > 0 && L > 0 && k >= 0 && k <= 16 && k <= L, "zs_prompt_assemble: bad shape");
   const size_t smem = (size_t)(D + L) * sizeof(float);
   ZS_REQUIRE(smem <= 64 * 1024, "zs_prompt_assemble: D+L too large");
-  hipLaunchKernelGGL(prompt_kernel, dim3(B), dim3(256), smem, S(stream), emb, D, labels, L, k,
+  hipLaunchKernelGGL(prompt_kernel, dim3(B), dim3(PB), smem, S(stream), emb, D, labels, L, k,
                      label_tok, label_len, max_tok, hard_ids, h_cap, hard_len, chosen);
   ZS_LAUNCH_CHECK();
   return 0;
@@ -491,7 +493,7 @@ extern "C" int zs_label_topk(const float* emb, int B, int D, const float* labels
   ZS_REQUIRE(emb && labels && rows, "zs_label_topk: null pointer");
   const size_t smem = (size_t)(D + L) * sizeof(float);
   ZS_REQUIRE(smem <= 64 * 1024, "zs_label_topk: D+L too large");
-  hipLaunchKernelGGL(label_topk_kernel, dim3(B), dim3(256), smem, S(stream), emb, D, labels, L, k,
+  hipLaunchKernelGGL(label_topk_kernel, dim3(B), dim3(PB), smem, S(stream), emb, D, labels, L, k,
                      idx, rows);
   ZS_LAUNCH_CHECK();
   return 0;
