@@ -74,6 +74,11 @@ def main():
     summ["G"] = round(float(np.median(g_phase)), 2)
     summ["step_us"] = round(float(np.median(end - start)), 1)
     print(json.dumps({"per_phase_kind_mean_us": summ}))
+    # phase F per workgroup, and by blockIdx % 8 (the XCD under round-robin dispatch)
+    fc = comp[-1]
+    print(json.dumps({"F_compute_by_wg": [round(float(x), 1) for x in fc],
+                      "F_compute_by_wg_mod8": [round(float(np.mean(fc[k::8])), 1) for k in range(8)],
+                      "F_slowest_wg": [int(i) for i in np.argsort(-fc)[:6]]}))
 
 
 if __name__ == "__main__":
