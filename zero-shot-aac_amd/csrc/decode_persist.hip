@@ -34,6 +34,7 @@
 
 namespace zs {
 int g_dp_xb = 1;   // zs_tune_set("dp_xb", 0): LayerNorm inputs from the f32 x (A/B)
+int g_dp_lmil = 1;   // zs_tune_set("dp_lmil", 0): LM-head vocab as one contiguous range per workgroup (A/B)
 int g_dp_nt = 2;   // zs_tune_set("dp_nt", m): non-temporal loads, bit 0 weights + LM head (slower:
                    // the concurrent grids share them through L2 / MALL), bit 1 cached K/V (default)
 namespace dpk {
@@ -66,7 +67,7 @@ constexpr int WS_XB = WS_HID + RM * DFF * 2;       // bf16 [64][768]: x for the 
 constexpr int WS_BYTES = WS_XB + RM * D * 2;
 
 struct Args {
-  int R, Lmax, max_steps, stop0, stop1, V;
+  int R, Lmax, max_steps, stop0, stop1, V, lm_il;
   const bf16_t* wte; const bf16_t* wpe;
   const bf16_t* wqkv[NLY]; const float* bqkv[NLY];
   const bf16_t* wproj[NLY]; const float* bproj[NLY];
@@ -758,14 +759,21 @@ __device__ __forceinline__ void phase_lm(const Args& a, const Rs& rs, char* smem
   const int nvb = (a.V + 15) / 16;
   const int b_lo = (int)((long)wg * nvb / gg), b_hi = (int)((long)(wg + 1) * nvb / gg);
   const int npair = (b_hi - b_lo + 1) / 2;              // the last pair may hold one block
-  const int npw = (npair - v + NW - 1) / NW;            // pairs of this wave (>= 1)
+  // lm_il (A/B): pairs interleaved over the grid (pair (m NW + v) gg + wg for wave v of workgroup
+  // wg), so every CU streams pieces of the whole table instead of one contiguous 1.6 MB range
+  const int P = (nvb + 1) / 2, x0 = v * gg + wg;
+  const int npw = a.lm_il ? (P - x0 + NW * gg - 1) / (NW * gg)
+                          : (npair - v + NW - 1) / NW;  // pairs of this wave (>= 1)
   float bv[16];
   int bi[16];
 #pragma unroll
   for (int e = 0; e < 16; ++e) { bv[e] = -INFINITY; bi[e] = 0x7fffffff; }
   // blocks of pair m of this wave (clamped into the WG's range: loads past it re-read its last
   // block; their columns are masked below)
-  auto blk = [&](int m, int h) { return min(b_lo + 2 * (v + NW * min(m, npw - 1)) + h, b_hi - 1); };
+  auto blk = [&](int m, int h) {
+    if (a.lm_il) return min(2 * ((min(m, npw - 1) * NW) * gg + x0) + h, nvb - 1);
+    return min(b_lo + 2 * (v + NW * min(m, npw - 1)) + h, b_hi - 1);
+  };
   const bool tmp = a.temp != 1.0f;
   bf16x8_t P0[8], P1[8], P2[8];
   lm_piece<NTL>(a.wtep, blk(0, 0), blk(0, 1), 0, P0);
@@ -790,11 +798,12 @@ __device__ __forceinline__ void phase_lm(const Args& a, const Rs& rs, char* smem
     lm_piece<NTL>(a.wtep, n0, n1, 1, P1);
     lm_consume(hs, 5, P2, acc);
     // blocks in increasing id order within the lane: strict > keeps the lower id on ties
-    const int p0 = b_lo + 2 * (v + NW * m);
+    const int p0 = a.lm_il ? 2 * (m * NW * gg + x0) : b_lo + 2 * (v + NW * m);
+    const int p_hi = a.lm_il ? nvb : b_hi;
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       const int col = 16 * (p0 + h) + fr;
-      if (p0 + h < b_hi && col < a.V) {
+      if (p0 + h < p_hi && col < a.V) {
 #pragma unroll
         for (int rb = 0; rb < 4; ++rb)
 #pragma unroll
@@ -1027,6 +1036,7 @@ extern "C" int zs_gpt2_decode_persist(int R, int Lmax, int max_steps, int stop0,
              out_len && step_ctr && all_done, "zs_gpt2_decode_persist: null pointer");
   Args a{};
   a.R = R; a.Lmax = Lmax; a.max_steps = max_steps; a.stop0 = stop0; a.stop1 = stop1; a.V = V;
+  a.lm_il = g_dp_lmil;
   a.wte = (const bf16_t*)wte; a.wpe = (const bf16_t*)wpe;
   for (int l = 0; l < NLY; ++l) {
     const void* const* p = layer_w + 8 * l;

@@ -264,6 +264,7 @@ extern int g_gemm_big;      // gemm.hip
 extern int g_big_min;       // gemm.hip
 extern int g_dp_xb;         // decode_persist.hip
 extern int g_dp_nt;         // decode_persist.hip
+extern int g_dp_lmil;       // decode_persist.hip
 extern int g_beam_xcd;      // attn.hip
 
 // choose K per workgroup: a multiple of 64 dividing K, each wave <= 128 deep, ~256-320 WGs
@@ -317,6 +318,7 @@ extern "C" int zs_tune_set(const char* key, int value) {
   if (!strcmp(key, "big_min")) { g_big_min = value; return 0; }
   if (!strcmp(key, "dp_xb")) { g_dp_xb = value; return 0; }
   if (!strcmp(key, "dp_nt")) { g_dp_nt = value; return 0; }
+  if (!strcmp(key, "dp_lmil")) { g_dp_lmil = value; return 0; }
   if (!strcmp(key, "beam_xcd")) { g_beam_xcd = value; return 0; }
   return fail(ZS_ERR_ARG, "zs_tune_set: unknown key %s", key);
 }
