@@ -466,10 +466,12 @@ int zs_greedy_step_map(const float* part_val, const int* part_idx, int R, const 
  * the logits before the argmax (gpt2_prefix_eval.py:196); kv: 24 pointers
  * {kc[0..11], vc[0..11]}, each [R][12][Lmax][64] bf16 (zs_kv_write layout).  ws: scratch of
  * zs_decode_persist_workspace_bytes() bytes, 256-byte aligned, private to one launch in flight.
- * row_split 1: zs_decode_persist_grid() workgroups each own a column slice of every GEMM for all
- * rows; 2: twice as many, each the same slice for half of the rows (half the per-workgroup
- * activation reads, a shorter step; for few batches in flight).
- * A grid that cannot become co-resident gives up after a bounded wait: then
+ * The grid is zs_decode_persist_grid() / col_split x row_split workgroups.  col_split 1: each
+ * workgroup owns one column slice of every GEMM; 2: two (half the workgroups per batch: the same
+ * activation reads per workgroup for twice the weights, less CU time per step, a longer step).
+ * row_split 1: every workgroup covers all rows; 2: twice as many, each its slice for half of the
+ * rows (half the per-workgroup activation reads, a shorter step; for few batches in flight).
+ * A grid that cannot become co-resident gives up after a bounded wait: then all_done[1] = -1,
  * zs_decode_persist_status reports timed_out != 0 and the outputs are invalid. */
 int zs_decode_persist_workspace_bytes(void);
 int zs_decode_persist_grid(void);
@@ -478,7 +480,8 @@ int zs_gpt2_decode_persist(int R, int Lmax, int max_steps, int stop0, int stop1,
                            float temperature, const void* const* layer_w,
                            const float* lnf_w, const float* lnf_b, void* const* kv, int* pos,
                            int* next_tok, int* done, int* out_ids, int* out_len, int* step_ctr,
-                           int* all_done, void* ws, long ws_bytes, int row_split, void* stream);
+                           int* all_done, void* ws, long ws_bytes, int row_split, int col_split,
+                           void* stream);
 int zs_decode_persist_status(const void* ws, int* timed_out);
 /* zs_decode_persist_set_stamps: diagnostic phase timing (tools/persist_stamps.py): with buf !=
  * NULL ([grid][128] u64), thread 0 of every workgroup of later launches writes s_memrealtime

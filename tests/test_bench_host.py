@@ -24,25 +24,38 @@ def test_persist_launch_bytes():
     assert bench.persist_launch_bytes(1000, [10], 1) == 0
 
 
-def test_choose_row_split_keeps_grids_coresident():
-    """ConcurrentRunner's row_split choice (zsaac.pipeline.choose_row_split): simulated begins and
-    finishes in random order, 5 pipelines, G = 48 on 256 CUs -- the workgroups in flight never
-    exceed the CUs, and a shard of two or three batches runs its first ones at row_split 2."""
+def test_choose_persist_shape_keeps_grids_coresident():
+    """ConcurrentRunner's persistent grid shape choice (zsaac.pipeline.choose_persist_shape):
+    simulated begins and finishes in random order, shapes (col_split, row_split) of 96 / 48 / 24
+    workgroups on 256 CUs with CUs // 24 pipelines -- the workgroups in flight never exceed the
+    CUs, a shard of two or three batches runs its first ones on the largest grid, and a long run
+    of batches takes the smallest."""
     import random
-    from zsaac.pipeline import choose_row_split
-    G, CUS, P = 48, 256, 5
-    rng = random.Random(0)
-    for n in list(range(1, 24)) * 20:
-        active, nxt, chosen = {}, 0, []
-        while nxt < n or active:
-            free = [i for i in range(P) if i not in active]
-            if nxt < n and free and rng.random() < 0.7:
-                rs = choose_row_split(sum(active.values()), n - nxt, G, CUS)
-                active[free[0]] = rs * G
-                chosen.append(rs)
-                nxt += 1
-                assert sum(active.values()) <= CUS, (n, chosen)
-            elif active:
-                del active[rng.choice(list(active))]
-    assert choose_row_split(0, 2, G, CUS) == 2 and choose_row_split(0, 3, G, CUS) == 2
-    assert choose_row_split(96, 2, G, CUS) == 2 and choose_row_split(0, 5, G, CUS) == 1
+    from zsaac import ops
+    from zsaac.pipeline import choose_persist_shape, persist_shapes
+    CUS = 256
+    for spec in ("12,11,21", "12,11", "21", "11,21"):
+        shapes = persist_shapes(spec)
+        grids = [ops.decode_persist_grid(rs, cs) for cs, rs in shapes]
+        assert grids == sorted(grids, reverse=True)
+        P = CUS // grids[-1]
+        rng = random.Random(0)
+        for n in list(range(1, 24)) * 10:
+            active, nxt, chosen = {}, 0, []
+            while nxt < n or active:
+                free = [i for i in range(P) if i not in active]
+                if nxt < n and free and rng.random() < 0.7:
+                    cs, rs = choose_persist_shape(sum(active.values()), n - nxt, shapes, CUS)
+                    active[free[0]] = ops.decode_persist_grid(rs, cs)
+                    chosen.append((cs, rs))
+                    nxt += 1
+                    assert sum(active.values()) <= CUS, (spec, n, chosen)
+                elif active:
+                    del active[rng.choice(list(active))]
+        assert choose_persist_shape(0, 2, shapes, CUS) == shapes[0]
+        assert choose_persist_shape(0, 17, shapes, CUS) == shapes[-1]
+    sh = persist_shapes("12,11,21")
+    assert sh == [(1, 2), (1, 1), (2, 1)]
+    assert choose_persist_shape(96, 2, sh, CUS) == (1, 2)
+    assert choose_persist_shape(0, 5, sh, CUS) == (1, 2)
+    assert choose_persist_shape(0, 8, sh, CUS) == (1, 1)

@@ -120,19 +120,52 @@ def test_persist_temperature(cuda, flat):
     assert res[0] == res[1]
 
 
-@pytest.mark.parametrize("B", [32, 7])
-def test_persist_row_split(cuda, flat, B):
-    """The row-split grid (row_split 2: twice the workgroups, each a column slice for half of the
-    rows) gives the ids and decode state of the default grid and the reference's ids."""
+@pytest.mark.parametrize("B", [64, 7])
+def test_persist_grid_shapes(cuda, flat, B):
+    """Every grid shape (col_split, row_split) -- row_split 2: twice the workgroups, each a column
+    slice for half of the rows; col_split 2: half the workgroups, each two column slices -- gives
+    the ids and decode state of the default grid, and the reference's ids."""
     from tools import idparity
-    emb = torch.from_numpy(flat["clap_emb"][:B]).to(cuda)
-    res = []
-    for rs in (1, 2):
+    emb = torch.from_numpy(flat["clap_emb"]).to(cuda)
+    emb = torch.cat([emb, emb])[:B]           # 64: the golden's 32 clips twice (a full batch)
+    res = {}
+    for cs, rs in ((1, 1), (1, 2), (2, 1), (2, 2)):
         p = _pipe(flat, cuda, True, batch=B)
-        p.decoder.persist_row_split = rs
+        p.decoder.persist_row_split, p.decoder.persist_col_split = rs, cs
         out = p.caption_emb(emb)
-        res.append((out.captions(), _state(p, B), p.decoder.step_ctr.item()))
-    assert res[0][0] == res[1][0]
-    for k in res[0][1]:
-        assert np.array_equal(res[0][1][k], res[1][1][k]), k
-    assert res[0][2] == res[1][2]
+        res[cs, rs] = (out.captions(), _state(p, B), p.decoder.step_ctr.item())
+    base = res[1, 1]
+    for shape, r in res.items():
+        assert r[0] == base[0], shape
+        for k in base[1]:
+            assert np.array_equal(r[1][k], base[1][k]), (shape, k)
+        assert r[2] == base[2], shape
+    if B == 64:
+        assert base[0][:32] == base[0][32:]
+        assert idparity.agreement(flat, base[0][:32])["exact_frac"] == 1.0
+
+
+def test_persist_give_up_resumes_stepwise(cuda, flat):
+    """A persistent launch whose grid barrier gives up (forced: zs_tune_set dp_spin < 0 gives up
+    at the first unmet poll) reports all_done[1] = -1 with its starting decode state intact; the
+    host resumes the batch on the per-step path and the ids equal a normal run's -- through
+    Gpt2Decoder.greedy (synchronous) and through ConcurrentRunner (two batches in flight)."""
+    from zsaac._lib import call
+    from zsaac.pipeline import ConcurrentRunner
+    emb = torch.from_numpy(flat["clap_emb"][:16]).to(cuda)
+    p = _pipe(flat, cuda, True, batch=16)
+    ref = p.caption_emb(emb).captions()
+    call("zs_tune_set", b"dp_spin", -1)
+    try:
+        g0 = p.decoder.gave_up
+        got = p.caption_emb(emb).captions()
+        assert p.decoder.gave_up == g0 + 1, "the forced give-up did not happen"
+        assert got == ref
+        runner = ConcurrentRunner(p, 2)
+        runner.warmup_emb(emb[:8])
+        outs = runner.run([emb[:8], emb[8:]], inputs="emb")
+        assert [c for o in outs for c in o.captions()] == ref
+        assert sum(q.decoder.gave_up for q in runner.pipes) >= 2
+    finally:
+        call("zs_tune_set", b"dp_spin", 0)
+    assert p.caption_emb(emb).captions() == ref

@@ -33,7 +33,8 @@ def main():
     wav = bench.synthetic_clips(64, 0, dev)
     pipe.caption_wav(wav)
     rs = int(os.environ.get("ZSAAC_PERSIST_RS", "1"))
-    G = ops.decode_persist_grid() * rs
+    cs = int(os.environ.get("ZSAAC_PERSIST_CS", "1"))
+    G = ops.decode_persist_grid(rs, cs)
     buf = torch.zeros(G, 128, dtype=torch.int64, device=dev)
     call("zs_decode_persist_set_stamps", buf.data_ptr(), step)
     dec = pipe.decoder

@@ -33,14 +33,32 @@
 #include "common.h"
 
 namespace zs {
-int g_dp_xb = 1;   // zs_tune_set("dp_xb", 0): LayerNorm inputs from the f32 x (A/B)
 int g_dp_lmil = 1;   // zs_tune_set("dp_lmil", 0): LM-head vocab as one contiguous range per workgroup (A/B)
-int g_dp_nt = 2;   // zs_tune_set("dp_nt", m): non-temporal loads, bit 0 weights + LM head (slower:
-                   // the concurrent grids share them through L2 / MALL), bit 1 cached K/V (default)
+int g_dp_nt = 2;   // zs_tune_set("dp_nt", 0): default-policy loads of the cached K/V (2: non-temporal).
+                   // nt weight / LM-head loads (round 3's bit 0) were slower: the concurrent grids
+                   // share the weights through L2 / MALL
+int g_dp_spin = 0; // zs_tune_set("dp_spin", n): give up a grid-barrier wait after n polls (0 = the
+                   // default 2^22, < 0: at the first unmet poll); tests/test_gpu_persist.py forces
+                   // the give-up path with it
 namespace dpk {
 
 constexpr int D = 768, NH = 12, HD = 64, DFF = 3072, NLY = 12, RM = 64, QKVN = 3 * D;
-constexpr int G = 48;                  // workgroups per batch, one per CU
+constexpr int G = 48;                  // workgroups per batch at CS = 1, one per CU
+// CS column slices per workgroup: the grid of one batch is GW = 48 / CS column-slice workgroups
+// (x RH row halves).  CS = 2 halves the CUs a batch holds: every workgroup still reads the whole
+// handed-off activation once per phase (the same bytes as at CS = 1) but streams twice the
+// weight columns, so the CU-time per step falls while the step grows by the weight share only.
+template <int CS>
+struct Geo {
+  static constexpr int GW = G / CS;      // column-slice workgroups
+  static constexpr int QN = 48 * CS;     // c_attn columns per workgroup
+  static constexpr int PN = 16 * CS;     // attn.c_proj / mlp.c_proj columns
+  static constexpr int FN = 64 * CS;     // c_fc columns
+  static constexpr int A_KP = 8 / CS;    // phase A waves: A_KP K parts x CS groups of 3 blocks
+  static constexpr int SA = 24 / A_KP;   // k-steps per wave in phase A
+  static constexpr int D_KP = 4 / CS;    // phase D waves: D_KP K parts x 2 CS groups of 2 blocks
+  static constexpr int SD = 24 / D_KP;   // k-steps per wave in phase D
+};
 constexpr int NW = 8, NT = 64 * NW;    // 8 waves
 constexpr int HLD = D + 8;             // bf16 row stride of the normalised rows in LDS
 constexpr unsigned SPIN_MAX = 1u << 22;
@@ -68,6 +86,7 @@ constexpr int WS_BYTES = WS_XB + RM * D * 2;
 
 struct Args {
   int R, Lmax, max_steps, stop0, stop1, V, lm_il;
+  unsigned spin_max;    // polls before a barrier wait gives up
   const bf16_t* wte; const bf16_t* wpe;
   const bf16_t* wqkv[NLY]; const float* bqkv[NLY];
   const bf16_t* wproj[NLY]; const float* bproj[NLY];
@@ -216,6 +235,7 @@ struct Bar {
   unsigned long long* sb;   // this workgroup's stamp row of the traced step (or NULL)
   unsigned n0;              // barrier count at the start of the traced step
   unsigned g;               // workgroups in the grid
+  unsigned spin_max;        // polls before giving up
 };
 __device__ __forceinline__ void bar_arrive(Bar& b) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -236,8 +256,8 @@ __device__ __forceinline__ bool bar_wait(Bar& b, volatile lds_int_t* s_ok) {
       ++spins;
       // bounded spin: give up (and tell every other workgroup) after ~2^22 polls, so a grid that
       // is not co-resident drains instead of hanging
-      if ((spins & 255) == 0 &&
-          (spins > SPIN_MAX || __hip_atomic_load(b.tmo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
+      if (spins > b.spin_max ||
+          ((spins & 255) == 0 && __hip_atomic_load(b.tmo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
         __hip_atomic_store(b.tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         ok = 0;
         break;
@@ -258,11 +278,12 @@ __device__ __forceinline__ bool bar_wait(Bar& b, volatile lds_int_t* s_ok) {
 // 1: the token embedding wte[tok] + wpe[pos] (layer 0; WG w also stores rows r % G == w of x);
 // 2: x with the ln_f affine.  The LN affine of ln_1 / ln_2 is folded into c_attn / c_fc.
 // NR rows (64, or 32 for a row-split grid) from row r0, TPR = 512 / NR threads per row, NQ column
-// quads per thread; rows land at LDS row r - r0.  MODE 1 stores x rows r % 48 == w of its range.
+// quads per thread; rows land at LDS row r - r0.  MODE 1 stores x rows r % gw == w of its range
+// (gw = the column-slice workgroups).
 template <int MODE, int NR = RM, bool XB = false>
 __device__ __forceinline__ void ln_rows(const Args& a, const Rs& rs, bf16_t* hs, const int* s_tok,
                                         const int* s_pos, int w, const float* s_lnf = nullptr,
-                                        int r0 = 0) {
+                                        int r0 = 0, int gw = G) {
   constexpr int TPR = NT / NR, NQ = D / 4 / TPR;
   const int tid = otid(), rl = tid / TPR, q = tid % TPR, r = r0 + rl;
   const int rr = min(r, a.R - 1);
@@ -335,7 +356,7 @@ __device__ __forceinline__ void ln_rows(const Args& a, const Rs& rs, bf16_t* hs,
             __uint_as_float(tu[i].y & 0xffff0000u) + __uint_as_float(pu[i].y & 0xffff0000u));
       __builtin_amdgcn_sched_barrier(0);
     }
-    if (r < a.R && r % 48 == w) {
+    if (r < a.R && r % gw == w) {
 #pragma unroll
       for (int i = 0; i < NQ; ++i)
         st16(rs.x, (r * D + 4 * (q + TPR * i)) * 4, f42u(xv[i].x, xv[i].y, xv[i].z, xv[i].w));
@@ -406,43 +427,47 @@ __device__ __forceinline__ void put_partial(float* red, int slab, int col0, cons
 }
 
 // ------------------------------------------------------------------ phase A: ln_1 + c_attn
-// RH = 1: all 64 rows; RH = 2: the 32 rows of half h (row-split grid)
-template <int RH, bool XB>
+// RH = 1: all 64 rows; RH = 2: the 32 rows of half h (row-split grid).  Wave v = (column group
+// v / A_KP of 3 blocks, K part v % A_KP); the A_KP partial slabs alias the LN rows (98,304 B at
+// every CS).
+template <int CS, int RH, bool XB>
 __device__ __forceinline__ void phase_qkv(const Args& a, const Rs& rs, int l, char* smem,
                                           const int* s_tok, const int* s_pos, int w, int h,
-                                          const bf16x8_t (&wq)[9]) {
-  constexpr int NR = RM / RH, NRB = NR / 16;
+                                          const bf16x8_t (&wq)[3 * Geo<CS>::SA]) {
+  using Gm = Geo<CS>;
+  constexpr int NR = RM / RH, NRB = NR / 16, QN = Gm::QN, KP = Gm::A_KP, QQ = QN / 4;
+  constexpr int NQD = (NR * QQ + NT - 1) / NT;      // epilogue quads per thread
   bf16_t* hs = reinterpret_cast<bf16_t*>(smem);
   float* red = reinterpret_cast<float*>(smem);
-  const int tid = otid(), v = tid >> 6, r0 = h * NR;
-  // epilogue quads: NR rows x 12 column quads, quads tid and tid + 512.  The bias quads are
-  // issued after the MFMAs (issued before the LayerNorm they were spilled, and the spill store
-  // waited for the load at the top of the phase)
-  const int c0 = 4 * (tid % 12), c1 = 4 * ((tid + 512) % 12);
-  if (l == 0) ln_rows<1, NR>(a, rs, hs, s_tok, s_pos, w, nullptr, r0);
-  else ln_rows<0, NR, XB>(a, rs, hs, s_tok, s_pos, w, nullptr, r0);
+  const int tid = otid(), v = tid >> 6, r0 = h * NR, ng = v / KP, kp = v % KP;
+  if (l == 0) ln_rows<1, NR>(a, rs, hs, s_tok, s_pos, w, nullptr, r0, Gm::GW);
+  else ln_rows<0, NR, XB>(a, rs, hs, s_tok, s_pos, w, nullptr, r0, Gm::GW);
   lds_sync();
   f32x4_t acc[NRB][3];
-  mma_lds<3, 3, NRB>(hs, 96 * v, wq, acc);
-  const float4 b0 = *reinterpret_cast<const float4*>(a.bqkv[l] + 48 * w + c0);
-  const float4 b1 = *reinterpret_cast<const float4*>(a.bqkv[l] + 48 * w + c1);
+  mma_lds<3, Gm::SA, NRB>(hs, 32 * Gm::SA * kp, wq, acc);
+  // the bias quads are issued after the MFMAs (issued before the LayerNorm they were spilled,
+  // and the spill store waited for the load at the top of the phase)
+  float4 bq[NQD];
+#pragma unroll
+  for (int i = 0; i < NQD; ++i)
+    bq[i] = *reinterpret_cast<const float4*>(a.bqkv[l] + QN * w + 4 * ((tid + NT * i) % QQ));
   lds_sync();
-  put_partial<3, 48, NRB>(red, v, 0, acc);
+  put_partial<3, QN, NRB>(red, kp, 48 * ng, acc);
   lds_sync();
 #pragma unroll
-  for (int hq = 0; hq < 2; ++hq) {
-    const int qd = tid + 512 * hq;
-    if (qd >= NR * 12) break;
-    const int rl = qd / 12, c = hq ? c1 : c0, row = r0 + rl;
-    const float4 bb = hq ? b1 : b0;
-    float4 sm = *reinterpret_cast<const float4*>(red + rl * 48 + c);
+  for (int i = 0; i < NQD; ++i) {
+    const int qd = tid + NT * i;
+    if (qd >= NR * QQ) break;
+    const int rl = qd / QQ, c = 4 * (qd % QQ), row = r0 + rl;
+    const float4 bb = bq[i];
+    float4 sm = *reinterpret_cast<const float4*>(red + rl * QN + c);
 #pragma unroll
-    for (int k = 1; k < NW; ++k) {
-      const float4 p = *reinterpret_cast<const float4*>(red + (k * NR + rl) * 48 + c);
+    for (int k = 1; k < KP; ++k) {
+      const float4 p = *reinterpret_cast<const float4*>(red + (k * NR + rl) * QN + c);
       sm.x += p.x; sm.y += p.y; sm.z += p.z; sm.w += p.w;
     }
     if (row < a.R)
-      st8(rs.qkv, (row * QKVN + 48 * w + c) * 2,
+      st8(rs.qkv, (row * QKVN + QN * w + c) * 2,
           u32x2_t{pk2bf(sm.x + bb.x, sm.y + bb.y), pk2bf(sm.z + bb.z, sm.w + bb.w)});
   }
 }
@@ -459,13 +484,14 @@ __device__ __forceinline__ uint4 sel4(bool c, const uint4& x, const uint4& y) {
 }
 __device__ __forceinline__ uint4 tou4(u32x4_t u) { return make_uint4(u.x, u.y, u.z, u.w); }
 
-// one wave per two (row, head) units (16 w + 2 v + k); keys in 64-key chunks, 8 lanes per key
-// (lane sub holds dims 8 sub .. 8 sub + 8), online softmax in f32 (decode_attn6 arithmetic).
-// The cached keys of the first chunk do not depend on this step's activations: attn_load issues
-// them BEFORE the workgroup waits on the c_attn barrier (kr / vr held across it).
+// one wave per KU (row, head) units; keys in chunks of 8 KC (KC keys per 8-lane group, 8 lanes
+// per key: lane sub holds dims 8 sub .. 8 sub + 8), online softmax in f32 (decode_attn6
+// arithmetic).  The cached keys of the first chunk do not depend on this step's activations:
+// attn_load issues them BEFORE the workgroup waits on the c_attn barrier (kr / vr held across it).
 // unit u = (row u / 12, head u % 12); wave v of a workgroup whose first unit is ub takes units
-// ub + KU v .. + KU (KU = 2: 16 units per workgroup of a 48-grid; 1: 8 per workgroup of a row
-// half, 96-grid)
+// ub + KU v .. + KU (KU = 2: 16 units per workgroup of a 48-grid; 4: 32 per workgroup of a
+// 24-grid, in 32-key chunks (KC 4) so the prefetched keys stay at 128 VGPRs; 1: 8 per workgroup
+// of a row half, 96-grid)
 __device__ __forceinline__ void attn_unit(const Args& a, const int* s_pos, int u,
                                           int& row, int& hh, int& p, long& base) {
   row = u / NH;
@@ -474,9 +500,9 @@ __device__ __forceinline__ void attn_unit(const Args& a, const int* s_pos, int u
   p = min(s_pos[rr], a.Lmax - 1);
   base = ((long)(rr * NH + hh) * a.Lmax) * HD + 8 * ((otid() & 63) & 7);
 }
-template <int KU, bool NTL = false>
+template <int KU, int KC, bool NTL = false>
 __device__ __forceinline__ void attn_load(const Args& a, int l, const int* s_pos, int ub, int cb,
-                                          uint4 (&kr)[KU][8], uint4 (&vr)[KU][8]) {
+                                          uint4 (&kr)[KU][KC], uint4 (&vr)[KU][KC]) {
   const int tid = otid(), v = tid >> 6, grp = (tid & 63) >> 3;
   const bf16_t* kc = a.kc[l];
   const bf16_t* vc = a.vc[l];
@@ -486,7 +512,7 @@ __device__ __forceinline__ void attn_load(const Args& a, int l, const int* s_pos
     long base;
     attn_unit(a, s_pos, ub + KU * v + k, row, hh, p, base);
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
+    for (int i = 0; i < KC; ++i) {
       const int jc = max(min(cb + 8 * i + grp, p - 1), 0);
       kr[k][i] = __builtin_bit_cast(uint4, ldg<NTL>(reinterpret_cast<const u32x4_t*>(kc + base + (long)jc * HD)));
       vr[k][i] = __builtin_bit_cast(uint4, ldg<NTL>(reinterpret_cast<const u32x4_t*>(vc + base + (long)jc * HD)));
@@ -495,21 +521,25 @@ __device__ __forceinline__ void attn_load(const Args& a, int l, const int* s_pos
 }
 // The new token (key pos, from qkv) is folded in after the cached keys 0..pos-1 (one more
 // online-softmax update with its score and v), so the cached chunks need no per-key selects.
-template <int KU, bool NTL = false>
+template <int KU, int KC, bool NTL = false>
 __device__ __forceinline__ void phase_attn(const Args& a, const Rs& rs, int l, const int* s_pos, int ub,
-                                           uint4 (&kr)[KU][8], uint4 (&vr)[KU][8]) {
+                                           uint4 (&kr)[KU][KC], uint4 (&vr)[KU][KC]) {
   const int tid = otid(), lane = tid & 63, v = tid >> 6, grp = lane >> 3, sub = lane & 7;
   float q[KU][8], o[KU][8], m[KU], sum[KU];
   uint4 knu[KU], vnu[KU];
   int p[KU], row[KU], hh[KU];
   long base[KU];
+  // KU = 4: the new token's k / v are loaded after the cached chunks (32 VGPRs less across them)
+  constexpr bool LATE_KV = KU > 2;
 #pragma unroll
   for (int k = 0; k < KU; ++k) {
     attn_unit(a, s_pos, ub + KU * v + k, row[k], hh[k], p[k], base[k]);
     const int off = (min(row[k], a.R - 1) * QKVN + hh[k] * HD + 8 * sub) * 2;
     const uint4 qu = tou4(ld16(rs.qkv, off));
-    knu[k] = tou4(ld16(rs.qkv, off + 2 * D));
-    vnu[k] = tou4(ld16(rs.qkv, off + 4 * D));
+    if constexpr (!LATE_KV) {
+      knu[k] = tou4(ld16(rs.qkv, off + 2 * D));
+      vnu[k] = tou4(ld16(rs.qkv, off + 4 * D));
+    }
     bf8_unpack(qu, q[k]);
 #pragma unroll
     for (int t = 0; t < 8; ++t) { q[k][t] *= 0.125f; o[k][t] = 0.f; }
@@ -519,15 +549,15 @@ __device__ __forceinline__ void phase_attn(const Args& a, const Rs& rs, int l, c
   int pmax = p[0];
 #pragma unroll
   for (int k = 1; k < KU; ++k) pmax = max(pmax, p[k]);
-  for (int cb = 0; cb < pmax; cb += 64) {       // cached keys 0 .. p - 1
-    if (cb > 0) attn_load<KU, NTL>(a, l, s_pos, ub, cb, kr, vr);
+  for (int cb = 0; cb < pmax; cb += 8 * KC) {   // cached keys 0 .. p - 1
+    if (cb > 0) attn_load<KU, KC, NTL>(a, l, s_pos, ub, cb, kr, vr);
 #pragma unroll
     for (int k = 0; k < KU; ++k) {
       if (cb >= p[k]) continue;                   // wave-uniform
-      float sc[8];
+      float sc[KC];
       float pm = -INFINITY;
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
+      for (int i = 0; i < KC; ++i) {
         float kf[8];
         bf8_unpack(kr[k][i], kf);
         float sv = 0.f;
@@ -547,7 +577,7 @@ __device__ __forceinline__ void phase_attn(const Args& a, const Rs& rs, int l, c
       for (int t = 0; t < 8; ++t) o[k][t] *= scale;
       m[k] = mn;
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
+      for (int i = 0; i < KC; ++i) {
         const float e = __expf(sc[i] - mn);     // masked keys: exp(-inf) = 0
         sum[k] += e;
         float vf[8];
@@ -555,6 +585,14 @@ __device__ __forceinline__ void phase_attn(const Args& a, const Rs& rs, int l, c
 #pragma unroll
         for (int t = 0; t < 8; ++t) o[k][t] += e * vf[t];
       }
+    }
+  }
+  if constexpr (LATE_KV) {
+#pragma unroll
+    for (int k = 0; k < KU; ++k) {
+      const int off = (min(row[k], a.R - 1) * QKVN + hh[k] * HD + 8 * sub) * 2;
+      knu[k] = tou4(ld16(rs.qkv, off + 2 * D));
+      vnu[k] = tou4(ld16(rs.qkv, off + 4 * D));
     }
   }
 #pragma unroll
@@ -592,21 +630,22 @@ __device__ __forceinline__ void phase_attn(const Args& a, const Rs& rs, int l, c
 }
 
 // ------------------------------------------------------------------ phases C / E: projections
-// x[:, 16w .. 16w + 16) += A W^T + b, A = att (K 768) or hid (K 3072) from the workspace in
-// A-fragment order; wave v takes k-steps [v S, (v+1) S), its A fragments in chunks of 4 k-steps
-// (two chunks in flight), each fragment load one contiguous KiB
-template <int S, int RH, bool XB>
+// x[:, PN w .. PN w + PN) += A W^T + b (PN = 16 CS columns, NB = CS blocks), A = att (K 768) or
+// hid (K 3072) from the workspace in A-fragment order; wave v takes k-steps [v S, (v+1) S), its A
+// fragments in chunks of CH k-steps (NIF chunks in flight), each fragment load one contiguous
+// KiB, every fragment read by exactly one wave and multiplied into all NB column blocks
+template <int S, int CS, int RH, bool XB, int CH = 4, int NIF = 2>
 __device__ __forceinline__ void phase_proj(const Args& a, const Rs& rs, __amdgpu_buffer_rsrc_t ra,
                                            int K, const float* bias, char* smem, int w, int h,
-                                           const bf16x8_t (&wb)[S]) {
-  constexpr int NR = RM / RH, NRB = NR / 16;
+                                           const bf16x8_t (&wb)[CS * S]) {
+  constexpr int NR = RM / RH, NRB = NR / 16, NB = CS, PN = 16 * CS, PQ = PN / 4;
   float* red = reinterpret_cast<float*>(smem);
   const int tid = otid(), lane = tid & 63, v = tid >> 6, r0 = h * NR;
-  // epilogue operands first: NR rows x 4 quads on threads 0 .. 4 NR - 1 (two threads per
+  // epilogue operands first: NR rows x PQ quads on threads 0 .. PQ NR - 1 (two threads per
   // 16-byte bf16 copy were tried: the longer per-thread epilogue cost more than the 8-byte stores)
-  const int erl = (tid >> 2) & (NR - 1), erow = r0 + erl, ec = 16 * w + 4 * (tid & 3);
+  const int erl = (tid / PQ) % NR, erow = r0 + erl, ec = PN * w + 4 * (tid % PQ);
   float4 eb = make_float4(0.f, 0.f, 0.f, 0.f), ex = eb;
-  if (tid < 4 * NR) {
+  if (tid < PQ * NR) {
     eb = *reinterpret_cast<const float4*>(bias + ec);
     ex = u2f4(ld16(rs.x, (min(erow, a.R - 1) * D + ec) * 4));
   }
@@ -615,14 +654,15 @@ __device__ __forceinline__ void phase_proj(const Args& a, const Rs& rs, __amdgpu
   int aoff[NRB];
 #pragma unroll
   for (int rb = 0; rb < NRB; ++rb) aoff[rb] = (((r0 / 16 + rb) * (K / 32) + v * S) * 64 + lane) * 16;
-  f32x4_t acc[NRB];
+  f32x4_t acc[NRB][NB];
 #pragma unroll
-  for (int rb = 0; rb < NRB; ++rb) acc[rb] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-  constexpr int CH = 4;                      // k-steps per chunk
+  for (int rb = 0; rb < NRB; ++rb)
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb) acc[rb][nb] = f32x4_t{0.f, 0.f, 0.f, 0.f};
   constexpr int NCH = (S + CH - 1) / CH;
   u32x4_t af[NCH][NRB * CH];
 #pragma unroll
-  for (int c = 0; c < NCH && c < 2; ++c)
+  for (int c = 0; c < NCH && c < NIF; ++c)
 #pragma unroll
     for (int s = 0; s < CH; ++s)
 #pragma unroll
@@ -634,22 +674,26 @@ __device__ __forceinline__ void phase_proj(const Args& a, const Rs& rs, __amdgpu
     for (int s = 0; s < CH; ++s)
 #pragma unroll
       for (int rb = 0; rb < NRB; ++rb)
-        if (c * CH + s < S) acc[rb] = mfma(bf8(af[c][s * NRB + rb]), wb[c * CH + s], acc[rb]);
-    if (c + 2 < NCH) {
+#pragma unroll
+        for (int nb = 0; nb < NB; ++nb)
+          if (c * CH + s < S)
+            acc[rb][nb] = mfma(bf8(af[c][s * NRB + rb]), wb[nb * S + c * CH + s], acc[rb][nb]);
+    if (c + NIF < NCH) {
 #pragma unroll
       for (int s = 0; s < CH; ++s)
 #pragma unroll
         for (int rb = 0; rb < NRB; ++rb)
-          if ((c + 2) * CH + s < S) af[c + 2][s * NRB + rb] = ld16(ra, aoff[rb] + 1024 * ((c + 2) * CH + s));
+          if ((c + NIF) * CH + s < S)
+            af[c + NIF][s * NRB + rb] = ld16(ra, aoff[rb] + 1024 * ((c + NIF) * CH + s));
     }
   }
-  put_partial<1, 16, NRB>(red, v, 0, reinterpret_cast<const f32x4_t(&)[NRB][1]>(acc));
+  put_partial<NB, PN, NRB>(red, v, 0, acc);
   lds_sync();
-  if (tid < 4 * NR) {
-    float4 sm = *reinterpret_cast<const float4*>(red + erl * 16 + 4 * (tid & 3));
+  if (tid < PQ * NR) {
+    float4 sm = *reinterpret_cast<const float4*>(red + erl * PN + 4 * (tid % PQ));
 #pragma unroll
     for (int k = 1; k < NW; ++k) {
-      const float4 p = *reinterpret_cast<const float4*>(red + (k * NR + erl) * 16 + 4 * (tid & 3));
+      const float4 p = *reinterpret_cast<const float4*>(red + (k * NR + erl) * PN + 4 * (tid % PQ));
       sm.x += p.x; sm.y += p.y; sm.z += p.z; sm.w += p.w;
     }
     if (erow < a.R) {
@@ -666,35 +710,39 @@ __device__ __forceinline__ float gelu_new_fast(float x) {
   const float u2 = -1.5957691216057308f * (x + 0.044715f * x * x * x);
   return x * __builtin_amdgcn_rcpf(1.0f + __expf(u2));
 }
-template <int RH, bool XB>
+// wave v = (column group v / D_KP of 2 blocks, K part v % D_KP); FN = 64 CS columns per workgroup;
+// the D_KP partial slabs (65,536 B at every CS) alias the LN rows
+template <int CS, int RH, bool XB>
 __device__ __forceinline__ void phase_fc(const Args& a, const Rs& rs, int l, char* smem,
                                          const int* s_tok, const int* s_pos, int w, int h,
-                                         const bf16x8_t (&wf)[12]) {
-  constexpr int NR = RM / RH, NRB = NR / 16;
+                                         const bf16x8_t (&wf)[2 * Geo<CS>::SD]) {
+  using Gm = Geo<CS>;
+  constexpr int NR = RM / RH, NRB = NR / 16, FN = Gm::FN, KP = Gm::D_KP, FQ = FN / 4;
+  constexpr int NQD = NR * FQ / NT;                 // epilogue quads per thread (same column quad)
+  static_assert(NT % FQ == 0 && (NR * FQ) % NT == 0, "phase D epilogue mapping");
   bf16_t* hs = reinterpret_cast<bf16_t*>(smem);
   float* red = reinterpret_cast<float*>(smem);
-  const int tid = otid(), v = tid >> 6, cg = v >> 2, kq = v & 3, r0 = h * NR;
-  // epilogue: NR rows x 16 quads, quads tid and tid + 512 (same column quad)
-  const int c = 4 * (tid & 15);
-  const float4 bb = *reinterpret_cast<const float4*>(a.bfc[l] + 64 * w + c);
-  ln_rows<0, NR, XB>(a, rs, hs, s_tok, s_pos, w, nullptr, r0);
+  const int tid = otid(), v = tid >> 6, cg = v / KP, kq = v % KP, r0 = h * NR;
+  const int c = 4 * (tid % FQ);
+  const float4 bb = *reinterpret_cast<const float4*>(a.bfc[l] + FN * w + c);
+  ln_rows<0, NR, XB>(a, rs, hs, s_tok, s_pos, w, nullptr, r0, Gm::GW);
   lds_sync();
   f32x4_t acc[NRB][2];
-  mma_lds<2, 6, NRB>(hs, 192 * kq, wf, acc);
+  mma_lds<2, Gm::SD, NRB>(hs, 32 * Gm::SD * kq, wf, acc);
   lds_sync();
-  put_partial<2, 64, NRB>(red, kq, 32 * cg, acc);
+  put_partial<2, FN, NRB>(red, kq, 32 * cg, acc);
   lds_sync();
 #pragma unroll
-  for (int hq = 0; hq < NR / 32; ++hq) {
-    const int rl = (tid >> 4) + 32 * hq, row = r0 + rl;
-    float4 sm = *reinterpret_cast<const float4*>(red + rl * 64 + c);
+  for (int hq = 0; hq < NQD; ++hq) {
+    const int rl = tid / FQ + (NT / FQ) * hq, row = r0 + rl;
+    float4 sm = *reinterpret_cast<const float4*>(red + rl * FN + c);
 #pragma unroll
-    for (int k = 1; k < 4; ++k) {
-      const float4 p = *reinterpret_cast<const float4*>(red + (k * NR + rl) * 64 + c);
+    for (int k = 1; k < KP; ++k) {
+      const float4 p = *reinterpret_cast<const float4*>(red + (k * NR + rl) * FN + c);
       sm.x += p.x; sm.y += p.y; sm.z += p.z; sm.w += p.w;
     }
-    // hid in A-fragment order: column k = 64 w + c -> k-step k / 32, lane (row & 15) + 16 ((k / 8) & 3)
-    const int k = 64 * w + c;
+    // hid in A-fragment order: column k = FN w + c -> k-step k / 32, lane (row & 15) + 16 ((k / 8) & 3)
+    const int k = FN * w + c;
     if (row < a.R)
       st8(rs.hid, ((((row >> 4) * (DFF / 32) + (k >> 5)) * 64 + (row & 15) + 16 * ((k >> 3) & 3)) * 8 + (k & 7)) * 2,
           u32x2_t{pk2bf(gelu_new_fast(sm.x + bb.x), gelu_new_fast(sm.y + bb.y)),
@@ -706,8 +754,8 @@ __device__ __forceinline__ void phase_fc(const Args& a, const Rs& rs, int l, cha
 // vocab blocks of 16 rows [wg nvb / gg, (wg+1) nvb / gg) of this WG (gg = the grid), taken in PAIRS (one A fragment
 // read from LDS feeds the MFMAs of both blocks: half the LDS traffic per MFMA); wave v takes
 // pairs v, v + 8, ..  A pair's weights (wtep: 24 KiB contiguous per block, one KiB per k-step in
-// B-fragment order) arrive as six 4-k-step pieces (both blocks) through a 3-slot register ring:
-// two pieces in flight while one is consumed.  Per lane a running (logit, id) best for each of
+// B-fragment order) arrive as six 4-k-step pieces (both blocks) through a 4-slot register ring:
+// three pieces in flight while one is consumed.  Per lane a running (logit, id) best for each of
 // its 16 rows.  The WG's best per row goes to a 64-bit agent-scope atomic max of
 // key = (order-preserving logit bits, ~id): larger logit wins, then the lower id (torch.argmax),
 // whatever order the workgroups arrive in.
@@ -775,29 +823,9 @@ __device__ __forceinline__ void phase_lm(const Args& a, const Rs& rs, char* smem
     return min(b_lo + 2 * (v + NW * min(m, npw - 1)) + h, b_hi - 1);
   };
   const bool tmp = a.temp != 1.0f;
-  bf16x8_t P0[8], P1[8], P2[8];
-  lm_piece<NTL>(a.wtep, blk(0, 0), blk(0, 1), 0, P0);
-  lm_piece<NTL>(a.wtep, blk(0, 0), blk(0, 1), 1, P1);
-  for (int m = 0; m < npw; ++m) {
-    const int b0 = blk(m, 0), b1 = blk(m, 1), n0 = blk(m + 1, 0), n1 = blk(m + 1, 1);
-    f32x4_t acc[2][4];
-#pragma unroll
-    for (int h = 0; h < 2; ++h)
-#pragma unroll
-      for (int rb = 0; rb < 4; ++rb) acc[h][rb] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-    lm_piece<NTL>(a.wtep, b0, b1, 2, P2);
-    lm_consume(hs, 0, P0, acc);
-    lm_piece<NTL>(a.wtep, b0, b1, 3, P0);
-    lm_consume(hs, 1, P1, acc);
-    lm_piece<NTL>(a.wtep, b0, b1, 4, P1);
-    lm_consume(hs, 2, P2, acc);
-    lm_piece<NTL>(a.wtep, b0, b1, 5, P2);
-    lm_consume(hs, 3, P0, acc);
-    lm_piece<NTL>(a.wtep, n0, n1, 0, P0);
-    lm_consume(hs, 4, P1, acc);
-    lm_piece<NTL>(a.wtep, n0, n1, 1, P1);
-    lm_consume(hs, 5, P2, acc);
-    // blocks in increasing id order within the lane: strict > keeps the lower id on ties
+  // the running (logit, id) best of pair m's two blocks (blocks in increasing id order within
+  // the lane: strict > keeps the lower id on ties)
+  auto best = [&](int m, const f32x4_t (&acc)[2][4]) {
     const int p0 = a.lm_il ? 2 * (m * NW * gg + x0) : b_lo + 2 * (v + NW * m);
     const int p_hi = a.lm_il ? nvb : b_hi;
 #pragma unroll
@@ -813,7 +841,43 @@ __device__ __forceinline__ void phase_lm(const Args& a, const Rs& rs, char* smem
           }
       }
     }
+  };
+  // the wave's piece stream j = 6 m + c (pair m, piece c) through a 4-slot register ring, slot
+  // j % 4: piece j + 3 is issued before piece j is consumed (three pieces, 24 KiB per wave, in
+  // flight); two pairs per iteration make every slot index a constant
+  bf16x8_t R0[8], R1[8], R2[8], R3[8];
+#define LMP(M_, C_, R_) lm_piece<NTL>(a.wtep, blk(M_, 0), blk(M_, 1), C_, R_)
+  LMP(0, 0, R0);
+  LMP(0, 1, R1);
+  LMP(0, 2, R2);
+  for (int m = 0; m < npw; m += 2) {
+    f32x4_t acc[2][4];
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int rb = 0; rb < 4; ++rb) acc[h][rb] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    LMP(m, 3, R3);     lm_consume(hs, 0, R0, acc);
+    LMP(m, 4, R0);     lm_consume(hs, 1, R1, acc);
+    LMP(m, 5, R1);     lm_consume(hs, 2, R2, acc);
+    LMP(m + 1, 0, R2); lm_consume(hs, 3, R3, acc);
+    LMP(m + 1, 1, R3); lm_consume(hs, 4, R0, acc);
+    LMP(m + 1, 2, R0); lm_consume(hs, 5, R1, acc);
+    best(m, acc);
+    if (m + 1 < npw) {         // wave-uniform
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int rb = 0; rb < 4; ++rb) acc[h][rb] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+      LMP(m + 1, 3, R1); lm_consume(hs, 0, R2, acc);
+      LMP(m + 1, 4, R2); lm_consume(hs, 1, R3, acc);
+      LMP(m + 1, 5, R3); lm_consume(hs, 2, R0, acc);
+      LMP(m + 2, 0, R0); lm_consume(hs, 3, R1, acc);
+      LMP(m + 2, 1, R1); lm_consume(hs, 4, R2, acc);
+      LMP(m + 2, 2, R2); lm_consume(hs, 5, R3, acc);
+      best(m + 1, acc);
+    }
   }
+#undef LMP
   // over the 16 lanes of each row group (columns), ties -> lower id
 #pragma unroll
   for (int o = 1; o < 16; o <<= 1)
@@ -865,8 +929,10 @@ __device__ __forceinline__ void gave_up(const Args& a) {
 // XB: the LayerNorm inputs are handed off as a bf16 copy of x (written by phases C / E beside
 // the f32 residual stream), halving the bytes every workgroup reads in phases A, D and F.
 // NTM: non-temporal loads, bit 0 the weight / LM-head streams, bit 1 the cached K/V
-template <int RH, bool XB, int NTM = 0>
+// CS: column slices per workgroup (Geo; grid = 48 / CS x RH workgroups)
+template <int CS, int RH, bool XB, int NTM = 0>
 __global__ __launch_bounds__(NT) void decode_persist_kernel(Args a) {
+  using Gm = Geo<CS>;
   constexpr bool NTW = NTM & 1, NTK = (NTM >> 1) & 1;
   __shared__ __attribute__((aligned(16))) char smem[SM_TOTAL];
   float* am_v = reinterpret_cast<float*>(smem + SM_HS);
@@ -875,17 +941,18 @@ __global__ __launch_bounds__(NT) void decode_persist_kernel(Args a) {
   int* s_pos = s_tok + RM;
   int* s_done = s_pos + RM;
   int* s_misc = s_done + RM;     // [0] rows still decoding, [8] barrier ok flag
-  constexpr int GG = G * RH;
+  constexpr int GW = Gm::GW, GG = GW * RH;
+  constexpr int KU = 2 * CS / RH, KC = KU > 2 ? 4 : 8;   // attention units per wave, keys per group
   const int wg = blockIdx.x;
   const int w = RH == 1 ? wg : (wg & 7) + 8 * (wg >> 4), h = RH == 1 ? 0 : (wg >> 3) & 1;
-  const int ub = RH == 1 ? 16 * w : 384 * h + 8 * w;    // first attention unit of this workgroup
+  const int ub = (RM * NH / RH) * h + 8 * KU * w;        // first attention unit of this workgroup
   Rs rs;
   rs.x = mk(a.ws + WS_X, RM * D * 4);
   rs.qkv = mk(a.ws + WS_QKV, RM * QKVN * 2);
   rs.att = mk(a.ws + WS_ATT, RM * D * 2);
   rs.hid = mk(a.ws + WS_HID, RM * DFF * 2);
   rs.xb = mk(a.ws + WS_XB, RM * D * 2);
-  Bar bar{(gu32*)(a.ws + WS_SYNC), (gu32*)(a.ws + WS_SYNC + 4), 0, nullptr, 0, GG};
+  Bar bar{(gu32*)(a.ws + WS_SYNC), (gu32*)(a.ws + WS_SYNC + 4), 0, nullptr, 0, GG, a.spin_max};
   gu64* const lmkey = (gu64*)(a.ws + WS_LMKEY);
   unsigned long long* const stamps = dp_stamp_buf;
   const int stamp_step = dp_stamp_step;
@@ -908,49 +975,62 @@ __global__ __launch_bounds__(NT) void decode_persist_kernel(Args a) {
   }
   __syncthreads();
 
-  bf16x8_t wq[9], wp[3], wf[12], wm[12];
+  // weight fragments of this workgroup's column slices (each prefetched across the barrier
+  // before its phase): c_attn (3 blocks x SA k-steps), attn.c_proj (CS blocks x 3), c_fc (2 blocks
+  // x SD), mlp.c_proj (CS blocks x 12)
+  bf16x8_t wq[3 * Gm::SA], wp[CS * 3], wf[2 * Gm::SD], wm[CS * 12];
 #define V_ (otid() >> 6)
-  load_w<3, 3, NTW>(a.wqkv[0], D, 48 * w, QKVN, 96 * V_, wq);
+#define LOAD_WQ(L_) load_w<3, Gm::SA, NTW>(a.wqkv[L_], D, Gm::QN * w + 48 * (V_ / Gm::A_KP), QKVN, \
+                                         32 * Gm::SA * (V_ % Gm::A_KP), wq)
+  LOAD_WQ(0);
   for (;;) {
     bar.sb = (stamps != nullptr && step == stamp_step) ? stamps + (long)wg * 2 * DP_NB : nullptr;
     bar.n0 = bar.n;
     stamp(bar.sb, 2 * DP_NB - 1);   // step start
     for (int l = 0; l < NLY; ++l) {
-      phase_qkv<RH, XB>(a, rs, l, smem, s_tok, s_pos, w, h, wq);
+      phase_qkv<CS, RH, XB>(a, rs, l, smem, s_tok, s_pos, w, h, wq);
       bar_arrive(bar);
-      uint4 kr[2 / RH][8], vr[2 / RH][8];
-      attn_load<2 / RH, NTK>(a, l, s_pos, ub, 0, kr, vr);
+      uint4 kr[KU][KC], vr[KU][KC];
+      attn_load<KU, KC, NTK>(a, l, s_pos, ub, 0, kr, vr);
       if (!bar_wait(bar, s_ok)) return gave_up(a);
       if (l == 0 && wg == 0 && otid() < RM)  // the previous step's argmax keys: every WG has read them
         __hip_atomic_store(lmkey + ((step + 1) & 1) * RM + otid(), 0ull, __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
 
-      phase_attn<2 / RH, NTK>(a, rs, l, s_pos, ub, kr, vr);
+      phase_attn<KU, KC, NTK>(a, rs, l, s_pos, ub, kr, vr);
       bar_arrive(bar);
-      load_w<1, 3, NTW>(a.wproj[l], D, 16 * w, D, 96 * V_, wp);
-      load_w<2, 6, NTW>(a.wfc[l], D, 64 * w + 32 * (V_ >> 2), DFF, 192 * (V_ & 3), wf);
+#define LOAD_WF load_w<2, Gm::SD, NTW>(a.wfc[l], D, Gm::FN * w + 32 * (V_ / Gm::D_KP), DFF, \
+                                     32 * Gm::SD * (V_ % Gm::D_KP), wf)
+      load_w<CS, 3, NTW>(a.wproj[l], D, Gm::PN * w, D, 96 * V_, wp);
+      // c_fc's fragments: across phase C at CS = 1 (12 fragments); at CS = 2 (24) they wait for
+      // C's barrier (held through C they spilled)
+      if constexpr (CS == 1) LOAD_WF;
       if (!bar_wait(bar, s_ok)) return gave_up(a);
 
-      phase_proj<3, RH, XB>(a, rs, rs.att, D, a.bproj[l], smem, w, h, wp);
+      phase_proj<3, CS, RH, XB>(a, rs, rs.att, D, a.bproj[l], smem, w, h, wp);
       bar_arrive(bar);
+      if constexpr (CS != 1) LOAD_WF;
+#undef LOAD_WF
       if (!bar_wait(bar, s_ok)) return gave_up(a);
 
-      phase_fc<RH, XB>(a, rs, l, smem, s_tok, s_pos, w, h, wf);
+      phase_fc<CS, RH, XB>(a, rs, l, smem, s_tok, s_pos, w, h, wf);
       bar_arrive(bar);
-      load_w<1, 12, NTW>(a.wmp[l], DFF, 16 * w, D, 384 * V_, wm);
+      load_w<CS, 12, NTW>(a.wmp[l], DFF, Gm::PN * w, D, 384 * V_, wm);
       if (!bar_wait(bar, s_ok)) return gave_up(a);
 
-      phase_proj<12, RH, XB>(a, rs, rs.hid, DFF, a.bmp[l], smem, w, h, wm);
+      // CS = 2: 2-k-step chunks, 3 in flight (the 24 weight fragments leave fewer VGPRs)
+      phase_proj<12, CS, RH, XB, (CS == 1 ? 4 : 2), (CS == 1 ? 2 : 3)>(
+          a, rs, rs.hid, DFF, a.bmp[l], smem, w, h, wm);
       bar_arrive(bar);
       // next block's c_attn.  Unconditional (a conditional load keeps the old wq live through
       // the whole block for the path that skips it); after block 11 the value is dead and wq is
       // reloaded after the LM head, which needs the VGPRs
-      load_w<3, 3, NTW>(a.wqkv[l + 1 < NLY ? l + 1 : 0], D, 48 * w, QKVN, 96 * V_, wq);
+      LOAD_WQ(l + 1 < NLY ? l + 1 : 0);
       if (!bar_wait(bar, s_ok)) return gave_up(a);
     }
     phase_lm<XB, NTW>(a, rs, smem, s_tok, s_pos, am_v, am_i, wg, GG, lmkey + (step & 1) * RM, s_lnf);
     bar_arrive(bar);
-    load_w<3, 3, NTW>(a.wqkv[0], D, 48 * w, QKVN, 96 * V_, wq);
+    LOAD_WQ(0);
     if (!bar_wait(bar, s_ok)) return gave_up(a);
 
     // ---- G: every WG reads the per-row argmax (one agent-scope key per row) and applies
@@ -1005,6 +1085,8 @@ __global__ __launch_bounds__(NT) void decode_persist_kernel(Args a) {
     __syncthreads();     // s_misc is rewritten next step
   }
 }
+#undef LOAD_WQ
+#undef V_
 
 }  // namespace dpk
 }  // namespace zs
@@ -1012,7 +1094,7 @@ __global__ __launch_bounds__(NT) void decode_persist_kernel(Args a) {
 using namespace zs;
 
 extern "C" int zs_decode_persist_workspace_bytes(void) { return dpk::WS_BYTES; }
-extern "C" int zs_decode_persist_grid(void) { return dpk::G; }
+extern "C" int zs_decode_persist_grid(void) { return dpk::G; }   // at col_split 1, row_split 1
 
 extern "C" int zs_gpt2_decode_persist(int R, int Lmax, int max_steps, int stop0, int stop1, int V,
                                       const void* wte, const void* wpe, const void* wte_packed,
@@ -1020,12 +1102,15 @@ extern "C" int zs_gpt2_decode_persist(int R, int Lmax, int max_steps, int stop0,
                                       const float* lnf_w, const float* lnf_b, void* const* kv,
                                       int* pos, int* next_tok, int* done, int* out_ids,
                                       int* out_len, int* step_ctr, int* all_done, void* ws,
-                                      long ws_bytes, int row_split, void* stream) {
+                                      long ws_bytes, int row_split, int col_split, void* stream) {
   using namespace dpk;
   ZS_REQUIRE(row_split == 1 || row_split == 2, "zs_gpt2_decode_persist: row_split 1 or 2 (got %d)",
              row_split);
+  ZS_REQUIRE(col_split == 1 || col_split == 2, "zs_gpt2_decode_persist: col_split 1 or 2 (got %d)",
+             col_split);
+  const int grid = G / col_split * row_split;
   ZS_REQUIRE(R >= 1 && R <= RM, "zs_gpt2_decode_persist: R in 1..%d (got %d)", RM, R);
-  ZS_REQUIRE(V >= 32 * NW * G * row_split && V <= 1 << 24, "zs_gpt2_decode_persist: vocab %d", V);
+  ZS_REQUIRE(V >= 32 * NW * grid && V <= 1 << 24, "zs_gpt2_decode_persist: vocab %d", V);
   ZS_REQUIRE(Lmax >= 2 && max_steps >= 1, "zs_gpt2_decode_persist: Lmax %d max_steps %d", Lmax, max_steps);
   ZS_REQUIRE(ws && ws_bytes >= WS_BYTES && ((uintptr_t)ws & 255) == 0,
              "zs_gpt2_decode_persist: workspace of %d bytes, 256-byte aligned", WS_BYTES);
@@ -1037,6 +1122,7 @@ extern "C" int zs_gpt2_decode_persist(int R, int Lmax, int max_steps, int stop0,
   Args a{};
   a.R = R; a.Lmax = Lmax; a.max_steps = max_steps; a.stop0 = stop0; a.stop1 = stop1; a.V = V;
   a.lm_il = g_dp_lmil;
+  a.spin_max = g_dp_spin > 0 ? (unsigned)g_dp_spin : g_dp_spin < 0 ? 0u : SPIN_MAX;
   a.wte = (const bf16_t*)wte; a.wpe = (const bf16_t*)wpe;
   for (int l = 0; l < NLY; ++l) {
     const void* const* p = layer_w + 8 * l;
@@ -1056,20 +1142,19 @@ extern "C" int zs_gpt2_decode_persist(int R, int Lmax, int max_steps, int stop0,
   a.step_ctr = step_ctr; a.all_done = all_done; a.ws = (char*)ws;
   // the barrier counter and timeout word: zeroed before every launch (a memset node under capture)
   ZS_CHECK_HIP(hipMemsetAsync(ws, 0, WS_SYNC_BYTES, S(stream)));
-#define DP_LAUNCH(RH_, XB_, NTM_) \
-  hipLaunchKernelGGL((decode_persist_kernel<RH_, XB_, NTM_>), dim3(RH_ * G), dim3(NT), 0, S(stream), a)
-  if (row_split == 2) {
-    if (!g_dp_xb) DP_LAUNCH(2, false, 0);
-    else if (g_dp_nt == 1) DP_LAUNCH(2, true, 1);
-    else if (g_dp_nt == 2) DP_LAUNCH(2, true, 2);
-    else if (g_dp_nt == 3) DP_LAUNCH(2, true, 3);
-    else DP_LAUNCH(2, true, 0);
+#define DP_LAUNCH(CS_, RH_)                                                                      \
+  do {                                                                                           \
+    if (g_dp_nt) hipLaunchKernelGGL((decode_persist_kernel<CS_, RH_, true, 2>), dim3(grid),      \
+                                    dim3(NT), 0, S(stream), a);                                  \
+    else hipLaunchKernelGGL((decode_persist_kernel<CS_, RH_, true, 0>), dim3(grid), dim3(NT), 0, \
+                            S(stream), a);                                                       \
+  } while (0)
+  if (col_split == 1) {
+    if (row_split == 1) DP_LAUNCH(1, 1);
+    else DP_LAUNCH(1, 2);
   } else {
-    if (!g_dp_xb) DP_LAUNCH(1, false, 0);
-    else if (g_dp_nt == 1) DP_LAUNCH(1, true, 1);
-    else if (g_dp_nt == 2) DP_LAUNCH(1, true, 2);
-    else if (g_dp_nt == 3) DP_LAUNCH(1, true, 3);
-    else DP_LAUNCH(1, true, 0);
+    if (row_split == 1) DP_LAUNCH(2, 1);
+    else DP_LAUNCH(2, 2);
   }
 #undef DP_LAUNCH
   ZS_LAUNCH_CHECK();

@@ -299,9 +299,17 @@ class Gpt2Decoder:
         # 2: the row-split grid (2 x decode_persist_grid() workgroups, a shorter step) -- chosen
         # by the caller when few batches are in flight (pipeline.ConcurrentRunner)
         self.persist_row_split = int(os.environ.get("ZSAAC_PERSIST_RS", "1"))
+        # 2: two column slices per workgroup (half the workgroups per batch, less CU time per
+        # step, a longer step) -- chosen with row_split by pipeline.ConcurrentRunner
+        self.persist_col_split = int(os.environ.get("ZSAAC_PERSIST_CS", "1"))
         if self.persist:
             import ctypes
             self.persist_ws = ops.decode_persist_workspace(dev)
+            # the shared packed LM head and pointer table, built now and synchronised: a twin
+            # decoder launched on another stream must never read a half-written wte_packed
+            w.wte_packed()
+            w.layer_ptrs()
+            torch.cuda.synchronize(dev)
             self._kv_ptrs = (ctypes.c_void_p * (2 * NL))(
                 *[t.data_ptr() for t in self.kc], *[t.data_ptr() for t in self.vc])
         self.rowmap = torch.zeros(self.R, **i32)
@@ -318,7 +326,11 @@ class Gpt2Decoder:
         self.tok_tmp = torch.zeros(self.R, max_steps, **i32)
         self.graphs: Dict[Tuple, torch.cuda.CUDAGraph] = {}
         self.n_captures = 0
-        self.rows_stepped = 0       # decode rows x steps enqueued by step_chunk (work counter)
+        self.rows_stepped = 0       # decode rows x steps run (work counter; persistent launches
+                                    # add theirs when the host sees them finish: note_persist_steps)
+        self.gave_up = 0            # persistent launches that gave up and resumed stepwise
+        self._eager = False         # step_chunk without graphs (the give-up fallback)
+        self._persist_R = 0         # rows of the persistent launch in flight (0: none)
         self.ws = ops.skinny_workspace(dev, [(M, N, K) for M in {self.R, self.Rp}
                                              for N, K in ((3 * D, D), (D, D), (4 * D, D), (D, 4 * D))])
 
@@ -481,7 +493,7 @@ class Gpt2Decoder:
         it only picks the compaction bucket, so None is always safe."""
         key, body, pre = self._chunk_plan(alive)
         self.rows_stepped += (key[2] if key[0] == "greedy_c" else self._rows_of(key)) * self.chunk
-        if self.use_graph:
+        if self.use_graph and not self._eager:
             self._graph(key, body, pre).replay()
         else:
             if pre is not None:
@@ -505,14 +517,36 @@ class Gpt2Decoder:
 
     def run_to_completion(self):
         """Synchronous loop: replay chunks until every row stopped or entry_length reached."""
+        if self._persist_R:
+            flag, arr, alive = self.all_done.tolist()
+            if arr >= 0:
+                self.note_persist_steps(int(self.step_ctr.item()))
+                return
+            self.resume_stepwise()
         for _ in range(self.n_chunks):
             flag, arr, alive = self.all_done.tolist()
-            if arr < 0:
-                raise RuntimeError("zs_gpt2_decode_persist: the persistent grid was not co-resident "
-                                   "(gave up waiting); too many launches in flight for the CUs")
             if flag:
                 break
             self.step_chunk(alive)
+
+    def note_persist_steps(self, steps: int):
+        """The host saw the persistent launch finish after ``steps`` decode steps (step_ctr):
+        count the rows it stepped (the launch runs steps 1 .. steps - 1)."""
+        if self._persist_R:
+            self.rows_stepped += self._persist_R * max(0, steps - 1)
+            self._persist_R = 0
+
+    def resume_stepwise(self):
+        """After a persistent launch gave up (all_done[1] = -1: its grid was not co-resident in
+        time): the kernel writes pos / done / next_tok / step_ctr only when it finishes, so the
+        decode state is still the one it started from (ids and K/V rows it wrote past it are
+        rewritten step by step).  Re-arm the flags; the remaining steps then run on the per-step
+        path, eagerly (no graph capture while other streams run).  Enqueued on the current
+        stream."""
+        self.all_done[:2].zero_()
+        self.gave_up += 1
+        self._persist_R = 0
+        self._eager = True
 
     def _state(self):
         return [self.pos, self.next_tok, self.done, self.out_ids, self.out_len, self.step_ctr,
@@ -534,6 +568,8 @@ class Gpt2Decoder:
         self._active = (("greedy", R, self.stop0, self.stop1, self.temperature),
                         lambda: self._greedy_step_body(R))
         self._cgreedy = R if (self.compact and R >= self.min_bucket) else None
+        self._eager = False
+        self._persist_R = 0
         if self.persist and R <= 64:
             w = self.w
             ev = PERSIST_LOG
@@ -546,10 +582,11 @@ class Gpt2Decoder:
                                     w.lnf[0], w.lnf[1], self._kv_ptrs,
                                     self.pos, self.next_tok, self.done, self.out_ids, self.out_len,
                                     self.step_ctr, self.all_done, self.persist_ws,
-                                    row_split=self.persist_row_split)
+                                    row_split=self.persist_row_split,
+                                    col_split=self.persist_col_split)
             if ev is not None:
                 ev[-1][1].record()
-            self.rows_stepped += R * (self.max_steps - 1)   # upper bound (rows that stop early end it)
+            self._persist_R = R
 
     def greedy(self, B: int, Pmax: int):
         """After :meth:`prefill` (row_stride 1): generate2 for all B rows.
@@ -582,6 +619,8 @@ class Gpt2Decoder:
     def beam_begin(self, C: int, beam: int):
         assert beam <= self.topk and C * beam <= self.R
         R = C * beam
+        self._eager = False
+        self._persist_R = 0
         ops.lmhead_topk(self.hf[:C], self.w.wte, self.topk, self.pstat, self.pval, self.pidx,
                         temperature=self.temperature)
         for t in (self.done, self.step_ctr, self.all_done, self.out_ids, self.scores):

@@ -468,8 +468,9 @@ def decode_persist_workspace(device) -> torch.Tensor:
     return torch.zeros(n + 256, dtype=torch.uint8, device=device)
 
 
-def decode_persist_grid() -> int:
-    return call("zs_decode_persist_grid")
+def decode_persist_grid(row_split: int = 1, col_split: int = 1) -> int:
+    """Workgroups (one per CU) of one zs_gpt2_decode_persist launch."""
+    return call("zs_decode_persist_grid") // col_split * row_split
 
 
 def pack_b_fragments(W: torch.Tensor) -> torch.Tensor:
@@ -487,10 +488,10 @@ def pack_b_fragments(W: torch.Tensor) -> torch.Tensor:
 
 def gpt2_decode_persist(R, Lmax, max_steps, stop0, stop1, V, wte, wpe, wte_packed, temperature,
                         layer_ptrs, lnf_w, lnf_b, kv_ptrs, pos, next_tok, done, out_ids, out_len,
-                        step_ctr, all_done, ws, row_split=1):
+                        step_ctr, all_done, ws, row_split=1, col_split=1):
     """The remaining greedy steps of one bs <= 64 batch in one persistent launch
-    (zs_gpt2_decode_persist) of decode_persist_grid() * row_split workgroups.  layer_ptrs /
-    kv_ptrs: ctypes arrays of 96 / 24 device pointers."""
+    (zs_gpt2_decode_persist) of decode_persist_grid(row_split, col_split) workgroups.
+    layer_ptrs / kv_ptrs: ctypes arrays of 96 / 24 device pointers."""
     _need(1 <= R <= 64, "gpt2_decode_persist: 1 <= R <= 64")
     _need(wte.dtype == torch.bfloat16 and wpe.dtype == torch.bfloat16, "gpt2_decode_persist: bf16")
     for t, n in ((pos, "pos"), (next_tok, "next_tok"), (done, "done"), (out_ids, "out_ids"),
@@ -503,4 +504,4 @@ def gpt2_decode_persist(R, Lmax, max_steps, stop0, stop1, V, wte, wpe, wte_packe
     call("zs_gpt2_decode_persist", R, Lmax, max_steps, stop0, stop1, V, _p(wte), _p(wpe),
          _p(wte_packed), float(temperature), layer_ptrs, _p(lnf_w), _p(lnf_b), kv_ptrs, _p(pos), _p(next_tok), _p(done), _p(out_ids),
          _p(out_len), _p(step_ctr), _p(all_done), base + off, ws.numel() - off, int(row_split),
-         _s())
+         int(col_split), _s())

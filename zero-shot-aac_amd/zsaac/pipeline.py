@@ -15,7 +15,7 @@ import copy
 import os
 import time
 from dataclasses import dataclass
-from typing import List, Optional, Sequence
+from typing import List, Optional, Sequence, Tuple
 
 import numpy as np
 import torch
@@ -228,14 +228,36 @@ class CaptionPipeline:
             dec.greedy_begin(B)
 
 
-def choose_row_split(in_flight: int, to_begin: int, grid: int, cus: int) -> int:
-    """row_split of the persistent decode launch of the next batch to begin, given the
-    workgroups of the grids already in flight and the batches still to begin (this one
-    included): 2 when this grid at that size and every other batch still to begin at row_split
-    1 fit beside the grids in flight.  Then every later begin still has room for row_split 1,
-    so (with at most cus // grid batches in flight at row_split 1) the grids in flight never
-    exceed the CUs and every persistent launch stays co-resident."""
-    return 2 if in_flight + grid * (to_begin + 1) <= cus else 1
+def persist_shapes(env: Optional[str] = None) -> List[Tuple[int, int]]:
+    """The persistent-decode grid shapes (col_split, row_split) a runner may use, largest grid
+    first: ZSAAC_PERSIST_SHAPES ("cs rs" digit pairs, e.g. "12,11,21") or, when ZSAAC_PERSIST_CS /
+    ZSAAC_PERSIST_RS fix a shape, that one alone."""
+    env = os.environ.get("ZSAAC_PERSIST_SHAPES", DEFAULT_PERSIST_SHAPES) if env is None else env
+    if "ZSAAC_PERSIST_CS" in os.environ or "ZSAAC_PERSIST_RS" in os.environ:
+        env = os.environ.get("ZSAAC_PERSIST_CS", "1") + os.environ.get("ZSAAC_PERSIST_RS", "1")
+    shapes = [(int(t[0]), int(t[1])) for t in env.replace(" ", "").split(",") if t]
+    for cs, rs in shapes:
+        assert cs in (1, 2) and rs in (1, 2), f"persist shape {cs}{rs}"
+    return sorted(set(shapes), key=lambda sh: -ops.decode_persist_grid(sh[1], sh[0]))
+
+
+# largest grid first; the last is the throughput shape every batch can fall back to
+DEFAULT_PERSIST_SHAPES = "12,11"
+
+
+def choose_persist_shape(in_flight: int, to_begin: int, shapes: List[Tuple[int, int]],
+                         cus: int) -> Tuple[int, int]:
+    """Grid shape (col_split, row_split) of the persistent decode launch of the next batch to
+    begin, given the workgroups of the grids already in flight and the batches still to begin
+    (this one included): the largest shape whose grid, beside the grids in flight and every
+    other batch still to begin at the smallest shape, fits the CUs.  Then every later begin still
+    has room for the smallest shape, so (with at most cus // smallest batches in flight) the
+    grids in flight never exceed the CUs and every persistent launch stays co-resident."""
+    g_min = ops.decode_persist_grid(shapes[-1][1], shapes[-1][0])
+    for cs, rs in shapes:
+        if in_flight + ops.decode_persist_grid(rs, cs) + g_min * (to_begin - 1) <= cus:
+            return cs, rs
+    return shapes[-1]
 
 
 class ConcurrentRunner:
@@ -247,11 +269,17 @@ class ConcurrentRunner:
 
     Results are copied out on the pipeline's stream before it takes the next batch."""
 
-    def __init__(self, pipe: CaptionPipeline, n_inflight: int = 2, streams: Optional[list] = None):
-        if pipe.decoder.persist:
-            # persistent decode grids must be co-resident: at most CUs // grid launches in flight
-            cus = torch.cuda.get_device_properties(pipe.dev).multi_processor_count
-            n_inflight = max(1, min(n_inflight, cus // ops.decode_persist_grid()))
+    def __init__(self, pipe: CaptionPipeline, n_inflight: int = 2, streams: Optional[list] = None,
+                 shapes: Optional[List[Tuple[int, int]]] = None):
+        self.cus = torch.cuda.get_device_properties(pipe.dev).multi_processor_count
+        # persistent grids (greedy bf16 at <= 64 rows; beam search never launches one), one shape
+        # per batch from `shapes` (largest first, see choose_persist_shape)
+        self.persist = pipe.decoder.persist and not pipe.cfg.beam
+        self.shapes = shapes or persist_shapes()
+        if self.persist:
+            # persistent decode grids must be co-resident: at most CUs // (smallest grid) in flight
+            g_min = ops.decode_persist_grid(self.shapes[-1][1], self.shapes[-1][0])
+            n_inflight = max(1, min(n_inflight, self.cus // g_min))
         self.n_inflight = n_inflight
         self.pipes = [pipe] + [pipe.twin() for _ in range(n_inflight - 1)]
         # dedicated streams on distinct hardware queues: pooled torch streams take their queue at
@@ -260,10 +288,6 @@ class ConcurrentRunner:
         self.streams = (list(streams[:len(self.pipes)]) if streams is not None
                         else ops.dedicated_streams(len(self.pipes), pipe.dev))
         assert len(self.streams) == len(self.pipes), "ConcurrentRunner: too few streams given"
-        # persistent grid per launch: decode_persist_grid() workgroups (row_split 1) or twice that
-        # (row_split 2, a ~25% shorter step for ~50% more CU time); see run()
-        self.cus = torch.cuda.get_device_properties(pipe.dev).multi_processor_count
-        self.auto_row_split = pipe.decoder.persist and "ZSAAC_PERSIST_RS" not in os.environ
 
     def warmup(self, wav: torch.Tensor):
         """Runs one batch per pipeline synchronously (captures every decode graph)."""
@@ -298,7 +322,7 @@ class ConcurrentRunner:
         self.decode_steps = [0] * len(batches)     # per batch: decode steps actually enqueued
         self.assign = []                           # (pipeline index, batch index), in begin order
         self.row_split = [1] * len(batches)
-        grid = ops.decode_persist_grid() if self.auto_row_split else 0
+        self.shape = [(1, 1)] * len(batches)      # persistent grid shape (col_split, row_split)
         slots = {}                                 # pipeline index -> its launch's workgroups
         while nxt < len(batches) or active:
             progressed = False
@@ -306,12 +330,13 @@ class ConcurrentRunner:
                 st = active.get(i)
                 if st is None:
                     if nxt < len(batches):
-                        if grid:
-                            rs = choose_row_split(sum(slots.values()), len(batches) - nxt,
-                                                  grid, self.cus)
-                            p.decoder.persist_row_split = rs
-                            slots[i] = rs * grid
+                        if self.persist:
+                            cs, rs = choose_persist_shape(sum(slots.values()), len(batches) - nxt,
+                                                          self.shapes, self.cus)
+                            p.decoder.persist_col_split, p.decoder.persist_row_split = cs, rs
+                            slots[i] = ops.decode_persist_grid(rs, cs)
                             self.row_split[nxt] = rs
+                            self.shape[nxt] = (cs, rs)
                         with torch.cuda.stream(s):
                             (p.begin_wav if inputs == "wav" else p.begin_emb)(batches[nxt])
                             ev, flag = p.decoder.finished_async()
@@ -325,8 +350,17 @@ class ConcurrentRunner:
                     continue
                 progressed = True
                 if int(flag[1]) < 0:
-                    raise RuntimeError("persistent decode gave up: grid not co-resident")
+                    # the persistent launch gave up waiting (its grid was not co-resident): finish
+                    # this batch on the per-step path from the state it started from
+                    with torch.cuda.stream(s):
+                        p.decoder.resume_stepwise()
+                        p.decoder.step_chunk(None)
+                        ev, flag = p.decoder.finished_async()
+                    slots.pop(i, None)
+                    active[i] = (bi, 1, ev, flag)
+                    continue
                 if int(flag[0]) or n >= p.decoder.n_chunks:
+                    p.decoder.note_persist_steps(int(flag[3]))
                     self.decode_steps[bi] = int(flag[3]) if not p.cfg.beam else 1 + n * p.decoder.chunk
                     with torch.cuda.stream(s):
                         r = p.result()
