@@ -9,10 +9,12 @@ eval batches of 64 clips exactly as the reference evaluates them: STFT/log-mel +
 audio_proj + L2 -> sound-effect hard prompt -> MLP mapper -> GPT-2 small prefill +
 get_prefix_tokens + greedy generate2 (entry_length 67, stop ids 13 / 764), bf16 operands / f32
 accumulation.  Every decode GEMM of a batch is a 64-row GEMM.  One "step" = one eval batch of
-64 clips (the last batch of the 1045 holds 21).  --inflight independent batches (default 5) are
+64 clips (the last batch of the 1045 holds 21).  --inflight independent batches (default 10) are
 in flight per GPU, each on its own HIP stream (pipeline twins sharing the weights,
-zsaac/pipeline.py ConcurrentRunner); GPU_MAX_HW_QUEUES is raised to --hw-queues (default 8, the
-runtime allows up to 32) so those streams get hardware queues of their own.  With N ranks the
+zsaac/pipeline.py ConcurrentRunner), each decoding in its own persistent launch of 24 workgroups
+(col_split 2; a larger grid when CUs are free, zsaac.pipeline.choose_persist_shape);
+GPU_MAX_HW_QUEUES is raised to --hw-queues (default 16, the runtime allows up to 32) so those
+streams get hardware queues of their own.  With N ranks the
 clips are sharded (zsaac/dist.py shard_range) and ONE RCCL all-gather of the generated token ids
 + lengths (zsaac/dist.py collect_captions) is inside the timed region.
 
@@ -55,7 +57,7 @@ import sys
 import time
 
 
-def _hw_queues_from_argv(default=8):
+def _hw_queues_from_argv(default=16):
     for i, a in enumerate(sys.argv):
         if a == "--hw-queues" and i + 1 < len(sys.argv):
             return int(sys.argv[i + 1])
@@ -113,16 +115,17 @@ def parse():
     ap.add_argument("--group", type=int, default=1,
                     help="eval batches decoded together in one decode step (1 = the metric's "
                          "bs=64; > 1 is the labelled throughput mode)")
-    ap.add_argument("--inflight", type=int, default=5,
+    ap.add_argument("--inflight", type=int, default=10,
                     help="independent batches in flight per GPU, each on its own HIP stream")
-    ap.add_argument("--hw-queues", type=int, default=8,
+    ap.add_argument("--hw-queues", type=int, default=16,
                     help="GPU_MAX_HW_QUEUES for this process (read before HIP initialises)")
     ap.add_argument("--compact", type=int, default=1,
                     help="greedy bf16 at >= 512 rows: decode only the rows that have not stopped")
     ap.add_argument("--extras", type=int, default=1,
                     help="N=1: also measure the throughput mode, the f32 mode and id agreement")
-    ap.add_argument("--cpu-baseline-clips", type=int, default=8,
-                    help="C2 clips timed on the CPU oracle (C1 takes 2x, C3 beam 5 takes 1/2)")
+    ap.add_argument("--cpu-baseline-clips", type=int, default=32,
+                    help="C2 clips timed on the CPU oracle (C1: all 50 golden clips, C3 beam 5: "
+                         "a quarter of this, at least 4)")
     ap.add_argument("--cpu-baseline-full", action="store_true",
                     help="the BASELINE.md §3 plan: 64 C2 clips, all 50 C1 clips, 64 C3 clips")
     ap.add_argument("--no-scaling-proxy", action="store_true")
@@ -254,9 +257,13 @@ def run_captions(args, world, rank, device, pipe, n_local, first, counts, inflig
         # the roofline's live launch timing: the same batches once more, untimed, with HIP events
         # around every persistent launch (events recorded inside the timed region cost it 3-5 %)
         zdec.PERSIST_LOG = []
-        runner.log_outs = runner.run(batches)
-        torch.cuda.synchronize()
-        runner.timed_log = list(zdec.PERSIST_LOG)
+        try:
+            runner.log_outs = runner.run(batches)
+            torch.cuda.synchronize()
+            runner.timed_log = list(zdec.PERSIST_LOG)
+        finally:
+            zdec.PERSIST_LOG = None         # no events around launches outside this pass
+        ALL_PERSIST_LOGS.extend(runner.timed_log)
     info = {"graph_captures_timed": sum(p.decoder.n_captures for p in runner.pipes) - cap0,
             "decode_rows_stepped_per_clip": round(
                 (sum(p.decoder.rows_stepped for p in runner.pipes) - rows0) / max(1, n_local), 2),
@@ -431,6 +438,16 @@ def persist_launch_bytes(w_step, plen, steps, kv_row=12 * 2 * 768 * 2):
 PMC_PERSIST_FILE = os.path.join(ROOT, "profiles", "r3_pmc_persist.json")
 
 
+def shape_counts(runner):
+    """{"cs<col_split>rs<row_split> (<workgroups> WGs)": launches} of a runner's last run."""
+    from zsaac import ops
+    out = {}
+    for cs, rs in getattr(runner, "shape", []):
+        k = f"cs{cs}rs{rs} ({ops.decode_persist_grid(rs, cs)} WGs)"
+        out[k] = out.get(k, 0) + 1
+    return out
+
+
 def persist_roofline(pipe, runner, outs, dt, log):
     """roofline of the dominant kernel, decode_persist_kernel: every launch of a repeat of the
     timed region (same batches, same streams and concurrency, untimed: HIP events recorded on each
@@ -458,10 +475,10 @@ def persist_roofline(pipe, runner, outs, dt, log):
     steps = sum(runner.decode_steps) / max(1, len(runner.decode_steps))
     return _hbm_entry(
         f"decode_persist_kernel (zs_gpt2_decode_persist): decode steps 1..{steps - 1:.0f} of one "
-        f"bs-64 eval batch in one launch (G={ops.decode_persist_grid()} workgroups), the {n} launches of "
+        f"bs-64 eval batch in one launch (grid shapes {shape_counts(runner)}), the {n} launches of "
         f"a repeat of the timed region, {runner.n_inflight} batches in flight", avg_b, avg_s,
         {"launches": n, "avg_launch_ms": round(avg_s * 1e3, 3),
-         "row_split2_launches": sum(1 for r in getattr(runner, "row_split", []) if r == 2),
+         "grid_shapes": shape_counts(runner),
          "weight_bytes_per_step": int(w_step), "steps_per_launch_mean": round(steps - 1, 2),
          "traffic": traffic, "traffic_source": tsrc,
          "traffic_note": "PMC FETCH_SIZE*2*1024 + WRITE_SIZE*1024 per launch, single-stream "
@@ -471,9 +488,13 @@ def persist_roofline(pipe, runner, outs, dt, log):
                                   "note": "all launches' algorithmic bytes / the headline's timed wall"}})
 
 
+ALL_PERSIST_LOGS = []     # (start, end, decoder) events of every logged persistent launch
+
+
 def persist_all_launches(log):
-    """Average duration of every persistent launch of this process (warmup, timed region and the
-    single-stream roofline runs): the number rocprofv3 --kernel-trace --stats reports."""
+    """Average duration of the logged persistent launches (the roofline's repeat of the timed
+    region and the single-stream step runs); rocprofv3 --kernel-trace --stats over the same
+    command also counts the warmup and timed-region launches."""
     d = [e0.elapsed_time(e1) for e0, e1, _ in log]
     return {"launches": len(d), "avg_ms": round(sum(d) / max(1, len(d)), 3)}
 
@@ -488,10 +509,15 @@ def decode_step_roofline(pipe, wav, agg_steps_per_s=None, reps=3):
     if dec.persist:
         per = []
         for _ in range(reps):
-            pipe.begin_wav(wav)
-            dec.run_to_completion()
-            torch.cuda.synchronize()
-            e0, e1, _ = zdec.PERSIST_LOG[-1]
+            zdec.PERSIST_LOG = []
+            try:
+                pipe.begin_wav(wav)
+                dec.run_to_completion()
+                torch.cuda.synchronize()
+            finally:
+                log, zdec.PERSIST_LOG = zdec.PERSIST_LOG, None
+            ALL_PERSIST_LOGS.extend(log)
+            e0, e1, _ = log[-1]
             steps = int(dec.step_ctr.item())
             per.append((e0.elapsed_time(e1) / 1e3, steps))
         dur, steps = sorted(per)[len(per) // 2]
@@ -1003,17 +1029,21 @@ def strong_scaling_proxy(args, device, pipe, t_full, n_full, n_ranks=8):
     shard: the reference's consecutive bs-64 batches (64 + 64 + 3) and near-equal batches over
     every in-flight stream (split_batches parts=inflight); the faster is what a rank runs."""
     from zsaac import dist as zd
+    full_src = "the headline's timed region"
+    if t_full is None:
+        t_full = run_captions(args, 1, 0, device, pipe, n_full, 0, [n_full], args.inflight, 0)[0]
+        full_src = "a separate run of the full set (not the headline's timed region)"
     lo, hi = zd.shard_range(n_full, 0, n_ranks)
     n = hi - lo
-    out = {"clips_full": n_full, "seconds_full": round(t_full, 4), "ranks": n_ranks,
-           "clips_per_rank": n}
+    out = {"clips_full": n_full, "seconds_full": round(t_full, 4), "full_timing": full_src,
+           "ranks": n_ranks, "clips_per_rank": n}
     best = None
     for name, parts in (("bs64_batches", 0), ("balanced_batches", args.inflight)):
         dt, outs, runner, _ = run_captions(args, 1, 0, device, pipe, n, lo, [n], args.inflight,
                                            0, parts=parts)
         sizes = [int(o.ids.shape[0]) for o in outs]
         out[name] = {"seconds": round(dt, 4), "batches": sizes,
-                     "row_split": list(getattr(runner, "row_split", [])),
+                     "grid_shapes": [f"cs{c}rs{r}" for c, r in getattr(runner, "shape", [])],
                      "predicted_speedup": round(t_full / dt, 2)}
         best = max(best or 0.0, t_full / dt)
         del outs, runner
@@ -1093,13 +1123,17 @@ def main():
         res["roofline_stepwise_mproj"] = roofline_rows_gemm(pipe, "mproj")
         res["roofline_stepwise_proj"] = roofline_rows_gemm(pipe, "proj")
         res["roofline_decode_attention"] = roofline_attention(pipe)
-        res["persist_launches_all"] = persist_all_launches(zdec.PERSIST_LOG or [])
+        res["persist_launches_all"] = persist_all_launches(ALL_PERSIST_LOGS)
         del wav
     elif rank == 0 and args.stages:
         res["stages"] = stage_times(pipe, synthetic_clips(B, 0, device))
-    if (rank == 0 and world == 1 and headline_cfg and not args.clips and not args.steps
+    if (rank == 0 and world == 1 and headline_cfg and not args.clips
             and not args.no_scaling_proxy):
-        res["strong_scaling_proxy"] = strong_scaling_proxy(args, device, pipe, dt, n_total)
+        # on the 1045-clip Clotho-eval set, also when --steps sized the timed run differently
+        # (then the 1045-clip set is timed here, outside the headline)
+        t_full = dt if n_total == CLOTHO_EVAL_CLIPS else None
+        res["strong_scaling_proxy"] = strong_scaling_proxy(args, device, pipe, t_full,
+                                                           CLOTHO_EVAL_CLIPS)
     del runner, outs
     if rank == 0 and world == 1 and args.extras and args.group == 1 and not args.beam:
         del pipe
@@ -1121,8 +1155,7 @@ def main():
                                "f32": idparity.summary(torch.float32, device)}
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.cpu_baseline_clips > 0:
         n2, n1, n3 = ((64, 50, 64) if args.cpu_baseline_full else
-                      (args.cpu_baseline_clips, min(50, 2 * args.cpu_baseline_clips),
-                       max(1, args.cpu_baseline_clips // 2)))
+                      (args.cpu_baseline_clips, 50, max(4, args.cpu_baseline_clips // 4)))
         res["cpu_baseline"] = cpu_baseline(args, csd, asd, n2, n1, n3)
     if rank == 0:
         print(json.dumps(res), flush=True)

@@ -194,8 +194,9 @@ __device__ __forceinline__ T ldg(const T* p) {
   else return *p;
 }
 
-// weight fragments of NB 16-column blocks x S k-steps (MFMA B operand, W [N][K] row-major)
-template <int NB, int S, bool NTL = false>
+// weight fragments of NB 16-column blocks x S k-steps (MFMA B operand, W [N][K] row-major);
+// only the k-steps [S0, S1) (a prefetch split around a barrier wait)
+template <int NB, int S, bool NTL = false, int S0 = 0, int S1 = S>
 __device__ __forceinline__ void load_w(const bf16_t* W, int K, int n0, int N, int kbase,
                                        bf16x8_t (&b)[NB * S]) {
   const int lane = otid() & 63, fr = lane & 15, fk = 8 * (lane >> 4);
@@ -203,7 +204,7 @@ __device__ __forceinline__ void load_w(const bf16_t* W, int K, int n0, int N, in
   for (int nb = 0; nb < NB; ++nb) {
     const bf16_t* row = W + (long)min(n0 + 16 * nb + fr, N - 1) * K + kbase + fk;
 #pragma unroll
-    for (int s = 0; s < S; ++s)
+    for (int s = S0; s < S1; ++s)
       b[nb * S + s] = ldg<NTL>(reinterpret_cast<const bf16x8_t*>(row + 32 * s));
   }
 }
@@ -280,10 +281,15 @@ __device__ __forceinline__ bool bar_wait(Bar& b, volatile lds_int_t* s_ok) {
 // NR rows (64, or 32 for a row-split grid) from row r0, TPR = 512 / NR threads per row, NQ column
 // quads per thread; rows land at LDS row r - r0.  MODE 1 stores x rows r % gw == w of its range
 // (gw = the column-slice workgroups).
-template <int MODE, int NR = RM, bool XB = false>
+struct NoLate {
+  __device__ __forceinline__ void operator()() const {}
+};
+// late(): loads issued right after the handed-off rows' loads (the rest of a weight prefetch
+// split around the barrier wait: younger than the rows, so the rows are not waited behind them)
+template <int MODE, int NR = RM, bool XB = false, typename Late = NoLate>
 __device__ __forceinline__ void ln_rows(const Args& a, const Rs& rs, bf16_t* hs, const int* s_tok,
                                         const int* s_pos, int w, const float* s_lnf = nullptr,
-                                        int r0 = 0, int gw = G) {
+                                        int r0 = 0, int gw = G, Late late = Late()) {
   constexpr int TPR = NT / NR, NQ = D / 4 / TPR;
   const int tid = otid(), rl = tid / TPR, q = tid % TPR, r = r0 + rl;
   const int rr = min(r, a.R - 1);
@@ -292,9 +298,16 @@ __device__ __forceinline__ void ln_rows(const Args& a, const Rs& rs, bf16_t* hs,
     // sc1 loads of 8 columns (octets q + TPR i); statistics in f32 over the bf16 values
     constexpr int NO = NQ / 2;
     float xv[NO][8];
+    u32x4_t xu[NO];
+#pragma unroll
+    for (int i = 0; i < NO; ++i) xu[i] = ld16(rs.xb, (rr * D + 8 * (q + TPR * i)) * 2);
+    late();
+    // all NO loads in flight before the first use (under the LM head's register pressure the
+    // compiler otherwise issued them one round trip at a time)
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int i = 0; i < NO; ++i) {
-      const u32x4_t u = ld16(rs.xb, (rr * D + 8 * (q + TPR * i)) * 2);
+      const u32x4_t u = xu[i];
       xv[i][0] = __uint_as_float(u.x << 16); xv[i][1] = __uint_as_float(u.x & 0xffff0000u);
       xv[i][2] = __uint_as_float(u.y << 16); xv[i][3] = __uint_as_float(u.y & 0xffff0000u);
       xv[i][4] = __uint_as_float(u.z << 16); xv[i][5] = __uint_as_float(u.z & 0xffff0000u);
@@ -430,18 +443,22 @@ __device__ __forceinline__ void put_partial(float* red, int slab, int col0, cons
 // RH = 1: all 64 rows; RH = 2: the 32 rows of half h (row-split grid).  Wave v = (column group
 // v / A_KP of 3 blocks, K part v % A_KP); the A_KP partial slabs alias the LN rows (98,304 B at
 // every CS).
-template <int CS, int RH, bool XB>
+template <int CS, int RH, bool XB, typename Late = NoLate>
 __device__ __forceinline__ void phase_qkv(const Args& a, const Rs& rs, int l, char* smem,
                                           const int* s_tok, const int* s_pos, int w, int h,
-                                          const bf16x8_t (&wq)[3 * Geo<CS>::SA]) {
+                                          const bf16x8_t (&wq)[3 * Geo<CS>::SA], Late late = Late()) {
   using Gm = Geo<CS>;
   constexpr int NR = RM / RH, NRB = NR / 16, QN = Gm::QN, KP = Gm::A_KP, QQ = QN / 4;
   constexpr int NQD = (NR * QQ + NT - 1) / NT;      // epilogue quads per thread
   bf16_t* hs = reinterpret_cast<bf16_t*>(smem);
   float* red = reinterpret_cast<float*>(smem);
   const int tid = otid(), v = tid >> 6, r0 = h * NR, ng = v / KP, kp = v % KP;
-  if (l == 0) ln_rows<1, NR>(a, rs, hs, s_tok, s_pos, w, nullptr, r0, Gm::GW);
-  else ln_rows<0, NR, XB>(a, rs, hs, s_tok, s_pos, w, nullptr, r0, Gm::GW);
+  if (l == 0) {
+    late();
+    ln_rows<1, NR>(a, rs, hs, s_tok, s_pos, w, nullptr, r0, Gm::GW);
+  } else {
+    ln_rows<0, NR, XB>(a, rs, hs, s_tok, s_pos, w, nullptr, r0, Gm::GW, late);
+  }
   lds_sync();
   f32x4_t acc[NRB][3];
   mma_lds<3, Gm::SA, NRB>(hs, 32 * Gm::SA * kp, wq, acc);
@@ -531,16 +548,22 @@ __device__ __forceinline__ void phase_attn(const Args& a, const Rs& rs, int l, c
   long base[KU];
   // KU = 4: the new token's k / v are loaded after the cached chunks (32 VGPRs less across them)
   constexpr bool LATE_KV = KU > 2;
+  // every unit's q (and k / v) load is issued before any is used: one round trip, not KU
+  uint4 qu[KU];
 #pragma unroll
   for (int k = 0; k < KU; ++k) {
     attn_unit(a, s_pos, ub + KU * v + k, row[k], hh[k], p[k], base[k]);
     const int off = (min(row[k], a.R - 1) * QKVN + hh[k] * HD + 8 * sub) * 2;
-    const uint4 qu = tou4(ld16(rs.qkv, off));
+    qu[k] = tou4(ld16(rs.qkv, off));
     if constexpr (!LATE_KV) {
       knu[k] = tou4(ld16(rs.qkv, off + 2 * D));
       vnu[k] = tou4(ld16(rs.qkv, off + 4 * D));
     }
-    bf8_unpack(qu, q[k]);
+  }
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int k = 0; k < KU; ++k) {
+    bf8_unpack(qu[k], q[k]);
 #pragma unroll
     for (int t = 0; t < 8; ++t) { q[k][t] *= 0.125f; o[k][t] = 0.f; }
     m[k] = -INFINITY;
@@ -594,6 +617,7 @@ __device__ __forceinline__ void phase_attn(const Args& a, const Rs& rs, int l, c
       knu[k] = tou4(ld16(rs.qkv, off + 2 * D));
       vnu[k] = tou4(ld16(rs.qkv, off + 4 * D));
     }
+    __builtin_amdgcn_sched_barrier(0);
   }
 #pragma unroll
   for (int k = 0; k < KU; ++k) {
@@ -634,10 +658,10 @@ __device__ __forceinline__ void phase_attn(const Args& a, const Rs& rs, int l, c
 // hid (K 3072) from the workspace in A-fragment order; wave v takes k-steps [v S, (v+1) S), its A
 // fragments in chunks of CH k-steps (NIF chunks in flight), each fragment load one contiguous
 // KiB, every fragment read by exactly one wave and multiplied into all NB column blocks
-template <int S, int CS, int RH, bool XB, int CH = 4, int NIF = 2>
+template <int S, int CS, int RH, bool XB, int CH = 4, int NIF = 2, typename Late = NoLate>
 __device__ __forceinline__ void phase_proj(const Args& a, const Rs& rs, __amdgpu_buffer_rsrc_t ra,
                                            int K, const float* bias, char* smem, int w, int h,
-                                           const bf16x8_t (&wb)[CS * S]) {
+                                           const bf16x8_t (&wb)[CS * S], Late late = Late()) {
   constexpr int NR = RM / RH, NRB = NR / 16, NB = CS, PN = 16 * CS, PQ = PN / 4;
   float* red = reinterpret_cast<float*>(smem);
   const int tid = otid(), lane = tid & 63, v = tid >> 6, r0 = h * NR;
@@ -668,6 +692,10 @@ __device__ __forceinline__ void phase_proj(const Args& a, const Rs& rs, __amdgpu
 #pragma unroll
       for (int rb = 0; rb < NRB; ++rb)
         if (c * CH + s < S) af[c][s * NRB + rb] = ld16(ra, aoff[rb] + 1024 * (c * CH + s));
+  late();
+  // keep the issued chunks in flight: without the scheduling barriers the compiler sank each
+  // fragment load to its MFMA under register pressure (one round trip per k-step)
+  __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
   for (int c = 0; c < NCH; ++c) {
 #pragma unroll
@@ -685,6 +713,7 @@ __device__ __forceinline__ void phase_proj(const Args& a, const Rs& rs, __amdgpu
         for (int rb = 0; rb < NRB; ++rb)
           if ((c + NIF) * CH + s < S)
             af[c + NIF][s * NRB + rb] = ld16(ra, aoff[rb] + 1024 * ((c + NIF) * CH + s));
+      __builtin_amdgcn_sched_barrier(0);
     }
   }
   put_partial<NB, PN, NRB>(red, v, 0, acc);
@@ -712,10 +741,10 @@ __device__ __forceinline__ float gelu_new_fast(float x) {
 }
 // wave v = (column group v / D_KP of 2 blocks, K part v % D_KP); FN = 64 CS columns per workgroup;
 // the D_KP partial slabs (65,536 B at every CS) alias the LN rows
-template <int CS, int RH, bool XB>
+template <int CS, int RH, bool XB, typename Late = NoLate>
 __device__ __forceinline__ void phase_fc(const Args& a, const Rs& rs, int l, char* smem,
                                          const int* s_tok, const int* s_pos, int w, int h,
-                                         const bf16x8_t (&wf)[2 * Geo<CS>::SD]) {
+                                         const bf16x8_t (&wf)[2 * Geo<CS>::SD], Late late = Late()) {
   using Gm = Geo<CS>;
   constexpr int NR = RM / RH, NRB = NR / 16, FN = Gm::FN, KP = Gm::D_KP, FQ = FN / 4;
   constexpr int NQD = NR * FQ / NT;                 // epilogue quads per thread (same column quad)
@@ -725,7 +754,7 @@ __device__ __forceinline__ void phase_fc(const Args& a, const Rs& rs, int l, cha
   const int tid = otid(), v = tid >> 6, cg = v / KP, kq = v % KP, r0 = h * NR;
   const int c = 4 * (tid % FQ);
   const float4 bb = *reinterpret_cast<const float4*>(a.bfc[l] + FN * w + c);
-  ln_rows<0, NR, XB>(a, rs, hs, s_tok, s_pos, w, nullptr, r0, Gm::GW);
+  ln_rows<0, NR, XB>(a, rs, hs, s_tok, s_pos, w, nullptr, r0, Gm::GW, late);
   lds_sync();
   f32x4_t acc[NRB][2];
   mma_lds<2, Gm::SD, NRB>(hs, 32 * Gm::SD * kq, wf, acc);
@@ -980,15 +1009,24 @@ __global__ __launch_bounds__(NT) void decode_persist_kernel(Args a) {
   // x SD), mlp.c_proj (CS blocks x 12)
   bf16x8_t wq[3 * Gm::SA], wp[CS * 3], wf[2 * Gm::SD], wm[CS * 12];
 #define V_ (otid() >> 6)
-#define LOAD_WQ(L_) load_w<3, Gm::SA, NTW>(a.wqkv[L_], D, Gm::QN * w + 48 * (V_ / Gm::A_KP), QKVN, \
-                                         32 * Gm::SA * (V_ % Gm::A_KP), wq)
+  // CS = 2: the big prefetches (c_attn, c_fc, mlp.c_proj: 72-96 VGPRs) are split around the
+  // barrier wait -- the first k-steps before it, the rest after -- so the polling wave's wait is
+  // not queued behind all of its own weight loads (vector loads return in order)
+  constexpr int SPL = CS == 1 ? 1 : 2;
+#define LOAD_WQ_H(L_, H_) load_w<3, Gm::SA, NTW, (H_) * Gm::SA / SPL, ((H_) + 1) * Gm::SA / SPL>( \
+      a.wqkv[L_], D, Gm::QN * w + 48 * (V_ / Gm::A_KP), QKVN, 32 * Gm::SA * (V_ % Gm::A_KP), wq)
+// c_attn: the first part before the barrier wait, the rest inside phase A (after the LN rows'
+// loads); at CS = 1 it is all before the wait
+#define LOAD_WQ(L_) LOAD_WQ_H(L_, 0)
   LOAD_WQ(0);
   for (;;) {
     bar.sb = (stamps != nullptr && step == stamp_step) ? stamps + (long)wg * 2 * DP_NB : nullptr;
     bar.n0 = bar.n;
     stamp(bar.sb, 2 * DP_NB - 1);   // step start
     for (int l = 0; l < NLY; ++l) {
-      phase_qkv<CS, RH, XB>(a, rs, l, smem, s_tok, s_pos, w, h, wq);
+      phase_qkv<CS, RH, XB>(a, rs, l, smem, s_tok, s_pos, w, h, wq, [&] {
+        if constexpr (SPL == 2) LOAD_WQ_H(l, 1);
+      });
       bar_arrive(bar);
       uint4 kr[KU][KC], vr[KU][KC];
       attn_load<KU, KC, NTK>(a, l, s_pos, ub, 0, kr, vr);
@@ -999,8 +1037,9 @@ __global__ __launch_bounds__(NT) void decode_persist_kernel(Args a) {
 
       phase_attn<KU, KC, NTK>(a, rs, l, s_pos, ub, kr, vr);
       bar_arrive(bar);
-#define LOAD_WF load_w<2, Gm::SD, NTW>(a.wfc[l], D, Gm::FN * w + 32 * (V_ / Gm::D_KP), DFF, \
-                                     32 * Gm::SD * (V_ % Gm::D_KP), wf)
+#define LOAD_WF_H(H_) load_w<2, Gm::SD, NTW, (H_) * Gm::SD / SPL, ((H_) + 1) * Gm::SD / SPL>( \
+      a.wfc[l], D, Gm::FN * w + 32 * (V_ / Gm::D_KP), DFF, 32 * Gm::SD * (V_ % Gm::D_KP), wf)
+#define LOAD_WF LOAD_WF_H(0); if constexpr (SPL == 2) LOAD_WF_H(1)
       load_w<CS, 3, NTW>(a.wproj[l], D, Gm::PN * w, D, 96 * V_, wp);
       // c_fc's fragments: across phase C at CS = 1 (12 fragments); at CS = 2 (24) they wait for
       // C's barrier (held through C they spilled)
@@ -1009,18 +1048,23 @@ __global__ __launch_bounds__(NT) void decode_persist_kernel(Args a) {
 
       phase_proj<3, CS, RH, XB>(a, rs, rs.att, D, a.bproj[l], smem, w, h, wp);
       bar_arrive(bar);
-      if constexpr (CS != 1) LOAD_WF;
-#undef LOAD_WF
+      if constexpr (CS != 1) LOAD_WF_H(0);
       if (!bar_wait(bar, s_ok)) return gave_up(a);
 
-      phase_fc<CS, RH, XB>(a, rs, l, smem, s_tok, s_pos, w, h, wf);
+      phase_fc<CS, RH, XB>(a, rs, l, smem, s_tok, s_pos, w, h, wf, [&] {
+        if constexpr (CS != 1) LOAD_WF_H(1);
+      });
+#undef LOAD_WF
+#undef LOAD_WF_H
       bar_arrive(bar);
-      load_w<CS, 12, NTW>(a.wmp[l], DFF, Gm::PN * w, D, 384 * V_, wm);
+      load_w<CS, 12, NTW, 0, 12 / SPL>(a.wmp[l], DFF, Gm::PN * w, D, 384 * V_, wm);
       if (!bar_wait(bar, s_ok)) return gave_up(a);
 
       // CS = 2: 2-k-step chunks, 3 in flight (the 24 weight fragments leave fewer VGPRs)
       phase_proj<12, CS, RH, XB, (CS == 1 ? 4 : 2), (CS == 1 ? 2 : 3)>(
-          a, rs, rs.hid, DFF, a.bmp[l], smem, w, h, wm);
+          a, rs, rs.hid, DFF, a.bmp[l], smem, w, h, wm, [&] {
+            if constexpr (SPL == 2) load_w<CS, 12, NTW, 6, 12>(a.wmp[l], DFF, Gm::PN * w, D, 384 * V_, wm);
+          });
       bar_arrive(bar);
       // next block's c_attn.  Unconditional (a conditional load keeps the old wq live through
       // the whole block for the path that skips it); after block 11 the value is dead and wq is
@@ -1086,6 +1130,7 @@ __global__ __launch_bounds__(NT) void decode_persist_kernel(Args a) {
   }
 }
 #undef LOAD_WQ
+#undef LOAD_WQ_H
 #undef V_
 
 }  // namespace dpk

@@ -241,8 +241,11 @@ def persist_shapes(env: Optional[str] = None) -> List[Tuple[int, int]]:
     return sorted(set(shapes), key=lambda sh: -ops.decode_persist_grid(sh[1], sh[0]))
 
 
-# largest grid first; the last is the throughput shape every batch can fall back to
-DEFAULT_PERSIST_SHAPES = "12,11"
+# largest grid first; the last is the throughput shape every batch can fall back to: 24
+# workgroups (col_split 2) cost ~30 % less CU time per decode step than 48 (tools/
+# persist_grid_bench.py), so up to CUs // 24 batches decode at once; a batch that begins when few
+# others wait gets a larger (faster) grid
+DEFAULT_PERSIST_SHAPES = "12,11,21"
 
 
 def choose_persist_shape(in_flight: int, to_begin: int, shapes: List[Tuple[int, int]],
