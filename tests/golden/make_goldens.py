@@ -23,7 +23,9 @@ Fixture list (reference call sites in brackets):
   variants.npz    ClapCaptionModel + sound-effect MLP, ClapCaptionCrossattention[_v2],
                   ClapCaptionPrefix: clap_to_gpt outputs and generate2 ids.
   c2_margin.npz   generate2 with the reference's top-1/top-2 logit margin at every generated
-  c2_margin_flat.npz  step, on smaller decoder weights (the bf16 id-parity check).
+  c2_margin_flat.npz  step, on smaller decoder weights (the bf16 id-parity check);
+  c2_gpt2init.npz     c2_gpt2init at GPT-2's own init scale.  "tolerance" adds to these and
+                  c1_greedy the reference's own bf16-vs-f32 logit error (bf16_ref_err*).
   mistral.npz     C5 Mistral decoder path: ClapCaption_Mistralai_prompt.clap_to_gpt
                   (caption_model.py:392-413) + LMmodel.generate(inputs_embeds, attention_mask=ones,
                   do_sample=False, max_length=60, eos/pad 2) as predict_mistralai_multilingual.py:
@@ -175,7 +177,11 @@ def _step_margins(model, pe, ids):
 # per clip) with step margins from ~0.01 to ~4 (logit std ~3); at GPT-2's own init scale 0.02
 # every caption collapses to one repeated token after a first step whose margin varies by clip
 MARGIN_GPT2_KW = {"c2_margin": dict(seed=7, std=0.05, emb_std=0.1, stop_boost=2.0),
-                  "c2_margin_flat": dict(seed=7, std=0.02, emb_std=0.1, stop_boost=2.0)}
+                  "c2_margin_flat": dict(seed=7, std=0.02, emb_std=0.1, stop_boost=2.0),
+                  # GPT-2's own init scale everywhere (blocks and embeddings 0.02, positions
+                  # 0.01): the regime of a trained model's small activations, where bf16 rounding
+                  # stays far below the logit margins at most steps
+                  "c2_gpt2init": dict(seed=11, std=0.02, emb_std=0.02, stop_boost=2.0)}
 
 
 def gen_margin(n_clips=32, entry_length=67, name="c2_margin"):
@@ -228,6 +234,53 @@ def gen_margin(n_clips=32, entry_length=67, name="c2_margin"):
           greedy_ids=greedy, greedy_len=greedy_len, margin=marg, logit_std=lstd,
           entry_length=np.int64(entry_length), gpt2_kw=np.array(
               [kw["seed"], kw["std"], kw["emb_std"], kw["stop_boost"]], np.float64))
+
+
+def gen_tolerance(names=("c1_greedy", "c2_margin", "c2_margin_flat", "c2_gpt2init")):
+    """The stated bf16 tolerance of each margin golden: the reference's OWN bf16 execution
+    (the same GPT2LMHeadModel cast to bfloat16, torch on the CPU) against its f32 execution,
+    teacher-forced over every golden clip's prompt + generated ids (the computation generate2
+    repeats each step, gpt2_prefix_eval.py:187-190).  Adds to the existing fixture (ids and
+    margins unchanged):
+      bf16_ref_err        max |logit_bf16 - logit_f32| of the first generated step over the clips
+      bf16_ref_err_steps  [B, L] the same per generated step
+    tests/test_gpu_idparity.py derives its fixed margin threshold from bf16_ref_err and asserts
+    the GPU's bf16 first-step error against it."""
+    import copy
+    from models.caption_model import ClapCaption_prompt
+    sys.path.insert(0, os.path.join(REPO, "tools"))
+    import idparity
+    for name in names:
+        path = os.path.join(HERE, name + ".npz")
+        g = dict(np.load(path))
+        sd = S.gpt2_state_dict(**idparity.golden_gpt2_kw(g))
+        sd.update(S.mlp_mapper_state_dict(1))
+        model = ClapCaption_prompt(10, clip_length=10, prefix_size=1024, num_layers=8,
+                                   mapping_type="mlp", only_prefix=False, only_soft_prompt=False)
+        model.load_state_dict(sd, strict=False)
+        model.eval()
+        m16 = copy.deepcopy(model.gpt).to(torch.bfloat16).eval()
+        emb = torch.from_numpy(g["clap_emb"])
+        B = emb.shape[0]
+        steps = np.zeros(g["greedy_ids"].shape, np.float32)
+        t0 = time.time()
+        for b in range(B):
+            e = torch.nn.functional.normalize(emb[b:b + 1], dim=-1)
+            hard = torch.from_numpy(g["hard_ids"][b, :g["hard_len"][b]]).long()[None]
+            ids = g["greedy_ids"][b, :g["greedy_len"][b]].tolist()
+            with torch.no_grad():
+                pe, _ = model.clap_to_gpt(e.unsqueeze(0), model.gpt.transformer.wte(hard))
+                seq = torch.cat([pe, model.gpt.transformer.wte(torch.tensor([ids[:-1]]))], 1) \
+                    if len(ids) > 1 else pe
+                l32 = model.gpt(inputs_embeds=seq).logits[0, pe.shape[1] - 1:]
+                assert torch.equal(l32.argmax(-1), torch.tensor(ids)), f"{name} clip {b}"
+                l16 = m16(inputs_embeds=seq.to(torch.bfloat16)).logits[0, pe.shape[1] - 1:].float()
+            steps[b, :len(ids)] = (l16 - l32).abs().max(-1).values.numpy()
+        g["bf16_ref_err_steps"] = steps
+        g["bf16_ref_err"] = np.float32(steps[:, 0].max())
+        _save(name + ".npz", **g)
+        print(f"  {name}: bf16 reference error first step {float(g['bf16_ref_err']):.4f}, all steps "
+              f"max {float(steps.max()):.4f} ({time.time() - t0:.0f}s)", flush=True)
 
 
 VARIANTS = ("se_mlp", "xattn", "xattn_v2", "prefix")
@@ -565,6 +618,7 @@ def gen_mistral(n_clips=6):
 ALL = {"prompt": gen_prompt, "mappers": gen_mappers, "htsat": gen_htsat, "cnn14": gen_cnn14,
        "beam": gen_beam, "c1": gen_c1, "keys": gen_keys,
        "margin": gen_margin, "margin_flat": lambda: gen_margin(name="c2_margin_flat"),
+       "gpt2init": lambda: gen_margin(name="c2_gpt2init"), "tolerance": gen_tolerance,
        "variants": gen_variants, "magic": gen_magic, "temperature": gen_temperature,
        "mistral": gen_mistral}
 

@@ -128,13 +128,19 @@ def test_persist_grid_shapes(cuda, flat, B):
     from tools import idparity
     emb = torch.from_numpy(flat["clap_emb"]).to(cuda)
     emb = torch.cat([emb, emb])[:B]           # 64: the golden's 32 clips twice (a full batch)
+    from zsaac._lib import call
     res = {}
-    for cs, rs in ((1, 1), (1, 2), (2, 1), (2, 2)):
+    # fuse 1: the MLP as phases D' + R (mlp.c_proj partial sums, zs_tune_set dp_fuse)
+    for cs, rs, fuse in ((1, 1, 0), (1, 2, 0), (2, 1, 0), (2, 2, 0), (1, 1, 1), (2, 1, 1)):
         p = _pipe(flat, cuda, True, batch=B)
         p.decoder.persist_row_split, p.decoder.persist_col_split = rs, cs
-        out = p.caption_emb(emb)
-        res[cs, rs] = (out.captions(), _state(p, B), p.decoder.step_ctr.item())
-    base = res[1, 1]
+        call("zs_tune_set", b"dp_fuse", fuse)
+        try:
+            out = p.caption_emb(emb)
+        finally:
+            call("zs_tune_set", b"dp_fuse", 0)
+        res[cs, rs, fuse] = (out.captions(), _state(p, B), p.decoder.step_ctr.item())
+    base = res[1, 1, 0]
     for shape, r in res.items():
         assert r[0] == base[0], shape
         for k in base[1]:
@@ -169,3 +175,35 @@ def test_persist_give_up_resumes_stepwise(cuda, flat):
     finally:
         call("zs_tune_set", b"dp_spin", 0)
     assert p.caption_emb(emb).captions() == ref
+
+
+def test_concurrent_runner_bf16_persist(cuda, flat):
+    """The headline's arrangement: bf16 batches through ConcurrentRunner (10 pipelines, persistent
+    grids of every shape -- 96 / 48 / 24 workgroups, chosen per batch by choose_persist_shape --
+    several in flight, ragged batches included): every batch's ids equal the single-stream
+    persistent run's and the reference's (c2_margin_flat, exact on every clip)."""
+    from tools import idparity
+    from zsaac.pipeline import ConcurrentRunner, persist_shapes
+    emb = torch.from_numpy(flat["clap_emb"]).to(cuda)
+    ref = [flat["greedy_ids"][b, :flat["greedy_len"][b]].tolist() for b in range(emb.shape[0])]
+    p = _pipe(flat, cuda, True)
+    single = p.caption_emb(emb).captions()
+    assert single == ref
+    runner = ConcurrentRunner(p, 10, shapes=persist_shapes("12,11,21"))
+    assert runner.n_inflight == 10
+    runner.warmup_emb(emb)
+    used = set()
+    for sizes in ([32] * 6 + [7, 3], [32, 21]):
+        batches, want = [], []
+        for i, n in enumerate(sizes):
+            rows = [(5 * i + j) % 32 for j in range(n)]
+            batches.append(emb[rows])
+            want.append([ref[r] for r in rows])
+        outs = runner.run(batches, inputs="emb")
+        for i, o in enumerate(outs):
+            assert o.captions() == want[i], (sizes, i, runner.shape[i])
+            assert int(o.lengths.shape[0]) == sizes[i]
+        used |= set(runner.shape[:len(sizes)])
+        assert all(s >= 2 for s in runner.decode_steps[:len(sizes)])
+    assert {(1, 2), (1, 1), (2, 1)} <= used, used
+    assert sum(q.decoder.gave_up for q in runner.pipes) == 0

@@ -124,3 +124,25 @@ def test_beam_temperature_oracle(golden, csd, tag, T):
     assert outs == ref
     ids = C.generate2(pe, csd, entry_length=int(g["entry_length"]), use_cache=True, temperature=0.7)
     assert ids == g["greedy_t07_ids"][c, :g["greedy_t07_len"][c]].tolist()
+
+
+@pytest.mark.parametrize("name,clip", [("c2_gpt2init", 0), ("c2_gpt2init", 5), ("c2_margin_flat", 2)])
+def test_margin_golden_greedy_kv_oracle(golden, name, clip):
+    """The margin goldens (incl. c2_gpt2init, GPT-2's init scale): the oracle's KV-cache greedy
+    reproduces the reference's ids, and the stored bf16 tolerance is a positive logit error below
+    the reference's median step margin (tools/idparity.py margin_gate)."""
+    from oracle import caption as C
+    from tools import idparity
+    g = golden(name + ".npz")
+    sd = S.gpt2_state_dict(**idparity.golden_gpt2_kw(g))
+    sd.update(S.mlp_mapper_state_dict(1))
+    n = int(g["hard_len"][clip])
+    hard = torch.from_numpy(g["hard_ids"][clip:clip + 1, :n])
+    pre = torch.nn.functional.normalize(torch.from_numpy(g["clap_emb"][clip:clip + 1]), dim=-1)[None]
+    with torch.no_grad():
+        pe = C.clap_to_gpt(pre, hard, sd)
+    toks = C.generate2(pe, sd, entry_length=int(g["entry_length"]), use_cache=True)
+    assert toks == g["greedy_ids"][clip, :g["greedy_len"][clip]].tolist()
+    err = float(g["bf16_ref_err"])
+    m = g["margin"][g["margin"] > 0]
+    assert 0 < err < float(np.median(m)), (err, float(np.median(m)))

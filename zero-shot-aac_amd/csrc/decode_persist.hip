@@ -30,13 +30,16 @@
 //      greedy_step's bookkeeping to its LDS copy of (token, position, done); WG 0 writes the
 //      state / ids.  Rows past R compute garbage that is never stored.
 // Barriers: 5 per block + 1 after F = 61 per step (one monotonic agent-scope counter).
+#include <type_traits>
+
 #include "common.h"
 
 namespace zs {
 int g_dp_lmil = 1;   // zs_tune_set("dp_lmil", 0): LM-head vocab as one contiguous range per workgroup (A/B)
-int g_dp_nt = 2;   // zs_tune_set("dp_nt", 0): default-policy loads of the cached K/V (2: non-temporal).
-                   // nt weight / LM-head loads (round 3's bit 0) were slower: the concurrent grids
-                   // share the weights through L2 / MALL
+int g_dp_nt = 2;   // the cached K/V are read non-temporally (round 3 A/B); nt
+                   // weight / LM-head loads were slower: the concurrent grids share the weights
+                   // through L2 / MALL.  (kept for zs_tune_set compatibility; no other value)
+int g_dp_fuse = 0; // zs_tune_set("dp_fuse", 1): the MLP as D' + R (partial sums; measured slower)
 int g_dp_spin = 0; // zs_tune_set("dp_spin", n): give up a grid-barrier wait after n polls (0 = the
                    // default 2^22, < 0: at the first unmet poll); tests/test_gpu_persist.py forces
                    // the give-up path with it
@@ -82,7 +85,14 @@ constexpr int WS_QKV = WS_X + RM * D * 4;          // bf16 [64][2304]
 constexpr int WS_ATT = WS_QKV + RM * QKVN * 2;     // bf16 fragment-packed [4][24][64][8]
 constexpr int WS_HID = WS_ATT + RM * D * 2;        // bf16 fragment-packed [4][96][64][8]
 constexpr int WS_XB = WS_HID + RM * DFF * 2;       // bf16 [64][768]: x for the LayerNorms
-constexpr int WS_BYTES = WS_XB + RM * D * 2;
+// fused MLP (FUSE): each workgroup's mlp.c_proj partial sums over its own c_fc columns, in MFMA
+// accumulator-tile order [producer w'][row half h][column slice j][row block rb][block bi][64
+// lanes][4] (bf16, PART_BF16, or f32), read back by the slice's owner in phase R; sized for the
+// 48-workgroup grids (the 24-workgroup grid uses half)
+constexpr int PART_BF16 = 1;
+constexpr int PART_EB = PART_BF16 ? 8 : 16;       // bytes per lane per tile
+constexpr int WS_PART = WS_XB + RM * D * 2;
+constexpr int WS_BYTES = WS_PART + G * RM * D * (PART_BF16 ? 2 : 4);
 
 struct Args {
   int R, Lmax, max_steps, stop0, stop1, V, lm_il;
@@ -111,7 +121,7 @@ static_assert(NW * RM * 48 * 4 <= SM_HS, "QKV partial slabs fit the aliased row 
 
 // ------------------------------------------------------------------ memory helpers
 struct Rs {
-  __amdgpu_buffer_rsrc_t x, qkv, att, hid, xb;
+  __amdgpu_buffer_rsrc_t x, qkv, att, hid, xb, part;
 };
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t mk(char* p, int bytes) {
   return __builtin_amdgcn_make_buffer_rsrc(p, (short)0, bytes, 0x00020000);
@@ -119,6 +129,9 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t mk(char* p, int bytes) {
 // aux 16 = sc1: stores write through (no release fence needed), loads bypass this CU's L1
 __device__ __forceinline__ u32x4_t ld16(__amdgpu_buffer_rsrc_t r, int off) {
   return __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 16);
+}
+__device__ __forceinline__ u32x2_t ld8(__amdgpu_buffer_rsrc_t r, int off) {
+  return __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 16);
 }
 __device__ __forceinline__ unsigned ld4(__amdgpu_buffer_rsrc_t r, int off) {
   return __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 16);
@@ -205,6 +218,20 @@ __device__ __forceinline__ void load_w(const bf16_t* W, int K, int n0, int N, in
     const bf16_t* row = W + (long)min(n0 + 16 * nb + fr, N - 1) * K + kbase + fk;
 #pragma unroll
     for (int s = S0; s < S1; ++s)
+      b[nb * S + s] = ldg<NTL>(reinterpret_cast<const bf16x8_t*>(row + 32 * s));
+  }
+}
+
+// the blocks [NB0, NB1) of the NB x S fragments load_w would load (a prefetch split by blocks)
+template <int NB, int S, int NB0, int NB1, bool NTL = false>
+__device__ __forceinline__ void load_w_nb(const bf16_t* W, int K, int n0, int N, int kbase,
+                                          bf16x8_t (&b)[NB * S]) {
+  const int lane = otid() & 63, fr = lane & 15, fk = 8 * (lane >> 4);
+#pragma unroll
+  for (int nb = NB0; nb < NB1; ++nb) {
+    const bf16_t* row = W + (long)min(n0 + 16 * nb + fr, N - 1) * K + kbase + fk;
+#pragma unroll
+    for (int s = 0; s < S; ++s)
       b[nb * S + s] = ldg<NTL>(reinterpret_cast<const bf16x8_t*>(row + 32 * s));
   }
 }
@@ -779,6 +806,157 @@ __device__ __forceinline__ void phase_fc(const Args& a, const Rs& rs, int l, cha
   }
 }
 
+// ------------------------------------------------------------------ fused MLP: D' and R
+// D' (FUSE): ln_2 + c_fc + gelu_new as phase D, but the workgroup's FN hid columns stay in LDS
+// (hl [NR][FN + 8] bf16) and are multiplied at once by the matching FN columns of mlp.c_proj:
+// out[rows, 768] = gelu(h[:, FN w ..]) Wmp[:, FN w ..]^T, a K-slice partial of the MLP output that
+// the workgroup stores (bf16 tiles, write-through) for the 48 / CS column-slice owners to sum in
+// phase R.  Every hid byte then stays on its CU (the unfused E phase had every workgroup read the
+// whole 393 KB hid), and R reads 98 KB of partials instead.  mlp.c_proj per wave: columns 96 v ..
+// + 96 (6 blocks, two rounds of 3), K = FN (2 CS k-steps), no cross-wave reduction.
+template <int CS, int RH>
+__device__ __forceinline__ void put_part_tile(const Rs& rs, int w, int h, int rb, int cb,
+                                              const f32x4_t& acc) {
+  using Gm = Geo<CS>;
+  constexpr int NRB = RM / RH / 16;
+  const int lane = otid() & 63, j = cb / CS, bi = cb % CS;
+  const int off = (((((w * RH + h) * Gm::GW + j) * NRB + rb) * CS + bi) * 64 + lane) * PART_EB;
+  if constexpr (PART_BF16) st8(rs.part, off, u32x2_t{pk2bf(acc[0], acc[1]), pk2bf(acc[2], acc[3])});
+  else st16(rs.part, off, f42u(acc[0], acc[1], acc[2], acc[3]));
+}
+template <int CS, int RH, bool XB, typename Late1, typename Mid, typename Late2>
+__device__ __forceinline__ void phase_fc_fused(const Args& a, const Rs& rs, int l, char* smem,
+                                               const int* s_tok, const int* s_pos, int w, int h,
+                                               const bf16x8_t (&wf)[2 * Geo<CS>::SD],
+                                               bf16x8_t (&wm)[6 * 2 * CS], Late1 late1, Mid mid,
+                                               Late2 late2) {
+  using Gm = Geo<CS>;
+  constexpr int NR = RM / RH, NRB = NR / 16, FN = Gm::FN, KP = Gm::D_KP, FQ = FN / 4;
+  constexpr int NQD = NR * FQ / NT, KS = FN / 32, HL = FN + 8;
+  static_assert(NT % FQ == 0 && (NR * FQ) % NT == 0, "phase D epilogue mapping");
+  static_assert(KP * NR * FN * 4 + NR * HL * 2 <= SM_HS, "slabs + hid tile fit the row buffer");
+  bf16_t* hs = reinterpret_cast<bf16_t*>(smem);
+  float* red = reinterpret_cast<float*>(smem);
+  bf16_t* hl = reinterpret_cast<bf16_t*>(smem + KP * NR * FN * 4);
+  const int tid = otid(), lane = tid & 63, v = tid >> 6, cg = v / KP, kq = v % KP;
+  const int c = 4 * (tid % FQ);
+  const float4 bb = *reinterpret_cast<const float4*>(a.bfc[l] + FN * w + c);
+  ln_rows<0, NR, XB>(a, rs, hs, s_tok, s_pos, w, nullptr, h * NR, Gm::GW, late1);
+  lds_sync();
+  mid();               // loads after the LN (its row values are dead)
+  f32x4_t acc[NRB][2];
+  mma_lds<2, Gm::SD, NRB>(hs, 32 * Gm::SD * kq, wf, acc);
+  late2();             // loads after c_fc's MFMAs (its fragments are dead)
+  lds_sync();
+  put_partial<2, FN, NRB>(red, kq, 32 * cg, acc);
+  lds_sync();
+#pragma unroll
+  for (int hq = 0; hq < NQD; ++hq) {
+    const int rl = tid / FQ + (NT / FQ) * hq;
+    float4 sm = *reinterpret_cast<const float4*>(red + rl * FN + c);
+#pragma unroll
+    for (int k = 1; k < KP; ++k) {
+      const float4 p = *reinterpret_cast<const float4*>(red + (k * NR + rl) * FN + c);
+      sm.x += p.x; sm.y += p.y; sm.z += p.z; sm.w += p.w;
+    }
+    *reinterpret_cast<uint2*>(hl + rl * HL + c) =
+        make_uint2(pk2bf(gelu_new_fast(sm.x + bb.x), gelu_new_fast(sm.y + bb.y)),
+                   pk2bf(gelu_new_fast(sm.z + bb.z), gelu_new_fast(sm.w + bb.w)));
+  }
+  lds_sync();
+  // mlp.c_proj partial: A = the hid tile (LDS), B = wm (blocks 6 v + 3 nh + nb, k-steps s)
+  const int fr = lane & 15, fk = 8 * (lane >> 4);
+  bf16x8_t af[NRB][KS];
+#pragma unroll
+  for (int rb = 0; rb < NRB; ++rb)
+#pragma unroll
+    for (int s2 = 0; s2 < KS; ++s2)
+      af[rb][s2] = *reinterpret_cast<const bf16x8_t*>(hl + (16 * rb + fr) * HL + 32 * s2 + fk);
+#pragma unroll
+  for (int nh = 0; nh < 2; ++nh) {
+    f32x4_t o[NRB][3];
+#pragma unroll
+    for (int rb = 0; rb < NRB; ++rb)
+#pragma unroll
+      for (int nb = 0; nb < 3; ++nb) {
+        o[rb][nb] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s2 = 0; s2 < KS; ++s2) o[rb][nb] = mfma(af[rb][s2], wm[(3 * nh + nb) * KS + s2], o[rb][nb]);
+      }
+#pragma unroll
+    for (int rb = 0; rb < NRB; ++rb)
+#pragma unroll
+      for (int nb = 0; nb < 3; ++nb) put_part_tile<CS, RH>(rs, w, h, rb, 6 * v + 3 * nh + nb, o[rb][nb]);
+  }
+}
+
+// R (FUSE): the owner of column slice w (PN = 16 CS columns) sums the GW workgroups' partials of
+// its tiles in a fixed order (producers in GP groups of PPG, the groups in order), adds the bias
+// and the residual: x[:, PN w ..] (f32 and its bf16 copy), as phase E did.
+__device__ __forceinline__ void part_unpack(const u32x2_t& v, float (&f)[4]) {
+  f[0] = __uint_as_float(v.x << 16); f[1] = __uint_as_float(v.x & 0xffff0000u);
+  f[2] = __uint_as_float(v.y << 16); f[3] = __uint_as_float(v.y & 0xffff0000u);
+}
+__device__ __forceinline__ void part_unpack(const u32x4_t& v, float (&f)[4]) {
+  f[0] = __uint_as_float(v.x); f[1] = __uint_as_float(v.y);
+  f[2] = __uint_as_float(v.z); f[3] = __uint_as_float(v.w);
+}
+template <int CS, int RH, bool XB>
+__device__ __forceinline__ void phase_red(const Args& a, const Rs& rs, const float* bias, char* smem,
+                                          int w, int h) {
+  using Gm = Geo<CS>;
+  constexpr int NR = RM / RH, NRB = NR / 16, PN = Gm::PN, PQ = PN / 4, GW = Gm::GW;
+  constexpr int UNITS = NRB * CS * 64, GP = NT / UNITS, PPG = GW / GP;
+  static_assert(NT % UNITS == 0 && GW % GP == 0, "phase R mapping");
+  float* red = reinterpret_cast<float*>(smem);
+  const int tid = otid(), r0 = h * NR;
+  const int u = tid % UNITS, g = tid / UNITS, lane = u & 63, t = u >> 6, rb = t / CS, bi = t % CS;
+  // epilogue operands first (as phase_proj)
+  const int erl = (tid / PQ) % NR, erow = r0 + erl, ec = PN * w + 4 * (tid % PQ);
+  float4 eb = make_float4(0.f, 0.f, 0.f, 0.f), ex = eb;
+  if (tid < PQ * NR) {
+    eb = *reinterpret_cast<const float4*>(bias + ec);
+    ex = u2f4(ld16(rs.x, (min(erow, a.R - 1) * D + ec) * 4));
+  }
+  typedef std::conditional_t<PART_BF16 != 0, u32x2_t, u32x4_t> pv_t;
+  pv_t pv[PPG];
+#pragma unroll
+  for (int i = 0; i < PPG; ++i) {
+    const int wp = g * PPG + i;
+    const int off = (((((wp * RH + h) * GW + w) * NRB + rb) * CS + bi) * 64 + lane) * PART_EB;
+    if constexpr (PART_BF16) pv[i] = ld8(rs.part, off);
+    else pv[i] = ld16(rs.part, off);
+  }
+  __builtin_amdgcn_sched_barrier(0);
+  float sm[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int i = 0; i < PPG; ++i) {
+    float f[4];
+    part_unpack(pv[i], f);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) sm[e] += f[e];
+  }
+  // group sums -> slab g, rows (16 rb + 4 (lane / 16) + e), column 16 bi + lane % 16
+#pragma unroll
+  for (int e = 0; e < 4; ++e)
+    red[(g * NR + 16 * rb + 4 * (lane >> 4) + e) * PN + 16 * bi + (lane & 15)] = sm[e];
+  lds_sync();
+  if (tid < PQ * NR) {
+    float4 s4 = *reinterpret_cast<const float4*>(red + erl * PN + 4 * (tid % PQ));
+#pragma unroll
+    for (int k = 1; k < GP; ++k) {
+      const float4 p = *reinterpret_cast<const float4*>(red + (k * NR + erl) * PN + 4 * (tid % PQ));
+      s4.x += p.x; s4.y += p.y; s4.z += p.z; s4.w += p.w;
+    }
+    if (erow < a.R) {
+      const float4 o = make_float4(s4.x + eb.x + ex.x, s4.y + eb.y + ex.y, s4.z + eb.z + ex.z,
+                                   s4.w + eb.w + ex.w);
+      st16(rs.x, (erow * D + ec) * 4, f42u(o.x, o.y, o.z, o.w));
+      if constexpr (XB) st8(rs.xb, (erow * D + ec) * 2, u32x2_t{pk2bf(o.x, o.y), pk2bf(o.z, o.w)});
+    }
+  }
+}
+
 // ------------------------------------------------------------------ phase F: ln_f + LM head
 // vocab blocks of 16 rows [wg nvb / gg, (wg+1) nvb / gg) of this WG (gg = the grid), taken in PAIRS (one A fragment
 // read from LDS feeds the MFMAs of both blocks: half the LDS traffic per MFMA); wave v takes
@@ -958,8 +1136,9 @@ __device__ __forceinline__ void gave_up(const Args& a) {
 // XB: the LayerNorm inputs are handed off as a bf16 copy of x (written by phases C / E beside
 // the f32 residual stream), halving the bytes every workgroup reads in phases A, D and F.
 // NTM: non-temporal loads, bit 0 the weight / LM-head streams, bit 1 the cached K/V
-// CS: column slices per workgroup (Geo; grid = 48 / CS x RH workgroups)
-template <int CS, int RH, bool XB, int NTM = 0>
+// CS: column slices per workgroup (Geo; grid = 48 / CS x RH workgroups).  FUSE: the MLP as
+// phases D' + R (partial mlp.c_proj sums, no hid hand-off) instead of D + E
+template <int CS, int RH, bool XB, int NTM = 0, bool FUSE = false>
 __global__ __launch_bounds__(NT) void decode_persist_kernel(Args a) {
   using Gm = Geo<CS>;
   constexpr bool NTW = NTM & 1, NTK = (NTM >> 1) & 1;
@@ -981,6 +1160,7 @@ __global__ __launch_bounds__(NT) void decode_persist_kernel(Args a) {
   rs.att = mk(a.ws + WS_ATT, RM * D * 2);
   rs.hid = mk(a.ws + WS_HID, RM * DFF * 2);
   rs.xb = mk(a.ws + WS_XB, RM * D * 2);
+  rs.part = mk(a.ws + WS_PART, G * RM * D * (PART_BF16 ? 2 : 4));
   Bar bar{(gu32*)(a.ws + WS_SYNC), (gu32*)(a.ws + WS_SYNC + 4), 0, nullptr, 0, GG, a.spin_max};
   gu64* const lmkey = (gu64*)(a.ws + WS_LMKEY);
   unsigned long long* const stamps = dp_stamp_buf;
@@ -1007,7 +1187,7 @@ __global__ __launch_bounds__(NT) void decode_persist_kernel(Args a) {
   // weight fragments of this workgroup's column slices (each prefetched across the barrier
   // before its phase): c_attn (3 blocks x SA k-steps), attn.c_proj (CS blocks x 3), c_fc (2 blocks
   // x SD), mlp.c_proj (CS blocks x 12)
-  bf16x8_t wq[3 * Gm::SA], wp[CS * 3], wf[2 * Gm::SD], wm[CS * 12];
+  bf16x8_t wq[3 * Gm::SA], wp[CS * 3], wf[2 * Gm::SD], wm[FUSE ? 1 : CS * 12];
 #define V_ (otid() >> 6)
   // CS = 2: the big prefetches (c_attn, c_fc, mlp.c_proj: 72-96 VGPRs) are split around the
   // barrier wait -- the first k-steps before it, the rest after -- so the polling wave's wait is
@@ -1051,26 +1231,53 @@ __global__ __launch_bounds__(NT) void decode_persist_kernel(Args a) {
       if constexpr (CS != 1) LOAD_WF_H(0);
       if (!bar_wait(bar, s_ok)) return gave_up(a);
 
-      phase_fc<CS, RH, XB>(a, rs, l, smem, s_tok, s_pos, w, h, wf, [&] {
-        if constexpr (CS != 1) LOAD_WF_H(1);
-      });
+      if constexpr (FUSE) {
+        // D': c_fc + gelu + this workgroup's K-slice of mlp.c_proj (mlp.c_proj fragments: all with
+        // the LN rows' loads at CS = 1; at CS = 2 blocks 0-2 after the LN, 3-5 after c_fc's MFMAs)
+        bf16x8_t wmf[6 * 2 * CS];
+#define LOAD_WMF(B0_, B1_) load_w_nb<6, 2 * CS, B0_, B1_, NTW>(a.wmp[l], DFF, 96 * V_, D, Gm::FN * w, wmf)
+        phase_fc_fused<CS, RH, XB>(
+            a, rs, l, smem, s_tok, s_pos, w, h, wf, wmf,
+            [&] {
+              if constexpr (CS != 1) LOAD_WF_H(1);
+              else LOAD_WMF(0, 6);
+            },
+            [&] {
+              if constexpr (CS != 1) LOAD_WMF(0, 3);
+            },
+            [&] {
+              if constexpr (CS != 1) LOAD_WMF(3, 6);
+            });
+#undef LOAD_WMF
+        bar_arrive(bar);
+        // next block's c_attn (first part), across phase R (few registers there)
+        LOAD_WQ(l + 1 < NLY ? l + 1 : 0);
+        if (!bar_wait(bar, s_ok)) return gave_up(a);
+        phase_red<CS, RH, XB>(a, rs, a.bmp[l], smem, w, h);
+        bar_arrive(bar);
+        if (!bar_wait(bar, s_ok)) return gave_up(a);
+      } else {
+        phase_fc<CS, RH, XB>(a, rs, l, smem, s_tok, s_pos, w, h, wf, [&] {
+          if constexpr (CS != 1) LOAD_WF_H(1);
+        });
+        bar_arrive(bar);
+        load_w<CS, 12, NTW, 0, 12 / SPL>(a.wmp[l], DFF, Gm::PN * w, D, 384 * V_, wm);
+        if (!bar_wait(bar, s_ok)) return gave_up(a);
+
+        // CS = 2: 2-k-step chunks, 3 in flight (the 24 weight fragments leave fewer VGPRs)
+        phase_proj<12, CS, RH, XB, (CS == 1 ? 4 : 2), (CS == 1 ? 2 : 3)>(
+            a, rs, rs.hid, DFF, a.bmp[l], smem, w, h, wm, [&] {
+              if constexpr (SPL == 2) load_w<CS, 12, NTW, 6, 12>(a.wmp[l], DFF, Gm::PN * w, D, 384 * V_, wm);
+            });
+        bar_arrive(bar);
+        // next block's c_attn.  Unconditional (a conditional load keeps the old wq live through
+        // the whole block for the path that skips it); after block 11 the value is dead and wq is
+        // reloaded after the LM head, which needs the VGPRs
+        LOAD_WQ(l + 1 < NLY ? l + 1 : 0);
+        if (!bar_wait(bar, s_ok)) return gave_up(a);
+      }
 #undef LOAD_WF
 #undef LOAD_WF_H
-      bar_arrive(bar);
-      load_w<CS, 12, NTW, 0, 12 / SPL>(a.wmp[l], DFF, Gm::PN * w, D, 384 * V_, wm);
-      if (!bar_wait(bar, s_ok)) return gave_up(a);
-
-      // CS = 2: 2-k-step chunks, 3 in flight (the 24 weight fragments leave fewer VGPRs)
-      phase_proj<12, CS, RH, XB, (CS == 1 ? 4 : 2), (CS == 1 ? 2 : 3)>(
-          a, rs, rs.hid, DFF, a.bmp[l], smem, w, h, wm, [&] {
-            if constexpr (SPL == 2) load_w<CS, 12, NTW, 6, 12>(a.wmp[l], DFF, Gm::PN * w, D, 384 * V_, wm);
-          });
-      bar_arrive(bar);
-      // next block's c_attn.  Unconditional (a conditional load keeps the old wq live through
-      // the whole block for the path that skips it); after block 11 the value is dead and wq is
-      // reloaded after the LM head, which needs the VGPRs
-      LOAD_WQ(l + 1 < NLY ? l + 1 : 0);
-      if (!bar_wait(bar, s_ok)) return gave_up(a);
     }
     phase_lm<XB, NTW>(a, rs, smem, s_tok, s_pos, am_v, am_i, wg, GG, lmkey + (step & 1) * RM, s_lnf);
     bar_arrive(bar);
@@ -1189,10 +1396,10 @@ extern "C" int zs_gpt2_decode_persist(int R, int Lmax, int max_steps, int stop0,
   ZS_CHECK_HIP(hipMemsetAsync(ws, 0, WS_SYNC_BYTES, S(stream)));
 #define DP_LAUNCH(CS_, RH_)                                                                      \
   do {                                                                                           \
-    if (g_dp_nt) hipLaunchKernelGGL((decode_persist_kernel<CS_, RH_, true, 2>), dim3(grid),      \
-                                    dim3(NT), 0, S(stream), a);                                  \
-    else hipLaunchKernelGGL((decode_persist_kernel<CS_, RH_, true, 0>), dim3(grid), dim3(NT), 0, \
-                            S(stream), a);                                                       \
+    if (g_dp_fuse) hipLaunchKernelGGL((decode_persist_kernel<CS_, RH_, true, 2, true>),          \
+                                      dim3(grid), dim3(NT), 0, S(stream), a);                    \
+    else hipLaunchKernelGGL((decode_persist_kernel<CS_, RH_, true, 2, false>), dim3(grid),       \
+                            dim3(NT), 0, S(stream), a);                                          \
   } while (0)
   if (col_split == 1) {
     if (row_split == 1) DP_LAUNCH(1, 1);
