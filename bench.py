@@ -213,7 +213,7 @@ def split_batches(n, B, parts=0):
 
 
 def run_captions(args, world, rank, device, pipe, n_local, first, counts, inflight, warmup,
-                 parts=0, log_pass=False):
+                 parts=0, log_pass=False, reps=1):
     """Times the captioning of this rank's n_local clips (clip ids first..) in batches of
     pipe.cfg.batch (split_batches) on `inflight` streams, then the all-gather; returns (seconds
     max over ranks, outs, runner, info)."""
@@ -238,15 +238,18 @@ def run_captions(args, world, rank, device, pipe, n_local, first, counts, inflig
     torch.cuda.synchronize()
     cap0 = sum(p.decoder.n_captures for p in runner.pipes)
     rows0 = sum(p.decoder.rows_stepped for p in runner.pipes)
-    t0 = time.perf_counter()
-    outs = runner.run(batches)
-    if world > 1:
-        zd.collect_captions(outs, counts)
-    torch.cuda.synchronize()
-    if world > 1:
-        torch.distributed.barrier()
-    torch.cuda.synchronize()
-    dt = time.perf_counter() - t0
+    times = []
+    for _ in range(reps):          # reps > 1 (single-rank side measurements): the median
+        t0 = time.perf_counter()
+        outs = runner.run(batches)
+        if world > 1:
+            zd.collect_captions(outs, counts)
+        torch.cuda.synchronize()
+        if world > 1:
+            torch.distributed.barrier()
+        torch.cuda.synchronize()
+        times.append(time.perf_counter() - t0)
+    dt = sorted(times)[len(times) // 2]
     if world > 1:
         t = torch.tensor([dt], device=device, dtype=torch.float64)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
@@ -1031,16 +1034,19 @@ def strong_scaling_proxy(args, device, pipe, t_full, n_full, n_ranks=8):
     from zsaac import dist as zd
     full_src = "the headline's timed region"
     if t_full is None:
-        t_full = run_captions(args, 1, 0, device, pipe, n_full, 0, [n_full], args.inflight, 0)[0]
-        full_src = "a separate run of the full set (not the headline's timed region)"
+        t_full = run_captions(args, 1, 0, device, pipe, n_full, 0, [n_full], args.inflight, 3,
+                              reps=3)[0]
+        full_src = "a separate run of the full set (median of 3, not the headline's timed region)"
     lo, hi = zd.shard_range(n_full, 0, n_ranks)
     n = hi - lo
     out = {"clips_full": n_full, "seconds_full": round(t_full, 4), "full_timing": full_src,
            "ranks": n_ranks, "clips_per_rank": n}
     best = None
-    for name, parts in (("bs64_batches", 0), ("balanced_batches", args.inflight)):
+    # the reference's consecutive bs-64 batches (64 + 64 + 3), and the same number of batches
+    # balanced (44 + 44 + 43); each warmed up, the median of 5 runs
+    for name, parts in (("bs64_batches", 0), ("balanced_batches", -(-n // pipe.cfg.batch))):
         dt, outs, runner, _ = run_captions(args, 1, 0, device, pipe, n, lo, [n], args.inflight,
-                                           0, parts=parts)
+                                           3, parts=parts, reps=5)
         sizes = [int(o.ids.shape[0]) for o in outs]
         out[name] = {"seconds": round(dt, 4), "batches": sizes,
                      "grid_shapes": [f"cs{c}rs{r}" for c, r in getattr(runner, "shape", [])],

@@ -470,12 +470,12 @@ __device__ __forceinline__ void put_partial(float* red, int slab, int col0, cons
 // RH = 1: all 64 rows; RH = 2: the 32 rows of half h (row-split grid).  Wave v = (column group
 // v / A_KP of 3 blocks, K part v % A_KP); the A_KP partial slabs alias the LN rows (98,304 B at
 // every CS).
-template <int CS, int RH, bool XB, typename Late = NoLate>
+template <int CS, int RH, bool XB, int RB = 4, typename Late = NoLate>
 __device__ __forceinline__ void phase_qkv(const Args& a, const Rs& rs, int l, char* smem,
                                           const int* s_tok, const int* s_pos, int w, int h,
                                           const bf16x8_t (&wq)[3 * Geo<CS>::SA], Late late = Late()) {
   using Gm = Geo<CS>;
-  constexpr int NR = RM / RH, NRB = NR / 16, QN = Gm::QN, KP = Gm::A_KP, QQ = QN / 4;
+  constexpr int NR = 16 * RB / RH, NRB = NR / 16, QN = Gm::QN, KP = Gm::A_KP, QQ = QN / 4;
   constexpr int NQD = (NR * QQ + NT - 1) / NT;      // epilogue quads per thread
   bf16_t* hs = reinterpret_cast<bf16_t*>(smem);
   float* red = reinterpret_cast<float*>(smem);
@@ -685,11 +685,11 @@ __device__ __forceinline__ void phase_attn(const Args& a, const Rs& rs, int l, c
 // hid (K 3072) from the workspace in A-fragment order; wave v takes k-steps [v S, (v+1) S), its A
 // fragments in chunks of CH k-steps (NIF chunks in flight), each fragment load one contiguous
 // KiB, every fragment read by exactly one wave and multiplied into all NB column blocks
-template <int S, int CS, int RH, bool XB, int CH = 4, int NIF = 2, typename Late = NoLate>
+template <int S, int CS, int RH, bool XB, int RB = 4, int CH = 4, int NIF = 2, typename Late = NoLate>
 __device__ __forceinline__ void phase_proj(const Args& a, const Rs& rs, __amdgpu_buffer_rsrc_t ra,
                                            int K, const float* bias, char* smem, int w, int h,
                                            const bf16x8_t (&wb)[CS * S], Late late = Late()) {
-  constexpr int NR = RM / RH, NRB = NR / 16, NB = CS, PN = 16 * CS, PQ = PN / 4;
+  constexpr int NR = 16 * RB / RH, NRB = NR / 16, NB = CS, PN = 16 * CS, PQ = PN / 4;
   float* red = reinterpret_cast<float*>(smem);
   const int tid = otid(), lane = tid & 63, v = tid >> 6, r0 = h * NR;
   // epilogue operands first: NR rows x PQ quads on threads 0 .. PQ NR - 1 (two threads per
@@ -768,14 +768,15 @@ __device__ __forceinline__ float gelu_new_fast(float x) {
 }
 // wave v = (column group v / D_KP of 2 blocks, K part v % D_KP); FN = 64 CS columns per workgroup;
 // the D_KP partial slabs (65,536 B at every CS) alias the LN rows
-template <int CS, int RH, bool XB, typename Late = NoLate>
+template <int CS, int RH, bool XB, int RB = 4, typename Late = NoLate>
 __device__ __forceinline__ void phase_fc(const Args& a, const Rs& rs, int l, char* smem,
                                          const int* s_tok, const int* s_pos, int w, int h,
                                          const bf16x8_t (&wf)[2 * Geo<CS>::SD], Late late = Late()) {
   using Gm = Geo<CS>;
-  constexpr int NR = RM / RH, NRB = NR / 16, FN = Gm::FN, KP = Gm::D_KP, FQ = FN / 4;
-  constexpr int NQD = NR * FQ / NT;                 // epilogue quads per thread (same column quad)
-  static_assert(NT % FQ == 0 && (NR * FQ) % NT == 0, "phase D epilogue mapping");
+  constexpr int NR = 16 * RB / RH, NRB = NR / 16, FN = Gm::FN, KP = Gm::D_KP, FQ = FN / 4;
+  // epilogue quads per thread (same column quad); 16 rows x 16 quads leave half the threads idle
+  constexpr int NQD = (NR * FQ + NT - 1) / NT;
+  static_assert(NT % FQ == 0, "phase D epilogue mapping");
   bf16_t* hs = reinterpret_cast<bf16_t*>(smem);
   float* red = reinterpret_cast<float*>(smem);
   const int tid = otid(), v = tid >> 6, cg = v / KP, kq = v % KP, r0 = h * NR;
@@ -791,6 +792,7 @@ __device__ __forceinline__ void phase_fc(const Args& a, const Rs& rs, int l, cha
 #pragma unroll
   for (int hq = 0; hq < NQD; ++hq) {
     const int rl = tid / FQ + (NT / FQ) * hq, row = r0 + rl;
+    if (rl >= NR) break;
     float4 sm = *reinterpret_cast<const float4*>(red + rl * FN + c);
 #pragma unroll
     for (int k = 1; k < KP; ++k) {
@@ -1138,7 +1140,9 @@ __device__ __forceinline__ void gave_up(const Args& a) {
 // NTM: non-temporal loads, bit 0 the weight / LM-head streams, bit 1 the cached K/V
 // CS: column slices per workgroup (Geo; grid = 48 / CS x RH workgroups).  FUSE: the MLP as
 // phases D' + R (partial mlp.c_proj sums, no hid hand-off) instead of D + E
-template <int CS, int RH, bool XB, int NTM = 0, bool FUSE = false>
+// RB: row blocks of 16 the grid covers (4: all 64 rows; 2 for batches of <= 32 rows, whose
+// phases then read half of the handed-off activations)
+template <int CS, int RH, bool XB, int NTM = 0, bool FUSE = false, int RB = 4>
 __global__ __launch_bounds__(NT) void decode_persist_kernel(Args a) {
   using Gm = Geo<CS>;
   constexpr bool NTW = NTM & 1, NTK = (NTM >> 1) & 1;
@@ -1150,10 +1154,16 @@ __global__ __launch_bounds__(NT) void decode_persist_kernel(Args a) {
   int* s_done = s_pos + RM;
   int* s_misc = s_done + RM;     // [0] rows still decoding, [8] barrier ok flag
   constexpr int GW = Gm::GW, GG = GW * RH;
-  constexpr int KU = 2 * CS / RH, KC = KU > 2 ? 4 : 8;   // attention units per wave, keys per group
+  // attention units (row, head) per workgroup, per wave, the waves that have units, keys per group
+  constexpr int UPW = 4 * RB * CS / RH, KU = UPW >= 8 ? UPW / 8 : 1, AW = UPW / KU;
+  constexpr int KC = KU > 2 ? 4 : 8;
+  static_assert(AW <= NW && AW * KU == UPW, "attention units");
+  static_assert(!FUSE || RB == 4, "the fused MLP covers all 64 rows");
   const int wg = blockIdx.x;
   const int w = RH == 1 ? wg : (wg & 7) + 8 * (wg >> 4), h = RH == 1 ? 0 : (wg >> 3) & 1;
-  const int ub = (RM * NH / RH) * h + 8 * KU * w;        // first attention unit of this workgroup
+  const int ub = (16 * RB * NH / RH) * h + UPW * w;       // first attention unit of this workgroup
+  // (a scalar, provably wave-uniform condition; constant true when every wave has units)
+  const bool attn_wave = AW == NW || __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) < AW;
   Rs rs;
   rs.x = mk(a.ws + WS_X, RM * D * 4);
   rs.qkv = mk(a.ws + WS_QKV, RM * QKVN * 2);
@@ -1204,18 +1214,18 @@ __global__ __launch_bounds__(NT) void decode_persist_kernel(Args a) {
     bar.n0 = bar.n;
     stamp(bar.sb, 2 * DP_NB - 1);   // step start
     for (int l = 0; l < NLY; ++l) {
-      phase_qkv<CS, RH, XB>(a, rs, l, smem, s_tok, s_pos, w, h, wq, [&] {
+      phase_qkv<CS, RH, XB, RB>(a, rs, l, smem, s_tok, s_pos, w, h, wq, [&] {
         if constexpr (SPL == 2) LOAD_WQ_H(l, 1);
       });
       bar_arrive(bar);
       uint4 kr[KU][KC], vr[KU][KC];
-      attn_load<KU, KC, NTK>(a, l, s_pos, ub, 0, kr, vr);
+      if (attn_wave) attn_load<KU, KC, NTK>(a, l, s_pos, ub, 0, kr, vr);
       if (!bar_wait(bar, s_ok)) return gave_up(a);
       if (l == 0 && wg == 0 && otid() < RM)  // the previous step's argmax keys: every WG has read them
         __hip_atomic_store(lmkey + ((step + 1) & 1) * RM + otid(), 0ull, __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
 
-      phase_attn<KU, KC, NTK>(a, rs, l, s_pos, ub, kr, vr);
+      if (attn_wave) phase_attn<KU, KC, NTK>(a, rs, l, s_pos, ub, kr, vr);
       bar_arrive(bar);
 #define LOAD_WF_H(H_) load_w<2, Gm::SD, NTW, (H_) * Gm::SD / SPL, ((H_) + 1) * Gm::SD / SPL>( \
       a.wfc[l], D, Gm::FN * w + 32 * (V_ / Gm::D_KP), DFF, 32 * Gm::SD * (V_ % Gm::D_KP), wf)
@@ -1226,7 +1236,7 @@ __global__ __launch_bounds__(NT) void decode_persist_kernel(Args a) {
       if constexpr (CS == 1) LOAD_WF;
       if (!bar_wait(bar, s_ok)) return gave_up(a);
 
-      phase_proj<3, CS, RH, XB>(a, rs, rs.att, D, a.bproj[l], smem, w, h, wp);
+      phase_proj<3, CS, RH, XB, RB>(a, rs, rs.att, D, a.bproj[l], smem, w, h, wp);
       bar_arrive(bar);
       if constexpr (CS != 1) LOAD_WF_H(0);
       if (!bar_wait(bar, s_ok)) return gave_up(a);
@@ -1257,7 +1267,7 @@ __global__ __launch_bounds__(NT) void decode_persist_kernel(Args a) {
         bar_arrive(bar);
         if (!bar_wait(bar, s_ok)) return gave_up(a);
       } else {
-        phase_fc<CS, RH, XB>(a, rs, l, smem, s_tok, s_pos, w, h, wf, [&] {
+        phase_fc<CS, RH, XB, RB>(a, rs, l, smem, s_tok, s_pos, w, h, wf, [&] {
           if constexpr (CS != 1) LOAD_WF_H(1);
         });
         bar_arrive(bar);
@@ -1265,7 +1275,7 @@ __global__ __launch_bounds__(NT) void decode_persist_kernel(Args a) {
         if (!bar_wait(bar, s_ok)) return gave_up(a);
 
         // CS = 2: 2-k-step chunks, 3 in flight (the 24 weight fragments leave fewer VGPRs)
-        phase_proj<12, CS, RH, XB, (CS == 1 ? 4 : 2), (CS == 1 ? 2 : 3)>(
+        phase_proj<12, CS, RH, XB, RB, (CS == 1 ? 4 : 2), (CS == 1 ? 2 : 3)>(
             a, rs, rs.hid, DFF, a.bmp[l], smem, w, h, wm, [&] {
               if constexpr (SPL == 2) load_w<CS, 12, NTW, 6, 12>(a.wmp[l], DFF, Gm::PN * w, D, 384 * V_, wm);
             });
@@ -1360,6 +1370,10 @@ extern "C" int zs_gpt2_decode_persist(int R, int Lmax, int max_steps, int stop0,
              row_split);
   ZS_REQUIRE(col_split == 1 || col_split == 2, "zs_gpt2_decode_persist: col_split 1 or 2 (got %d)",
              col_split);
+  // batches of <= 32 rows: the grid covers 1 or 2 row blocks (row_split 2 would leave a half
+  // without rows; it is taken as 1, a grid no larger than the caller reserved)
+  const int rb = R <= 32 ? 2 : 4;     // (one row block, RB 1, spilled 59 VGPRs: not built)
+  if (rb < 4) row_split = 1;
   const int grid = G / col_split * row_split;
   ZS_REQUIRE(R >= 1 && R <= RM, "zs_gpt2_decode_persist: R in 1..%d (got %d)", RM, R);
   ZS_REQUIRE(V >= 32 * NW * grid && V <= 1 << 24, "zs_gpt2_decode_persist: vocab %d", V);
@@ -1394,21 +1408,24 @@ extern "C" int zs_gpt2_decode_persist(int R, int Lmax, int max_steps, int stop0,
   a.step_ctr = step_ctr; a.all_done = all_done; a.ws = (char*)ws;
   // the barrier counter and timeout word: zeroed before every launch (a memset node under capture)
   ZS_CHECK_HIP(hipMemsetAsync(ws, 0, WS_SYNC_BYTES, S(stream)));
+#define DP_K(CS_, RH_, FUSE_, RB_) decode_persist_kernel<CS_, RH_, true, 2, FUSE_, RB_>
+#define DP_GO(K_) hipLaunchKernelGGL((K_), dim3(grid), dim3(NT), 0, S(stream), a)
 #define DP_LAUNCH(CS_, RH_)                                                                      \
   do {                                                                                           \
-    if (g_dp_fuse) hipLaunchKernelGGL((decode_persist_kernel<CS_, RH_, true, 2, true>),          \
-                                      dim3(grid), dim3(NT), 0, S(stream), a);                    \
-    else hipLaunchKernelGGL((decode_persist_kernel<CS_, RH_, true, 2, false>), dim3(grid),       \
-                            dim3(NT), 0, S(stream), a);                                          \
+    if (rb == 2) DP_GO((DP_K(CS_, RH_, false, 2)));                                              \
+    else if (g_dp_fuse) DP_GO((DP_K(CS_, RH_, true, 4)));                                        \
+    else DP_GO((DP_K(CS_, RH_, false, 4)));                                                      \
   } while (0)
   if (col_split == 1) {
     if (row_split == 1) DP_LAUNCH(1, 1);
-    else DP_LAUNCH(1, 2);
+    else DP_GO((DP_K(1, 2, false, 4)));
   } else {
     if (row_split == 1) DP_LAUNCH(2, 1);
-    else DP_LAUNCH(2, 2);
+    else DP_GO((DP_K(2, 2, false, 4)));
   }
 #undef DP_LAUNCH
+#undef DP_GO
+#undef DP_K
   ZS_LAUNCH_CHECK();
   return 0;
 }
