@@ -438,7 +438,7 @@ def persist_launch_bytes(w_step, plen, steps, kv_row=12 * 2 * 768 * 2):
     return n * w_step + kv_row * (keys + len(plen) * n)
 
 
-PMC_PERSIST_FILE = os.path.join(ROOT, "profiles", "r3_pmc_persist.json")
+PMC_PERSIST_FILE = os.path.join(ROOT, "profiles", "r4", "pmc_persist_cs2.json")
 
 
 def shape_counts(runner):
@@ -1002,10 +1002,54 @@ def roofline_lmhead_beam(pipe, reps=20):
             "flops_per_launch": int(fl)}
 
 
+def roofline_c3_step(pipe, reps=20):
+    """C3's dominant kernels per beam decode step at its rows (256 clips x beam 5 = 1280):
+    the four decode GEMMs of a block as _layers issues them (qkv, attn.c_proj + residual, c_fc
+    + gelu_new, mlp.c_proj + residual; HIP events, back-to-back launches in one graph), their
+    MFMA fraction as sum(FLOP) / sum(time) over the 12 blocks, the decode attention's HBM
+    fraction (unique K / V bytes, cold caches: roofline_attention) and the LM head's MFMA
+    fraction (roofline_lmhead_beam); shares of the modelled step time."""
+    from zsaac import ops
+    dec, ly = pipe.decoder, pipe.gpt.layers[0]
+    R = pipe.cfg.batch * max(1, pipe.cfg.beam)
+    h, qkv, att, hid, x = dec.h[:R], dec.qkv[:R], dec.att[:R], dec.hid[:R], dec.x[:R]
+    shapes = {
+        "qkv": (lambda i: ops.gemm(h, ly["attn_w"], qkv, bias=ly["attn_b"], workspace=dec.ws), 3 * 768, 768),
+        "proj": (lambda i: ops.gemm(att, ly["proj_w"], x, bias=ly["proj_b"], residual=x,
+                                    workspace=dec.ws), 768, 768),
+        "fc": (lambda i: ops.gemm(h, ly["fc_w"], hid, bias=ly["fc_b"], act=ops.ACT_GELU_TANH,
+                                  workspace=dec.ws), 3072, 768),
+        "mproj": (lambda i: ops.gemm(hid, ly["mproj_w"], x, bias=ly["mproj_b"], residual=x,
+                                     workspace=dec.ws), 768, 3072),
+    }
+    gem, fl_tot, t_tot = {}, 0.0, 0.0
+    for name, (launch, N, K) in shapes.items():
+        avg = _graph_time(launch, reps)
+        fl = 2.0 * R * N * K
+        gem[name] = {"avg_us": round(avg * 1e6, 2), "tflops": round(fl / avg / 1e12, 1)}
+        fl_tot += fl
+        t_tot += avg
+    tf = fl_tot / t_tot / 1e12
+    attn = roofline_attention(pipe)
+    lm = roofline_lmhead_beam(pipe)
+    step = {"gemms": 12 * t_tot, "attention": 12 * attn["avg_launch_us"] * 1e-6,
+            "lm_head": lm["avg_launch_us"] * 1e-6}
+    tot = sum(step.values())
+    return {"decode_gemms": {"kernel": f"the 4 decode GEMMs of a block at M={R} (zs_gemm: lean "
+                                       f"bf16 MFMA tiles)", "bound": "mfma",
+                             "achieved": round(tf, 1), "peak": MFMA_BF16_PEAK_TFLOPS,
+                             "unit": "TFLOP/s", "frac": round(tf / MFMA_BF16_PEAK_TFLOPS, 4),
+                             "per_gemm": gem},
+            "decode_attention": attn, "lm_head": lm,
+            "step_share": {k: round(v / tot, 3) for k, v in step.items()},
+            "modelled_step_us": round(tot * 1e6, 1)}
+
+
 def c3_beam5(args, device, n_clips=1024, inflight=2):
     """C3 (BASELINE.json configs[2]): the same wav -> HTSAT -> MLP -> GPT-2 path with
     generate_beam (beam 5) on eval batches of 256 clips (1280 decode rows), 1024 synthetic clips,
-    `inflight` batches in flight; plus the MFMA roofline of its dominant GEMM (the LM head)."""
+    `inflight` batches in flight; plus the rooflines of its dominant kernels per decode step
+    (roofline_c3_step: the decode GEMMs' MFMA fraction, attention, LM head)."""
     import copy
     a3 = copy.copy(args)
     a3.beam, a3.batch, a3.group, a3.encoder_batch = 5, 256, 1, 0
@@ -1019,7 +1063,10 @@ def c3_beam5(args, device, n_clips=1024, inflight=2):
                                                    "beam 5, entry_length 67", "eval_batch": 256,
                                        "decode_rows_per_gemm": 1280,
                                        "steps_in_flight_per_gpu": inflight, **info},
-           "roofline": roofline_lmhead_beam(pipe)}
+           "roofline": None}
+    step = roofline_c3_step(pipe)
+    res["roofline"] = step["decode_gemms"]
+    res["roofline_step"] = step
     del runner, outs, pipe
     torch.cuda.synchronize()
     torch.cuda.empty_cache()
