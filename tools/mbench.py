@@ -101,6 +101,10 @@ def bench_gemm_c3():
         b = torch.randn(N, device=dev)
         out = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
         res = {"default": timeit(lambda: ops.gemm(a, w, out, bias=b, split_k=1))}
+        ws = torch.zeros(8 * M * N, device=dev)
+        for sk in (2, 3, 4, 6):               # split-K on the fast tiles + the reduce launch
+            if K % (32 * sk) == 0:
+                res[f"sk{sk}"] = timeit(lambda: ops.gemm(a, w, out, bias=b, split_k=sk, workspace=ws))
         for lt in (1, 2, 3, 5, 6, 8, 9, 10, 11, 12, 13):
             call("zs_tune_set", b"fast_tile", 100 + lt)
             try:
