@@ -95,7 +95,7 @@ def log(msg):
     print(f"[bench {time.time() - _T0:7.1f}s] {msg}", file=sys.stderr, flush=True)
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=None,
@@ -144,7 +144,7 @@ def parse():
     ap.add_argument("--embeddings-only", action="store_true",
                     help="C4: batched HTSAT/CNN14 encode_audio + one RCCL all-gather of the "
                          "[N,1024] embeddings (no caption decode)")
-    return ap.parse_args()
+    return ap.parse_args(argv)
 
 
 def dist_setup(args):

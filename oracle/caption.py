@@ -164,11 +164,18 @@ def generate2(embed: torch.Tensor, sd, entry_length=67, use_cache=False,
 
 
 def generate_beam(embed: torch.Tensor, sd, beam_size=5, entry_length=67,
-                  use_cache=False, temperature=1.0) -> Tuple[List[List[int]], List[float]]:
+                  use_cache=False, temperature=1.0,
+                  gaps: Optional[List[float]] = None) -> Tuple[List[List[int]], List[float]]:
     """generate_beam (gpt2_prefix_eval.py:99-158): logits / temperature (line 121, ``temperature
     if temperature > 0 else 1.0``), log(softmax) scores, stopped
     beams only extend with id 0 at zero cost, length-normalised top-k over beam x vocab, stop when
-    every beam has emitted 13.  Returns (token lists ordered best-first, their final scores)."""
+    every beam has emitted 13.  Returns (token lists ordered best-first, their final scores).
+
+    ``gaps`` (test instrumentation, not in the reference): when a list is given, every selection
+    appends the score gap between the last kept and the first dropped candidate (step 0: log-probs;
+    later steps: the length-normalised sums the top-k ranks), and the end appends the gap between
+    the best and second-best final scores -- the margins a perturbed search must clear to make the
+    same choices."""
     wte = sd["gpt.transformer.wte.weight"]
     tokens = None
     scores = None
@@ -186,6 +193,9 @@ def generate_beam(embed: torch.Tensor, sd, beam_size=5, entry_length=67,
                 logits, _ = gpt2_logits(generated, sd)
             logits = (logits[:, -1, :] / (temperature if temperature > 0 else 1.0)).softmax(-1).log()
             if scores is None:
+                if gaps is not None:
+                    v = logits[0].topk(beam_size + 1).values
+                    gaps.append(float(v[beam_size - 1] - v[beam_size]))
                 scores, next_tokens = logits.topk(beam_size, -1)
                 generated = generated.expand(beam_size, *generated.shape[1:])
                 if past is not None:
@@ -199,6 +209,9 @@ def generate_beam(embed: torch.Tensor, sd, beam_size=5, entry_length=67,
                 scores_sum = scores[:, None] + logits
                 seq_lengths[~is_stopped] += 1
                 avg = scores_sum / seq_lengths[:, None]
+                if gaps is not None:
+                    v = avg.view(-1).topk(beam_size + 1).values
+                    gaps.append(float(v[beam_size - 1] - v[beam_size]))
                 avg, next_tokens = avg.view(-1).topk(beam_size, -1)
                 src = next_tokens // scores_sum.shape[1]
                 seq_lengths = seq_lengths[src]
@@ -217,6 +230,8 @@ def generate_beam(embed: torch.Tensor, sd, beam_size=5, entry_length=67,
     scores = scores / seq_lengths
     outs = [tokens[i, :int(seq_lengths[i])].tolist() for i in range(beam_size)]
     order = scores.argsort(descending=True)
+    if gaps is not None:
+        gaps.append(float(scores[order[0]] - scores[order[1]]))
     return [outs[i] for i in order], [float(scores[i]) for i in order]
 
 

@@ -6,7 +6,20 @@
       is itself bit-exact to the reference goldens (test_gpu_parity.py).
   C3  beam 5 at batch 256 (1280 decode rows, beam kvrow indirection): f32 beams (ids and order)
       equal the oracle's generate_beam on 8 clips and the same clips decoded at batch 4; bf16
-      agreement with f32 reported with a floor.
+      beams pass the beam score rule against f32 (below) at the bench's weight scale and at
+      GPT-2's init scale.
+
+The beam score rule.  A beam search keeps, at every step, the top 5 of beam x vocab
+length-normalised scores; the gap between the 5th and 6th candidate is ~0.01 at most steps
+(oracle generate_beam(gaps=...)), so no bf16 execution can be required to reproduce f32's beam
+SETS -- the per-token margin rule of the greedy tests compares nothing here.  What a bf16 search
+must not do is lose quality: the f32 model's own length-normalised log-probability of the bf16
+best beam (teacher-forced rescoring by the oracle, the score generate_beam ranks by,
+gpt2_prefix_eval.py:150-156) may not fall more than tau_b below that of the f32 best beam.  With
+e = the measured bf16 first-step log-prob error, an EXACT maximiser of the bf16 score would end
+within 2e (S32(h16) >= S16(h16) - e >= S16(h32) - e >= S32(h32) - 2e); beam search is not exact,
+so tau_b = 4e (twice that bound; measured worst case at GPT-2's init scale 0.96 e,
+profiles/r4/c3_beam_rule.txt).  The exact-best-beam fraction is printed and floored.
 (C4's sharded embedding all-gather is covered on CPU/gloo by tests/test_dist.py.)
 """
 import numpy as np
@@ -136,6 +149,45 @@ def _beam_caps(csd, dtype, emb, beam):
     return out.beams()
 
 
+def _rescore(csd, pe, toks):
+    """f32 length-normalised log-probability of ``toks`` after prefix embedding ``pe`` (the
+    final score of gpt2_prefix_eval.py:150-156 for a beam ending with these ids)."""
+    from oracle import caption as OC
+    wte = csd["gpt.transformer.wte.weight"]
+    seq = torch.cat([pe, wte[toks[:-1]][None]], 1) if len(toks) > 1 else pe
+    with torch.no_grad():
+        lg, _ = OC.gpt2_logits(seq, csd)
+    lp = lg[0, pe.shape[1] - 1:].log_softmax(-1)
+    return float(lp[torch.arange(len(toks)), torch.tensor(toks)].mean())
+
+
+def _beam_score_rule(csd, emb, b16, b32, n, tau_b, label):
+    from oracle import caption as OC
+    from zsaac import synthetic as S
+    table, lt = S.label_table(), S.label_token_table()
+    diffs, exact = [], 0
+    for c in range(n):
+        e = emb[c:c + 1].cpu()
+        hard = torch.tensor([OC.prompt_ids(OC.sound_effect_choice(e, table, 3)[0].tolist(), lt)])
+        pe = OC.clap_to_gpt(torch.nn.functional.normalize(e, dim=-1)[None], hard, csd)
+        d = _rescore(csd, pe, b16[c][0]) - _rescore(csd, pe, b32[c][0])
+        diffs.append(d)
+        exact += b16[c][0] == b32[c][0]
+    worst = min(diffs)
+    print(f"{label} beam score rule: tau_b {tau_b:.4f}; f32 score of the bf16 best beam minus the "
+          f"f32 best beam's over {n} clips: min {worst:.4f} mean {sum(diffs) / n:.4f}; exact best "
+          f"beams {exact}/{n}")
+    assert worst >= -tau_b, (label, worst, tau_b, diffs)
+    return exact
+
+
+def _tau_b(csd, emb):
+    """4 e, e = max |log_softmax(bf16) - log_softmax(f32)| of the first generated step."""
+    l16 = _first_step_logits(_pipe(csd, None, torch.bfloat16, emb.shape[0]), emb)
+    l32 = _first_step_logits(_pipe(csd, None, torch.float32, emb.shape[0]), emb)
+    return 4.0 * float((l16.log_softmax(-1) - l32.log_softmax(-1)).abs().max())
+
+
 def test_c3_beam5_batch256(cuda, sds):
     from oracle import caption as OC
     from zsaac import synthetic as S
@@ -154,10 +206,26 @@ def test_c3_beam5_batch256(cuda, sds):
     # a clip's beams do not depend on the batch it shares (1280 rows vs 20 rows)
     small = _beam_caps(csd, torch.float32, emb[:4], beam)
     assert small == b32[:4]
-    # bf16 at 1280 rows: best-beam agreement with f32, reported with a floor
+    # bf16 at 1280 rows: the beam score rule against f32 on 64 clips (host rescoring)
     b16 = _beam_caps(csd, torch.bfloat16, emb, beam)
     lead = [_lead(b16[c][0], b32[c][0]) for c in range(C)]
     first = sum(b16[c][0][:1] == b32[c][0][:1] for c in range(C))
     print(f"C3 beam5 C=256 bf16 vs f32: best-beam first token {first}/{C}, leading tokens "
           f"{sum(lead)}/{sum(len(b32[c][0]) for c in range(C))}")
-    assert first >= C * 3 // 4
+    _beam_score_rule(csd, emb, b16, b32, 64, _tau_b(csd, emb[:64]), "C3 std-0.1")
+
+
+def test_c3_beam5_bf16_gpt2init(cuda):
+    """C3 at GPT-2's init scale (the c2_gpt2init golden's weights, bf16 error ~0.03): the beam
+    score rule on 64 of 256 clips decoded together (1280 rows), tau_b from the measured error."""
+    from zsaac import synthetic as S
+    csd = S.gpt2_state_dict(seed=11, std=0.02, emb_std=0.02, stop_boost=2.0)
+    csd.update(S.mlp_mapper_state_dict(1))
+    C, beam = 256, 5
+    emb = S.synthetic_clap_embeddings(C, seed=37).to(cuda)
+    b32 = _beam_caps(csd, torch.float32, emb, beam)
+    b16 = _beam_caps(csd, torch.bfloat16, emb, beam)
+    tau_b = _tau_b(csd, emb[:64])
+    assert tau_b < 0.2, tau_b
+    exact = _beam_score_rule(csd, emb, b16, b32, 64, tau_b, "C3 gpt2init")
+    assert exact >= 32, exact          # measured 47 / 64
