@@ -212,6 +212,20 @@ def split_batches(n, B, parts=0):
     return out
 
 
+_STREAMS = {}
+
+
+def run_streams(device, n):
+    """n dedicated HIP streams (distinct hardware queues), created once per process and shared by
+    every runner of this bench: a fresh set per runner would wrap past GPU_MAX_HW_QUEUES and put
+    a later runner's batches on shared queues (serialized)."""
+    from zsaac import ops
+    have = _STREAMS.setdefault(str(device), [])
+    if len(have) < n:
+        have += ops.dedicated_streams(n - len(have), device)
+    return have[:n]
+
+
 def run_captions(args, world, rank, device, pipe, n_local, first, counts, inflight, warmup,
                  parts=0, log_pass=False, reps=1):
     """Times the captioning of this rank's n_local clips (clip ids first..) in batches of
@@ -225,7 +239,8 @@ def run_captions(args, world, rank, device, pipe, n_local, first, counts, inflig
     log(f"{n_local} clips in {len(batches)} batches of <= {B}, {inflight} in flight: capturing")
     if len(batches) == 0:
         raise ValueError("no clips on this rank")
-    runner = ConcurrentRunner(pipe, max(1, inflight))
+    runner = ConcurrentRunner(pipe, max(1, inflight),
+                              streams=run_streams(device, max(1, inflight)))
     for size in sorted({b.shape[0] for b in batches}, reverse=True):   # captures every graph
         runner.warmup(next(b for b in batches if b.shape[0] == size))
         log(f"captured the decode graphs of {size}-clip batches")
