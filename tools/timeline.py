@@ -60,7 +60,10 @@ def main(d, out, first=8, n=17):
            "gap_before_launch_ms": {"mean": round(sum(gaps) / max(1, len(gaps)), 3),
                                     "max": round(max(gaps or [0]), 3), "n": len(gaps)},
            "other_kernels_ms_in_region": {k: round(v, 3) for k, v in top.items()},
-           "other_kernels_total_ms": round(sum(other.values()), 3)}
+           "other_kernels_total_ms": round(sum(other.values()), 3),
+           # every timed persistent launch: [start, end] ms from the region's start, its queue
+           "launches_ms": [[round((r[0] - t0) / 1e6, 2), round((r[1] - t0) / 1e6, 2), r[3]]
+                           for r in timed]}
     with open(out, "w") as f:
         json.dump(res, f, indent=1)
     print(json.dumps(res))
