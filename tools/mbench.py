@@ -148,6 +148,40 @@ def bench_gemm_htsat():
                   "  ".join(f"{k}={v:8.2f}us" for k, v in res.items()), flush=True)
 
 
+def bench_gemm_f32():
+    """The f32 parity mode's tiled GEMMs (HTSAT unfused at 64 clips + GPT-2 prefill at 64 x 27
+    rows): zs_gemm f32 vs torch.nn.functional.linear (hipBLASLt, exact f32), us and TF/s."""
+    from zsaac import ops
+    dev = torch.device("cuda", 0)
+    shapes = []
+    for C, T in ((96, 4096), (192, 1024), (384, 256), (768, 64)):
+        M = 64 * T
+        shapes += [(M, 3 * C, C, f"C{C} qkv"), (M, C, C, f"C{C} proj"), (M, 4 * C, C, f"C{C} fc1"),
+                   (M, C, 4 * C, f"C{C} fc2")]
+        if C < 768:
+            shapes.append((M // 4, 2 * C, 4 * C, f"C{C} merge"))
+    P = 64 * 27
+    shapes += [(P, 2304, 768, "pre qkv"), (P, 768, 768, "pre proj"), (P, 3072, 768, "pre fc"),
+               (P, 768, 3072, "pre mproj")]
+    tot = {"zs": 0.0, "torch": 0.0}
+    for M, N, K, name in shapes:
+        a = torch.randn(M, K, device=dev)
+        w = torch.randn(N, K, device=dev) * 0.02
+        b = torch.randn(N, device=dev)
+        out = torch.empty(M, N, device=dev)
+        r = {"zs": timeit(lambda: ops.gemm(a, w, out, bias=b, split_k=1), reps=10),
+             "torch": timeit(lambda: torch.nn.functional.linear(a, w, b), reps=10)}
+        for k in tot:
+            tot[k] += r[k] * (2 if not name.endswith("merge") and not name.startswith("pre") and
+                              not name.startswith("C768") else 1)
+        fl = 2 * M * N * K
+        gbs = (M * K + M * N + N * K) * 4 / r["zs"] / 1e3
+        print(f"{name:10s} M{M:7d} N{N:5d} K{K:5d}  " +
+              "  ".join(f"{k}={v:8.1f}us/{fl / v / 1e6:4.0f}TF" for k, v in r.items()) +
+              f"  zs {gbs:5.0f} GB/s", flush=True)
+    print(f"sum (HTSAT blocks x2 per stage except C768 x1... see shapes): {tot}", flush=True)
+
+
 def bench_gemm_dbg():
     """Where the fast GEMM's time goes: full / no-MFMA / no-DMA at a few encoder shapes."""
     from zsaac import ops
@@ -580,4 +614,4 @@ if __name__ == "__main__":
             call("zs_tune_set", k.encode(), int(v))
     which = sys.argv[1:] or ["gemm", "attn"]
     for wname in which:
-        {"gemm": bench_gemm, "rows": bench_rows, "gemm_m": bench_gemm_m, "gemm_c3": bench_gemm_c3, "gemm_htsat": bench_gemm_htsat, "gemm_dbg": bench_gemm_dbg, "lmhead": bench_lmhead, "overhead": bench_overhead, "front": bench_front, "window": bench_window, "decode_gemm": bench_decode_gemm, "attn": bench_attn, "attn_beam": bench_attn_beam, "gemm_big": bench_gemm_big, "inflight": bench_inflight, "buckets": bench_buckets, "compact_ab": bench_compact_ab, "host": bench_host}[wname]()
+        {"gemm": bench_gemm, "rows": bench_rows, "gemm_m": bench_gemm_m, "gemm_c3": bench_gemm_c3, "gemm_htsat": bench_gemm_htsat, "gemm_f32": bench_gemm_f32, "gemm_dbg": bench_gemm_dbg, "lmhead": bench_lmhead, "overhead": bench_overhead, "front": bench_front, "window": bench_window, "decode_gemm": bench_decode_gemm, "attn": bench_attn, "attn_beam": bench_attn_beam, "gemm_big": bench_gemm_big, "inflight": bench_inflight, "buckets": bench_buckets, "compact_ab": bench_compact_ab, "host": bench_host}[wname]()
