@@ -223,6 +223,44 @@ def test_gemm_ln(cuda, M, N):
     assert torch.equal(o1[0], out[0])
 
 
+@pytest.mark.parametrize("M,N,K", [(16384, 1152, 384), (65536, 192, 768), (1728, 2304, 768),
+                                   (4096, 384, 96), (8192, 96, 96), (300, 160, 96)])
+def test_gemm_f32_fast_tiles(cuda, M, N, K):
+    """The f32 GEMM on the LDS-DMA ring (gemm_fast_kernel F32: 128x128 / 128x64 / 64x128 / 64x64
+    tiles, ragged M / N) against the register-staged f32 kernel and fp64: exact on small integers
+    (any fragment / k-permutation slip shows), 2e-6 of the output scale on random data, with
+    bias + GELU + residual and a split-K slab reduction."""
+    from zsaac import ops
+    from zsaac._lib import call
+    g = torch.Generator(device="cuda").manual_seed(M + N + K)
+    ai = torch.randint(-3, 4, (M, K), device=cuda, generator=g).float()
+    wi = torch.randint(-3, 4, (N, K), device=cuda, generator=g).float()
+    out = torch.empty(M, N, device=cuda)
+    ops.gemm(ai, wi, out)
+    assert torch.equal(out, ai @ wi.t())
+    a = torch.randn(M, K, device=cuda, generator=g)
+    w = torch.randn(N, K, device=cuda, generator=g) / math.sqrt(K)
+    bias = torch.randn(N, device=cuda, generator=g)
+    res = torch.randn(M, N, device=cuda, generator=g)
+    ref = torch.nn.functional.gelu(a.double() @ w.double().t() + bias.double()) + res.double()
+    out = res.clone()
+    ops.gemm(a, w, out, bias=bias, act=ops.ACT_GELU_ERF, residual=out)
+    assert float((out.double() - ref).abs().max() / ref.abs().max()) < 2e-6
+    call("zs_tune_set", b"f32_fast", 0)
+    try:
+        old = res.clone()
+        ops.gemm(a, w, old, bias=bias, act=ops.ACT_GELU_ERF, residual=old)
+    finally:
+        call("zs_tune_set", b"f32_fast", 1)
+    assert float((out - old).abs().max() / old.abs().max()) < 2e-6
+    if K % 64 == 0:
+        ws = torch.empty(2 * M * N, device=cuda)
+        o2 = torch.empty(M, N, device=cuda)
+        ops.gemm(a, w, o2, bias=bias, split_k=2, workspace=ws)
+        ref2 = a.double() @ w.double().t() + bias.double()
+        assert float((o2.double() - ref2).abs().max() / ref2.abs().max()) < 2e-6
+
+
 def test_gemm_f32_exact_small_ints(cuda):
     """f32 mode with small integers is exact: catches any fragment/layout transposition."""
     from zsaac import ops

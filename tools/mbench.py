@@ -169,8 +169,16 @@ def bench_gemm_f32():
         w = torch.randn(N, K, device=dev) * 0.02
         b = torch.randn(N, device=dev)
         out = torch.empty(M, N, device=dev)
-        r = {"zs": timeit(lambda: ops.gemm(a, w, out, bias=b, split_k=1), reps=10),
-             "torch": timeit(lambda: torch.nn.functional.linear(a, w, b), reps=10)}
+        from zsaac._lib import call
+        r = {"zs": timeit(lambda: ops.gemm(a, w, out, bias=b, split_k=1), reps=10)}
+        ref = torch.nn.functional.linear(a.double(), w.double(), b.double())
+        err_new = float(((out.double() - ref).abs().max() / ref.abs().max()))
+        call("zs_tune_set", b"f32_fast", 0)
+        r["old"] = timeit(lambda: ops.gemm(a, w, out, bias=b, split_k=1), reps=10)
+        err_old = float(((out.double() - ref).abs().max() / ref.abs().max()))
+        call("zs_tune_set", b"f32_fast", 1)
+        r["torch"] = timeit(lambda: torch.nn.functional.linear(a, w, b), reps=10)
+        tot.setdefault("old", 0.0)
         for k in tot:
             tot[k] += r[k] * (2 if not name.endswith("merge") and not name.startswith("pre") and
                               not name.startswith("C768") else 1)
@@ -178,7 +186,7 @@ def bench_gemm_f32():
         gbs = (M * K + M * N + N * K) * 4 / r["zs"] / 1e3
         print(f"{name:10s} M{M:7d} N{N:5d} K{K:5d}  " +
               "  ".join(f"{k}={v:8.1f}us/{fl / v / 1e6:4.0f}TF" for k, v in r.items()) +
-              f"  zs {gbs:5.0f} GB/s", flush=True)
+              f"  zs {gbs:5.0f} GB/s  err new {err_new:.1e} old {err_old:.1e}", flush=True)
     print(f"sum (HTSAT blocks x2 per stage except C768 x1... see shapes): {tot}", flush=True)
 
 

@@ -170,13 +170,17 @@ __device__ __forceinline__ void epi_res_load(const GemmArgs& g, int mr0, int nc0
 // 32-row slab of its accumulators ([32][WN] f32, static register indexing), then re-reads it
 // row-wise so every lane owns 4 consecutive columns: bias / activation / residual / store move
 // 16 B (f32) or 8 B (bf16) per lane in full rows instead of 2-4 B column-strided scalars.
-template <int BM, int BN, int NS, int WGM, int WGN, int BK_>
+template <int BM, int BN, int NS, int WGM, int WGN, int BK_, bool F32 = false>
 // 4-wave tiles are held to 2 waves per SIMD (<= 256 unified VGPRs): two resident blocks per CU,
 // so one block's epilogue and DMA waits overlap the other's MFMAs (at 312 registers the 128x128
 // tile ran one block per CU)
+// F32 (the f32 parity mode): f32 A / W staged as bf16 rows of twice the length (KF = 2 bf16 units
+// per f32 element), consumed by v_mfma_f32_32x32x2f32 (fast_compute F32); same ring, tile order
+// and epilogue
 __global__ __launch_bounds__(64 * WGM * WGN,
                              (WGM * WGN == 4 && NS * FastTile<BM, BN, WGM, WGN, BK_>::STAGE <= 80 * 1024)
                                  ? 2 : 1) void gemm_fast_kernel(GemmArgs g) {
+  constexpr int KF = F32 ? 2 : 1;
   using FT = FastTile<BM, BN, WGM, WGN, BK_>;
   __shared__ __attribute__((aligned(16))) char lds[NS * FT::STAGE];
   constexpr int TM = FT::TM, TN = FT::TN, WN = FT::WN;
@@ -225,18 +229,18 @@ __global__ __launch_bounds__(64 * WGM * WGN,
   bool pre = false, xs = false;
   if (XPF && t < ntiles && g.dbg != 2 && g.dbg != 3) {
     const int kb = z * g.k_per_split;
-    fast_prologue<BM, BN, NS, WGM, WGN, BK_>(DenseRows{(const bf16_t*)g.A, g.lda, g.M, m0},
-                                             DenseRows{(const bf16_t*)g.W, g.ldw, g.N, n0}, kb,
-                                             min(g.K, kb + g.k_per_split), lds);
+    fast_prologue<BM, BN, NS, WGM, WGN, BK_>(DenseRows{(const bf16_t*)g.A, KF * g.lda, g.M, m0},
+                                             DenseRows{(const bf16_t*)g.W, KF * g.ldw, g.N, n0},
+                                             KF * kb, KF * min(g.K, kb + g.k_per_split), lds);
     pre = true;
   }
   for (; t < ntiles; t += gridDim.x) {
   const int kbeg = z * g.k_per_split, kend = min(g.K, kbeg + g.k_per_split);
   f32x16_t acc[TM][TN];
-  const DenseRows A{(const bf16_t*)g.A, g.lda, g.M, m0};
-  const DenseRows B{(const bf16_t*)g.W, g.ldw, g.N, n0};
-  fast_mainloop<BM, BN, NS, WGM, WGN, BK_, false, XS>(A, B, kbeg, kend, lds, acc, g.dbg, nullptr,
-                                                      pre, xs);   // ends with a barrier
+  const DenseRows A{(const bf16_t*)g.A, KF * g.lda, g.M, m0};
+  const DenseRows B{(const bf16_t*)g.W, KF * g.ldw, g.N, n0};
+  fast_mainloop<BM, BN, NS, WGM, WGN, BK_, false, XS, F32>(A, B, KF * kbeg, KF * kend, lds, acc,
+                                                           g.dbg, nullptr, pre, xs);   // ends with a barrier
   const int cm0 = m0, cn0 = n0, cz = z;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int wr0 = (wid / WGN) * FT::WM, wc0 = (wid % WGN) * WN;
@@ -268,9 +272,9 @@ __global__ __launch_bounds__(64 * WGM * WGN,
   if (XPF && t + (int)gridDim.x < ntiles && g.dbg != 2 && g.dbg != 3) {
     tile(t + gridDim.x, m0, n0, z);
     const int kb = z * g.k_per_split;
-    fast_prologue<BM, BN, NS, WGM, WGN, BK_>(DenseRows{(const bf16_t*)g.A, g.lda, g.M, m0},
-                                             DenseRows{(const bf16_t*)g.W, g.ldw, g.N, n0}, kb,
-                                             min(g.K, kb + g.k_per_split), lds);
+    fast_prologue<BM, BN, NS, WGM, WGN, BK_>(DenseRows{(const bf16_t*)g.A, KF * g.lda, g.M, m0},
+                                             DenseRows{(const bf16_t*)g.W, KF * g.ldw, g.N, n0},
+                                             KF * kb, KF * min(g.K, kb + g.k_per_split), lds);
     pre = true;
     xs = g.dbg != 4 && cm0 + BM <= g.M && cn0 + BN <= g.N;   // full tile: >= XS stores follow
   } else if (t + (int)gridDim.x < ntiles) {
@@ -649,14 +653,14 @@ static int launch_lean(GemmArgs& g, hipStream_t st) {
 
 int g_fast_persist = 1;   // zs_tune_set("fast_persist", 0): one workgroup per tile
 
-template <int BM, int BN, int NS, int WGM = 2, int WGN = 2, int BK_ = 64>
+template <int BM, int BN, int NS, int WGM = 2, int WGN = 2, int BK_ = 64, bool F32 = false>
 static int launch_fast(GemmArgs& g, hipStream_t st) {
   using FT = FastTile<BM, BN, WGM, WGN, BK_>;
   const long nt = (long)cdiv(g.N, BN) * cdiv(g.M, BM) * g.split_k;
   const int per_cu = max(1, min(160 * 1024 / (NS * FT::STAGE), 8 / FT::NW * 2));
   dim3 grid(g_fast_persist ? (int)std::min<long>(nt, 256L * per_cu) : (int)nt);
-  hipLaunchKernelGGL((gemm_fast_kernel<BM, BN, NS, WGM, WGN, BK_>), grid, dim3(64 * WGM * WGN), 0,
-                     st, g);
+  hipLaunchKernelGGL((gemm_fast_kernel<BM, BN, NS, WGM, WGN, BK_, F32>), grid,
+                     dim3(64 * WGM * WGN), 0, st, g);
   ZS_LAUNCH_CHECK();
   return 0;
 }
@@ -755,9 +759,25 @@ static int launch_gemm(GemmArgs& g, hipStream_t st) {
   return 0;
 }
 
+// f32 parity mode on the LDS-DMA ring (gemm_fast_kernel F32): 16 f32 k per stage, 4 stages
+// (3 in flight: ~2.6 us of k-loop at 0.85 us of f32 MFMA per stage) at 64 KiB, two blocks per CU.
+// Needs 16-byte rows (K, lda, ldw multiples of 4, aligned bases); else the register-staged
+// gemm_kernel<float>.
+int g_f32_fast = 1;    // zs_tune_set("f32_fast", 0): f32 GEMMs on the register-staged kernel
+static int dispatch_fast_f32(GemmArgs& g, hipStream_t st) {
+  if (nblocks(g, 128, 128) >= 256) return launch_fast<128, 128, 4, 2, 2, 32, true>(g, st);
+  if (nblocks(g, 128, 64) >= 256)
+    return g.M >= g.N ? launch_fast<128, 64, 4, 2, 2, 32, true>(g, st)
+                      : launch_fast<64, 128, 4, 2, 2, 32, true>(g, st);
+  return launch_fast<64, 64, 4, 2, 2, 32, true>(g, st);
+}
+
 template <typename T>
 static int dispatch_gemm(GemmArgs& g, hipStream_t st) {
   if (sizeof(T) == 2 && g_gemm_fast) return dispatch_fast(g, st);
+  if (sizeof(T) == 4 && g_f32_fast && g.K % 4 == 0 && g.lda % 4 == 0 && g.ldw % 4 == 0 &&
+      g.k_per_split % 4 == 0 && ((uintptr_t)g.A & 15) == 0 && ((uintptr_t)g.W & 15) == 0)
+    return dispatch_fast_f32(g, st);
   const bool small_m = g.M <= 64;
   const bool wide_n = g.N >= 2048 && !small_m;
   if (small_m) return wide_n ? launch_gemm<T, 64, 128>(g, st) : launch_gemm<T, 64, 64>(g, st);

@@ -84,7 +84,15 @@ __device__ __forceinline__ void fast_issue_t(const ASrc& A, const BSrc& B, int k
 // SSQ: also accumulate, per lane, the sum of squares of the B fragments it reads (row
 // wc0 + j*32 + (lane & 31), its half of every k-slice): with the xor-32 partner's sum that is
 // the squared norm of the B row — the LM head's get_prefix_tokens row norms for free
-template <int BM, int BN, int WGM, int WGN, int BK_, bool SSQ = false, bool PRIO = false>
+//
+// F32: the staged rows hold f32 (RB bytes = RB / 4 k per row; callers stage an f32 matrix as a
+// bf16 one of twice the leading dimension and twice the k range, so the DMA, the swizzle and the
+// ring are byte-for-byte the bf16 ones).  A 16-byte chunk is then 4 consecutive k, consumed by 4
+// v_mfma_f32_32x32x2f32 (exact f32 products, f32 accumulation): MFMA e of chunk pair s pairs
+// k = 4 (2s) + e (lane half 0) with k = 4 (2s + 1) + e (half 1), the same permutation of k on
+// the A and B sides.
+template <int BM, int BN, int WGM, int WGN, int BK_, bool SSQ = false, bool PRIO = false,
+          bool F32 = false>
 __device__ __forceinline__ void fast_compute(
     const char* stage,
     f32x16_t (&acc)[FastTile<BM, BN, WGM, WGN, BK_>::TM][FastTile<BM, BN, WGM, WGN, BK_>::TN],
@@ -92,6 +100,34 @@ __device__ __forceinline__ void fast_compute(
   using FT = FastTile<BM, BN, WGM, WGN, BK_>;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, r = lane & 31, h = lane >> 5;
   const int wr0 = (wid / WGN) * FT::WM, wc0 = BM + (wid % WGN) * FT::WN;
+  if constexpr (F32) {
+#pragma unroll
+    for (int s = 0; s < BK_ / 16; ++s) {
+      const int c = 2 * s + h;
+      float4 a[FT::TM], b[FT::TN];
+#pragma unroll
+      for (int i = 0; i < FT::TM; ++i) {
+        const int row = wr0 + i * 32 + r;
+        a[i] = *reinterpret_cast<const float4*>(stage + row * FT::RB + 16 * (c ^ FT::swz(row)));
+      }
+#pragma unroll
+      for (int j = 0; j < FT::TN; ++j) {
+        const int row = wc0 + j * 32 + r;
+        b[j] = *reinterpret_cast<const float4*>(stage + row * FT::RB + 16 * (c ^ FT::swz(row)));
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+#pragma unroll
+        for (int i = 0; i < FT::TM; ++i)
+#pragma unroll
+          for (int j = 0; j < FT::TN; ++j) {
+            const float av = e == 0 ? a[i].x : e == 1 ? a[i].y : e == 2 ? a[i].z : a[i].w;
+            const float bv = e == 0 ? b[j].x : e == 1 ? b[j].y : e == 2 ? b[j].z : b[j].w;
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc[i][j], 0, 0, 0);
+          }
+    }
+    return;
+  }
 #pragma unroll
   for (int s = 0; s < BK_ / 16; ++s) {
     const int c = 2 * s + h;
@@ -156,7 +192,7 @@ __device__ __forceinline__ void fast_prologue(const ASrc& A, const BSrc& B, int 
 // (MI355X_MICROARCH.md), so the waits for the prologue stages may leave those XS younger
 // operations in flight: the stores then drain under the next tile's first k-steps.
 template <int BM, int BN, int NS = 2, int WGM = 2, int WGN = 2, int BK_ = 64, bool SSQ = false,
-          int XS = 0, typename ASrc, typename BSrc>
+          int XS = 0, bool F32 = false, typename ASrc, typename BSrc>
 __device__ __forceinline__ void fast_mainloop(
     const ASrc& A, const BSrc& B, int kbeg, int kend, char* lds,
     f32x16_t (&acc)[FastTile<BM, BN, WGM, WGN, BK_>::TM][FastTile<BM, BN, WGM, WGN, BK_>::TN],
@@ -188,7 +224,7 @@ __device__ __forceinline__ void fast_mainloop(
       fast_issue_t<BM, BN, WGM, WGN, BK_>(A, B, kbeg + tn * BK_, kend, lds + sn * FT::STAGE);
     }
     if (dbg != 1 && dbg != 3)
-      fast_compute<BM, BN, WGM, WGN, BK_, SSQ>(lds + st * FT::STAGE, acc, ssq);
+      fast_compute<BM, BN, WGM, WGN, BK_, SSQ, false, F32>(lds + st * FT::STAGE, acc, ssq);
     st = st == NS - 1 ? 0 : st + 1;
   }
   __syncthreads();   // callers may reuse the LDS for the epilogue

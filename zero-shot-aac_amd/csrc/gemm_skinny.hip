@@ -236,6 +236,7 @@ __global__ __launch_bounds__(256) void gemm_skinny_kernel(SkinnyArgs g) {
 
 static int g_skinny_mode = 1;
 extern int g_gemm_fast;     // gemm.hip
+extern int g_f32_fast;      // gemm.hip
 extern int g_decode_attn5;  // attn.hip
 extern int g_window_mfma;   // attn.hip
 extern int g_fast_ns;       // gemm.hip
@@ -291,6 +292,7 @@ extern "C" int zs_tune_set(const char* key, int value) {
   if (!key) return ZS_ERR_ARG;
   if (!strcmp(key, "skinny_mode")) { g_skinny_mode = value; return 0; }
   if (!strcmp(key, "gemm_fast")) { g_gemm_fast = value; return 0; }
+  if (!strcmp(key, "f32_fast")) { g_f32_fast = value; return 0; }
   if (!strcmp(key, "decode_attn5")) { g_decode_attn5 = value; return 0; }
   if (!strcmp(key, "window_mfma")) { g_window_mfma = value; return 0; }
   if (!strcmp(key, "fast_ns")) { g_fast_ns = value; return 0; }
