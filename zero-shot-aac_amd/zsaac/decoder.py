@@ -556,7 +556,12 @@ class Gpt2Decoder:
     def greedy_begin(self, B: int):
         """Enqueue step 0 of generate2 from the prefill rows (no host sync); afterwards
         :meth:`step_chunk` advances ``chunk`` steps at a time."""
-        R = B
+        self.greedy_begin_device(B)
+        self.greedy_begin_host(B)
+
+    def greedy_begin_device(self, R: int):
+        """The device work of :meth:`greedy_begin` (LM head, step-0 bookkeeping): no host
+        state, so a pipeline can capture it in its begin graph."""
         ops.lmhead_topk(self.hf[:R], self.w.wte, 1, None, self.pval1, self.pidx1,
                         temperature=self.temperature)
         self.pos[:R].copy_(self.plen[:R] - 1)
@@ -565,6 +570,10 @@ class Gpt2Decoder:
         ops.greedy_step(self.pval1, self.pidx1, R, self.nblk, self.step_ctr, self.max_steps,
                         self.stop0, self.stop1, self.out_ids, self.out_len, self.done, self.pos,
                         self.next_tok, self.all_done)
+
+    def greedy_begin_host(self, R: int):
+        """The host state of :meth:`greedy_begin` and, for the persistent decode, its launch (a
+        grid shape chosen per batch by the runner: never captured)."""
         self._active = (("greedy", R, self.stop0, self.stop1, self.temperature),
                         lambda: self._greedy_step_body(R))
         self._cgreedy = R if (self.compact and R >= self.min_bucket) else None
