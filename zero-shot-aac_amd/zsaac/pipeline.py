@@ -138,8 +138,8 @@ class CaptionPipeline:
         self.prefix_ids = torch.zeros(B * self.Pmax, **i32)
         self.emb_buf = torch.empty(B, 1024, device=dev)
         # begin_wav's hipGraphs (per batch size) and their waveform staging buffer: private to
-        # each twin; ZSAAC_BEGIN_GRAPH=0 enqueues every begin eagerly
-        self.begin_graph = os.environ.get("ZSAAC_BEGIN_GRAPH", "1") != "0"
+        # each twin; ZSAAC_BEGIN_GRAPH=1 turns them on (off by default: measured slower)
+        self.begin_graph = os.environ.get("ZSAAC_BEGIN_GRAPH", "0") != "0"
         self._wav_stage = None
         self._bgraphs = {}
         self.begin_done = None       # event after the last begin's device work (begin graphs)
