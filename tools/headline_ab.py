@@ -66,13 +66,7 @@ def main():
     for rep in range(a.reps + 1):
         for name, r, kn in arms:
             for k, v in {**base, **kn}.items():
-                if k == "begin_graph":      # host-side knob: graph-replayed begins (pipeline.py)
-                    for p in r.pipes:
-                        p.begin_graph = bool(v)
-                elif k == "max_begins":     # host-side knob: begins on the GPU at once
-                    r.max_begins = v
-                else:
-                    _lib.call("zs_tune_set", k.encode(), v)
+                _lib.call("zs_tune_set", k.encode(), v)
             torch.cuda.synchronize()
             t0 = time.perf_counter()
             r.run(batches)

@@ -137,12 +137,6 @@ class CaptionPipeline:
         self.embed = torch.empty(B * self.Pmax, 768, device=dev)
         self.prefix_ids = torch.zeros(B * self.Pmax, **i32)
         self.emb_buf = torch.empty(B, 1024, device=dev)
-        # begin_wav's hipGraphs (per batch size) and their waveform staging buffer: private to
-        # each twin; ZSAAC_BEGIN_GRAPH=1 turns them on (off by default: measured slower)
-        self.begin_graph = os.environ.get("ZSAAC_BEGIN_GRAPH", "0") != "0"
-        self._wav_stage = None
-        self._bgraphs = {}
-        self.begin_done = None       # event after the last begin's device work (begin graphs)
 
     def _setup_tables(self, label_table, label_tokens):
         cfg, dev = self.cfg, self.dev
@@ -182,37 +176,7 @@ class CaptionPipeline:
 
     # ------------------------------------------------------------------ async (no host sync)
     def begin_wav(self, wav: torch.Tensor):
-        """encode + begin_emb.  Greedy: everything up to the decode launch replays as ONE hipGraph
-        per batch size (captured on first use, after an eager run): ~150 launches through the
-        C-ABI cost ~4 ms of host time per batch, longer than the GPU takes for them alone, and a
-        runner's single host thread refills its decode slots one begin at a time.  The waveforms
-        are copied into a staging buffer the graph reads (82 MB at 64 clips, ~30 us)."""
-        if not self.begin_graph or self.cfg.beam or self.encoder is None:
-            return self.begin_emb(self.encode(wav))
-        B = wav.shape[0]
-        if self._wav_stage is None:
-            self._wav_stage = torch.empty(self.cfg.batch, wav.shape[1], device=self.dev)
-        stage = self._wav_stage[:B]
-        stage.copy_(wav)
-        g = self._bgraphs.get(B)
-        if g is None:
-            emb = self._begin_device(stage)               # eager (the graph only records)
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):                     # (a side capture stream)
-                self._begin_device(stage)
-            self._bgraphs[B] = (g, emb)
-        else:
-            g[0].replay()
-            emb = g[1]
-        self._B, self._emb = B, emb
-        self.begin_done = torch.cuda.Event()
-        self.begin_done.record()
-        self.decoder.greedy_begin_host(B)
-
-    def _begin_device(self, wav: torch.Tensor) -> torch.Tensor:
-        emb = self.encode(wav)
-        self.begin_emb(emb, host=False)
-        return emb
+        self.begin_emb(self.encode(wav))
 
     def result(self) -> CaptionBatch:
         """Views of the current batch's outputs (valid until the next begin_*)."""
@@ -238,10 +202,9 @@ class CaptionPipeline:
         else:
             dec.prefix_tokens(self.embed[:B * Pmax], self.prefix_ids[:B * Pmax])
 
-    def begin_emb(self, emb: torch.Tensor, host: bool = True):
+    def begin_emb(self, emb: torch.Tensor):
         """Enqueue prompt assembly, mapper, prefill, get_prefix_tokens and decode step 0 for a
-        batch of CLAP embeddings, without any host synchronisation (host=False, greedy: the
-        device work only, for begin_wav's graph)."""
+        batch of CLAP embeddings, without any host synchronisation."""
         cfg, B, Pmax = self.cfg, emb.shape[0], self.Pmax
         self._B, self._emb = B, emb
         assert B <= cfg.batch
@@ -264,11 +227,7 @@ class CaptionPipeline:
             dec.beam_begin(B, cfg.beam)
         else:
             dec.prefill(B, Pmax)
-            dec.greedy_begin_device(B)
-            if host:
-                self.begin_done = torch.cuda.Event()
-                self.begin_done.record()
-                dec.greedy_begin_host(B)
+            dec.greedy_begin(B)
 
 
 def persist_shapes(env: Optional[str] = None) -> List[Tuple[int, int]]:
@@ -327,9 +286,6 @@ class ConcurrentRunner:
             g_min = ops.decode_persist_grid(self.shapes[-1][1], self.shapes[-1][0])
             n_inflight = max(1, min(n_inflight, self.cus // g_min))
         self.n_inflight = n_inflight
-        # at most this many begins (encode .. step 0) on the GPU at once (0: no limit): a new
-        # batch begins only when fewer earlier begins are still running
-        self.max_begins = int(os.environ.get("ZSAAC_MAX_BEGINS", "0"))
         self.pipes = [pipe] + [pipe.twin() for _ in range(n_inflight - 1)]
         # dedicated streams on distinct hardware queues: pooled torch streams take their queue at
         # first use and can end up sharing one, which serializes the batches
@@ -378,12 +334,6 @@ class ConcurrentRunner:
             for i, (p, s) in enumerate(zip(self.pipes, self.streams)):
                 st = active.get(i)
                 if st is None:
-                    if nxt < len(batches) and self.max_begins > 0:
-                        busy = sum(1 for j in active
-                                   if self.pipes[j].begin_done is not None
-                                   and not self.pipes[j].begin_done.query())
-                        if busy >= self.max_begins:
-                            continue
                     if nxt < len(batches):
                         if self.persist:
                             cs, rs = choose_persist_shape(sum(slots.values()), len(batches) - nxt,
