@@ -40,7 +40,8 @@ Rank 0 prints ONE JSON line.  Besides the contract fields (value = whole-job cli
   c3_beam5:          BASELINE configs[2] (beam 5, batch 256) with its LM head's MFMA roofline;
   throughput_mode:   the same path with 128 eval batches decoded per step (8192-row GEMMs) —
                      a different configuration, NOT the metric;
-  f32_parity_mode:   the bs-64 headline in f32 (the mode whose greedy ids are bit-exact);
+  f32_parity_mode:   the bs-64 headline (1045 clips) in f32 (the mode whose greedy ids are
+                     bit-exact);
   id_agreement:      greedy ids against the reference goldens (bf16 and f32), first divergence
                      and the reference's own top-2 logit margin there (tools/idparity.py);
   cpu_baseline:      the oracle (reference semantics: batch 1, full recompute, fp32) on bounded
@@ -1215,8 +1216,10 @@ def main():
         log("C3 beam 5")
         res["c3_beam5"] = c3_beam5(args, device)
         log("f32 parity mode")
-        res["f32_parity_mode"] = sub_run(args, device, torch.float32, 1, args.inflight, 6 * 64, 1)
-        res["f32_parity_mode"]["note"] = "bs=64 in f32: the mode whose greedy ids are bit-exact"
+        res["f32_parity_mode"] = sub_run(args, device, torch.float32, 1, args.inflight,
+                                         CLOTHO_EVAL_CLIPS, 1)
+        res["f32_parity_mode"]["note"] = ("the headline's 1045 clips at bs=64 in f32: the mode "
+                                          "whose greedy ids are bit-exact")
         log("id agreement")
         from tools import idparity
         res["id_agreement"] = {"bf16": idparity.summary(torch.bfloat16, device),
