@@ -13,22 +13,66 @@ namespace zs {
 constexpr int PB = 1024;   // threads per prompt / label-top-k block (4x the label rows in flight of 256)
 // sound_effect_choice (utils.py:131-137 / caption_model.py:15-20): the k labels of highest
 // similarity emb . label (softmax is monotone, so top-k of the raw similarities), best first,
-// ties to the lower label index; one block per row (PB threads: one label row per thread, so
-// the block keeps PB rows streaming at once), result in sel[0..k).
+// ties to the lower label index; one block per row (PB threads: each wave dots one label row at a
+// time with coalesced 16-byte loads, four rows in flight), result in sel[0..k).
 __device__ __forceinline__ void label_select(const float* __restrict__ emb, int D,
                                              const float* __restrict__ labels, int L, int k,
                                              float* e, float* sim, int* sel, float* rv, int* ri) {
   const int b = blockIdx.x;
   for (int d = threadIdx.x; d < D; d += PB) e[d] = emb[(long)b * D + d];
   __syncthreads();
-  for (int l = threadIdx.x; l < L; l += PB) {
-    const float* lr = labels + (long)l * D;
-    float s = 0.f;
-    for (int d = 0; d < D; ++d) s += e[d] * lr[d];
-    sim[l] = s;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if ((D & 3) == 0 && ((uintptr_t)labels & 15) == 0) {
+    // one label row per wave at a time, 16-byte coalesced loads (a 4 KB row is 4 wave loads),
+    // four rows in flight per wave, lane partials reduced across the wave
+    constexpr int NR = 4, NWV = PB / 64;
+    const float4* e4 = reinterpret_cast<const float4*>(e);
+    const int D4 = D >> 2;
+    for (int l0 = wid; l0 < L; l0 += NR * NWV) {
+      const float4* r[NR];
+#pragma unroll
+      for (int j = 0; j < NR; ++j)
+        r[j] = reinterpret_cast<const float4*>(labels + (long)min(l0 + j * NWV, L - 1) * D);
+      float sj[NR] = {};
+      if (D4 == 256) {                 // CLAP width 1024: every row chunk issued before any use
+        float4 a[4][NR];
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+          for (int j = 0; j < NR; ++j) a[u][j] = r[j][lane + 64 * u];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const float4 v = e4[lane + 64 * u];
+#pragma unroll
+          for (int j = 0; j < NR; ++j)
+            sj[j] += (a[u][j].x * v.x + a[u][j].y * v.y) + (a[u][j].z * v.z + a[u][j].w * v.w);
+        }
+      } else {
+        for (int c = lane; c < D4; c += 64) {
+          float4 a[NR];
+#pragma unroll
+          for (int j = 0; j < NR; ++j) a[j] = r[j][c];
+          const float4 v = e4[c];
+#pragma unroll
+          for (int j = 0; j < NR; ++j) sj[j] += (a[j].x * v.x + a[j].y * v.y) + (a[j].z * v.z + a[j].w * v.w);
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < NR; ++j) {
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) sj[j] += __shfl_xor(sj[j], o, 64);
+        if (lane == 0 && l0 + j * NWV < L) sim[l0 + j * NWV] = sj[j];
+      }
+    }
+  } else {
+    for (int l = threadIdx.x; l < L; l += PB) {
+      const float* lr = labels + (long)l * D;
+      float s = 0.f;
+      for (int d = 0; d < D; ++d) s += e[d] * lr[d];
+      sim[l] = s;
+    }
   }
   __syncthreads();
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   for (int q = 0; q < k; ++q) {
     float bv = -INFINITY;
     int bi = 0x7fffffff;
@@ -67,8 +111,17 @@ __global__ __launch_bounds__(PB) void prompt_kernel(const float* __restrict__ em
   __shared__ int sel[16];
   __shared__ float rv[PB / 64];
   __shared__ int ri[PB / 64];
+  __shared__ int stok[16 * 32], slen[16];
   const int b = blockIdx.x;
   label_select(emb, D, labels, L, k, sm, sm + D, sel, rv, ri);
+  // the chosen labels' token ids gathered in parallel (one load round trip, not one per token)
+  const int mt = min(max_tok, 32);
+  if (threadIdx.x < k * mt) {
+    const int q = threadIdx.x / mt, t = threadIdx.x % mt;
+    stok[q * 32 + t] = ltok[(long)sel[q] * max_tok + t];
+  }
+  if (threadIdx.x < k) slen[threadIdx.x] = llen[sel[threadIdx.x]];
+  __syncthreads();
   if (threadIdx.x == 0) {
     int* out = hard_ids + (long)b * h_cap;
     int n = 0;
@@ -79,7 +132,7 @@ __global__ __launch_bounds__(PB) void prompt_kernel(const float* __restrict__ em
     } else {
       for (int q = 0; q < k; ++q) {
         const int l = sel[q];
-        for (int t = 0; t < llen[l] && t < max_tok; ++t) put(ltok[(long)l * max_tok + t]);
+        for (int t = 0; t < slen[q] && t < mt; ++t) put(stok[q * 32 + t]);
         if (q + 1 < k) put(11);             // ","
         if (chosen) chosen[(long)b * k + q] = l;
       }
@@ -478,7 +531,7 @@ extern "C" int zs_prompt_assemble(const float* emb, int B, int D, const float* l
                                   int k, const int* label_tok, const int* label_len, int max_tok,
                                   int* hard_ids, int h_cap, int* hard_len, int* chosen,
                                   void* stream) {
-  ZS_REQUIRE(B > 0 && D > 0 && L > 0 && k >= 0 && k <= 16 && k <= L, "zs_prompt_assemble: bad shape");
+  ZS_REQUIRE(B > 0 && D > 0 && L > 0 && k >= 0 && k <= 16 && k <= L && max_tok <= 32, "zs_prompt_assemble: bad shape");
   const size_t smem = (size_t)(D + L) * sizeof(float);
   ZS_REQUIRE(smem <= 64 * 1024, "zs_prompt_assemble: D+L too large");
   hipLaunchKernelGGL(prompt_kernel, dim3(B), dim3(PB), smem, S(stream), emb, D, labels, L, k,
