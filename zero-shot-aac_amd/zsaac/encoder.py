@@ -21,8 +21,12 @@ from .frontend import tables_from_state_dict
 DEPTHS, HEADS, EMBED, WIN = (2, 2, 6, 2), (4, 8, 16, 32), 96, 8
 CNN14_CH = (64, 128, 256, 512, 1024, 2048)
 # stages whose blocks run as ONE fused kernel per block (zs_swin_block, bf16 only); the env var
-# ZSAAC_FUSED_SWIN (comma-separated channel widths, "" = none) overrides it for A/B runs
-FUSED_SWIN_C = tuple(int(c) for c in os.environ.get("ZSAAC_FUSED_SWIN", "96,192,384").split(",")
+# ZSAAC_FUSED_SWIN (comma-separated channel widths, "" = none) overrides it for A/B runs.
+# Stage 3 (C = 384) runs unfused: its fused kernel holds a whole CU per window (155 KB of LDS) at
+# ~17 % MFMA for 133 us, while the unfused block's 16384-row GEMMs are MFMA-efficient; beside the
+# decode grids CU time, not latency, is what a begin costs (headline A/B: fused 96,192,384
+# 6.32-6.46k, 96,192 6.70-6.88k, 96 6.63-6.66k, none 6.19-6.20k clips/s)
+FUSED_SWIN_C = tuple(int(c) for c in os.environ.get("ZSAAC_FUSED_SWIN", "96,192").split(",")
                      if c.strip())
 
 
