@@ -1,0 +1,29 @@
+#!/usr/bin/env python3
+"""C3 (beam 5, eval batches of 256) throughput at several in-flight depths (bench.py c3_beam5):
+    python tools/c3_probe.py [inflight=2,4] [clips=1024]"""
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "zero-shot-aac_amd"))
+import torch  # noqa: E402
+
+import bench  # noqa: E402
+
+os.environ["GPU_MAX_HW_QUEUES"] = "16"
+
+
+def main():
+    infl = [int(c) for c in (sys.argv[1] if len(sys.argv) > 1 else "2,4").split(",")]
+    n = int(sys.argv[2]) if len(sys.argv) > 2 else 1024
+    args = bench.parse([])
+    dev = torch.device("cuda", 0)
+    for k in infl:
+        r = bench.c3_beam5(args, dev, n, k)
+        print(json.dumps({"inflight": k, "clips": n, "value": r["value"]}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
