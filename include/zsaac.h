@@ -184,6 +184,16 @@ int zs_row_attention(const void* q, int ldq, const void* k, const void* v, int l
                      const int* len, int heads, int hd, int causal, float scale, void* out, int ldo,
                      int dtype, void* stream);
 
+/* zs_row_attention_kv: the GPT-2 prompt prefill's attention fused with its KV-cache write
+ * (gpt2_prefix_eval.py:99-158 via transformers GPT2Attention with use_cache; replaces the
+ * zs_kv_write + zs_row_attention pair of a layer): qkv [B*L][3*heads*64] bf16 (q | k | v, head
+ * dim 64), causal over j < len[b], L <= 32; out rows with ldo; k / v of all L rows stored into
+ * kc / vc [B*row_stride][heads][Lmax][64] at positions 0..L-1 exactly as zs_kv_write (pos0 NULL)
+ * stores them. */
+int zs_row_attention_kv(const void* qkv, int B, int L, const int* len, int heads, float scale,
+                        void* out, int ldo, void* kc, void* vc, int Lmax, int row_stride,
+                        void* stream);
+
 /* zs_cross_attention: nn.MultiheadAttention's core (after in_proj, before out_proj) for short
  * key sets: out(b, i, h) = softmax_j(scale * q(b,i,h) . k(b,j,h)) v(b,j,h), j < Lk; q rows
  * b*Lq + i (ldq), k / v rows b*Lk + j (ldkv), head h at columns h*hd.. (dtype).  Serves the
@@ -442,6 +452,12 @@ int zs_prefix_ids_assemble(const int* hard_ids, int h_cap, const int* hard_len, 
 int zs_greedy_step(const float* part_val, const int* part_idx, int R, int nblk, int* step_ctr,
                    int max_steps, int stop0, int stop1, int* out_ids, int* out_len, int* done,
                    int* pos, int* next_tok, int* all_done, void* stream);
+
+/* zs_greedy_init: generate2's state before step 0 (gpt2_prefix_eval.py:186-196) for R rows:
+ * pos[r] = plen[r] - 1 (the last prompt position), done = out_len = 0, out_ids[r][0..max_steps)
+ * = 0, *step_ctr = 0, all_done[0..2] = 0 -- what zs_greedy_step expects before its first call. */
+int zs_greedy_init(int R, const int* plen, int* pos, int* done, int* out_len, int* out_ids,
+                   int max_steps, int* step_ctr, int* all_done, void* stream);
 
 /* zs_greedy_step_map: zs_greedy_step where partial row c belongs to physical row rowmap[c]
  * (out_ids, out_len, done, pos, next_tok are physical); padding slots are skipped. */

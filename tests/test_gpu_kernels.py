@@ -851,3 +851,40 @@ def test_pack_clips(cuda):
     for b, c in enumerate(clips):
         ref = torch.nn.functional.pad(c[:T], [0, max(0, T - len(c))])
         assert torch.equal(out[b].cpu(), ref), b
+
+
+@pytest.mark.parametrize("B,L,row_stride", [(64, 27, 1), (5, 32, 5), (3, 9, 1)])
+def test_row_attention_kv_fused(cuda, B, L, row_stride):
+    """zs_row_attention_kv (the prefill's attention + KV-cache write in one launch) against the
+    zs_kv_write + zs_row_attention pair: bit-identical attention rows and caches."""
+    from zsaac import ops
+    heads, D, Lmax = 12, 768, 70
+    g = torch.Generator(device="cuda").manual_seed(B * L)
+    qkv = torch.randn(B * L, 3 * D, device=cuda, generator=g).bfloat16()
+    lens = torch.randint(1, L + 1, (B,), device=cuda, generator=g, dtype=torch.int32)
+    R = B * row_stride
+    kc0 = torch.zeros(R, heads, Lmax, 64, device=cuda, dtype=torch.bfloat16)
+    vc0, kc1, vc1 = kc0.clone(), kc0.clone(), kc0.clone()
+    a0 = torch.zeros(B * L, D, device=cuda, dtype=torch.bfloat16)
+    a1 = a0.clone()
+    ops.kv_write(qkv, B, L, D, heads, kc0, vc0, Lmax, row_stride=row_stride)
+    ops.row_attention(qkv, 3 * D, qkv[:, D:], qkv[:, 2 * D:], 3 * D, B, L, heads, 64, True,
+                      0.125, a0, D, lens=lens)
+    ops.row_attention_kv(qkv, B, L, heads, 0.125, a1, kc1, vc1, Lmax, lens, row_stride=row_stride)
+    assert torch.equal(kc0, kc1) and torch.equal(vc0, vc1)
+    assert torch.equal(a0, a1)
+
+
+def test_greedy_init(cuda):
+    """zs_greedy_init leaves generate2's pre-step-0 state (pos = plen - 1, zeros elsewhere)."""
+    from zsaac import ops
+    R, S = 37, 67
+    i32 = dict(device=cuda, dtype=torch.int32)
+    plen = torch.randint(5, 30, (R,), **i32)
+    pos, done, out_len = (torch.full((R,), 9, **i32) for _ in range(3))
+    out_ids = torch.full((R, S), 7, **i32)
+    step_ctr, all_done = torch.full((1,), 5, **i32), torch.full((3,), -1, **i32)
+    ops.greedy_init(R, plen, pos, done, out_len, out_ids, S, step_ctr, all_done)
+    assert torch.equal(pos, plen - 1)
+    assert int(done.abs().sum() + out_len.abs().sum() + out_ids.abs().sum()) == 0
+    assert int(step_ctr[0]) == 0 and all_done.tolist() == [0, 0, 0]

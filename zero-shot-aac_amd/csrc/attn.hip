@@ -306,10 +306,16 @@ __global__ __launch_bounds__(64) void row_attn_kernel(const T* __restrict__ q, i
 // The scalar row_attn_kernel (one thread per query, 64-dim dot products from LDS) ran ~4k VALU
 // instructions per thread for what is 8 MFMAs per wave here.
 constexpr int RA_NW = 4;
+// kc != nullptr (zs_row_attention_kv, the GPT-2 prefill): the wave also stores its (row, head)'s
+// L keys and values into the KV cache, slot ((b * row_stride * heads + head) * Lmax + j) * 64 --
+// zs_kv_write's layout and values (the bf16 qkv elements as they are), from the fragments it
+// loads anyway: one launch and one read of k / v per layer instead of two.
 __global__ __launch_bounds__(64 * RA_NW) void row_attn_mfma_kernel(
     const bf16_t* __restrict__ q, int ldq, const bf16_t* __restrict__ k,
     const bf16_t* __restrict__ v, int ldkv, int L, const int* __restrict__ lens, int causal,
-    float scale, bf16_t* __restrict__ out, int ldo, int B, int heads) {
+    float scale, bf16_t* __restrict__ out, int ldo, int B, int heads,
+    bf16_t* __restrict__ kc = nullptr, bf16_t* __restrict__ vc = nullptr, int Lmax = 0,
+    int row_stride = 1) {
   __shared__ __attribute__((aligned(16))) bf16_t sVt[RA_NW][64 * 32];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int item = blockIdx.x * RA_NW + wv;
@@ -324,6 +330,8 @@ __global__ __launch_bounds__(64 * RA_NW) void row_attn_mfma_kernel(
     const int j = 8 * it + (lane >> 3), d0 = 8 * (lane & 7);
     uint4 u = make_uint4(0, 0, 0, 0);
     if (j < L) u = *reinterpret_cast<const uint4*>(v + ((long)b * L + j) * ldkv + hh * 64 + d0);
+    if (vc && j < L)
+      *reinterpret_cast<uint4*>(vc + (((long)b * row_stride * heads + hh) * Lmax + j) * 64 + d0) = u;
     const bf16_t* e = reinterpret_cast<const bf16_t*>(&u);
 #pragma unroll
     for (int t = 0; t < 8; ++t) {
@@ -343,6 +351,9 @@ __global__ __launch_bounds__(64 * RA_NW) void row_attn_mfma_kernel(
     if (r < L) {
       ku = *reinterpret_cast<const uint4*>(krow + 16 * ks);
       qu = *reinterpret_cast<const uint4*>(qrow + 16 * ks);
+      if (kc)
+        *reinterpret_cast<uint4*>(kc + (((long)b * row_stride * heads + hh) * Lmax + r) * 64 +
+                                  16 * ks + 8 * h) = ku;
     }
     st = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(wa_bf16x8_t, ku),
                                                   __builtin_bit_cast(wa_bf16x8_t, qu), st, 0, 0, 0);
@@ -1004,6 +1015,25 @@ extern "C" int zs_window_attention(const void* qkv, int B, int H, int W, int C, 
     return fail(ZS_ERR_UNSUPPORTED, "zs_window_attention: head_dim %d unsupported (24, 32)", hd);
   }
 #undef WA
+  ZS_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int zs_row_attention_kv(const void* qkv, int B, int L, const int* len, int heads,
+                                   float scale, void* out, int ldo, void* kc, void* vc, int Lmax,
+                                   int row_stride, void* stream) {
+  // causal self-attention over the rows of qkv [B*L][3 * heads * 64] bf16 (q | k | v), and the
+  // k / v rows stored into the cache as zs_kv_write(qkv, B, L, ..., pos0 = NULL, row_stride)
+  ZS_REQUIRE(B > 0 && L > 0 && L <= 32 && heads > 0 && Lmax >= L && row_stride >= 1,
+             "zs_row_attention_kv: 1 <= L <= 32 <= Lmax (B=%d L=%d Lmax=%d)", B, L, Lmax);
+  ZS_REQUIRE(qkv && out && kc && vc && ldo % 4 == 0 && ((uintptr_t)qkv & 15) == 0 &&
+             ((uintptr_t)kc & 15) == 0 && ((uintptr_t)vc & 15) == 0,
+             "zs_row_attention_kv: null or misaligned pointer");
+  const int D = heads * 64;
+  const bf16_t* q = (const bf16_t*)qkv;
+  hipLaunchKernelGGL(row_attn_mfma_kernel, dim3(cdiv((long)B * heads, RA_NW)), dim3(64 * RA_NW), 0,
+                     S(stream), q, 3 * D, q + D, q + 2 * D, 3 * D, L, len, 1, scale, (bf16_t*)out,
+                     ldo, B, heads, (bf16_t*)kc, (bf16_t*)vc, Lmax, row_stride);
   ZS_LAUNCH_CHECK();
   return 0;
 }

@@ -653,6 +653,39 @@ extern "C" int zs_greedy_step_map(const float* part_val, const int* part_idx, in
   return 0;
 }
 
+// generate2's state before step 0 for R rows: pos = plen - 1, done = out_len = 0, out_ids rows
+// zeroed, *step_ctr = 0, all_done = {0, 0, 0} -- one launch instead of six fills and copies
+__global__ __launch_bounds__(256) void greedy_init_kernel(int R, const int* __restrict__ plen,
+                                                          int* __restrict__ pos,
+                                                          int* __restrict__ done,
+                                                          int* __restrict__ out_len,
+                                                          int* __restrict__ out_ids, int max_steps,
+                                                          int* __restrict__ step_ctr,
+                                                          int* __restrict__ all_done) {
+  const int r = blockIdx.x;
+  if (threadIdx.x == 0) {
+    pos[r] = plen[r] - 1;
+    done[r] = 0;
+    out_len[r] = 0;
+    if (r == 0) {
+      *step_ctr = 0;
+      all_done[0] = all_done[1] = all_done[2] = 0;
+    }
+  }
+  for (int t = threadIdx.x; t < max_steps; t += 256) out_ids[(long)r * max_steps + t] = 0;
+}
+
+extern "C" int zs_greedy_init(int R, const int* plen, int* pos, int* done, int* out_len,
+                              int* out_ids, int max_steps, int* step_ctr, int* all_done,
+                              void* stream) {
+  ZS_REQUIRE(R > 0 && max_steps > 0 && plen && pos && done && out_len && out_ids && step_ctr &&
+             all_done, "zs_greedy_init: bad arguments");
+  hipLaunchKernelGGL(greedy_init_kernel, dim3(R), dim3(256), 0, S(stream), R, plen, pos, done,
+                     out_len, out_ids, max_steps, step_ctr, all_done);
+  ZS_LAUNCH_CHECK();
+  return 0;
+}
+
 extern "C" int zs_greedy_step(const float* part_val, const int* part_idx, int R, int nblk,
                               int* step_ctr, int max_steps, int stop0, int stop1, int* out_ids,
                               int* out_len, int* done, int* pos, int* next_tok, int* all_done,

@@ -52,6 +52,7 @@ SIGNATURES = {
     "zs_cast": [P, L, P, I, P],
     "zs_prompt_assemble": [P, I, I, P, I, I, P, P, I, P, I, P, P, P],
     "zs_row_attention": [P, I, P, P, I, I, I, P, I, I, I, F, P, I, I, P],
+    "zs_row_attention_kv": [P, I, I, P, I, F, P, I, P, P, I, I, P],
     "zs_cross_attention": [P, I, P, P, I, I, I, I, I, I, F, P, I, I, P],
     "zs_label_topk": [P, I, I, P, I, I, P, P, P],
     "zs_gpt2_prefill_embed": [P, P, I, P, I, I, P, P, I, I, I, P, P, P, P, I, P],
@@ -68,6 +69,7 @@ SIGNATURES = {
     "zs_argmax_finalize": [P, P, I, I, P, P],
     "zs_prefix_ids_assemble": [P, I, P, P, I, I, I, P, P],
     "zs_greedy_step": [P, P, I, I, P, I, I, I, P, P, P, P, P, P, P],
+    "zs_greedy_init": [I, P, P, P, P, P, I, P, P, P],
     "zs_decode_persist_workspace_bytes": [],
     "zs_decode_persist_grid": [],
     "zs_gpt2_decode_persist": [I, I, I, I, I, I, P, P, P, F, P, P, P, P, P, P, P, P, P, P, P, P, L, I, I, P],

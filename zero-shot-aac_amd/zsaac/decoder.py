@@ -376,7 +376,13 @@ class Gpt2Decoder:
         row's last prompt position in ``self.hf[:B]``."""
         M = B * Pmax
 
+        fused = self.dtype == torch.bfloat16 and Pmax <= 32
+
         def attn(l, qkv, att):
+            if fused:       # one launch: attention + the layer's KV-cache write
+                ops.row_attention_kv(qkv, B, Pmax, NH, 1.0 / math.sqrt(HD), att, self.kc[l],
+                                     self.vc[l], self.Lmax, self.plen[:B], row_stride=row_stride)
+                return
             ops.kv_write(qkv, B, Pmax, D, NH, self.kc[l], self.vc[l], self.Lmax, row_stride=row_stride)
             ops.row_attention(qkv, 3 * D, qkv[:, D:], qkv[:, 2 * D:], 3 * D, B, Pmax, NH, HD, True,
                               1.0 / math.sqrt(HD), att, D, lens=self.plen[:B])
@@ -564,9 +570,8 @@ class Gpt2Decoder:
         state, so a pipeline can capture it in its begin graph."""
         ops.lmhead_topk(self.hf[:R], self.w.wte, 1, None, self.pval1, self.pidx1,
                         temperature=self.temperature)
-        self.pos[:R].copy_(self.plen[:R] - 1)
-        for t in (self.done, self.out_len, self.step_ctr, self.all_done, self.out_ids):
-            t.zero_()
+        ops.greedy_init(R, self.plen, self.pos, self.done, self.out_len, self.out_ids,
+                        self.max_steps, self.step_ctr, self.all_done)
         ops.greedy_step(self.pval1, self.pidx1, R, self.nblk, self.step_ctr, self.max_steps,
                         self.stop0, self.stop1, self.out_ids, self.out_len, self.done, self.pos,
                         self.next_tok, self.all_done)

@@ -284,6 +284,21 @@ def prefill_embed(hard_ids, hard_len, soft, soft_ld, n_soft, wte, wpe, B, Pmax, 
          _p(last_row), dt(wte), _s())
 
 
+def row_attention_kv(qkv, B, L, heads, scale, out, kc, vc, Lmax, lens, row_stride=1):
+    """Causal prefill attention over qkv [B*L, 3*heads*64] bf16 fused with the KV-cache write
+    (zs_row_attention_kv: kv_write + row_attention of one layer in one launch, L <= 32)."""
+    _i32(lens, "lens")
+    call("zs_row_attention_kv", _p(qkv), B, L, _p(lens), heads, float(scale), _p(out),
+         out.stride(0), _p(kc), _p(vc), Lmax, row_stride, _s())
+    return out
+
+
+def greedy_init(R, plen, pos, done, out_len, out_ids, max_steps, step_ctr, all_done):
+    """generate2's state before step 0 in one launch (zs_greedy_init)."""
+    call("zs_greedy_init", R, _p(plen), _p(pos), _p(done), _p(out_len), _p(out_ids), max_steps,
+         _p(step_ctr), _p(all_done), _s())
+
+
 def kv_write(qkv, R, n, D, heads, kc, vc, Lmax, pos0=None, row_stride=1):
     call("zs_kv_write", _p(qkv), R, n, D, heads, _p(pos0), row_stride, _p(kc), _p(vc), Lmax,
          dt(qkv), _s())
