@@ -1061,24 +1061,34 @@ def roofline_c3_step(pipe, reps=20):
             "modelled_step_us": round(tot * 1e6, 1)}
 
 
-def c3_beam5(args, device, n_clips=1024, inflight=2):
+def c3_beam5(args, device, n_clips=1024, inflight=4):
     """C3 (BASELINE.json configs[2]): the same wav -> HTSAT -> MLP -> GPT-2 path with
     generate_beam (beam 5) on eval batches of 256 clips (1280 decode rows), 1024 synthetic clips,
     `inflight` batches in flight; plus the rooflines of its dominant kernels per decode step
-    (roofline_c3_step: the decode GEMMs' MFMA fraction, attention, LM head)."""
+    (roofline_c3_step: the decode GEMMs' MFMA fraction, attention, LM head).  With every batch
+    co-running, 128 x 128 tiles for all GEMMs (`lean_min128` 0: the CU-cheapest tile, not the
+    fastest alone) -- tools/c3_probe.py, profiles/r4/c3_probe.txt: 2 in flight 3.17k, 4: 3.41k,
+    4 + 128 x 128 tiles 3.56k clips/s."""
     import copy
+    from zsaac._lib import call
     a3 = copy.copy(args)
     a3.beam, a3.batch, a3.group, a3.encoder_batch = 5, 256, 1, 0
     pipe, _, _ = build(a3, device, dtype=torch.bfloat16, group=1)
-    dt, outs, runner, info = run_captions(a3, 1, 0, device, pipe, n_clips, 3 * 10 ** 6, [n_clips],
-                                          inflight, 1)
+    call("zs_tune_set", b"lean_min128", 0)
+    try:
+        dt, outs, runner, info = run_captions(a3, 1, 0, device, pipe, n_clips, 3 * 10 ** 6,
+                                              [n_clips], inflight, 1)
+    finally:
+        call("zs_tune_set", b"lean_min128", 256)
     res = {"metric": "audio clips/sec end-to-end (encode+mapper+GPT-2 decode), AudioCaps-eval "
                      "beam 5 bs=256", "value": round(n_clips / dt, 2), "unit": "clips/s",
            "clips": n_clips, "ms_per_step": round(dt / math.ceil(n_clips / 256) * 1e3, 3),
            "dtype": "bf16", "config": {"workload": "C3: HTSAT + MLP mapper + GPT-2 generate_beam, "
                                                    "beam 5, entry_length 67", "eval_batch": 256,
                                        "decode_rows_per_gemm": 1280,
-                                       "steps_in_flight_per_gpu": inflight, **info},
+                                       "steps_in_flight_per_gpu": inflight,
+                                       "gemm_tiles": "128x128 for every lean GEMM (lean_min128 0)",
+                                       **info},
            "roofline": None}
     step = roofline_c3_step(pipe)
     res["roofline"] = step["decode_gemms"]

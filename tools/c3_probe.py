@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
-"""C3 (beam 5, eval batches of 256) throughput at several in-flight depths (bench.py c3_beam5):
-    python tools/c3_probe.py [inflight=2,4] [clips=1024]"""
+"""C3 (beam 5, eval batches of 256) throughput at several in-flight depths (bench.py c3_beam5),
+optionally under zs_tune_set knob sets (";"-separated "k=v,k=v", each reset to 0 after):
+    python tools/c3_probe.py [inflight=2,4] [clips=1024] [sets]"""
 import json
 import os
 import sys
@@ -18,11 +19,20 @@ os.environ["GPU_MAX_HW_QUEUES"] = "16"
 def main():
     infl = [int(c) for c in (sys.argv[1] if len(sys.argv) > 1 else "2,4").split(",")]
     n = int(sys.argv[2]) if len(sys.argv) > 2 else 1024
+    sets = (sys.argv[3] if len(sys.argv) > 3 else "").split(";")
+    from zsaac._lib import call
     args = bench.parse([])
     dev = torch.device("cuda", 0)
     for k in infl:
-        r = bench.c3_beam5(args, dev, n, k)
-        print(json.dumps({"inflight": k, "clips": n, "value": r["value"]}), flush=True)
+        for ks in sets:
+            kv = dict(x.split("=") for x in ks.split(",") if x)
+            for key, v in kv.items():
+                call("zs_tune_set", key.encode(), int(v))
+            r = bench.c3_beam5(args, dev, n, k)
+            for key in kv:
+                call("zs_tune_set", key.encode(), 0)
+            print(json.dumps({"inflight": k, "clips": n, "knobs": ks, "value": r["value"]}),
+                  flush=True)
 
 
 if __name__ == "__main__":
