@@ -42,6 +42,8 @@ Rank 0 prints ONE JSON line.  Besides the contract fields (value = whole-job cli
                      a different configuration, NOT the metric;
   f32_parity_mode:   the bs-64 headline (1045 clips) in f32 (the mode whose greedy ids are
                      bit-exact);
+  c5_mistral:        BASELINE configs C5 (Mistral-7B fp8 decoder, 3 language tags, bs 32) with its
+                     decode-step HBM roofline (also alone: --mistral);
   id_agreement:      greedy ids against the reference goldens (bf16 and f32), first divergence
                      and the reference's own top-2 logit margin there (tools/idparity.py);
   cpu_baseline:      the oracle (reference semantics: batch 1, full recompute, fp32) on bounded
@@ -847,7 +849,7 @@ def main_magic(args, device):
         return mag.beam_magic(pipe.hard_ids[:B], pipe.hard_len[:B], soft, 10, prefix,
                               WordTokenizer(), tok, beam, width, entry, 0.1, 0.2, bert.temp,
                               soft_ld=pipe.mapper.soft_ld)
-    for _ in range(max(1, args.warmup)):
+    for _ in range(max(1, warmup)):
         one()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -901,6 +903,11 @@ def main_magic(args, device):
 
 
 def main_mistral(args, device):
+    """`--mistral`: the C5 line alone (c5_mistral)."""
+    print(json.dumps(c5_mistral(args, device, args.steps or 2, args.warmup)), flush=True)
+
+
+def c5_mistral(args, device, n=2, warmup=1):
     """C5 (predict_mistralai_multilingual.py:90-111): per batch of 32 clips, HTSAT encode ->
     hard prompt (Mistral ids, padded to the batch's longest) -> MLP mapper (1024 -> 20480 ->
     40960) -> for each language tag a batched greedy generate(max_length 60, eos 2) on a
@@ -941,7 +948,6 @@ def main_mistral(args, device):
     for kv in filter(None, os.environ.get("ZS_MISTRAL_RUN_CFG", "").split(",")):   # e.g. down=2x2
         k, v = kv.split("=")
         dec.run_cfg[k] = tuple(int(t) for t in v.split("x"))
-    n = args.steps or 2
     wav = synthetic_clips(B, 0, device)
 
     def one():
@@ -951,7 +957,7 @@ def main_mistral(args, device):
         soft = mapper(ops.l2norm(emb)).view(B, 10, D).float().contiguous()
         hard = hard_ids[:, :H].contiguous()
         return [dec.generate(hard, soft, tags[t], max_length=60) for t in ("en", "zh", "fr")]
-    for _ in range(max(1, args.warmup)):
+    for _ in range(max(1, warmup)):
         one()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -977,10 +983,10 @@ def main_mistral(args, device):
     e1.synchronize()
     step_s = e0.elapsed_time(e1) / 1e3 / reps
     byts = w.nbytes()
-    print(json.dumps({
+    res = {
         "metric": "audio clips/sec, Mistral-7B caption decoder (en+zh+fr greedy generate), bs=32",
         "value": round(n * B / dt_s, 3), "unit": "clips/s", "n_gpus": 1, "steps": n,
-        "warmup": args.warmup, "ms_per_step": round(dt_s / n * 1e3, 1), "higher_is_better": True,
+        "warmup": warmup, "ms_per_step": round(dt_s / n * 1e3, 1), "higher_is_better": True,
         "dtype": "fp8 weights (e4m3, per-channel scale) x bf16 activations, f32 accumulation",
         "data": DATA + "; Mistral-7B geometry, synthetic fp8 weights",
         "config": {"workload": "C5: wav -> HTSAT -> prompt + MLP mapper (1024->20480->40960) -> "
@@ -991,8 +997,11 @@ def main_mistral(args, device):
                      "achieved": round(byts / step_s / 1e9, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(byts / step_s / 1e9 / HBM_PEAK_GBS, 4),
                      "step_us": round(step_s * 1e6, 1), "algo_bytes_per_step": int(byts)},
-        "note": "secondary config C5 (predict_mistralai_multilingual.py); not the headline metric"}),
-        flush=True)
+        "note": "secondary config C5 (predict_mistralai_multilingual.py); not the headline metric"}
+    del dec, w, enc, mapper
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    return res
 
 
 def roofline_lmhead_beam(pipe, reps=20):
@@ -1230,6 +1239,8 @@ def main():
                                          CLOTHO_EVAL_CLIPS, 1)
         res["f32_parity_mode"]["note"] = ("the headline's 1045 clips at bs=64 in f32: the mode "
                                           "whose greedy ids are bit-exact")
+        log("C5 Mistral-7B")
+        res["c5_mistral"] = c5_mistral(args, device)
         log("id agreement")
         from tools import idparity
         res["id_agreement"] = {"bf16": idparity.summary(torch.bfloat16, device),
