@@ -916,7 +916,7 @@ def c5_mistral(args, device, n=2, warmup=1):
     from zsaac import ops, synthetic as S
     from zsaac.decoder import MlpMapper
     from zsaac.encoder import AudioEncoder
-    from zsaac.mistral import MistralDecoder, MistralWeights
+    from zsaac.mistral import MistralDecoder, MistralWeights, generate_concurrent
     B = 32
     dt = torch.bfloat16
     asd = S.htsat_state_dict(3)
@@ -940,14 +940,21 @@ def c5_mistral(args, device, n=2, warmup=1):
     hard_len = torch.zeros(B, dtype=torch.int32, device=device)
     tags = {"en": [1, 523, 269, 28767], "zh": [1, 523, 26715, 28767], "fr": [1, 523, 1642, 28767]}
     tags = {k: torch.tensor(v, dtype=torch.int32, device=device) for k, v in tags.items()}
-    dec = MistralDecoder(w, max_batch=B, max_prompt=Hc + 10 + 4, max_new=60)
-    dec.fused_decode_attn = os.environ.get("ZS_MISTRAL_FUSED_ATTN", "1") != "0"   # A/B knobs
-    dec.use_graph = os.environ.get("ZS_MISTRAL_GRAPH", "1") != "0"
-    dec.prefill_unpack = os.environ.get("ZS_MISTRAL_UNPACK", "1") != "0"
-    dec.fused_glu = os.environ.get("ZS_MISTRAL_RUN", "1") != "0"
-    for kv in filter(None, os.environ.get("ZS_MISTRAL_RUN_CFG", "").split(",")):   # e.g. down=2x2
-        k, v = kv.split("=")
-        dec.run_cfg[k] = tuple(int(t) for t in v.split("x"))
+    # the 3 language tags of a batch decode concurrently (generate_concurrent: one decoder per
+    # tag sharing the weights, one stream each); ZS_MISTRAL_CONCURRENT=0 runs them one by one
+    conc = os.environ.get("ZS_MISTRAL_CONCURRENT", "1") != "0"
+    decs = [MistralDecoder(w, max_batch=B, max_prompt=Hc + 10 + 4, max_new=60)
+            for _ in range(3 if conc else 1)]
+    for dec in decs:
+        dec.fused_decode_attn = os.environ.get("ZS_MISTRAL_FUSED_ATTN", "1") != "0"   # A/B knobs
+        dec.use_graph = os.environ.get("ZS_MISTRAL_GRAPH", "1") != "0"
+        dec.prefill_unpack = os.environ.get("ZS_MISTRAL_UNPACK", "1") != "0"
+        dec.fused_glu = os.environ.get("ZS_MISTRAL_RUN", "1") != "0"
+        for kv in filter(None, os.environ.get("ZS_MISTRAL_RUN_CFG", "").split(",")):   # e.g. down=2x2
+            k, v = kv.split("=")
+            dec.run_cfg[k] = tuple(int(t) for t in v.split("x"))
+    dec = decs[0]
+    streams = ops.dedicated_streams(3, device) if conc else None
     wav = synthetic_clips(B, 0, device)
 
     def one():
@@ -956,6 +963,9 @@ def c5_mistral(args, device, n=2, warmup=1):
         H = int(hard_len.max())          # padding_captions pads to the batch's longest
         soft = mapper(ops.l2norm(emb)).view(B, 10, D).float().contiguous()
         hard = hard_ids[:, :H].contiguous()
+        if conc:
+            return generate_concurrent(decs, streams, [(hard, soft, tags[t], 60)
+                                                       for t in ("en", "zh", "fr")])
         return [dec.generate(hard, soft, tags[t], max_length=60) for t in ("en", "zh", "fr")]
     for _ in range(max(1, warmup)):
         one()
@@ -991,14 +1001,15 @@ def c5_mistral(args, device, n=2, warmup=1):
         "data": DATA + "; Mistral-7B geometry, synthetic fp8 weights",
         "config": {"workload": "C5: wav -> HTSAT -> prompt + MLP mapper (1024->20480->40960) -> "
                                "Mistral-7B greedy generate(max_length 60, eos 2) x 3 language tags",
-                   "batch": B, "generated_tokens": ntok},
+                   "batch": B, "generated_tokens": ntok,
+                   "language_tags_concurrent": conc},
         "roofline": {"kernel": "one Mistral-7B decode step at 32 rows (32 layers: fp8 GEMMs + "
                                "RoPE/attention/norms, bf16 LM head argmax)", "bound": "hbm",
                      "achieved": round(byts / step_s / 1e9, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(byts / step_s / 1e9 / HBM_PEAK_GBS, 4),
                      "step_us": round(step_s * 1e6, 1), "algo_bytes_per_step": int(byts)},
         "note": "secondary config C5 (predict_mistralai_multilingual.py); not the headline metric"}
-    del dec, w, enc, mapper
+    del dec, decs, w, enc, mapper
     torch.cuda.synchronize()
     torch.cuda.empty_cache()
     return res

@@ -328,3 +328,25 @@ def test_dropin_generate_trims_and_reuses_engine(cuda, golden):
     big = lm.engine(cuda, 64, 64, 60)
     assert big is not decs[0] and big.B >= 64
     assert lm.engine(cuda, 8, 16, 10) is big
+
+
+@pytest.mark.parametrize("mode", ["fp8", "f32"])
+def test_generate_concurrent_equals_sequential(cuda, setup, mode):
+    """zsaac.mistral.generate_concurrent (the language tags of a batch on separate streams and
+    decoders sharing the weights, advanced in chunks without blocking on one another) returns
+    exactly each decoder's sequential generate ids."""
+    from zsaac import ops
+    from zsaac.mistral import MistralDecoder, MistralWeights, generate_concurrent
+    g, sd, pes = setup
+    w = MistralWeights(sd, cuda, mode, n_heads=H, n_kv_heads=KVH, eps=EPS)
+    hard = torch.from_numpy(g["hard_ids"]).to(torch.int32).to(cuda)
+    jobs = [(hard, soft.contiguous().to(cuda), torch.from_numpy(g[f"tag_{t}"]).to(torch.int32).to(cuda), 60)
+            for t, (pe, soft) in pes.items()]
+    seq = MistralDecoder(w, max_batch=8, max_prompt=32, max_new=40)
+    ref = [seq.generate(*j) for j in jobs]
+    decs = [MistralDecoder(w, max_batch=8, max_prompt=32, max_new=40) for _ in jobs]
+    streams = ops.dedicated_streams(len(jobs), cuda)
+    for _ in range(2):          # the second pass replays graphs captured in the first
+        out = generate_concurrent(decs, streams, jobs)
+        torch.cuda.synchronize()
+        assert out == ref

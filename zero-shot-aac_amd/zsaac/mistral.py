@@ -27,6 +27,7 @@ all-ones attention mask does; soft rows; language tag ids) is prefilled as B x P
 from __future__ import annotations
 
 import math
+import time
 from typing import Dict, List, Optional, Sequence
 
 import torch
@@ -484,6 +485,60 @@ class MistralDecoder:
         ids, ln = self.out_ids[:B].cpu(), self.out_len[:B].cpu()
         return [ids[b, :int(ln[b])].tolist() for b in range(B)]
 
+    # ---------------------------------------------------------------- async form (no host sync)
+    def begin(self, hard_ids: torch.Tensor, soft: torch.Tensor, tail_ids: torch.Tensor,
+              max_length: int = 60, eos: int = 2) -> bool:
+        """:meth:`generate`'s prefill and step 0 enqueued on the current stream; then
+        :meth:`advance` chunks of steps and :meth:`ready` / :meth:`ids` (generate_concurrent).
+        Returns False when there is nothing to generate."""
+        w, st = self.w, torch.cuda.current_stream().cuda_stream
+        B, H = hard_ids.shape
+        ns, nt = soft.shape[1], tail_ids.numel()
+        P = H + ns + nt
+        new = max_length - P
+        if B > self.B or P > self.Pmax or new > self.max_new:
+            raise ValueError(f"mistral begin: B={B} P={P} new={new} exceeds the engine")
+        self._aB, self._anew, self._as, self._aeos = B, new, 1, eos
+        if new <= 0:
+            return False
+        M = B * P
+        call("zs_mistral_embed", hard_ids.data_ptr(), H, soft.data_ptr(), ns, tail_ids.data_ptr(),
+             nt, None, w.emb.data_ptr(), w.D, M, self.x.data_ptr(), ops.dt(w.emb), st)
+        self.pos[:M].copy_(torch.arange(P, device=w.dev, dtype=torch.int32).repeat(B))
+        self._layers(M, P)
+        self.last[:B].copy_(self.h[:M].view(B, P, w.D)[:, P - 1])
+        self._lm_argmax(self.last[:B], B)
+        for t in (self.done, self.out_len, self.step_ctr, self.all_done, self.out_ids):
+            t.zero_()
+        self.pos[:B].fill_(P - 1)
+        ops.greedy_step(self.pval, self.pidx, B, self.nblk, self.step_ctr, self.max_new, eos, eos,
+                        self.out_ids, self.out_len, self.done, self.pos, self.next_tok, self.all_done)
+        return True
+
+    def advance(self, n: int = 8):
+        """Enqueue up to n more decode steps (the same steps generate's loop runs between its
+        all-done checks), then an async copy of the all-done flag and an event after it."""
+        stop = min(self._anew, self._as + n)
+        while self._as < stop:
+            self.decode_step(self._aB, self._aeos)
+            self._as += 1
+        if not hasattr(self, "_aflag"):
+            self._aflag = torch.zeros(1, dtype=torch.int32, pin_memory=True)
+        self._aflag.copy_(self.all_done[:1], non_blocking=True)
+        self._aev = torch.cuda.Event()
+        self._aev.record()
+
+    def ready(self) -> Optional[bool]:
+        """None while the last advance is in flight; else True when generation is over."""
+        if not self._aev.query():
+            return None
+        return bool(int(self._aflag[0])) or self._as >= self._anew
+
+    def ids(self) -> List[List[int]]:
+        B = self._aB
+        ids, ln = self.out_ids[:B].cpu(), self.out_len[:B].cpu()
+        return [ids[b, :int(ln[b])].tolist() for b in range(B)]
+
     def _step_body(self, B, eos):
         w, st = self.w, torch.cuda.current_stream().cuda_stream
         call("zs_mistral_embed", None, 0, None, 0, None, 0, self.next_tok.data_ptr(),
@@ -536,3 +591,42 @@ class MistralDecoder:
         return self.generate(empty, embeds.float().contiguous(), torch.zeros(0, dtype=torch.int32,
                                                                               device=dev),
                              max_length=max_length, eos=eos)
+
+
+def generate_concurrent(decoders: Sequence["MistralDecoder"], streams: Sequence, jobs):
+    """Several independent greedy generates at once, one decoder (sharing the weights) and one
+    stream per job: jobs = [(hard_ids, soft, tail_ids, max_length)], each exactly
+    :meth:`MistralDecoder.generate`'s result (the 3 language tags of a C5 batch co-run: every
+    step of one is a chain of latency-bound launches the others' weight streams overlap).  The
+    host never blocks on one job while another could be advanced."""
+    assert len(decoders) >= len(jobs) and len(streams) >= len(jobs)
+    caller = torch.cuda.current_stream()
+    live = []
+    for i, (hard, soft, tail, max_length) in enumerate(jobs):
+        s = streams[i]
+        s.wait_stream(caller)
+        with torch.cuda.stream(s):
+            if decoders[i].begin(hard, soft, tail, max_length):
+                decoders[i].advance(7)       # generate checks all-done first at step 8
+                live.append(i)
+    out = [[[] for _ in range(hard.shape[0])] for hard, *_ in jobs]
+    while live:
+        progressed = False
+        for i in list(live):
+            r = decoders[i].ready()
+            if r is None:
+                continue
+            progressed = True
+            if r:
+                with torch.cuda.stream(streams[i]):
+                    out[i] = decoders[i].ids()
+                live.remove(i)
+            else:
+                with torch.cuda.stream(streams[i]):
+                    decoders[i].advance(8)
+        if not progressed:
+            time.sleep(20e-6)
+    for s in streams[:len(jobs)]:
+        caller.wait_stream(s)
+    return out
+
