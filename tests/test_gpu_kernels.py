@@ -675,10 +675,11 @@ def _decode_map_body(cuda):
     assert int(b["flag"][2]) == int((b["done"] == 0).sum())
 
 
+@pytest.mark.parametrize("M", [70, 64])          # the 128- and 64-row tiles (f32: the LDS-DMA ring)
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-def test_lmhead_topk(cuda, dtype):
+def test_lmhead_topk(cuda, dtype, M):
     from zsaac import ops
-    M, K, V, k = 70, 768, 50257, 5
+    K, V, k = 768, 50257, 5
     a = torch.randn(M, K, device=cuda).to(dtype)
     w = (torch.randn(V, K, device=cuda) * 0.05).to(dtype)
     nblk = ops.lmhead_nblk(V)

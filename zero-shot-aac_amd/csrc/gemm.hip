@@ -790,7 +790,9 @@ constexpr int LM_BN = 128;
 constexpr int MAXK = 8;
 int g_lm_prio = 1;   // zs_tune_set("lm_prio", 0): LM head main loop without s_setprio
 
-template <typename T, int BM, int KMAX>
+// RING (f32 only; bf16 always): the LDS-DMA ring main loop and the transposed register epilogue
+// (f32 rows staged as bf16 rows of twice the length, fast_compute F32)
+template <typename T, int BM, int KMAX, bool RING = sizeof(T) == 2>
 __global__ __launch_bounds__(256) void lmhead_kernel(int xcd_order, int M, int K, int V, const T* A, int lda,
                                                      const T* W, int topk, int row_norm,
                                                      float* part_stat, float* part_val,
@@ -802,7 +804,7 @@ __global__ __launch_bounds__(256) void lmhead_kernel(int xcd_order, int M, int K
   constexpr int TM = BM / 64, TN = LM_BN / 64;
   constexpr int SM_MAIN = 2 * (BM + LM_BN) * LDW * (int)sizeof(T);
   constexpr int SM_EPI = BM * (LM_BN + 1) * 4;
-  constexpr bool FAST = sizeof(T) == 2;
+  constexpr bool FAST = RING;
   constexpr int SM_LOOP = FAST ? 2 * FastTile<BM, LM_BN>::STAGE : SM_MAIN;  // 4 waves (2x2)
   constexpr int SM = SM_LOOP > SM_EPI ? SM_LOOP : SM_EPI;
   // ONE __shared__ array (a second object can de-pipeline the DMA loop: §5 item 4(a))
@@ -830,7 +832,16 @@ __global__ __launch_bounds__(256) void lmhead_kernel(int xcd_order, int M, int K
   // sit in registers of one lane pair (see the epilogue below)
   f32x16_t acct[LM_BN / 64][BM / 64];
   float ssq[BM / 64];     // per lane: its half of the squared norm of token wc0 + j*32 + (lane&31)
-  if constexpr (FAST) {
+  if constexpr (FAST && sizeof(T) == 4) {
+    const DenseRows ra{(const bf16_t*)A, 2 * lda, M, m0};
+    const DenseRows rw{(const bf16_t*)W, 2 * K, V, n0};
+#pragma unroll
+    for (int j = 0; j < BM / 64; ++j) ssq[j] = 0.f;
+    if (row_norm)
+      fast_mainloop<LM_BN, BM, 2, 2, 2, 64, true, 0, true>(rw, ra, 0, 2 * K, smem_raw, acct, 0, ssq);
+    else
+      fast_mainloop<LM_BN, BM, 2, 2, 2, 64, false, 0, true>(rw, ra, 0, 2 * K, smem_raw, acct);
+  } else if constexpr (FAST) {
     const DenseRows ra{(const bf16_t*)A, lda, M, m0};
     const DenseRows rw{(const bf16_t*)W, K, V, n0};
 #pragma unroll
@@ -1180,11 +1191,21 @@ extern "C" int zs_lmhead_topk_t(int M, int K, int V, int dtype, const void* A, i
   ZS_REQUIRE(topk >= 1 && topk <= MAXK, "zs_lmhead_topk: 1 <= topk <= 8");
   hipStream_t st = S(stream);
   const int nblk = cdiv(V, LM_BN);
+  // f32 on the LDS-DMA ring when its 16-byte rows allow (lda % 4 already holds: lda % 8)
+  const bool ring = dtype != ZS_BF16 && g_f32_fast && K % 4 == 0;
 #define LMH(T, BM_, KM_)                                                                     \
-  hipLaunchKernelGGL((lmhead_kernel<T, BM_, KM_>), dim3(nblk * cdiv(M, BM_)), dim3(256), 0, st, \
-                     (g_fast_xcd ? 1 : 0) | (g_lm_prio ? 2 : 0), M, K, V, (const T*)A, lda,       \
-                     (const T*)W, topk, row_norm, part_stat,                                      \
-                     part_val, part_idx, temperature)
+  do {                                                                                       \
+    if (sizeof(T) == 4 && ring)                                                              \
+      hipLaunchKernelGGL((lmhead_kernel<T, BM_, KM_, true>), dim3(nblk * cdiv(M, BM_)), dim3(256), \
+                         0, st, (g_fast_xcd ? 1 : 0) | (g_lm_prio ? 2 : 0), M, K, V, (const T*)A, \
+                         lda, (const T*)W, topk, row_norm, part_stat, part_val, part_idx,       \
+                         temperature);                                                       \
+    else                                                                                     \
+      hipLaunchKernelGGL((lmhead_kernel<T, BM_, KM_>), dim3(nblk * cdiv(M, BM_)), dim3(256), 0, \
+                         st, (g_fast_xcd ? 1 : 0) | (g_lm_prio ? 2 : 0), M, K, V, (const T*)A,  \
+                         lda, (const T*)W, topk, row_norm, part_stat, part_val, part_idx,       \
+                         temperature);                                                       \
+  } while (0)
   // top-k lists of 1 (argmax), 5 (beam <= 5: generate_beam's default) or 8 entries per block
 #define LMH_K(T, BM_)                                                                          \
   do {                                                                                         \

@@ -114,6 +114,7 @@ __device__ __forceinline__ void fast_compute(
       for (int j = 0; j < FT::TN; ++j) {
         const int row = wc0 + j * 32 + r;
         b[j] = *reinterpret_cast<const float4*>(stage + row * FT::RB + 16 * (c ^ FT::swz(row)));
+        if constexpr (SSQ) ssq[j] += (b[j].x * b[j].x + b[j].y * b[j].y) + (b[j].z * b[j].z + b[j].w * b[j].w);
       }
 #pragma unroll
       for (int e = 0; e < 4; ++e)
