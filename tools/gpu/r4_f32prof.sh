@@ -4,7 +4,7 @@ cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 O=gpurun_out/${1:-r4_f32prof}
 mkdir -p $O
-timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $O/prof -o run --output-format csv -- python3 tools/f32_probe.py 1045 10 > $O/f32.txt 2> $O/f32.log || { tail -30 $O/f32.log; exit 1; }
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $O/prof -o run --output-format csv -- python3 tools/f32_probe.py 1045 ${2:-10} > $O/f32.txt 2> $O/f32.log || { tail -30 $O/f32.log; exit 1; }
 cat $O/f32.txt
 find gpurun_out -name "*kernel_trace.csv" -size +4M -delete
 python3 - <<PY
