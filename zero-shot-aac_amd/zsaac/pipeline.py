@@ -164,9 +164,7 @@ class CaptionPipeline:
         return self.emb_buf[:B]
 
     def caption_wav(self, wav: torch.Tensor) -> CaptionBatch:
-        self.begin_wav(wav)
-        self.decoder.run_to_completion()
-        return self.result()
+        return self.caption_emb(self.encode(wav))
 
     def caption_emb(self, emb: torch.Tensor) -> CaptionBatch:
         """From CLAP audio embeddings [B, 1024] (the pickle's ``audio_embedding``)."""
