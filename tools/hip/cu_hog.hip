@@ -29,3 +29,15 @@ extern "C" int cu_hog_launch(int waves, int blocks, int lds, const int* flag, in
     return 1;
   return (int)hipGetLastError();
 }
+
+// XCC_ID of the XCD each workgroup runs on (hardware register), per workgroup
+__global__ void xcc_probe_kernel(int* out) {
+  unsigned x;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
+  if (threadIdx.x == 0) out[blockIdx.x] = (int)x;
+}
+
+extern "C" int xcc_probe(int blocks, int* out, void* stream) {
+  hipLaunchKernelGGL(xcc_probe_kernel, dim3(blocks), dim3(64), 0, (hipStream_t)stream, out);
+  return (int)hipGetLastError();
+}
