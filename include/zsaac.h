@@ -468,36 +468,44 @@ int zs_greedy_step_map(const float* part_val, const int* part_idx, int R, const 
 
 /* zs_gpt2_decode_persist: every remaining step of generate2 (gpt2_prefix_eval.py:161-222: the
  * 67-step loop of model.gpt(inputs_embeds=...) -> argmax -> stop check) for ONE batch of R <= 64
- * rows (the reference's eval batch), bf16, as one persistent launch of
- * zs_decode_persist_grid() workgroups (one per CU; the caller keeps the concurrent launches'
- * grids within the CU count): per step the 12 GPT2Blocks (ln_1 affine folded into c_attn and
- * ln_2's into c_fc, as zs_gemm_ln), ln_f, the tied LM head with its argmax (ties -> lower id)
- * and zs_greedy_step's bookkeeping, until every row stopped or max_steps.  Starts from the state
- * zs_greedy_step left after step 0 (next_tok, pos, done, out_ids, out_len, *step_ctr,
- * all_done[0]); leaves it as the per-step path would.  layer_w: 12 x 8 device pointers
- * {c_attn W [2304][768] bf16, its bias f32, attn.c_proj W [768][768], bias, c_fc W [3072][768],
- * bias, mlp.c_proj W [768][3072], bias} (W = Conv1D weight transposed); wte_packed: the tied
- * LM head in MFMA B-fragment order, [ceil(V/16)][24][64][8] bf16 (zs layout of block j, k-step s,
- * lane l = W[16 j + l % 16][32 s + 8 (l / 16) .. + 8], rows past V zero); temperature > 0 divides
- * the logits before the argmax (gpt2_prefix_eval.py:196); kv: 24 pointers
- * {kc[0..11], vc[0..11]}, each [R][12][Lmax][64] bf16 (zs_kv_write layout).  ws: scratch of
- * zs_decode_persist_workspace_bytes() bytes, 256-byte aligned, private to one launch in flight.
- * The grid is zs_decode_persist_grid() / col_split x row_split workgroups.  col_split 1: each
- * workgroup owns one column slice of every GEMM; 2: two (half the workgroups per batch: the same
- * activation reads per workgroup for twice the weights, less CU time per step, a longer step).
- * row_split 1: every workgroup covers all rows; 2: twice as many, each its slice for half of the
- * rows (half the per-workgroup activation reads, a shorter step; for few batches in flight).
- * A grid that cannot become co-resident gives up after a bounded wait: then all_done[1] = -1,
- * zs_decode_persist_status reports timed_out != 0 and the outputs are invalid. */
+ * rows (the reference's eval batch), bf16, as one persistent launch of `grid` (48, 96 or 192)
+ * 256-thread workgroups (half a CU each; the caller keeps the concurrent launches' grids
+ * co-resident): per step the 12 GPT2Blocks (ln_1 affine folded into c_attn and ln_2's into c_fc),
+ * ln_f, the tied LM head with its argmax (ties -> lower id) and zs_greedy_step's bookkeeping,
+ * until every row stopped or max_steps.  Starts from the state zs_greedy_step left after step 0
+ * (next_tok, pos, done, out_ids, out_len, *step_ctr, all_done[0]) and commits that state after
+ * every step.  layer_w: 12 x 8 device pointers {c_attn W, its bias f32, attn.c_proj W, bias,
+ * c_fc W, bias, mlp.c_proj W, bias}, each W (= Conv1D weight transposed, [N][K] bf16) in MFMA
+ * fragment order [N/16][K/32][64][8] (block j, k-step s, lane l = W[16 j + l % 16][32 s + 8 (l /
+ * 16) .. + 8]); wte_packed: the tied LM head with ln_f's weight folded in, bf16(g o wte[v]), in the
+ * same order, [ceil(V/16)][24][64][8] (rows past V zero), and lm_bias [ceil(V/16) 16] f32 = ln_f's
+ * bias through the head (beta . wte[v]): logit[v] = LN(x) . (g o wte[v]) + lm_bias[v]; temperature > 0 divides the logits before the argmax (gpt2_prefix_eval.py:196);
+ * kv: 24 pointers {kc[0..11], vc[0..11]}, each [R][12][Lmax][64] bf16 (zs_kv_write layout),
+ * 128-byte aligned.  ws: scratch of zs_decode_persist_workspace_bytes() bytes, 256-byte aligned,
+ * private to one launch in flight.  Every output element is computed by the same operations
+ * whatever `grid` (each GEMM element: four K-quarter MFMA chains summed (p0 + p1) + (p2 + p3);
+ * LayerNorm, attention and argmax in fixed orders), so ids and state do not depend on the grid
+ * and equal zs_gpt2_decode_phases'.  A grid that cannot become co-resident gives up after a
+ * bounded wait: all_done[1] = -1, zs_decode_persist_status reports timed_out != 0, and the state
+ * in memory is the last committed step's (resume with zs_gpt2_decode_phases). */
 int zs_decode_persist_workspace_bytes(void);
-int zs_decode_persist_grid(void);
 int zs_gpt2_decode_persist(int R, int Lmax, int max_steps, int stop0, int stop1, int V,
                            const void* wte, const void* wpe, const void* wte_packed,
                            float temperature, const void* const* layer_w,
-                           const float* lnf_w, const float* lnf_b, void* const* kv, int* pos,
+                           const float* lm_bias, void* const* kv, int* pos,
                            int* next_tok, int* done, int* out_ids, int* out_len, int* step_ctr,
-                           int* all_done, void* ws, long ws_bytes, int row_split, int col_split,
-                           void* stream);
+                           int* all_done, void* ws, long ws_bytes, int grid, void* stream);
+/* zs_gpt2_decode_phases: `steps` decode steps of the same computation as separate launches (one
+ * per phase of every block, the LM head and the bookkeeping: 62 per step; each a no-op once
+ * all_done[0] is set, so a graph-captured chunk can run past the end) -- the per-step path of
+ * zs_gpt2_decode_persist (no co-residency needed; the give-up fallback), bit-identical to it. */
+int zs_gpt2_decode_phases(int R, int Lmax, int max_steps, int stop0, int stop1, int V,
+                          const void* wte, const void* wpe, const void* wte_packed,
+                          float temperature, const void* const* layer_w,
+                          const float* lm_bias, void* const* kv, int* pos,
+                          int* next_tok, int* done, int* out_ids, int* out_len, int* step_ctr,
+                          int* all_done, void* ws, long ws_bytes, int steps, int grid,
+                          void* stream);
 int zs_decode_persist_status(const void* ws, int* timed_out);
 /* zs_decode_persist_set_stamps: diagnostic phase timing (tools/persist_stamps.py): with buf !=
  * NULL ([grid][128] u64), thread 0 of every workgroup of later launches writes s_memrealtime

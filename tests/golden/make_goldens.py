@@ -26,6 +26,9 @@ Fixture list (reference call sites in brackets):
   c2_margin_flat.npz  step, on smaller decoder weights (the bf16 id-parity check);
   c2_gpt2init.npz     c2_gpt2init at GPT-2's own init scale.  "tolerance" adds to these and
                   c1_greedy the reference's own bf16-vs-f32 logit error (bf16_ref_err*).
+  beam_tol.npz    the C3 bf16 beam tolerance: the reference's own bf16-vs-f32 first-step
+                  log-prob error and best-beam score loss (generate_beam, gpt2_prefix_eval.py:
+                  99-158) on the two weight sets of the C3 tests.
   mistral.npz     C5 Mistral decoder path: ClapCaption_Mistralai_prompt.clap_to_gpt
                   (caption_model.py:392-413) + LMmodel.generate(inputs_embeds, attention_mask=ones,
                   do_sample=False, max_length=60, eos/pad 2) as predict_mistralai_multilingual.py:
@@ -281,6 +284,77 @@ def gen_tolerance(names=("c1_greedy", "c2_margin", "c2_margin_flat", "c2_gpt2ini
         _save(name + ".npz", **g)
         print(f"  {name}: bf16 reference error first step {float(g['bf16_ref_err']):.4f}, all steps "
               f"max {float(steps.max()):.4f} ({time.time() - t0:.0f}s)", flush=True)
+
+
+# C3 beam-search tolerance: the weight sets of tests/test_gpu_configs.py's beam checks
+BEAM_TOL_SETS = {"std01": (dict(GPT2_KW), 31), "gpt2init": (MARGIN_GPT2_KW["c2_gpt2init"], 37)}
+
+
+def gen_beam_tolerance(n_clips=4, beam=5, entry_length=67):
+    """beam_tol.npz: the stated tolerance of the C3 bf16 beam score rule, from the REFERENCE's
+    own bf16 execution.  For each weight set (BEAM_TOL_SETS: decoder weights, CLAP-embedding seed
+    of the test) and each of the first n_clips clips (hard prompt as dataset.py:441-453):
+      {set}_first_err   max |log_softmax(logits_bf16) - log_softmax(logits_f32)| of the first
+                        generated step, the reference's GPT2LMHeadModel cast to bfloat16 (torch
+                        CPU) against its f32 run, softmax taken exactly on both logit sets;
+      {set}_score_loss  f32 length-normalised score (gpt2_prefix_eval.py:150-156) of the best beam
+                        of the reference's generate_beam run in bf16, minus that of its f32 run's
+                        best beam (teacher-forced f32 rescoring): what bf16 costs the reference;
+      {set}_tau_b       4 x max first_err: the beam score rule's bound (tests/test_gpu_configs.py:
+                        an exact maximiser of the bf16 score ends within 2 e, beam search is not
+                        exact, hence twice that)."""
+    import copy
+    import gpt2_prefix_eval as G
+    from models.caption_model import ClapCaption_prompt
+    from oracle import caption as OC
+
+    class _Gpt(torch.nn.Module):        # generate_beam only touches model.gpt
+        def __init__(self, gpt):
+            super().__init__()
+            self.gpt = gpt
+
+    def score(model, pe, toks):
+        wte = model.gpt.transformer.wte
+        seq = torch.cat([pe, wte(torch.tensor([toks[:-1]]))], 1) if len(toks) > 1 else pe
+        lp = model.gpt(inputs_embeds=seq).logits[0, pe.shape[1] - 1:].log_softmax(-1)
+        return float(lp[torch.arange(len(toks)), torch.tensor(toks)].mean())
+
+    table, label_ids = S.label_table(), S.label_token_table()
+    out = {}
+    for name, (kw, seed) in BEAM_TOL_SETS.items():
+        sd = S.gpt2_state_dict(**kw)
+        sd.update(S.mlp_mapper_state_dict(1))
+        model = ClapCaption_prompt(10, clip_length=10, prefix_size=1024, num_layers=8,
+                                   mapping_type="mlp", only_prefix=False, only_soft_prompt=False)
+        model.load_state_dict(sd, strict=False)
+        model.eval()
+        m16 = _Gpt(copy.deepcopy(model.gpt).to(torch.bfloat16)).eval()
+        emb = S.synthetic_clap_embeddings(n_clips, seed=seed)
+        first, loss = [], []
+        t0 = time.time()
+        for i in range(n_clips):
+            e = torch.nn.functional.normalize(emb[i:i + 1], dim=-1)
+            idx = OC.sound_effect_choice(emb[i:i + 1], table, SOUND_EFFECT_NUM)[0].tolist()
+            hard = torch.tensor([OC.prompt_ids(idx, label_ids)])
+            with torch.no_grad():
+                pe, _ = model.clap_to_gpt(e.unsqueeze(0), model.gpt.transformer.wte(hard))
+                l32 = model.gpt(inputs_embeds=pe).logits[0, -1]
+                l16 = m16.gpt(inputs_embeds=pe.to(torch.bfloat16)).logits[0, -1].float()
+                first.append(float((l16.log_softmax(-1) - l32.log_softmax(-1)).abs().max()))
+                t32 = G.generate_beam(model, IdTokenizer(), beam_size=beam, embed=pe,
+                                      entry_length=entry_length)
+                t16 = G.generate_beam(m16, IdTokenizer(), beam_size=beam,
+                                      embed=pe.to(torch.bfloat16), entry_length=entry_length)
+                b32 = [int(t) for t in t32[0].split()]
+                b16 = [int(t) for t in t16[0].split()]
+                loss.append(score(model, pe, b16) - score(model, pe, b32))
+            print(f"  {name} clip {i}: first err {first[-1]:.4f} score loss {loss[-1]:.4f} "
+                  f"exact {b16 == b32} ({time.time() - t0:.0f}s)", flush=True)
+        out[f"{name}_clap_emb"] = emb.numpy()
+        out[f"{name}_first_err"] = np.array(first, np.float32)
+        out[f"{name}_score_loss"] = np.array(loss, np.float32)
+        out[f"{name}_tau_b"] = np.float32(4.0 * max(first))
+    _save("beam_tol.npz", **out)
 
 
 VARIANTS = ("se_mlp", "xattn", "xattn_v2", "prefix")
@@ -620,6 +694,7 @@ ALL = {"prompt": gen_prompt, "mappers": gen_mappers, "htsat": gen_htsat, "cnn14"
        "margin": gen_margin, "margin_flat": lambda: gen_margin(name="c2_margin_flat"),
        "gpt2init": lambda: gen_margin(name="c2_gpt2init"), "tolerance": gen_tolerance,
        "variants": gen_variants, "magic": gen_magic, "temperature": gen_temperature,
+       "beam_tol": gen_beam_tolerance,
        "mistral": gen_mistral}
 
 if __name__ == "__main__":

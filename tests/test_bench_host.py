@@ -24,38 +24,49 @@ def test_persist_launch_bytes():
     assert bench.persist_launch_bytes(1000, [10], 1) == 0
 
 
-def test_choose_persist_shape_keeps_grids_coresident():
-    """ConcurrentRunner's persistent grid shape choice (zsaac.pipeline.choose_persist_shape):
-    simulated begins and finishes in random order, shapes (col_split, row_split) of 96 / 48 / 24
-    workgroups on 256 CUs with CUs // 24 pipelines -- the workgroups in flight never exceed the
-    CUs, a shard of two or three batches runs its first ones on the largest grid, and a long run
-    of batches takes the smallest."""
+def test_choose_persist_grid_keeps_grids_coresident():
+    """ConcurrentRunner's persistent grid choice (zsaac.pipeline.choose_persist_grid), pure host
+    logic: simulated begins and finishes in random order, grids of 192 / 96 / 48 half-CU
+    workgroups within a budget of workgroup slots, budget // 48 pipelines -- the workgroups in
+    flight never exceed the budget, a shard of two or three batches runs its first ones on the
+    largest grid, and a long run of batches takes the smallest."""
     import random
-    from zsaac import ops
-    from zsaac.pipeline import choose_persist_shape, persist_shapes
-    CUS = 256
-    for spec in ("12,11,21", "12,11", "21", "11,21"):
-        shapes = persist_shapes(spec)
-        grids = [ops.decode_persist_grid(rs, cs) for cs, rs in shapes]
-        assert grids == sorted(grids, reverse=True)
-        P = CUS // grids[-1]
-        rng = random.Random(0)
-        for n in list(range(1, 24)) * 10:
-            active, nxt, chosen = {}, 0, []
-            while nxt < n or active:
-                free = [i for i in range(P) if i not in active]
-                if nxt < n and free and rng.random() < 0.7:
-                    cs, rs = choose_persist_shape(sum(active.values()), n - nxt, shapes, CUS)
-                    active[free[0]] = ops.decode_persist_grid(rs, cs)
-                    chosen.append((cs, rs))
-                    nxt += 1
-                    assert sum(active.values()) <= CUS, (spec, n, chosen)
-                elif active:
-                    del active[rng.choice(list(active))]
-        assert choose_persist_shape(0, 2, shapes, CUS) == shapes[0]
-        assert choose_persist_shape(0, 17, shapes, CUS) == shapes[-1]
-    sh = persist_shapes("12,11,21")
-    assert sh == [(1, 2), (1, 1), (2, 1)]
-    assert choose_persist_shape(96, 2, sh, CUS) == (1, 2)
-    assert choose_persist_shape(0, 5, sh, CUS) == (1, 2)
-    assert choose_persist_shape(0, 8, sh, CUS) == (1, 1)
+    from zsaac.pipeline import choose_persist_grid, persist_grids
+    for budget in (256, 384, 512):
+        for spec in ("192,96,48", "96,48", "48", "192,48"):
+            grids = persist_grids(spec)
+            assert grids == sorted(grids, reverse=True)
+            P = budget // grids[-1]
+            rng = random.Random(0)
+            for n in list(range(1, 24)) * 10:
+                active, nxt, chosen = {}, 0, []
+                while nxt < n or active:
+                    free = [i for i in range(P) if i not in active]
+                    if nxt < n and free and rng.random() < 0.7:
+                        g = choose_persist_grid(sum(active.values()), n - nxt, grids, budget)
+                        active[free[0]] = g
+                        chosen.append(g)
+                        nxt += 1
+                        assert sum(active.values()) <= budget, (spec, n, chosen)
+                    elif active:
+                        del active[rng.choice(list(active))]
+            assert choose_persist_grid(0, 17, grids, budget) == grids[-1]
+    g = persist_grids("192,96,48")
+    assert g == [192, 96, 48]
+    assert choose_persist_grid(0, 2, g, 256) == 192         # 192 + one 48 beside it
+    assert choose_persist_grid(0, 3, g, 256) == 96          # 96 + two 48s
+    assert choose_persist_grid(96, 2, g, 256) == 96
+    assert choose_persist_grid(0, 6, g, 512) == 192
+    assert choose_persist_grid(0, 5, g, 256) == 48
+
+
+def test_persist_grids_env(monkeypatch):
+    """An explicit spec is never overridden by the environment (ZSAAC_PERSIST_GRID applies only
+    when no spec is given)."""
+    from zsaac.pipeline import persist_grids
+    monkeypatch.setenv("ZSAAC_PERSIST_GRID", "96")
+    assert persist_grids("192,48") == [192, 48]
+    assert persist_grids() == [96]
+    monkeypatch.delenv("ZSAAC_PERSIST_GRID")
+    monkeypatch.setenv("ZSAAC_PERSIST_GRIDS", "48,96")
+    assert persist_grids() == [96, 48]

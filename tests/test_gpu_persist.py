@@ -1,16 +1,17 @@
-"""The persistent greedy decode (zs_gpt2_decode_persist: all steps of generate2 after step 0 for
-one bs <= 64 batch in one launch) against the per-step launch chain it replaces and against the
-reference goldens.
+"""The grid decode of one bs <= 64 greedy batch (decode_grid.hip): the persistent launch
+(zs_gpt2_decode_persist) at every grid size and the phase launches (zs_gpt2_decode_phases, the
+per-step path and the give-up fallback) run one canonical arithmetic, so
 
-Both bf16 paths round the same values to bf16 (LN-folded c_attn / c_fc weights, bf16 q/k/v,
-attention output and MLP hidden rows, f32 residual stream) but sum in different orders, so ids
-agree wherever the reference's own top-1 / top-2 margin is not within bf16 noise:
-  * c2_margin_flat (reference margins large at every step): persistent ids == stepwise ids ==
-    reference ids on every clip, at the full batch and at ragged batches of 1, 7 and 21 rows;
-  * decode state after the launch (pos, done, out_len, step counter, finished flag) equals the
-    stepwise path's, including entry_length 1 (no persistent step) and 2 (one step);
-  * the margin-gated reference parity of tests/test_gpu_idparity.py runs this path too (bf16 at
-    <= 64 rows is persistent by default).
+  * ids AND decode state (pos, done, out_len, next_tok, step counter, finished flag) are
+    bit-identical across grids 48 / 96 / 192 and the phase launches at grids 48 / 96 / 192, on the
+    bench-scale goldens c1_greedy (std-0.1 weights) and c2_gpt2init (GPT-2's init scale) as well as
+    c2_margin_flat -- whatever grid a concurrent schedule picks, a caption does not change;
+  * on c2_margin_flat (reference margins large at every step) the ids equal the reference's;
+  * ragged batches (1, 7, 21 rows), entry_length 1 / 2 / 5 and temperature behave as the full
+    batch / the phase launches;
+  * a give-up (forced at the first barrier, or in the middle of the launch at a chosen step)
+    resumes from the last committed step on the phase launches with ids equal to an
+    uninterrupted run's, synchronously and under ConcurrentRunner.
 """
 import os
 import sys
@@ -24,6 +25,8 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
+GRIDS = (48, 96, 192)
+
 
 def _pipe(g, device, persist, batch=None, entry_length=None):
     from tools import idparity
@@ -35,165 +38,169 @@ def _pipe(g, device, persist, batch=None, entry_length=None):
                         entry_length=entry_length or int(g["entry_length"]),
                         persist_decode=persist)
     p = CaptionPipeline(csd, None, S.label_table(), S.label_token_table(), cfg, device=device)
-    assert p.decoder.persist == persist
+    assert p.decoder.persist == persist and p.decoder.grid_decode
     return p
 
 
 def _state(p, B):
     d = p.decoder
-    return {k: t[:B].cpu().numpy().copy() for k, t in
-            (("pos", d.pos), ("done", d.done), ("out_len", d.out_len), ("next_tok", d.next_tok))}
+    st = {k: t[:B].cpu().numpy().copy() for k, t in
+          (("pos", d.pos), ("done", d.done), ("out_len", d.out_len), ("next_tok", d.next_tok),
+           ("out_ids", d.out_ids))}
+    st["step_ctr"] = np.array([d.step_ctr.item()])
+    st["finished"] = np.array([d.all_done[0].item(), d.all_done[2].item()])
+    return st
 
 
-@pytest.fixture(scope="module")
-def flat():
-    from tools import idparity
-    return idparity.load("c2_margin_flat")
-
-
-def test_persist_equals_stepwise_and_reference(cuda, flat):
-    from tools import idparity
-    emb = torch.from_numpy(flat["clap_emb"]).to(cuda)
+def _run_all(g, device, emb, batch=None, entry_length=None):
+    """{(mode, grid): (captions, state)} for the persistent launch and the phase launches."""
+    res = {}
     B = emb.shape[0]
-    outs = {}
-    for persist in (True, False):
-        p = _pipe(flat, cuda, persist)
-        out = p.caption_emb(emb)
-        outs[persist] = (out.captions(), _state(p, B), p.decoder.step_ctr.item(),
-                         p.decoder.all_done.tolist())
-    (cp, sp, kp, ap), (cs, ss, ks, as_) = outs[True], outs[False]
-    assert cp == cs
-    for k in sp:
-        assert np.array_equal(sp[k], ss[k]), k
-    assert kp == ks and ap[0] == as_[0] == 1 and ap[2] == as_[2]
-    r = idparity.agreement(flat, cp)
-    assert r["exact_frac"] == 1.0, r
+    for mode in ("persist", "phases"):
+        p = _pipe(g, device, mode == "persist", batch=batch, entry_length=entry_length)
+        for grid in GRIDS:
+            if mode == "persist":
+                p.decoder.persist_grid = grid
+            else:
+                p.decoder.phase_grid = grid
+                p.decoder.graphs.clear()      # the captured chunk holds the old grid
+            out = p.caption_emb(emb)
+            res[mode, grid] = (out.captions(), _state(p, B))
+            assert p.decoder.gave_up == 0
+    return res
+
+
+def _assert_identical(res):
+    base = res["persist", 48]
+    for key, (caps, st) in res.items():
+        assert caps == base[0], key
+        for k in base[1]:
+            assert np.array_equal(st[k], base[1][k]), (key, k)
+
+
+@pytest.mark.parametrize("name", ["c1_greedy", "c2_gpt2init", "c2_margin_flat"])
+def test_grids_and_phases_bit_identical(cuda, name):
+    from tools import idparity
+    g = idparity.load(name)
+    emb = torch.from_numpy(g["clap_emb"]).to(cuda)
+    emb = emb[:64]
+    res = _run_all(g, cuda, emb)
+    _assert_identical(res)
+    caps = res["persist", 48][0]
+    if name == "c2_margin_flat":
+        assert idparity.agreement(g, caps)["exact_frac"] == 1.0
+    if "bf16_ref_err" in g:       # the stored-tolerance rule holds on the grid decode's ids
+        assert idparity.margin_gate(g, caps)["violations"] == []
+
+
+def test_full_batch_of_64(cuda):
+    """A full 64-row batch (every row block of every tile live): the golden's 32 clips twice."""
+    from tools import idparity
+    g = idparity.load("c2_margin_flat")
+    e = torch.from_numpy(g["clap_emb"]).to(cuda)
+    emb = torch.cat([e, e])[:64]
+    res = _run_all(g, cuda, emb, batch=64)
+    _assert_identical(res)
+    caps = res["persist", 192][0]
+    assert caps[:32] == caps[32:]
+    assert idparity.agreement(g, caps[:32])["exact_frac"] == 1.0
 
 
 @pytest.mark.parametrize("B", [1, 7, 21])
-def test_persist_ragged_batches(cuda, flat, B):
-    emb = torch.from_numpy(flat["clap_emb"]).to(cuda)
-    full = _pipe(flat, cuda, True).caption_emb(emb).captions()
-    p = _pipe(flat, cuda, True, batch=B)
-    for c0 in range(0, emb.shape[0], B):
-        got = p.caption_emb(emb[c0:c0 + B]).captions()
-        assert got == full[c0:c0 + B], c0
+def test_ragged_batches(cuda, B):
+    from tools import idparity
+    g = idparity.load("c2_gpt2init")
+    emb = torch.from_numpy(g["clap_emb"]).to(cuda)
+    full = _pipe(g, cuda, True).caption_emb(emb).captions()
+    for persist in (True, False):
+        p = _pipe(g, cuda, persist, batch=B)
+        for c0 in range(0, emb.shape[0], B):
+            got = p.caption_emb(emb[c0:c0 + B]).captions()
+            assert got == full[c0:c0 + B], (persist, c0)
 
 
 @pytest.mark.parametrize("entry", [1, 2, 5])
-def test_persist_short_entry_length(cuda, flat, entry):
-    emb = torch.from_numpy(flat["clap_emb"][:16]).to(cuda)
-    res = []
+def test_short_entry_length(cuda, entry):
+    from tools import idparity
+    g = idparity.load("c2_margin_flat")
+    emb = torch.from_numpy(g["clap_emb"][:16]).to(cuda)
+    res = {}
     for persist in (True, False):
-        p = _pipe(flat, cuda, persist, batch=16, entry_length=entry)
+        p = _pipe(g, cuda, persist, batch=16, entry_length=entry)
         out = p.caption_emb(emb)
-        res.append((out.captions(), _state(p, 16), p.decoder.step_ctr.item()))
-    assert res[0][0] == res[1][0]
-    for k in res[0][1]:
-        assert np.array_equal(res[0][1][k], res[1][1][k]), (entry, k)
-    assert res[0][2] <= entry   # the stepwise graph chunks run a few no-op steps past the end
+        res[persist] = (out.captions(), _state(p, 16))
+    assert res[True][0] == res[False][0]
+    for k in ("pos", "done", "out_len", "next_tok", "out_ids", "finished"):
+        assert np.array_equal(res[True][1][k], res[False][1][k]), (entry, k)
+    assert res[True][1]["step_ctr"][0] <= entry
 
 
-def test_persist_bench_weights_agreement(cuda):
-    """The bench's decoder weights (margins mostly within bf16 noise after a few steps): the two
-    bf16 paths agree on every clip's first generated ids and on most tokens."""
+def test_temperature(cuda):
+    """generate2's temperature (logits / T before the argmax): persistent == phase launches at
+    T = 0.7."""
     from tools import idparity
     g = idparity.load("c1_greedy")
-    emb = torch.from_numpy(g["clap_emb"]).to(cuda)
-    a = _pipe(g, cuda, True).caption_emb(emb).captions()
-    b = _pipe(g, cuda, False).caption_emb(emb).captions()
-    lead = [next((i for i, (x, y) in enumerate(zip(u, v)) if x != y), min(len(u), len(v)))
-            for u, v in zip(a, b)]
-    assert min(lead) >= 1, lead
-    assert np.mean(lead) >= 4, lead
-
-
-def test_persist_temperature(cuda, flat):
-    """generate2's temperature (logits / T before the argmax) in the persistent kernel: ids equal
-    the stepwise path's (zs_lmhead_topk_t) at T = 0.7 on the large-margin golden."""
-    emb = torch.from_numpy(flat["clap_emb"][:16]).to(cuda)
-    res = []
-    for persist in (True, False):
-        p = _pipe(flat, cuda, persist, batch=16)
-        p.decoder.temperature = 0.7
-        res.append(p.caption_emb(emb).captions())
-    assert res[0] == res[1]
-
-
-@pytest.mark.parametrize("B", [64, 7])
-def test_persist_grid_shapes(cuda, flat, B):
-    """Every grid shape (col_split, row_split) -- row_split 2: twice the workgroups, each a column
-    slice for half of the rows; col_split 2: half the workgroups, each two column slices -- gives
-    the ids and decode state of the default grid, and the reference's ids."""
-    from tools import idparity
-    emb = torch.from_numpy(flat["clap_emb"]).to(cuda)
-    emb = torch.cat([emb, emb])[:B]           # 64: the golden's 32 clips twice (a full batch)
-    from zsaac._lib import call
+    emb = torch.from_numpy(g["clap_emb"][:16]).to(cuda)
     res = {}
-    # fuse 1: the MLP as phases D' + R (mlp.c_proj partial sums, zs_tune_set dp_fuse)
-    for cs, rs, fuse in ((1, 1, 0), (1, 2, 0), (2, 1, 0), (2, 2, 0), (1, 1, 1), (2, 1, 1)):
-        p = _pipe(flat, cuda, True, batch=B)
-        p.decoder.persist_row_split, p.decoder.persist_col_split = rs, cs
-        call("zs_tune_set", b"dp_fuse", fuse)
-        try:
-            out = p.caption_emb(emb)
-        finally:
-            call("zs_tune_set", b"dp_fuse", 0)
-        res[cs, rs, fuse] = (out.captions(), _state(p, B), p.decoder.step_ctr.item())
-    base = res[1, 1, 0]
-    for shape, r in res.items():
-        assert r[0] == base[0], shape
-        for k in base[1]:
-            assert np.array_equal(r[1][k], base[1][k]), (shape, k)
-        assert r[2] == base[2], shape
-    if B == 64:
-        assert base[0][:32] == base[0][32:]
-        assert idparity.agreement(flat, base[0][:32])["exact_frac"] == 1.0
+    for persist in (True, False):
+        p = _pipe(g, cuda, persist, batch=16)
+        p.decoder.temperature = 0.7
+        res[persist] = p.caption_emb(emb).captions()
+    assert res[True] == res[False]
 
 
-def test_persist_give_up_resumes_stepwise(cuda, flat):
-    """A persistent launch whose grid barrier gives up (forced: zs_tune_set dp_spin < 0 gives up
-    at the first unmet poll) reports all_done[1] = -1 with its starting decode state intact; the
-    host resumes the batch on the per-step path and the ids equal a normal run's -- through
-    Gpt2Decoder.greedy (synchronous) and through ConcurrentRunner (two batches in flight)."""
+@pytest.mark.parametrize("how", ["first_poll", "step_3"])
+def test_give_up_resumes_on_phases(cuda, how):
+    """A persistent launch that gives up (forced: zs_tune_set dp_spin -1 gives up at the first
+    unmet poll; dp_abort_step 3: every workgroup gives up at the start of step 3, after steps
+    1-2 were committed) reports all_done[1] = -1; the host resumes from the committed state on
+    the phase launches and the ids equal an uninterrupted run's -- synchronously and through
+    ConcurrentRunner (two batches in flight)."""
+    from tools import idparity
     from zsaac._lib import call
     from zsaac.pipeline import ConcurrentRunner
-    emb = torch.from_numpy(flat["clap_emb"][:16]).to(cuda)
-    p = _pipe(flat, cuda, True, batch=16)
+    g = idparity.load("c2_gpt2init")
+    emb = torch.from_numpy(g["clap_emb"][:16]).to(cuda)
+    p = _pipe(g, cuda, True, batch=16)
     ref = p.caption_emb(emb).captions()
-    call("zs_tune_set", b"dp_spin", -1)
+    ref_state = _state(p, 16)
+    knob = (b"dp_spin", -1) if how == "first_poll" else (b"dp_abort_step", 3)
+    call("zs_tune_set", *knob)
     try:
         g0 = p.decoder.gave_up
         got = p.caption_emb(emb).captions()
         assert p.decoder.gave_up == g0 + 1, "the forced give-up did not happen"
         assert got == ref
-        runner = ConcurrentRunner(p, 2)
+        st = _state(p, 16)
+        for k in ("pos", "done", "out_len", "next_tok", "out_ids"):
+            assert np.array_equal(st[k], ref_state[k]), k
+        runner = ConcurrentRunner(p, 2, grids=[48], budget=512)
         runner.warmup_emb(emb[:8])
         outs = runner.run([emb[:8], emb[8:]], inputs="emb")
         assert [c for o in outs for c in o.captions()] == ref
-        assert sum(q.decoder.gave_up for q in runner.pipes) >= 2
+        assert runner.gave_up == 2
     finally:
-        call("zs_tune_set", b"dp_spin", 0)
+        call("zs_tune_set", knob[0], 0 if how == "first_poll" else -1)
     assert p.caption_emb(emb).captions() == ref
 
 
-def test_concurrent_runner_bf16_persist(cuda, flat):
-    """The headline's arrangement: bf16 batches through ConcurrentRunner (10 pipelines, persistent
-    grids of every shape -- 96 / 48 / 24 workgroups, chosen per batch by choose_persist_shape --
-    several in flight, ragged batches included): every batch's ids equal the single-stream
-    persistent run's and the reference's (c2_margin_flat, exact on every clip)."""
+def test_concurrent_runner_mixed_grids(cuda):
+    """The headline's arrangement: bf16 batches through ConcurrentRunner with grids 192 / 96 / 48
+    chosen per batch by choose_persist_grid (several in flight, ragged batches included): every
+    batch's ids equal the single-stream run's and the reference's (c2_margin_flat, exact on every
+    clip), and no launch gave up."""
     from tools import idparity
-    from zsaac.pipeline import ConcurrentRunner, persist_shapes
-    emb = torch.from_numpy(flat["clap_emb"]).to(cuda)
-    ref = [flat["greedy_ids"][b, :flat["greedy_len"][b]].tolist() for b in range(emb.shape[0])]
-    p = _pipe(flat, cuda, True)
-    single = p.caption_emb(emb).captions()
-    assert single == ref
-    runner = ConcurrentRunner(p, 10, shapes=persist_shapes("12,11,21"))
-    assert runner.n_inflight == 10
+    from zsaac.pipeline import ConcurrentRunner
+    g = idparity.load("c2_margin_flat")
+    emb = torch.from_numpy(g["clap_emb"]).to(cuda)
+    ref = [g["greedy_ids"][b, :g["greedy_len"][b]].tolist() for b in range(emb.shape[0])]
+    p = _pipe(g, cuda, True)
+    assert p.caption_emb(emb).captions() == ref
+    runner = ConcurrentRunner(p, 8, grids=[192, 96, 48], budget=384)
+    assert runner.n_inflight == 8
     runner.warmup_emb(emb)
     used = set()
-    for sizes in ([32] * 6 + [7, 3], [32, 21]):
+    for sizes in ([32] * 6 + [7, 3], [32, 21], [32, 32, 32]):
         batches, want = [], []
         for i, n in enumerate(sizes):
             rows = [(5 * i + j) % 32 for j in range(n)]
@@ -201,9 +208,9 @@ def test_concurrent_runner_bf16_persist(cuda, flat):
             want.append([ref[r] for r in rows])
         outs = runner.run(batches, inputs="emb")
         for i, o in enumerate(outs):
-            assert o.captions() == want[i], (sizes, i, runner.shape[i])
+            assert o.captions() == want[i], (sizes, i, runner.grid[i])
             assert int(o.lengths.shape[0]) == sizes[i]
-        used |= set(runner.shape[:len(sizes)])
+        used |= set(runner.grid[:len(sizes)])
         assert all(s >= 2 for s in runner.decode_steps[:len(sizes)])
-    assert {(1, 2), (1, 1), (2, 1)} <= used, used
-    assert sum(q.decoder.gave_up for q in runner.pipes) == 0
+    assert {192, 96, 48} <= used, used
+    assert runner.gave_up == 0

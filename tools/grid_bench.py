@@ -1,14 +1,15 @@
 #!/usr/bin/env python3
-"""The bs=64 persistent greedy decode (zs_gpt2_decode_persist) at each grid shape
-(col_split, row_split) -> workgroups per batch = 48 / col_split * row_split:
+"""The bs=64 greedy grid decode (decode_grid.hip) per grid size (256-thread workgroups):
 
-  * one batch alone: microseconds per decode step, and the generated ids against the
-    (1, 1) shape's (exact rows, token agreement);
+  * one batch alone: microseconds per decode step of the persistent launch
+    (zs_gpt2_decode_persist) and of the phase launches (zs_gpt2_decode_phases, the per-step
+    path), and the ids against grid 48's (they must be identical);
   * k batches at once on k pipeline twins / dedicated streams (decode only: every repetition
     restarts generate2 from the same prefill), aggregate decode steps per second and the
-    CU-microseconds one step costs (k x workgroups x wall / steps).
+    workgroup-microseconds one step costs (k x workgroups x wall / steps; a workgroup is half a
+    CU).
 
-    python tools/persist_grid_bench.py [reps=4] [shapes=11,21,22,12] [ks=1,2,4,5,8,10]
+    python tools/grid_bench.py [reps=4] [grids=48,96,192] [ks=1,2,4,5,8,10]
 """
 import json
 import os
@@ -28,7 +29,7 @@ os.environ["GPU_MAX_HW_QUEUES"] = "16"
 
 def main():
     reps = int(sys.argv[1]) if len(sys.argv) > 1 else 4
-    shapes = [(int(s[0]), int(s[1])) for s in (sys.argv[2] if len(sys.argv) > 2 else "11,21,22,12").split(",")]
+    grids = [int(g) for g in (sys.argv[2] if len(sys.argv) > 2 else "48,96,192").split(",")]
     ks = [int(k) for k in (sys.argv[3] if len(sys.argv) > 3 else "1,2,4,5,8,10").split(",")]
     from zsaac import ops
 
@@ -40,7 +41,7 @@ def main():
     cus = torch.cuda.get_device_properties(dev).multi_processor_count
     pipe, _, _ = bench.build(A, dev)
     wav = bench.synthetic_clips(64, 0, dev)
-    nmax = max(k for k in ks if k * min(ops.decode_persist_grid(rs, cs) for cs, rs in shapes) <= cus)
+    nmax = max(k for k in ks if k * min(grids) <= 2 * cus)
     pipes = [pipe] + [pipe.twin() for _ in range(nmax - 1)]
     streams = ops.dedicated_streams(nmax, dev)
     for p, s in zip(pipes, streams):
@@ -49,57 +50,63 @@ def main():
             p.caption_wav(wav)
     torch.cuda.synchronize()
 
-    def decode(ps, ss, cs, rs):
+    def decode(ps, ss, g):
         for p, s in zip(ps, ss):
-            p.decoder.persist_col_split, p.decoder.persist_row_split = cs, rs
+            p.decoder.persist_grid = g
             with torch.cuda.stream(s):
                 p.decoder.greedy_begin(64)
 
     res = {"cus": cus, "alone": {}, "concurrent": {}}
     ref = None
-    for cs, rs in shapes:
-        key = f"cs{cs}_rs{rs}"
-        g = ops.decode_persist_grid(rs, cs)
-        decode(pipes[:1], streams[:1], cs, rs)
+    dec = pipe.decoder
+    # the phase launches (one batch, eager: 62 launches per step)
+    dec.persist = False
+    dec.greedy_begin(64)
+    dec.run_to_completion()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    dec.greedy_begin(64)
+    dec.run_to_completion()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    steps = int(dec.step_ctr.item())
+    ref = (dec.out_ids[:64].clone(), dec.out_len[:64].clone())
+    res["phases"] = {"grid": dec.phase_grid, "us_per_step": round(dt * 1e6 / max(1, steps - 1), 1),
+                     "steps": steps, "note": "graph-replayed chunks incl. host polling"}
+    print(json.dumps({"phases": res["phases"]}), flush=True)
+    dec.persist = True
+    for g in grids:
+        key = f"g{g}"
+        decode(pipes[:1], streams[:1], g)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for _ in range(reps):
-            decode(pipes[:1], streams[:1], cs, rs)
+            decode(pipes[:1], streams[:1], g)
         torch.cuda.synchronize()
         dt = (time.perf_counter() - t0) / reps
-        dec = pipe.decoder
         assert int(dec.all_done[1].item()) >= 0, "gave up"
         steps = int(dec.step_ctr.item())
-        ids = dec.out_ids[:64].clone()
-        lens = dec.out_len[:64].clone()
+        ids, lens = dec.out_ids[:64].clone(), dec.out_len[:64].clone()
         r = {"workgroups": g, "decode_ms": round(dt * 1e3, 3), "steps": steps,
-             "us_per_step": round(dt * 1e6 / max(1, steps - 1), 1)}
-        if ref is None:
-            ref = (ids, lens)
-        else:
-            same = [(lens[i] == ref[1][i]).item() and bool((ids[i, :lens[i]] == ref[0][i, :lens[i]]).all())
-                    for i in range(64)]
-            n = torch.minimum(lens, ref[1])
-            agree = sum(int((ids[i, :n[i]] == ref[0][i, :n[i]]).sum()) for i in range(64))
-            r["rows_equal_to_cs1_rs1"] = sum(same)
-            r["token_agreement"] = round(agree / max(1, int(ref[1].sum())), 4)
+             "us_per_step": round(dt * 1e6 / max(1, steps - 1), 1),
+             "identical_to_phases": bool(torch.equal(ids, ref[0]) and torch.equal(lens, ref[1]))}
         res["alone"][key] = r
         print(json.dumps({key: r}), flush=True)
         conc = {}
         for k in ks:
-            if k * g > cus or k > nmax:
+            if k * g > 2 * cus or k > nmax:
                 continue
-            decode(pipes[:k], streams[:k], cs, rs)
+            decode(pipes[:k], streams[:k], g)
             torch.cuda.synchronize()
             t0 = time.perf_counter()
             for _ in range(reps):
-                decode(pipes[:k], streams[:k], cs, rs)
+                decode(pipes[:k], streams[:k], g)
             torch.cuda.synchronize()
             dt = time.perf_counter() - t0
             assert all(int(p.decoder.all_done[1].item()) >= 0 for p in pipes[:k]), "gave up"
             st = sum(int(p.decoder.step_ctr.item()) - 1 for p in pipes[:k]) * reps
             conc[k] = {"agg_steps_per_s": round(st / dt, 1),
-                       "cu_us_per_step": round(k * g * dt * 1e6 / st, 1)}
+                       "wg_us_per_step": round(k * g * dt * 1e6 / st, 1)}
         res["concurrent"][key] = conc
         print(json.dumps({key: conc}), flush=True)
     print(json.dumps(res), flush=True)

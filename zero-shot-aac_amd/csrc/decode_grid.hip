@@ -1,0 +1,1242 @@
+// GPT-2 greedy decode of ONE eval batch (R <= 64 rows, the reference's bs = 64): every step of
+// generate2 after step 0 (gpt2_prefix_eval.py:161-222 over transformers' GPT2LMHeadModel with a
+// KV cache) -- 12 blocks, ln_f, the tied LM head with its argmax and the stop / length
+// bookkeeping -- on a grid of G 4-wave workgroups, either
+//   * persistent: ONE launch runs every remaining step, phases separated by grid barriers
+//     (zs_gpt2_decode_persist), or
+//   * phase launches: each phase of each step is its own launch (zs_gpt2_decode_phases; the
+//     per-step path: no co-residency needed, graph-capturable, the give-up fallback),
+// and both run the SAME device code for every phase.
+//
+// Canonical arithmetic (why the grid size never changes a caption).  Every output element of
+// every phase is computed by one fixed sequence of operations whatever G is and whichever mode
+// runs it:
+//   * a GEMM element out[r][n] = sum_k a[r][k] W[n][k] is four partial sums, one per K quarter
+//     (wave w of the workgroup owning the element takes k in [K w / 4, K (w+1) / 4)), each an MFMA
+//     16x16x32 chain over its k-steps in increasing order from 0, added as (p0 + p1) + (p2 + p3);
+//     then + bias (and the activation / + residual).  The grid only decides WHICH workgroup owns
+//     an element (tiles of 16 x 16 are independent in the MFMA);
+//   * a LayerNorm row (ln_1 / ln_2 / ln_f) reads bf16(x), sums each wave's quarter in a fixed
+//     in-lane order, across the 4 lanes of a row by swap-adds, across the waves as (w0 + w1) +
+//     (w2 + w3): mean, then the squared deviations the same way (two-pass), rstd = rsqrt(q / 768 +
+//     1e-5);
+//   * an attention unit (row, head) runs the online softmax over its cached keys in 32-key chunks
+//     (8 lane groups x 4 keys), then folds in the new key;
+//   * the argmax over the vocabulary is exact (ties -> lower id, as torch.argmax).
+// So ids and decode state are identical for G = 48 / 96 / 192 and for the phase launches
+// (tests/test_gpu_persist.py asserts it).
+//
+// Why 4-wave workgroups (half a CU: 256 threads, <= 256 registers per lane, ~41 KB of LDS): a
+// persistent grid spends much of each step waiting on hand-offs; at 8 waves x 256 registers a
+// grid workgroup held its whole CU, so the other batches' encode / prefill kernels could not use
+// it while it waited (DESIGN.md §18 co-residency probe: a begin +50 % beside full-CU grids, +12 %
+// beside half-CU ones).  Each wave keeps its K quarter of the activation in registers (B operand
+// of a TRANSPOSED product: lane = (row r % 16, 4 consecutive output columns), so a lane's four
+// accumulators are 4 consecutive columns of one row: 8 / 16-byte epilogue stores), and the LDS
+// holds only the partial-sum slabs of the cross-wave reduction.
+//
+// Hand-offs (MI355X_MICROARCH.md § Workgroup dispatch, Valid forms row 1: sc1 stores, every
+// storing wave's vmcnt(0), a workgroup barrier, one lane's agent-scope add to a counter -- here 8
+// sharded counters -- and sc1 polls / loads):
+//   A  ln_1 + c_attn -> q [64][768] bf16; k / v straight into the KV cache at each row's pos
+//   B  attention (row, head) units -> att [4][24][64][8] bf16 (MFMA fragment order)
+//   C  attn.c_proj + residual -> x (f32, held in the owning thread's registers across the whole
+//      step; phase launches keep it in the workspace) and its bf16 copy xb (fragment order)
+//   D  ln_2 + c_fc + gelu_new -> hid [4][96][64][8] bf16
+//   E  mlp.c_proj + residual -> x, xb
+//   F  ln_f + LM head over vocab blocks b = w, w + G, ..: per-row best (logit, id) -> a 64-bit
+//      agent-scope atomic max of (order-preserving logit bits, ~id).  ln_f's affine is folded into
+//      the LM head: logit[v] = y . (g o wte[v]) + (beta . wte[v]) with y the normalised row (the
+//      table packed as bf16(g o wte), the per-token bias in f32), as ln_1 / ln_2 into c_attn / c_fc
+//   G  every workgroup applies generate2's bookkeeping to its LDS copy of the row state;
+//      workgroup 0 commits ids and state to memory after every step (a give-up resumes there)
+// 5 barriers per block + 1 after F = 61 per step.
+#include <type_traits>
+
+#include "common.h"
+
+// No implicit FP contraction in this file: whether the compiler fuses a multiply into a
+// following add depends on the surrounding code, which differs between the grid sizes' template
+// instances -- every fused multiply-add below is an explicit fmaf, so each instance rounds alike.
+#pragma clang fp contract(off)
+
+namespace zs {
+int g_dp_spin = 0;   // zs_tune_set("dp_spin", n): give up a grid-barrier wait after n polls (0 =
+                     // the default 2^22, < 0: at the first unmet poll); tests force the give-up
+int g_dp_abort = -1; // zs_tune_set("dp_abort_step", k): every workgroup gives up at the start of
+                     // decode step k (a mid-launch give-up for the resume test); -1 = never
+namespace dg {
+
+constexpr int D = 768, NH = 12, HD = 64, DFF = 3072, NLY = 12, RM = 64, QKVN = 3 * D;
+constexpr int NW = 4, NT = 64 * NW;
+constexpr int KSD = D / 32, KSF = DFF / 32;          // k-steps of K = 768 / 3072
+constexpr int QS = KSD / NW, QF = KSF / NW;          // k-steps of one wave's K quarter: 6 / 24
+constexpr int NCB_Q = QKVN / 16, NCB_D = D / 16, NCB_F = DFF / 16;   // 16-column blocks
+constexpr unsigned SPIN_MAX = 1u << 22;
+constexpr int NSH = 8;                               // barrier counter shards, one 128-B line each
+constexpr int KC = 4;                                // attention keys per lane group per chunk
+constexpr int ECH = 4;                               // phase E: k-steps per streamed chunk
+
+// Tiles per workgroup of each GEMM phase: CB column blocks x RB row blocks of 16 (workgroup w
+// takes column group w % (blocks / CB) and row group w / (blocks / CB)); PF = column blocks of
+// weights prefetched across the barrier (all of them, or one round's).  The grid size changes
+// only these ownerships, never the arithmetic of an element.
+template <int G> struct Geo;
+template <> struct Geo<48> {
+  static constexpr int ACB = 3, ARB = 4, APF = 2, DCB = 4, DRB = 4, DPF = 2, ECB = 2, ERB = 2;
+};
+template <> struct Geo<96> {
+  static constexpr int ACB = 3, ARB = 2, APF = 3, DCB = 4, DRB = 2, DPF = 4, ECB = 2, ERB = 1;
+};
+template <> struct Geo<192> {
+  static constexpr int ACB = 3, ARB = 1, APF = 3, DCB = 2, DRB = 2, DPF = 2, ECB = 1, ERB = 1;
+};
+template <int G> struct Units {
+  static constexpr int UPG = RM * NH / G;   // attention units per workgroup
+  static constexpr int KU = UPG / NW;       // per wave
+};
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8_t;
+typedef __attribute__((ext_vector_type(4))) float f32x4_t;
+typedef __attribute__((ext_vector_type(4))) unsigned u32x4_t;
+typedef __attribute__((ext_vector_type(2))) unsigned u32x2_t;
+typedef __attribute__((address_space(1))) unsigned gu32;
+typedef __attribute__((address_space(1))) unsigned long long gu64;
+typedef __attribute__((address_space(3))) int lds_int_t;
+
+// ------------------------------------------------------------------ workspace
+constexpr int WS_SH = 0;                          // NSH counters, 128 B apart
+constexpr int WS_TMO = NSH * 128;                 // timeout word
+constexpr int WS_KEY = WS_TMO + 128;              // u64 [2][64] LM-head argmax keys (step parity)
+constexpr int WS_SYNC_BYTES = 4096;               // zeroed by the launcher
+constexpr int WS_Q = WS_SYNC_BYTES;               // bf16 [64][768]
+constexpr int WS_ATT = WS_Q + RM * D * 2;         // bf16 [4][24][64][8] (fragment order)
+constexpr int WS_XB = WS_ATT + RM * D * 2;        // bf16 [4][24][64][8]
+constexpr int WS_HID = WS_XB + RM * D * 2;        // bf16 [4][96][64][8]
+constexpr int WS_X = WS_HID + RM * DFF * 2;       // f32  [64][768] (phase launches only)
+constexpr int WS_BYTES = WS_X + RM * D * 4;
+
+// ------------------------------------------------------------------ LDS (35,648 B)
+constexpr int SM_RED = 0;                         // f32x4 [2048]: partial slabs (32 KiB)
+constexpr int SM_LN = SM_RED + 32768;             // f32 [2][4][64]: LayerNorm partials
+constexpr int SM_ST = SM_LN + 2048;               // int tok[64], pos[64], done[64], misc[16]
+constexpr int SM_TOTAL = SM_ST + (3 * RM + 16) * 4;
+
+struct Args {
+  int R, Lmax, max_steps, stop0, stop1, V, layer, abort_step;
+  unsigned spin_max;
+  int kv_bytes;         // bytes of one layer's K (or V) cache
+  float temp;
+  const bf16_t* wte; const bf16_t* wpe;
+  // weights in MFMA fragment order (ops.pack_b_fragments): [N/16][K/32][64][8] bf16
+  const bf16_t* wq[NLY]; const float* bq[NLY];     // c_attn (ln_1 affine folded in), bias
+  const bf16_t* wo[NLY]; const float* bo[NLY];     // attn.c_proj
+  const bf16_t* wf[NLY]; const float* bfc[NLY];    // c_fc (ln_2 affine folded in)
+  const bf16_t* wm[NLY]; const float* bm[NLY];     // mlp.c_proj
+  const bf16_t* wtep;     // tied LM head with ln_f's weight folded in, fragment order
+  const float* lmb;       // beta . wte[v] (ln_f's bias through the LM head), [ceil(V/16) 16]
+  bf16_t* kc[NLY]; bf16_t* vc[NLY];
+  int* pos; int* next_tok; int* done; int* out_ids; int* out_len; int* step_ctr; int* all_done;
+  char* ws;
+};
+
+// ------------------------------------------------------------------ memory helpers
+struct Rs {
+  __amdgpu_buffer_rsrc_t q, att, xb, hid;
+};
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t mk(void* p, int bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(p, (short)0, bytes, 0x00020000);
+}
+__device__ __forceinline__ Rs make_rs(char* ws) {
+  Rs r;
+  r.q = mk(ws + WS_Q, RM * D * 2);
+  r.att = mk(ws + WS_ATT, RM * D * 2);
+  r.xb = mk(ws + WS_XB, RM * D * 2);
+  r.hid = mk(ws + WS_HID, RM * DFF * 2);
+  return r;
+}
+// aux 16 = sc1: stores write through, loads bypass this CU's L1 (the hand-off forms)
+__device__ __forceinline__ u32x4_t ld16(__amdgpu_buffer_rsrc_t r, int off) {
+  return __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 16);
+}
+__device__ __forceinline__ void st16(__amdgpu_buffer_rsrc_t r, int off, u32x4_t v) {
+  __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, 16);
+}
+__device__ __forceinline__ void st8(__amdgpu_buffer_rsrc_t r, int off, u32x2_t v) {
+  __builtin_amdgcn_raw_buffer_store_b64(v, r, off, 0, 16);
+}
+__device__ __forceinline__ bf16x8_t bf8(u32x4_t u) { return __builtin_bit_cast(bf16x8_t, u); }
+// transposed product: A = weight fragment (lane: output column n0 + l % 16), B = activation
+// fragment (lane: row l % 16); lane l then holds out[row l % 16][n0 + 4 (l / 16) + i], i < 4
+__device__ __forceinline__ f32x4_t mfma(u32x4_t w, u32x4_t a, f32x4_t c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf8(w), bf8(a), c, 0, 0, 0);
+}
+// threadIdx.x through an empty asm: lane arithmetic is recomputed per phase instead of being
+// hoisted out of the step loop (and spilled)
+__device__ __forceinline__ int otid() {
+  int t = threadIdx.x;
+  asm volatile("" : "+v"(t));
+  return t;
+}
+template <int CTRL>
+__device__ __forceinline__ float dppf(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xf, 0xf, false));
+}
+__device__ __forceinline__ float sum8(float s) {     // over the 8 lanes of each 8-lane group
+  s += dppf<0xB1>(s);
+  s += dppf<0x4E>(s);
+  return s + dppf<0x141>(s);
+}
+__device__ __forceinline__ float xor8(float v) { return dppf<0x128>(v); }   // row_ror:8
+// v + the partner lane's v (lane ^ 16 / lane ^ 32), the same value on both lanes
+__device__ __forceinline__ float add16(float v) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+__device__ __forceinline__ float add32(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+__device__ __forceinline__ float max16(float v) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float max32(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+// workgroup barrier for LDS hand-offs; waits for nothing in flight in vector memory
+__device__ __forceinline__ void lds_sync() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+__device__ __forceinline__ void unpack8(const u32x4_t& u, float (&f)[8]) {
+  f[0] = __uint_as_float(u.x << 16); f[1] = __uint_as_float(u.x & 0xffff0000u);
+  f[2] = __uint_as_float(u.y << 16); f[3] = __uint_as_float(u.y & 0xffff0000u);
+  f[4] = __uint_as_float(u.z << 16); f[5] = __uint_as_float(u.z & 0xffff0000u);
+  f[6] = __uint_as_float(u.w << 16); f[7] = __uint_as_float(u.w & 0xffff0000u);
+}
+__device__ __forceinline__ u32x4_t pack8(const float (&f)[8]) {
+  return u32x4_t{pk2bf(f[0], f[1]), pk2bf(f[2], f[3]), pk2bf(f[4], f[5]), pk2bf(f[6], f[7])};
+}
+template <int I, int N, typename F>
+__device__ __forceinline__ void static_for_i(F&& f) {
+  if constexpr (I < N) {
+    f(std::integral_constant<int, I>{});
+    static_for_i<I + 1, N>(f);
+  }
+}
+template <int N, typename F>
+__device__ __forceinline__ void static_for(F&& f) { static_for_i<0, N>(f); }
+
+// weight fragments (packed [nblk][KS][64][8]) of col blocks cb0 .. cb0 + NB, k-steps s0 .. s0 + S
+template <int NB, int S>
+__device__ __forceinline__ void ldw(const bf16_t* Wp, int KS, int cb0, int s0, u32x4_t* w) {
+  const int lane = otid() & 63;
+#pragma unroll
+  for (int nb = 0; nb < NB; ++nb)
+#pragma unroll
+    for (int s = 0; s < S; ++s)
+      w[nb * S + s] =
+          *reinterpret_cast<const u32x4_t*>(Wp + ((long)((cb0 + nb) * KS + s0 + s) * 64 + lane) * 8);
+}
+// handed-off activation fragments ([4][KS][64][8] bf16, sc1): row blocks rb0 .., k-steps s0 ..
+template <int NRB, int S>
+__device__ __forceinline__ void lda(__amdgpu_buffer_rsrc_t r, int KS, int rb0, int s0, u32x4_t* a) {
+  const int lane = otid() & 63;
+#pragma unroll
+  for (int rb = 0; rb < NRB; ++rb)
+#pragma unroll
+    for (int s = 0; s < S; ++s) a[rb * S + s] = ld16(r, (((rb0 + rb) * KS + s0 + s) * 64 + lane) * 16);
+}
+// byte offset of element (row, col) (col % 4 == 0) in a fragment-order activation of KS k-steps
+__device__ __forceinline__ int frag_off(int row, int col, int KS) {
+  return ((((row >> 4) * KS + (col >> 5)) * 64 + (row & 15) + 16 * ((col >> 3) & 3)) * 8 + (col & 7)) * 2;
+}
+
+// ------------------------------------------------------------------ diagnostic stamps
+// zs_decode_persist_set_stamps(buf, step): thread 0 of every workgroup writes s_memrealtime
+// (100 MHz) after each barrier arrive (slot 2i) and wait (2i + 1) of decode step `step`, and at
+// its start (127) / end (126), into buf[w][128] (tools/persist_stamps.py).  NULL = off.
+__device__ unsigned long long* dp_stamp_buf;
+__device__ int dp_stamp_step;
+#define DP_NB 64
+__device__ __forceinline__ void stamp(unsigned long long* sb, int slot) {
+  if (sb != nullptr && threadIdx.x == 0) {
+    unsigned long long t;
+    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    ((gu64*)sb)[slot] = t;
+  }
+}
+
+// ------------------------------------------------------------------ grid barrier
+// Producer (R1): every storing wave drains its sc1 stores, the workgroup meets, ONE lane adds to
+// its shard (w % 8) of the counter.  Consumer: lanes 0..7 of wave 0 poll the 8 shards (relaxed
+// sc1 loads), the workgroup meets, then every load of handed-off bytes is an sc1 load.  arrive()
+// and wait() are split so a workgroup issues its next phase's weight loads in between.
+struct Bar {
+  gu32* sh;
+  gu32* tmo;
+  unsigned n;               // barriers passed
+  unsigned per;             // workgroups per shard
+  unsigned spin_max;
+  unsigned long long* sb;   // this workgroup's stamp row of the traced step (or NULL)
+  unsigned n0;
+};
+__device__ __forceinline__ void bar_arrive(Bar& b, int w) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  if (threadIdx.x == 0)
+    __hip_atomic_fetch_add(b.sh + (w & (NSH - 1)) * 32, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  stamp(b.sb, 2 * (b.n - b.n0));
+  ++b.n;
+}
+__device__ __forceinline__ bool bar_wait(Bar& b, volatile lds_int_t* s_ok) {
+  if (threadIdx.x < 64) {
+    const int lane = threadIdx.x;
+    const unsigned target = b.n * b.per;
+    unsigned spins = 0;
+    int ok = 1;
+    for (;;) {
+      const unsigned c = lane < NSH
+          ? __hip_atomic_load(b.sh + lane * 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : target;
+      if (__ballot(c < target) == 0) break;
+      ++spins;
+      // bounded: give up (and tell every other workgroup) after spin_max polls, so a grid that
+      // is not co-resident drains instead of hanging
+      if (spins > b.spin_max ||
+          ((spins & 255) == 0 && __hip_atomic_load(b.tmo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
+        if (lane == 0) __hip_atomic_store(b.tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        ok = 0;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    if (lane == 0) *s_ok = ok;
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  stamp(b.sb, 2 * (b.n - b.n0) - 1);
+  return *s_ok != 0;
+}
+
+// ------------------------------------------------------------------ LDS views
+struct Sm {
+  f32x4_t* red;
+  float* ln;
+  int* tok;
+  int* pos;
+  int* done;
+  int* misc;     // [0] rows still decoding, [8] barrier ok flag
+  __device__ __forceinline__ explicit Sm(char* s)
+      : red(reinterpret_cast<f32x4_t*>(s + SM_RED)), ln(reinterpret_cast<float*>(s + SM_LN)),
+        tok(reinterpret_cast<int*>(s + SM_ST)),
+        pos(reinterpret_cast<int*>(s + SM_ST) + RM), done(reinterpret_cast<int*>(s + SM_ST) + 2 * RM),
+        misc(reinterpret_cast<int*>(s + SM_ST) + 3 * RM) {}
+};
+
+// ------------------------------------------------------------------ cross-wave reduction
+// The 4 waves' partial tiles (acc[t], t < T: this wave's K quarter) summed as (w0 + w1) + (w2 +
+// w3) through LDS; wave v finalises tiles t = 4 j + v: epi(j, t, sum) with the lane's 4 columns
+// (j is a compile-time index after unrolling: per-tile operands live in arrays indexed by j).
+template <int T, typename Epi>
+__device__ __forceinline__ void reduce_tiles(f32x4_t* red, const f32x4_t (&acc)[T], Epi&& epi) {
+  static_assert(T * NW * 64 <= 2048, "partial slabs fit the LDS region");
+  const int tid = otid(), v = tid >> 6, lane = tid & 63;
+  lds_sync();                 // the previous round's readers are done with the slabs
+#pragma unroll
+  for (int t = 0; t < T; ++t) red[(v * T + t) * 64 + lane] = acc[t];
+  lds_sync();
+#pragma unroll
+  for (int j = 0; j * NW < T; ++j) {
+    const int t = NW * j + v;
+    if (t < T) {
+      const f32x4_t p0 = red[t * 64 + lane], p1 = red[(T + t) * 64 + lane];
+      const f32x4_t p2 = red[(2 * T + t) * 64 + lane], p3 = red[(3 * T + t) * 64 + lane];
+      epi(j, t, (p0 + p1) + (p2 + p3));
+    }
+  }
+}
+
+// ------------------------------------------------------------------ LayerNorm in registers
+// an opaque redefinition of fragments: keeps the compiler from merging the unpacks of the
+// LayerNorm's three passes (it held all 192 unpacked f32 values across them, and spilled)
+template <int N>
+__device__ __forceinline__ void opaque(u32x4_t* x) {
+#pragma unroll
+  for (int i = 0; i < N; ++i) asm volatile("" : "+v"(x[i]));
+}
+// xf: this wave's K-quarter fragments of row blocks rb0 .. rb0 + NRB (lane: row 16 rb + l % 16,
+// columns 32 (6 v + i) + 8 (l / 16) .. + 8), normalised in place (bf16; every LayerNorm's affine is
+// folded into the GEMM that consumes it).
+template <int NRB>
+__device__ __forceinline__ void ln_frags(u32x4_t* xf, const Sm& sm, int rb0) {
+  const int tid = otid(), v = tid >> 6, lane = tid & 63, fr = lane & 15;
+  float mean[NRB], rstd[NRB];
+#pragma unroll
+  for (int rb = 0; rb < NRB; ++rb) {
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < QS; ++i) {
+      float f[8];
+      unpack8(xf[rb * QS + i], f);
+      s += ((f[0] + f[1]) + (f[2] + f[3])) + ((f[4] + f[5]) + (f[6] + f[7]));
+    }
+    s = add32(add16(s));
+    if (lane < 16) sm.ln[v * RM + 16 * (rb0 + rb) + fr] = s;
+  }
+  opaque<NRB * QS>(xf);
+  lds_sync();
+#pragma unroll
+  for (int rb = 0; rb < NRB; ++rb) {
+    const int r = 16 * (rb0 + rb) + fr;
+    mean[rb] = ((sm.ln[r] + sm.ln[RM + r]) + (sm.ln[2 * RM + r] + sm.ln[3 * RM + r])) * (1.0f / D);
+    float q = 0.f;
+#pragma unroll
+    for (int i = 0; i < QS; ++i) {
+      float f[8];
+      unpack8(xf[rb * QS + i], f);
+#pragma unroll
+      for (int t = 0; t < 8; ++t) f[t] -= mean[rb];
+      q += (fmaf(f[1], f[1], f[0] * f[0]) + fmaf(f[3], f[3], f[2] * f[2])) +
+           (fmaf(f[5], f[5], f[4] * f[4]) + fmaf(f[7], f[7], f[6] * f[6]));
+    }
+    q = add32(add16(q));
+    if (lane < 16) sm.ln[NW * RM + v * RM + r] = q;
+  }
+  opaque<NRB * QS>(xf);
+  lds_sync();
+#pragma unroll
+  for (int rb = 0; rb < NRB; ++rb) {
+    const int r = 16 * (rb0 + rb) + fr;
+    const float* l2 = sm.ln + NW * RM;
+    rstd[rb] = rsqrtf(((l2[r] + l2[RM + r]) + (l2[2 * RM + r] + l2[3 * RM + r])) * (1.0f / D) + 1e-5f);
+#pragma unroll
+    for (int i = 0; i < QS; ++i) {
+      float f[8];
+      unpack8(xf[rb * QS + i], f);
+#pragma unroll
+      for (int t = 0; t < 8; ++t) f[t] = (f[t] - mean[rb]) * rstd[rb];
+      xf[rb * QS + i] = pack8(f);
+    }
+  }
+}
+
+// layer 0's LayerNorm input: bf16(wte[tok] + wpe[pos]) (the f32 sum rounded once)
+template <int NRB>
+__device__ __forceinline__ void embed_frags(const Args& a, const Sm& sm, int rb0, u32x4_t* xf) {
+  const int tid = otid(), v = tid >> 6, lane = tid & 63, fr = lane & 15, fk = 8 * (lane >> 4);
+#pragma unroll
+  for (int rb = 0; rb < NRB; ++rb) {
+    const int row = 16 * (rb0 + rb) + fr;
+    const bf16_t* te = a.wte + (long)sm.tok[row] * D + fk;
+#pragma unroll
+    for (int i = 0; i < QS; ++i)
+      xf[rb * QS + i] = *reinterpret_cast<const u32x4_t*>(te + 32 * (QS * v + i));
+  }
+#pragma unroll
+  for (int rb = 0; rb < NRB; ++rb) {
+    const int row = 16 * (rb0 + rb) + fr;
+    const bf16_t* pe = a.wpe + (long)sm.pos[row] * D + fk;
+    u32x4_t pu[QS];
+#pragma unroll
+    for (int i = 0; i < QS; ++i) pu[i] = *reinterpret_cast<const u32x4_t*>(pe + 32 * (QS * v + i));
+#pragma unroll
+    for (int i = 0; i < QS; ++i) {
+      float t[8], p[8];
+      unpack8(xf[rb * QS + i], t);
+      unpack8(pu[i], p);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) t[e] += p[e];
+      xf[rb * QS + i] = pack8(t);
+    }
+  }
+}
+// the f32 embedding quad (row, col .. col + 3): the residual stream at layer 0
+__device__ __forceinline__ float4 embed_quad(const Args& a, const Sm& sm, int row, int col) {
+  const uint2 t = *reinterpret_cast<const uint2*>(a.wte + (long)sm.tok[row] * D + col);
+  const uint2 p = *reinterpret_cast<const uint2*>(a.wpe + (long)sm.pos[row] * D + col);
+  return make_float4(__uint_as_float(t.x << 16) + __uint_as_float(p.x << 16),
+                     __uint_as_float(t.x & 0xffff0000u) + __uint_as_float(p.x & 0xffff0000u),
+                     __uint_as_float(t.y << 16) + __uint_as_float(p.y << 16),
+                     __uint_as_float(t.y & 0xffff0000u) + __uint_as_float(p.y & 0xffff0000u));
+}
+
+// ------------------------------------------------------------------ A / D: LayerNorm + GEMM
+// The tile's CB col blocks x RB row blocks in rounds of CPR col blocks (<= 8 tiles of slabs);
+// weights: PF == CB (all in wpf) or PF == CPR (wpf holds one round; loadw(c, n, wpf) refills it
+// with the n col blocks from c after a round's MFMAs).  epi(r, j, c, rb, sum) per finalised quad
+// (round r, j as reduce_tiles).
+template <int CB, int RB>
+struct Rounds {
+  static constexpr int CPR = CB < 8 / RB ? CB : 8 / RB;      // col blocks per round
+  static constexpr int NR = (CB + CPR - 1) / CPR;             // rounds
+  static constexpr int NJ = (CPR * RB + NW - 1) / NW;         // finalised tiles per wave per round
+};
+// per-(round, j) operand quads of the tiles this wave finalises: f(c) for col block c of the tile
+template <int CB, int RB, int NR, int NJ, typename F>
+__device__ __forceinline__ void round_quads(float4 (&q)[NR][NJ], F&& f) {
+  using Rn = Rounds<CB, RB>;
+  static_assert(NR == Rn::NR && NJ == Rn::NJ, "round_quads shape");
+  const int v = otid() >> 6;
+#pragma unroll
+  for (int r = 0; r < NR; ++r)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int t = NW * j + v, c = r * Rn::CPR + t / RB;
+      q[r][j] = (t < Rn::CPR * RB && c < CB) ? f(c) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+}
+template <int CB, int RB, int PF, typename LoadW, typename Epi>
+__device__ __forceinline__ void gemm_rounds(const u32x4_t* xf, u32x4_t* wpf, f32x4_t* red,
+                                            LoadW&& loadw, Epi&& epi) {
+  constexpr int CPR = Rounds<CB, RB>::CPR, NR = Rounds<CB, RB>::NR;
+  static_assert(PF == CB || PF == CPR, "weight prefetch rounds");
+  static_for<NR>([&](auto rr) {
+    constexpr int r = decltype(rr)::value, c0 = r * CPR;
+    constexpr int NC = CB - c0 < CPR ? CB - c0 : CPR;
+    f32x4_t acc[NC * RB];
+#pragma unroll
+    for (int t = 0; t < NC * RB; ++t) acc[t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < QS; ++s)
+#pragma unroll
+      for (int c = 0; c < NC; ++c)
+#pragma unroll
+        for (int rb = 0; rb < RB; ++rb)
+          acc[c * RB + rb] = mfma(wpf[((PF == CB ? c0 : 0) + c) * QS + s], xf[rb * QS + s], acc[c * RB + rb]);
+    if constexpr (PF != CB && c0 + CPR < CB) {
+      loadw(c0 + CPR, std::integral_constant<int, (CB - c0 - CPR < CPR ? CB - c0 - CPR : CPR)>{}, wpf);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    reduce_tiles<NC * RB>(red, acc, [&](int j, int t, f32x4_t s) { epi(r, j, c0 + t / RB, t % RB, s); });
+  });
+}
+
+// A: ln_1 + c_attn.  q -> WS_Q; k / v -> the KV cache at the row's position (sc1: phase B reads
+// them in this step).  wq: the prefetched weights (PM: loaded here).
+template <int G, bool PM>
+__device__ __forceinline__ void phase_a(const Args& a, const Rs& rs, int l, int w, const Sm& sm,
+                                        u32x4_t* wq) {
+  using Gm = Geo<G>;
+  constexpr int CB = Gm::ACB, RB = Gm::ARB, NCG = NCB_Q / CB;
+  const int tid = otid(), v = tid >> 6, lane = tid & 63;
+  const int cb0 = (w % NCG) * CB, rb0 = (w / NCG) * RB;
+  u32x4_t xf[RB * QS];
+  if (l == 0) embed_frags<RB>(a, sm, rb0, xf);
+  else lda<RB, QS>(rs.xb, KSD, rb0, QS * v, xf);
+  if constexpr (PM) ldw<Gm::APF, QS>(a.wq[l], KSD, cb0, QS * v, wq);
+  using Rn = Rounds<CB, RB>;
+  float4 bq[Rn::NR][Rn::NJ];
+  round_quads<CB, RB>(bq, [&](int c) {
+    return *reinterpret_cast<const float4*>(a.bq[l] + 16 * (cb0 + c) + 4 * (lane >> 4));
+  });
+  __builtin_amdgcn_sched_barrier(0);
+  ln_frags<RB>(xf, sm, rb0);
+  const __amdgpu_buffer_rsrc_t rk = mk(a.kc[l], a.kv_bytes), rv = mk(a.vc[l], a.kv_bytes);
+  gemm_rounds<CB, RB, Gm::APF>(xf, wq, sm.red,
+      [&](int c, auto n, u32x4_t* wr) { ldw<decltype(n)::value, QS>(a.wq[l], KSD, cb0 + c, QS * (otid() >> 6), wr); },
+      [&](int r, int j, int c, int rb, f32x4_t s) {
+        const int row = 16 * (rb0 + rb) + (lane & 15), col = 16 * (cb0 + c) + 4 * (lane >> 4);
+        if (row >= a.R) return;
+        const float4 b = bq[r][j];
+        const u32x2_t o{pk2bf(s[0] + b.x, s[1] + b.y), pk2bf(s[2] + b.z, s[3] + b.w)};
+        if (col < D) {
+          st8(rs.q, (row * D + col) * 2, o);
+        } else {
+          const int j = col - D, kv = j >= D, jj = kv ? j - D : j;
+          const int off = ((((row * NH + jj / HD) * a.Lmax) + sm.pos[row]) * HD + (jj % HD)) * 2;
+          st8(kv ? rv : rk, off, o);
+        }
+      });
+}
+
+// D: ln_2 + c_fc + gelu_new -> hid (fragment order).  wf: the first round's prefetched weights.
+__device__ __forceinline__ float gelu_new_fast(float x) {
+  const float u2 = -1.5957691216057308f * fmaf(0.044715f * x * x, x, x);
+  return x * __builtin_amdgcn_rcpf(1.0f + __expf(u2));
+}
+template <int G, bool PM>
+__device__ __forceinline__ void phase_d(const Args& a, const Rs& rs, int l, int w, const Sm& sm,
+                                        u32x4_t* wf) {
+  using Gm = Geo<G>;
+  constexpr int CB = Gm::DCB, RB = Gm::DRB, NCG = NCB_F / CB;
+  const int tid = otid(), v = tid >> 6, lane = tid & 63;
+  const int cb0 = (w % NCG) * CB, rb0 = (w / NCG) * RB;
+  u32x4_t xf[RB * QS];
+  lda<RB, QS>(rs.xb, KSD, rb0, QS * v, xf);
+  if constexpr (PM) ldw<Gm::DPF, QS>(a.wf[l], KSD, cb0, QS * v, wf);
+  using Rn = Rounds<CB, RB>;
+  float4 bb[Rn::NR][Rn::NJ];
+  round_quads<CB, RB>(bb, [&](int c) {
+    return *reinterpret_cast<const float4*>(a.bfc[l] + 16 * (cb0 + c) + 4 * (lane >> 4));
+  });
+  __builtin_amdgcn_sched_barrier(0);
+  ln_frags<RB>(xf, sm, rb0);
+  gemm_rounds<CB, RB, Gm::DPF>(xf, wf, sm.red,
+      [&](int c, auto n, u32x4_t* wr) { ldw<decltype(n)::value, QS>(a.wf[l], KSD, cb0 + c, QS * (otid() >> 6), wr); },
+      [&](int r, int j, int c, int rb, f32x4_t s) {
+        const int row = 16 * (rb0 + rb) + (lane & 15), col = 16 * (cb0 + c) + 4 * (lane >> 4);
+        if (row >= a.R) return;
+        const float4 b = bb[r][j];
+        st8(rs.hid, frag_off(row, col, KSF),
+            u32x2_t{pk2bf(gelu_new_fast(s[0] + b.x), gelu_new_fast(s[1] + b.y)),
+                    pk2bf(gelu_new_fast(s[2] + b.z), gelu_new_fast(s[3] + b.w))});
+      });
+}
+
+// ------------------------------------------------------------------ C / E: projection + residual
+// The residual quad this thread owns (tile t = wave v of the C / E tiling; T <= 4 in every
+// geometry): x_old from the embedding (layer 0), from the owner's registers (persistent) or from
+// the workspace (phase launches); x_new = (sum + bias) + x_old -> registers / workspace and xb.
+template <int G>
+__device__ __forceinline__ void ce_tile(int w, int t, int& row, int& col) {
+  using Gm = Geo<G>;
+  constexpr int NCG = NCB_D / Gm::ECB;
+  const int lane = otid() & 63;
+  const int cb0 = (w % NCG) * Gm::ECB, rb0 = (w / NCG) * Gm::ERB;
+  row = 16 * (rb0 + t % Gm::ERB) + (lane & 15);
+  col = 16 * (cb0 + t / Gm::ERB) + 4 * (lane >> 4);
+}
+// (embed: the step's first residual update -- phase C of layer 0 -- whose x_old is the embedding)
+template <int G, bool PM>
+__device__ __forceinline__ void ce_operands(const Args& a, const Sm& sm, bool embed, int w,
+                                            const float* bias, const f32x4_t& xo, float4& b,
+                                            float4& xold) {
+  constexpr int T = Geo<G>::ECB * Geo<G>::ERB;
+  const int v = otid() >> 6;
+  b = make_float4(0.f, 0.f, 0.f, 0.f);
+  xold = b;
+  if (v < T) {
+    int row, col;
+    ce_tile<G>(w, v, row, col);
+    b = *reinterpret_cast<const float4*>(bias + col);
+    if (embed) {
+      xold = embed_quad(a, sm, row, col);
+    } else if constexpr (PM) {
+      xold = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(a.ws + WS_X) + row * D + col);
+    } else {
+      xold = make_float4(xo[0], xo[1], xo[2], xo[3]);
+    }
+  }
+}
+template <int G, bool PM>
+__device__ __forceinline__ void ce_epilogue(const Args& a, const Rs& rs, int w, int t, f32x4_t s,
+                                            const float4& b, const float4& xold, f32x4_t& xo) {
+  int row, col;
+  ce_tile<G>(w, t, row, col);
+  const f32x4_t o{(s[0] + b.x) + xold.x, (s[1] + b.y) + xold.y, (s[2] + b.z) + xold.z,
+                  (s[3] + b.w) + xold.w};
+  xo = o;
+  if (row < a.R) {
+    st8(rs.xb, frag_off(row, col, KSD), u32x2_t{pk2bf(o[0], o[1]), pk2bf(o[2], o[3])});
+    if constexpr (PM)
+      *reinterpret_cast<float4*>(reinterpret_cast<float*>(a.ws + WS_X) + row * D + col) =
+          make_float4(o[0], o[1], o[2], o[3]);
+  }
+}
+
+// C: attn.c_proj + residual (K = 768, all 6 k-steps of the quarter at once)
+template <int G, bool PM>
+__device__ __forceinline__ void phase_c(const Args& a, const Rs& rs, int l, int w, const Sm& sm,
+                                        u32x4_t* wo, f32x4_t& xo) {
+  using Gm = Geo<G>;
+  constexpr int CB = Gm::ECB, RB = Gm::ERB, T = CB * RB, NCG = NCB_D / CB;
+  const int v = otid() >> 6;
+  const int cb0 = (w % NCG) * CB, rb0 = (w / NCG) * RB;
+  u32x4_t af[RB * QS];
+  lda<RB, QS>(rs.att, KSD, rb0, QS * v, af);
+  if constexpr (PM) ldw<CB, QS>(a.wo[l], KSD, cb0, QS * v, wo);
+  float4 b, xold;
+  ce_operands<G, PM>(a, sm, l == 0, w, a.bo[l], xo, b, xold);
+  __builtin_amdgcn_sched_barrier(0);
+  f32x4_t acc[T];
+#pragma unroll
+  for (int t = 0; t < T; ++t) acc[t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int s = 0; s < QS; ++s)
+#pragma unroll
+    for (int c = 0; c < CB; ++c)
+#pragma unroll
+      for (int rb = 0; rb < RB; ++rb) acc[c * RB + rb] = mfma(wo[c * QS + s], af[rb * QS + s], acc[c * RB + rb]);
+  reduce_tiles<T>(sm.red, acc, [&](int, int t, f32x4_t s) { ce_epilogue<G, PM>(a, rs, w, t, s, b, xold, xo); });
+}
+
+// E: mlp.c_proj + residual (K = 3072: the quarter's 24 k-steps streamed in chunks of ECH, two in
+// flight; wm holds the first two chunks' weights: prefetched, or loaded here (PM))
+template <int G, bool PM>
+__device__ __forceinline__ void phase_e(const Args& a, const Rs& rs, int l, int w, const Sm& sm,
+                                        u32x4_t* wm, f32x4_t& xo) {
+  using Gm = Geo<G>;
+  constexpr int CB = Gm::ECB, RB = Gm::ERB, T = CB * RB, NCG = NCB_D / CB, NCH = QF / ECH;
+  const int v = otid() >> 6;
+  const int cb0 = (w % NCG) * CB, rb0 = (w / NCG) * RB, s0 = QF * v;
+  if constexpr (PM) {
+    ldw<CB, ECH>(a.wm[l], KSF, cb0, s0, wm);
+    ldw<CB, ECH>(a.wm[l], KSF, cb0, s0 + ECH, wm + CB * ECH);
+  }
+  u32x4_t af[2 * RB * ECH];
+  lda<RB, ECH>(rs.hid, KSF, rb0, s0, af);
+  lda<RB, ECH>(rs.hid, KSF, rb0, s0 + ECH, af + RB * ECH);
+  float4 b, xold;
+  ce_operands<G, PM>(a, sm, false, w, a.bm[l], xo, b, xold);
+  __builtin_amdgcn_sched_barrier(0);
+  f32x4_t acc[T];
+#pragma unroll
+  for (int t = 0; t < T; ++t) acc[t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  static_for<NCH>([&](auto cc) {
+    constexpr int c = decltype(cc)::value, sl = c & 1;
+#pragma unroll
+    for (int s = 0; s < ECH; ++s)
+#pragma unroll
+      for (int cb = 0; cb < CB; ++cb)
+#pragma unroll
+        for (int rb = 0; rb < RB; ++rb)
+          acc[cb * RB + rb] = mfma(wm[(sl * CB + cb) * ECH + s], af[(sl * RB + rb) * ECH + s], acc[cb * RB + rb]);
+    if constexpr (c + 2 < NCH) {
+      ldw<CB, ECH>(a.wm[l], KSF, cb0, s0 + ECH * (c + 2), wm + sl * CB * ECH);
+      lda<RB, ECH>(rs.hid, KSF, rb0, s0 + ECH * (c + 2), af + sl * RB * ECH);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  });
+  reduce_tiles<T>(sm.red, acc, [&](int, int t, f32x4_t s) { ce_epilogue<G, PM>(a, rs, w, t, s, b, xold, xo); });
+}
+
+// ------------------------------------------------------------------ B: attention
+// unit u = (row u / 12, head u % 12); wave v of workgroup w takes units w UPG + v KU .. + KU.
+// 8 lanes per key (lane sub = l % 8 holds dims 8 sub .. + 8), 8 key groups (grp = l / 8), chunks
+// of 8 KC keys; online softmax in f32.  The cached keys 0 .. pos - 1 are read with plain loads
+// (chunk 0 issued before the workgroup waits on the c_attn barrier); the new key / value (pos)
+// and q are hand-offs (sc1).
+__device__ __forceinline__ void attn_unit(const Args& a, const Sm& sm, int u, int& row, int& hh,
+                                          int& p, long& base) {
+  row = u / NH;
+  hh = u % NH;
+  const int rr = min(row, a.R - 1);
+  p = min(sm.pos[rr], a.Lmax - 1);
+  base = ((long)(rr * NH + hh) * a.Lmax) * HD + 8 * ((otid() & 63) & 7);
+}
+template <int KU>
+__device__ __forceinline__ void attn_load(const Args& a, int l, const Sm& sm, int ub, int cb,
+                                          u32x4_t (&kr)[KU][KC], u32x4_t (&vr)[KU][KC]) {
+  const int tid = otid(), v = tid >> 6, grp = (tid & 63) >> 3;
+  const bf16_t* kc = a.kc[l];
+  const bf16_t* vc = a.vc[l];
+#pragma unroll
+  for (int k = 0; k < KU; ++k) {
+    int row, hh, p;
+    long base;
+    attn_unit(a, sm, ub + KU * v + k, row, hh, p, base);
+#pragma unroll
+    for (int i = 0; i < KC; ++i) {
+      const int jc = max(min(cb + 8 * i + grp, p - 1), 0);
+      kr[k][i] = __builtin_nontemporal_load(reinterpret_cast<const u32x4_t*>(kc + base + (long)jc * HD));
+      vr[k][i] = __builtin_nontemporal_load(reinterpret_cast<const u32x4_t*>(vc + base + (long)jc * HD));
+    }
+  }
+}
+template <int KU>
+__device__ __forceinline__ void phase_b(const Args& a, const Rs& rs, int l, const Sm& sm, int ub,
+                                        u32x4_t (&kr)[KU][KC], u32x4_t (&vr)[KU][KC]) {
+  const int tid = otid(), lane = tid & 63, v = tid >> 6, grp = lane >> 3, sub = lane & 7;
+  const __amdgpu_buffer_rsrc_t rk = mk(a.kc[l], a.kv_bytes), rv = mk(a.vc[l], a.kv_bytes);
+  float q[KU][8], o[KU][8], m[KU], sum[KU];
+  int p[KU], row[KU], hh[KU];
+  long base[KU];
+  u32x4_t qu[KU];
+#pragma unroll
+  for (int k = 0; k < KU; ++k) {
+    attn_unit(a, sm, ub + KU * v + k, row[k], hh[k], p[k], base[k]);
+    qu[k] = ld16(rs.q, (min(row[k], a.R - 1) * D + hh[k] * HD + 8 * sub) * 2);
+  }
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int k = 0; k < KU; ++k) {
+    unpack8(qu[k], q[k]);
+#pragma unroll
+    for (int t = 0; t < 8; ++t) { q[k][t] *= 0.125f; o[k][t] = 0.f; }
+    m[k] = -INFINITY;
+    sum[k] = 0.f;
+  }
+  int pmax = p[0];
+#pragma unroll
+  for (int k = 1; k < KU; ++k) pmax = max(pmax, p[k]);
+  for (int cb = 0; cb < pmax; cb += 8 * KC) {
+    if (cb > 0) attn_load<KU>(a, l, sm, ub, cb, kr, vr);
+#pragma unroll
+    for (int k = 0; k < KU; ++k) {
+      if (cb >= p[k]) continue;                   // wave-uniform
+      float sc[KC];
+      float pm = -INFINITY;
+#pragma unroll
+      for (int i = 0; i < KC; ++i) {
+        float kf[8];
+        unpack8(kr[k][i], kf);
+        float sv = 0.f;
+#pragma unroll
+        for (int t = 0; t < 8; ++t) sv = fmaf(q[k][t], kf[t], sv);
+        sv = sum8(sv);
+        sc[i] = cb + 8 * i + grp < p[k] ? sv : -INFINITY;
+        pm = fmaxf(pm, sc[i]);
+      }
+      pm = fmaxf(pm, xor8(pm));
+      pm = max16(pm);
+      pm = max32(pm);
+      const float mn = fmaxf(m[k], pm);
+      const float scale = __expf(m[k] - mn);
+      sum[k] *= scale;
+#pragma unroll
+      for (int t = 0; t < 8; ++t) o[k][t] *= scale;
+      m[k] = mn;
+#pragma unroll
+      for (int i = 0; i < KC; ++i) {
+        const float e = __expf(sc[i] - mn);
+        sum[k] += e;
+        float vf[8];
+        unpack8(vr[k][i], vf);
+#pragma unroll
+        for (int t = 0; t < 8; ++t) o[k][t] = fmaf(e, vf[t], o[k][t]);
+      }
+    }
+  }
+  // the new key / value (position pos, written by phase A this step)
+  u32x4_t knu[KU], vnu[KU];
+#pragma unroll
+  for (int k = 0; k < KU; ++k) {
+    const int off = (int)((base[k] + (long)p[k] * HD) * 2);
+    knu[k] = ld16(rk, off);
+    vnu[k] = ld16(rv, off);
+  }
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int k = 0; k < KU; ++k) {
+    sum[k] = add32(add16(sum[k] + xor8(sum[k])));
+#pragma unroll
+    for (int t = 0; t < 8; ++t) o[k][t] = add32(add16(o[k][t] + xor8(o[k][t])));
+    float kf[8], vf[8];
+    unpack8(knu[k], kf);
+    unpack8(vnu[k], vf);
+    float sn = 0.f;
+#pragma unroll
+    for (int t = 0; t < 8; ++t) sn = fmaf(q[k][t], kf[t], sn);
+    sn = sum8(sn);
+    const float mn = fmaxf(m[k], sn);
+    const float sc = __expf(m[k] - mn), en = __expf(sn - mn);
+    const float inv = 1.0f / fmaf(sum[k], sc, en);
+    float of[8];
+#pragma unroll
+    for (int t = 0; t < 8; ++t) of[t] = fmaf(en, vf[t], o[k][t] * sc) * inv;
+    if (grp == 0 && row[k] < a.R) {
+      // att in fragment order: row r, dims 64 h + 8 sub .. + 8 = k-step 2 h + sub / 4,
+      // lane (r & 15) + 16 (sub & 3)
+      const int r = row[k];
+      st16(rs.att, (((r >> 4) * KSD + 2 * hh[k] + (sub >> 2)) * 64 + (r & 15) + 16 * (sub & 3)) * 16,
+           pack8(of));
+    }
+  }
+}
+
+// ------------------------------------------------------------------ F: ln_f + LM head
+// Vocab blocks of 16 b = w, w + G, ..; per block each wave multiplies its K quarter (6 KiB of the
+// fragment-packed table) into all 64 rows, the 4 partial tiles go through double-buffered slabs,
+// and wave v finalises row block v: 4 logits per lane, a running (logit, id) best per lane.
+// A ring of 3 blocks of weights per wave is in flight.
+template <int G>
+__device__ __forceinline__ void phase_f(const Args& a, const Rs& rs, int w, const Sm& sm, gu64* keys) {
+  const int tid = otid(), v = tid >> 6, lane = tid & 63;
+  u32x4_t xf[4 * QS];
+  lda<4, QS>(rs.xb, KSD, 0, QS * v, xf);
+  const int nvb = (a.V + 15) >> 4;
+  const int nb = (nvb - w + G - 1) / G;
+  u32x4_t R0[QS], R1[QS], R2[QS];
+  // the first block's weights stream during the LayerNorm; the other two slots are issued after
+  // it (all three in flight across it left too few registers for the normalisation)
+  ldw<1, QS>(a.wtep, KSD, w, QS * v, R0);
+  __builtin_amdgcn_sched_barrier(0);
+  ln_frags<4>(xf, sm, 0);
+  if (nb > 1) ldw<1, QS>(a.wtep, KSD, w + G, QS * v, R1);
+  if (nb > 2) ldw<1, QS>(a.wtep, KSD, w + 2 * G, QS * v, R2);
+  float bv = -INFINITY;
+  int bi = 0x7fffffff;
+  const bool tmp = a.temp != 1.0f;
+  int buf = 0;
+  lds_sync();     // the previous phase's slab readers are done
+  auto consume = [&](int i, const u32x4_t (&Rr)[QS]) {
+    f32x4_t acc[4];
+#pragma unroll
+    for (int rb = 0; rb < 4; ++rb) acc[rb] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < QS; ++s)
+#pragma unroll
+      for (int rb = 0; rb < 4; ++rb) acc[rb] = mfma(Rr[s], xf[rb * QS + s], acc[rb]);
+    f32x4_t* red = sm.red + buf * 1024;
+#pragma unroll
+    for (int rb = 0; rb < 4; ++rb) red[(v * 4 + rb) * 64 + lane] = acc[rb];
+    lds_sync();
+    const f32x4_t s = (red[v * 64 + lane] + red[(4 + v) * 64 + lane]) +
+                      (red[(8 + v) * 64 + lane] + red[(12 + v) * 64 + lane]);
+    const int col0 = 16 * (w + G * i) + 4 * (lane >> 4);
+    const float4 lb = *reinterpret_cast<const float4*>(a.lmb + col0);
+    const float lbv[4] = {lb.x, lb.y, lb.z, lb.w};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float lg = s[e] + lbv[e];
+      const float val = tmp ? lg / a.temp : lg;
+      if (col0 + e < a.V && val > bv) { bv = val; bi = col0 + e; }
+    }
+    buf ^= 1;
+  };
+#pragma nounroll
+  for (int i = 0; i < nb; i += 3) {
+    consume(i, R0);
+    if (i + 3 < nb) ldw<1, QS>(a.wtep, KSD, w + G * (i + 3), QS * v, R0);
+    if (i + 1 < nb) {
+      consume(i + 1, R1);
+      if (i + 4 < nb) ldw<1, QS>(a.wtep, KSD, w + G * (i + 4), QS * v, R1);
+    }
+    if (i + 2 < nb) {
+      consume(i + 2, R2);
+      if (i + 5 < nb) ldw<1, QS>(a.wtep, KSD, w + G * (i + 5), QS * v, R2);
+    }
+  }
+  // the 4 lanes of a row (l % 16 equal): larger logit, then the lower id
+#pragma unroll
+  for (int o = 16; o < 64; o <<= 1) {
+    const float ov = __shfl_xor(bv, o, 64);
+    const int oi = __shfl_xor(bi, o, 64);
+    if (ov > bv || (ov == bv && oi < bi)) { bv = ov; bi = oi; }
+  }
+  if (lane < 16) {
+    const unsigned long long key = ((unsigned long long)f2key(bv) << 32) | (unsigned)(~bi);
+    __hip_atomic_fetch_max(keys + 16 * v + lane, key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+// ------------------------------------------------------------------ row state
+__device__ __forceinline__ void load_state(const Args& a, const Sm& sm) {
+  const int tid = otid();
+  if (tid < RM) {
+    const bool in = tid < a.R;
+    sm.tok[tid] = in ? a.next_tok[tid] : 0;
+    sm.pos[tid] = in ? a.pos[tid] : 0;
+    sm.done[tid] = in ? a.done[tid] : 1;
+  }
+}
+// generate2's bookkeeping of step `step` from the argmax keys (greedy_step_kernel, gpt2.hip):
+// every workgroup updates its LDS copy; `commit`: also ids and the state in memory.  Returns the
+// rows still decoding (in sm.misc[0] after the caller's barrier).
+__device__ __forceinline__ void bookkeep(const Args& a, const Sm& sm, gu64* keys, int step, bool commit) {
+  const int tid = otid();
+  int alive = 0;
+  if (tid < RM) {
+    const unsigned long long key = __hip_atomic_load(keys + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int t = (int)~(unsigned)key;
+    if (tid < a.R) {
+      int d = sm.done[tid];
+      if (!d) {
+        if (commit) {
+          a.out_ids[(long)tid * a.max_steps + step] = t;
+          a.out_len[tid] = step + 1;
+        }
+        if (t == a.stop0 || t == a.stop1) d = 1;
+      }
+      alive = !d;
+      sm.done[tid] = d;
+      sm.tok[tid] = t;
+      sm.pos[tid] += 1;
+      if (commit) {
+        a.done[tid] = d;
+        a.pos[tid] = sm.pos[tid];
+        a.next_tok[tid] = t;
+      }
+    }
+  }
+  const unsigned long long bal = __ballot(alive);
+  if (tid == 0) sm.misc[0] = (int)__popcll(bal);
+}
+
+// a workgroup that gave up waiting (grid not co-resident): all_done = {1, -1} tells the host
+__device__ __forceinline__ void gave_up(const Args& a) {
+  if (threadIdx.x == 0) {
+    __hip_atomic_store(&a.all_done[1], -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&a.all_done[0], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+// ------------------------------------------------------------------ persistent kernel
+template <int G>
+__global__ __launch_bounds__(NT, 2) void dg_persist_kernel(Args a) {
+  using Gm = Geo<G>;
+  constexpr int KU = Units<G>::KU;
+  __shared__ __attribute__((aligned(16))) char smem[SM_TOTAL];
+  const Sm sm(smem);
+  const int w = blockIdx.x;
+  if (a.all_done[0]) return;                 // every row stopped at step 0 (uniform)
+  int step = *a.step_ctr;
+  if (step >= a.max_steps) return;
+  load_state(a, sm);
+  __syncthreads();
+  const Rs rs = make_rs(a.ws);
+  Bar bar{(gu32*)(a.ws + WS_SH), (gu32*)(a.ws + WS_TMO), 0, G / NSH, a.spin_max, nullptr, 0};
+  gu64* const keys = (gu64*)(a.ws + WS_KEY);
+  volatile lds_int_t* s_ok = (volatile lds_int_t*)(sm.misc + 8);
+  unsigned long long* const stamps = dp_stamp_buf;
+  const int stamp_step = dp_stamp_step;
+  const int ub = w * Units<G>::UPG;
+  constexpr int ANCG = NCB_Q / Gm::ACB, DNCG = NCB_F / Gm::DCB, ENCG = NCB_D / Gm::ECB;
+  const int acb0 = (w % ANCG) * Gm::ACB, dcb0 = (w % DNCG) * Gm::DCB, ecb0 = (w % ENCG) * Gm::ECB;
+#define V_ (otid() >> 6)
+  u32x4_t wq[Gm::APF * QS];
+  ldw<Gm::APF, QS>(a.wq[0], KSD, acb0, QS * V_, wq);
+  f32x4_t xo{0.f, 0.f, 0.f, 0.f};
+  for (;;) {
+    bar.sb = (stamps != nullptr && step == stamp_step) ? stamps + (long)w * 2 * DP_NB : nullptr;
+    bar.n0 = bar.n;
+    stamp(bar.sb, 2 * DP_NB - 1);
+    if (step == a.abort_step) return gave_up(a);    // (test knob: every workgroup, same point)
+    for (int l = 0; l < NLY; ++l) {
+      phase_a<G, false>(a, rs, l, w, sm, wq);
+      bar_arrive(bar, w);
+      u32x4_t kr[KU][KC], vr[KU][KC];
+      attn_load<KU>(a, l, sm, ub, 0, kr, vr);
+      if (!bar_wait(bar, s_ok)) return gave_up(a);
+      if (l == 0 && w == 0 && otid() < RM)   // last step's keys: every workgroup has read them
+        __hip_atomic_store(keys + ((step + 1) & 1) * RM + otid(), 0ull, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+      phase_b<KU>(a, rs, l, sm, ub, kr, vr);
+      bar_arrive(bar, w);
+      u32x4_t wo[Gm::ECB * QS];
+      ldw<Gm::ECB, QS>(a.wo[l], KSD, ecb0, QS * V_, wo);
+      if (!bar_wait(bar, s_ok)) return gave_up(a);
+      phase_c<G, false>(a, rs, l, w, sm, wo, xo);
+      bar_arrive(bar, w);
+      u32x4_t wf[Gm::DPF * QS];
+      ldw<Gm::DPF, QS>(a.wf[l], KSD, dcb0, QS * V_, wf);
+      if (!bar_wait(bar, s_ok)) return gave_up(a);
+      phase_d<G, false>(a, rs, l, w, sm, wf);
+      bar_arrive(bar, w);
+      u32x4_t wm[2 * Gm::ECB * ECH];
+      ldw<Gm::ECB, ECH>(a.wm[l], KSF, ecb0, QF * V_, wm);
+      ldw<Gm::ECB, ECH>(a.wm[l], KSF, ecb0, QF * V_ + ECH, wm + Gm::ECB * ECH);
+      if (!bar_wait(bar, s_ok)) return gave_up(a);
+      phase_e<G, false>(a, rs, l, w, sm, wm, xo);
+      bar_arrive(bar, w);
+      if (l + 1 < NLY) ldw<Gm::APF, QS>(a.wq[l + 1], KSD, acb0, QS * V_, wq);
+      if (!bar_wait(bar, s_ok)) return gave_up(a);
+    }
+    phase_f<G>(a, rs, w, sm, keys + (step & 1) * RM);
+    bar_arrive(bar, w);
+    ldw<Gm::APF, QS>(a.wq[0], KSD, acb0, QS * V_, wq);
+    if (!bar_wait(bar, s_ok)) return gave_up(a);
+    // ---- every workgroup applies the bookkeeping; workgroup 0 commits it
+    bookkeep(a, sm, keys + (step & 1) * RM, step, w == 0);
+    __syncthreads();
+    stamp(bar.sb, 2 * DP_NB - 2);
+    const int total = sm.misc[0];
+    const bool fin = total == 0 || step + 1 >= a.max_steps;
+    if (w == 0 && otid() == 0) {
+      *a.step_ctr = step + 1;
+      a.all_done[2] = total;
+      if (fin) a.all_done[0] = 1;
+    }
+    if (fin) return;
+    ++step;
+    __syncthreads();     // sm.misc is rewritten next step
+  }
+#undef V_
+}
+
+// ------------------------------------------------------------------ phase launches
+enum { PH_A = 0, PH_B, PH_C, PH_D, PH_E, PH_F };
+template <int G, int PH>
+__global__ __launch_bounds__(NT, 2) void dg_phase_kernel(Args a) {
+  using Gm = Geo<G>;
+  __shared__ __attribute__((aligned(16))) char smem[SM_TOTAL];
+  const Sm sm(smem);
+  const int w = blockIdx.x, l = a.layer;
+  if (a.all_done[0]) return;                 // finished: the rest of a replayed chunk is a no-op
+  if (*a.step_ctr >= a.max_steps) return;
+  load_state(a, sm);
+  __syncthreads();
+  const Rs rs = make_rs(a.ws);
+  if constexpr (PH == PH_A) {
+    u32x4_t wq[Gm::APF * QS];
+    phase_a<G, true>(a, rs, l, w, sm, wq);
+  } else if constexpr (PH == PH_B) {
+    constexpr int KU = Units<G>::KU;
+    u32x4_t kr[KU][KC], vr[KU][KC];
+    attn_load<KU>(a, l, sm, w * Units<G>::UPG, 0, kr, vr);
+    phase_b<KU>(a, rs, l, sm, w * Units<G>::UPG, kr, vr);
+  } else if constexpr (PH == PH_C) {
+    u32x4_t wo[Gm::ECB * QS];
+    f32x4_t xo{0.f, 0.f, 0.f, 0.f};
+    phase_c<G, true>(a, rs, l, w, sm, wo, xo);
+  } else if constexpr (PH == PH_D) {
+    u32x4_t wf[Gm::DPF * QS];
+    phase_d<G, true>(a, rs, l, w, sm, wf);
+  } else if constexpr (PH == PH_E) {
+    u32x4_t wm[2 * Gm::ECB * ECH];
+    f32x4_t xo{0.f, 0.f, 0.f, 0.f};
+    phase_e<G, true>(a, rs, l, w, sm, wm, xo);
+  } else {
+    phase_f<G>(a, rs, w, sm, (gu64*)(a.ws + WS_KEY));
+  }
+}
+// the step's bookkeeping (phase launches): one workgroup of 64 threads; zeroes the keys
+__global__ __launch_bounds__(64) void dg_book_kernel(Args a) {
+  __shared__ __attribute__((aligned(16))) char smem[SM_TOTAL];
+  const Sm sm(smem);
+  if (a.all_done[0]) return;
+  const int step = *a.step_ctr;
+  if (step >= a.max_steps) return;
+  load_state(a, sm);
+  __syncthreads();
+  gu64* keys = (gu64*)(a.ws + WS_KEY);
+  bookkeep(a, sm, keys, step, true);
+  __syncthreads();
+  if (threadIdx.x < RM) keys[threadIdx.x] = 0ull;
+  if (threadIdx.x == 0) {
+    const int total = sm.misc[0];
+    *a.step_ctr = step + 1;
+    a.all_done[2] = total;
+    if (total == 0 || step + 1 >= a.max_steps) a.all_done[0] = 1;
+  }
+}
+
+}  // namespace dg
+}  // namespace zs
+
+using namespace zs;
+
+namespace {
+// validation + Args shared by both entry points
+int dg_args(dg::Args& a, int R, int Lmax, int max_steps, int stop0, int stop1, int V,
+            const void* wte, const void* wpe, const void* wte_packed, float temperature,
+            const void* const* layer_w, const float* lm_bias, void* const* kv,
+            int* pos, int* next_tok, int* done, int* out_ids, int* out_len, int* step_ctr,
+            int* all_done, void* ws, long ws_bytes, int grid) {
+  using namespace dg;
+  ZS_REQUIRE(grid == 48 || grid == 96 || grid == 192, "zs_gpt2_decode: grid 48, 96 or 192 (got %d)", grid);
+  ZS_REQUIRE(R >= 1 && R <= RM, "zs_gpt2_decode: R in 1..%d (got %d)", RM, R);
+  ZS_REQUIRE(V >= 16 * grid * 3 && V <= 1 << 24, "zs_gpt2_decode: vocab %d", V);
+  ZS_REQUIRE(Lmax >= 2 && max_steps >= 1, "zs_gpt2_decode: Lmax %d max_steps %d", Lmax, max_steps);
+  ZS_REQUIRE((long)R * NH * Lmax * HD * 2 < (1L << 31), "zs_gpt2_decode: KV cache too large");
+  ZS_REQUIRE(ws && ws_bytes >= WS_BYTES && ((uintptr_t)ws & 255) == 0,
+             "zs_gpt2_decode: workspace of %d bytes, 256-byte aligned", WS_BYTES);
+  ZS_REQUIRE(temperature > 0.f, "zs_gpt2_decode: temperature %g (> 0)", temperature);
+  ZS_REQUIRE(wte_packed && ((uintptr_t)wte_packed & 15) == 0,
+             "zs_gpt2_decode: wte_packed null or not 16-byte aligned");
+  ZS_REQUIRE(wte && wpe && layer_w && lm_bias && kv && pos && next_tok && done && out_ids &&
+             out_len && step_ctr && all_done, "zs_gpt2_decode: null pointer");
+  a = Args{};
+  a.R = R; a.Lmax = Lmax; a.max_steps = max_steps; a.stop0 = stop0; a.stop1 = stop1; a.V = V;
+  a.spin_max = g_dp_spin > 0 ? (unsigned)g_dp_spin : g_dp_spin < 0 ? 0u : SPIN_MAX;
+  a.abort_step = g_dp_abort;
+  a.kv_bytes = R * NH * Lmax * HD * 2;
+  a.temp = temperature;
+  a.wte = (const bf16_t*)wte; a.wpe = (const bf16_t*)wpe;
+  for (int l = 0; l < NLY; ++l) {
+    const void* const* p = layer_w + 8 * l;
+    for (int k = 0; k < 8; ++k)
+      ZS_REQUIRE(p[k] && ((uintptr_t)p[k] & 15) == 0,
+                 "zs_gpt2_decode: layer %d pointer %d null or not 16-byte aligned", l, k);
+    a.wq[l] = (const bf16_t*)p[0]; a.bq[l] = (const float*)p[1];
+    a.wo[l] = (const bf16_t*)p[2]; a.bo[l] = (const float*)p[3];
+    a.wf[l] = (const bf16_t*)p[4]; a.bfc[l] = (const float*)p[5];
+    a.wm[l] = (const bf16_t*)p[6]; a.bm[l] = (const float*)p[7];
+    ZS_REQUIRE(kv[l] && kv[NLY + l] && ((uintptr_t)kv[l] & 127) == 0 && ((uintptr_t)kv[NLY + l] & 127) == 0,
+               "zs_gpt2_decode: KV cache pointer of layer %d null or not 128-byte aligned", l);
+    a.kc[l] = (bf16_t*)kv[l];
+    a.vc[l] = (bf16_t*)kv[NLY + l];
+  }
+  a.lmb = lm_bias; a.wtep = (const bf16_t*)wte_packed;
+  a.pos = pos; a.next_tok = next_tok; a.done = done; a.out_ids = out_ids; a.out_len = out_len;
+  a.step_ctr = step_ctr; a.all_done = all_done; a.ws = (char*)ws;
+  return 0;
+}
+}  // namespace
+
+extern "C" int zs_decode_persist_workspace_bytes(void) { return dg::WS_BYTES; }
+
+extern "C" int zs_gpt2_decode_persist(int R, int Lmax, int max_steps, int stop0, int stop1, int V,
+                                      const void* wte, const void* wpe, const void* wte_packed,
+                                      float temperature, const void* const* layer_w,
+                                      const float* lm_bias, void* const* kv,
+                                      int* pos, int* next_tok, int* done, int* out_ids,
+                                      int* out_len, int* step_ctr, int* all_done, void* ws,
+                                      long ws_bytes, int grid, void* stream) {
+  dg::Args a;
+  const int rc = dg_args(a, R, Lmax, max_steps, stop0, stop1, V, wte, wpe, wte_packed, temperature,
+                         layer_w, lm_bias, kv, pos, next_tok, done, out_ids, out_len, step_ctr,
+                         all_done, ws, ws_bytes, grid);
+  if (rc) return rc;
+  // the barrier shards, timeout word and argmax keys: zeroed before every launch
+  ZS_CHECK_HIP(hipMemsetAsync(ws, 0, dg::WS_SYNC_BYTES, S(stream)));
+  if (grid == 48) hipLaunchKernelGGL(dg::dg_persist_kernel<48>, dim3(48), dim3(dg::NT), 0, S(stream), a);
+  else if (grid == 96) hipLaunchKernelGGL(dg::dg_persist_kernel<96>, dim3(96), dim3(dg::NT), 0, S(stream), a);
+  else hipLaunchKernelGGL(dg::dg_persist_kernel<192>, dim3(192), dim3(dg::NT), 0, S(stream), a);
+  ZS_LAUNCH_CHECK();
+  return 0;
+}
+
+namespace {
+template <int G>
+int dg_phase_step(dg::Args& a, hipStream_t st) {
+  using namespace dg;
+  for (int l = 0; l < NLY; ++l) {
+    a.layer = l;
+    hipLaunchKernelGGL((dg_phase_kernel<G, PH_A>), dim3(G), dim3(NT), 0, st, a);
+    hipLaunchKernelGGL((dg_phase_kernel<G, PH_B>), dim3(G), dim3(NT), 0, st, a);
+    hipLaunchKernelGGL((dg_phase_kernel<G, PH_C>), dim3(G), dim3(NT), 0, st, a);
+    hipLaunchKernelGGL((dg_phase_kernel<G, PH_D>), dim3(G), dim3(NT), 0, st, a);
+    hipLaunchKernelGGL((dg_phase_kernel<G, PH_E>), dim3(G), dim3(NT), 0, st, a);
+  }
+  a.layer = 0;
+  hipLaunchKernelGGL((dg_phase_kernel<G, PH_F>), dim3(G), dim3(NT), 0, st, a);
+  hipLaunchKernelGGL(dg_book_kernel, dim3(1), dim3(64), 0, st, a);
+  ZS_LAUNCH_CHECK();
+  return 0;
+}
+}  // namespace
+
+// `steps` decode steps as phase launches (62 per step), each a no-op once all_done[0] is set
+extern "C" int zs_gpt2_decode_phases(int R, int Lmax, int max_steps, int stop0, int stop1, int V,
+                                     const void* wte, const void* wpe, const void* wte_packed,
+                                     float temperature, const void* const* layer_w,
+                                     const float* lm_bias, void* const* kv,
+                                     int* pos, int* next_tok, int* done, int* out_ids,
+                                     int* out_len, int* step_ctr, int* all_done, void* ws,
+                                     long ws_bytes, int steps, int grid, void* stream) {
+  dg::Args a;
+  const int rc = dg_args(a, R, Lmax, max_steps, stop0, stop1, V, wte, wpe, wte_packed, temperature,
+                         layer_w, lm_bias, kv, pos, next_tok, done, out_ids, out_len, step_ctr,
+                         all_done, ws, ws_bytes, grid);
+  if (rc) return rc;
+  ZS_REQUIRE(steps >= 1, "zs_gpt2_decode_phases: steps %d", steps);
+  ZS_CHECK_HIP(hipMemsetAsync(ws, 0, dg::WS_SYNC_BYTES, S(stream)));
+  for (int s = 0; s < steps; ++s) {
+    const int r = grid == 48 ? dg_phase_step<48>(a, S(stream))
+                : grid == 96 ? dg_phase_step<96>(a, S(stream)) : dg_phase_step<192>(a, S(stream));
+    if (r) return r;
+  }
+  return 0;
+}
+
+extern "C" int zs_decode_persist_set_stamps(void* buf, int step) {
+  ZS_CHECK_HIP(hipMemcpyToSymbol(HIP_SYMBOL(dg::dp_stamp_buf), &buf, sizeof(buf)));
+  ZS_CHECK_HIP(hipMemcpyToSymbol(HIP_SYMBOL(dg::dp_stamp_step), &step, sizeof(step)));
+  return 0;
+}
+
+// timeout word of the last launch on this workspace (non-zero: the grid was not co-resident and
+// the launch gave up; the state in memory is the last committed step's).  Host-side read.
+extern "C" int zs_decode_persist_status(const void* ws, int* timed_out) {
+  ZS_REQUIRE(ws && timed_out, "zs_decode_persist_status: null pointer");
+  unsigned t = 0;
+  ZS_CHECK_HIP(hipMemcpy(&t, (const char*)ws + dg::WS_TMO, 4, hipMemcpyDeviceToHost));
+  *timed_out = (int)t;
+  return 0;
+}

@@ -263,10 +263,8 @@ extern int g_small_attn;    // attn.hip
 extern int g_small_rmax;    // attn.hip
 extern int g_gemm_big;      // gemm.hip
 extern int g_big_min;       // gemm.hip
-extern int g_dp_spin;       // decode_persist.hip
-extern int g_dp_fuse;       // decode_persist.hip
-extern int g_dp_nt;         // decode_persist.hip
-extern int g_dp_lmil;       // decode_persist.hip
+extern int g_dp_spin;       // decode_grid.hip
+extern int g_dp_abort;      // decode_grid.hip
 extern int g_beam_xcd;      // attn.hip
 
 // choose K per workgroup: a multiple of 64 dividing K, each wave <= 128 deep, ~256-320 WGs
@@ -320,9 +318,7 @@ extern "C" int zs_tune_set(const char* key, int value) {
   if (!strcmp(key, "gemm_big")) { g_gemm_big = value; return 0; }
   if (!strcmp(key, "big_min")) { g_big_min = value; return 0; }
   if (!strcmp(key, "dp_spin")) { g_dp_spin = value; return 0; }
-  if (!strcmp(key, "dp_fuse")) { g_dp_fuse = value; return 0; }
-  if (!strcmp(key, "dp_nt")) { g_dp_nt = value; return 0; }
-  if (!strcmp(key, "dp_lmil")) { g_dp_lmil = value; return 0; }
+  if (!strcmp(key, "dp_abort_step")) { g_dp_abort = value; return 0; }
   if (!strcmp(key, "beam_xcd")) { g_beam_xcd = value; return 0; }
   return fail(ZS_ERR_ARG, "zs_tune_set: unknown key %s", key);
 }

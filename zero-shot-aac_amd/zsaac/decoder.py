@@ -203,22 +203,44 @@ class Gpt2Weights:
             })
         self.lnf = (_f32(sd[p + "ln_f.weight"], device), _f32(sd[p + "ln_f.bias"], device))
         self._layer_ptrs = None
+        self._wte_packed = self._lm_bias = None
+        if self.folded:
+            # the bs <= 64 greedy decode (zs_gpt2_decode_persist / _phases) folds ln_f's affine into
+            # the tied LM head as ln_1 / ln_2 into c_attn / c_fc: logit[v] = y . (g o wte[v]) +
+            # beta . wte[v] with y the normalised row (g o wte rounded to bf16 once, from f32)
+            wte32 = sd[p + "wte.weight"].to(device=device, dtype=torch.float32)
+            g, beta = self.lnf
+            self._wte_packed = ops.pack_b_fragments((wte32 * g[None, :]).to(torch.bfloat16))
+            nvb = -(-self.V // 16)
+            lmb = torch.zeros(nvb * 16, device=device)
+            lmb[:self.V] = (wte32.double() @ beta.double()).float()
+            self._lm_bias = lmb
+            del wte32
 
-    def layer_ptrs(self):
-        """The 12 x 8 device pointers zs_gpt2_decode_persist takes (c_attn W, b, attn.c_proj W, b,
-        c_fc W, b, mlp.c_proj W, b per block; bf16 with the LN affine folded)."""
+    def packed_layer_ptrs(self):
+        """The 12 x 8 device pointers zs_gpt2_decode_persist / _phases take: per block c_attn W,
+        b, attn.c_proj W, b, c_fc W, b, mlp.c_proj W, b -- each W (bf16, LN affine folded) in MFMA
+        fragment order (ops.pack_b_fragments), packed once."""
         if self._layer_ptrs is None:
             import ctypes
+            assert self.folded, "the grid decode runs the bf16 (LN-folded) weights"
+            self._packed = [{k: (ops.pack_b_fragments(ly[k]) if k.endswith("_w") else ly[k])
+                             for k in ("attn_w", "attn_b", "proj_w", "proj_b", "fc_w", "fc_b",
+                                       "mproj_w", "mproj_b")} for ly in self.layers]
             keys = ("attn_w", "attn_b", "proj_w", "proj_b", "fc_w", "fc_b", "mproj_w", "mproj_b")
             self._layer_ptrs = (ctypes.c_void_p * (8 * NL))(
-                *[ly[k].data_ptr() for ly in self.layers for k in keys])
+                *[pl[k].data_ptr() for pl in self._packed for k in keys])
         return self._layer_ptrs
 
     def wte_packed(self):
-        """The tied LM head in MFMA B-fragment order (zs_gpt2_decode_persist), built once."""
-        if getattr(self, "_wte_packed", None) is None:
-            self._wte_packed = ops.pack_b_fragments(self.wte)
+        """The tied LM head with ln_f's weight folded in, MFMA fragment order (bf16 only)."""
+        assert self._wte_packed is not None, "the grid decode runs the bf16 (LN-folded) weights"
         return self._wte_packed
+
+    def lm_bias(self):
+        """ln_f's bias through the tied LM head, beta . wte[v], f32 [ceil(V/16) 16]."""
+        assert self._lm_bias is not None, "the grid decode runs the bf16 (LN-folded) weights"
+        return self._lm_bias
 
     def nbytes(self) -> int:
         n = self.wte.numel() + self.wpe.numel()
@@ -291,24 +313,25 @@ class Gpt2Decoder:
             compact = dt == torch.bfloat16
         self.compact = (compact and dt == torch.bfloat16 and self.Lmax <= 128
                         and self.R >= self.min_bucket)
-        # greedy bf16 decode of one eval batch (<= 64 rows): all steps after step 0 in one
-        # persistent launch (zs_gpt2_decode_persist) instead of graph-replayed per-step chains
+        # greedy bf16 decode of one eval batch (<= 64 rows): the grid decode (decode_grid.hip)
+        # -- every step after step 0 in one persistent launch (zs_gpt2_decode_persist), or, as
+        # the per-step path (persist off, or the give-up fallback), the same computation as phase
+        # launches (zs_gpt2_decode_phases); ids and state are identical at every grid size
+        self.grid_decode = (dt == torch.bfloat16 and w.folded and self.R <= 64
+                            and os.environ.get("ZSAAC_GRID_DECODE", "1") != "0")   # 0: A/B only
         if persist is None:
             persist = os.environ.get("ZSAAC_PERSIST", "1") != "0"
-        self.persist = bool(persist) and dt == torch.bfloat16 and w.folded and self.R <= 64
-        # 2: the row-split grid (2 x decode_persist_grid() workgroups, a shorter step) -- chosen
-        # by the caller when few batches are in flight (pipeline.ConcurrentRunner)
-        self.persist_row_split = int(os.environ.get("ZSAAC_PERSIST_RS", "1"))
-        # 2: two column slices per workgroup (half the workgroups per batch, less CU time per
-        # step, a longer step) -- chosen with row_split by pipeline.ConcurrentRunner
-        self.persist_col_split = int(os.environ.get("ZSAAC_PERSIST_CS", "1"))
-        if self.persist:
+        self.persist = bool(persist) and self.grid_decode
+        # workgroups (256 threads, half a CU each) of the persistent launch: 48 / 96 / 192,
+        # chosen per batch by pipeline.ConcurrentRunner (more when CUs are free)
+        self.persist_grid = int(os.environ.get("ZSAAC_PERSIST_GRID", "48"))
+        self.phase_grid = 96           # the phase launches' grid (any size gives the same ids)
+        if self.grid_decode:
             import ctypes
             self.persist_ws = ops.decode_persist_workspace(dev)
-            # the shared packed LM head and pointer table, built now and synchronised: a twin
-            # decoder launched on another stream must never read a half-written wte_packed
-            w.wte_packed()
-            w.layer_ptrs()
+            # the shared packed weights and pointer table, built now and synchronised: a twin
+            # decoder launched on another stream must never read a half-written copy
+            w.packed_layer_ptrs()
             torch.cuda.synchronize(dev)
             self._kv_ptrs = (ctypes.c_void_p * (2 * NL))(
                 *[t.data_ptr() for t in self.kc], *[t.data_ptr() for t in self.vc])
@@ -450,7 +473,17 @@ class Gpt2Decoder:
         for Rb in sorted({self._bucket_rows(R, a) for a in range(0, R + 1, self.bucket)}):
             self._graph(*self._chunk_plan(Rb))
 
+    def _grid_args(self, R):
+        w = self.w
+        return (R, self.Lmax, self.max_steps, self.stop0, self.stop1, w.V, w.wte, w.wpe,
+                w.wte_packed(), self.temperature, w.packed_layer_ptrs(), w.lm_bias(),
+                self._kv_ptrs, self.pos, self.next_tok, self.done, self.out_ids, self.out_len,
+                self.step_ctr, self.all_done, self.persist_ws)
+
     def _greedy_step_body(self, R):
+        if self.grid_decode:      # the persistent launch's computation, one launch per phase
+            ops.gpt2_decode_phases(*self._grid_args(R), steps=1, grid=self.phase_grid)
+            return
         self._decode_forward(R)
         ops.lmhead_topk(self.hf[:R], self.w.wte, 1, None, self.pval1, self.pidx1,
                         temperature=self.temperature)
@@ -544,11 +577,12 @@ class Gpt2Decoder:
 
     def resume_stepwise(self):
         """After a persistent launch gave up (all_done[1] = -1: its grid was not co-resident in
-        time): the kernel writes pos / done / next_tok / step_ctr only when it finishes, so the
-        decode state is still the one it started from (ids and K/V rows it wrote past it are
-        rewritten step by step).  Re-arm the flags; the remaining steps then run on the per-step
-        path, eagerly (no graph capture while other streams run).  Enqueued on the current
-        stream."""
+        time): the kernel commits ids, out_len, pos / done / next_tok and step_ctr after every
+        step it completes (workgroup 0, once every workgroup's LM-head keys are in), so the state
+        in memory is the last completed step's; K/V rows written past it are rewritten with the
+        same values.  Re-arm the flags; the remaining steps run as phase launches (the same
+        arithmetic: ids equal an uninterrupted launch's), eagerly (no graph capture while other
+        streams run).  Enqueued on the current stream."""
         self.all_done[:2].zero_()
         self.gave_up += 1
         self._persist_R = 0
@@ -585,19 +619,12 @@ class Gpt2Decoder:
         self._eager = False
         self._persist_R = 0
         if self.persist and R <= 64:
-            w = self.w
             ev = PERSIST_LOG
             if ev is not None:          # bench.py's roofline: HIP events around each launch
                 ev.append((torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True),
                            id(self)))
                 ev[-1][0].record()
-            ops.gpt2_decode_persist(R, self.Lmax, self.max_steps, self.stop0, self.stop1, w.V, w.wte,
-                                    w.wpe, w.wte_packed(), self.temperature, w.layer_ptrs(),
-                                    w.lnf[0], w.lnf[1], self._kv_ptrs,
-                                    self.pos, self.next_tok, self.done, self.out_ids, self.out_len,
-                                    self.step_ctr, self.all_done, self.persist_ws,
-                                    row_split=self.persist_row_split,
-                                    col_split=self.persist_col_split)
+            ops.gpt2_decode_persist(*self._grid_args(R), grid=self.persist_grid)
             if ev is not None:
                 ev[-1][1].record()
             self._persist_R = R

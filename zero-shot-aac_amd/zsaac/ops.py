@@ -477,15 +477,19 @@ def magic_step(score, cand, C, b, W, first, greedy, stop, step, max_steps, score
          _p(kvrow), kvrow.shape[1], _p(pos), _p(cdone), _p(ntok), _p(hid), _p(sel_h), dt(hid), _s())
 
 
-# ---------------------------------------------------------------- persistent greedy decode
+# ---------------------------------------------------------------- greedy decode on a grid (bs <= 64)
+PERSIST_GRIDS = (48, 96, 192)     # workgroups of 256 threads (half a CU each) per launch
+
+
 def decode_persist_workspace(device) -> torch.Tensor:
     n = call("zs_decode_persist_workspace_bytes")
     return torch.zeros(n + 256, dtype=torch.uint8, device=device)
 
 
-def decode_persist_grid(row_split: int = 1, col_split: int = 1) -> int:
-    """Workgroups (one per CU) of one zs_gpt2_decode_persist launch."""
-    return call("zs_decode_persist_grid") // col_split * row_split
+def decode_persist_grid(grid: int = 48) -> int:
+    """Workgroups of one zs_gpt2_decode_persist launch (48, 96 or 192, each 256 threads)."""
+    _need(grid in PERSIST_GRIDS, f"decode grid {grid} (one of {PERSIST_GRIDS})")
+    return grid
 
 
 def pack_b_fragments(W: torch.Tensor) -> torch.Tensor:
@@ -501,22 +505,35 @@ def pack_b_fragments(W: torch.Tensor) -> torch.Tensor:
             .view(Np // 16, K // 32, 64, 8))
 
 
-def gpt2_decode_persist(R, Lmax, max_steps, stop0, stop1, V, wte, wpe, wte_packed, temperature,
-                        layer_ptrs, lnf_w, lnf_b, kv_ptrs, pos, next_tok, done, out_ids, out_len,
-                        step_ctr, all_done, ws, row_split=1, col_split=1):
-    """The remaining greedy steps of one bs <= 64 batch in one persistent launch
-    (zs_gpt2_decode_persist) of decode_persist_grid(row_split, col_split) workgroups.
-    layer_ptrs / kv_ptrs: ctypes arrays of 96 / 24 device pointers."""
-    _need(1 <= R <= 64, "gpt2_decode_persist: 1 <= R <= 64")
-    _need(wte.dtype == torch.bfloat16 and wpe.dtype == torch.bfloat16, "gpt2_decode_persist: bf16")
+def _decode_grid_args(R, Lmax, max_steps, stop0, stop1, V, wte, wpe, wte_packed, temperature,
+                      layer_ptrs, lm_bias, kv_ptrs, pos, next_tok, done, out_ids, out_len,
+                      step_ctr, all_done, ws, grid):
+    _need(1 <= R <= 64, "gpt2 decode grid: 1 <= R <= 64")
+    _need(wte.dtype == torch.bfloat16 and wpe.dtype == torch.bfloat16, "gpt2 decode grid: bf16")
     for t, n in ((pos, "pos"), (next_tok, "next_tok"), (done, "done"), (out_ids, "out_ids"),
                  (out_len, "out_len"), (step_ctr, "step_ctr"), (all_done, "all_done")):
         _i32(t, n)
-    _need(out_ids.shape[-1] == max_steps, "gpt2_decode_persist: out_ids [R, max_steps]")
+    _need(out_ids.shape[-1] == max_steps, "gpt2 decode grid: out_ids [R, max_steps]")
+    _need(lm_bias.dtype == torch.float32 and lm_bias.numel() >= -(-V // 16) * 16,
+          "gpt2 decode grid: lm_bias f32 [ceil(V/16) 16]")
+    _need(temperature > 0, "gpt2 decode grid: temperature > 0")
+    decode_persist_grid(grid)
     base = ws.data_ptr()
     off = (-base) % 256
-    _need(temperature > 0, "gpt2_decode_persist: temperature > 0")
-    call("zs_gpt2_decode_persist", R, Lmax, max_steps, stop0, stop1, V, _p(wte), _p(wpe),
-         _p(wte_packed), float(temperature), layer_ptrs, _p(lnf_w), _p(lnf_b), kv_ptrs, _p(pos), _p(next_tok), _p(done), _p(out_ids),
-         _p(out_len), _p(step_ctr), _p(all_done), base + off, ws.numel() - off, int(row_split),
-         int(col_split), _s())
+    return (R, Lmax, max_steps, stop0, stop1, V, _p(wte), _p(wpe), _p(wte_packed),
+            float(temperature), layer_ptrs, _p(lm_bias), kv_ptrs, _p(pos), _p(next_tok), _p(done),
+            _p(out_ids), _p(out_len), _p(step_ctr), _p(all_done), base + off, ws.numel() - off)
+
+
+def gpt2_decode_persist(*args, grid=48):
+    """The remaining greedy steps of one bs <= 64 batch in one persistent launch
+    (zs_gpt2_decode_persist) of `grid` 256-thread workgroups.  Arguments as
+    _decode_grid_args (layer_ptrs / kv_ptrs: ctypes arrays of 96 / 24 device pointers; the
+    weights in fragment order, Gpt2Weights.packed_layer_ptrs)."""
+    call("zs_gpt2_decode_persist", *_decode_grid_args(*args, grid), int(grid), _s())
+
+
+def gpt2_decode_phases(*args, steps=1, grid=96):
+    """`steps` decode steps of the same computation as phase launches (zs_gpt2_decode_phases:
+    bit-identical to the persistent launch at any grid; graph-capturable)."""
+    call("zs_gpt2_decode_phases", *_decode_grid_args(*args, grid), int(steps), int(grid), _s())

@@ -228,39 +228,44 @@ class CaptionPipeline:
             dec.greedy_begin(B)
 
 
-def persist_shapes(env: Optional[str] = None) -> List[Tuple[int, int]]:
-    """The persistent-decode grid shapes (col_split, row_split) a runner may use, largest grid
-    first: ZSAAC_PERSIST_SHAPES ("cs rs" digit pairs, e.g. "12,11,21") or, when ZSAAC_PERSIST_CS /
-    ZSAAC_PERSIST_RS fix a shape, that one alone."""
-    env = os.environ.get("ZSAAC_PERSIST_SHAPES", DEFAULT_PERSIST_SHAPES) if env is None else env
-    if "ZSAAC_PERSIST_CS" in os.environ or "ZSAAC_PERSIST_RS" in os.environ:
-        env = os.environ.get("ZSAAC_PERSIST_CS", "1") + os.environ.get("ZSAAC_PERSIST_RS", "1")
-    shapes = [(int(t[0]), int(t[1])) for t in env.replace(" ", "").split(",") if t]
-    for cs, rs in shapes:
-        assert cs in (1, 2) and rs in (1, 2), f"persist shape {cs}{rs}"
-    return sorted(set(shapes), key=lambda sh: -ops.decode_persist_grid(sh[1], sh[0]))
+def persist_grids(env: Optional[str] = None) -> List[int]:
+    """The persistent-decode grid sizes (workgroups of 256 threads, ops.PERSIST_GRIDS) a runner
+    may use, largest first: ``env`` or ZSAAC_PERSIST_GRIDS ("192,96,48"); with ``env`` None and
+    ZSAAC_PERSIST_GRID set, that one size alone.  Every size gives the same ids (decode_grid.hip's
+    canonical arithmetic), so the choice is a scheduling decision only."""
+    if env is None:
+        env = (os.environ["ZSAAC_PERSIST_GRID"] if "ZSAAC_PERSIST_GRID" in os.environ
+               else os.environ.get("ZSAAC_PERSIST_GRIDS", DEFAULT_PERSIST_GRIDS))
+    grids = sorted({int(t) for t in env.replace(" ", "").split(",") if t}, reverse=True)
+    for g in grids:
+        assert g in ops.PERSIST_GRIDS, f"persist grid {g} (one of {ops.PERSIST_GRIDS})"
+    return grids
 
 
-# largest grid first; the last is the throughput shape every batch can fall back to: 24
-# workgroups (col_split 2) cost ~30 % less CU time per decode step than 48 (tools/
-# persist_grid_bench.py), so up to CUs // 24 batches decode at once; a batch that begins when few
-# others wait gets a larger (faster) grid
-DEFAULT_PERSIST_SHAPES = "12,11,21"
+# largest first; the last is the throughput grid every batch can fall back to
+DEFAULT_PERSIST_GRIDS = "192,96,48"
 
 
-def choose_persist_shape(in_flight: int, to_begin: int, shapes: List[Tuple[int, int]],
-                         cus: int) -> Tuple[int, int]:
-    """Grid shape (col_split, row_split) of the persistent decode launch of the next batch to
-    begin, given the workgroups of the grids already in flight and the batches still to begin
-    (this one included): the largest shape whose grid, beside the grids in flight and every
-    other batch still to begin at the smallest shape, fits the CUs.  Then every later begin still
-    has room for the smallest shape, so (with at most cus // smallest batches in flight) the
-    grids in flight never exceed the CUs and every persistent launch stays co-resident."""
-    g_min = ops.decode_persist_grid(shapes[-1][1], shapes[-1][0])
-    for cs, rs in shapes:
-        if in_flight + ops.decode_persist_grid(rs, cs) + g_min * (to_begin - 1) <= cus:
-            return cs, rs
-    return shapes[-1]
+def persist_budget(cus: int) -> int:
+    """Workgroup slots the in-flight persistent grids may hold together: a grid workgroup takes
+    half a CU (4 waves x <= 256 registers), so 2 x CUs is the chip; the default, one per CU,
+    leaves the other half of every grid CU to the begins' kernels (encode .. prefill);
+    ZSAAC_PERSIST_BUDGET overrides."""
+    return int(os.environ.get("ZSAAC_PERSIST_BUDGET", str(cus)))
+
+
+def choose_persist_grid(in_flight: int, to_begin: int, grids: List[int], budget: int) -> int:
+    """Grid size of the persistent decode launch of the next batch to begin, given the workgroups
+    of the grids already in flight and the batches still to begin (this one included): the
+    largest grid that, beside the grids in flight and every other batch still to begin at the
+    smallest size, fits the budget.  Then every later begin still has room for the smallest grid,
+    so (with at most budget // smallest batches in flight) the grids in flight never exceed the
+    budget and every persistent launch can be co-resident."""
+    g_min = grids[-1]
+    for g in grids:
+        if in_flight + g + g_min * (to_begin - 1) <= budget:
+            return g
+    return g_min
 
 
 class ConcurrentRunner:
@@ -273,16 +278,16 @@ class ConcurrentRunner:
     Results are copied out on the pipeline's stream before it takes the next batch."""
 
     def __init__(self, pipe: CaptionPipeline, n_inflight: int = 2, streams: Optional[list] = None,
-                 shapes: Optional[List[Tuple[int, int]]] = None):
+                 grids: Optional[List[int]] = None, budget: Optional[int] = None):
         self.cus = torch.cuda.get_device_properties(pipe.dev).multi_processor_count
-        # persistent grids (greedy bf16 at <= 64 rows; beam search never launches one), one shape
-        # per batch from `shapes` (largest first, see choose_persist_shape)
+        # persistent grids (greedy bf16 at <= 64 rows; beam search never launches one), one size
+        # per batch from `grids` (largest first, see choose_persist_grid)
         self.persist = pipe.decoder.persist and not pipe.cfg.beam
-        self.shapes = shapes or persist_shapes()
+        self.grids = grids or persist_grids()
+        self.budget = budget or persist_budget(self.cus)
         if self.persist:
-            # persistent decode grids must be co-resident: at most CUs // (smallest grid) in flight
-            g_min = ops.decode_persist_grid(self.shapes[-1][1], self.shapes[-1][0])
-            n_inflight = max(1, min(n_inflight, self.cus // g_min))
+            # persistent decode grids must be co-resident: at most budget // (smallest grid)
+            n_inflight = max(1, min(n_inflight, self.budget // self.grids[-1]))
         self.n_inflight = n_inflight
         self.pipes = [pipe] + [pipe.twin() for _ in range(n_inflight - 1)]
         # dedicated streams on distinct hardware queues: pooled torch streams take their queue at
@@ -324,8 +329,8 @@ class ConcurrentRunner:
         nxt = 0
         self.decode_steps = [0] * len(batches)     # per batch: decode steps actually enqueued
         self.assign = []                           # (pipeline index, batch index), in begin order
-        self.row_split = [1] * len(batches)
-        self.shape = [(1, 1)] * len(batches)      # persistent grid shape (col_split, row_split)
+        self.grid = [0] * len(batches)             # persistent grid size per batch (0: none)
+        self.gave_up = 0                           # launches of this run that resumed stepwise
         slots = {}                                 # pipeline index -> its launch's workgroups
         while nxt < len(batches) or active:
             progressed = False
@@ -334,12 +339,11 @@ class ConcurrentRunner:
                 if st is None:
                     if nxt < len(batches):
                         if self.persist:
-                            cs, rs = choose_persist_shape(sum(slots.values()), len(batches) - nxt,
-                                                          self.shapes, self.cus)
-                            p.decoder.persist_col_split, p.decoder.persist_row_split = cs, rs
-                            slots[i] = ops.decode_persist_grid(rs, cs)
-                            self.row_split[nxt] = rs
-                            self.shape[nxt] = (cs, rs)
+                            g = choose_persist_grid(sum(slots.values()), len(batches) - nxt,
+                                                    self.grids, self.budget)
+                            p.decoder.persist_grid = g
+                            slots[i] = g
+                            self.grid[nxt] = g
                         with torch.cuda.stream(s):
                             (p.begin_wav if inputs == "wav" else p.begin_emb)(batches[nxt])
                             ev, flag = p.decoder.finished_async()
@@ -355,6 +359,7 @@ class ConcurrentRunner:
                 if int(flag[1]) < 0:
                     # the persistent launch gave up waiting (its grid was not co-resident): finish
                     # this batch on the per-step path from the state it started from
+                    self.gave_up += 1
                     with torch.cuda.stream(s):
                         p.decoder.resume_stepwise()
                         p.decoder.step_chunk(None)
