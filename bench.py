@@ -9,10 +9,11 @@ eval batches of 64 clips exactly as the reference evaluates them: STFT/log-mel +
 audio_proj + L2 -> sound-effect hard prompt -> MLP mapper -> GPT-2 small prefill +
 get_prefix_tokens + greedy generate2 (entry_length 67, stop ids 13 / 764), bf16 operands / f32
 accumulation.  Every decode GEMM of a batch is a 64-row GEMM.  One "step" = one eval batch of
-64 clips (the last batch of the 1045 holds 21).  --inflight independent batches (default 10) are
-in flight per GPU, each on its own HIP stream (pipeline twins sharing the weights,
-zsaac/pipeline.py ConcurrentRunner), each decoding in its own persistent launch of 24 workgroups
-(col_split 2; a larger grid when CUs are free, zsaac.pipeline.choose_persist_shape);
+64 clips (the last batch of the 1045 holds 21).  Independent batches are in flight per GPU (up to
+--inflight, within --persist-budget), each on its own HIP stream (pipeline twins sharing the
+weights, zsaac/pipeline.py ConcurrentRunner), each decoding in its own persistent launch of 48
+half-CU workgroups (a larger grid when few batches wait, zsaac.pipeline.choose_persist_grid; the
+grid never changes an id, decode_grid.hip); the timed region runs --reps times (median reported);
 GPU_MAX_HW_QUEUES is raised to --hw-queues (default 16, the runtime allows up to 32) so those
 streams get hardware queues of their own.  With N ranks the
 clips are sharded (zsaac/dist.py shard_range) and ONE RCCL all-gather of the generated token ids
@@ -24,7 +25,7 @@ clips are sharded (zsaac/dist.py shard_range) and ONE RCCL all-gather of the gen
     torchrun --nproc-per-node N bench.py --gpus N    # one process per GPU, RCCL
 
 Rank 0 prints ONE JSON line.  Besides the contract fields (value = whole-job clips/s) it holds
-  roofline:          the dominant kernel, decode_persist_kernel (zs_gpt2_decode_persist: every
+  roofline:          the dominant kernel, dg_persist_kernel (zs_gpt2_decode_persist: every
                      decode step after step 0 of one eval batch in one launch), HBM-bound:
                      algorithmic bytes per launch (weights per step + every row's K/V reads and
                      appends, persist_launch_bytes) / its average duration over the timed region's
@@ -83,7 +84,13 @@ import torch  # noqa: E402
 HBM_PEAK_GBS = 8000.0           # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 MFMA_BF16_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense bf16 MFMA (no sparsity)
 MFMA_F32_PEAK_TFLOPS = 157.3    # MI355X_MICROARCH.md: dense f32 MFMA
-GPT2_KW = dict(seed=0, std=0.1, emb_std=0.1, stop_boost=2.0)
+# the decoder weights: GPT-2's own init scale (blocks and embeddings std 0.02, the c2_gpt2init
+# golden's weights), where the reference's own bf16 logit error (0.032) is far below most step
+# margins, so the bf16 id-parity gate compares ~64 % of the tokens the bench generates
+# (id_agreement.bench_weights); the stop-token boost makes '.' fire for part of the clips
+GPT2_KW = dict(seed=11, std=0.02, emb_std=0.02, stop_boost=2.0)
+BENCH_WEIGHTS_GOLDEN = "c2_gpt2init"
+HEADLINE_REPS = 3
 CLOTHO_EVAL_CLIPS = 1045
 METRIC = "audio clips/sec end-to-end (encode+mapper+GPT-2 decode), Clotho-eval bs=64"
 DATA = ("synthetic 10 s / 32 kHz waveforms (randn*0.1) resident in HBM; seeded random-init "
@@ -119,7 +126,13 @@ def parse(argv=None):
                     help="eval batches decoded together in one decode step (1 = the metric's "
                          "bs=64; > 1 is the labelled throughput mode)")
     ap.add_argument("--inflight", type=int, default=10,
-                    help="independent batches in flight per GPU, each on its own HIP stream")
+                    help="independent batches in flight per GPU, each on its own HIP stream "
+                         "(capped by --persist-budget // the smallest grid)")
+    ap.add_argument("--persist-budget", type=int, default=0,
+                    help="workgroup slots (half a CU each) the in-flight persistent decode grids "
+                         "may hold together (0: ZSAAC_PERSIST_BUDGET or one per CU)")
+    ap.add_argument("--reps", type=int, default=HEADLINE_REPS,
+                    help="timed repetitions of the headline region (value = their median)")
     ap.add_argument("--hw-queues", type=int, default=16,
                     help="GPU_MAX_HW_QUEUES for this process (read before HIP initialises)")
     ap.add_argument("--compact", type=int, default=1,
@@ -243,7 +256,8 @@ def run_captions(args, world, rank, device, pipe, n_local, first, counts, inflig
     if len(batches) == 0:
         raise ValueError("no clips on this rank")
     runner = ConcurrentRunner(pipe, max(1, inflight),
-                              streams=run_streams(device, max(1, inflight)))
+                              streams=run_streams(device, max(1, inflight)),
+                              budget=getattr(args, "persist_budget", 0) or None)
     for size in sorted({b.shape[0] for b in batches}, reverse=True):   # captures every graph
         runner.warmup(next(b for b in batches if b.shape[0] == size))
         log(f"captured the decode graphs of {size}-clip batches")
@@ -256,8 +270,8 @@ def run_captions(args, world, rank, device, pipe, n_local, first, counts, inflig
     torch.cuda.synchronize()
     cap0 = sum(p.decoder.n_captures for p in runner.pipes)
     rows0 = sum(p.decoder.rows_stepped for p in runner.pipes)
-    times = []
-    for _ in range(reps):          # reps > 1 (single-rank side measurements): the median
+    times, gave_up = [], 0
+    for _ in range(reps):          # every repetition the whole region; the median is reported
         t0 = time.perf_counter()
         outs = runner.run(batches)
         if world > 1:
@@ -266,13 +280,17 @@ def run_captions(args, world, rank, device, pipe, n_local, first, counts, inflig
         if world > 1:
             torch.distributed.barrier()
         torch.cuda.synchronize()
-        times.append(time.perf_counter() - t0)
+        dt_r = time.perf_counter() - t0
+        if world > 1:             # the job's time of this repetition: the slowest rank's
+            t = torch.tensor([dt_r], device=device, dtype=torch.float64)
+            torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+            dt_r = float(t)
+        times.append(dt_r)
+        gave_up += getattr(runner, "gave_up", 0)
     dt = sorted(times)[len(times) // 2]
-    if world > 1:
-        t = torch.tensor([dt], device=device, dtype=torch.float64)
-        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-        dt = float(t)
-    log(f"timed: {n_local} clips in {dt:.3f} s")
+    log(f"timed: {n_local} clips in {dt:.3f} s (median of {reps}: {[round(t, 4) for t in times]})")
+    if gave_up:
+        log(f"WARNING: {gave_up} persistent launches gave up and finished on the phase launches")
     runner.timed_log, runner.log_outs = [], None
     if log_pass and pipe.decoder.persist:
         # the roofline's live launch timing: the same batches once more, untimed, with HIP events
@@ -286,6 +304,11 @@ def run_captions(args, world, rank, device, pipe, n_local, first, counts, inflig
             zdec.PERSIST_LOG = None         # no events around launches outside this pass
         ALL_PERSIST_LOGS.extend(runner.timed_log)
     info = {"graph_captures_timed": sum(p.decoder.n_captures for p in runner.pipes) - cap0,
+            "timed_reps_s": [round(t, 5) for t in times],
+            "persist_gave_up": gave_up,
+            "persist_grids": grid_counts(runner),
+            "persist_budget_wg_slots": getattr(runner, "budget", None),
+            "batches_in_flight": runner.n_inflight,
             "decode_rows_stepped_per_clip": round(
                 (sum(p.decoder.rows_stepped for p in runner.pipes) - rows0) / max(1, n_local), 2),
             "decode_steps_mean": round(sum(runner.decode_steps) / max(1, len(runner.decode_steps)), 2),
@@ -459,13 +482,12 @@ def persist_launch_bytes(w_step, plen, steps, kv_row=12 * 2 * 768 * 2):
 PMC_PERSIST_FILE = os.path.join(ROOT, "profiles", "r4", "pmc_persist_cs2.json")
 
 
-def shape_counts(runner):
-    """{"cs<col_split>rs<row_split> (<workgroups> WGs)": launches} of a runner's last run."""
-    from zsaac import ops
+def grid_counts(runner):
+    """{"<workgroups> WGs": launches} of a runner's last run (persistent decode grids)."""
     out = {}
-    for cs, rs in getattr(runner, "shape", []):
-        k = f"cs{cs}rs{rs} ({ops.decode_persist_grid(rs, cs)} WGs)"
-        out[k] = out.get(k, 0) + 1
+    for g in getattr(runner, "grid", []):
+        if g:
+            out[f"{g} WGs"] = out.get(f"{g} WGs", 0) + 1
     return out
 
 
@@ -491,15 +513,16 @@ def persist_roofline(pipe, runner, outs, dt, log):
     if os.path.exists(PMC_PERSIST_FILE):     # rocprofv3 --pmc passes (tools/pmc_traffic.py persist)
         with open(PMC_PERSIST_FILE) as f:
             pmc = json.load(f)
-        if pmc.get("kernel", "").startswith("decode_persist_kernel"):
+        if pmc.get("kernel", "").startswith("dg_persist_kernel"):
             traffic, tsrc = pmc["hbm_bytes_per_launch"], os.path.relpath(PMC_PERSIST_FILE, ROOT)
     steps = sum(runner.decode_steps) / max(1, len(runner.decode_steps))
     return _hbm_entry(
-        f"decode_persist_kernel (zs_gpt2_decode_persist): decode steps 1..{steps - 1:.0f} of one "
-        f"bs-64 eval batch in one launch (grid shapes {shape_counts(runner)}), the {n} launches of "
-        f"a repeat of the timed region, {runner.n_inflight} batches in flight", avg_b, avg_s,
+        f"dg_persist_kernel (zs_gpt2_decode_persist): decode steps 1..{steps - 1:.0f} of one "
+        f"bs-64 eval batch in one launch (grids {grid_counts(runner)} of 256-thread workgroups), "
+        f"the {n} launches of a repeat of the timed region, {runner.n_inflight} batches in flight",
+        avg_b, avg_s,
         {"launches": n, "avg_launch_ms": round(avg_s * 1e3, 3),
-         "grid_shapes": shape_counts(runner),
+         "grids": grid_counts(runner),
          "weight_bytes_per_step": int(w_step), "steps_per_launch_mean": round(steps - 1, 2),
          "traffic": traffic, "traffic_source": tsrc,
          "traffic_note": "PMC FETCH_SIZE*2*1024 + WRITE_SIZE*1024 per launch, single-stream "
@@ -1142,7 +1165,7 @@ def strong_scaling_proxy(args, device, pipe, t_full, n_full, n_ranks=8):
                                            3, parts=parts, reps=5)
         sizes = [int(o.ids.shape[0]) for o in outs]
         out[name] = {"seconds": round(dt, 4), "batches": sizes,
-                     "grid_shapes": [f"cs{c}rs{r}" for c, r in getattr(runner, "shape", [])],
+                     "grids": [g for g in getattr(runner, "grid", [])],
                      "predicted_speedup": round(t_full / dt, 2)}
         best = max(best or 0.0, t_full / dt)
         del outs, runner
@@ -1179,7 +1202,8 @@ def main():
     want_roof = (rank == 0 and not args.no_roofline and args.group == 1 and B <= 64
                  and not args.beam and args.dtype == "bf16")
     dt, outs, runner, info = run_captions(args, world, rank, device, pipe, n_local, lo, counts,
-                                          args.inflight, args.warmup, log_pass=want_roof)
+                                          args.inflight, args.warmup, log_pass=want_roof,
+                                          reps=max(1, args.reps))
     workload = (("C3 AudioCaps-eval" if args.beam else "C2 Clotho-eval")
                 + (" (1045 clips per rank)" if not (args.steps or args.clips) else "")
                 + ": STFT/log-mel + " + args.encoder.upper() + " + " + args.mapper
@@ -1204,6 +1228,28 @@ def main():
                    "parallelism": f"dp{world} (clip-sharded, RCCL all-gather of token ids)",
                    **info},
     }
+    reps_t = info["timed_reps_s"]
+    res["value_spread"] = {"median": res["value"], "min": round(n_total / max(reps_t), 2),
+                           "max": round(n_total / min(reps_t), 2), "reps": len(reps_t),
+                           "note": "value = the median of the timed repetitions of the whole "
+                                   "region (each: barrier + sync on both sides, max over ranks)"}
+    if info["persist_gave_up"]:
+        res["warning"] = (f"{info['persist_gave_up']} persistent decode launches gave up (grid "
+                          "not co-resident) and finished on the phase launches")
+    if world > 1 and not args.clips and args.group == 1 and not args.beam:
+        # strong scaling on the Clotho-eval set itself: its 1045 clips sharded over the ranks
+        # (what north_star's ">= 6x from 1 to 8 GPUs on Clotho-eval" measures), timed beside the
+        # weak-scaling value
+        slo, shi = zd.shard_range(CLOTHO_EVAL_CLIPS, rank, world)
+        scounts = zd.shard_counts(CLOTHO_EVAL_CLIPS, world)
+        dts, _, srun, sinfo = run_captions(args, world, rank, device, pipe, shi - slo, slo, scounts,
+                                           args.inflight, 1, reps=max(1, args.reps))
+        res["strong_1045"] = {"value": round(CLOTHO_EVAL_CLIPS / dts, 2), "unit": "clips/s",
+                              "clips_total": CLOTHO_EVAL_CLIPS, "clips_per_rank": scounts,
+                              "seconds": round(dts, 5), "timed_reps_s": sinfo["timed_reps_s"],
+                              "scaling": "strong",
+                              "grids_rank0": sinfo["persist_grids"]}
+        del srun
     headline_cfg = rank == 0 and args.group == 1 and B <= 64 and not args.beam
     if rank == 0 and not args.no_roofline and headline_cfg and args.dtype == "bf16":
         log("rooflines")
@@ -1254,7 +1300,8 @@ def main():
         res["c5_mistral"] = c5_mistral(args, device)
         log("id agreement")
         from tools import idparity
-        res["id_agreement"] = {"bf16": idparity.summary(torch.bfloat16, device),
+        res["id_agreement"] = {"bench_weights": BENCH_WEIGHTS_GOLDEN,
+                               "bf16": idparity.summary(torch.bfloat16, device),
                                "f32": idparity.summary(torch.float32, device)}
     if rank == 0 and world == 1 and not args.no_cpu_baseline and args.cpu_baseline_clips > 0:
         n2, n1, n3 = ((64, 50, 64) if args.cpu_baseline_full else

@@ -9,7 +9,11 @@ tools/idparity.py runs the batched pipeline on their CLAP embeddings).
     above tau at every step are bit-exact end to end.  tau is FIXED per golden: 2 x the
     reference's own bf16-vs-f32 first-step logit error, stored with the golden
     (make_goldens.py gen_tolerance); the GPU's bf16 error must not exceed it.  The compared
-    fraction of tokens is asserted per golden (c2_gpt2init, GPT-2's init scale: >= 0.6).
+    fraction of tokens is asserted per golden: c2_gpt2init (GPT-2's init scale, the bench's own
+    weights) >= 0.6, c2_margin_flat >= 0.5.  c1_greedy and c2_margin (std 0.1 / 0.05 blocks) are
+    too chaotic for a bf16 id gate -- the reference's OWN bf16 run is off by ~1 logit at step 0,
+    so their rule would compare < 2 % of the tokens; they are bit-exact in f32 only and are not
+    listed as bf16 gates.
 """
 import os
 import sys
@@ -23,6 +27,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 GOLDENS = ["c1_greedy", "c2_margin", "c2_margin_flat", "c2_gpt2init"]
+GOLDENS_BF16 = ["c2_margin_flat", "c2_gpt2init"]       # the goldens whose bf16 gate bites
 
 
 @pytest.mark.parametrize("name", GOLDENS)
@@ -36,7 +41,7 @@ def test_f32_ids_bit_exact(cuda, name):
     assert not bad, f"{name}: f32 greedy ids differ on clips {bad}"
 
 
-@pytest.mark.parametrize("name", GOLDENS)
+@pytest.mark.parametrize("name", GOLDENS_BF16)
 def test_bf16_ids_exact_above_margin(cuda, name):
     """The bf16 rule with a FIXED tolerance stored with the golden (tools/idparity.py
     margin_gate): tau = 2 x the reference's own bf16-vs-f32 first-step logit error; the GPU's bf16

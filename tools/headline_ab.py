@@ -2,12 +2,13 @@
 """Headline A/B in ONE process: the bench's C2 timed region (1045 clips, bs 64, persistent
 decode) repeated for several arms, interleaved, so box-to-box and run-to-run spread cancel.
 
-An arm is "name:inflight:knob=v,knob=v[:shapes]" (zs_tune_set knobs, reset to the baseline values
-given with --base between arms; shapes: the persistent-decode grid shapes the runner may use,
-zsaac.pipeline.persist_shapes, e.g. "21" or "12,11"); every arm runs on the first arm's streams,
-so list the arm with the most batches in flight first.
+An arm is "name:inflight:knob=v,knob=v[:grids[:budget]]" (zs_tune_set knobs, reset to the baseline
+values given with --base between arms; grids: the persistent-decode grid sizes the runner may use,
+zsaac.pipeline.persist_grids, e.g. "48" or "96-48" ('-'-separated); budget: workgroup slots of the
+in-flight grids); every arm runs on the first arm's streams, so list the arm with the most batches
+in flight first.
 
-    python tools/headline_ab.py --reps 6 "cs2:10::21" "base:5:" "l64:5:lean_min128=64"
+    python tools/headline_ab.py --reps 6 "b512:10::48:512" "base:5::48:256" "l64:5:lean_min128=64"
 """
 import argparse
 import os
@@ -24,7 +25,7 @@ import torch  # noqa: E402
 
 import bench  # noqa: E402
 from zsaac import _lib  # noqa: E402
-from zsaac.pipeline import ConcurrentRunner, persist_shapes  # noqa: E402
+from zsaac.pipeline import ConcurrentRunner, persist_grids  # noqa: E402
 
 # one hardware queue per stream (read at HIP init; after bench, whose import sets its default)
 os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("AB_HW_QUEUES", "16")
@@ -57,7 +58,8 @@ def main():
     for spec in a.arms:
         name, inflight, kn, *sh = spec.split(":")
         r = ConcurrentRunner(pipe, int(inflight), streams=streams,
-                             shapes=persist_shapes(sh[0]) if sh and sh[0] else None)
+                             grids=persist_grids(sh[0].replace("-", ",")) if sh and sh[0] else None,
+                             budget=int(sh[1]) if len(sh) > 1 and sh[1] else None)
         streams = streams or r.streams
         for size in sorted({b.shape[0] for b in batches}, reverse=True):
             r.warmup(next(b for b in batches if b.shape[0] == size))
@@ -72,6 +74,7 @@ def main():
             r.run(batches)
             torch.cuda.synchronize()
             dt = time.perf_counter() - t0
+            assert r.gave_up == 0, f"{name}: {r.gave_up} persistent launches gave up"
             if rep:                     # rep 0 warms every arm's kernels up
                 res[name].append(a.clips / dt)
         if rep:

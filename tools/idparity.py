@@ -121,11 +121,13 @@ def agreement(g, caps, hards=None) -> dict:
 # Every token before that step is compared; the compared fraction per golden is stated and
 # asserted (MIN_COMPARED_FRAC).
 TAU_MULT = 2.0
-MIN_COMPARED_FRAC = {"c1_greedy": 0.0,       # std-0.1 weights: the reference's own bf16 error is
-                     "c2_margin": 0.01,      #   1.0 logit at step 0, margins are within it at once
-                     "c2_margin_flat": 0.5,
-                     "c2_gpt2init": 0.6}     # GPT-2's init scale: the substantive bf16 check
+MIN_COMPARED_FRAC = {"c2_margin_flat": 0.5,
+                     "c2_gpt2init": 0.6}     # GPT-2's init scale (the bench's weights)
+# the bf16 gates: c1_greedy (std 0.1) and c2_margin (std 0.05) are reported by summary() but not
+# gated -- the reference's own bf16 error there is ~1 / 0.23 logit at step 0, so the rule would
+# compare < 2 % of their tokens
 GOLDENS_BF16 = ("c1_greedy", "c2_margin", "c2_margin_flat", "c2_gpt2init")
+GATED_BF16 = ("c2_margin_flat", "c2_gpt2init")
 
 
 def margin_gate(g, caps) -> dict:
@@ -175,6 +177,7 @@ def summary(dtype, device, names=GOLDENS_BF16) -> dict:
             if "bf16_ref_err" in g:
                 gate = margin_gate(g, caps)
                 gate["violations"] = len(gate["violations"])
+                gate["gated"] = name in GATED_BF16
                 r["margin_gate"] = gate
         out[name] = r
     return out

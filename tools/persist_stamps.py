@@ -3,7 +3,7 @@
 decode step, the median over workgroups of the compute before it (previous wait end -> arrive),
 the wait (arrive -> wait end) and the arrival skew (last - first arrive), in microseconds.
 
-    python tools/persist_stamps.py [step=3]
+    python tools/persist_stamps.py [step=3] [grid=48]
 """
 import json
 import os
@@ -32,12 +32,11 @@ def main():
     pipe, _, _ = bench.build(A, dev)
     wav = bench.synthetic_clips(64, 0, dev)
     pipe.caption_wav(wav)
-    rs = int(os.environ.get("ZSAAC_PERSIST_RS", "1"))
-    cs = int(os.environ.get("ZSAAC_PERSIST_CS", "1"))
-    G = ops.decode_persist_grid(rs, cs)
+    G = ops.decode_persist_grid(int(sys.argv[2]) if len(sys.argv) > 2 else 48)
     buf = torch.zeros(G, 128, dtype=torch.int64, device=dev)
     call("zs_decode_persist_set_stamps", buf.data_ptr(), step)
     dec = pipe.decoder
+    dec.persist_grid = G
     for _ in range(3):
         dec.greedy_begin(64)
         torch.cuda.synchronize()

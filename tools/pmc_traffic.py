@@ -118,16 +118,14 @@ def run_persist(reps=3):
         info.append(int(pipe.decoder.step_ctr.item()))
     plen = pipe.decoder.plen[:64].tolist()
     algo = bench.persist_launch_bytes(bench.gpt2_step_weight_bytes(pipe), plen, info[-1])
-    from zsaac import ops
     d = pipe.decoder
     with open(os.path.join(ROOT, "gpurun_out", "pmc_persist_run.json"), "w") as f:
         json.dump({"steps": info, "plen": plen, "algo_bytes_per_launch": algo,
-                   "col_split": d.persist_col_split, "row_split": d.persist_row_split,
-                   "workgroups": ops.decode_persist_grid(d.persist_row_split, d.persist_col_split)}, f)
+                   "workgroups": d.persist_grid}, f)
     print(json.dumps({"launches": reps, "steps": info, "algo_bytes_per_launch": algo}))
 
 
-def parse_persist(dfetch, dwrite, out, kname="decode_persist_kernel"):
+def parse_persist(dfetch, dwrite, out, kname="dg_persist_kernel"):
     fetch_kib, n_f = _per_dispatch(dfetch, "FETCH_SIZE", kname)
     write_kib, n_w = _per_dispatch(dwrite, "WRITE_SIZE", kname)
     rd, wr = 2 * 1024 * fetch_kib, 1024 * write_kib
@@ -135,8 +133,7 @@ def parse_persist(dfetch, dwrite, out, kname="decode_persist_kernel"):
         run_info = json.load(f)
     res = {"kernel": f"{kname} (zs_gpt2_decode_persist): one bs-64 eval batch of the bench "
                      f"(64 synthetic clips), decode steps 1..{run_info['steps'][-1] - 1}, one stream, "
-                     f"grid shape col_split {run_info.get('col_split', 1)} row_split "
-                     f"{run_info.get('row_split', 1)} ({run_info.get('workgroups', 48)} workgroups)",
+                     f"grid of {run_info.get('workgroups', 48)} 256-thread workgroups",
            "fetch_size_kib_median": fetch_kib, "write_size_kib_median": write_kib,
            "dispatches": [n_f, n_w], "hbm_read_bytes_per_launch": int(rd),
            "hbm_write_bytes_per_launch": int(wr), "hbm_bytes_per_launch": int(rd + wr),
