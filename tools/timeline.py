@@ -4,7 +4,7 @@ where the trace CSV lives; writes a small JSON summary):
 
     python3 tools/timeline.py <kernel_trace.csv dir> <out.json> [first_timed=8] [n_timed=17]
 
-The timed region = from the first to the last of the n_timed decode_persist_kernel dispatches
+The timed region = from the first to the last of the n_timed dg_persist_kernel dispatches
 starting at index first_timed (bench.py's order: per-pipeline warmups, warmup batches, then the
 timed batches).  Reports: how many persistent grids run at once over the region (time-weighted),
 each timed batch's gap on its queue between the previous persistent launch's end and its own
@@ -26,8 +26,8 @@ def main(d, out, first=8, n=17):
                 rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"],
                              r.get("Queue_Id") or r.get("Stream_Id") or ""))
     rows.sort()
-    per = [r for r in rows if "decode_persist_kernel" in r[2]]
-    timed = per[first:first + n]
+    per = [r for r in rows if "dg_persist_kernel" in r[2]]
+    timed = per[first:first + n] if first >= 0 else per[len(per) - n:]    # first < 0: the last n
     t0 = min(r[0] for r in timed)
     t1 = max(r[1] for r in timed)
     # time-weighted count of concurrent persistent grids
@@ -41,7 +41,7 @@ def main(d, out, first=8, n=17):
     conc = {k: round(v / span, 4) for k, v in sorted(hist.items())}
     # per-queue gaps before each timed persistent launch
     byq = {}
-    for r in per[:first + n]:
+    for r in per[:per.index(timed[-1]) + 1]:
         byq.setdefault(r[3], []).append(r)
     gaps = []
     for q, rs in byq.items():
@@ -50,7 +50,7 @@ def main(d, out, first=8, n=17):
                 gaps.append((b[0] - a[1]) / 1e6)
     other = {}
     for r in rows:
-        if r[0] >= t0 and r[1] <= t1 and "decode_persist_kernel" not in r[2]:
+        if r[0] >= t0 and r[1] <= t1 and "dg_persist_kernel" not in r[2]:
             k = r[2].split("(")[0][:80]
             other[k] = other.get(k, 0) + (r[1] - r[0]) / 1e6
     top = dict(sorted(other.items(), key=lambda kv: -kv[1])[:15])

@@ -851,39 +851,51 @@ __device__ __forceinline__ void phase_f(const Args& a, const Rs& rs, int w, cons
   lda<4, QS>(rs.xb, KSD, 0, QS * v, xf);
   const int nvb = (a.V + 15) >> 4;
   const int nb = (nvb - w + G - 1) / G;
-  u32x4_t R0[QS], R1[QS], R2[QS];
-  // the first block's weights stream during the LayerNorm; the other two slots are issued after
-  // it (all three in flight across it left too few registers for the normalisation)
-  ldw<1, QS>(a.wtep, KSD, w, QS * v, R0);
+  // ring of 3 block slots, each this wave's 6 weight fragments of the block plus the lane's 4
+  // per-token biases; every refill is unconditional (block index clamped to the workgroup's last
+  // block: a conditional load left the compiler counting conservatively, vmcnt(0) before every
+  // block, one round trip per block)
+  struct Slot {
+    u32x4_t w[QS];
+    float4 b;
+  };
+  Slot R0, R1, R2;
+  auto fill = [&](int i, Slot& r) {
+    const int blk = w + G * min(i, nb - 1);
+    ldw<1, QS>(a.wtep, KSD, blk, QS * v, r.w);
+    r.b = *reinterpret_cast<const float4*>(a.lmb + 16 * blk + 4 * (lane >> 4));
+  };
+  // the first block streams during the LayerNorm; the other two slots are issued after it (all
+  // three in flight across it left too few registers for the normalisation)
+  fill(0, R0);
   __builtin_amdgcn_sched_barrier(0);
   ln_frags<4>(xf, sm, 0);
-  if (nb > 1) ldw<1, QS>(a.wtep, KSD, w + G, QS * v, R1);
-  if (nb > 2) ldw<1, QS>(a.wtep, KSD, w + 2 * G, QS * v, R2);
+  fill(1, R1);
+  fill(2, R2);
   float bv = -INFINITY;
   int bi = 0x7fffffff;
   const bool tmp = a.temp != 1.0f;
   int buf = 0;
   lds_sync();     // the previous phase's slab readers are done
-  auto consume = [&](int i, const u32x4_t (&Rr)[QS]) {
+  auto consume = [&](int i, const Slot& r) {
     f32x4_t acc[4];
 #pragma unroll
     for (int rb = 0; rb < 4; ++rb) acc[rb] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int s = 0; s < QS; ++s)
 #pragma unroll
-      for (int rb = 0; rb < 4; ++rb) acc[rb] = mfma(Rr[s], xf[rb * QS + s], acc[rb]);
+      for (int rb = 0; rb < 4; ++rb) acc[rb] = mfma(r.w[s], xf[rb * QS + s], acc[rb]);
     f32x4_t* red = sm.red + buf * 1024;
 #pragma unroll
     for (int rb = 0; rb < 4; ++rb) red[(v * 4 + rb) * 64 + lane] = acc[rb];
     lds_sync();
-    const f32x4_t s = (red[v * 64 + lane] + red[(4 + v) * 64 + lane]) +
-                      (red[(8 + v) * 64 + lane] + red[(12 + v) * 64 + lane]);
+    const f32x4_t sum = (red[v * 64 + lane] + red[(4 + v) * 64 + lane]) +
+                        (red[(8 + v) * 64 + lane] + red[(12 + v) * 64 + lane]);
     const int col0 = 16 * (w + G * i) + 4 * (lane >> 4);
-    const float4 lb = *reinterpret_cast<const float4*>(a.lmb + col0);
-    const float lbv[4] = {lb.x, lb.y, lb.z, lb.w};
+    const float lbv[4] = {r.b.x, r.b.y, r.b.z, r.b.w};
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      const float lg = s[e] + lbv[e];
+      const float lg = sum[e] + lbv[e];
       const float val = tmp ? lg / a.temp : lg;
       if (col0 + e < a.V && val > bv) { bv = val; bi = col0 + e; }
     }
@@ -892,15 +904,11 @@ __device__ __forceinline__ void phase_f(const Args& a, const Rs& rs, int w, cons
 #pragma nounroll
   for (int i = 0; i < nb; i += 3) {
     consume(i, R0);
-    if (i + 3 < nb) ldw<1, QS>(a.wtep, KSD, w + G * (i + 3), QS * v, R0);
-    if (i + 1 < nb) {
-      consume(i + 1, R1);
-      if (i + 4 < nb) ldw<1, QS>(a.wtep, KSD, w + G * (i + 4), QS * v, R1);
-    }
-    if (i + 2 < nb) {
-      consume(i + 2, R2);
-      if (i + 5 < nb) ldw<1, QS>(a.wtep, KSD, w + G * (i + 5), QS * v, R2);
-    }
+    fill(i + 3, R0);
+    if (i + 1 < nb) consume(i + 1, R1);     // (wave-uniform)
+    fill(i + 4, R1);
+    if (i + 2 < nb) consume(i + 2, R2);
+    fill(i + 5, R2);
   }
   // the 4 lanes of a row (l % 16 equal): larger logit, then the lower id
 #pragma unroll
