@@ -510,8 +510,9 @@ int zs_decode_persist_status(const void* ws, int* timed_out);
 /* zs_decode_persist_set_stamps: diagnostic phase timing (tools/persist_stamps.py): with buf !=
  * NULL ([grid][128] u64), thread 0 of every workgroup of later launches writes s_memrealtime
  * (100 MHz) at each barrier arrive (slot 2i) / wait end (2i + 1) of decode step `step`, and at
- * that step's start (127) / end (126).  NULL turns it off. */
-int zs_decode_persist_set_stamps(void* buf, int step);
+ * that step's start (127) / end (126); ws != NULL: only the launches on that workspace (one of
+ * several concurrent grids).  buf NULL turns it off. */
+int zs_decode_persist_set_stamps(void* buf, int step, const void* ws);
 
 /* zs_beam_step: generate_beam's per-step update (gpt2_prefix_eval.py:119-151) for C clips x
  * `beam` rows, from zs_lmhead_topk partials (topk >= beam) with log(softmax) semantics.

@@ -9,7 +9,10 @@
     workgroup-microseconds one step costs (k x workgroups x wall / steps; a workgroup is half a
     CU).
 
-    python tools/grid_bench.py [reps=4] [grids=48,96,192] [ks=1,2,4,5,8,10]
+    python tools/grid_bench.py [reps=4] [grids=48,96,192] [ks=1,2,4,5,8,10] [exps=0]
+
+exps: zs_tune_set("dg_exp") traffic experiments (bit 0: hand-off loads / stores dropped, bit 1:
+attention reads one cached key): ids are garbage under them, only the rates mean something.
 """
 import json
 import os
@@ -31,7 +34,9 @@ def main():
     reps = int(sys.argv[1]) if len(sys.argv) > 1 else 4
     grids = [int(g) for g in (sys.argv[2] if len(sys.argv) > 2 else "48,96,192").split(",")]
     ks = [int(k) for k in (sys.argv[3] if len(sys.argv) > 3 else "1,2,4,5,8,10").split(",")]
+    exps = [int(k) for k in (sys.argv[4] if len(sys.argv) > 4 else "0").split(",")]
     from zsaac import ops
+    from zsaac._lib import call
 
     class A:
         batch, dtype, encoder, mapper, beam, entry_length, group, compact = \
@@ -75,8 +80,9 @@ def main():
                      "steps": steps, "note": "graph-replayed chunks incl. host polling"}
     print(json.dumps({"phases": res["phases"]}), flush=True)
     dec.persist = True
-    for g in grids:
-        key = f"g{g}"
+    for exp, g in [(e, g) for e in exps for g in grids]:
+        call("zs_tune_set", b"dg_exp", exp)
+        key = f"g{g}" + (f"_exp{exp}" if exp else "")
         decode(pipes[:1], streams[:1], g)
         torch.cuda.synchronize()
         t0 = time.perf_counter()

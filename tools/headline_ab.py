@@ -2,11 +2,11 @@
 """Headline A/B in ONE process: the bench's C2 timed region (1045 clips, bs 64, persistent
 decode) repeated for several arms, interleaved, so box-to-box and run-to-run spread cancel.
 
-An arm is "name:inflight:knob=v,knob=v[:grids[:budget]]" (zs_tune_set knobs, reset to the baseline
-values given with --base between arms; grids: the persistent-decode grid sizes the runner may use,
-zsaac.pipeline.persist_grids, e.g. "48" or "96-48" ('-'-separated); budget: workgroup slots of the
-in-flight grids); every arm runs on the first arm's streams, so list the arm with the most batches
-in flight first.
+An arm is "name:inflight:knob=v,knob=v[:grids[:budget[:encode_ahead]]]" (zs_tune_set knobs, reset
+to the baseline values given with --base between arms; grids: the persistent-decode grid sizes the
+runner may use, zsaac.pipeline.persist_grids, e.g. "48" or "96-48" ('-'-separated); budget:
+workgroup slots of the in-flight grids; encode_ahead: clips per up-front encoder pass, 0 = each
+batch encodes its own clips, suffix "f": every begin waits for the whole encode); every arm runs on one shared set of streams.
 
     python tools/headline_ab.py --reps 6 "b512:10::48:512" "base:5::48:256" "l64:5:lean_min128=64"
 """
@@ -54,13 +54,16 @@ def main():
     batches = [pool[x:y] for x, y in bench.split_batches(a.clips, 64)]
     base = knobs(a.base)
     arms = []
-    streams = None       # one set of dedicated streams for every arm (distinct hardware queues)
+    from zsaac import ops
+    # one set of dedicated streams for every arm (distinct hardware queues)
+    streams = ops.dedicated_streams(max(int(x.split(":")[1]) for x in a.arms) + 1, dev)
     for spec in a.arms:
         name, inflight, kn, *sh = spec.split(":")
         r = ConcurrentRunner(pipe, int(inflight), streams=streams,
                              grids=persist_grids(sh[0].replace("-", ",")) if sh and sh[0] else None,
-                             budget=int(sh[1]) if len(sh) > 1 and sh[1] else None)
-        streams = streams or r.streams
+                             budget=int(sh[1]) if len(sh) > 1 and sh[1] else None,
+                             encode_ahead=int(sh[2].rstrip("f")) if len(sh) > 2 and sh[2] else 0,
+                             encode_first=len(sh) > 2 and sh[2].endswith("f"))
         for size in sorted({b.shape[0] for b in batches}, reverse=True):
             r.warmup(next(b for b in batches if b.shape[0] == size))
         arms.append((name, r, knobs(kn)))

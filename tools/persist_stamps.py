@@ -2,8 +2,10 @@
 """Phase timing inside the persistent decode (zs_decode_persist_set_stamps): per barrier of one
 decode step, the median over workgroups of the compute before it (previous wait end -> arrive),
 the wait (arrive -> wait end) and the arrival skew (last - first arrive), in microseconds.
+bg > 0: the traced grid runs beside bg other batches' grids of the same size (pipeline twins on
+their own streams, decode only), the load of the headline.
 
-    python tools/persist_stamps.py [step=3] [grid=48]
+    python tools/persist_stamps.py [step=3] [grid=48] [bg=0]
 """
 import json
 import os
@@ -33,14 +35,24 @@ def main():
     wav = bench.synthetic_clips(64, 0, dev)
     pipe.caption_wav(wav)
     G = ops.decode_persist_grid(int(sys.argv[2]) if len(sys.argv) > 2 else 48)
+    nbg = int(sys.argv[3]) if len(sys.argv) > 3 else 0
+    pipes = [pipe] + [pipe.twin() for _ in range(nbg)]
+    streams = ops.dedicated_streams(len(pipes), dev)
+    for p, s in zip(pipes, streams):
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            p.caption_wav(wav)
+        p.decoder.persist_grid = G
+    torch.cuda.synchronize()
     buf = torch.zeros(G, 128, dtype=torch.int64, device=dev)
-    call("zs_decode_persist_set_stamps", buf.data_ptr(), step)
     dec = pipe.decoder
-    dec.persist_grid = G
+    call("zs_decode_persist_set_stamps", buf.data_ptr(), step, dec.persist_ws.data_ptr())
     for _ in range(3):
-        dec.greedy_begin(64)
+        for p, s in reversed(list(zip(pipes, streams))):   # the traced grid last
+            with torch.cuda.stream(s):
+                p.decoder.greedy_begin(64)
         torch.cuda.synchronize()
-    call("zs_decode_persist_set_stamps", None, 0)
+    call("zs_decode_persist_set_stamps", None, 0, None)
     t = buf.cpu().numpy().astype(np.float64) / 100.0     # us (100 MHz)
     start, end = t[:, 127], t[:, 126]
     names = []
@@ -73,7 +85,7 @@ def main():
     summ["F"] = {"compute_med": rows[-1]["compute_med"], "wait_med": rows[-1]["wait_med"]}
     summ["G"] = round(float(np.median(g_phase)), 2)
     summ["step_us"] = round(float(np.median(end - start)), 1)
-    print(json.dumps({"per_phase_kind_mean_us": summ}))
+    print(json.dumps({"grid": G, "background_grids": nbg, "per_phase_kind_mean_us": summ}))
     # phase F per workgroup, and by blockIdx % 8 (the XCD under round-robin dispatch)
     fc = comp[-1]
     print(json.dumps({"F_compute_by_wg": [round(float(x), 1) for x in fc],

@@ -63,6 +63,7 @@
 namespace zs {
 int g_dp_spin = 0;   // zs_tune_set("dp_spin", n): give up a grid-barrier wait after n polls (0 =
                      // the default 2^22, < 0: at the first unmet poll); tests force the give-up
+int g_dg_exp = 0;    // zs_tune_set("dg_exp", m): traffic experiments (grid_bench only; ids garbage)
 int g_dp_abort = -1; // zs_tune_set("dp_abort_step", k): every workgroup gives up at the start of
                      // decode step k (a mid-launch give-up for the resume test); -1 = never
 namespace dg {
@@ -123,7 +124,7 @@ constexpr int SM_ST = SM_LN + 2048;               // int tok[64], pos[64], done[
 constexpr int SM_TOTAL = SM_ST + (3 * RM + 16) * 4;
 
 struct Args {
-  int R, Lmax, max_steps, stop0, stop1, V, layer, abort_step;
+  int R, Lmax, max_steps, stop0, stop1, V, layer, abort_step, exp;
   unsigned spin_max;
   int kv_bytes;         // bytes of one layer's K (or V) cache
   float temp;
@@ -147,12 +148,13 @@ struct Rs {
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t mk(void* p, int bytes) {
   return __builtin_amdgcn_make_buffer_rsrc(p, (short)0, bytes, 0x00020000);
 }
-__device__ __forceinline__ Rs make_rs(char* ws) {
+__device__ __forceinline__ Rs make_rs(char* ws, int exp) {
   Rs r;
-  r.q = mk(ws + WS_Q, RM * D * 2);
-  r.att = mk(ws + WS_ATT, RM * D * 2);
-  r.xb = mk(ws + WS_XB, RM * D * 2);
-  r.hid = mk(ws + WS_HID, RM * DFF * 2);
+  const int z = (exp & 1) ? 0 : 1;
+  r.q = mk(ws + WS_Q, z * RM * D * 2);
+  r.att = mk(ws + WS_ATT, z * RM * D * 2);
+  r.xb = mk(ws + WS_XB, z * RM * D * 2);
+  r.hid = mk(ws + WS_HID, z * RM * DFF * 2);
   return r;
 }
 // aux 16 = sc1: stores write through, loads bypass this CU's L1 (the hand-off forms)
@@ -261,6 +263,7 @@ __device__ __forceinline__ int frag_off(int row, int col, int KS) {
 // its start (127) / end (126), into buf[w][128] (tools/persist_stamps.py).  NULL = off.
 __device__ unsigned long long* dp_stamp_buf;
 __device__ int dp_stamp_step;
+__device__ const char* dp_stamp_ws;   // only the launch on this workspace (NULL: every launch)
 #define DP_NB 64
 __device__ __forceinline__ void stamp(unsigned long long* sb, int slot) {
   if (sb != nullptr && threadIdx.x == 0) {
@@ -716,7 +719,7 @@ __device__ __forceinline__ void attn_unit(const Args& a, const Sm& sm, int u, in
   row = u / NH;
   hh = u % NH;
   const int rr = min(row, a.R - 1);
-  p = min(sm.pos[rr], a.Lmax - 1);
+  p = (a.exp & 2) ? 1 : min(sm.pos[rr], a.Lmax - 1);
   base = ((long)(rr * NH + hh) * a.Lmax) * HD + 8 * ((otid() & 63) & 7);
 }
 template <int KU>
@@ -987,11 +990,12 @@ __global__ __launch_bounds__(NT, 2) void dg_persist_kernel(Args a) {
   if (step >= a.max_steps) return;
   load_state(a, sm);
   __syncthreads();
-  const Rs rs = make_rs(a.ws);
+  const Rs rs = make_rs(a.ws, a.exp);
   Bar bar{(gu32*)(a.ws + WS_SH), (gu32*)(a.ws + WS_TMO), 0, G / NSH, a.spin_max, nullptr, 0};
   gu64* const keys = (gu64*)(a.ws + WS_KEY);
   volatile lds_int_t* s_ok = (volatile lds_int_t*)(sm.misc + 8);
-  unsigned long long* const stamps = dp_stamp_buf;
+  unsigned long long* const stamps =
+      (dp_stamp_ws == nullptr || dp_stamp_ws == a.ws) ? dp_stamp_buf : nullptr;
   const int stamp_step = dp_stamp_step;
   const int ub = w * Units<G>::UPG;
   constexpr int ANCG = NCB_Q / Gm::ACB, DNCG = NCB_F / Gm::DCB, ENCG = NCB_D / Gm::ECB;
@@ -1069,7 +1073,7 @@ __global__ __launch_bounds__(NT, 2) void dg_phase_kernel(Args a) {
   if (*a.step_ctr >= a.max_steps) return;
   load_state(a, sm);
   __syncthreads();
-  const Rs rs = make_rs(a.ws);
+  const Rs rs = make_rs(a.ws, a.exp);
   if constexpr (PH == PH_A) {
     u32x4_t wq[Gm::APF * QS];
     phase_a<G, true>(a, rs, l, w, sm, wq);
@@ -1143,6 +1147,7 @@ int dg_args(dg::Args& a, int R, int Lmax, int max_steps, int stop0, int stop1, i
   a.R = R; a.Lmax = Lmax; a.max_steps = max_steps; a.stop0 = stop0; a.stop1 = stop1; a.V = V;
   a.spin_max = g_dp_spin > 0 ? (unsigned)g_dp_spin : g_dp_spin < 0 ? 0u : SPIN_MAX;
   a.abort_step = g_dp_abort;
+  a.exp = g_dg_exp;
   a.kv_bytes = R * NH * Lmax * HD * 2;
   a.temp = temperature;
   a.wte = (const bf16_t*)wte; a.wpe = (const bf16_t*)wpe;
@@ -1233,8 +1238,9 @@ extern "C" int zs_gpt2_decode_phases(int R, int Lmax, int max_steps, int stop0, 
   return 0;
 }
 
-extern "C" int zs_decode_persist_set_stamps(void* buf, int step) {
+extern "C" int zs_decode_persist_set_stamps(void* buf, int step, const void* ws) {
   ZS_CHECK_HIP(hipMemcpyToSymbol(HIP_SYMBOL(dg::dp_stamp_buf), &buf, sizeof(buf)));
+  ZS_CHECK_HIP(hipMemcpyToSymbol(HIP_SYMBOL(dg::dp_stamp_ws), &ws, sizeof(ws)));
   ZS_CHECK_HIP(hipMemcpyToSymbol(HIP_SYMBOL(dg::dp_stamp_step), &step, sizeof(step)));
   return 0;
 }

@@ -717,7 +717,9 @@ static int dispatch_fast(GemmArgs& g, hipStream_t st) {
     if (!lt && g_lean96 && g.N % 96 == 0 && g.N <= 1536 && nblocks(g, 128, 96) >= 384)
       return launch_lean<128, 96, 2, 64, 4, 1>(g, st);
     if (lt == 1 || (!lt && n128 >= g_lean_min128)) return launch_lean<128, 128, 2, 64>(g, st);
-    if (!lt && n128 >= 128) return launch_lean<128, 128, 4, 64, 2, 4>(g, st);
+    // (3 stages, 96 KiB of LDS: the 4-stage ring's 128 KiB does not fit beside a persistent decode
+    // workgroup's 35 KiB, and the prefill would wait for a decode grid to end)
+    if (!lt && n128 >= 128) return launch_lean<128, 128, 3, 64, 2, 4>(g, st);
     if (lt == 2 || (!lt && nblocks(g, 128, 64) >= 256))
       return g.M >= g.N ? launch_lean<128, 64, 3, 64>(g, st) : launch_lean<64, 128, 3, 64>(g, st);
     // 64x64 with 128-deep k-steps when a 64x64 grid is still under one tile per CU at >= 512

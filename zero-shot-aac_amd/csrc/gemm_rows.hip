@@ -64,8 +64,11 @@ struct RowsArgs {
   const float* Af; const float* Wf;         // f32 operands (gemm_rows_f32_kernel)
 };
 
+// 8-wave instances at <= 128 registers (4 waves per SIMD's worth): two of their waves per SIMD
+// then fit beside a persistent decode workgroup (4 waves x 256 registers), so a begin's mapper
+// GEMM does not wait for a decode grid to end
 template <int NT, int WAVES, int LNM, int S>
-__global__ __launch_bounds__(64 * WAVES) void gemm_rows_kernel(RowsArgs g) {
+__global__ __launch_bounds__(64 * WAVES, WAVES == 8 ? 4 : 1) void gemm_rows_kernel(RowsArgs g) {
   constexpr bool LN = LNM != 0, AFF = LNM == 1;
   // S = 32-deep k-steps per wave (K = 32 * WAVES * S), a template parameter so that every load
   // is issued unconditionally and up front (a runtime trip count put each load in its own

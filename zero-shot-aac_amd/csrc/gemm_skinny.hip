@@ -265,6 +265,7 @@ extern int g_gemm_big;      // gemm.hip
 extern int g_big_min;       // gemm.hip
 extern int g_dp_spin;       // decode_grid.hip
 extern int g_dp_abort;      // decode_grid.hip
+extern int g_dg_exp;
 extern int g_beam_xcd;      // attn.hip
 
 // choose K per workgroup: a multiple of 64 dividing K, each wave <= 128 deep, ~256-320 WGs
@@ -319,6 +320,7 @@ extern "C" int zs_tune_set(const char* key, int value) {
   if (!strcmp(key, "big_min")) { g_big_min = value; return 0; }
   if (!strcmp(key, "dp_spin")) { g_dp_spin = value; return 0; }
   if (!strcmp(key, "dp_abort_step")) { g_dp_abort = value; return 0; }
+  if (!strcmp(key, "dg_exp")) { g_dg_exp = value; return 0; }
   if (!strcmp(key, "beam_xcd")) { g_beam_xcd = value; return 0; }
   return fail(ZS_ERR_ARG, "zs_tune_set: unknown key %s", key);
 }

@@ -74,7 +74,7 @@ SIGNATURES = {
     "zs_gpt2_decode_persist": [I, I, I, I, I, I, P, P, P, F, P, P, P, P, P, P, P, P, P, P, P, L, I, P],
     "zs_gpt2_decode_phases": [I, I, I, I, I, I, P, P, P, F, P, P, P, P, P, P, P, P, P, P, P, L, I, I, P],
     "zs_decode_persist_status": [P, P],
-    "zs_decode_persist_set_stamps": [P, I],
+    "zs_decode_persist_set_stamps": [P, I, P],
     "zs_beam_step": [P, P, P, I, I, I, I, I, I, P, I, P, P, P, P, P, P, P, I, P, P, P, P],
     "zs_bert_embed_ln": [P, I, I, P, P, P, P, P, F, P, P, I, P],
     "zs_layernorm_dual": [P, I, I, I, P, P, F, P, I, P, I, I, P],

@@ -173,9 +173,12 @@ class AudioEncoder:
         self.proj = AudioProjWeights(sd, self.dev, dtype) if "audio_proj.0.weight" in sd else None
         self._alloc()
 
-    def twin(self):
-        """Same packed weights, private activation buffers (for another stream)."""
+    def twin(self, max_batch=None):
+        """Same packed weights, private activation buffers (for another stream), sized for
+        ``max_batch`` clips per pass (default: this encoder's)."""
         t = copy.copy(self)
+        if max_batch:
+            t.B = int(max_batch)
         t._alloc()
         return t
 

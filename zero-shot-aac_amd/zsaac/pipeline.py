@@ -278,7 +278,8 @@ class ConcurrentRunner:
     Results are copied out on the pipeline's stream before it takes the next batch."""
 
     def __init__(self, pipe: CaptionPipeline, n_inflight: int = 2, streams: Optional[list] = None,
-                 grids: Optional[List[int]] = None, budget: Optional[int] = None):
+                 grids: Optional[List[int]] = None, budget: Optional[int] = None,
+                 encode_ahead: int = 0, encode_first: bool = False):
         self.cus = torch.cuda.get_device_properties(pipe.dev).multi_processor_count
         # persistent grids (greedy bf16 at <= 64 rows; beam search never launches one), one size
         # per batch from `grids` (largest first, see choose_persist_grid)
@@ -290,12 +291,25 @@ class ConcurrentRunner:
             n_inflight = max(1, min(n_inflight, self.budget // self.grids[-1]))
         self.n_inflight = n_inflight
         self.pipes = [pipe] + [pipe.twin() for _ in range(n_inflight - 1)]
+        # encode_ahead > 0 (waveform inputs): one encoder twin sized for that many clips encodes
+        # every batch's clips up front, in passes of up to encode_ahead clips (consecutive
+        # batches), on a stream of its own; a batch's begin (mapper .. step 0) waits only for its
+        # own pass.  The encoder then runs at its most efficient size and before the decode grids
+        # fill the chip; captions do not depend on it (a clip's embedding is its own).
+        # encode_first: every begin waits for the LAST pass (encoding and decoding do not share
+        # the chip).
+        self.encode_ahead = int(encode_ahead) if pipe.encoder is not None else 0
+        self.encode_first = bool(encode_first)
+        self.enc = pipe.encoder.twin(max_batch=self.encode_ahead) if self.encode_ahead else None
+        need = len(self.pipes) + (1 if self.enc is not None else 0)
         # dedicated streams on distinct hardware queues: pooled torch streams take their queue at
         # first use and can end up sharing one, which serializes the batches
         # (``streams``: reuse another runner's, at least as many -- tools/headline_ab.py)
-        self.streams = (list(streams[:len(self.pipes)]) if streams is not None
-                        else ops.dedicated_streams(len(self.pipes), pipe.dev))
-        assert len(self.streams) == len(self.pipes), "ConcurrentRunner: too few streams given"
+        streams = (list(streams[:need]) if streams is not None
+                   else ops.dedicated_streams(need, pipe.dev))
+        assert len(streams) == need, "ConcurrentRunner: too few streams given"
+        self.streams = streams[:len(self.pipes)]
+        self.enc_stream = streams[len(self.pipes)] if self.enc is not None else None
 
     def warmup(self, wav: torch.Tensor):
         """Runs one batch per pipeline synchronously (captures every decode graph)."""
@@ -325,6 +339,9 @@ class ConcurrentRunner:
         caller = torch.cuda.current_stream(self.pipes[0].dev)
         for s in self.streams:           # inputs were produced on the caller's stream
             s.wait_stream(caller)
+        ahead = None
+        if inputs == "wav" and self.enc is not None:
+            ahead = self._encode_ahead(batches, caller)
         active = {}
         nxt = 0
         self.decode_steps = [0] * len(batches)     # per batch: decode steps actually enqueued
@@ -345,7 +362,12 @@ class ConcurrentRunner:
                             slots[i] = g
                             self.grid[nxt] = g
                         with torch.cuda.stream(s):
-                            (p.begin_wav if inputs == "wav" else p.begin_emb)(batches[nxt])
+                            if ahead is not None:
+                                embs, evs = ahead
+                                s.wait_event(evs[nxt])
+                                p.begin_emb(embs[nxt])
+                            else:
+                                (p.begin_wav if inputs == "wav" else p.begin_emb)(batches[nxt])
                             ev, flag = p.decoder.finished_async()
                         active[i] = (nxt, 0, ev, flag)
                         self.assign.append((i, nxt))
@@ -386,7 +408,58 @@ class ConcurrentRunner:
                 time.sleep(20e-6)
         for s in self.streams:           # results are consumed on the caller's stream
             caller.wait_stream(s)
+        if ahead is not None:
+            caller.wait_stream(self.enc_stream)
         return results
+
+    def _encode_ahead(self, batches, caller):
+        """Enqueues the encoder passes of every batch on the encoder stream: consecutive batches
+        grouped up to encode_ahead clips (one view when they are adjacent rows of one tensor, as
+        the bench's are, else concatenated).  Returns (per-batch embedding views, per-batch
+        event of the pass that produced them)."""
+        E, enc, es = self.encode_ahead, self.enc, self.enc_stream
+        n = sum(int(b.shape[0]) for b in batches)
+        emb = torch.empty(n, 1024, device=self.pipes[0].dev)
+        es.wait_stream(caller)
+        embs, evs = [], []
+        i, c0 = 0, 0
+        with torch.cuda.stream(es):
+            while i < len(batches):
+                j, m = i, 0
+                while j < len(batches) and m + int(batches[j].shape[0]) <= E:
+                    m += int(batches[j].shape[0])
+                    j += 1
+                assert j > i, f"a batch of {batches[i].shape[0]} clips > encode_ahead {E}"
+                wav = _rows_span(batches[i:j])
+                emb[c0:c0 + m].copy_(enc.encode(wav))
+                ev = torch.cuda.Event()
+                ev.record(es)
+                for b in batches[i:j]:
+                    embs.append(emb[c0:c0 + int(b.shape[0])])
+                    evs.append(ev)
+                    c0 += int(b.shape[0])
+                i = j
+        if self.encode_first:
+            evs = [evs[-1]] * len(evs)
+        return embs, evs
+
+
+def _rows_span(ts: Sequence[torch.Tensor]) -> torch.Tensor:
+    """The row-wise concatenation of 2-D tensors: a view when they are adjacent row ranges of one
+    contiguous tensor, else a copy."""
+    if len(ts) == 1:
+        return ts[0]
+    t0 = ts[0]
+    adjacent = all(t.is_contiguous() and t.dtype == t0.dtype and t.shape[1:] == t0.shape[1:]
+                   for t in ts)
+    ptr = t0.data_ptr()
+    for t in ts:
+        adjacent = adjacent and t.data_ptr() == ptr
+        ptr += t.numel() * t.element_size()
+    if adjacent:
+        rows = sum(int(t.shape[0]) for t in ts)
+        return t0.as_strided((rows,) + tuple(t0.shape[1:]), t0.stride())
+    return torch.cat(list(ts))
 
 
 def _copy_batch(r: CaptionBatch, consumer=None) -> CaptionBatch:
