@@ -114,3 +114,95 @@ def test_bench_gather_path_gloo_world2():
         assert gl[c] == L and gi[c][:L] == [1000 * c + t for t in range(L)]
         assert bl[c] == L and bi[c][:L] == [1000 * c + 100 * (c % 3) + t for t in range(L)]
         assert ge[c] == [float(c)] * 4
+
+
+class _CpuRunner:
+    """A CPU stand-in for zsaac.pipeline.ConcurrentRunner: one 'caption' per clip derived from its
+    waveform (so the test can recompute it from bench.synthetic_clips), after a rank-dependent
+    sleep (so the job time must be the slower rank's)."""
+    delay = 0.0
+
+    def __init__(self, pipe, n_inflight=2, streams=None, grids=None, budget=None, **kw):
+        self.pipes, self.n_inflight, self.gave_up = [pipe], n_inflight, 0
+        self.grid, self.decode_steps = [], []
+
+    def warmup(self, wav):
+        pass
+
+    def run(self, batches, keep=None, inputs="wav"):
+        import time
+        from types import SimpleNamespace
+        time.sleep(self.delay)
+        self.grid = [0] * len(batches)
+        self.decode_steps = [1] * len(batches)
+        return [SimpleNamespace(ids=_fake_ids(b), lengths=_fake_len(b), scores=None)
+                for b in batches]
+
+
+def _fake_ids(wav):
+    return (wav[:, :6] * 1e4).round().to(torch.int32)
+
+
+def _fake_len(wav):
+    return (wav[:, 0].abs() * 1e4).round().to(torch.int32) % 6 + 1
+
+
+def _run_captions_worker(rank, world, port, n, B, reps, q):
+    """bench.run_captions' world > 1 branch on CPU (gloo): collect_captions inside the timed
+    region, the barrier, the all_reduce(MAX) of each repetition's time, the median."""
+    import sys
+    import torch.distributed as dist
+    from types import SimpleNamespace
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    import bench
+    import zsaac.pipeline as zp
+    from zsaac import dist as zd
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.cuda.synchronize = lambda *a, **k: None       # no GPU here: nothing to wait for
+    bench.run_streams = lambda device, k: [None] * k
+    zp.ConcurrentRunner = _CpuRunner
+    _CpuRunner.delay = 0.05 * rank                      # rank 1 is the slow one
+    lo, hi = zd.shard_range(n, rank, world)
+    counts = zd.shard_counts(n, world)
+    pipe = SimpleNamespace(cfg=SimpleNamespace(batch=B, beam=0),
+                           decoder=SimpleNamespace(n_captures=0, rows_stepped=0, persist=False))
+    args = SimpleNamespace(persist_budget=0)
+    dt, outs, runner, info = bench.run_captions(args, world, rank, torch.device("cpu"), pipe,
+                                                hi - lo, lo, counts, 2, 1, reps=reps)
+    ids, lens = zd.collect_captions(outs, counts)
+    q.put((rank, dt, info["timed_reps_s"], info["persist_gave_up"],
+           ids.tolist() if rank == 0 else None, lens.tolist() if rank == 0 else None))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_run_captions_world2_gloo():
+    """bench.run_captions at world 2 (its world > 1 branch, bench.py): both ranks report the
+    slower rank's time for every repetition (all_reduce MAX), the median of `reps`, and the
+    gathered captions are every clip's in clip order (ragged shards: 13 + 12 clips, batches of 4)."""
+    n, B, world, reps = 25, 4, 2, 3
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_run_captions_worker, args=(r, world, port, n, B, reps, q))
+          for r in range(world)]
+    for p in ps:
+        p.start()
+    got = dict((r[0], r[1:]) for r in (q.get(timeout=180) for _ in range(world)))
+    for p in ps:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    (dt0, reps0, gu0, ids, lens), (dt1, reps1, gu1, _, _) = got[0], got[1]
+    assert len(reps0) == reps and reps0 == reps1          # the same (max-over-ranks) times
+    assert dt0 == dt1 and min(reps0) >= 0.05               # rank 1's 50 ms sleep bounds them
+    assert abs(dt0 - sorted(reps0)[reps // 2]) < 1e-4       # the median (times rounded to 10 us)
+    assert gu0 == gu1 == 0
+    wav = bench.synthetic_clips(n, 0, torch.device("cpu"))
+    assert lens == _fake_len(wav).tolist()
+    assert all(ids[c][:lens[c]] == _fake_ids(wav)[c, :lens[c]].tolist() for c in range(n))

@@ -6,7 +6,8 @@ An arm is "name:inflight:knob=v,knob=v[:grids[:budget[:encode_ahead]]]" (zs_tune
 to the baseline values given with --base between arms; grids: the persistent-decode grid sizes the
 runner may use, zsaac.pipeline.persist_grids, e.g. "48" or "96-48" ('-'-separated); budget:
 workgroup slots of the in-flight grids; encode_ahead: clips per up-front encoder pass, 0 = each
-batch encodes its own clips, suffix "f": every begin waits for the whole encode); every arm runs on one shared set of streams.
+batch encodes its own clips, suffix "f": every begin waits for the whole encode; a 7th field "bf":
+begin_first, every pipeline begins at once and the launches follow within the budget); every arm runs on one shared set of streams.
 
     python tools/headline_ab.py --reps 6 "b512:10::48:512" "base:5::48:256" "l64:5:lean_min128=64"
 """
@@ -63,7 +64,8 @@ def main():
                              grids=persist_grids(sh[0].replace("-", ",")) if sh and sh[0] else None,
                              budget=int(sh[1]) if len(sh) > 1 and sh[1] else None,
                              encode_ahead=int(sh[2].rstrip("f")) if len(sh) > 2 and sh[2] else 0,
-                             encode_first=len(sh) > 2 and sh[2].endswith("f"))
+                             encode_first=len(sh) > 2 and sh[2].endswith("f"),
+                             begin_first=len(sh) > 3 and sh[3] == "bf")
         for size in sorted({b.shape[0] for b in batches}, reverse=True):
             r.warmup(next(b for b in batches if b.shape[0] == size))
         arms.append((name, r, knobs(kn)))

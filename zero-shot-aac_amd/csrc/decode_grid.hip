@@ -365,65 +365,62 @@ __device__ __forceinline__ void reduce_tiles(f32x4_t* red, const f32x4_t (&acc)[
 }
 
 // ------------------------------------------------------------------ LayerNorm in registers
-// an opaque redefinition of fragments: keeps the compiler from merging the unpacks of the
-// LayerNorm's three passes (it held all 192 unpacked f32 values across them, and spilled)
-template <int N>
-__device__ __forceinline__ void opaque(u32x4_t* x) {
-#pragma unroll
-  for (int i = 0; i < N; ++i) asm volatile("" : "+v"(x[i]));
+typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2_t;
+typedef __attribute__((ext_vector_type(2))) float f32x2_t;
+// x.lo * y.lo + x.hi * y.hi + c over a bf16 pair (v_dot2c_f32_bf16)
+__device__ __forceinline__ float dot2bf(unsigned x, unsigned y, float c) {
+  return __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2_t, x), __builtin_bit_cast(bf16x2_t, y),
+                                         c, false);
 }
 // xf: this wave's K-quarter fragments of row blocks rb0 .. rb0 + NRB (lane: row 16 rb + l % 16,
 // columns 32 (6 v + i) + 8 (l / 16) .. + 8), normalised in place (bf16; every LayerNorm's affine is
-// folded into the GEMM that consumes it).
+// folded into the GEMM that consumes it).  One pass over the bf16 pairs gives sum x and sum x^2
+// (v_dot2: no unpacking), summed over the row's 4 lanes and then the 4 waves (one LDS exchange);
+// var = E[x^2] - mean^2 (the residual stream's mean is small against its spread, so the one-pass
+// form loses nothing at bf16 output precision); y = x rstd - mean rstd (packed FMA).
 template <int NRB>
 __device__ __forceinline__ void ln_frags(u32x4_t* xf, const Sm& sm, int rb0) {
   const int tid = otid(), v = tid >> 6, lane = tid & 63, fr = lane & 15;
-  float mean[NRB], rstd[NRB];
+  constexpr unsigned ONE2 = 0x3f803f80u;   // bf16 (1, 1)
 #pragma unroll
   for (int rb = 0; rb < NRB; ++rb) {
-    float s = 0.f;
+    float s = 0.f, q = 0.f;
 #pragma unroll
     for (int i = 0; i < QS; ++i) {
-      float f[8];
-      unpack8(xf[rb * QS + i], f);
-      s += ((f[0] + f[1]) + (f[2] + f[3])) + ((f[4] + f[5]) + (f[6] + f[7]));
+      const u32x4_t u = xf[rb * QS + i];
+      s = dot2bf(u.x, ONE2, s); q = dot2bf(u.x, u.x, q);
+      s = dot2bf(u.y, ONE2, s); q = dot2bf(u.y, u.y, q);
+      s = dot2bf(u.z, ONE2, s); q = dot2bf(u.z, u.z, q);
+      s = dot2bf(u.w, ONE2, s); q = dot2bf(u.w, u.w, q);
     }
     s = add32(add16(s));
-    if (lane < 16) sm.ln[v * RM + 16 * (rb0 + rb) + fr] = s;
-  }
-  opaque<NRB * QS>(xf);
-  lds_sync();
-#pragma unroll
-  for (int rb = 0; rb < NRB; ++rb) {
-    const int r = 16 * (rb0 + rb) + fr;
-    mean[rb] = ((sm.ln[r] + sm.ln[RM + r]) + (sm.ln[2 * RM + r] + sm.ln[3 * RM + r])) * (1.0f / D);
-    float q = 0.f;
-#pragma unroll
-    for (int i = 0; i < QS; ++i) {
-      float f[8];
-      unpack8(xf[rb * QS + i], f);
-#pragma unroll
-      for (int t = 0; t < 8; ++t) f[t] -= mean[rb];
-      q += (fmaf(f[1], f[1], f[0] * f[0]) + fmaf(f[3], f[3], f[2] * f[2])) +
-           (fmaf(f[5], f[5], f[4] * f[4]) + fmaf(f[7], f[7], f[6] * f[6]));
-    }
     q = add32(add16(q));
-    if (lane < 16) sm.ln[NW * RM + v * RM + r] = q;
+    if (lane < 16) {
+      sm.ln[v * RM + 16 * (rb0 + rb) + fr] = s;
+      sm.ln[(NW + v) * RM + 16 * (rb0 + rb) + fr] = q;
+    }
   }
-  opaque<NRB * QS>(xf);
   lds_sync();
 #pragma unroll
   for (int rb = 0; rb < NRB; ++rb) {
     const int r = 16 * (rb0 + rb) + fr;
     const float* l2 = sm.ln + NW * RM;
-    rstd[rb] = rsqrtf(((l2[r] + l2[RM + r]) + (l2[2 * RM + r] + l2[3 * RM + r])) * (1.0f / D) + 1e-5f);
+    const float mean = ((sm.ln[r] + sm.ln[RM + r]) + (sm.ln[2 * RM + r] + sm.ln[3 * RM + r])) * (1.0f / D);
+    const float ex2 = ((l2[r] + l2[RM + r]) + (l2[2 * RM + r] + l2[3 * RM + r])) * (1.0f / D);
+    const float rstd = rsqrtf(fmaxf(fmaf(-mean, mean, ex2), 0.f) + 1e-5f);
+    const f32x2_t rs2 = {rstd, rstd}, nb2 = {-mean * rstd, -mean * rstd};
 #pragma unroll
     for (int i = 0; i < QS; ++i) {
-      float f[8];
-      unpack8(xf[rb * QS + i], f);
+      const u32x4_t u = xf[rb * QS + i];
+      const unsigned w[4] = {u.x, u.y, u.z, u.w};
+      unsigned o[4];
 #pragma unroll
-      for (int t = 0; t < 8; ++t) f[t] = (f[t] - mean[rb]) * rstd[rb];
-      xf[rb * QS + i] = pack8(f);
+      for (int e = 0; e < 4; ++e) {
+        const f32x2_t f = {__uint_as_float(w[e] << 16), __uint_as_float(w[e] & 0xffff0000u)};
+        const f32x2_t y = __builtin_elementwise_fma(f, rs2, nb2);
+        o[e] = pk2bf(y.x, y.y);
+      }
+      xf[rb * QS + i] = u32x4_t{o[0], o[1], o[2], o[3]};
     }
   }
 }
@@ -746,24 +743,44 @@ __device__ __forceinline__ void phase_b(const Args& a, const Rs& rs, int l, cons
                                         u32x4_t (&kr)[KU][KC], u32x4_t (&vr)[KU][KC]) {
   const int tid = otid(), lane = tid & 63, v = tid >> 6, grp = lane >> 3, sub = lane & 7;
   const __amdgpu_buffer_rsrc_t rk = mk(a.kc[l], a.kv_bytes), rv = mk(a.vc[l], a.kv_bytes);
-  float q[KU][8], o[KU][8], m[KU], sum[KU];
+  float m[KU], sum[KU];
+  f32x2_t o[KU][4];
   int p[KU], row[KU], hh[KU];
   long base[KU];
-  u32x4_t qu[KU];
+  u32x4_t qu[KU], knu[KU], vnu[KU];
+  // q and the new key / value (position pos, written by phase A this step) in one round trip
 #pragma unroll
   for (int k = 0; k < KU; ++k) {
     attn_unit(a, sm, ub + KU * v + k, row[k], hh[k], p[k], base[k]);
     qu[k] = ld16(rs.q, (min(row[k], a.R - 1) * D + hh[k] * HD + 8 * sub) * 2);
+    const int off = (int)((base[k] + (long)p[k] * HD) * 2);
+    knu[k] = ld16(rk, off);
+    vnu[k] = ld16(rv, off);
   }
   __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
   for (int k = 0; k < KU; ++k) {
-    unpack8(qu[k], q[k]);
 #pragma unroll
-    for (int t = 0; t < 8; ++t) { q[k][t] *= 0.125f; o[k][t] = 0.f; }
+    for (int t = 0; t < 4; ++t) o[k][t] = f32x2_t{0.f, 0.f};
     m[k] = -INFINITY;
     sum[k] = 0.f;
   }
+  // q . k over the lane's 8 dims: four bf16-pair dots, then the 8 lanes of the key, / sqrt(64)
+  auto qk = [&](const u32x4_t& qv, const u32x4_t& kv) {
+    float sv = dot2bf(qv.x, kv.x, 0.f);
+    sv = dot2bf(qv.y, kv.y, sv);
+    sv = dot2bf(qv.z, kv.z, sv);
+    sv = dot2bf(qv.w, kv.w, sv);
+    return sum8(sv) * 0.125f;
+  };
+  auto vacc = [&](f32x2_t (&acc)[4], float e, const u32x4_t& vv) {
+    const unsigned w[4] = {vv.x, vv.y, vv.z, vv.w};
+    const f32x2_t e2 = {e, e};
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+      acc[t] = __builtin_elementwise_fma(e2, f32x2_t{__uint_as_float(w[t] << 16),
+                                                     __uint_as_float(w[t] & 0xffff0000u)}, acc[t]);
+  };
   int pmax = p[0];
 #pragma unroll
   for (int k = 1; k < KU; ++k) pmax = max(pmax, p[k]);
@@ -776,12 +793,7 @@ __device__ __forceinline__ void phase_b(const Args& a, const Rs& rs, int l, cons
       float pm = -INFINITY;
 #pragma unroll
       for (int i = 0; i < KC; ++i) {
-        float kf[8];
-        unpack8(kr[k][i], kf);
-        float sv = 0.f;
-#pragma unroll
-        for (int t = 0; t < 8; ++t) sv = fmaf(q[k][t], kf[t], sv);
-        sv = sum8(sv);
+        const float sv = qk(qu[k], kr[k][i]);
         sc[i] = cb + 8 * i + grp < p[k] ? sv : -INFINITY;
         pm = fmaxf(pm, sc[i]);
       }
@@ -791,47 +803,37 @@ __device__ __forceinline__ void phase_b(const Args& a, const Rs& rs, int l, cons
       const float mn = fmaxf(m[k], pm);
       const float scale = __expf(m[k] - mn);
       sum[k] *= scale;
+      const f32x2_t sc2 = {scale, scale};
 #pragma unroll
-      for (int t = 0; t < 8; ++t) o[k][t] *= scale;
+      for (int t = 0; t < 4; ++t) o[k][t] *= sc2;
       m[k] = mn;
 #pragma unroll
       for (int i = 0; i < KC; ++i) {
         const float e = __expf(sc[i] - mn);
         sum[k] += e;
-        float vf[8];
-        unpack8(vr[k][i], vf);
-#pragma unroll
-        for (int t = 0; t < 8; ++t) o[k][t] = fmaf(e, vf[t], o[k][t]);
+        vacc(o[k], e, vr[k][i]);
       }
     }
   }
-  // the new key / value (position pos, written by phase A this step)
-  u32x4_t knu[KU], vnu[KU];
-#pragma unroll
-  for (int k = 0; k < KU; ++k) {
-    const int off = (int)((base[k] + (long)p[k] * HD) * 2);
-    knu[k] = ld16(rk, off);
-    vnu[k] = ld16(rv, off);
-  }
-  __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
   for (int k = 0; k < KU; ++k) {
     sum[k] = add32(add16(sum[k] + xor8(sum[k])));
+    float of[8];
 #pragma unroll
-    for (int t = 0; t < 8; ++t) o[k][t] = add32(add16(o[k][t] + xor8(o[k][t])));
-    float kf[8], vf[8];
-    unpack8(knu[k], kf);
-    unpack8(vnu[k], vf);
-    float sn = 0.f;
-#pragma unroll
-    for (int t = 0; t < 8; ++t) sn = fmaf(q[k][t], kf[t], sn);
-    sn = sum8(sn);
+    for (int t = 0; t < 4; ++t) {
+      of[2 * t] = add32(add16(o[k][t].x + xor8(o[k][t].x)));
+      of[2 * t + 1] = add32(add16(o[k][t].y + xor8(o[k][t].y)));
+    }
+    const float sn = qk(qu[k], knu[k]);
     const float mn = fmaxf(m[k], sn);
     const float sc = __expf(m[k] - mn), en = __expf(sn - mn);
     const float inv = 1.0f / fmaf(sum[k], sc, en);
-    float of[8];
+    const unsigned w[4] = {vnu[k].x, vnu[k].y, vnu[k].z, vnu[k].w};
 #pragma unroll
-    for (int t = 0; t < 8; ++t) of[t] = fmaf(en, vf[t], o[k][t] * sc) * inv;
+    for (int t = 0; t < 4; ++t) {
+      of[2 * t] = fmaf(en, __uint_as_float(w[t] << 16), of[2 * t] * sc) * inv;
+      of[2 * t + 1] = fmaf(en, __uint_as_float(w[t] & 0xffff0000u), of[2 * t + 1] * sc) * inv;
+    }
     if (grp == 0 && row[k] < a.R) {
       // att in fragment order: row r, dims 64 h + 8 sub .. + 8 = k-step 2 h + sub / 4,
       // lane (r & 15) + 16 (sub & 3)

@@ -354,6 +354,8 @@ class Gpt2Decoder:
         self.gave_up = 0            # persistent launches that gave up and resumed stepwise
         self._eager = False         # step_chunk without graphs (the give-up fallback)
         self._persist_R = 0         # rows of the persistent launch in flight (0: none)
+        self._persist_pending = 0   # rows of a greedy begin whose launch is deferred
+        self.defer_launch = False   # greedy_begin leaves the persistent launch to launch_pending
         self.ws = ops.skinny_workspace(dev, [(M, N, K) for M in {self.R, self.Rp}
                                              for N, K in ((3 * D, D), (D, D), (4 * D, D), (D, 4 * D))])
 
@@ -619,15 +621,25 @@ class Gpt2Decoder:
         self._eager = False
         self._persist_R = 0
         if self.persist and R <= 64:
-            ev = PERSIST_LOG
-            if ev is not None:          # bench.py's roofline: HIP events around each launch
-                ev.append((torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True),
-                           id(self)))
-                ev[-1][0].record()
-            ops.gpt2_decode_persist(*self._grid_args(R), grid=self.persist_grid)
-            if ev is not None:
-                ev[-1][1].record()
-            self._persist_R = R
+            self._persist_pending = R
+            if not self.defer_launch:
+                self.launch_pending()
+
+    def launch_pending(self):
+        """Enqueues the persistent decode launch greedy_begin set up (at once, or -- with
+        ``defer_launch`` set during the begin -- when the runner has room for its grid)."""
+        R = self._persist_pending
+        assert R, "launch_pending: no greedy begin waiting for its persistent launch"
+        ev = PERSIST_LOG
+        if ev is not None:          # bench.py's roofline: HIP events around each launch
+            ev.append((torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True),
+                       id(self)))
+            ev[-1][0].record()
+        ops.gpt2_decode_persist(*self._grid_args(R), grid=self.persist_grid)
+        if ev is not None:
+            ev[-1][1].record()
+        self._persist_R = R
+        self._persist_pending = 0
 
     def greedy(self, B: int, Pmax: int):
         """After :meth:`prefill` (row_stride 1): generate2 for all B rows.

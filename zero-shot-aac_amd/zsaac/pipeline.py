@@ -279,14 +279,18 @@ class ConcurrentRunner:
 
     def __init__(self, pipe: CaptionPipeline, n_inflight: int = 2, streams: Optional[list] = None,
                  grids: Optional[List[int]] = None, budget: Optional[int] = None,
-                 encode_ahead: int = 0, encode_first: bool = False):
+                 encode_ahead: int = 0, encode_first: bool = False, begin_first: bool = False):
         self.cus = torch.cuda.get_device_properties(pipe.dev).multi_processor_count
         # persistent grids (greedy bf16 at <= 64 rows; beam search never launches one), one size
         # per batch from `grids` (largest first, see choose_persist_grid)
         self.persist = pipe.decoder.persist and not pipe.cfg.beam
         self.grids = grids or persist_grids()
         self.budget = budget or persist_budget(self.cus)
-        if self.persist:
+        # begin_first (persistent decode only): every pipeline begins its batch (prompt .. step 0)
+        # at once, and the persistent launches follow as the budget frees, the first ones after
+        # every first-round begin -- the begins run on the whole chip instead of beside the grids
+        self.begin_first = bool(begin_first) and self.persist
+        if self.persist and not self.begin_first:
             # persistent decode grids must be co-resident: at most budget // (smallest grid)
             n_inflight = max(1, min(n_inflight, self.budget // self.grids[-1]))
         self.n_inflight = n_inflight
@@ -342,6 +346,8 @@ class ConcurrentRunner:
         ahead = None
         if inputs == "wav" and self.enc is not None:
             ahead = self._encode_ahead(batches, caller)
+        if self.begin_first:
+            return self._run_staged(batches, keep, inputs, caller, ahead)
         active = {}
         nxt = 0
         self.decode_steps = [0] * len(batches)     # per batch: decode steps actually enqueued
@@ -407,6 +413,102 @@ class ConcurrentRunner:
             if not progressed:
                 time.sleep(20e-6)
         for s in self.streams:           # results are consumed on the caller's stream
+            caller.wait_stream(s)
+        if ahead is not None:
+            caller.wait_stream(self.enc_stream)
+        return results
+
+    def _begin(self, i, bi, batches, inputs, ahead):
+        p, s = self.pipes[i], self.streams[i]
+        with torch.cuda.stream(s):
+            if ahead is not None:
+                embs, evs = ahead
+                s.wait_event(evs[bi])
+                p.begin_emb(embs[bi])
+            else:
+                (p.begin_wav if inputs == "wav" else p.begin_emb)(batches[bi])
+
+    def _run_staged(self, batches, keep, inputs, caller, ahead):
+        """run() with begin_first: begins on every free pipeline first (persistent launches
+        deferred), launches in batch order while the grids in flight fit the budget."""
+        n = len(batches)
+        results: List[Optional[CaptionBatch]] = [None] * n
+        self.decode_steps = [0] * n
+        self.assign, self.grid, self.gave_up = [], [0] * n, 0
+        free = list(range(len(self.pipes)))
+        begun, active, slots = [], {}, {}
+        first_round, gate = True, []
+        nxt = 0
+        while nxt < n or begun or active:
+            progressed = False
+            while nxt < n and free:
+                i = free.pop(0)
+                self.pipes[i].decoder.defer_launch = True
+                try:
+                    self._begin(i, nxt, batches, inputs, ahead)
+                finally:
+                    self.pipes[i].decoder.defer_launch = False
+                if first_round:
+                    ev = torch.cuda.Event()
+                    ev.record(self.streams[i])
+                    gate.append(ev)
+                begun.append((nxt, i))
+                self.assign.append((i, nxt))
+                nxt += 1
+                progressed = True
+            first_round = False
+            while begun:
+                bi, i = begun[0]
+                used = sum(slots.values())
+                g = choose_persist_grid(used, len(begun) + n - nxt, self.grids, self.budget)
+                if used + g > self.budget:
+                    break
+                p, s = self.pipes[i], self.streams[i]
+                p.decoder.persist_grid = g
+                with torch.cuda.stream(s):
+                    for ev in gate:          # the first round's launches: after every begin
+                        s.wait_event(ev)
+                    p.decoder.launch_pending()
+                    ev, flag = p.decoder.finished_async()
+                slots[i] = g
+                self.grid[bi] = g
+                active[i] = (bi, 0, ev, flag)
+                begun.pop(0)
+                progressed = True
+            gate = []
+            for i in list(active):
+                bi, k, ev, flag = active[i]
+                if not ev.query():
+                    continue
+                progressed = True
+                p, s = self.pipes[i], self.streams[i]
+                if int(flag[1]) < 0:          # gave up (not co-resident): finish stepwise
+                    self.gave_up += 1
+                    with torch.cuda.stream(s):
+                        p.decoder.resume_stepwise()
+                        p.decoder.step_chunk(None)
+                        ev, flag = p.decoder.finished_async()
+                    slots.pop(i, None)
+                    active[i] = (bi, 1, ev, flag)
+                    continue
+                if int(flag[0]) or k >= p.decoder.n_chunks:
+                    p.decoder.note_persist_steps(int(flag[3]))
+                    self.decode_steps[bi] = int(flag[3])
+                    with torch.cuda.stream(s):
+                        results[bi] = _copy_batch(p.result(), caller)
+                        if keep is not None:
+                            keep(results[bi])
+                    del active[i]
+                    slots.pop(i, None)
+                    free.append(i)
+                else:
+                    with torch.cuda.stream(s):
+                        p.decoder.step_chunk(int(flag[2]))
+                        ev, flag = p.decoder.finished_async()
+                    active[i] = (bi, k + 1, ev, flag)
+            if not progressed:
+                time.sleep(20e-6)
+        for s in self.streams:
             caller.wait_stream(s)
         if ahead is not None:
             caller.wait_stream(self.enc_stream)
