@@ -474,17 +474,22 @@ int zs_greedy_step_map(const float* part_val, const int* part_idx, int R, const 
  * ln_f, the tied LM head with its argmax (ties -> lower id) and zs_greedy_step's bookkeeping,
  * until every row stopped or max_steps.  Starts from the state zs_greedy_step left after step 0
  * (next_tok, pos, done, out_ids, out_len, *step_ctr, all_done[0]) and commits that state after
- * every step.  layer_w: 12 x 8 device pointers {c_attn W, its bias f32, attn.c_proj W, bias,
- * c_fc W, bias, mlp.c_proj W, bias}, each W (= Conv1D weight transposed, [N][K] bf16) in MFMA
- * fragment order [N/16][K/32][64][8] (block j, k-step s, lane l = W[16 j + l % 16][32 s + 8 (l /
- * 16) .. + 8]); wte_packed: the tied LM head with ln_f's weight folded in, bf16(g o wte[v]), in the
- * same order, [ceil(V/16)][24][64][8] (rows past V zero), and lm_bias [ceil(V/16) 16] f32 = ln_f's
- * bias through the head (beta . wte[v]): logit[v] = LN(x) . (g o wte[v]) + lm_bias[v]; temperature > 0 divides the logits before the argmax (gpt2_prefix_eval.py:196);
+ * every step.  layer_w: 12 x 8 device pointers {c_attn W, its bias, attn.c_proj W, bias, c_fc W,
+ * its bias, mlp.c_proj W, bias}, each W (= Conv1D weight transposed, [N][K] bf16; c_attn's with
+ * ln_1's weight folded in, c_fc's with ln_2's) in MFMA fragment order [N/16][K/32][64][8] (block j,
+ * k-step s, lane l = W[16 j + l % 16][32 s + 8 (l / 16) .. + 8]); the c_attn and c_fc biases are f32
+ * [2][N]: row 0 the bias with the LayerNorm's beta folded in (b + beta W), row 1 the folded
+ * weight's column sums cs[n] = sum_k W'[n][k] -- the LayerNorm runs in the GEMM epilogue as
+ * rstd (x W' - mean cs) + b'; the projections' biases are f32 [N].  wte_packed: the tied LM head
+ * with ln_f's weight folded in, bf16(g o wte[v]), in the same order, [ceil(V/16)][24][64][8] (rows
+ * past V zero); lm_bias f32 [2][ceil(V/16) 16]: beta . wte[v] (ln_f's bias through the head), then
+ * the column sums of the folded head; logit[v] = LN(x) . (g o wte[v]) + lm_bias[0][v];
+ * temperature > 0 divides the logits before the argmax (gpt2_prefix_eval.py:196);
  * kv: 24 pointers {kc[0..11], vc[0..11]}, each [R][12][Lmax][64] bf16 (zs_kv_write layout),
  * 128-byte aligned.  ws: scratch of zs_decode_persist_workspace_bytes() bytes, 256-byte aligned,
  * private to one launch in flight.  Every output element is computed by the same operations
  * whatever `grid` (each GEMM element: four K-quarter MFMA chains summed (p0 + p1) + (p2 + p3);
- * LayerNorm, attention and argmax in fixed orders), so ids and state do not depend on the grid
+ * LayerNorm statistics (one pass, sum x and sum x^2), attention and argmax in fixed orders), so ids and state do not depend on the grid
  * and equal zs_gpt2_decode_phases'.  A grid that cannot become co-resident gives up after a
  * bounded wait: all_done[1] = -1, zs_decode_persist_status reports timed_out != 0, and the state
  * in memory is the last committed step's (resume with zs_gpt2_decode_phases). */

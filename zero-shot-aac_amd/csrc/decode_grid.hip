@@ -117,10 +117,11 @@ constexpr int WS_HID = WS_XB + RM * D * 2;        // bf16 [4][96][64][8]
 constexpr int WS_X = WS_HID + RM * DFF * 2;       // f32  [64][768] (phase launches only)
 constexpr int WS_BYTES = WS_X + RM * D * 4;
 
-// ------------------------------------------------------------------ LDS (35,648 B)
+// ------------------------------------------------------------------ LDS (36,160 B)
 constexpr int SM_RED = 0;                         // f32x4 [2048]: partial slabs (32 KiB)
 constexpr int SM_LN = SM_RED + 32768;             // f32 [2][4][64]: LayerNorm partials
-constexpr int SM_ST = SM_LN + 2048;               // int tok[64], pos[64], done[64], misc[16]
+constexpr int SM_CB = SM_LN + 2048;               // f32 [2][64]: the tile's bias / column sums
+constexpr int SM_ST = SM_CB + 512;                // int tok[64], pos[64], done[64], misc[16]
 constexpr int SM_TOTAL = SM_ST + (3 * RM + 16) * 4;
 
 struct Args {
@@ -330,12 +331,14 @@ __device__ __forceinline__ bool bar_wait(Bar& b, volatile lds_int_t* s_ok) {
 struct Sm {
   f32x4_t* red;
   float* ln;
+  float* cb;     // [2][64]: bias, then column sums, of the A / D tile's columns
   int* tok;
   int* pos;
   int* done;
   int* misc;     // [0] rows still decoding, [8] barrier ok flag
   __device__ __forceinline__ explicit Sm(char* s)
       : red(reinterpret_cast<f32x4_t*>(s + SM_RED)), ln(reinterpret_cast<float*>(s + SM_LN)),
+        cb(reinterpret_cast<float*>(s + SM_CB)),
         tok(reinterpret_cast<int*>(s + SM_ST)),
         pos(reinterpret_cast<int*>(s + SM_ST) + RM), done(reinterpret_cast<int*>(s + SM_ST) + 2 * RM),
         misc(reinterpret_cast<int*>(s + SM_ST) + 3 * RM) {}
@@ -372,14 +375,15 @@ __device__ __forceinline__ float dot2bf(unsigned x, unsigned y, float c) {
   return __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2_t, x), __builtin_bit_cast(bf16x2_t, y),
                                          c, false);
 }
-// xf: this wave's K-quarter fragments of row blocks rb0 .. rb0 + NRB (lane: row 16 rb + l % 16,
-// columns 32 (6 v + i) + 8 (l / 16) .. + 8), normalised in place (bf16; every LayerNorm's affine is
-// folded into the GEMM that consumes it).  One pass over the bf16 pairs gives sum x and sum x^2
-// (v_dot2: no unpacking), summed over the row's 4 lanes and then the 4 waves (one LDS exchange);
-// var = E[x^2] - mean^2 (the residual stream's mean is small against its spread, so the one-pass
-// form loses nothing at bf16 output precision); y = x rstd - mean rstd (packed FMA).
+// LayerNorm folded into the GEMM that consumes it: with W' = diag(g) W (packed) and
+// b' = b + beta W, LN(x) W + b = rstd (x W' - mean cs) + b' where cs[n] = sum_k W'[k][n] -- so the
+// MFMAs run on the raw bf16 rows as soon as they land, and only the epilogue needs the row's
+// statistics.  ln_stats: this wave's K-quarter fragments of row blocks rb0 .. rb0 + NRB (lane: row
+// 16 rb + l % 16, columns 32 (6 v + i) + 8 (l / 16) .. + 8): sum x and sum x^2 over the bf16 pairs
+// (v_dot2), then over the row's 4 lanes, into the LDS partials of wave v -- read after the next
+// workgroup barrier (every caller has one before its epilogue) by ln_row.
 template <int NRB>
-__device__ __forceinline__ void ln_frags(u32x4_t* xf, const Sm& sm, int rb0) {
+__device__ __forceinline__ void ln_stats(const u32x4_t* xf, const Sm& sm, int rb0) {
   const int tid = otid(), v = tid >> 6, lane = tid & 63, fr = lane & 15;
   constexpr unsigned ONE2 = 0x3f803f80u;   // bf16 (1, 1)
 #pragma unroll
@@ -400,29 +404,32 @@ __device__ __forceinline__ void ln_frags(u32x4_t* xf, const Sm& sm, int rb0) {
       sm.ln[(NW + v) * RM + 16 * (rb0 + rb) + fr] = q;
     }
   }
-  lds_sync();
-#pragma unroll
-  for (int rb = 0; rb < NRB; ++rb) {
-    const int r = 16 * (rb0 + rb) + fr;
-    const float* l2 = sm.ln + NW * RM;
-    const float mean = ((sm.ln[r] + sm.ln[RM + r]) + (sm.ln[2 * RM + r] + sm.ln[3 * RM + r])) * (1.0f / D);
-    const float ex2 = ((l2[r] + l2[RM + r]) + (l2[2 * RM + r] + l2[3 * RM + r])) * (1.0f / D);
-    const float rstd = rsqrtf(fmaxf(fmaf(-mean, mean, ex2), 0.f) + 1e-5f);
-    const f32x2_t rs2 = {rstd, rstd}, nb2 = {-mean * rstd, -mean * rstd};
-#pragma unroll
-    for (int i = 0; i < QS; ++i) {
-      const u32x4_t u = xf[rb * QS + i];
-      const unsigned w[4] = {u.x, u.y, u.z, u.w};
-      unsigned o[4];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const f32x2_t f = {__uint_as_float(w[e] << 16), __uint_as_float(w[e] & 0xffff0000u)};
-        const f32x2_t y = __builtin_elementwise_fma(f, rs2, nb2);
-        o[e] = pk2bf(y.x, y.y);
-      }
-      xf[rb * QS + i] = u32x4_t{o[0], o[1], o[2], o[3]};
-    }
-  }
+}
+// the row's mean and 1 / sqrt(var + eps) from the 4 waves' partials; var = E[x^2] - mean^2 (the
+// residual stream's mean is small against its spread: the one-pass form loses nothing at bf16
+// output precision)
+__device__ __forceinline__ void ln_row(const Sm& sm, int r, float& mean, float& rstd) {
+  const float* l2 = sm.ln + NW * RM;
+  mean = ((sm.ln[r] + sm.ln[RM + r]) + (sm.ln[2 * RM + r] + sm.ln[3 * RM + r])) * (1.0f / D);
+  const float ex2 = ((l2[r] + l2[RM + r]) + (l2[2 * RM + r] + l2[3 * RM + r])) * (1.0f / D);
+  rstd = rsqrtf(fmaxf(fmaf(-mean, mean, ex2), 0.f) + 1e-5f);
+}
+// the tile's NC columns from n0 of a [2][N] bias (row 0 bias, row 1 column sums) into LDS (read
+// after the next workgroup barrier)
+template <int NC>
+__device__ __forceinline__ void stage_cb(const Sm& sm, const float* b2, int N, int n0) {
+  static_assert(NC <= 64, "SM_CB holds 64 columns");
+  const int t = otid();
+  if (t < NC) sm.cb[t] = b2[n0 + t];
+  else if (t >= 64 && t < 64 + NC) sm.cb[t] = b2[N + n0 + t - 64];
+}
+__device__ __forceinline__ float4 cb_quad(const Sm& sm, int lc, int row1) {
+  return *reinterpret_cast<const float4*>(sm.cb + 64 * row1 + lc);
+}
+// rstd (sum - mean cs) + b for a lane's 4 columns
+__device__ __forceinline__ float4 ln_fold(f32x4_t s, float mean, float rstd, float4 cs, float4 b) {
+  return make_float4(fmaf(rstd, fmaf(-mean, cs.x, s[0]), b.x), fmaf(rstd, fmaf(-mean, cs.y, s[1]), b.y),
+                     fmaf(rstd, fmaf(-mean, cs.z, s[2]), b.z), fmaf(rstd, fmaf(-mean, cs.w, s[3]), b.w));
 }
 
 // layer 0's LayerNorm input: bf16(wte[tok] + wpe[pos]) (the f32 sum rounded once)
@@ -476,20 +483,6 @@ struct Rounds {
   static constexpr int NR = (CB + CPR - 1) / CPR;             // rounds
   static constexpr int NJ = (CPR * RB + NW - 1) / NW;         // finalised tiles per wave per round
 };
-// per-(round, j) operand quads of the tiles this wave finalises: f(c) for col block c of the tile
-template <int CB, int RB, int NR, int NJ, typename F>
-__device__ __forceinline__ void round_quads(float4 (&q)[NR][NJ], F&& f) {
-  using Rn = Rounds<CB, RB>;
-  static_assert(NR == Rn::NR && NJ == Rn::NJ, "round_quads shape");
-  const int v = otid() >> 6;
-#pragma unroll
-  for (int r = 0; r < NR; ++r)
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) {
-      const int t = NW * j + v, c = r * Rn::CPR + t / RB;
-      q[r][j] = (t < Rn::CPR * RB && c < CB) ? f(c) : make_float4(0.f, 0.f, 0.f, 0.f);
-    }
-}
 template <int CB, int RB, int PF, typename LoadW, typename Epi>
 __device__ __forceinline__ void gemm_rounds(const u32x4_t* xf, u32x4_t* wpf, f32x4_t* red,
                                             LoadW&& loadw, Epi&& epi) {
@@ -529,21 +522,20 @@ __device__ __forceinline__ void phase_a(const Args& a, const Rs& rs, int l, int 
   if (l == 0) embed_frags<RB>(a, sm, rb0, xf);
   else lda<RB, QS>(rs.xb, KSD, rb0, QS * v, xf);
   if constexpr (PM) ldw<Gm::APF, QS>(a.wq[l], KSD, cb0, QS * v, wq);
-  using Rn = Rounds<CB, RB>;
-  float4 bq[Rn::NR][Rn::NJ];
-  round_quads<CB, RB>(bq, [&](int c) {
-    return *reinterpret_cast<const float4*>(a.bq[l] + 16 * (cb0 + c) + 4 * (lane >> 4));
-  });
+  stage_cb<16 * CB>(sm, a.bq[l], QKVN, 16 * cb0);
   __builtin_amdgcn_sched_barrier(0);
-  ln_frags<RB>(xf, sm, rb0);
+  ln_stats<RB>(xf, sm, rb0);
   const __amdgpu_buffer_rsrc_t rk = mk(a.kc[l], a.kv_bytes), rv = mk(a.vc[l], a.kv_bytes);
   gemm_rounds<CB, RB, Gm::APF>(xf, wq, sm.red,
       [&](int c, auto n, u32x4_t* wr) { ldw<decltype(n)::value, QS>(a.wq[l], KSD, cb0 + c, QS * (otid() >> 6), wr); },
       [&](int r, int j, int c, int rb, f32x4_t s) {
         const int row = 16 * (rb0 + rb) + (lane & 15), col = 16 * (cb0 + c) + 4 * (lane >> 4);
         if (row >= a.R) return;
-        const float4 b = bq[r][j];
-        const u32x2_t o{pk2bf(s[0] + b.x, s[1] + b.y), pk2bf(s[2] + b.z, s[3] + b.w)};
+        float mean, rstd;
+        ln_row(sm, row, mean, rstd);
+        const int lc = 16 * c + 4 * (lane >> 4);
+        const float4 o4 = ln_fold(s, mean, rstd, cb_quad(sm, lc, 1), cb_quad(sm, lc, 0));
+        const u32x2_t o{pk2bf(o4.x, o4.y), pk2bf(o4.z, o4.w)};
         if (col < D) {
           st8(rs.q, (row * D + col) * 2, o);
         } else {
@@ -569,22 +561,21 @@ __device__ __forceinline__ void phase_d(const Args& a, const Rs& rs, int l, int 
   u32x4_t xf[RB * QS];
   lda<RB, QS>(rs.xb, KSD, rb0, QS * v, xf);
   if constexpr (PM) ldw<Gm::DPF, QS>(a.wf[l], KSD, cb0, QS * v, wf);
-  using Rn = Rounds<CB, RB>;
-  float4 bb[Rn::NR][Rn::NJ];
-  round_quads<CB, RB>(bb, [&](int c) {
-    return *reinterpret_cast<const float4*>(a.bfc[l] + 16 * (cb0 + c) + 4 * (lane >> 4));
-  });
+  stage_cb<16 * CB>(sm, a.bfc[l], DFF, 16 * cb0);
   __builtin_amdgcn_sched_barrier(0);
-  ln_frags<RB>(xf, sm, rb0);
+  ln_stats<RB>(xf, sm, rb0);
   gemm_rounds<CB, RB, Gm::DPF>(xf, wf, sm.red,
       [&](int c, auto n, u32x4_t* wr) { ldw<decltype(n)::value, QS>(a.wf[l], KSD, cb0 + c, QS * (otid() >> 6), wr); },
       [&](int r, int j, int c, int rb, f32x4_t s) {
         const int row = 16 * (rb0 + rb) + (lane & 15), col = 16 * (cb0 + c) + 4 * (lane >> 4);
         if (row >= a.R) return;
-        const float4 b = bb[r][j];
+        float mean, rstd;
+        ln_row(sm, row, mean, rstd);
+        const int lc = 16 * c + 4 * (lane >> 4);
+        const float4 h = ln_fold(s, mean, rstd, cb_quad(sm, lc, 1), cb_quad(sm, lc, 0));
         st8(rs.hid, frag_off(row, col, KSF),
-            u32x2_t{pk2bf(gelu_new_fast(s[0] + b.x), gelu_new_fast(s[1] + b.y)),
-                    pk2bf(gelu_new_fast(s[2] + b.z), gelu_new_fast(s[3] + b.w))});
+            u32x2_t{pk2bf(gelu_new_fast(h.x), gelu_new_fast(h.y)),
+                    pk2bf(gelu_new_fast(h.z), gelu_new_fast(h.w))});
       });
 }
 
@@ -854,7 +845,7 @@ __device__ __forceinline__ void phase_f(const Args& a, const Rs& rs, int w, cons
   const int tid = otid(), v = tid >> 6, lane = tid & 63;
   u32x4_t xf[4 * QS];
   lda<4, QS>(rs.xb, KSD, 0, QS * v, xf);
-  const int nvb = (a.V + 15) >> 4;
+  const int nvb = (a.V + 15) >> 4, lmv = 16 * nvb;    // lmb: [2][16 nvb] bias, then cs
   const int nb = (nvb - w + G - 1) / G;
   // ring of 3 block slots, each this wave's 6 weight fragments of the block plus the lane's 4
   // per-token biases; every refill is unconditional (block index clamped to the workgroup's last
@@ -862,26 +853,29 @@ __device__ __forceinline__ void phase_f(const Args& a, const Rs& rs, int w, cons
   // block, one round trip per block)
   struct Slot {
     u32x4_t w[QS];
-    float4 b;
+    float4 b, cs;
   };
   Slot R0, R1, R2;
   auto fill = [&](int i, Slot& r) {
     const int blk = w + G * min(i, nb - 1);
     ldw<1, QS>(a.wtep, KSD, blk, QS * v, r.w);
     r.b = *reinterpret_cast<const float4*>(a.lmb + 16 * blk + 4 * (lane >> 4));
+    r.cs = *reinterpret_cast<const float4*>(a.lmb + lmv + 16 * blk + 4 * (lane >> 4));
   };
   // the first block streams during the LayerNorm; the other two slots are issued after it (all
   // three in flight across it left too few registers for the normalisation)
   fill(0, R0);
-  __builtin_amdgcn_sched_barrier(0);
-  ln_frags<4>(xf, sm, 0);
   fill(1, R1);
   fill(2, R2);
+  __builtin_amdgcn_sched_barrier(0);
+  ln_stats<4>(xf, sm, 0);
   float bv = -INFINITY;
   int bi = 0x7fffffff;
   const bool tmp = a.temp != 1.0f;
   int buf = 0;
-  lds_sync();     // the previous phase's slab readers are done
+  lds_sync();     // the previous phase's slab readers are done; the row statistics are in
+  float mean, rstd;
+  ln_row(sm, 16 * v + (lane & 15), mean, rstd);   // wave v finalises row block v
   auto consume = [&](int i, const Slot& r) {
     f32x4_t acc[4];
 #pragma unroll
@@ -897,10 +891,11 @@ __device__ __forceinline__ void phase_f(const Args& a, const Rs& rs, int w, cons
     const f32x4_t sum = (red[v * 64 + lane] + red[(4 + v) * 64 + lane]) +
                         (red[(8 + v) * 64 + lane] + red[(12 + v) * 64 + lane]);
     const int col0 = 16 * (w + G * i) + 4 * (lane >> 4);
-    const float lbv[4] = {r.b.x, r.b.y, r.b.z, r.b.w};
+    const float4 lg4 = ln_fold(sum, mean, rstd, r.cs, r.b);
+    const float lgv[4] = {lg4.x, lg4.y, lg4.z, lg4.w};
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      const float lg = sum[e] + lbv[e];
+      const float lg = lgv[e];
       const float val = tmp ? lg / a.temp : lg;
       if (col0 + e < a.V && val > bv) { bv = val; bi = col0 + e; }
     }

@@ -159,6 +159,12 @@ def build_mapper(sd, mapping_type, device, dtype, max_batch, clip_length=10, num
 
 
 # ------------------------------------------------------------------------------- GPT-2
+def colsum(W: torch.Tensor) -> torch.Tensor:
+    """Per output column n of a [N][K] bf16 weight: sum_k W[n][k] of the bf16 values (f64, then
+    f32) -- the LayerNorm fold's mean correction in the grid decode's epilogues."""
+    return W.double().sum(dim=1).float().contiguous()
+
+
 class Gpt2Weights:
     """HF GPT-2 small (``gpt.`` keys under ClapCaption_prompt): Conv1D [in,out] -> [out,in]."""
 
@@ -208,14 +214,18 @@ class Gpt2Weights:
             # the bs <= 64 greedy decode (zs_gpt2_decode_persist / _phases) folds ln_f's affine into
             # the tied LM head as ln_1 / ln_2 into c_attn / c_fc: logit[v] = y . (g o wte[v]) +
             # beta . wte[v] with y the normalised row (g o wte rounded to bf16 once, from f32)
+            # lm_bias [2][16 nvb]: beta . wte[v], then the column sums of the folded head (the
+            # grid decode runs the LayerNorm in the GEMM epilogue: rstd (x W' - mean cs) + b')
             wte32 = sd[p + "wte.weight"].to(device=device, dtype=torch.float32)
             g, beta = self.lnf
-            self._wte_packed = ops.pack_b_fragments((wte32 * g[None, :]).to(torch.bfloat16))
+            wg = (wte32 * g[None, :]).to(torch.bfloat16)
+            self._wte_packed = ops.pack_b_fragments(wg)
             nvb = -(-self.V // 16)
-            lmb = torch.zeros(nvb * 16, device=device)
-            lmb[:self.V] = (wte32.double() @ beta.double()).float()
+            lmb = torch.zeros(2, nvb * 16, device=device)
+            lmb[0, :self.V] = (wte32.double() @ beta.double()).float()
+            lmb[1, :self.V] = colsum(wg)
             self._lm_bias = lmb
-            del wte32
+            del wte32, wg
 
     def packed_layer_ptrs(self):
         """The 12 x 8 device pointers zs_gpt2_decode_persist / _phases take: per block c_attn W,
@@ -224,7 +234,11 @@ class Gpt2Weights:
         if self._layer_ptrs is None:
             import ctypes
             assert self.folded, "the grid decode runs the bf16 (LN-folded) weights"
-            self._packed = [{k: (ops.pack_b_fragments(ly[k]) if k.endswith("_w") else ly[k])
+            # the LayerNorm-fed GEMMs' biases as [2][N]: b' (beta folded), then the folded
+            # weight's column sums cs[n] = sum_k W'[n][k] (the epilogue's rstd (x W' - mean cs) + b')
+            self._packed = [{k: (ops.pack_b_fragments(ly[k]) if k.endswith("_w") else
+                                 torch.stack([ly[k], colsum(ly[k[:-2] + "_w"])])
+                                 if k in ("attn_b", "fc_b") else ly[k])
                              for k in ("attn_w", "attn_b", "proj_w", "proj_b", "fc_w", "fc_b",
                                        "mproj_w", "mproj_b")} for ly in self.layers]
             keys = ("attn_w", "attn_b", "proj_w", "proj_b", "fc_w", "fc_b", "mproj_w", "mproj_b")

@@ -514,8 +514,8 @@ def _decode_grid_args(R, Lmax, max_steps, stop0, stop1, V, wte, wpe, wte_packed,
                  (out_len, "out_len"), (step_ctr, "step_ctr"), (all_done, "all_done")):
         _i32(t, n)
     _need(out_ids.shape[-1] == max_steps, "gpt2 decode grid: out_ids [R, max_steps]")
-    _need(lm_bias.dtype == torch.float32 and lm_bias.numel() >= -(-V // 16) * 16,
-          "gpt2 decode grid: lm_bias f32 [ceil(V/16) 16]")
+    _need(lm_bias.dtype == torch.float32 and lm_bias.numel() >= 2 * (-(-V // 16) * 16),
+          "gpt2 decode grid: lm_bias f32 [2][ceil(V/16) 16]")
     _need(temperature > 0, "gpt2 decode grid: temperature > 0")
     decode_persist_grid(grid)
     base = ws.data_ptr()
