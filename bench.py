@@ -128,9 +128,14 @@ def parse(argv=None):
     ap.add_argument("--inflight", type=int, default=10,
                     help="independent batches in flight per GPU, each on its own HIP stream "
                          "(capped by --persist-budget // the smallest grid)")
+    ap.add_argument("--encode-ahead", type=int, default=256,
+                    help="clips per up-front encoder pass of the caption runs (the encoder twin "
+                         "encodes consecutive eval batches together on a stream of its own, each "
+                         "batch's begin waits for its own pass; 0 = every batch encodes its own "
+                         "clips at --batch)")
     ap.add_argument("--persist-budget", type=int, default=0,
                     help="workgroup slots (half a CU each) the in-flight persistent decode grids "
-                         "may hold together (0: ZSAAC_PERSIST_BUDGET or one per CU)")
+                         "may hold together (0: ZSAAC_PERSIST_BUDGET or two per CU)")
     ap.add_argument("--reps", type=int, default=HEADLINE_REPS,
                     help="timed repetitions of the headline region (value = their median)")
     ap.add_argument("--hw-queues", type=int, default=16,
@@ -255,9 +260,11 @@ def run_captions(args, world, rank, device, pipe, n_local, first, counts, inflig
     log(f"{n_local} clips in {len(batches)} batches of <= {B}, {inflight} in flight: capturing")
     if len(batches) == 0:
         raise ValueError("no clips on this rank")
+    ahead = getattr(args, "encode_ahead", 0) if not getattr(args, "beam", 0) else 0
     runner = ConcurrentRunner(pipe, max(1, inflight),
-                              streams=run_streams(device, max(1, inflight)),
-                              budget=getattr(args, "persist_budget", 0) or None)
+                              streams=run_streams(device, max(1, inflight) + (1 if ahead else 0)),
+                              budget=getattr(args, "persist_budget", 0) or None,
+                              encode_ahead=ahead)
     for size in sorted({b.shape[0] for b in batches}, reverse=True):   # captures every graph
         runner.warmup(next(b for b in batches if b.shape[0] == size))
         log(f"captured the decode graphs of {size}-clip batches")
@@ -1224,7 +1231,12 @@ def main():
                    "clips_per_rank": n_local, "clips_total": n_total,
                    "global_batch": B * world, "steps_in_flight_per_gpu": max(1, args.inflight),
                    "hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "4")),
-                   "encoder_batch": pipe.encoder.B,
+                   "encoder_batch": (runner.enc.B if getattr(runner, "enc", None) is not None
+                                     else pipe.encoder.B),
+                   "encoder_note": ("the encoder (wav -> CLAP embedding) runs ahead in passes of "
+                                    "encoder_batch clips (consecutive eval batches; the reference "
+                                    "extracts embeddings offline, data_handing/"
+                                    "embeddings_generator.py), the caption path at eval_batch"),
                    "parallelism": f"dp{world} (clip-sharded, RCCL all-gather of token ids)",
                    **info},
     }

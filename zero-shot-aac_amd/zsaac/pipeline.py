@@ -248,10 +248,11 @@ DEFAULT_PERSIST_GRIDS = "192,96,48"
 
 def persist_budget(cus: int) -> int:
     """Workgroup slots the in-flight persistent grids may hold together: a grid workgroup takes
-    half a CU (4 waves x <= 256 registers), so 2 x CUs is the chip; the default, one per CU,
-    leaves the other half of every grid CU to the begins' kernels (encode .. prefill);
-    ZSAAC_PERSIST_BUDGET overrides."""
-    return int(os.environ.get("ZSAAC_PERSIST_BUDGET", str(cus)))
+    half a CU (4 waves x <= 256 registers), so 2 x CUs is the chip -- the default (measured,
+    tools/headline_ab.py: one slot per CU leaves the chip to the begins and loses ~10 % of the
+    headline); the begins' kernels fit beside one grid workgroup per CU.  ZSAAC_PERSIST_BUDGET
+    overrides."""
+    return int(os.environ.get("ZSAAC_PERSIST_BUDGET", str(2 * cus)))
 
 
 def choose_persist_grid(in_flight: int, to_begin: int, grids: List[int], budget: int) -> int:
