@@ -260,7 +260,9 @@ def run_captions(args, world, rank, device, pipe, n_local, first, counts, inflig
     log(f"{n_local} clips in {len(batches)} batches of <= {B}, {inflight} in flight: capturing")
     if len(batches) == 0:
         raise ValueError("no clips on this rank")
-    ahead = getattr(args, "encode_ahead", 0) if not getattr(args, "beam", 0) else 0
+    ahead = getattr(args, "encode_ahead", 0)
+    if getattr(args, "beam", 0) or ahead < B:      # beam runs / larger batches: encoder per batch
+        ahead = 0
     runner = ConcurrentRunner(pipe, max(1, inflight),
                               streams=run_streams(device, max(1, inflight) + (1 if ahead else 0)),
                               budget=getattr(args, "persist_budget", 0) or None,
@@ -800,8 +802,12 @@ def main_embeddings(args, world, rank, device, pipe):
     n_total = args.clips or B * steps * world
     lo, hi = zd.shard_range(n_total, rank, world)
     counts = zd.shard_counts(n_total, world)
+    # (clip c of the shard encodes pool[c % len(pool)]: the waveforms are regenerated per
+    # pass-sized window to bound memory; the encoder work per clip is the same)
     pool = synthetic_clips(min(hi - lo, 2 * B), lo, device)
     embs = torch.empty(hi - lo, 1024, device=device)
+    gathered = [embs]
+    dist_on = torch.distributed.is_available() and torch.distributed.is_initialized()
 
     def run(n_batches, keep):
         for i in range(n_batches):
@@ -810,8 +816,8 @@ def main_embeddings(args, world, rank, device, pipe):
             e = pipe.encode(pool[(c0 % pool.shape[0]):(c0 % pool.shape[0]) + (c1 - c0)])
             if keep:
                 embs[c0:c1].copy_(e)
-        if keep and world > 1:
-            zd.gather_rows(embs, counts)
+        if keep and dist_on:          # the RCCL all-gather (at world 1 too, under a process group)
+            gathered[0] = zd.gather_rows(embs, counts)
     nb = -(-(hi - lo) // B)
     run(min(args.warmup, nb), False)
     torch.cuda.synchronize()
@@ -841,8 +847,7 @@ def main_embeddings(args, world, rank, device, pipe):
                       "parallelism": f"dp{world} (clip-sharded)"}}
     if rank == 0:
         print(json.dumps(res), flush=True)
-    if world > 1:
-        torch.distributed.destroy_process_group()
+    return res, gathered[0]
 
 
 # ------------------------------------------------------------------ main
@@ -1193,7 +1198,10 @@ def main():
         return main_mistral(args, torch.device("cuda", 0))
     pipe, csd, asd = build(args, device)
     if args.embeddings_only:
-        return main_embeddings(args, world, rank, device, pipe)
+        main_embeddings(args, world, rank, device, pipe)
+        if world > 1:
+            torch.distributed.destroy_process_group()
+        return
     B = pipe.cfg.batch
     if args.clips:                              # strong scaling: a fixed clip set, sharded
         n_total, scaling = args.clips, "strong"

@@ -3,7 +3,8 @@ on device tensors -- zsaac/dist.py gather_rows (the C4 embedding all-gather) and
 collect_captions (the caption path's one all-gather of token ids + lengths) -- in a fresh process
 whose FIRST GPU call is the process-group bring-up, as a bench rank's is.  The gathered rows must
 equal the local ones (world 1), for ragged counts, greedy and beam batches, and a real bs-64
-caption batch of the bench's pipeline."""
+caption batch of the bench's pipeline; and C4 end to end: bench.main_embeddings (batched HTSAT
+encode_audio + gather_rows) against the oracle's f32 embedding chain."""
 import os
 import socket
 
@@ -65,6 +66,32 @@ def _worker(port, q):
         r = pipe.caption_wav(bench.synthetic_clips(64, 0, dev))
         ci, cl = zd.collect_captions([r], [64])
         out["collect_pipeline"] = bool(torch.equal(ci, r.ids) and torch.equal(cl, r.lengths.int()))
+        # C4: bench.main_embeddings (batched HTSAT encode_audio, then the RCCL gather_rows of the
+        # [N, 1024] embeddings) on 10 clips in passes of 4, against the f32 oracle chain
+        # (wav -> log-mel -> HTSAT -> audio_proj) on clips 1 and 9 (= pool row 1: the bench
+        # re-encodes a 2-pass window of waveforms)
+        import numpy as np
+        from types import SimpleNamespace
+        from oracle import audio as OA, frontend as OF
+        from zsaac import synthetic as S
+
+        class E:
+            batch, group, dtype, encoder, mapper, beam, entry_length, compact = \
+                4, 1, "bf16", "htsat", "mlp", 0, 67, 1
+            encoder_batch = 4
+        epipe, _, asd = bench.build(E, dev)
+        eargs = SimpleNamespace(steps=None, clips=10, warmup=1, encoder="htsat", dtype="bf16")
+        res, embs = bench.main_embeddings(eargs, 1, 0, dev, epipe)
+        out["c4_value"] = res["value"]
+        out["c4_rows"] = int(embs.shape[0])
+        wav = bench.synthetic_clips(2, 0, torch.device("cpu"))[1:2]
+        with torch.no_grad():
+            ref = OA.audio_project(OA.htsat_embedding(OF.logmel(wav), asd), asd)[0].numpy()
+        got = embs.cpu().numpy()
+        cos = [float((got[c] * ref).sum() / np.linalg.norm(got[c]) / np.linalg.norm(ref))
+               for c in (1, 9)]
+        out["c4_cos"] = cos
+        out["c4_same_clip"] = bool(np.array_equal(got[1], got[9]))
         torch.cuda.synchronize()
         dist.barrier()
         dist.destroy_process_group()
@@ -78,10 +105,14 @@ def test_nccl_world1_collectives(cuda):
     q = ctx.Queue()
     p = ctx.Process(target=_worker, args=(_free_port(), q))
     p.start()
-    res = q.get(timeout=240)
+    res = q.get(timeout=420)
     p.join(timeout=60)
     assert "error" not in res, res
     assert p.exitcode == 0
     assert res["backend"] == "nccl"
     for k in ("gather_rows", "collect_greedy", "collect_beam", "collect_pipeline"):
         assert res[k], (k, res)
+    # C4 (BASELINE.json configs[3]): bench.main_embeddings' batched encode + RCCL gather_rows
+    assert res["c4_rows"] == 10 and res["c4_value"] > 0
+    assert res["c4_same_clip"], "the same waveform must give the same embedding in any pass"
+    assert min(res["c4_cos"]) > 0.995, res["c4_cos"]      # bf16 encoder vs the f32 oracle

@@ -75,7 +75,6 @@ constexpr int QS = KSD / NW, QF = KSF / NW;          // k-steps of one wave's K 
 constexpr int NCB_Q = QKVN / 16, NCB_D = D / 16, NCB_F = DFF / 16;   // 16-column blocks
 constexpr unsigned SPIN_MAX = 1u << 22;
 constexpr int NSH = 8;                               // barrier counter shards, one 128-B line each
-constexpr int KC = 4;                                // attention keys per lane group per chunk
 constexpr int ECH = 4;                               // phase E: k-steps per streamed chunk
 
 // Tiles per workgroup of each GEMM phase: CB column blocks x RB row blocks of 16 (workgroup w
@@ -95,6 +94,8 @@ template <> struct Geo<192> {
 template <int G> struct Units {
   static constexpr int UPG = RM * NH / G;   // attention units per workgroup
   static constexpr int KU = UPG / NW;       // per wave
+  static constexpr int KC = KU >= 2 ? 4 : 8;   // keys per lane group per loaded chunk (KU KC 8
+                                               // registers; a multiple of 4, phase_b)
 };
 
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8_t;
@@ -710,7 +711,7 @@ __device__ __forceinline__ void attn_unit(const Args& a, const Sm& sm, int u, in
   p = (a.exp & 2) ? 1 : min(sm.pos[rr], a.Lmax - 1);
   base = ((long)(rr * NH + hh) * a.Lmax) * HD + 8 * ((otid() & 63) & 7);
 }
-template <int KU>
+template <int KU, int KC>
 __device__ __forceinline__ void attn_load(const Args& a, int l, const Sm& sm, int ub, int cb,
                                           u32x4_t (&kr)[KU][KC], u32x4_t (&vr)[KU][KC]) {
   const int tid = otid(), v = tid >> 6, grp = (tid & 63) >> 3;
@@ -729,7 +730,7 @@ __device__ __forceinline__ void attn_load(const Args& a, int l, const Sm& sm, in
     }
   }
 }
-template <int KU>
+template <int KU, int KC>
 __device__ __forceinline__ void phase_b(const Args& a, const Rs& rs, int l, const Sm& sm, int ub,
                                         u32x4_t (&kr)[KU][KC], u32x4_t (&vr)[KU][KC]) {
   const int tid = otid(), lane = tid & 63, v = tid >> 6, grp = lane >> 3, sub = lane & 7;
@@ -775,34 +776,40 @@ __device__ __forceinline__ void phase_b(const Args& a, const Rs& rs, int l, cons
   int pmax = p[0];
 #pragma unroll
   for (int k = 1; k < KU; ++k) pmax = max(pmax, p[k]);
+  // loads in chunks of 8 KC keys; the online softmax always steps 32 keys at a time (the same
+  // recurrence, so the same rounding, whatever KC a grid size loads with)
   for (int cb = 0; cb < pmax; cb += 8 * KC) {
-    if (cb > 0) attn_load<KU>(a, l, sm, ub, cb, kr, vr);
+    if (cb > 0) attn_load<KU, KC>(a, l, sm, ub, cb, kr, vr);
 #pragma unroll
-    for (int k = 0; k < KU; ++k) {
-      if (cb >= p[k]) continue;                   // wave-uniform
-      float sc[KC];
-      float pm = -INFINITY;
+    for (int h = 0; h < KC / 4; ++h) {
+      const int cs = cb + 32 * h;
 #pragma unroll
-      for (int i = 0; i < KC; ++i) {
-        const float sv = qk(qu[k], kr[k][i]);
-        sc[i] = cb + 8 * i + grp < p[k] ? sv : -INFINITY;
-        pm = fmaxf(pm, sc[i]);
-      }
-      pm = fmaxf(pm, xor8(pm));
-      pm = max16(pm);
-      pm = max32(pm);
-      const float mn = fmaxf(m[k], pm);
-      const float scale = __expf(m[k] - mn);
-      sum[k] *= scale;
-      const f32x2_t sc2 = {scale, scale};
+      for (int k = 0; k < KU; ++k) {
+        if (cs >= p[k]) continue;                   // wave-uniform
+        float sc[4];
+        float pm = -INFINITY;
 #pragma unroll
-      for (int t = 0; t < 4; ++t) o[k][t] *= sc2;
-      m[k] = mn;
+        for (int i = 0; i < 4; ++i) {
+          const float sv = qk(qu[k], kr[k][4 * h + i]);
+          sc[i] = cs + 8 * i + grp < p[k] ? sv : -INFINITY;
+          pm = fmaxf(pm, sc[i]);
+        }
+        pm = fmaxf(pm, xor8(pm));
+        pm = max16(pm);
+        pm = max32(pm);
+        const float mn = fmaxf(m[k], pm);
+        const float scale = __expf(m[k] - mn);
+        sum[k] *= scale;
+        const f32x2_t sc2 = {scale, scale};
 #pragma unroll
-      for (int i = 0; i < KC; ++i) {
-        const float e = __expf(sc[i] - mn);
-        sum[k] += e;
-        vacc(o[k], e, vr[k][i]);
+        for (int t = 0; t < 4; ++t) o[k][t] *= sc2;
+        m[k] = mn;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float e = __expf(sc[i] - mn);
+          sum[k] += e;
+          vacc(o[k], e, vr[k][4 * h + i]);
+        }
       }
     }
   }
@@ -978,7 +985,7 @@ __device__ __forceinline__ void gave_up(const Args& a) {
 template <int G>
 __global__ __launch_bounds__(NT, 2) void dg_persist_kernel(Args a) {
   using Gm = Geo<G>;
-  constexpr int KU = Units<G>::KU;
+  constexpr int KU = Units<G>::KU, KC = Units<G>::KC;
   __shared__ __attribute__((aligned(16))) char smem[SM_TOTAL];
   const Sm sm(smem);
   const int w = blockIdx.x;
@@ -1010,12 +1017,12 @@ __global__ __launch_bounds__(NT, 2) void dg_persist_kernel(Args a) {
       phase_a<G, false>(a, rs, l, w, sm, wq);
       bar_arrive(bar, w);
       u32x4_t kr[KU][KC], vr[KU][KC];
-      attn_load<KU>(a, l, sm, ub, 0, kr, vr);
+      attn_load<KU, KC>(a, l, sm, ub, 0, kr, vr);
       if (!bar_wait(bar, s_ok)) return gave_up(a);
       if (l == 0 && w == 0 && otid() < RM)   // last step's keys: every workgroup has read them
         __hip_atomic_store(keys + ((step + 1) & 1) * RM + otid(), 0ull, __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
-      phase_b<KU>(a, rs, l, sm, ub, kr, vr);
+      phase_b<KU, KC>(a, rs, l, sm, ub, kr, vr);
       bar_arrive(bar, w);
       u32x4_t wo[Gm::ECB * QS];
       ldw<Gm::ECB, QS>(a.wo[l], KSD, ecb0, QS * V_, wo);
@@ -1075,10 +1082,10 @@ __global__ __launch_bounds__(NT, 2) void dg_phase_kernel(Args a) {
     u32x4_t wq[Gm::APF * QS];
     phase_a<G, true>(a, rs, l, w, sm, wq);
   } else if constexpr (PH == PH_B) {
-    constexpr int KU = Units<G>::KU;
+    constexpr int KU = Units<G>::KU, KC = Units<G>::KC;
     u32x4_t kr[KU][KC], vr[KU][KC];
-    attn_load<KU>(a, l, sm, w * Units<G>::UPG, 0, kr, vr);
-    phase_b<KU>(a, rs, l, sm, w * Units<G>::UPG, kr, vr);
+    attn_load<KU, KC>(a, l, sm, w * Units<G>::UPG, 0, kr, vr);
+    phase_b<KU, KC>(a, rs, l, sm, w * Units<G>::UPG, kr, vr);
   } else if constexpr (PH == PH_C) {
     u32x4_t wo[Gm::ECB * QS];
     f32x4_t xo{0.f, 0.f, 0.f, 0.f};
