@@ -12,7 +12,7 @@ The persistent decode kernel (bench.py's roofline since round 3): ``run_persist`
 bench's first eval batch (64 synthetic clips, 67 greedy steps) three times on one stream, and
 ``parse_persist`` writes profiles/r3_pmc_persist.json (per-launch bytes, median launch):
 
-    rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_pf -o run --output-format csv -- python3 tools/pmc_traffic.py run_persist
+    rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc_pf -o run --output-format csv -- python3 tools/pmc_traffic.py run_persist [grid]
     rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmc_pw -o run --output-format csv -- python3 tools/pmc_traffic.py run_persist
     python3 tools/pmc_traffic.py parse_persist gpurun_out/pmc_pf gpurun_out/pmc_pw profiles/r3_pmc_persist.json
 
@@ -105,10 +105,12 @@ def _bench_pipe():
     return bench, pipe
 
 
-def run_persist(reps=3):
+def run_persist(reps=3, grid=None):
     import torch
     bench, pipe = _bench_pipe()
     assert pipe.decoder.persist, "the persistent decode path is off"
+    if grid:
+        pipe.decoder.persist_grid = int(grid)
     wav = bench.synthetic_clips(64, 0, torch.device("cuda", 0))
     info = []
     for _ in range(reps):
@@ -150,7 +152,7 @@ if __name__ == "__main__":
     if sys.argv[1] == "run":
         run()
     elif sys.argv[1] == "run_persist":
-        run_persist()
+        run_persist(grid=sys.argv[2] if len(sys.argv) > 2 else None)
     elif sys.argv[1] == "parse_persist":
         parse_persist(*sys.argv[2:5])
     else:

@@ -1,59 +1,53 @@
 #!/usr/bin/env python3
-"""Trace-side cross-check of bench.py's roofline: the average duration rocprofv3 recorded for
-the roofline kernel's dispatches (same kernel template, same grid) in a kernel trace of the bench
-command, next to the value bench.py measured with HIP events in that same run.
+"""Cross-check of bench.py's roofline against a rocprofv3 kernel trace of the same command: the
+dg_persist_kernel launches grouped into runs of the caption region (launches overlapping in time,
+separated by idle gaps), the average duration of every 17-launch run, and bench's own
+roofline.avg_launch_us (its last run before the single-stream extras is the untimed log pass the
+roofline is measured on).
 
-    python3 tools/roofline_check.py <rocprof dir> <bench stdout log>
+    python3 tools/roofline_check.py <trace dir> <bench json> <out json>
 """
 import csv
 import glob
 import json
 import os
-import statistics
 import sys
 
 
-def main(pdir, bench_log):
-    line = [l for l in open(bench_log) if l.startswith("{")][-1]
-    b = json.loads(line)
-    rl = b["roofline"]
-    # the roofline launches: gemm_lean_kernel dispatches with the c_fc grid of their own tile
-    # (template args BM, BN) that run back to back — the decode never launches two c_fc in a row,
-    # bench.py's roofline graph replays nothing else, so runs of >= 32 consecutive such
-    # dispatches are exactly the timed launches (without the concurrent streams' contention)
-    mm = int(rl["kernel"].split("[")[1].split("x")[0])
+def main(d, bench_json, out):
     rows = []
-    for fn in glob.glob(os.path.join(pdir, "**", "*kernel_trace.csv"), recursive=True):
-        rows += list(csv.DictReader(open(fn)))
-    rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-
-    def is_cfc(r):
-        name = r["Kernel_Name"]
-        if "gemm_lean_kernel<" not in name:
-            return None
-        targs = [int(v.strip(" >()")) for v in
-                 name.split("gemm_lean_kernel<")[1].split(">")[0].split(",")]
-        bm, bn = targs[:2]
-        threads = 64 * targs[4] * targs[5] if len(targs) >= 6 else 256
-        g = -(-3072 // bn) * -(-mm // bm) * threads
-        return g if int(r["Grid_Size_X"]) == g else None
-
-    durs, grid, run = [], None, []
-    for r in rows + [None]:
-        g = is_cfc(r) if r is not None else None
-        if g is not None:
-            grid = g
-            run.append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
-            continue
-        if len(run) >= 32:
-            durs += run
-        run = []
-    out = {"kernel": rl["kernel"], "grid_size_x": grid, "dispatches": len(durs),
-           "trace_avg_us": round(statistics.mean(durs), 3) if durs else None,
-           "trace_median_us": round(statistics.median(durs), 3) if durs else None,
-           "bench_hip_event_avg_us": rl["avg_launch_us"]}
-    print(json.dumps(out, indent=1))
+    for fn in glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True):
+        with open(fn) as f:
+            for r in csv.DictReader(f):
+                if "dg_persist_kernel" in r["Kernel_Name"]:
+                    rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]),
+                                 r["Kernel_Name"].split("(")[0]))
+    rows.sort()
+    runs, cur, end = [], [], 0
+    for r in rows:
+        if cur and r[0] > end:          # nothing in flight: a new run
+            runs.append(cur)
+            cur = []
+        cur.append(r)
+        end = max(end, r[1]) if len(cur) > 1 else r[1]
+    if cur:
+        runs.append(cur)
+    with open(bench_json) as f:
+        b = json.loads(f.read().strip().split("\n")[-1])
+    n = b["roofline"].get("launches", 17)
+    full = [[round(sum(e - s for s, e, _ in r) / len(r) / 1e3, 1), len(r)] for r in runs if len(r) == n]
+    res = {"bench_roofline_avg_launch_us": b["roofline"]["avg_launch_us"],
+           "bench_value": b["value"],
+           "rocprof_runs_of_%d_launches_avg_us" % n: full,
+           "rocprof_log_pass_avg_us": full[-1][0] if full else None,
+           "agreement": (round(full[-1][0] / b["roofline"]["avg_launch_us"], 3) if full else None),
+           "note": "runs = groups of dg_persist_kernel launches with no idle gap; the bench's "
+                   "timed repetitions then its untimed log pass (HIP events around each launch) "
+                   "are the 17-launch runs, in order"}
+    with open(out, "w") as f:
+        json.dump(res, f, indent=1)
+    print(json.dumps(res))
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], sys.argv[2])
+    main(*sys.argv[1:4])

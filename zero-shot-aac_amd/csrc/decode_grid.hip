@@ -750,13 +750,6 @@ __device__ __forceinline__ void phase_b(const Args& a, const Rs& rs, int l, cons
     vnu[k] = ld16(rv, off);
   }
   __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-  for (int k = 0; k < KU; ++k) {
-#pragma unroll
-    for (int t = 0; t < 4; ++t) o[k][t] = f32x2_t{0.f, 0.f};
-    m[k] = -INFINITY;
-    sum[k] = 0.f;
-  }
   // q . k over the lane's 8 dims: four bf16-pair dots, then the 8 lanes of the key, / sqrt(64)
   auto qk = [&](const u32x4_t& qv, const u32x4_t& kv) {
     float sv = dot2bf(qv.x, kv.x, 0.f);
@@ -765,6 +758,19 @@ __device__ __forceinline__ void phase_b(const Args& a, const Rs& rs, int l, cons
     sv = dot2bf(qv.w, kv.w, sv);
     return sum8(sv) * 0.125f;
   };
+  // the online softmax starts from the new key (position pos): its score is every lane's running
+  // max, and lane group 0 alone carries its weight 1 and its value (the groups are summed at the
+  // end), so the new key / value registers are free before the cached keys stream in
+#pragma unroll
+  for (int k = 0; k < KU; ++k) {
+    m[k] = qk(qu[k], knu[k]);
+    sum[k] = grp == 0 ? 1.f : 0.f;
+    const unsigned w[4] = {vnu[k].x, vnu[k].y, vnu[k].z, vnu[k].w};
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+      o[k][t] = grp == 0 ? f32x2_t{__uint_as_float(w[t] << 16), __uint_as_float(w[t] & 0xffff0000u)}
+                         : f32x2_t{0.f, 0.f};
+  }
   auto vacc = [&](f32x2_t (&acc)[4], float e, const u32x4_t& vv) {
     const unsigned w[4] = {vv.x, vv.y, vv.z, vv.w};
     const f32x2_t e2 = {e, e};
@@ -815,22 +821,12 @@ __device__ __forceinline__ void phase_b(const Args& a, const Rs& rs, int l, cons
   }
 #pragma unroll
   for (int k = 0; k < KU; ++k) {
-    sum[k] = add32(add16(sum[k] + xor8(sum[k])));
+    const float inv = 1.0f / add32(add16(sum[k] + xor8(sum[k])));
     float of[8];
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
-      of[2 * t] = add32(add16(o[k][t].x + xor8(o[k][t].x)));
-      of[2 * t + 1] = add32(add16(o[k][t].y + xor8(o[k][t].y)));
-    }
-    const float sn = qk(qu[k], knu[k]);
-    const float mn = fmaxf(m[k], sn);
-    const float sc = __expf(m[k] - mn), en = __expf(sn - mn);
-    const float inv = 1.0f / fmaf(sum[k], sc, en);
-    const unsigned w[4] = {vnu[k].x, vnu[k].y, vnu[k].z, vnu[k].w};
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      of[2 * t] = fmaf(en, __uint_as_float(w[t] << 16), of[2 * t] * sc) * inv;
-      of[2 * t + 1] = fmaf(en, __uint_as_float(w[t] & 0xffff0000u), of[2 * t + 1] * sc) * inv;
+      of[2 * t] = add32(add16(o[k][t].x + xor8(o[k][t].x))) * inv;
+      of[2 * t + 1] = add32(add16(o[k][t].y + xor8(o[k][t].y))) * inv;
     }
     if (grp == 0 && row[k] < a.R) {
       // att in fragment order: row r, dims 64 h + 8 sub .. + 8 = k-step 2 h + sub / 4,
