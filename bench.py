@@ -135,7 +135,7 @@ def parse(argv=None):
                          "clips at --batch)")
     ap.add_argument("--persist-budget", type=int, default=0,
                     help="workgroup slots (half a CU each) the in-flight persistent decode grids "
-                         "may hold together (0: ZSAAC_PERSIST_BUDGET or two per CU)")
+                         "may hold together (0: ZSAAC_PERSIST_BUDGET or 1.5 per CU)")
     ap.add_argument("--reps", type=int, default=HEADLINE_REPS,
                     help="timed repetitions of the headline region (value = their median)")
     ap.add_argument("--hw-queues", type=int, default=16,

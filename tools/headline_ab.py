@@ -3,6 +3,7 @@
 decode) repeated for several arms, interleaved, so box-to-box and run-to-run spread cancel.
 
 An arm is "name:inflight:knob=v,knob=v[:grids[:budget[:encode_ahead]]]" (zs_tune_set knobs, reset
+(knob late=0: the runner sizes each grid at its batch's begin instead of at its launch)
 to the baseline values given with --base between arms; grids: the persistent-decode grid sizes the
 runner may use, zsaac.pipeline.persist_grids, e.g. "48" or "96-48" ('-'-separated); budget:
 workgroup slots of the in-flight grids; encode_ahead: clips per up-front encoder pass, 0 = each
@@ -68,7 +69,9 @@ def main():
                              begin_first=len(sh) > 3 and sh[3] == "bf")
         for size in sorted({b.shape[0] for b in batches}, reverse=True):
             r.warmup(next(b for b in batches if b.shape[0] == size))
-        arms.append((name, r, knobs(kn)))
+        kn = knobs(kn)
+        r.late_grid = bool(kn.pop("late", 1))      # runner option, not a zs_tune_set knob
+        arms.append((name, r, kn))
     res = {n: [] for n, _, _ in arms}
     for rep in range(a.reps + 1):
         for name, r, kn in arms:

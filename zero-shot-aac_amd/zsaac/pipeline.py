@@ -248,11 +248,11 @@ DEFAULT_PERSIST_GRIDS = "192,96,48"
 
 def persist_budget(cus: int) -> int:
     """Workgroup slots the in-flight persistent grids may hold together: a grid workgroup takes
-    half a CU (4 waves x <= 256 registers), so 2 x CUs is the chip -- the default (measured,
-    tools/headline_ab.py: one slot per CU leaves the chip to the begins and loses ~10 % of the
-    headline); the begins' kernels fit beside one grid workgroup per CU.  ZSAAC_PERSIST_BUDGET
-    overrides."""
-    return int(os.environ.get("ZSAAC_PERSIST_BUDGET", str(2 * cus)))
+    half a CU (4 waves x <= 256 registers), so 2 x CUs is the chip.  The default, 1.5 x CUs (8
+    grids of 48), leaves a quarter of the slots to the begins' kernels: measured in one process
+    (tools/headline_ab.py, 12 reps, encode-ahead 256, grids sized at launch): 5.73k clips/s
+    against 5.33k at 2 x CUs and 4.71k at 1 x CUs.  ZSAAC_PERSIST_BUDGET overrides."""
+    return int(os.environ.get("ZSAAC_PERSIST_BUDGET", str(3 * cus // 2)))
 
 
 def choose_persist_grid(in_flight: int, to_begin: int, grids: List[int], budget: int) -> int:
@@ -291,6 +291,7 @@ class ConcurrentRunner:
         # at once, and the persistent launches follow as the budget frees, the first ones after
         # every first-round begin -- the begins run on the whole chip instead of beside the grids
         self.begin_first = bool(begin_first) and self.persist
+        self.late_grid = True     # grid size chosen when the begin has finished (False: at begin)
         if self.persist and not self.begin_first:
             # persistent decode grids must be co-resident: at most budget // (smallest grid)
             n_inflight = max(1, min(n_inflight, self.budget // self.grids[-1]))
@@ -362,24 +363,47 @@ class ConcurrentRunner:
                 st = active.get(i)
                 if st is None:
                     if nxt < len(batches):
-                        if self.persist:
+                        # persistent decode: the begin is enqueued now, the grid launch when the
+                        # begin has finished (its size chosen then, from the grids in flight and
+                        # the batches not yet launched: bigger grids once few batches remain)
+                        if self.persist and not self.late_grid:    # (A/B: size at begin)
                             g = choose_persist_grid(sum(slots.values()), len(batches) - nxt,
                                                     self.grids, self.budget)
+                            self.grid[nxt] = slots[i] = g
                             p.decoder.persist_grid = g
-                            slots[i] = g
-                            self.grid[nxt] = g
+                        p.decoder.defer_launch = self.persist and self.late_grid
+                        try:
+                            self._begin(i, nxt, batches, inputs, ahead)
+                        finally:
+                            p.decoder.defer_launch = False
                         with torch.cuda.stream(s):
-                            if ahead is not None:
-                                embs, evs = ahead
-                                s.wait_event(evs[nxt])
-                                p.begin_emb(embs[nxt])
+                            if self.persist and self.late_grid:
+                                ev = torch.cuda.Event()
+                                ev.record(s)
+                                active[i] = ("begun", nxt, ev)
                             else:
-                                (p.begin_wav if inputs == "wav" else p.begin_emb)(batches[nxt])
-                            ev, flag = p.decoder.finished_async()
-                        active[i] = (nxt, 0, ev, flag)
+                                ev, flag = p.decoder.finished_async()
+                                active[i] = (nxt, 0, ev, flag)
                         self.assign.append((i, nxt))
                         nxt += 1
                         progressed = True
+                    continue
+                if st[0] == "begun":
+                    _, bi, ev = st
+                    if not ev.query():
+                        continue
+                    unlaunched = len(batches) - nxt + sum(1 for a in active.values()
+                                                          if a[0] == "begun")
+                    g = choose_persist_grid(sum(slots.values()), unlaunched, self.grids,
+                                            self.budget)
+                    p.decoder.persist_grid = g
+                    slots[i] = g
+                    self.grid[bi] = g
+                    with torch.cuda.stream(s):
+                        p.decoder.launch_pending()
+                        ev, flag = p.decoder.finished_async()
+                    active[i] = (bi, 0, ev, flag)
+                    progressed = True
                     continue
                 bi, n, ev, flag = st
                 if not ev.query():
