@@ -487,7 +487,10 @@ int zs_greedy_step_map(const float* part_val, const int* part_idx, int R, const 
  * temperature > 0 divides the logits before the argmax (gpt2_prefix_eval.py:196);
  * kv: 24 pointers {kc[0..11], vc[0..11]}, each [R][12][Lmax][64] bf16 (zs_kv_write layout),
  * 128-byte aligned.  ws: scratch of zs_decode_persist_workspace_bytes() bytes, 256-byte aligned,
- * private to one launch in flight.  Every output element is computed by the same operations
+ * private to one launch in flight.  exclusive != 0: each workgroup also requests LDS past half a
+ * CU, so no two exclusive workgroups share a CU (the dispatcher otherwise doubles workgroups up
+ * while CUs idle); the caller keeps the exclusive workgroups in flight <= the CU count.  Every
+ * output element is computed by the same operations
  * whatever `grid` (each GEMM element: four K-quarter MFMA chains summed (p0 + p1) + (p2 + p3);
  * LayerNorm statistics (one pass, sum x and sum x^2), attention and argmax in fixed orders), so ids and state do not depend on the grid
  * and equal zs_gpt2_decode_phases'.  A grid that cannot become co-resident gives up after a
@@ -499,7 +502,8 @@ int zs_gpt2_decode_persist(int R, int Lmax, int max_steps, int stop0, int stop1,
                            float temperature, const void* const* layer_w,
                            const float* lm_bias, void* const* kv, int* pos,
                            int* next_tok, int* done, int* out_ids, int* out_len, int* step_ctr,
-                           int* all_done, void* ws, long ws_bytes, int grid, void* stream);
+                           int* all_done, void* ws, long ws_bytes, int grid, int exclusive,
+                           void* stream);
 /* zs_gpt2_decode_phases: `steps` decode steps of the same computation as separate launches (one
  * per phase of every block, the LM head and the bookkeeping: 62 per step; each a no-op once
  * all_done[0] is set, so a graph-captured chunk can run past the end) -- the per-step path of

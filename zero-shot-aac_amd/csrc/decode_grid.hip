@@ -124,6 +124,7 @@ constexpr int SM_LN = SM_RED + 32768;             // f32 [2][4][64]: LayerNorm p
 constexpr int SM_CB = SM_LN + 2048;               // f32 [2][64]: the tile's bias / column sums
 constexpr int SM_ST = SM_CB + 512;                // int tok[64], pos[64], done[64], misc[16]
 constexpr int SM_TOTAL = SM_ST + (3 * RM + 16) * 4;
+constexpr int EXCL_LDS = 80 * 1024 + 512;        // an exclusive launch's LDS per workgroup (> 1/2 CU)
 
 struct Args {
   int R, Lmax, max_steps, stop0, stop1, V, layer, abort_step, exp;
@@ -263,6 +264,8 @@ __device__ __forceinline__ int frag_off(int row, int col, int KS) {
 // zs_decode_persist_set_stamps(buf, step): thread 0 of every workgroup writes s_memrealtime
 // (100 MHz) after each barrier arrive (slot 2i) and wait (2i + 1) of decode step `step`, and at
 // its start (127) / end (126), into buf[w][128] (tools/persist_stamps.py).  NULL = off.
+// step -2: every persistent workgroup w writes (XCC_ID << 32 | HW_ID) to its launch's workspace at
+// WS_X + 8 w instead (tools/placement.py: which CU each workgroup of concurrent grids landed on).
 __device__ unsigned long long* dp_stamp_buf;
 __device__ int dp_stamp_step;
 __device__ const char* dp_stamp_ws;   // only the launch on this workspace (NULL: every launch)
@@ -997,6 +1000,12 @@ __global__ __launch_bounds__(NT, 2) void dg_persist_kernel(Args a) {
   unsigned long long* const stamps =
       (dp_stamp_ws == nullptr || dp_stamp_ws == a.ws) ? dp_stamp_buf : nullptr;
   const int stamp_step = dp_stamp_step;
+  if (stamp_step == -2 && threadIdx.x == 0) {   // diagnostic: where this workgroup runs
+    unsigned hw, xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    ((gu64*)(a.ws + WS_X))[w] = ((unsigned long long)xcc << 32) | hw;
+  }
   const int ub = w * Units<G>::UPG;
   constexpr int ANCG = NCB_Q / Gm::ACB, DNCG = NCB_F / Gm::DCB, ENCG = NCB_D / Gm::ECB;
   const int acb0 = (w % ANCG) * Gm::ACB, dcb0 = (w % DNCG) * Gm::DCB, ecb0 = (w % ENCG) * Gm::ECB;
@@ -1180,17 +1189,30 @@ extern "C" int zs_gpt2_decode_persist(int R, int Lmax, int max_steps, int stop0,
                                       const float* lm_bias, void* const* kv,
                                       int* pos, int* next_tok, int* done, int* out_ids,
                                       int* out_len, int* step_ctr, int* all_done, void* ws,
-                                      long ws_bytes, int grid, void* stream) {
+                                      long ws_bytes, int grid, int exclusive, void* stream) {
   dg::Args a;
   const int rc = dg_args(a, R, Lmax, max_steps, stop0, stop1, V, wte, wpe, wte_packed, temperature,
                          layer_w, lm_bias, kv, pos, next_tok, done, out_ids, out_len, step_ctr,
                          all_done, ws, ws_bytes, grid);
   if (rc) return rc;
+  // exclusive: dynamic LDS past half a CU's 160 KiB, so no two such workgroups share a CU (the
+  // dispatcher otherwise doubles workgroups up on CUs while others idle: tools/placement.py)
+  const size_t dyn = exclusive ? (size_t)(dg::EXCL_LDS - dg::SM_TOTAL) : 0;
+  static bool attr = false;
+  if (exclusive && !attr) {
+    ZS_CHECK_HIP(hipFuncSetAttribute((const void*)dg::dg_persist_kernel<48>,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, dg::EXCL_LDS - dg::SM_TOTAL));
+    ZS_CHECK_HIP(hipFuncSetAttribute((const void*)dg::dg_persist_kernel<96>,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, dg::EXCL_LDS - dg::SM_TOTAL));
+    ZS_CHECK_HIP(hipFuncSetAttribute((const void*)dg::dg_persist_kernel<192>,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, dg::EXCL_LDS - dg::SM_TOTAL));
+    attr = true;
+  }
   // the barrier shards, timeout word and argmax keys: zeroed before every launch
   ZS_CHECK_HIP(hipMemsetAsync(ws, 0, dg::WS_SYNC_BYTES, S(stream)));
-  if (grid == 48) hipLaunchKernelGGL(dg::dg_persist_kernel<48>, dim3(48), dim3(dg::NT), 0, S(stream), a);
-  else if (grid == 96) hipLaunchKernelGGL(dg::dg_persist_kernel<96>, dim3(96), dim3(dg::NT), 0, S(stream), a);
-  else hipLaunchKernelGGL(dg::dg_persist_kernel<192>, dim3(192), dim3(dg::NT), 0, S(stream), a);
+  if (grid == 48) hipLaunchKernelGGL(dg::dg_persist_kernel<48>, dim3(48), dim3(dg::NT), dyn, S(stream), a);
+  else if (grid == 96) hipLaunchKernelGGL(dg::dg_persist_kernel<96>, dim3(96), dim3(dg::NT), dyn, S(stream), a);
+  else hipLaunchKernelGGL(dg::dg_persist_kernel<192>, dim3(192), dim3(dg::NT), dyn, S(stream), a);
   ZS_LAUNCH_CHECK();
   return 0;
 }

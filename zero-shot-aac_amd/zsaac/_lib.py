@@ -71,7 +71,7 @@ SIGNATURES = {
     "zs_greedy_step": [P, P, I, I, P, I, I, I, P, P, P, P, P, P, P],
     "zs_greedy_init": [I, P, P, P, P, P, I, P, P, P],
     "zs_decode_persist_workspace_bytes": [],
-    "zs_gpt2_decode_persist": [I, I, I, I, I, I, P, P, P, F, P, P, P, P, P, P, P, P, P, P, P, L, I, P],
+    "zs_gpt2_decode_persist": [I, I, I, I, I, I, P, P, P, F, P, P, P, P, P, P, P, P, P, P, P, L, I, I, P],
     "zs_gpt2_decode_phases": [I, I, I, I, I, I, P, P, P, F, P, P, P, P, P, P, P, P, P, P, P, L, I, I, P],
     "zs_decode_persist_status": [P, P],
     "zs_decode_persist_set_stamps": [P, I, P],

@@ -370,6 +370,7 @@ class Gpt2Decoder:
         self._persist_R = 0         # rows of the persistent launch in flight (0: none)
         self._persist_pending = 0   # rows of a greedy begin whose launch is deferred
         self.defer_launch = False   # greedy_begin leaves the persistent launch to launch_pending
+        self.persist_exclusive = False   # the launch takes a CU per workgroup (runner's choice)
         self.ws = ops.skinny_workspace(dev, [(M, N, K) for M in {self.R, self.Rp}
                                              for N, K in ((3 * D, D), (D, D), (4 * D, D), (D, 4 * D))])
 
@@ -649,7 +650,8 @@ class Gpt2Decoder:
             ev.append((torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True),
                        id(self)))
             ev[-1][0].record()
-        ops.gpt2_decode_persist(*self._grid_args(R), grid=self.persist_grid)
+        ops.gpt2_decode_persist(*self._grid_args(R), grid=self.persist_grid,
+                                exclusive=self.persist_exclusive)
         if ev is not None:
             ev[-1][1].record()
         self._persist_R = R

@@ -525,12 +525,14 @@ def _decode_grid_args(R, Lmax, max_steps, stop0, stop1, V, wte, wpe, wte_packed,
             _p(out_ids), _p(out_len), _p(step_ctr), _p(all_done), base + off, ws.numel() - off)
 
 
-def gpt2_decode_persist(*args, grid=48):
+def gpt2_decode_persist(*args, grid=48, exclusive=False):
     """The remaining greedy steps of one bs <= 64 batch in one persistent launch
-    (zs_gpt2_decode_persist) of `grid` 256-thread workgroups.  Arguments as
-    _decode_grid_args (layer_ptrs / kv_ptrs: ctypes arrays of 96 / 24 device pointers; the
-    weights in fragment order, Gpt2Weights.packed_layer_ptrs)."""
-    call("zs_gpt2_decode_persist", *_decode_grid_args(*args, grid), int(grid), _s())
+    (zs_gpt2_decode_persist) of `grid` 256-thread workgroups (`exclusive`: one per CU at most
+    among exclusive launches).  Arguments as _decode_grid_args (layer_ptrs / kv_ptrs: ctypes
+    arrays of 96 / 24 device pointers; the weights in fragment order,
+    Gpt2Weights.packed_layer_ptrs)."""
+    call("zs_gpt2_decode_persist", *_decode_grid_args(*args, grid), int(grid), int(bool(exclusive)),
+         _s())
 
 
 def gpt2_decode_phases(*args, steps=1, grid=96):

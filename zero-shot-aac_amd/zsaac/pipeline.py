@@ -242,8 +242,10 @@ def persist_grids(env: Optional[str] = None) -> List[int]:
     return grids
 
 
-# largest first; the last is the throughput grid every batch can fall back to
-DEFAULT_PERSIST_GRIDS = "192,96,48"
+# largest first; the last is the throughput grid every batch can fall back to (192 stays
+# available: alone it has the shortest step, but beside other grids 96 wins -- a 131-clip shard
+# 3.47k vs 2.42k clips/s, the headline equal)
+DEFAULT_PERSIST_GRIDS = "96,48"
 
 
 def persist_budget(cus: int) -> int:
@@ -292,6 +294,7 @@ class ConcurrentRunner:
         # every first-round begin -- the begins run on the whole chip instead of beside the grids
         self.begin_first = bool(begin_first) and self.persist
         self.late_grid = True     # grid size chosen when the begin has finished (False: at begin)
+        self.spread = False       # A/B: exclusive (one CU per workgroup) grids while CUs allow
         if self.persist and not self.begin_first:
             # persistent decode grids must be co-resident: at most budget // (smallest grid)
             n_inflight = max(1, min(n_inflight, self.budget // self.grids[-1]))
@@ -346,10 +349,22 @@ class ConcurrentRunner:
         for s in self.streams:           # inputs were produced on the caller's stream
             s.wait_stream(caller)
         ahead = None
-        if inputs == "wav" and self.enc is not None:
+        if inputs == "wav" and self.enc is not None and len(batches) > len(self.pipes):
+            # (a run that fits its pipelines at once begins sooner encoding per batch: measured
+            # on a 131-clip shard, 37.5 vs 40 ms)
             ahead = self._encode_ahead(batches, caller)
         if self.begin_first:
             return self._run_staged(batches, keep, inputs, caller, ahead)
+        # a run that fits its pipelines at once (a small shard) has no later begins to leave room
+        # for: its grids may fill the chip, and they take one CU per workgroup (exclusive
+        # launches) while the CUs allow -- left to itself the dispatcher doubles workgroups up on
+        # CUs while others idle (tools/placement.py: 3 grids of 96 covered 185 CUs, 103 twice)
+        small = self.persist and len(batches) <= len(self.pipes)
+        exclusive = False
+        spread = self.spread or small
+        budget = 2 * self.cus if small else self.budget
+        excl_slots = {}
+        excl_in_flight = lambda: sum(excl_slots.values())
         active = {}
         nxt = 0
         self.decode_steps = [0] * len(batches)     # per batch: decode steps actually enqueued
@@ -368,9 +383,10 @@ class ConcurrentRunner:
                         # the batches not yet launched: bigger grids once few batches remain)
                         if self.persist and not self.late_grid:    # (A/B: size at begin)
                             g = choose_persist_grid(sum(slots.values()), len(batches) - nxt,
-                                                    self.grids, self.budget)
+                                                    self.grids, budget)
                             self.grid[nxt] = slots[i] = g
                             p.decoder.persist_grid = g
+                            p.decoder.persist_exclusive = exclusive
                         p.decoder.defer_launch = self.persist and self.late_grid
                         try:
                             self._begin(i, nxt, batches, inputs, ahead)
@@ -395,9 +411,14 @@ class ConcurrentRunner:
                     unlaunched = len(batches) - nxt + sum(1 for a in active.values()
                                                           if a[0] == "begun")
                     g = choose_persist_grid(sum(slots.values()), unlaunched, self.grids,
-                                            self.budget)
+                                            budget)
+                    # spread (A/B option): while the exclusive workgroups in flight leave room,
+                    # a grid takes one CU per workgroup (it shares CUs with normal grids only)
+                    excl = exclusive or (spread and excl_in_flight() + g <= self.cus)
                     p.decoder.persist_grid = g
+                    p.decoder.persist_exclusive = excl
                     slots[i] = g
+                    excl_slots[i] = g if excl else 0
                     self.grid[bi] = g
                     with torch.cuda.stream(s):
                         p.decoder.launch_pending()
@@ -418,6 +439,7 @@ class ConcurrentRunner:
                         p.decoder.step_chunk(None)
                         ev, flag = p.decoder.finished_async()
                     slots.pop(i, None)
+                    excl_slots.pop(i, None)
                     active[i] = (bi, 1, ev, flag)
                     continue
                 if int(flag[0]) or n >= p.decoder.n_chunks:
@@ -430,6 +452,7 @@ class ConcurrentRunner:
                             keep(results[bi])
                     del active[i]
                     slots.pop(i, None)
+                    excl_slots.pop(i, None)
                 else:
                     with torch.cuda.stream(s):
                         p.decoder.step_chunk(int(flag[2]))
