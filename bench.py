@@ -242,9 +242,18 @@ def run_streams(device, n):
     a later runner's batches on shared queues (serialized)."""
     from zsaac import ops
     have = _STREAMS.setdefault(str(device), [])
-    if len(have) < n:
-        have += ops.dedicated_streams(n - len(have), device)
+    if len(have) < n:        # the pipelines' streams at high priority (the encoder's is low)
+        have += ops.dedicated_streams(n - len(have), device, priority=-1)
     return have[:n]
+
+
+def enc_stream(device):
+    """The low-priority stream the caption runs' encoder twin runs ahead on (one per process)."""
+    from zsaac import ops
+    key = "enc:" + str(device)
+    if key not in _STREAMS:
+        _STREAMS[key] = ops.dedicated_streams(1, device, priority=1)[0]
+    return _STREAMS[key]
 
 
 def run_captions(args, world, rank, device, pipe, n_local, first, counts, inflight, warmup,
@@ -264,9 +273,9 @@ def run_captions(args, world, rank, device, pipe, n_local, first, counts, inflig
     if getattr(args, "beam", 0) or ahead < B:      # beam runs / larger batches: encoder per batch
         ahead = 0
     runner = ConcurrentRunner(pipe, max(1, inflight),
-                              streams=run_streams(device, max(1, inflight) + (1 if ahead else 0)),
+                              streams=run_streams(device, max(1, inflight)),
                               budget=getattr(args, "persist_budget", 0) or None,
-                              encode_ahead=ahead)
+                              encode_ahead=ahead, enc_stream=enc_stream(device) if ahead else None)
     for size in sorted({b.shape[0] for b in batches}, reverse=True):   # captures every graph
         runner.warmup(next(b for b in batches if b.shape[0] == size))
         log(f"captured the decode graphs of {size}-clip batches")

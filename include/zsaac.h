@@ -38,8 +38,9 @@ int zs_tune_set(const char* key, int value);  /* tuning knobs, e.g. "skinny_mode
 /* zs_stream_create: a new non-blocking HIP stream, bound to its hardware queue at once (ROCclr
  * assigns queues round-robin at a stream's first dispatch), so streams created back to back run
  * on distinct hardware queues while GPU_MAX_HW_QUEUES allows.  Used for the concurrent batch
- * streams (two streams sharing a hardware queue serialize). */
-int zs_stream_create(void** stream);
+ * streams (two streams sharing a hardware queue serialize).  priority < 0: the device's highest
+ * stream priority, > 0: its lowest, 0: the default. */
+int zs_stream_create(void** stream, int priority);
 int zs_stream_destroy(void* stream);
 
 /* ------------------------------------------------------------------ audio front end

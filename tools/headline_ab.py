@@ -3,8 +3,10 @@
 decode) repeated for several arms, interleaved, so box-to-box and run-to-run spread cancel.
 
 An arm is "name:inflight:knob=v,knob=v[:grids[:budget[:encode_ahead]]]" (zs_tune_set knobs, reset
-(knob late=0: the runner sizes each grid at its batch's begin instead of at its launch; spread=1:
-exclusive one-CU-per-workgroup grids while the CUs allow)
+(runner options among the knobs: late=0 sizes each grid at its batch's begin instead of at its
+launch; spread=1: exclusive one-CU-per-workgroup grids while the CUs allow; prio=0: default stream
+priorities instead of high for the pipelines and low for the encoder; extra=k: k pipelines beyond
+the grids the budget holds)
 to the baseline values given with --base between arms; grids: the persistent-decode grid sizes the
 runner may use, zsaac.pipeline.persist_grids, e.g. "48" or "96-48" ('-'-separated); budget:
 workgroup slots of the in-flight grids; encode_ahead: clips per up-front encoder pass, 0 = each
@@ -58,11 +60,19 @@ def main():
     base = knobs(a.base)
     arms = []
     from zsaac import ops
-    # one set of dedicated streams for every arm (distinct hardware queues)
-    streams = ops.dedicated_streams(max(int(x.split(":")[1]) for x in a.arms) + 1, dev)
+    # one set of dedicated streams per priority for every arm (distinct hardware queues): the
+    # pipelines' (prio=1 arms: high priority) and the encoder's (prio=1: low priority)
+    nmax = max(int(x.split(":")[1]) for x in a.arms) + 4
+    sets = {1: (ops.dedicated_streams(nmax, dev, priority=-1),
+                ops.dedicated_streams(1, dev, priority=1)[0])}
+    if any("prio=0" in x for x in a.arms):
+        sets[0] = (ops.dedicated_streams(nmax, dev), ops.dedicated_streams(1, dev)[0])
     for spec in a.arms:
         name, inflight, kn, *sh = spec.split(":")
-        r = ConcurrentRunner(pipe, int(inflight), streams=streams,
+        kn = knobs(kn)
+        streams, enc_stream = sets[kn.pop("prio", 1)]
+        r = ConcurrentRunner(pipe, int(inflight), streams=streams, enc_stream=enc_stream,
+                             extra_pipes=kn.pop("extra", 0),
                              grids=persist_grids(sh[0].replace("-", ",")) if sh and sh[0] else None,
                              budget=int(sh[1]) if len(sh) > 1 and sh[1] else None,
                              encode_ahead=int(sh[2].rstrip("f")) if len(sh) > 2 and sh[2] else 0,
@@ -70,7 +80,6 @@ def main():
                              begin_first=len(sh) > 3 and sh[3] == "bf")
         for size in sorted({b.shape[0] for b in batches}, reverse=True):
             r.warmup(next(b for b in batches if b.shape[0] == size))
-        kn = knobs(kn)
         r.late_grid = bool(kn.pop("late", 1))      # runner options, not zs_tune_set knobs
         r.spread = bool(kn.pop("spread", 0))
         arms.append((name, r, kn))
@@ -90,6 +99,9 @@ def main():
                 res[name].append(a.clips / dt)
         if rep:
             print(f"rep {rep}: " + "  ".join(f"{n} {res[n][-1]:.0f}" for n in res), flush=True)
+            for name, r, _ in arms:
+                if getattr(r, "trace", None):
+                    print(name, "host trace (ms):", r.trace, flush=True)
     for n, v in res.items():
         print(f"{n:12s} median {statistics.median(v):8.1f} clips/s  min {min(v):8.1f}  max {max(v):8.1f}")
 

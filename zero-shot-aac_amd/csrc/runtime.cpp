@@ -45,12 +45,20 @@ extern "C" int zs_device_arch(char* buf, size_t len) {
 // stay idle while other code creates and uses streams can end up sharing one queue — and two
 // streams on one queue run strictly one after the other.  One 4-byte fill + sync right after
 // creation makes streams created back to back take consecutive queues.
-extern "C" int zs_stream_create(void** stream) {
+// priority < 0: the device's highest stream priority, > 0: its lowest, 0: the default (the caption
+// runner puts the pipelines' begins and decode grids above the encoder that runs ahead).
+extern "C" int zs_stream_create(void** stream, int priority) {
   if (!stream) return ZS_ERR_ARG;
   static int* scratch = nullptr;
   if (!scratch) ZS_CHECK_HIP(hipMalloc(&scratch, 256));
   hipStream_t s = nullptr;
-  ZS_CHECK_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  if (priority == 0) {
+    ZS_CHECK_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  } else {
+    int least = 0, greatest = 0;
+    ZS_CHECK_HIP(hipDeviceGetStreamPriorityRange(&least, &greatest));
+    ZS_CHECK_HIP(hipStreamCreateWithPriority(&s, hipStreamNonBlocking, priority < 0 ? greatest : least));
+  }
   ZS_CHECK_HIP(hipMemsetAsync(scratch, 0, 4, s));
   ZS_CHECK_HIP(hipStreamSynchronize(s));
   *stream = (void*)s;

@@ -332,16 +332,17 @@ def label_topk(emb, labels, k, rows, idx=None):
     return rows
 
 
-def dedicated_streams(n: int, device) -> list:
+def dedicated_streams(n: int, device, priority: int = 0) -> list:
     """n new HIP streams bound to distinct hardware queues (zs_stream_create), as torch streams.
     torch's pooled streams get their hardware queue at first use, so concurrent batch streams
-    can silently land on one queue and serialize."""
+    can silently land on one queue and serialize.  priority < 0: the highest stream priority,
+    > 0: the lowest."""
     import ctypes as C
     out = []
     with torch.cuda.device(device):
         for _ in range(n):
             h = C.c_void_p()
-            call("zs_stream_create", C.byref(h))
+            call("zs_stream_create", C.byref(h), int(priority))
             out.append(torch.cuda.ExternalStream(h.value, device=device))
     return out
 

@@ -282,7 +282,8 @@ class ConcurrentRunner:
 
     def __init__(self, pipe: CaptionPipeline, n_inflight: int = 2, streams: Optional[list] = None,
                  grids: Optional[List[int]] = None, budget: Optional[int] = None,
-                 encode_ahead: int = 0, encode_first: bool = False, begin_first: bool = False):
+                 encode_ahead: int = 0, encode_first: bool = False, begin_first: bool = False,
+                 extra_pipes: int = 0, enc_stream=None):
         self.cus = torch.cuda.get_device_properties(pipe.dev).multi_processor_count
         # persistent grids (greedy bf16 at <= 64 rows; beam search never launches one), one size
         # per batch from `grids` (largest first, see choose_persist_grid)
@@ -299,7 +300,10 @@ class ConcurrentRunner:
             # persistent decode grids must be co-resident: at most budget // (smallest grid)
             n_inflight = max(1, min(n_inflight, self.budget // self.grids[-1]))
         self.n_inflight = n_inflight
-        self.pipes = [pipe] + [pipe.twin() for _ in range(n_inflight - 1)]
+        # extra_pipes: pipelines beyond the grids the budget holds, so the next batches' begins
+        # (prefill etc.) run while every grid slot decodes and launch the moment one frees
+        n_pipes = n_inflight + (max(0, int(extra_pipes)) if self.persist else 0)
+        self.pipes = [pipe] + [pipe.twin() for _ in range(n_pipes - 1)]
         # encode_ahead > 0 (waveform inputs): one encoder twin sized for that many clips encodes
         # every batch's clips up front, in passes of up to encode_ahead clips (consecutive
         # batches), on a stream of its own; a batch's begin (mapper .. step 0) waits only for its
@@ -310,15 +314,19 @@ class ConcurrentRunner:
         self.encode_ahead = int(encode_ahead) if pipe.encoder is not None else 0
         self.encode_first = bool(encode_first)
         self.enc = pipe.encoder.twin(max_batch=self.encode_ahead) if self.encode_ahead else None
-        need = len(self.pipes) + (1 if self.enc is not None else 0)
         # dedicated streams on distinct hardware queues: pooled torch streams take their queue at
         # first use and can end up sharing one, which serializes the batches
         # (``streams``: reuse another runner's, at least as many -- tools/headline_ab.py)
+        need = len(self.pipes)
         streams = (list(streams[:need]) if streams is not None
-                   else ops.dedicated_streams(need, pipe.dev))
+                   else ops.dedicated_streams(need, pipe.dev, priority=-1))
         assert len(streams) == need, "ConcurrentRunner: too few streams given"
-        self.streams = streams[:len(self.pipes)]
-        self.enc_stream = streams[len(self.pipes)] if self.enc is not None else None
+        self.streams = streams
+        # the encoder running ahead yields to the begins and grids: a low-priority stream
+        self.enc_stream = None
+        if self.enc is not None:
+            self.enc_stream = (enc_stream if enc_stream is not None
+                               else ops.dedicated_streams(1, pipe.dev, priority=1)[0])
 
     def warmup(self, wav: torch.Tensor):
         """Runs one batch per pipeline synchronously (captures every decode graph)."""
@@ -367,6 +375,8 @@ class ConcurrentRunner:
         excl_in_flight = lambda: sum(excl_slots.values())
         active = {}
         nxt = 0
+        trace = self.trace = [] if os.environ.get("ZSAAC_RUNNER_TRACE") else None
+        t_run = time.perf_counter()
         self.decode_steps = [0] * len(batches)     # per batch: decode steps actually enqueued
         self.assign = []                           # (pipeline index, batch index), in begin order
         self.grid = [0] * len(batches)             # persistent grid size per batch (0: none)
@@ -374,6 +384,8 @@ class ConcurrentRunner:
         slots = {}                                 # pipeline index -> its launch's workgroups
         while nxt < len(batches) or active:
             progressed = False
+            if ahead is not None:
+                ahead.pump()
             for i, (p, s) in enumerate(zip(self.pipes, self.streams)):
                 st = active.get(i)
                 if st is None:
@@ -401,6 +413,8 @@ class ConcurrentRunner:
                                 ev, flag = p.decoder.finished_async()
                                 active[i] = (nxt, 0, ev, flag)
                         self.assign.append((i, nxt))
+                        if trace is not None:
+                            trace.append(("begin", nxt, round((time.perf_counter() - t_run) * 1e3, 2)))
                         nxt += 1
                         progressed = True
                     continue
@@ -412,6 +426,8 @@ class ConcurrentRunner:
                                                           if a[0] == "begun")
                     g = choose_persist_grid(sum(slots.values()), unlaunched, self.grids,
                                             budget)
+                    if sum(slots.values()) + g > budget:
+                        continue               # (extra pipelines: wait for a grid to finish)
                     # spread (A/B option): while the exclusive workgroups in flight leave room,
                     # a grid takes one CU per workgroup (it shares CUs with normal grids only)
                     excl = exclusive or (spread and excl_in_flight() + g <= self.cus)
@@ -424,6 +440,8 @@ class ConcurrentRunner:
                         p.decoder.launch_pending()
                         ev, flag = p.decoder.finished_async()
                     active[i] = (bi, 0, ev, flag)
+                    if trace is not None:
+                        trace.append(("launch", bi, round((time.perf_counter() - t_run) * 1e3, 2)))
                     progressed = True
                     continue
                 bi, n, ev, flag = st
@@ -470,9 +488,8 @@ class ConcurrentRunner:
         p, s = self.pipes[i], self.streams[i]
         with torch.cuda.stream(s):
             if ahead is not None:
-                embs, evs = ahead
-                s.wait_event(evs[bi])
-                p.begin_emb(embs[bi])
+                s.wait_event(ahead.ready(bi))
+                p.begin_emb(ahead.embs[bi])
             else:
                 (p.begin_wav if inputs == "wav" else p.begin_emb)(batches[bi])
 
@@ -563,35 +580,55 @@ class ConcurrentRunner:
         return results
 
     def _encode_ahead(self, batches, caller):
-        """Enqueues the encoder passes of every batch on the encoder stream: consecutive batches
-        grouped up to encode_ahead clips (one view when they are adjacent rows of one tensor, as
-        the bench's are, else concatenated).  Returns (per-batch embedding views, per-batch
-        event of the pass that produced them)."""
-        E, enc, es = self.encode_ahead, self.enc, self.enc_stream
+        """The encoder passes of every batch on the encoder stream: consecutive batches grouped
+        up to encode_ahead clips (one view when they are adjacent rows of one tensor, as the
+        bench's are, else concatenated), enqueued one pass at a time (_EncodeAhead.pump): a pass
+        queued far ahead would hold the GPU ahead of the begins issued after it."""
+        return _EncodeAhead(self, batches, caller)
+
+
+class _EncodeAhead:
+    def __init__(self, runner, batches, caller):
+        E = runner.encode_ahead
+        self.enc, self.es, self.batches = runner.enc, runner.enc_stream, batches
         n = sum(int(b.shape[0]) for b in batches)
-        emb = torch.empty(n, 1024, device=self.pipes[0].dev)
-        es.wait_stream(caller)
-        embs, evs = [], []
+        self.emb = torch.empty(n, 1024, device=runner.pipes[0].dev)
+        self.es.wait_stream(caller)
+        self.passes, self.pass_of, self.embs = [], [], []
         i, c0 = 0, 0
-        with torch.cuda.stream(es):
-            while i < len(batches):
-                j, m = i, 0
-                while j < len(batches) and m + int(batches[j].shape[0]) <= E:
-                    m += int(batches[j].shape[0])
-                    j += 1
-                assert j > i, f"a batch of {batches[i].shape[0]} clips > encode_ahead {E}"
-                wav = _rows_span(batches[i:j])
-                emb[c0:c0 + m].copy_(enc.encode(wav))
+        while i < len(batches):
+            j, m = i, 0
+            while j < len(batches) and m + int(batches[j].shape[0]) <= E:
+                m += int(batches[j].shape[0])
+                j += 1
+            assert j > i, f"a batch of {batches[i].shape[0]} clips > encode_ahead {E}"
+            self.passes.append((i, j, c0, m))
+            for b in batches[i:j]:
+                self.pass_of.append(len(self.passes) - 1)
+                self.embs.append(self.emb[c0:c0 + int(b.shape[0])])
+                c0 += int(b.shape[0])
+            i = j
+        self.events = []
+        self.first = runner.encode_first
+        self.pump(force=1)
+
+    def pump(self, force=0):
+        """Enqueues the next pass when none is in flight (or until `force` passes are)."""
+        while len(self.events) < len(self.passes):
+            if len(self.events) >= force and self.events and not self.events[-1].query():
+                return
+            i, j, c0, m = self.passes[len(self.events)]
+            with torch.cuda.stream(self.es):
+                self.emb[c0:c0 + m].copy_(self.enc.encode(_rows_span(self.batches[i:j])))
                 ev = torch.cuda.Event()
-                ev.record(es)
-                for b in batches[i:j]:
-                    embs.append(emb[c0:c0 + int(b.shape[0])])
-                    evs.append(ev)
-                    c0 += int(b.shape[0])
-                i = j
-        if self.encode_first:
-            evs = [evs[-1]] * len(evs)
-        return embs, evs
+                ev.record(self.es)
+            self.events.append(ev)
+
+    def ready(self, b):
+        """The event batch b's begin waits for (its pass enqueued first if needed)."""
+        k = len(self.passes) - 1 if self.first else self.pass_of[b]
+        self.pump(force=k + 1)
+        return self.events[k]
 
 
 def _rows_span(ts: Sequence[torch.Tensor]) -> torch.Tensor:
