@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Cross-check of bench.py's roofline against a rocprofv3 kernel trace of the same command: the
-dg_persist_kernel launches grouped into runs of the caption region (launches overlapping in time,
-separated by idle gaps), the average duration of every 17-launch run, and bench's own
+dg_persist_kernel launches grouped into runs of the caption region (launches less than 20 ms
+after the previous one's end; the regions are separated by their encode + begins), the average duration of every 17-launch run, and bench's own
 roofline.avg_launch_us (its last run before the single-stream extras is the untimed log pass the
 roofline is measured on).
 
@@ -24,8 +24,9 @@ def main(d, bench_json, out):
                                  r["Kernel_Name"].split("(")[0]))
     rows.sort()
     runs, cur, end = [], [], 0
-    for r in rows:
-        if cur and r[0] > end:          # nothing in flight: a new run
+    gap_ns = 20e6                       # a run: launches closer than 20 ms to the last one's end
+    for r in rows:                      # (the waves of one region are closer; regions are not)
+        if cur and r[0] > end + gap_ns:
             runs.append(cur)
             cur = []
         cur.append(r)
