@@ -498,6 +498,7 @@ def persist_launch_bytes(w_step, plen, steps, kv_row=12 * 2 * 768 * 2):
 
 
 PMC_PERSIST_FILE = os.path.join(ROOT, "profiles", "r5", "pmc_persist_g48.json")
+F32_INFLIGHT = 4
 
 
 def grid_counts(runner):
@@ -1321,7 +1322,9 @@ def main():
         log("C3 beam 5")
         res["c3_beam5"] = c3_beam5(args, device)
         log("f32 parity mode")
-        res["f32_parity_mode"] = sub_run(args, device, torch.float32, 1, args.inflight,
+        # 4 batches in flight: the f32 decode saturates there (tools/f32_profile.py: 3 / 4 / 6 /
+        # 10 in flight 1.40k / 1.41k / 1.39k / 1.26k clips/s)
+        res["f32_parity_mode"] = sub_run(args, device, torch.float32, 1, F32_INFLIGHT,
                                          CLOTHO_EVAL_CLIPS, 1)
         res["f32_parity_mode"]["note"] = ("the headline's 1045 clips at bs=64 in f32: the mode "
                                           "whose greedy ids are bit-exact")
