@@ -275,7 +275,8 @@ def run_captions(args, world, rank, device, pipe, n_local, first, counts, inflig
     runner = ConcurrentRunner(pipe, max(1, inflight),
                               streams=run_streams(device, max(1, inflight)),
                               budget=getattr(args, "persist_budget", 0) or None,
-                              encode_ahead=ahead, enc_stream=enc_stream(device) if ahead else None)
+                              encode_ahead=ahead, enc_stream=enc_stream(device) if ahead else None,
+                              extra_pipes=getattr(args, "extra_pipes", 0))
     for size in sorted({b.shape[0] for b in batches}, reverse=True):   # captures every graph
         runner.warmup(next(b for b in batches if b.shape[0] == size))
         log(f"captured the decode graphs of {size}-clip batches")

@@ -516,6 +516,31 @@ int zs_gpt2_decode_phases(int R, int Lmax, int max_steps, int stop0, int stop1, 
                           int* next_tok, int* done, int* out_ids, int* out_len, int* step_ctr,
                           int* all_done, void* ws, long ws_bytes, int steps, int grid,
                           void* stream);
+/* zs_gpt2_decode_persist_f32 / zs_gpt2_decode_phases_f32: the same decode in f32 (the parity
+ * mode; replaces the same generate2 loop, gpt2_prefix_eval.py:161-222, in fp32): wte / wpe f32
+ * [V][768] / [1024][768]; layer_w 12 x 8 pointers in the same order, each W f32 in 16-k fragment
+ * order [N/16][K/16][64][4] (block j, k-step s, lane l = W[16 j + l % 16][16 s + 4 (l / 16) .. + 4]),
+ * c_attn's / c_fc's with the LayerNorm's weight folded in (W diag(g), f32) and biases f32 [N]
+ * (b + W beta); wte_packed f32 g o wte[v] (ln_f's weight) in that order [ceil(V/16)][48][64][4];
+ * lm_bias f32 [ceil(V/16) 16] (beta . wte[v]); kv f32 [R][12][Lmax][64]; ws of
+ * zs_decode_persist_f32_workspace_bytes().  The LayerNorms are two-pass (mean, then squared
+ * deviations) and normalise rows in registers before exact-f32 MFMAs (v_mfma_f32_16x16x4_f32);
+ * grid 192 only.  The persistent and phase forms give identical ids, as the bf16 pair. */
+int zs_decode_persist_f32_workspace_bytes(void);
+int zs_gpt2_decode_persist_f32(int R, int Lmax, int max_steps, int stop0, int stop1, int V,
+                               const void* wte, const void* wpe, const void* wte_packed,
+                               float temperature, const void* const* layer_w,
+                               const float* lm_bias, void* const* kv, int* pos,
+                               int* next_tok, int* done, int* out_ids, int* out_len, int* step_ctr,
+                               int* all_done, void* ws, long ws_bytes, int grid, int exclusive,
+                               void* stream);
+int zs_gpt2_decode_phases_f32(int R, int Lmax, int max_steps, int stop0, int stop1, int V,
+                              const void* wte, const void* wpe, const void* wte_packed,
+                              float temperature, const void* const* layer_w,
+                              const float* lm_bias, void* const* kv, int* pos,
+                              int* next_tok, int* done, int* out_ids, int* out_len, int* step_ctr,
+                              int* all_done, void* ws, long ws_bytes, int steps, int grid,
+                              void* stream);
 int zs_decode_persist_status(const void* ws, int* timed_out);
 /* zs_decode_persist_set_stamps: diagnostic phase timing (tools/persist_stamps.py): with buf !=
  * NULL ([grid][128] u64), thread 0 of every workgroup of later launches writes s_memrealtime

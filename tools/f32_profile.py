@@ -1,8 +1,11 @@
 #!/usr/bin/env python3
-"""The bench's f32 parity-mode line alone (1045 clips, bs 64, 10 batches in flight) -- run it under
-rocprofv3 --kernel-trace --stats to see where the f32 mode's time goes.
+"""The bench's f32 parity-mode line alone (1045 clips, bs 64) -- run it under rocprofv3
+--kernel-trace --stats to see where the f32 mode's time goes; or sweep configurations:
 
-    python tools/f32_profile.py [clips=1045] [inflight=10]
+    python tools/f32_profile.py [clips=1045] [inflight=4] [budget=0] [extra=0] [grid=1] [ahead=256]
+
+grid 0: the round-4 f32 row-kernel decode (ZSAAC_GRID_DECODE_F32=0) instead of the f32 grid decode;
+budget / extra: the runner's persistent budget (0 = default) and extra pipelines.
 """
 import json
 import os
@@ -20,13 +23,20 @@ os.environ["GPU_MAX_HW_QUEUES"] = "16"
 
 
 def main():
-    n = int(sys.argv[1]) if len(sys.argv) > 1 else 1045
-    k = int(sys.argv[2]) if len(sys.argv) > 2 else 10
+    v = [int(x) for x in sys.argv[1:]] + [None] * 6
+    n, k = v[0] or 1045, v[1] or 4
+    budget, extra = v[2] or 0, v[3] or 0
+    grid = 1 if v[4] is None else v[4]
+    ahead = 256 if v[5] is None else v[5]
+    os.environ["ZSAAC_GRID_DECODE_F32"] = str(grid)
     args = SimpleNamespace(dtype="f32", group=1, encoder="htsat", mapper="mlp", batch=64,
-                           encoder_batch=0, beam=0, entry_length=67, compact=1, persist_budget=0,
-                           encode_ahead=256)
+                           encoder_batch=0, beam=0, entry_length=67, compact=1,
+                           persist_budget=budget, encode_ahead=ahead, extra_pipes=extra)
     res = bench.sub_run(args, torch.device("cuda", 0), torch.float32, 1, k, n, 1)
-    print(json.dumps({"value": res["value"], "ms_per_step": res["ms_per_step"]}), flush=True)
+    print(json.dumps({"inflight": k, "budget": budget, "extra": extra, "grid_decode_f32": grid,
+                      "encode_ahead": ahead, "value": res["value"], "ms_per_step": res["ms_per_step"],
+                      "runner": {kk: res["config"].get(kk) for kk in ("persist_grids", "persist_gave_up", "batches_in_flight")}}),
+          flush=True)
 
 
 if __name__ == "__main__":

@@ -930,7 +930,8 @@ __device__ __forceinline__ void phase_f(const Args& a, const Rs& rs, int w, cons
 }
 
 // ------------------------------------------------------------------ row state
-__device__ __forceinline__ void load_state(const Args& a, const Sm& sm) {
+template <typename A>
+__device__ __forceinline__ void load_state(const A& a, const Sm& sm) {
   const int tid = otid();
   if (tid < RM) {
     const bool in = tid < a.R;
@@ -942,7 +943,8 @@ __device__ __forceinline__ void load_state(const Args& a, const Sm& sm) {
 // generate2's bookkeeping of step `step` from the argmax keys (greedy_step_kernel, gpt2.hip):
 // every workgroup updates its LDS copy; `commit`: also ids and the state in memory.  Returns the
 // rows still decoding (in sm.misc[0] after the caller's barrier).
-__device__ __forceinline__ void bookkeep(const Args& a, const Sm& sm, gu64* keys, int step, bool commit) {
+template <typename A>
+__device__ __forceinline__ void bookkeep(const A& a, const Sm& sm, gu64* keys, int step, bool commit) {
   const int tid = otid();
   int alive = 0;
   if (tid < RM) {
@@ -973,7 +975,8 @@ __device__ __forceinline__ void bookkeep(const Args& a, const Sm& sm, gu64* keys
 }
 
 // a workgroup that gave up waiting (grid not co-resident): all_done = {1, -1} tells the host
-__device__ __forceinline__ void gave_up(const Args& a) {
+template <typename A>
+__device__ __forceinline__ void gave_up(const A& a) {
   if (threadIdx.x == 0) {
     __hip_atomic_store(&a.all_done[1], -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_store(&a.all_done[0], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1045,7 +1048,10 @@ __global__ __launch_bounds__(NT, 2) void dg_persist_kernel(Args a) {
       if (!bar_wait(bar, s_ok)) return gave_up(a);
       phase_e<G, false>(a, rs, l, w, sm, wm, xo);
       bar_arrive(bar, w);
+      // (the last layer's branch overwrites wq too: otherwise the merge keeps A's operands live
+      // through B .. E of every layer)
       if (l + 1 < NLY) ldw<Gm::APF, QS>(a.wq[l + 1], KSD, acb0, QS * V_, wq);
+      else for (int i = 0; i < Gm::APF * QS; ++i) wq[i] = u32x4_t{0u, 0u, 0u, 0u};
       if (!bar_wait(bar, s_ok)) return gave_up(a);
     }
     phase_f<G>(a, rs, w, sm, keys + (step & 1) * RM);
@@ -1107,7 +1113,8 @@ __global__ __launch_bounds__(NT, 2) void dg_phase_kernel(Args a) {
   }
 }
 // the step's bookkeeping (phase launches): one workgroup of 64 threads; zeroes the keys
-__global__ __launch_bounds__(64) void dg_book_kernel(Args a) {
+template <typename A>
+__global__ __launch_bounds__(64) void dg_book_kernel(A a) {
   __shared__ __attribute__((aligned(16))) char smem[SM_TOTAL];
   const Sm sm(smem);
   if (a.all_done[0]) return;
@@ -1126,6 +1133,613 @@ __global__ __launch_bounds__(64) void dg_book_kernel(Args a) {
     if (total == 0 || step + 1 >= a.max_steps) a.all_done[0] = 1;
   }
 }
+
+// ================================================================== f32 parity mode
+// The same grid decode in f32 (zs_gpt2_decode_persist_f32 / _phases_f32): f32 weights, f32
+// activations, KV cache and hand-offs, exact f32 products (v_mfma_f32_16x16x4_f32: bitwise an fmaf
+// chain), two-pass LayerNorms (mean, then the squared deviations) whose affine is folded into the
+// consuming GEMM in f32 (W' = W diag(g), b' = b + W beta, the host's f64 sums rounded once; ln_f's
+// into the tied LM head plus a per-token bias) -- the normalised row feeds the MFMAs directly.
+// A 16-byte lane fragment holds 4 f32 of one row (k-steps of 16: lane l holds k = 16 s + 4 (l / 16)
+// .. + 4 of row / column l % 16), so one fragment feeds four MFMAs and a wave's K quarter is 12
+// fragments (K = 768) or 48 (K = 3072): twice the bf16 registers, so one geometry, G = 192.  The
+// canonical-arithmetic rules of the bf16 kernel hold here too (K quarters, (p0 + p1) + (p2 + p3),
+// 32-key softmax steps), so the persistent and the phase launches give identical ids.
+namespace f32 {
+constexpr int KSD = D / 16, KSF = DFF / 16;      // 16-k fragments of K = 768 / 3072
+constexpr int QS = KSD / NW, QF = KSF / NW;      // per wave quarter: 12 / 48
+constexpr int G = 192;
+// tiles per workgroup: A 3 column blocks x 1 row block (c_attn: 144 blocks / 3 = 48 column groups
+// x 4 row groups), C / E 1 x 1 (48 x 4), D 2 x 2 (96 x 2); F one row half (2 row blocks) over the
+// vocab blocks w / 2 + 96 i
+constexpr int ACB = 3, ARB = 1, DCB = 2, DRB = 2, ECB = 1, ERB = 1;
+constexpr int APF = 3;          // c_attn column blocks prefetched across the barrier (the rest: in A)
+constexpr int UPG = RM * NH / G, KC = 4;   // attention: UPG / 4 = 1 unit per wave
+constexpr int FH = G / 2;                        // LM-head workgroups per row half
+
+constexpr int WS_Q = WS_SYNC_BYTES;              // f32 [64][768]
+constexpr int WS_ATT = WS_Q + RM * D * 4;        // f32 [4][48][64][4] (fragment order)
+constexpr int WS_XB = WS_ATT + RM * D * 4;       // f32 [4][48][64][4]: the residual stream x
+constexpr int WS_HID = WS_XB + RM * D * 4;       // f32 [4][192][64][4]
+constexpr int WS_BYTES = WS_HID + RM * DFF * 4;
+constexpr int SM_TOTAL32 = SM_TOTAL;
+
+struct Args {
+  int R, Lmax, max_steps, stop0, stop1, V, layer, abort_step;
+  unsigned spin_max;
+  int kv_bytes;
+  float temp;
+  const float* wte; const float* wpe;
+  // per block, weights in f32 fragment order [N/16][K/16][64][4] (ops.pack_f32_fragments), the
+  // LayerNorm-fed ones with the affine folded in
+  const float* wq[NLY]; const float* bq[NLY];
+  const float* wo[NLY]; const float* bo[NLY];
+  const float* wf[NLY]; const float* bfc[NLY];
+  const float* wm[NLY]; const float* bm[NLY];
+  const float* wtep;                             // the tied LM head (g o wte), fragment order
+  const float* lmb;                              // beta . wte[v], [ceil(V/16) 16]
+  float* kc[NLY]; float* vc[NLY];
+  int* pos; int* next_tok; int* done; int* out_ids; int* out_len; int* step_ctr; int* all_done;
+  char* ws;
+};
+
+struct Rs {
+  __amdgpu_buffer_rsrc_t q, att, xb, hid;
+};
+__device__ __forceinline__ Rs make_rs(char* ws) {
+  return Rs{mk(ws + WS_Q, RM * D * 4), mk(ws + WS_ATT, RM * D * 4), mk(ws + WS_XB, RM * D * 4),
+            mk(ws + WS_HID, RM * DFF * 4)};
+}
+
+// 4 chained MFMAs over a fragment pair: the MFMA's k index g stands for k + 4 g + j in MFMA j
+__device__ __forceinline__ f32x4_t mfma4(const u32x4_t& w, const u32x4_t& a, f32x4_t c) {
+  c = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(w.x), __uint_as_float(a.x), c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(w.y), __uint_as_float(a.y), c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(w.z), __uint_as_float(a.z), c, 0, 0, 0);
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(w.w), __uint_as_float(a.w), c, 0, 0, 0);
+}
+// Fragment loads as buffer loads: one VGPR offset (the lane's and the wave's part) and the
+// fragment's compile-time part in the scalar offset, so a batch of loads costs no address
+// registers (the f32 phases hold up to 60 fragments).  Weights: plain loads; hand-offs: sc1.
+template <int NB, int S>
+__device__ __forceinline__ void ldw(const float* Wp, int KS, int cb0, int s0, u32x4_t* w) {
+  const __amdgpu_buffer_rsrc_t r = mk(const_cast<float*>(Wp), 0x7ffffff0);
+  const int vo = ((cb0 * KS + s0) * 64 + (otid() & 63)) * 16;
+#pragma unroll
+  for (int nb = 0; nb < NB; ++nb)
+#pragma unroll
+    for (int s = 0; s < S; ++s) w[nb * S + s] = __builtin_amdgcn_raw_buffer_load_b128(r, vo, (nb * KS + s) * 1024, 0);
+}
+template <int NRB, int S>
+__device__ __forceinline__ void lda(__amdgpu_buffer_rsrc_t r, int KS, int rb0, int s0, u32x4_t* a) {
+  const int vo = ((rb0 * KS + s0) * 64 + (otid() & 63)) * 16;
+#pragma unroll
+  for (int rb = 0; rb < NRB; ++rb)
+#pragma unroll
+    for (int s = 0; s < S; ++s) a[rb * S + s] = __builtin_amdgcn_raw_buffer_load_b128(r, vo, (rb * KS + s) * 1024, 16);
+}
+// byte offset of the quad (row, col .. col + 3) (col % 4 == 0) in a fragment-order f32 activation
+__device__ __forceinline__ int frag_off(int row, int col, int KS) {
+  return (((row >> 4) * KS + (col >> 4)) * 64 + (row & 15) + 16 * ((col >> 2) & 3)) * 16;
+}
+__device__ __forceinline__ u32x4_t u4(const float4& f) {
+  return u32x4_t{__float_as_uint(f.x), __float_as_uint(f.y), __float_as_uint(f.z), __float_as_uint(f.w)};
+}
+__device__ __forceinline__ float4 f4(const u32x4_t& u) {
+  return make_float4(__uint_as_float(u.x), __uint_as_float(u.y), __uint_as_float(u.z), __uint_as_float(u.w));
+}
+__device__ __forceinline__ float4 add4(const float4& a, const float4& b) {
+  return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
+}
+
+// LayerNorm of row blocks rb0 .. rb0 + NRB held in registers (lane: row 16 rb + l % 16, this wave's
+// K quarter), in place: mean from the row's 4 lanes and the 4 waves' partials ((w0 + w1) + (w2 +
+// w3)), then the squared deviations the same way, rstd = rsqrt(var + 1e-5), y = (x - mean) rstd
+// (the affine is in the weights).  Two workgroup barriers.
+template <int NRB>
+__device__ __forceinline__ void ln_apply(u32x4_t* xf, const Sm& sm, int rb0) {
+  const int tid = otid(), v = tid >> 6, lane = tid & 63, fr = lane & 15;
+#pragma unroll
+  for (int rb = 0; rb < NRB; ++rb) {
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < QS; ++i) {
+      const float4 x = f4(xf[rb * QS + i]);
+      s += (x.x + x.y) + (x.z + x.w);
+    }
+    s = add32(add16(s));
+    if (lane < 16) sm.ln[v * RM + 16 * (rb0 + rb) + fr] = s;
+  }
+  lds_sync();
+#pragma unroll
+  for (int rb = 0; rb < NRB; ++rb) {
+    const int r = 16 * (rb0 + rb) + fr;
+    const float mean = ((sm.ln[r] + sm.ln[RM + r]) + (sm.ln[2 * RM + r] + sm.ln[3 * RM + r])) * (1.0f / D);
+    float q = 0.f;
+#pragma unroll
+    for (int i = 0; i < QS; ++i) {
+      const float4 x = f4(xf[rb * QS + i]);
+      const float4 d = make_float4(x.x - mean, x.y - mean, x.z - mean, x.w - mean);
+      q += (d.x * d.x + d.y * d.y) + (d.z * d.z + d.w * d.w);
+      xf[rb * QS + i] = u4(d);
+    }
+    q = add32(add16(q));
+    if (lane < 16) sm.ln[(NW + v) * RM + r] = q;
+  }
+  lds_sync();
+#pragma unroll
+  for (int rb = 0; rb < NRB; ++rb) {
+    const int r = 16 * (rb0 + rb) + fr;
+    const float* l2 = sm.ln + NW * RM;
+    const float var = ((l2[r] + l2[RM + r]) + (l2[2 * RM + r] + l2[3 * RM + r])) * (1.0f / D);
+    const float rstd = rsqrtf(var + 1e-5f);
+#pragma unroll
+    for (int i = 0; i < QS; ++i) {
+      const float4 d = f4(xf[rb * QS + i]);
+      xf[rb * QS + i] = u4(make_float4(d.x * rstd, d.y * rstd, d.z * rstd, d.w * rstd));
+    }
+  }
+}
+
+// layer 0's input rows: wte[tok] + wpe[pos] (f32)
+template <int NRB>
+__device__ __forceinline__ void embed_frags(const Args& a, const Sm& sm, int rb0, u32x4_t* xf) {
+  const int tid = otid(), v = tid >> 6, lane = tid & 63, fr = lane & 15, fk = 4 * (lane >> 4);
+#pragma unroll
+  for (int rb = 0; rb < NRB; ++rb) {
+    const int row = 16 * (rb0 + rb) + fr;
+    const float* te = a.wte + (long)sm.tok[row] * D + fk;
+    const float* pe = a.wpe + (long)sm.pos[row] * D + fk;
+#pragma unroll
+    for (int i = 0; i < QS; ++i)
+      xf[rb * QS + i] = u4(add4(*reinterpret_cast<const float4*>(te + 16 * (QS * v + i)),
+                                *reinterpret_cast<const float4*>(pe + 16 * (QS * v + i))));
+  }
+}
+__device__ __forceinline__ float4 embed_quad(const Args& a, const Sm& sm, int row, int col) {
+  return add4(*reinterpret_cast<const float4*>(a.wte + (long)sm.tok[row] * D + col),
+              *reinterpret_cast<const float4*>(a.wpe + (long)sm.pos[row] * D + col));
+}
+
+// one GEMM round: CB x RB tiles of this wave's K quarter, then the cross-wave sum
+template <int CB, int RB, typename Epi>
+__device__ __forceinline__ void gemm_tiles(const u32x4_t* xf, const u32x4_t* wr, const Sm& sm, Epi&& epi) {
+  f32x4_t acc[CB * RB];
+#pragma unroll
+  for (int t = 0; t < CB * RB; ++t) acc[t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int s = 0; s < QS; ++s)
+#pragma unroll
+    for (int c = 0; c < CB; ++c)
+#pragma unroll
+      for (int rb = 0; rb < RB; ++rb) acc[c * RB + rb] = mfma4(wr[c * QS + s], xf[rb * QS + s], acc[c * RB + rb]);
+  reduce_tiles<CB * RB>(sm.red, acc, epi);
+}
+// the bias quad of the tile wave v finalises (t = v; every phase here has <= 4 tiles)
+template <int CB, int RB>
+__device__ __forceinline__ float4 bias_quad(const float* b, int cb0) {
+  const int tid = otid(), v = tid >> 6, lane = tid & 63;
+  if (v >= CB * RB) return make_float4(0.f, 0.f, 0.f, 0.f);
+  return *reinterpret_cast<const float4*>(b + 16 * (cb0 + v / RB) + 4 * (lane >> 4));
+}
+
+// A: ln_1 + c_attn -> q (WS_Q, row-major), k / v into the KV cache at the row's position
+template <bool PM>
+__device__ __forceinline__ void phase_a(const Args& a, const Rs& rs, int l, int w, const Sm& sm, u32x4_t* wq) {
+  constexpr int CB = ACB, RB = ARB, NCG = NCB_Q / CB;
+  const int tid = otid(), v = tid >> 6, lane = tid & 63;
+  const int cb0 = (w % NCG) * CB, rb0 = (w / NCG) * RB;
+  u32x4_t xf[RB * QS];
+  if (l == 0) embed_frags<RB>(a, sm, rb0, xf);
+  else lda<RB, QS>(rs.xb, KSD, rb0, QS * v, xf);
+  if constexpr (PM) ldw<APF, QS>(a.wq[l], KSD, cb0, QS * v, wq);
+  u32x4_t wr[CB * QS];
+#pragma unroll
+  for (int i = 0; i < APF * QS; ++i) wr[i] = wq[i];
+  ldw<CB - APF, QS>(a.wq[l], KSD, cb0 + APF, QS * v, wr + APF * QS);
+  const float4 bq = bias_quad<CB, RB>(a.bq[l], cb0);
+  __builtin_amdgcn_sched_barrier(0);
+  ln_apply<RB>(xf, sm, rb0);
+  const __amdgpu_buffer_rsrc_t rk = mk(a.kc[l], a.kv_bytes), rv = mk(a.vc[l], a.kv_bytes);
+  gemm_tiles<CB, RB>(xf, wr, sm, [&](int, int t, f32x4_t s) {
+    const int row = 16 * (rb0 + t % RB) + (lane & 15), col = 16 * (cb0 + t / RB) + 4 * (lane >> 4);
+    if (row >= a.R) return;
+    const u32x4_t o = u4(make_float4(s[0] + bq.x, s[1] + bq.y, s[2] + bq.z, s[3] + bq.w));
+    if (col < D) {
+      st16(rs.q, (row * D + col) * 4, o);
+    } else {
+      const int j = col - D, kv = j >= D, jj = kv ? j - D : j;
+      st16(kv ? rv : rk, ((((row * NH + jj / HD) * a.Lmax) + sm.pos[row]) * HD + (jj % HD)) * 4, o);
+    }
+  });
+}
+
+// D: ln_2 + c_fc + gelu_new -> hid (fragment order)
+template <bool PM>
+__device__ __forceinline__ void phase_d(const Args& a, const Rs& rs, int l, int w, const Sm& sm, u32x4_t* wf) {
+  constexpr int CB = DCB, RB = DRB, NCG = NCB_F / CB;
+  const int tid = otid(), v = tid >> 6, lane = tid & 63;
+  const int cb0 = (w % NCG) * CB, rb0 = (w / NCG) * RB;
+  u32x4_t xf[RB * QS];
+  lda<RB, QS>(rs.xb, KSD, rb0, QS * v, xf);
+  if constexpr (PM) ldw<CB, QS>(a.wf[l], KSD, cb0, QS * v, wf);
+  const float4 bq = bias_quad<CB, RB>(a.bfc[l], cb0);
+  __builtin_amdgcn_sched_barrier(0);
+  ln_apply<RB>(xf, sm, rb0);
+  gemm_tiles<CB, RB>(xf, wf, sm, [&](int, int t, f32x4_t s) {
+    const int row = 16 * (rb0 + t % RB) + (lane & 15), col = 16 * (cb0 + t / RB) + 4 * (lane >> 4);
+    if (row >= a.R) return;
+    st16(rs.hid, frag_off(row, col, KSF),
+         u4(make_float4(act_apply(s[0] + bq.x, ACT_GELU_TANH), act_apply(s[1] + bq.y, ACT_GELU_TANH),
+                        act_apply(s[2] + bq.z, ACT_GELU_TANH), act_apply(s[3] + bq.w, ACT_GELU_TANH))));
+  });
+}
+
+// C / E: projection + residual; the C / E tile is one 16 x 16 block per workgroup, finalised by
+// wave 0, whose lanes hold the residual quad across the step (persistent) -- the phase launches
+// read it back from xb (the f32 stream itself: no separate copy)
+__device__ __forceinline__ void ce_tile(int w, int& row, int& col) {
+  constexpr int NCG = NCB_D / ECB;
+  const int lane = otid() & 63;
+  row = 16 * ((w / NCG) * ERB) + (lane & 15);
+  col = 16 * ((w % NCG) * ECB) + 4 * (lane >> 4);
+}
+template <bool PM>
+__device__ __forceinline__ void ce_operands(const Args& a, const Rs& rs, const Sm& sm, bool embed, int w,
+                                            const float* bias, const f32x4_t& xo, float4& b, float4& xold) {
+  const int v = otid() >> 6;
+  b = make_float4(0.f, 0.f, 0.f, 0.f);
+  xold = b;
+  if (v == 0) {
+    int row, col;
+    ce_tile(w, row, col);
+    b = *reinterpret_cast<const float4*>(bias + col);
+    if (embed) xold = embed_quad(a, sm, row, col);
+    else if constexpr (PM) xold = f4(ld16(rs.xb, frag_off(row, col, KSD)));
+    else xold = make_float4(xo[0], xo[1], xo[2], xo[3]);
+  }
+}
+__device__ __forceinline__ void ce_epilogue(const Args& a, const Rs& rs, int w, f32x4_t s, const float4& b,
+                                            const float4& xold, f32x4_t& xo) {
+  int row, col;
+  ce_tile(w, row, col);
+  const f32x4_t o{(s[0] + b.x) + xold.x, (s[1] + b.y) + xold.y, (s[2] + b.z) + xold.z, (s[3] + b.w) + xold.w};
+  xo = o;
+  if (row < a.R) st16(rs.xb, frag_off(row, col, KSD), u4(make_float4(o[0], o[1], o[2], o[3])));
+}
+template <bool PM>
+__device__ __forceinline__ void phase_c(const Args& a, const Rs& rs, int l, int w, const Sm& sm, u32x4_t* wo,
+                                        f32x4_t& xo) {
+  constexpr int NCG = NCB_D / ECB;
+  const int v = otid() >> 6;
+  const int cb0 = (w % NCG) * ECB, rb0 = (w / NCG) * ERB;
+  u32x4_t af[QS];
+  lda<1, QS>(rs.att, KSD, rb0, QS * v, af);
+  if constexpr (PM) ldw<1, QS>(a.wo[l], KSD, cb0, QS * v, wo);
+  float4 b, xold;
+  ce_operands<PM>(a, rs, sm, l == 0, w, a.bo[l], xo, b, xold);
+  __builtin_amdgcn_sched_barrier(0);
+  gemm_tiles<1, 1>(af, wo, sm, [&](int, int, f32x4_t s) { ce_epilogue(a, rs, w, s, b, xold, xo); });
+}
+// E: K = 3072, the quarter's 48 k-steps streamed in chunks of ECH, two in flight
+template <bool PM>
+__device__ __forceinline__ void phase_e(const Args& a, const Rs& rs, int l, int w, const Sm& sm, u32x4_t* wm,
+                                        f32x4_t& xo) {
+  constexpr int NCG = NCB_D / ECB, NCH = QF / ECH;
+  const int v = otid() >> 6;
+  const int cb0 = (w % NCG) * ECB, rb0 = (w / NCG) * ERB, s0 = QF * v;
+  if constexpr (PM) {
+    ldw<1, ECH>(a.wm[l], KSF, cb0, s0, wm);
+    ldw<1, ECH>(a.wm[l], KSF, cb0, s0 + ECH, wm + ECH);
+  }
+  u32x4_t af[2 * ECH];
+  lda<1, ECH>(rs.hid, KSF, rb0, s0, af);
+  lda<1, ECH>(rs.hid, KSF, rb0, s0 + ECH, af + ECH);
+  float4 b, xold;
+  ce_operands<PM>(a, rs, sm, false, w, a.bm[l], xo, b, xold);
+  __builtin_amdgcn_sched_barrier(0);
+  f32x4_t acc[1] = {f32x4_t{0.f, 0.f, 0.f, 0.f}};
+  static_for<NCH>([&](auto cc) {
+    constexpr int c = decltype(cc)::value, sl = c & 1;
+#pragma unroll
+    for (int s = 0; s < ECH; ++s) acc[0] = mfma4(wm[sl * ECH + s], af[sl * ECH + s], acc[0]);
+    if constexpr (c + 2 < NCH) {
+      ldw<1, ECH>(a.wm[l], KSF, cb0, s0 + ECH * (c + 2), wm + sl * ECH);
+      lda<1, ECH>(rs.hid, KSF, rb0, s0 + ECH * (c + 2), af + sl * ECH);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  });
+  reduce_tiles<1>(sm.red, acc, [&](int, int, f32x4_t s) { ce_epilogue(a, rs, w, s, b, xold, xo); });
+}
+
+// B: attention, unit u = (row u / 12, head u % 12), one per wave; 8 lanes per key (lane sub holds
+// dims 8 sub .. + 8: two 16-byte halves), 8 key groups, chunks of 32 keys, online softmax in f32
+// starting from the new key, as the bf16 phase_b
+__device__ __forceinline__ void attn_unit(const Args& a, const Sm& sm, int u, int& row, int& hh, int& p,
+                                          long& base) {
+  row = u / NH;
+  hh = u % NH;
+  const int rr = min(row, a.R - 1);
+  p = min(sm.pos[rr], a.Lmax - 1);
+  base = ((long)(rr * NH + hh) * a.Lmax) * HD + 8 * ((otid() & 63) & 7);
+}
+__device__ __forceinline__ void attn_load(const Args& a, int l, const Sm& sm, int ub, int cb,
+                                          u32x4_t (&kr)[KC][2], u32x4_t (&vr)[KC][2]) {
+  const int tid = otid(), v = tid >> 6, grp = (tid & 63) >> 3;
+  int row, hh, p;
+  long base;
+  attn_unit(a, sm, ub + v, row, hh, p, base);
+#pragma unroll
+  for (int i = 0; i < KC; ++i) {
+    const int jc = max(min(cb + 8 * i + grp, p - 1), 0);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      kr[i][h] = __builtin_nontemporal_load(reinterpret_cast<const u32x4_t*>(a.kc[l] + base + (long)jc * HD + 4 * h));
+      vr[i][h] = __builtin_nontemporal_load(reinterpret_cast<const u32x4_t*>(a.vc[l] + base + (long)jc * HD + 4 * h));
+    }
+  }
+}
+__device__ __forceinline__ void phase_b(const Args& a, const Rs& rs, int l, const Sm& sm, int ub,
+                                        u32x4_t (&kr)[KC][2], u32x4_t (&vr)[KC][2]) {
+  const int tid = otid(), lane = tid & 63, v = tid >> 6, grp = lane >> 3, sub = lane & 7;
+  const __amdgpu_buffer_rsrc_t rk = mk(a.kc[l], a.kv_bytes), rv = mk(a.vc[l], a.kv_bytes);
+  int row, hh, p;
+  long base;
+  attn_unit(a, sm, ub + v, row, hh, p, base);
+  u32x4_t qu[2], knu[2], vnu[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    qu[h] = ld16(rs.q, (min(row, a.R - 1) * D + hh * HD + 8 * sub + 4 * h) * 4);
+    const int off = (int)((base + (long)p * HD + 4 * h) * 4);
+    knu[h] = ld16(rk, off);
+    vnu[h] = ld16(rv, off);
+  }
+  __builtin_amdgcn_sched_barrier(0);
+  const float4 q0 = f4(qu[0]), q1 = f4(qu[1]);
+  auto qk = [&](const u32x4_t (&kv)[2]) {
+    const float4 k0 = f4(kv[0]), k1 = f4(kv[1]);
+    float sv = q0.x * k0.x;
+    sv = fmaf(q0.y, k0.y, sv); sv = fmaf(q0.z, k0.z, sv); sv = fmaf(q0.w, k0.w, sv);
+    sv = fmaf(q1.x, k1.x, sv); sv = fmaf(q1.y, k1.y, sv); sv = fmaf(q1.z, k1.z, sv); sv = fmaf(q1.w, k1.w, sv);
+    return sum8(sv) * 0.125f;
+  };
+  float m = qk(knu), sum = grp == 0 ? 1.f : 0.f;
+  f32x2_t o[4];
+  {
+    const float4 v0 = f4(vnu[0]), v1 = f4(vnu[1]);
+    const bool g0 = grp == 0;
+    o[0] = g0 ? f32x2_t{v0.x, v0.y} : f32x2_t{0.f, 0.f};
+    o[1] = g0 ? f32x2_t{v0.z, v0.w} : f32x2_t{0.f, 0.f};
+    o[2] = g0 ? f32x2_t{v1.x, v1.y} : f32x2_t{0.f, 0.f};
+    o[3] = g0 ? f32x2_t{v1.z, v1.w} : f32x2_t{0.f, 0.f};
+  }
+  for (int cb = 0; cb < p; cb += 8 * KC) {
+    if (cb > 0) attn_load(a, l, sm, ub, cb, kr, vr);
+    float sc[KC];
+    float pm = -INFINITY;
+#pragma unroll
+    for (int i = 0; i < KC; ++i) {
+      const float sv = qk(kr[i]);
+      sc[i] = cb + 8 * i + grp < p ? sv : -INFINITY;
+      pm = fmaxf(pm, sc[i]);
+    }
+    pm = fmaxf(pm, xor8(pm));
+    pm = max16(pm);
+    pm = max32(pm);
+    const float mn = fmaxf(m, pm);
+    const float scale = __expf(m - mn);
+    sum *= scale;
+    const f32x2_t sc2 = {scale, scale};
+#pragma unroll
+    for (int t = 0; t < 4; ++t) o[t] *= sc2;
+    m = mn;
+#pragma unroll
+    for (int i = 0; i < KC; ++i) {
+      const float e = __expf(sc[i] - mn);
+      sum += e;
+      const f32x2_t e2 = {e, e};
+      const float4 v0 = f4(vr[i][0]), v1 = f4(vr[i][1]);
+      o[0] = __builtin_elementwise_fma(e2, f32x2_t{v0.x, v0.y}, o[0]);
+      o[1] = __builtin_elementwise_fma(e2, f32x2_t{v0.z, v0.w}, o[1]);
+      o[2] = __builtin_elementwise_fma(e2, f32x2_t{v1.x, v1.y}, o[2]);
+      o[3] = __builtin_elementwise_fma(e2, f32x2_t{v1.z, v1.w}, o[3]);
+    }
+  }
+  const float inv = 1.0f / add32(add16(sum + xor8(sum)));
+  float of[8];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    of[2 * t] = add32(add16(o[t].x + xor8(o[t].x))) * inv;
+    of[2 * t + 1] = add32(add16(o[t].y + xor8(o[t].y))) * inv;
+  }
+  if (grp == 0 && row < a.R) {
+    const int c0 = hh * HD + 8 * sub;
+    st16(rs.att, frag_off(row, c0, KSD), u4(make_float4(of[0], of[1], of[2], of[3])));
+    st16(rs.att, frag_off(row, c0 + 4, KSD), u4(make_float4(of[4], of[5], of[6], of[7])));
+  }
+}
+
+// F: ln_f + LM head.  Workgroup w takes row half w % 2 (row blocks 2 (w % 2) .. + 2) and vocab
+// blocks w / 2 + 96 i; per block each wave multiplies its K quarter into the 32 rows, the 4 partial
+// tiles go through double-buffered slabs, waves 0 / 1 finalise row block 2 (w % 2) + v.  A ring of 2
+// blocks of weights per wave is in flight.
+__device__ __forceinline__ void phase_f(const Args& a, const Rs& rs, int w, const Sm& sm, gu64* keys) {
+  const int tid = otid(), v = tid >> 6, lane = tid & 63;
+  const int half = w & 1, wh = w >> 1, rb0 = 2 * half;
+  u32x4_t xf[2 * QS];
+  lda<2, QS>(rs.xb, KSD, rb0, QS * v, xf);
+  const int nvb = (a.V + 15) >> 4;
+  const int nb = (nvb - wh + FH - 1) / FH;
+  // ring of 2 block slots: this wave's 12 fragments of the block and the lane's 4 per-token biases
+  struct Slot {
+    u32x4_t w[QS];
+    float4 b;
+  };
+  Slot R0, R1;
+  auto fill = [&](int i, Slot& r) {
+    const int blk = wh + FH * min(i, nb - 1);
+    ldw<1, QS>(a.wtep, KSD, blk, QS * v, r.w);
+    r.b = *reinterpret_cast<const float4*>(a.lmb + 16 * blk + 4 * (lane >> 4));
+  };
+  fill(0, R0);
+  fill(1, R1);
+  __builtin_amdgcn_sched_barrier(0);
+  ln_apply<2>(xf, sm, rb0);
+  float bv = -INFINITY;
+  int bi = 0x7fffffff;
+  const bool tmp = a.temp != 1.0f;
+  int buf = 0;
+  auto consume = [&](int i, const Slot& r) {
+    f32x4_t acc[2] = {f32x4_t{0.f, 0.f, 0.f, 0.f}, f32x4_t{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+    for (int s = 0; s < QS; ++s)
+#pragma unroll
+      for (int rb = 0; rb < 2; ++rb) acc[rb] = mfma4(r.w[s], xf[rb * QS + s], acc[rb]);
+    f32x4_t* red = sm.red + buf * 512;
+#pragma unroll
+    for (int rb = 0; rb < 2; ++rb) red[(v * 2 + rb) * 64 + lane] = acc[rb];
+    lds_sync();
+    if (v < 2) {
+      const f32x4_t sum = (red[v * 64 + lane] + red[(2 + v) * 64 + lane]) +
+                          (red[(4 + v) * 64 + lane] + red[(6 + v) * 64 + lane]);
+      const int col0 = 16 * (wh + FH * i) + 4 * (lane >> 4);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float lg = sum[e] + (e == 0 ? r.b.x : e == 1 ? r.b.y : e == 2 ? r.b.z : r.b.w);
+        const float val = tmp ? lg / a.temp : lg;
+        if (col0 + e < a.V && val > bv) { bv = val; bi = col0 + e; }
+      }
+    }
+    buf ^= 1;
+  };
+#pragma nounroll
+  for (int i = 0; i < nb; i += 2) {
+    consume(i, R0);
+    fill(i + 2, R0);
+    if (i + 1 < nb) consume(i + 1, R1);     // (wave-uniform)
+    fill(i + 3, R1);
+  }
+  if (v < 2) {
+#pragma unroll
+    for (int o = 16; o < 64; o <<= 1) {
+      const float ov = __shfl_xor(bv, o, 64);
+      const int oi = __shfl_xor(bi, o, 64);
+      if (ov > bv || (ov == bv && oi < bi)) { bv = ov; bi = oi; }
+    }
+    if (lane < 16) {
+      const unsigned long long key = ((unsigned long long)f2key(bv) << 32) | (unsigned)(~bi);
+      __hip_atomic_fetch_max(keys + 16 * (rb0 + v) + lane, key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+__global__ __launch_bounds__(NT, 2) void dg32_persist_kernel(Args a) {
+  __shared__ __attribute__((aligned(16))) char smem[SM_TOTAL32];
+  const Sm sm(smem);
+  const int w = blockIdx.x;
+  if (a.all_done[0]) return;
+  int step = *a.step_ctr;
+  if (step >= a.max_steps) return;
+  load_state(a, sm);
+  __syncthreads();
+  const Rs rs = make_rs(a.ws);
+  Bar bar{(gu32*)(a.ws + WS_SH), (gu32*)(a.ws + WS_TMO), 0, G / NSH, a.spin_max, nullptr, 0};
+  gu64* const keys = (gu64*)(a.ws + WS_KEY);
+  volatile lds_int_t* s_ok = (volatile lds_int_t*)(sm.misc + 8);
+  const int ub = w * UPG;
+  constexpr int ANCG = NCB_Q / ACB, DNCG = NCB_F / DCB, ENCG = NCB_D / ECB;
+  const int acb0 = (w % ANCG) * ACB, dcb0 = (w % DNCG) * DCB, ecb0 = (w % ENCG) * ECB;
+#define V_ (otid() >> 6)
+  u32x4_t wq[APF * QS];
+  ldw<APF, QS>(a.wq[0], KSD, acb0, QS * V_, wq);
+  f32x4_t xo{0.f, 0.f, 0.f, 0.f};
+  for (;;) {
+    if (step == a.abort_step) return gave_up(a);
+    for (int l = 0; l < NLY; ++l) {
+      phase_a<false>(a, rs, l, w, sm, wq);
+      bar_arrive(bar, w);
+      u32x4_t kr[KC][2], vr[KC][2];
+      attn_load(a, l, sm, ub, 0, kr, vr);
+      if (!bar_wait(bar, s_ok)) return gave_up(a);
+      if (l == 0 && w == 0 && otid() < RM)
+        __hip_atomic_store(keys + ((step + 1) & 1) * RM + otid(), 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      phase_b(a, rs, l, sm, ub, kr, vr);
+      bar_arrive(bar, w);
+      u32x4_t wo[QS];
+      ldw<1, QS>(a.wo[l], KSD, ecb0, QS * V_, wo);
+      if (!bar_wait(bar, s_ok)) return gave_up(a);
+      phase_c<false>(a, rs, l, w, sm, wo, xo);
+      bar_arrive(bar, w);
+      u32x4_t wf[DCB * QS];
+      ldw<DCB, QS>(a.wf[l], KSD, dcb0, QS * V_, wf);
+      if (!bar_wait(bar, s_ok)) return gave_up(a);
+      phase_d<false>(a, rs, l, w, sm, wf);
+      bar_arrive(bar, w);
+      u32x4_t wm[2 * ECH];
+      ldw<1, ECH>(a.wm[l], KSF, ecb0, QF * V_, wm);
+      ldw<1, ECH>(a.wm[l], KSF, ecb0, QF * V_ + ECH, wm + ECH);
+      if (!bar_wait(bar, s_ok)) return gave_up(a);
+      phase_e<false>(a, rs, l, w, sm, wm, xo);
+      bar_arrive(bar, w);
+      // (the last layer's branch overwrites wq too: otherwise the merge keeps A's operands live
+      // through B .. E of every layer, and the register allocator spills them)
+      if (l + 1 < NLY) ldw<APF, QS>(a.wq[l + 1], KSD, acb0, QS * V_, wq);
+      else for (int i = 0; i < APF * QS; ++i) wq[i] = u32x4_t{0u, 0u, 0u, 0u};
+      if (!bar_wait(bar, s_ok)) return gave_up(a);
+    }
+    phase_f(a, rs, w, sm, keys + (step & 1) * RM);
+    bar_arrive(bar, w);
+    ldw<APF, QS>(a.wq[0], KSD, acb0, QS * V_, wq);
+    if (!bar_wait(bar, s_ok)) return gave_up(a);
+    bookkeep(a, sm, keys + (step & 1) * RM, step, w == 0);
+    __syncthreads();
+    const int total = sm.misc[0];
+    const bool fin = total == 0 || step + 1 >= a.max_steps;
+    if (w == 0 && otid() == 0) {
+      *a.step_ctr = step + 1;
+      a.all_done[2] = total;
+      if (fin) a.all_done[0] = 1;
+    }
+    if (fin) return;
+    ++step;
+    __syncthreads();
+  }
+#undef V_
+}
+
+template <int PH>
+__global__ __launch_bounds__(NT, 2) void dg32_phase_kernel(Args a) {
+  __shared__ __attribute__((aligned(16))) char smem[SM_TOTAL32];
+  const Sm sm(smem);
+  const int w = blockIdx.x, l = a.layer;
+  if (a.all_done[0]) return;
+  if (*a.step_ctr >= a.max_steps) return;
+  load_state(a, sm);
+  __syncthreads();
+  const Rs rs = make_rs(a.ws);
+  if constexpr (PH == PH_A) {
+    u32x4_t wq[APF * QS];
+    phase_a<true>(a, rs, l, w, sm, wq);
+  } else if constexpr (PH == PH_B) {
+    u32x4_t kr[KC][2], vr[KC][2];
+    attn_load(a, l, sm, w * UPG, 0, kr, vr);
+    phase_b(a, rs, l, sm, w * UPG, kr, vr);
+  } else if constexpr (PH == PH_C) {
+    u32x4_t wo[QS];
+    f32x4_t xo{0.f, 0.f, 0.f, 0.f};
+    phase_c<true>(a, rs, l, w, sm, wo, xo);
+  } else if constexpr (PH == PH_D) {
+    u32x4_t wf[DCB * QS];
+    phase_d<true>(a, rs, l, w, sm, wf);
+  } else if constexpr (PH == PH_E) {
+    u32x4_t wm[2 * ECH];
+    f32x4_t xo{0.f, 0.f, 0.f, 0.f};
+    phase_e<true>(a, rs, l, w, sm, wm, xo);
+  } else {
+    phase_f(a, rs, w, sm, (gu64*)(a.ws + WS_KEY));
+  }
+}
+}  // namespace f32
 
 }  // namespace dg
 }  // namespace zs
@@ -1231,7 +1845,7 @@ int dg_phase_step(dg::Args& a, hipStream_t st) {
   }
   a.layer = 0;
   hipLaunchKernelGGL((dg_phase_kernel<G, PH_F>), dim3(G), dim3(NT), 0, st, a);
-  hipLaunchKernelGGL(dg_book_kernel, dim3(1), dim3(64), 0, st, a);
+  hipLaunchKernelGGL(dg_book_kernel<Args>, dim3(1), dim3(64), 0, st, a);
   ZS_LAUNCH_CHECK();
   return 0;
 }
@@ -1274,5 +1888,115 @@ extern "C" int zs_decode_persist_status(const void* ws, int* timed_out) {
   unsigned t = 0;
   ZS_CHECK_HIP(hipMemcpy(&t, (const char*)ws + dg::WS_TMO, 4, hipMemcpyDeviceToHost));
   *timed_out = (int)t;
+  return 0;
+}
+
+// ------------------------------------------------------------------ f32 parity mode entry points
+namespace {
+int dg32_args(dg::f32::Args& a, int R, int Lmax, int max_steps, int stop0, int stop1, int V,
+              const void* wte, const void* wpe, const void* wte_packed, float temperature,
+              const void* const* layer_w, const float* lm_bias, void* const* kv, int* pos,
+              int* next_tok, int* done, int* out_ids, int* out_len, int* step_ctr, int* all_done,
+              void* ws, long ws_bytes, int grid) {
+  using namespace dg;
+  ZS_REQUIRE(grid == f32::G, "zs_gpt2_decode_f32: grid %d (got %d)", f32::G, grid);
+  ZS_REQUIRE(R >= 1 && R <= RM, "zs_gpt2_decode_f32: R in 1..%d (got %d)", RM, R);
+  ZS_REQUIRE(V >= 16 * f32::FH && V <= 1 << 24, "zs_gpt2_decode_f32: vocab %d", V);
+  ZS_REQUIRE(Lmax >= 2 && max_steps >= 1, "zs_gpt2_decode_f32: Lmax %d max_steps %d", Lmax, max_steps);
+  ZS_REQUIRE((long)R * NH * Lmax * HD * 4 < (1L << 31), "zs_gpt2_decode_f32: KV cache too large");
+  ZS_REQUIRE(ws && ws_bytes >= f32::WS_BYTES && ((uintptr_t)ws & 255) == 0,
+             "zs_gpt2_decode_f32: workspace of %d bytes, 256-byte aligned", f32::WS_BYTES);
+  ZS_REQUIRE(temperature > 0.f, "zs_gpt2_decode_f32: temperature %g (> 0)", temperature);
+  ZS_REQUIRE(wte && wpe && wte_packed && lm_bias && layer_w && kv && pos && next_tok && done &&
+             out_ids && out_len && step_ctr && all_done, "zs_gpt2_decode_f32: null pointer");
+  ZS_REQUIRE(((uintptr_t)wte & 15) == 0 && ((uintptr_t)wpe & 15) == 0 && ((uintptr_t)wte_packed & 15) == 0 &&
+             ((uintptr_t)lm_bias & 15) == 0,
+             "zs_gpt2_decode_f32: wte / wpe / wte_packed / lm_bias not 16-byte aligned");
+  a = f32::Args{};
+  a.R = R; a.Lmax = Lmax; a.max_steps = max_steps; a.stop0 = stop0; a.stop1 = stop1; a.V = V;
+  a.spin_max = g_dp_spin > 0 ? (unsigned)g_dp_spin : g_dp_spin < 0 ? 0u : SPIN_MAX;
+  a.abort_step = g_dp_abort;
+  a.kv_bytes = R * NH * Lmax * HD * 4;
+  a.temp = temperature;
+  a.wte = (const float*)wte; a.wpe = (const float*)wpe; a.wtep = (const float*)wte_packed;
+  a.lmb = lm_bias;
+  for (int l = 0; l < NLY; ++l) {
+    const void* const* p = layer_w + 8 * l;
+    for (int k = 0; k < 8; ++k)
+      ZS_REQUIRE(p[k] && ((uintptr_t)p[k] & 15) == 0,
+                 "zs_gpt2_decode_f32: layer %d pointer %d null or not 16-byte aligned", l, k);
+    a.wq[l] = (const float*)p[0]; a.bq[l] = (const float*)p[1];
+    a.wo[l] = (const float*)p[2]; a.bo[l] = (const float*)p[3];
+    a.wf[l] = (const float*)p[4]; a.bfc[l] = (const float*)p[5];
+    a.wm[l] = (const float*)p[6]; a.bm[l] = (const float*)p[7];
+    ZS_REQUIRE(kv[l] && kv[NLY + l] && ((uintptr_t)kv[l] & 127) == 0 && ((uintptr_t)kv[NLY + l] & 127) == 0,
+               "zs_gpt2_decode_f32: KV cache pointer of layer %d null or not 128-byte aligned", l);
+    a.kc[l] = (float*)kv[l];
+    a.vc[l] = (float*)kv[NLY + l];
+  }
+  a.pos = pos; a.next_tok = next_tok; a.done = done; a.out_ids = out_ids; a.out_len = out_len;
+  a.step_ctr = step_ctr; a.all_done = all_done; a.ws = (char*)ws;
+  return 0;
+}
+}  // namespace
+
+extern "C" int zs_decode_persist_f32_workspace_bytes(void) { return dg::f32::WS_BYTES; }
+
+extern "C" int zs_gpt2_decode_persist_f32(int R, int Lmax, int max_steps, int stop0, int stop1, int V,
+                                          const void* wte, const void* wpe, const void* wte_packed,
+                                          float temperature, const void* const* layer_w,
+                                          const float* lm_bias, void* const* kv, int* pos,
+                                          int* next_tok, int* done, int* out_ids, int* out_len,
+                                          int* step_ctr, int* all_done, void* ws, long ws_bytes,
+                                          int grid, int exclusive, void* stream) {
+  dg::f32::Args a;
+  const int rc = dg32_args(a, R, Lmax, max_steps, stop0, stop1, V, wte, wpe, wte_packed, temperature,
+                           layer_w, lm_bias, kv, pos, next_tok, done, out_ids, out_len, step_ctr,
+                           all_done, ws, ws_bytes, grid);
+  if (rc) return rc;
+  const size_t dyn = exclusive ? (size_t)(dg::EXCL_LDS - dg::f32::SM_TOTAL32) : 0;
+  static bool attr = false;
+  if (exclusive && !attr) {
+    ZS_CHECK_HIP(hipFuncSetAttribute((const void*)dg::f32::dg32_persist_kernel,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     dg::EXCL_LDS - dg::f32::SM_TOTAL32));
+    attr = true;
+  }
+  ZS_CHECK_HIP(hipMemsetAsync(ws, 0, dg::WS_SYNC_BYTES, S(stream)));
+  hipLaunchKernelGGL(dg::f32::dg32_persist_kernel, dim3(dg::f32::G), dim3(dg::NT), dyn, S(stream), a);
+  ZS_LAUNCH_CHECK();
+  return 0;
+}
+
+extern "C" int zs_gpt2_decode_phases_f32(int R, int Lmax, int max_steps, int stop0, int stop1, int V,
+                                         const void* wte, const void* wpe, const void* wte_packed,
+                                         float temperature, const void* const* layer_w,
+                                         const float* lm_bias, void* const* kv, int* pos,
+                                         int* next_tok, int* done, int* out_ids, int* out_len,
+                                         int* step_ctr, int* all_done, void* ws, long ws_bytes,
+                                         int steps, int grid, void* stream) {
+  using namespace dg;
+  f32::Args a;
+  const int rc = dg32_args(a, R, Lmax, max_steps, stop0, stop1, V, wte, wpe, wte_packed, temperature,
+                           layer_w, lm_bias, kv, pos, next_tok, done, out_ids, out_len, step_ctr,
+                           all_done, ws, ws_bytes, grid);
+  if (rc) return rc;
+  ZS_REQUIRE(steps >= 1, "zs_gpt2_decode_phases_f32: steps %d", steps);
+  const hipStream_t st = S(stream);
+  ZS_CHECK_HIP(hipMemsetAsync(ws, 0, WS_SYNC_BYTES, st));
+  for (int s = 0; s < steps; ++s) {
+    for (int l = 0; l < NLY; ++l) {
+      a.layer = l;
+      hipLaunchKernelGGL(f32::dg32_phase_kernel<PH_A>, dim3(f32::G), dim3(NT), 0, st, a);
+      hipLaunchKernelGGL(f32::dg32_phase_kernel<PH_B>, dim3(f32::G), dim3(NT), 0, st, a);
+      hipLaunchKernelGGL(f32::dg32_phase_kernel<PH_C>, dim3(f32::G), dim3(NT), 0, st, a);
+      hipLaunchKernelGGL(f32::dg32_phase_kernel<PH_D>, dim3(f32::G), dim3(NT), 0, st, a);
+      hipLaunchKernelGGL(f32::dg32_phase_kernel<PH_E>, dim3(f32::G), dim3(NT), 0, st, a);
+    }
+    a.layer = 0;
+    hipLaunchKernelGGL(f32::dg32_phase_kernel<PH_F>, dim3(f32::G), dim3(NT), 0, st, a);
+    hipLaunchKernelGGL(dg_book_kernel<f32::Args>, dim3(1), dim3(64), 0, st, a);
+    ZS_LAUNCH_CHECK();
+  }
   return 0;
 }

@@ -73,6 +73,9 @@ SIGNATURES = {
     "zs_decode_persist_workspace_bytes": [],
     "zs_gpt2_decode_persist": [I, I, I, I, I, I, P, P, P, F, P, P, P, P, P, P, P, P, P, P, P, L, I, I, P],
     "zs_gpt2_decode_phases": [I, I, I, I, I, I, P, P, P, F, P, P, P, P, P, P, P, P, P, P, P, L, I, I, P],
+    "zs_decode_persist_f32_workspace_bytes": [],
+    "zs_gpt2_decode_persist_f32": [I, I, I, I, I, I, P, P, P, F, P, P, P, P, P, P, P, P, P, P, P, L, I, I, P],
+    "zs_gpt2_decode_phases_f32": [I, I, I, I, I, I, P, P, P, F, P, P, P, P, P, P, P, P, P, P, P, L, I, I, P],
     "zs_decode_persist_status": [P, P],
     "zs_decode_persist_set_stamps": [P, I, P],
     "zs_beam_step": [P, P, P, I, I, I, I, I, I, P, I, P, P, P, P, P, P, P, I, P, P, P, P],

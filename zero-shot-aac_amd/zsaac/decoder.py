@@ -230,29 +230,59 @@ class Gpt2Weights:
     def packed_layer_ptrs(self):
         """The 12 x 8 device pointers zs_gpt2_decode_persist / _phases take: per block c_attn W,
         b, attn.c_proj W, b, c_fc W, b, mlp.c_proj W, b -- each W (bf16, LN affine folded) in MFMA
-        fragment order (ops.pack_b_fragments), packed once."""
+        fragment order (ops.pack_b_fragments), packed once.  f32 model: the same table for
+        zs_gpt2_decode_persist_f32 / _phases_f32 (_pack_f32)."""
         if self._layer_ptrs is None:
             import ctypes
-            assert self.folded, "the grid decode runs the bf16 (LN-folded) weights"
-            # the LayerNorm-fed GEMMs' biases as [2][N]: b' (beta folded), then the folded
-            # weight's column sums cs[n] = sum_k W'[n][k] (the epilogue's rstd (x W' - mean cs) + b')
-            self._packed = [{k: (ops.pack_b_fragments(ly[k]) if k.endswith("_w") else
-                                 torch.stack([ly[k], colsum(ly[k[:-2] + "_w"])])
-                                 if k in ("attn_b", "fc_b") else ly[k])
-                             for k in ("attn_w", "attn_b", "proj_w", "proj_b", "fc_w", "fc_b",
-                                       "mproj_w", "mproj_b")} for ly in self.layers]
+            if self.dtype == torch.float32:
+                self._pack_f32()
+            else:
+                assert self.folded, "the grid decode runs the bf16 (LN-folded) weights"
+                # the LayerNorm-fed GEMMs' biases as [2][N]: b' (beta folded), then the folded
+                # weight's column sums cs[n] = sum_k W'[n][k] (the epilogue's rstd (x W' - mean cs) + b')
+                self._packed = [{k: (ops.pack_b_fragments(ly[k]) if k.endswith("_w") else
+                                     torch.stack([ly[k], colsum(ly[k[:-2] + "_w"])])
+                                     if k in ("attn_b", "fc_b") else ly[k])
+                                 for k in ("attn_w", "attn_b", "proj_w", "proj_b", "fc_w", "fc_b",
+                                           "mproj_w", "mproj_b")} for ly in self.layers]
             keys = ("attn_w", "attn_b", "proj_w", "proj_b", "fc_w", "fc_b", "mproj_w", "mproj_b")
             self._layer_ptrs = (ctypes.c_void_p * (8 * NL))(
                 *[pl[k].data_ptr() for pl in self._packed for k in keys])
         return self._layer_ptrs
 
+    def _pack_f32(self):
+        """The f32 grid decode's tables (the parity mode): ln_1 / ln_2's affine folded into c_attn /
+        c_fc in f32 (W' = W diag(g), b' = b + W beta summed in f64), ln_f's into the tied LM head
+        (g o wte, per-token bias beta . wte[v]); every W in f32 fragment order
+        (ops.pack_f32_fragments)."""
+        def fold(W, b, ln):
+            g, beta = ln
+            return (ops.pack_f32_fragments(W * g[None, :]),
+                    (b.double() + W.double() @ beta.double()).float().contiguous())
+        self._packed = []
+        for ly in self.layers:
+            aw, ab = fold(ly["attn_w"], ly["attn_b"], ly["ln1"])
+            fw, fb = fold(ly["fc_w"], ly["fc_b"], ly["ln2"])
+            self._packed.append({"attn_w": aw, "attn_b": ab,
+                                 "proj_w": ops.pack_f32_fragments(ly["proj_w"]), "proj_b": ly["proj_b"],
+                                 "fc_w": fw, "fc_b": fb,
+                                 "mproj_w": ops.pack_f32_fragments(ly["mproj_w"]), "mproj_b": ly["mproj_b"]})
+        g, beta = self.lnf
+        self._wte_packed = ops.pack_f32_fragments(self.wte * g[None, :])
+        nvb = -(-self.V // 16)
+        lmb = torch.zeros(nvb * 16, device=self.wte.device)
+        lmb[:self.V] = (self.wte.double() @ beta.double()).float()
+        self._lm_bias = lmb
+
     def wte_packed(self):
-        """The tied LM head with ln_f's weight folded in, MFMA fragment order (bf16 only)."""
+        """The tied LM head with ln_f's weight folded in, MFMA fragment order (bf16, or f32 after
+        packed_layer_ptrs of an f32 model)."""
         assert self._wte_packed is not None, "the grid decode runs the bf16 (LN-folded) weights"
         return self._wte_packed
 
     def lm_bias(self):
-        """ln_f's bias through the tied LM head, beta . wte[v], f32 [ceil(V/16) 16]."""
+        """ln_f's bias through the tied LM head, beta . wte[v], f32 [ceil(V/16) 16] (bf16 model:
+        [2][ceil(V/16) 16], the folded head's column sums in row 1)."""
         assert self._lm_bias is not None, "the grid decode runs the bf16 (LN-folded) weights"
         return self._lm_bias
 
@@ -333,6 +363,10 @@ class Gpt2Decoder:
         # launches (zs_gpt2_decode_phases); ids and state are identical at every grid size
         self.grid_decode = (dt == torch.bfloat16 and w.folded and self.R <= 64
                             and os.environ.get("ZSAAC_GRID_DECODE", "1") != "0")   # 0: A/B only
+        # f32 parity mode: the same grid decode in f32 (zs_gpt2_decode_persist_f32, G = 192)
+        self.f32_grid = (dt == torch.float32 and self.R <= 64
+                         and os.environ.get("ZSAAC_GRID_DECODE_F32", "1") != "0")
+        self.grid_decode = self.grid_decode or self.f32_grid
         if persist is None:
             persist = os.environ.get("ZSAAC_PERSIST", "1") != "0"
         self.persist = bool(persist) and self.grid_decode
@@ -340,9 +374,12 @@ class Gpt2Decoder:
         # chosen per batch by pipeline.ConcurrentRunner (more when CUs are free)
         self.persist_grid = int(os.environ.get("ZSAAC_PERSIST_GRID", "48"))
         self.phase_grid = 96           # the phase launches' grid (any size gives the same ids)
+        if self.f32_grid:
+            self.persist_grid = self.phase_grid = ops.PERSIST_GRIDS_F32[0]
         if self.grid_decode:
             import ctypes
-            self.persist_ws = ops.decode_persist_workspace(dev)
+            self.persist_ws = (ops.decode_persist_f32_workspace(dev) if self.f32_grid
+                               else ops.decode_persist_workspace(dev))
             # the shared packed weights and pointer table, built now and synchronised: a twin
             # decoder launched on another stream must never read a half-written copy
             w.packed_layer_ptrs()
@@ -499,7 +536,8 @@ class Gpt2Decoder:
 
     def _greedy_step_body(self, R):
         if self.grid_decode:      # the persistent launch's computation, one launch per phase
-            ops.gpt2_decode_phases(*self._grid_args(R), steps=1, grid=self.phase_grid)
+            phases = ops.gpt2_decode_phases_f32 if self.f32_grid else ops.gpt2_decode_phases
+            phases(*self._grid_args(R), steps=1, grid=self.phase_grid)
             return
         self._decode_forward(R)
         ops.lmhead_topk(self.hf[:R], self.w.wte, 1, None, self.pval1, self.pidx1,
@@ -650,8 +688,8 @@ class Gpt2Decoder:
             ev.append((torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True),
                        id(self)))
             ev[-1][0].record()
-        ops.gpt2_decode_persist(*self._grid_args(R), grid=self.persist_grid,
-                                exclusive=self.persist_exclusive)
+        persist = ops.gpt2_decode_persist_f32 if self.f32_grid else ops.gpt2_decode_persist
+        persist(*self._grid_args(R), grid=self.persist_grid, exclusive=self.persist_exclusive)
         if ev is not None:
             ev[-1][1].record()
         self._persist_R = R

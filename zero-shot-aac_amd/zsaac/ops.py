@@ -506,19 +506,46 @@ def pack_b_fragments(W: torch.Tensor) -> torch.Tensor:
             .view(Np // 16, K // 32, 64, 8))
 
 
+def pack_f32_fragments(W: torch.Tensor) -> torch.Tensor:
+    """W [N][K] (f32, K % 16 == 0) -> the f32 grid decode's fragment order
+    [ceil(N/16)][K/16][64][4]: block j, k-step s, lane l holds W[16 j + l % 16][16 s + 4 (l // 16)
+    .. + 4] (v_mfma_f32_16x16x4_f32, four MFMAs per fragment); rows past N are zero."""
+    N, K = W.shape
+    _need(W.dtype == torch.float32 and K % 16 == 0, "pack_f32_fragments: f32, K % 16")
+    Np = -(-N // 16) * 16
+    Wp = torch.zeros(Np, K, dtype=W.dtype, device=W.device)
+    Wp[:N] = W
+    return (Wp.view(Np // 16, 16, K // 16, 4, 4).permute(0, 2, 3, 1, 4).contiguous()
+            .view(Np // 16, K // 16, 64, 4))
+
+
+def decode_persist_f32_workspace(device) -> torch.Tensor:
+    n = call("zs_decode_persist_f32_workspace_bytes")
+    return torch.zeros(n + 256, dtype=torch.uint8, device=device)
+
+
+PERSIST_GRIDS_F32 = (192,)
+
+
 def _decode_grid_args(R, Lmax, max_steps, stop0, stop1, V, wte, wpe, wte_packed, temperature,
                       layer_ptrs, lm_bias, kv_ptrs, pos, next_tok, done, out_ids, out_len,
-                      step_ctr, all_done, ws, grid):
+                      step_ctr, all_done, ws, grid, f32=False):
     _need(1 <= R <= 64, "gpt2 decode grid: 1 <= R <= 64")
-    _need(wte.dtype == torch.bfloat16 and wpe.dtype == torch.bfloat16, "gpt2 decode grid: bf16")
+    dt = torch.float32 if f32 else torch.bfloat16
+    _need(wte.dtype == dt and wpe.dtype == dt and wte_packed.dtype == dt,
+          f"gpt2 decode grid: {dt} wte / wpe / wte_packed")
     for t, n in ((pos, "pos"), (next_tok, "next_tok"), (done, "done"), (out_ids, "out_ids"),
                  (out_len, "out_len"), (step_ctr, "step_ctr"), (all_done, "all_done")):
         _i32(t, n)
     _need(out_ids.shape[-1] == max_steps, "gpt2 decode grid: out_ids [R, max_steps]")
-    _need(lm_bias.dtype == torch.float32 and lm_bias.numel() >= 2 * (-(-V // 16) * 16),
-          "gpt2 decode grid: lm_bias f32 [2][ceil(V/16) 16]")
+    nb = (1 if f32 else 2) * (-(-V // 16) * 16)
+    _need(lm_bias.dtype == torch.float32 and lm_bias.numel() >= nb,
+          f"gpt2 decode grid: lm_bias f32 [{nb}]")
     _need(temperature > 0, "gpt2 decode grid: temperature > 0")
-    decode_persist_grid(grid)
+    if f32:
+        _need(grid in PERSIST_GRIDS_F32, f"f32 decode grid {grid} (one of {PERSIST_GRIDS_F32})")
+    else:
+        decode_persist_grid(grid)
     base = ws.data_ptr()
     off = (-base) % 256
     return (R, Lmax, max_steps, stop0, stop1, V, _p(wte), _p(wpe), _p(wte_packed),
@@ -540,3 +567,17 @@ def gpt2_decode_phases(*args, steps=1, grid=96):
     """`steps` decode steps of the same computation as phase launches (zs_gpt2_decode_phases:
     bit-identical to the persistent launch at any grid; graph-capturable)."""
     call("zs_gpt2_decode_phases", *_decode_grid_args(*args, grid), int(steps), int(grid), _s())
+
+
+def gpt2_decode_persist_f32(*args, grid=192, exclusive=False):
+    """gpt2_decode_persist in f32 (zs_gpt2_decode_persist_f32: the parity mode; weights in f32
+    fragment order, Gpt2Weights.packed_layer_ptrs of an f32 model)."""
+    call("zs_gpt2_decode_persist_f32", *_decode_grid_args(*args, grid, f32=True), int(grid),
+         int(bool(exclusive)), _s())
+
+
+def gpt2_decode_phases_f32(*args, steps=1, grid=192):
+    """The f32 decode's phase launches (zs_gpt2_decode_phases_f32, bit-identical to the persistent
+    f32 launch)."""
+    call("zs_gpt2_decode_phases_f32", *_decode_grid_args(*args, grid, f32=True), int(steps),
+         int(grid), _s())

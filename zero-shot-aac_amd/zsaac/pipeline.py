@@ -288,7 +288,8 @@ class ConcurrentRunner:
         # persistent grids (greedy bf16 at <= 64 rows; beam search never launches one), one size
         # per batch from `grids` (largest first, see choose_persist_grid)
         self.persist = pipe.decoder.persist and not pipe.cfg.beam
-        self.grids = grids or persist_grids()
+        self.grids = grids or (list(ops.PERSIST_GRIDS_F32) if getattr(pipe.decoder, "f32_grid", False)
+                               else persist_grids())
         self.budget = budget or persist_budget(self.cus)
         # begin_first (persistent decode only): every pipeline begins its batch (prompt .. step 0)
         # at once, and the persistent launches follow as the budget frees, the first ones after
