@@ -272,11 +272,12 @@ def run_captions(args, world, rank, device, pipe, n_local, first, counts, inflig
     ahead = getattr(args, "encode_ahead", 0)
     if getattr(args, "beam", 0) or ahead < B:      # beam runs / larger batches: encoder per batch
         ahead = 0
+    extra = getattr(args, "extra_pipes", 0)
     runner = ConcurrentRunner(pipe, max(1, inflight),
-                              streams=run_streams(device, max(1, inflight)),
+                              streams=run_streams(device, max(1, inflight) + extra),
                               budget=getattr(args, "persist_budget", 0) or None,
                               encode_ahead=ahead, enc_stream=enc_stream(device) if ahead else None,
-                              extra_pipes=getattr(args, "extra_pipes", 0))
+                              extra_pipes=extra)
     for size in sorted({b.shape[0] for b in batches}, reverse=True):   # captures every graph
         runner.warmup(next(b for b in batches if b.shape[0] == size))
         log(f"captured the decode graphs of {size}-clip batches")

@@ -26,7 +26,7 @@ def main(d, out, first=8, n=17):
                 rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"],
                              r.get("Queue_Id") or r.get("Stream_Id") or ""))
     rows.sort()
-    per = [r for r in rows if "dg_persist_kernel" in r[2]]
+    per = [r for r in rows if "persist_kernel" in r[2]]
     timed = per[first:first + n] if first >= 0 else per[len(per) - n:]    # first < 0: the last n
     t0 = min(r[0] for r in timed)
     t1 = max(r[1] for r in timed)
@@ -50,7 +50,7 @@ def main(d, out, first=8, n=17):
                 gaps.append((b[0] - a[1]) / 1e6)
     other = {}
     for r in rows:
-        if r[0] >= t0 and r[1] <= t1 and "dg_persist_kernel" not in r[2]:
+        if r[0] >= t0 and r[1] <= t1 and "persist_kernel" not in r[2]:
             k = r[2].split("(")[0][:80]
             other[k] = other.get(k, 0) + (r[1] - r[0]) / 1e6
     top = dict(sorted(other.items(), key=lambda kv: -kv[1])[:15])
