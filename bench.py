@@ -338,11 +338,12 @@ def run_captions(args, world, rank, device, pipe, n_local, first, counts, inflig
     return dt, outs, runner, info
 
 
-def sub_run(args, device, dtype, group, inflight, n_clips, warmup, encoder_batch=None):
-    """A secondary single-GPU configuration (throughput mode / f32 mode): value + config."""
+def sub_run(args, device, dtype, group, inflight, n_clips, warmup, encoder_batch=None, reps=1):
+    """A secondary single-GPU configuration (throughput mode / f32 mode): value (the median of
+    `reps` timed repetitions) + config."""
     pipe, _, _ = build(args, device, dtype=dtype, group=group, encoder_batch=encoder_batch)
     dt, outs, runner, info = run_captions(args, 1, 0, device, pipe, n_clips, 10 ** 6, [n_clips],
-                                          inflight, warmup)
+                                          inflight, warmup, reps=reps)
     B = pipe.cfg.batch
     res = {"value": round(n_clips / dt, 2), "unit": "clips/s", "clips": n_clips,
            "ms_per_step": round(dt / math.ceil(n_clips / B) * 1e3, 3),
@@ -1324,10 +1325,10 @@ def main():
         log("C3 beam 5")
         res["c3_beam5"] = c3_beam5(args, device)
         log("f32 parity mode")
-        # 4 batches in flight: the f32 decode saturates there (tools/f32_profile.py: 3 / 4 / 6 /
-        # 10 in flight 1.40k / 1.41k / 1.39k / 1.26k clips/s)
+        # the f32 grid decode (G = 192): two grids co-resident, so 2 pipelines run (4 asked;
+        # tools/f32_profile.py, profiles/r5/f32_sweep.txt)
         res["f32_parity_mode"] = sub_run(args, device, torch.float32, 1, F32_INFLIGHT,
-                                         CLOTHO_EVAL_CLIPS, 1)
+                                         CLOTHO_EVAL_CLIPS, 1, reps=3)
         res["f32_parity_mode"]["note"] = ("the headline's 1045 clips at bs=64 in f32: the mode "
                                           "whose greedy ids are bit-exact")
         log("C5 Mistral-7B")
