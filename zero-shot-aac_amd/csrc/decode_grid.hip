@@ -1154,7 +1154,9 @@ constexpr int G = 192;
 // vocab blocks w / 2 + 96 i
 constexpr int ACB = 3, ARB = 1, DCB = 2, DRB = 2, ECB = 1, ERB = 1;
 constexpr int APF = 3;          // c_attn column blocks prefetched across the barrier (the rest: in A)
-constexpr int UPG = RM * NH / G, KC = 4;   // attention: UPG / 4 = 1 unit per wave
+constexpr int UPG = RM * NH / G, KC = 8;   // attention: UPG / 4 = 1 unit per wave; 8 KC keys loaded per
+                                           // chunk, the softmax stepping 32 at a time
+constexpr int ESL = 4;                     // E: chunks of ECH k-steps in flight
 constexpr int FH = G / 2;                        // LM-head workgroups per row half
 
 constexpr int WS_Q = WS_SYNC_BYTES;              // f32 [64][768]
@@ -1421,31 +1423,28 @@ __device__ __forceinline__ void phase_c(const Args& a, const Rs& rs, int l, int 
   __builtin_amdgcn_sched_barrier(0);
   gemm_tiles<1, 1>(af, wo, sm, [&](int, int, f32x4_t s) { ce_epilogue(a, rs, w, s, b, xold, xo); });
 }
-// E: K = 3072, the quarter's 48 k-steps streamed in chunks of ECH, two in flight
+// E: K = 3072, the quarter's 48 k-steps streamed in chunks of ECH, ESL in flight (wm: the first
+// ESL chunks' weights, prefetched across the barrier or loaded here (PM))
 template <bool PM>
 __device__ __forceinline__ void phase_e(const Args& a, const Rs& rs, int l, int w, const Sm& sm, u32x4_t* wm,
                                         f32x4_t& xo) {
   constexpr int NCG = NCB_D / ECB, NCH = QF / ECH;
   const int v = otid() >> 6;
   const int cb0 = (w % NCG) * ECB, rb0 = (w / NCG) * ERB, s0 = QF * v;
-  if constexpr (PM) {
-    ldw<1, ECH>(a.wm[l], KSF, cb0, s0, wm);
-    ldw<1, ECH>(a.wm[l], KSF, cb0, s0 + ECH, wm + ECH);
-  }
-  u32x4_t af[2 * ECH];
-  lda<1, ECH>(rs.hid, KSF, rb0, s0, af);
-  lda<1, ECH>(rs.hid, KSF, rb0, s0 + ECH, af + ECH);
+  if constexpr (PM) ldw<1, ESL * ECH>(a.wm[l], KSF, cb0, s0, wm);
+  u32x4_t af[ESL * ECH];
+  lda<1, ESL * ECH>(rs.hid, KSF, rb0, s0, af);
   float4 b, xold;
   ce_operands<PM>(a, rs, sm, false, w, a.bm[l], xo, b, xold);
   __builtin_amdgcn_sched_barrier(0);
   f32x4_t acc[1] = {f32x4_t{0.f, 0.f, 0.f, 0.f}};
   static_for<NCH>([&](auto cc) {
-    constexpr int c = decltype(cc)::value, sl = c & 1;
+    constexpr int c = decltype(cc)::value, sl = c % ESL;
 #pragma unroll
     for (int s = 0; s < ECH; ++s) acc[0] = mfma4(wm[sl * ECH + s], af[sl * ECH + s], acc[0]);
-    if constexpr (c + 2 < NCH) {
-      ldw<1, ECH>(a.wm[l], KSF, cb0, s0 + ECH * (c + 2), wm + sl * ECH);
-      lda<1, ECH>(rs.hid, KSF, rb0, s0 + ECH * (c + 2), af + sl * ECH);
+    if constexpr (c + ESL < NCH) {
+      ldw<1, ECH>(a.wm[l], KSF, cb0, s0 + ECH * (c + ESL), wm + sl * ECH);
+      lda<1, ECH>(rs.hid, KSF, rb0, s0 + ECH * (c + ESL), af + sl * ECH);
       __builtin_amdgcn_sched_barrier(0);
     }
   });
@@ -1513,36 +1512,42 @@ __device__ __forceinline__ void phase_b(const Args& a, const Rs& rs, int l, cons
     o[2] = g0 ? f32x2_t{v1.x, v1.y} : f32x2_t{0.f, 0.f};
     o[3] = g0 ? f32x2_t{v1.z, v1.w} : f32x2_t{0.f, 0.f};
   }
+  // loads in chunks of 8 KC keys; the online softmax steps 32 keys at a time
   for (int cb = 0; cb < p; cb += 8 * KC) {
     if (cb > 0) attn_load(a, l, sm, ub, cb, kr, vr);
-    float sc[KC];
-    float pm = -INFINITY;
 #pragma unroll
-    for (int i = 0; i < KC; ++i) {
-      const float sv = qk(kr[i]);
-      sc[i] = cb + 8 * i + grp < p ? sv : -INFINITY;
-      pm = fmaxf(pm, sc[i]);
-    }
-    pm = fmaxf(pm, xor8(pm));
-    pm = max16(pm);
-    pm = max32(pm);
-    const float mn = fmaxf(m, pm);
-    const float scale = __expf(m - mn);
-    sum *= scale;
-    const f32x2_t sc2 = {scale, scale};
+    for (int hq = 0; hq < KC / 4; ++hq) {
+      const int cs = cb + 32 * hq;
+      if (cs >= p) break;                          // wave-uniform
+      float sc[4];
+      float pm = -INFINITY;
 #pragma unroll
-    for (int t = 0; t < 4; ++t) o[t] *= sc2;
-    m = mn;
+      for (int i = 0; i < 4; ++i) {
+        const float sv = qk(kr[4 * hq + i]);
+        sc[i] = cs + 8 * i + grp < p ? sv : -INFINITY;
+        pm = fmaxf(pm, sc[i]);
+      }
+      pm = fmaxf(pm, xor8(pm));
+      pm = max16(pm);
+      pm = max32(pm);
+      const float mn = fmaxf(m, pm);
+      const float scale = __expf(m - mn);
+      sum *= scale;
+      const f32x2_t sc2 = {scale, scale};
 #pragma unroll
-    for (int i = 0; i < KC; ++i) {
-      const float e = __expf(sc[i] - mn);
-      sum += e;
-      const f32x2_t e2 = {e, e};
-      const float4 v0 = f4(vr[i][0]), v1 = f4(vr[i][1]);
-      o[0] = __builtin_elementwise_fma(e2, f32x2_t{v0.x, v0.y}, o[0]);
-      o[1] = __builtin_elementwise_fma(e2, f32x2_t{v0.z, v0.w}, o[1]);
-      o[2] = __builtin_elementwise_fma(e2, f32x2_t{v1.x, v1.y}, o[2]);
-      o[3] = __builtin_elementwise_fma(e2, f32x2_t{v1.z, v1.w}, o[3]);
+      for (int t = 0; t < 4; ++t) o[t] *= sc2;
+      m = mn;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float e = __expf(sc[i] - mn);
+        sum += e;
+        const f32x2_t e2 = {e, e};
+        const float4 v0 = f4(vr[4 * hq + i][0]), v1 = f4(vr[4 * hq + i][1]);
+        o[0] = __builtin_elementwise_fma(e2, f32x2_t{v0.x, v0.y}, o[0]);
+        o[1] = __builtin_elementwise_fma(e2, f32x2_t{v0.z, v0.w}, o[1]);
+        o[2] = __builtin_elementwise_fma(e2, f32x2_t{v1.x, v1.y}, o[2]);
+        o[3] = __builtin_elementwise_fma(e2, f32x2_t{v1.z, v1.w}, o[3]);
+      }
     }
   }
   const float inv = 1.0f / add32(add16(sum + xor8(sum)));
@@ -1675,9 +1680,8 @@ __global__ __launch_bounds__(NT, 2) void dg32_persist_kernel(Args a) {
       if (!bar_wait(bar, s_ok)) return gave_up(a);
       phase_d<false>(a, rs, l, w, sm, wf);
       bar_arrive(bar, w);
-      u32x4_t wm[2 * ECH];
-      ldw<1, ECH>(a.wm[l], KSF, ecb0, QF * V_, wm);
-      ldw<1, ECH>(a.wm[l], KSF, ecb0, QF * V_ + ECH, wm + ECH);
+      u32x4_t wm[ESL * ECH];
+      ldw<1, ESL * ECH>(a.wm[l], KSF, ecb0, QF * V_, wm);
       if (!bar_wait(bar, s_ok)) return gave_up(a);
       phase_e<false>(a, rs, l, w, sm, wm, xo);
       bar_arrive(bar, w);
@@ -1732,7 +1736,7 @@ __global__ __launch_bounds__(NT, 2) void dg32_phase_kernel(Args a) {
     u32x4_t wf[DCB * QS];
     phase_d<true>(a, rs, l, w, sm, wf);
   } else if constexpr (PH == PH_E) {
-    u32x4_t wm[2 * ECH];
+    u32x4_t wm[ESL * ECH];
     f32x4_t xo{0.f, 0.f, 0.f, 0.f};
     phase_e<true>(a, rs, l, w, sm, wm, xo);
   } else {
