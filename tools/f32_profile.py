@@ -32,9 +32,14 @@ def main():
     args = SimpleNamespace(dtype="f32", group=1, encoder="htsat", mapper="mlp", batch=64,
                            encoder_batch=0, beam=0, entry_length=67, compact=1,
                            persist_budget=budget, encode_ahead=ahead, extra_pipes=extra)
+    bench.ALL_PERSIST_LOGS.clear()
     res = bench.sub_run(args, torch.device("cuda", 0), torch.float32, 1, k, n, 1)
+    logs = bench.ALL_PERSIST_LOGS
+    launch_ms = [e0.elapsed_time(e1) for e0, e1, _ in logs]
     print(json.dumps({"inflight": k, "budget": budget, "extra": extra, "grid_decode_f32": grid,
                       "encode_ahead": ahead, "value": res["value"], "ms_per_step": res["ms_per_step"],
+                      "persist_launch_ms_mean": round(sum(launch_ms) / max(1, len(launch_ms)), 2),
+                      "persist_launches": len(launch_ms),
                       "runner": {kk: res["config"].get(kk) for kk in ("persist_grids", "persist_gave_up", "batches_in_flight")}}),
           flush=True)
 

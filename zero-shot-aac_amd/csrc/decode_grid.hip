@@ -82,14 +82,26 @@ constexpr int ECH = 4;                               // phase E: k-steps per str
 // weights prefetched across the barrier (all of them, or one round's).  The grid size changes
 // only these ownerships, never the arithmetic of an element.
 template <int G> struct Geo;
+// ESL: phase E's chunks in flight (tools/grid_bench.py, profiles/r5/esl_ab.txt: 3 / 3 / 4 vs 2 / 2 / 2
+// alone 428 / 304 / 252 vs 436 / 313 / 271 us per step, 10 x G48 equal, 5 x G96 +2 %; 4 at G48:
+// 484 us alone)
+#ifndef DG_ESL48
+#define DG_ESL48 3
+#endif
+#ifndef DG_ESL96
+#define DG_ESL96 3
+#endif
+#ifndef DG_ESL192
+#define DG_ESL192 4
+#endif
 template <> struct Geo<48> {
-  static constexpr int ACB = 3, ARB = 4, APF = 2, DCB = 4, DRB = 4, DPF = 2, ECB = 2, ERB = 2;
+  static constexpr int ACB = 3, ARB = 4, APF = 2, DCB = 4, DRB = 4, DPF = 2, ECB = 2, ERB = 2, ESL = DG_ESL48;
 };
 template <> struct Geo<96> {
-  static constexpr int ACB = 3, ARB = 2, APF = 3, DCB = 4, DRB = 2, DPF = 4, ECB = 2, ERB = 1;
+  static constexpr int ACB = 3, ARB = 2, APF = 3, DCB = 4, DRB = 2, DPF = 4, ECB = 2, ERB = 1, ESL = DG_ESL96;
 };
 template <> struct Geo<192> {
-  static constexpr int ACB = 3, ARB = 1, APF = 3, DCB = 2, DRB = 2, DPF = 2, ECB = 1, ERB = 1;
+  static constexpr int ACB = 3, ARB = 1, APF = 3, DCB = 2, DRB = 2, DPF = 2, ECB = 1, ERB = 1, ESL = DG_ESL192;
 };
 template <int G> struct Units {
   static constexpr int UPG = RM * NH / G;   // attention units per workgroup
@@ -660,22 +672,22 @@ __device__ __forceinline__ void phase_c(const Args& a, const Rs& rs, int l, int 
   reduce_tiles<T>(sm.red, acc, [&](int, int t, f32x4_t s) { ce_epilogue<G, PM>(a, rs, w, t, s, b, xold, xo); });
 }
 
-// E: mlp.c_proj + residual (K = 3072: the quarter's 24 k-steps streamed in chunks of ECH, two in
-// flight; wm holds the first two chunks' weights: prefetched, or loaded here (PM))
+// E: mlp.c_proj + residual (K = 3072: the quarter's 24 k-steps streamed in chunks of ECH, ESL in
+// flight; wm holds the first ESL chunks' weights: prefetched, or loaded here (PM))
 template <int G, bool PM>
 __device__ __forceinline__ void phase_e(const Args& a, const Rs& rs, int l, int w, const Sm& sm,
                                         u32x4_t* wm, f32x4_t& xo) {
   using Gm = Geo<G>;
-  constexpr int CB = Gm::ECB, RB = Gm::ERB, T = CB * RB, NCG = NCB_D / CB, NCH = QF / ECH;
+  constexpr int CB = Gm::ECB, RB = Gm::ERB, T = CB * RB, NCG = NCB_D / CB, NCH = QF / ECH, ESL = Gm::ESL;
   const int v = otid() >> 6;
   const int cb0 = (w % NCG) * CB, rb0 = (w / NCG) * RB, s0 = QF * v;
   if constexpr (PM) {
-    ldw<CB, ECH>(a.wm[l], KSF, cb0, s0, wm);
-    ldw<CB, ECH>(a.wm[l], KSF, cb0, s0 + ECH, wm + CB * ECH);
+#pragma unroll
+    for (int k = 0; k < ESL; ++k) ldw<CB, ECH>(a.wm[l], KSF, cb0, s0 + ECH * k, wm + k * CB * ECH);
   }
-  u32x4_t af[2 * RB * ECH];
-  lda<RB, ECH>(rs.hid, KSF, rb0, s0, af);
-  lda<RB, ECH>(rs.hid, KSF, rb0, s0 + ECH, af + RB * ECH);
+  u32x4_t af[ESL * RB * ECH];
+#pragma unroll
+  for (int k = 0; k < ESL; ++k) lda<RB, ECH>(rs.hid, KSF, rb0, s0 + ECH * k, af + k * RB * ECH);
   float4 b, xold;
   ce_operands<G, PM>(a, sm, false, w, a.bm[l], xo, b, xold);
   __builtin_amdgcn_sched_barrier(0);
@@ -683,7 +695,7 @@ __device__ __forceinline__ void phase_e(const Args& a, const Rs& rs, int l, int 
 #pragma unroll
   for (int t = 0; t < T; ++t) acc[t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
   static_for<NCH>([&](auto cc) {
-    constexpr int c = decltype(cc)::value, sl = c & 1;
+    constexpr int c = decltype(cc)::value, sl = c % ESL;
 #pragma unroll
     for (int s = 0; s < ECH; ++s)
 #pragma unroll
@@ -691,9 +703,9 @@ __device__ __forceinline__ void phase_e(const Args& a, const Rs& rs, int l, int 
 #pragma unroll
         for (int rb = 0; rb < RB; ++rb)
           acc[cb * RB + rb] = mfma(wm[(sl * CB + cb) * ECH + s], af[(sl * RB + rb) * ECH + s], acc[cb * RB + rb]);
-    if constexpr (c + 2 < NCH) {
-      ldw<CB, ECH>(a.wm[l], KSF, cb0, s0 + ECH * (c + 2), wm + sl * CB * ECH);
-      lda<RB, ECH>(rs.hid, KSF, rb0, s0 + ECH * (c + 2), af + sl * RB * ECH);
+    if constexpr (c + ESL < NCH) {
+      ldw<CB, ECH>(a.wm[l], KSF, cb0, s0 + ECH * (c + ESL), wm + sl * CB * ECH);
+      lda<RB, ECH>(rs.hid, KSF, rb0, s0 + ECH * (c + ESL), af + sl * RB * ECH);
       __builtin_amdgcn_sched_barrier(0);
     }
   });
@@ -1042,9 +1054,10 @@ __global__ __launch_bounds__(NT, 2) void dg_persist_kernel(Args a) {
       if (!bar_wait(bar, s_ok)) return gave_up(a);
       phase_d<G, false>(a, rs, l, w, sm, wf);
       bar_arrive(bar, w);
-      u32x4_t wm[2 * Gm::ECB * ECH];
-      ldw<Gm::ECB, ECH>(a.wm[l], KSF, ecb0, QF * V_, wm);
-      ldw<Gm::ECB, ECH>(a.wm[l], KSF, ecb0, QF * V_ + ECH, wm + Gm::ECB * ECH);
+      u32x4_t wm[Gm::ESL * Gm::ECB * ECH];
+#pragma unroll
+      for (int k = 0; k < Gm::ESL; ++k)
+        ldw<Gm::ECB, ECH>(a.wm[l], KSF, ecb0, QF * V_ + ECH * k, wm + k * Gm::ECB * ECH);
       if (!bar_wait(bar, s_ok)) return gave_up(a);
       phase_e<G, false>(a, rs, l, w, sm, wm, xo);
       bar_arrive(bar, w);
@@ -1105,7 +1118,7 @@ __global__ __launch_bounds__(NT, 2) void dg_phase_kernel(Args a) {
     u32x4_t wf[Gm::DPF * QS];
     phase_d<G, true>(a, rs, l, w, sm, wf);
   } else if constexpr (PH == PH_E) {
-    u32x4_t wm[2 * Gm::ECB * ECH];
+    u32x4_t wm[Gm::ESL * Gm::ECB * ECH];
     f32x4_t xo{0.f, 0.f, 0.f, 0.f};
     phase_e<G, true>(a, rs, l, w, sm, wm, xo);
   } else {
