@@ -94,14 +94,22 @@ template <int G> struct Geo;
 #ifndef DG_ESL192
 #define DG_ESL192 4
 #endif
+// FSL: phase F's vocab blocks in flight
+// (profiles/r5/fsl_ab.txt: 4 vs 3 slots, alone -1.5 to -2 %; 6 spills)
+#ifndef DG_FSL
+#define DG_FSL 4
+#endif
 template <> struct Geo<48> {
-  static constexpr int ACB = 3, ARB = 4, APF = 2, DCB = 4, DRB = 4, DPF = 2, ECB = 2, ERB = 2, ESL = DG_ESL48;
+  static constexpr int ACB = 3, ARB = 4, APF = 2, DCB = 4, DRB = 4, DPF = 2, ECB = 2, ERB = 2, ESL = DG_ESL48,
+                       FSL = DG_FSL;
 };
 template <> struct Geo<96> {
-  static constexpr int ACB = 3, ARB = 2, APF = 3, DCB = 4, DRB = 2, DPF = 4, ECB = 2, ERB = 1, ESL = DG_ESL96;
+  static constexpr int ACB = 3, ARB = 2, APF = 3, DCB = 4, DRB = 2, DPF = 4, ECB = 2, ERB = 1, ESL = DG_ESL96,
+                       FSL = DG_FSL;
 };
 template <> struct Geo<192> {
-  static constexpr int ACB = 3, ARB = 1, APF = 3, DCB = 2, DRB = 2, DPF = 2, ECB = 1, ERB = 1, ESL = DG_ESL192;
+  static constexpr int ACB = 3, ARB = 1, APF = 3, DCB = 2, DRB = 2, DPF = 2, ECB = 1, ERB = 1, ESL = DG_ESL192,
+                       FSL = DG_FSL;
 };
 template <int G> struct Units {
   static constexpr int UPG = RM * NH / G;   // attention units per workgroup
@@ -857,7 +865,7 @@ __device__ __forceinline__ void phase_b(const Args& a, const Rs& rs, int l, cons
 // Vocab blocks of 16 b = w, w + G, ..; per block each wave multiplies its K quarter (6 KiB of the
 // fragment-packed table) into all 64 rows, the 4 partial tiles go through double-buffered slabs,
 // and wave v finalises row block v: 4 logits per lane, a running (logit, id) best per lane.
-// A ring of 3 blocks of weights per wave is in flight.
+// A ring of FSL blocks of weights per wave is in flight.
 template <int G>
 __device__ __forceinline__ void phase_f(const Args& a, const Rs& rs, int w, const Sm& sm, gu64* keys) {
   const int tid = otid(), v = tid >> 6, lane = tid & 63;
@@ -865,26 +873,26 @@ __device__ __forceinline__ void phase_f(const Args& a, const Rs& rs, int w, cons
   lda<4, QS>(rs.xb, KSD, 0, QS * v, xf);
   const int nvb = (a.V + 15) >> 4, lmv = 16 * nvb;    // lmb: [2][16 nvb] bias, then cs
   const int nb = (nvb - w + G - 1) / G;
-  // ring of 3 block slots, each this wave's 6 weight fragments of the block plus the lane's 4
-  // per-token biases; every refill is unconditional (block index clamped to the workgroup's last
-  // block: a conditional load left the compiler counting conservatively, vmcnt(0) before every
-  // block, one round trip per block)
+  // ring of FSL block slots, each this wave's 6 weight fragments of the block; every refill is
+  // unconditional (block index clamped to the workgroup's last block: a conditional load left the
+  // compiler counting conservatively, vmcnt(0) before every block, one round trip per block).  The
+  // lane's 4 per-token biases and column sums of a block are loaded one block ahead (FSL even: the
+  // pair a block uses is fixed at compile time)
+  static_assert(Geo<G>::FSL % 2 == 0, "F ring: an even number of slots");
   struct Slot {
     u32x4_t w[QS];
-    float4 b, cs;
   };
-  Slot R0, R1, R2;
-  auto fill = [&](int i, Slot& r) {
+  constexpr int NSL = Geo<G>::FSL;
+  Slot R[NSL];
+  auto fill = [&](int i, Slot& r) { ldw<1, QS>(a.wtep, KSD, w + G * min(i, nb - 1), QS * v, r.w); };
+  float4 bq[2], cq[2];
+  auto fill_b = [&](int i, float4& b, float4& c) {
     const int blk = w + G * min(i, nb - 1);
-    ldw<1, QS>(a.wtep, KSD, blk, QS * v, r.w);
-    r.b = *reinterpret_cast<const float4*>(a.lmb + 16 * blk + 4 * (lane >> 4));
-    r.cs = *reinterpret_cast<const float4*>(a.lmb + lmv + 16 * blk + 4 * (lane >> 4));
+    b = *reinterpret_cast<const float4*>(a.lmb + 16 * blk + 4 * (lane >> 4));
+    c = *reinterpret_cast<const float4*>(a.lmb + lmv + 16 * blk + 4 * (lane >> 4));
   };
-  // the first block streams during the LayerNorm; the other two slots are issued after it (all
-  // three in flight across it left too few registers for the normalisation)
-  fill(0, R0);
-  fill(1, R1);
-  fill(2, R2);
+  static_for<NSL>([&](auto k) { fill(decltype(k)::value, R[decltype(k)::value]); });
+  fill_b(0, bq[0], cq[0]);
   __builtin_amdgcn_sched_barrier(0);
   ln_stats<4>(xf, sm, 0);
   float bv = -INFINITY;
@@ -894,7 +902,7 @@ __device__ __forceinline__ void phase_f(const Args& a, const Rs& rs, int w, cons
   lds_sync();     // the previous phase's slab readers are done; the row statistics are in
   float mean, rstd;
   ln_row(sm, 16 * v + (lane & 15), mean, rstd);   // wave v finalises row block v
-  auto consume = [&](int i, const Slot& r) {
+  auto consume = [&](int i, const Slot& r, const float4& rb_, const float4& rc_) {
     f32x4_t acc[4];
 #pragma unroll
     for (int rb = 0; rb < 4; ++rb) acc[rb] = f32x4_t{0.f, 0.f, 0.f, 0.f};
@@ -909,7 +917,7 @@ __device__ __forceinline__ void phase_f(const Args& a, const Rs& rs, int w, cons
     const f32x4_t sum = (red[v * 64 + lane] + red[(4 + v) * 64 + lane]) +
                         (red[(8 + v) * 64 + lane] + red[(12 + v) * 64 + lane]);
     const int col0 = 16 * (w + G * i) + 4 * (lane >> 4);
-    const float4 lg4 = ln_fold(sum, mean, rstd, r.cs, r.b);
+    const float4 lg4 = ln_fold(sum, mean, rstd, rc_, rb_);
     const float lgv[4] = {lg4.x, lg4.y, lg4.z, lg4.w};
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
@@ -920,13 +928,15 @@ __device__ __forceinline__ void phase_f(const Args& a, const Rs& rs, int w, cons
     buf ^= 1;
   };
 #pragma nounroll
-  for (int i = 0; i < nb; i += 3) {
-    consume(i, R0);
-    fill(i + 3, R0);
-    if (i + 1 < nb) consume(i + 1, R1);     // (wave-uniform)
-    fill(i + 4, R1);
-    if (i + 2 < nb) consume(i + 2, R2);
-    fill(i + 5, R2);
+  for (int i = 0; i < nb; i += NSL) {
+    static_for<NSL>([&](auto kk) {
+      constexpr int k = decltype(kk)::value;
+      if (k == 0 || i + k < nb) {                       // (wave-uniform)
+        fill_b(i + k + 1, bq[(k + 1) % 2], cq[(k + 1) % 2]);
+        consume(i + k, R[k], bq[k % 2], cq[k % 2]);
+      }
+      fill(i + k + NSL, R[k]);
+    });
   }
   // the 4 lanes of a row (l % 16 equal): larger logit, then the lower id
 #pragma unroll
