@@ -1317,13 +1317,6 @@ def main():
         del pipe
         torch.cuda.synchronize()
         torch.cuda.empty_cache()
-        log("throughput mode")
-        res["throughput_mode"] = sub_run(args, device, torch.bfloat16, 128, 3, 3 * 8192, 1,
-                                         encoder_batch=256)
-        res["throughput_mode"]["note"] = ("128 eval batches decoded together (8192-row decode "
-                                          "GEMMs), 3 in flight: NOT the metric's bs=64")
-        log("C3 beam 5")
-        res["c3_beam5"] = c3_beam5(args, device)
         log("f32 parity mode")
         # the f32 grid decode (G = 192): two grids co-resident, so 2 pipelines run (4 asked;
         # tools/f32_profile.py, profiles/r5/f32_sweep.txt)
@@ -1331,6 +1324,13 @@ def main():
                                          CLOTHO_EVAL_CLIPS, 1, reps=3)
         res["f32_parity_mode"]["note"] = ("the headline's 1045 clips at bs=64 in f32: the mode "
                                           "whose greedy ids are bit-exact")
+        log("throughput mode")
+        res["throughput_mode"] = sub_run(args, device, torch.bfloat16, 128, 3, 3 * 8192, 1,
+                                         encoder_batch=256)
+        res["throughput_mode"]["note"] = ("128 eval batches decoded together (8192-row decode "
+                                          "GEMMs), 3 in flight: NOT the metric's bs=64")
+        log("C3 beam 5")
+        res["c3_beam5"] = c3_beam5(args, device)
         log("C5 Mistral-7B")
         res["c5_mistral"] = c5_mistral(args, device)
         log("id agreement")
