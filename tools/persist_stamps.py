@@ -5,7 +5,9 @@ the wait (arrive -> wait end) and the arrival skew (last - first arrive), in mic
 bg > 0: the traced grid runs beside bg other batches' grids of the same size (pipeline twins on
 their own streams, decode only), the load of the headline.
 
-    python tools/persist_stamps.py [step=3] [grid=48] [bg=0]
+    python tools/persist_stamps.py [step=3] [grid=48] [bg=0] [dtype=bf16]
+
+dtype f32: the f32 parity mode's grid decode (zs_gpt2_decode_persist_f32, grid 192).
 """
 import json
 import os
@@ -26,15 +28,17 @@ def main():
     from zsaac import ops
     from zsaac._lib import call
 
+    f32 = len(sys.argv) > 4 and sys.argv[4] == "f32"
+
     class A:
         batch, dtype, encoder, mapper, beam, entry_length, group, compact = \
-            64, "bf16", "htsat", "mlp", 0, 67, 1, 1
+            64, "f32" if f32 else "bf16", "htsat", "mlp", 0, 67, 1, 1
         encoder_batch = 64
     dev = torch.device("cuda", 0)
-    pipe, _, _ = bench.build(A, dev)
+    pipe, _, _ = bench.build(A, dev, dtype=torch.float32 if f32 else torch.bfloat16)
     wav = bench.synthetic_clips(64, 0, dev)
     pipe.caption_wav(wav)
-    G = ops.decode_persist_grid(int(sys.argv[2]) if len(sys.argv) > 2 else 48)
+    G = 192 if f32 else ops.decode_persist_grid(int(sys.argv[2]) if len(sys.argv) > 2 else 48)
     nbg = int(sys.argv[3]) if len(sys.argv) > 3 else 0
     pipes = [pipe] + [pipe.twin() for _ in range(nbg)]
     streams = ops.dedicated_streams(len(pipes), dev)

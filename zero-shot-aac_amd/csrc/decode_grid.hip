@@ -1674,6 +1674,9 @@ __global__ __launch_bounds__(NT, 2) void dg32_persist_kernel(Args a) {
   Bar bar{(gu32*)(a.ws + WS_SH), (gu32*)(a.ws + WS_TMO), 0, G / NSH, a.spin_max, nullptr, 0};
   gu64* const keys = (gu64*)(a.ws + WS_KEY);
   volatile lds_int_t* s_ok = (volatile lds_int_t*)(sm.misc + 8);
+  unsigned long long* const stamps =       // (diagnostic stamps, as the bf16 kernel)
+      (dp_stamp_ws == nullptr || dp_stamp_ws == a.ws) ? dp_stamp_buf : nullptr;
+  const int stamp_step = dp_stamp_step;
   const int ub = w * UPG;
   constexpr int ANCG = NCB_Q / ACB, DNCG = NCB_F / DCB, ENCG = NCB_D / ECB;
   const int acb0 = (w % ANCG) * ACB, dcb0 = (w % DNCG) * DCB, ecb0 = (w % ENCG) * ECB;
@@ -1682,6 +1685,9 @@ __global__ __launch_bounds__(NT, 2) void dg32_persist_kernel(Args a) {
   ldw<APF, QS>(a.wq[0], KSD, acb0, QS * V_, wq);
   f32x4_t xo{0.f, 0.f, 0.f, 0.f};
   for (;;) {
+    bar.sb = (stamps != nullptr && step == stamp_step) ? stamps + (long)w * 2 * DP_NB : nullptr;
+    bar.n0 = bar.n;
+    stamp(bar.sb, 2 * DP_NB - 1);
     if (step == a.abort_step) return gave_up(a);
     for (int l = 0; l < NLY; ++l) {
       phase_a<false>(a, rs, l, w, sm, wq);
@@ -1720,6 +1726,7 @@ __global__ __launch_bounds__(NT, 2) void dg32_persist_kernel(Args a) {
     if (!bar_wait(bar, s_ok)) return gave_up(a);
     bookkeep(a, sm, keys + (step & 1) * RM, step, w == 0);
     __syncthreads();
+    stamp(bar.sb, 2 * DP_NB - 2);
     const int total = sm.misc[0];
     const bool fin = total == 0 || step + 1 >= a.max_steps;
     if (w == 0 && otid() == 0) {
