@@ -94,13 +94,21 @@ template <int G> struct Geo;
 #ifndef DG_ESL192
 #define DG_ESL192 4
 #endif
+// G = 48: c_attn / c_fc column blocks prefetched across the barrier (the rest: after round 1;
+// profiles/r5/pf_ab.txt: all of them, 3 / 4, vs 2 / 2: within noise, ~+1 %)
+#ifndef DG_APF48
+#define DG_APF48 3
+#endif
+#ifndef DG_DPF48
+#define DG_DPF48 4
+#endif
 // FSL: phase F's vocab blocks in flight
 // (profiles/r5/fsl_ab.txt: 4 vs 3 slots, alone -1.5 to -2 %; 6 spills)
 #ifndef DG_FSL
 #define DG_FSL 4
 #endif
 template <> struct Geo<48> {
-  static constexpr int ACB = 3, ARB = 4, APF = 2, DCB = 4, DRB = 4, DPF = 2, ECB = 2, ERB = 2, ESL = DG_ESL48,
+  static constexpr int ACB = 3, ARB = 4, APF = DG_APF48, DCB = 4, DRB = 4, DPF = DG_DPF48, ECB = 2, ERB = 2, ESL = DG_ESL48,
                        FSL = DG_FSL;
 };
 template <> struct Geo<96> {
@@ -1174,7 +1182,7 @@ constexpr int QS = KSD / NW, QF = KSF / NW;      // per wave quarter: 12 / 48
 constexpr int G = 192;
 // tiles per workgroup: A 3 column blocks x 1 row block (c_attn: 144 blocks / 3 = 48 column groups
 // x 4 row groups), C / E 1 x 1 (48 x 4), D 2 x 2 (96 x 2); F one row half (2 row blocks) over the
-// vocab blocks w / 2 + 96 i
+// vocab blocks (w % 8 + 8 (w / 16)) + 96 i: the two workgroups of a block share an XCD
 constexpr int ACB = 3, ARB = 1, DCB = 2, DRB = 2, ECB = 1, ERB = 1;
 constexpr int APF = 3;          // c_attn column blocks prefetched across the barrier (the rest: in A)
 constexpr int UPG = RM * NH / G, KC = 8;   // attention: UPG / 4 = 1 unit per wave; 8 KC keys loaded per
@@ -1587,13 +1595,15 @@ __device__ __forceinline__ void phase_b(const Args& a, const Rs& rs, int l, cons
   }
 }
 
-// F: ln_f + LM head.  Workgroup w takes row half w % 2 (row blocks 2 (w % 2) .. + 2) and vocab
-// blocks w / 2 + 96 i; per block each wave multiplies its K quarter into the 32 rows, the 4 partial
-// tiles go through double-buffered slabs, waves 0 / 1 finalise row block 2 (w % 2) + v.  A ring of 2
-// blocks of weights per wave is in flight.
+// F: ln_f + LM head.  Workgroup w takes row half h = (w / 8) % 2 (row blocks 2 h .. + 2) and vocab
+// blocks wh + 96 i, wh = w % 8 + 8 (w / 16); per block each wave multiplies its K quarter into
+// the 32 rows, the 4 partial tiles go through double-buffered slabs, waves 0 / 1 finalise row
+// block 2 h + v.  A ring of 2 blocks of weights per wave is in flight.
 __device__ __forceinline__ void phase_f(const Args& a, const Rs& rs, int w, const Sm& sm, gu64* keys) {
   const int tid = otid(), v = tid >> 6, lane = tid & 63;
-  const int half = w & 1, wh = w >> 1, rb0 = 2 * half;
+  // the two workgroups of a vocab block (one per row half) are w and w + 8: the same XCD under
+  // round-robin dispatch, so the second read of the block hits that XCD's L2
+  const int half = (w >> 3) & 1, wh = (w & 7) + 8 * (w >> 4), rb0 = 2 * half;
   u32x4_t xf[2 * QS];
   lda<2, QS>(rs.xb, KSD, rb0, QS * v, xf);
   const int nvb = (a.V + 15) >> 4;
