@@ -296,6 +296,10 @@ class ConcurrentRunner:
         # every first-round begin -- the begins run on the whole chip instead of beside the grids
         self.begin_first = bool(begin_first) and self.persist
         self.late_grid = True     # grid size chosen when the begin has finished (False: at begin)
+        # one begin per pass over the pipelines: a begin costs milliseconds of host enqueue, so
+        # beginning every idle pipeline in one pass delayed the first grids' launches until the
+        # last begin was enqueued (~43 ms into the headline, tools/timeline.py)
+        self.one_begin = True
         self.spread = False       # A/B: exclusive (one CU per workgroup) grids while CUs allow
         if self.persist and not self.begin_first:
             # persistent decode grids must be co-resident: at most budget // (smallest grid)
@@ -418,6 +422,8 @@ class ConcurrentRunner:
                             trace.append(("begin", nxt, round((time.perf_counter() - t_run) * 1e3, 2)))
                         nxt += 1
                         progressed = True
+                        if self.one_begin:
+                            break       # launches / completions before the next begin
                     continue
                 if st[0] == "begun":
                     _, bi, ev = st
