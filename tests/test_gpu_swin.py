@@ -109,3 +109,24 @@ def test_htsat_fused_matches_unfused(cuda, monkeypatch):
     b = eu.encode(wav).clone()
     cos = torch.nn.functional.cosine_similarity(a, b, dim=-1)
     assert float(cos.min()) > 0.999, cos
+
+
+def test_htsat_encode_graphed_bit_identical(cuda):
+    """Encoder.encode_graphed (the concurrent runner's up-front passes: everything after the
+    log-mel front end replayed from a per-size hipGraph captured on a side stream) gives exactly
+    encode()'s embeddings, at two batch sizes and on a second replay."""
+    from zsaac import synthetic as S
+    from zsaac import encoder as E
+    sd = S.htsat_state_dict(3)
+    sd.update(S.audio_proj_state_dict(5))
+    wav = S.synthetic_waveforms(4).to(cuda)
+    enc = E.AudioEncoder(sd, "htsat", torch.bfloat16, 4, cuda)
+    ref = {B: enc.encode(wav[:B]).clone() for B in (4, 3)}
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        got = [(B, enc.encode_graphed(wav[:B]).clone()) for B in (4, 3, 4, 3)]
+    torch.cuda.current_stream().wait_stream(s)
+    torch.cuda.synchronize()
+    for B, e in got:
+        assert torch.equal(e, ref[B]), B

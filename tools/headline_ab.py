@@ -6,7 +6,8 @@ An arm is "name:inflight:knob=v,knob=v[:grids[:budget[:encode_ahead]]]" (zs_tune
 (runner options among the knobs: late=0 sizes each grid at its batch's begin instead of at its
 launch; spread=1: exclusive one-CU-per-workgroup grids while the CUs allow; prio=0: default stream
 priorities instead of high for the pipelines and low for the encoder; extra=k: k pipelines beyond
-the grids the budget holds; one=0: begin every idle pipeline in one pass instead of one per pass)
+the grids the budget holds; one=0: begin every idle pipeline in one pass instead of one per pass; eg=0: encoder passes
+enqueued kernel by kernel instead of replayed from a hipGraph)
 to the baseline values given with --base between arms; grids: the persistent-decode grid sizes the
 runner may use, zsaac.pipeline.persist_grids, e.g. "48" or "96-48" ('-'-separated); budget:
 workgroup slots of the in-flight grids; encode_ahead: clips per up-front encoder pass, 0 = each
@@ -83,6 +84,7 @@ def main():
         r.late_grid = bool(kn.pop("late", 1))      # runner options, not zs_tune_set knobs
         r.spread = bool(kn.pop("spread", 0))
         r.one_begin = bool(kn.pop("one", 1))
+        r.enc_graph = bool(kn.pop("eg", 1))
         arms.append((name, r, kn))
     res = {n: [] for n, _, _ in arms}
     for rep in range(a.reps + 1):

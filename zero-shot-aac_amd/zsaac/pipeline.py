@@ -300,6 +300,8 @@ class ConcurrentRunner:
         # beginning every idle pipeline in one pass delayed the first grids' launches until the
         # last begin was enqueued (~43 ms into the headline, tools/timeline.py)
         self.one_begin = True
+        # the encoder's up-front passes replayed from per-size hipGraphs (Encoder.encode_graphed)
+        self.enc_graph = True
         self.spread = False       # A/B: exclusive (one CU per workgroup) grids while CUs allow
         if self.persist and not self.begin_first:
             # persistent decode grids must be co-resident: at most budget // (smallest grid)
@@ -616,6 +618,7 @@ class _EncodeAhead:
                 c0 += int(b.shape[0])
             i = j
         self.events = []
+        self.graph = runner.enc_graph
         self.first = runner.encode_first
         self.pump(force=1)
 
@@ -626,7 +629,8 @@ class _EncodeAhead:
                 return
             i, j, c0, m = self.passes[len(self.events)]
             with torch.cuda.stream(self.es):
-                self.emb[c0:c0 + m].copy_(self.enc.encode(_rows_span(self.batches[i:j])))
+                enc = self.enc.encode_graphed if self.graph else self.enc.encode
+                self.emb[c0:c0 + m].copy_(enc(_rows_span(self.batches[i:j])))
                 ev = torch.cuda.Event()
                 ev.record(self.es)
             self.events.append(ev)
