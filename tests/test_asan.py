@@ -35,7 +35,7 @@ def test_host_validators_under_asan():
     res = json.loads(r.stdout.strip().splitlines()[-1])
     assert res["functions"] >= 60
     # size / count queries return their value; everything else an error code or 0
-    queries = {"zs_decode_persist_workspace_bytes", "zs_fp8_splits",
+    queries = {"zs_decode_persist_workspace_bytes", "zs_decode_persist_f32_workspace_bytes", "zs_fp8_splits",
                "zs_last_error", "zs_lmhead_nblk", "zs_version", "zs_gemm_workspace_floats"}
     bad = {k: v for k, v in res["rc"].items() if k not in queries and any(c > 0 for c in v)}
     assert not bad, bad
