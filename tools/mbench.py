@@ -190,6 +190,45 @@ def bench_gemm_f32():
     print(f"sum (HTSAT blocks x2 per stage except C768 x1... see shapes): {tot}", flush=True)
 
 
+def bench_gemm_f32_tiles():
+    """The f32 parity mode's big tiled GEMM shapes under each zs_tune_set("f32_tile", t) variant
+    (gemm.hip dispatch_fast_f32), us per shape and the HTSAT + prefill total; outputs must be
+    bit-identical to variant 0 (the same k order)."""
+    from zsaac import ops
+    from zsaac._lib import call
+    dev = torch.device("cuda", 0)
+    shapes = []
+    for C, T in ((96, 4096), (192, 1024), (384, 256), (768, 64)):
+        M = 64 * T
+        shapes += [(M, 3 * C, C, f"C{C} qkv", 2), (M, C, C, f"C{C} proj", 2),
+                   (M, 4 * C, C, f"C{C} fc1", 2), (M, C, 4 * C, f"C{C} fc2", 2)]
+        if C < 768:
+            shapes.append((M // 4, 2 * C, 4 * C, f"C{C} merge", 1))
+    P = 64 * 27
+    shapes += [(P, 2304, 768, "pre qkv", 12), (P, 768, 768, "pre proj", 12), (P, 3072, 768, "pre fc", 12),
+               (P, 768, 3072, "pre mproj", 12)]
+    tot = {}
+    for M, N, K, name, mult in shapes:
+        a = torch.randn(M, K, device=dev)
+        w = torch.randn(N, K, device=dev) * 0.02
+        b = torch.randn(N, device=dev)
+        out = torch.empty(M, N, device=dev)
+        row = []
+        ref = None
+        for t in (0, 2, 6, 7, 8):
+            call("zs_tune_set", b"f32_tile", t)
+            us = timeit(lambda: ops.gemm(a, w, out, bias=b, split_k=1), reps=10)
+            same = True if ref is None else bool(torch.equal(out, ref))
+            if ref is None:
+                ref = out.clone()
+            tot[t] = tot.get(t, 0.0) + us * mult
+            row.append(f"t{t}={us:7.1f}{'' if same else '!'}")
+        call("zs_tune_set", b"f32_tile", 8)       # the default
+        print(f"{name:10s} M{M:7d} N{N:5d} K{K:5d}  " + " ".join(row), flush=True)
+    print("weighted total us (HTSAT x2 per block, prefill x12 layers):",
+          {t: round(v, 1) for t, v in tot.items()}, flush=True)
+
+
 def bench_gemm_dbg():
     """Where the fast GEMM's time goes: full / no-MFMA / no-DMA at a few encoder shapes."""
     from zsaac import ops
@@ -622,4 +661,4 @@ if __name__ == "__main__":
             call("zs_tune_set", k.encode(), int(v))
     which = sys.argv[1:] or ["gemm", "attn"]
     for wname in which:
-        {"gemm": bench_gemm, "rows": bench_rows, "gemm_m": bench_gemm_m, "gemm_c3": bench_gemm_c3, "gemm_htsat": bench_gemm_htsat, "gemm_f32": bench_gemm_f32, "gemm_dbg": bench_gemm_dbg, "lmhead": bench_lmhead, "overhead": bench_overhead, "front": bench_front, "window": bench_window, "decode_gemm": bench_decode_gemm, "attn": bench_attn, "attn_beam": bench_attn_beam, "gemm_big": bench_gemm_big, "inflight": bench_inflight, "buckets": bench_buckets, "compact_ab": bench_compact_ab, "host": bench_host}[wname]()
+        {"gemm": bench_gemm, "rows": bench_rows, "gemm_m": bench_gemm_m, "gemm_c3": bench_gemm_c3, "gemm_htsat": bench_gemm_htsat, "gemm_f32": bench_gemm_f32, "gemm_f32_tiles": bench_gemm_f32_tiles, "gemm_dbg": bench_gemm_dbg, "lmhead": bench_lmhead, "overhead": bench_overhead, "front": bench_front, "window": bench_window, "decode_gemm": bench_decode_gemm, "attn": bench_attn, "attn_beam": bench_attn_beam, "gemm_big": bench_gemm_big, "inflight": bench_inflight, "buckets": bench_buckets, "compact_ab": bench_compact_ab, "host": bench_host}[wname]()

@@ -761,12 +761,37 @@ static int launch_gemm(GemmArgs& g, hipStream_t st) {
   return 0;
 }
 
-// f32 parity mode on the LDS-DMA ring (gemm_fast_kernel F32): 16 f32 k per stage, 4 stages
-// (3 in flight: ~2.6 us of k-loop at 0.85 us of f32 MFMA per stage) at 64 KiB, two blocks per CU.
+// f32 parity mode on the LDS-DMA ring (gemm_fast_kernel F32): 32 f32 k per stage, 2 stages at
+// 64 KiB (g_f32_tile 8), two blocks per CU; round 4's 16 k per stage x 4 stages at g_f32_tile 0.
 // Needs 16-byte rows (K, lda, ldw multiples of 4, aligned bases); else the register-staged
 // gemm_kernel<float>.
 int g_f32_fast = 1;    // zs_tune_set("f32_fast", 0): f32 GEMMs on the register-staged kernel
+// zs_tune_set("f32_tile", t): the f32 tile variant (tools/mbench.py gemm_f32_tiles,
+// profiles/r5/f32_gemm_tiles.txt): 8 (default) = 64-k stages, 2 in flight, at every tile size --
+// the f32 parity mode's HTSAT + prefill GEMMs 11.15 -> 10.00 ms, bit-identical (same k order);
+// 0 = 16-k stages, 4 in flight (round 4); 1-7 = other variants
+int g_f32_tile = 8;
 static int dispatch_fast_f32(GemmArgs& g, hipStream_t st) {
+  if (g_f32_tile >= 7) {     // 64-k stages, 2 in flight, at every tile size
+    if (nblocks(g, 128, 128) >= 256)
+      return g_f32_tile == 7 ? launch_fast<128, 128, 2, 2, 4, 64, true>(g, st)
+                             : launch_fast<128, 128, 2, 2, 2, 64, true>(g, st);
+    if (nblocks(g, 128, 64) >= 256)
+      return g.M >= g.N ? launch_fast<128, 64, 2, 2, 2, 64, true>(g, st)
+                        : launch_fast<64, 128, 2, 2, 2, 64, true>(g, st);
+    return launch_fast<64, 64, 2, 2, 2, 64, true>(g, st);
+  }
+  if (g_f32_tile && nblocks(g, 128, 128) >= 256) {
+    switch (g_f32_tile) {
+      case 1: return launch_fast<128, 128, 3, 2, 2, 64, true>(g, st);
+      case 2: return launch_fast<128, 128, 2, 2, 2, 64, true>(g, st);
+      case 3: return launch_fast<256, 128, 4, 4, 2, 32, true>(g, st);
+      case 4: return launch_fast<128, 256, 4, 2, 4, 32, true>(g, st);
+      case 5: return launch_fast<128, 128, 6, 2, 2, 32, true>(g, st);
+      case 6: return launch_fast<128, 128, 4, 2, 4, 32, true>(g, st);
+      default: break;
+    }
+  }
   if (nblocks(g, 128, 128) >= 256) return launch_fast<128, 128, 4, 2, 2, 32, true>(g, st);
   if (nblocks(g, 128, 64) >= 256)
     return g.M >= g.N ? launch_fast<128, 64, 4, 2, 2, 32, true>(g, st)
