@@ -773,9 +773,13 @@ int g_f32_fast = 1;    // zs_tune_set("f32_fast", 0): f32 GEMMs on the register-
 int g_f32_tile = 8;
 static int dispatch_fast_f32(GemmArgs& g, hipStream_t st) {
   if (g_f32_tile >= 7) {     // 64-k stages, 2 in flight, at every tile size
-    if (nblocks(g, 128, 128) >= 256)
+    if (nblocks(g, 128, 128) >= 256) {
+      if (g_f32_tile == 10) return launch_fast<128, 128, 2, 2, 2, 128, true>(g, st);
+      if (g_f32_tile == 11 && nblocks(g, 256, 128) >= 256)
+        return launch_fast<256, 128, 2, 4, 2, 64, true>(g, st);
       return g_f32_tile == 7 ? launch_fast<128, 128, 2, 2, 4, 64, true>(g, st)
                              : launch_fast<128, 128, 2, 2, 2, 64, true>(g, st);
+    }
     if (nblocks(g, 128, 64) >= 256)
       return g.M >= g.N ? launch_fast<128, 64, 2, 2, 2, 64, true>(g, st)
                         : launch_fast<64, 128, 2, 2, 2, 64, true>(g, st);
