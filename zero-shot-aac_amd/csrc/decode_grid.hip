@@ -102,6 +102,10 @@ template <int G> struct Geo;
 #ifndef DG_DPF48
 #define DG_DPF48 4
 #endif
+// barrier poll interval (s_sleep units of 64 clocks)
+#ifndef DG_SLEEP
+#define DG_SLEEP 1
+#endif
 // FSL: phase F's vocab blocks in flight
 // (profiles/r5/fsl_ab.txt: 4 vs 3 slots, alone -1.5 to -2 %; 6 spills)
 #ifndef DG_FSL
@@ -348,7 +352,7 @@ __device__ __forceinline__ bool bar_wait(Bar& b, volatile lds_int_t* s_ok) {
         ok = 0;
         break;
       }
-      __builtin_amdgcn_s_sleep(1);
+      __builtin_amdgcn_s_sleep(DG_SLEEP);
     }
     if (lane == 0) *s_ok = ok;
   }
