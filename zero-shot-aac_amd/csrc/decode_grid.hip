@@ -102,9 +102,10 @@ template <int G> struct Geo;
 #ifndef DG_DPF48
 #define DG_DPF48 4
 #endif
-// barrier poll interval (s_sleep units of 64 clocks)
+// barrier poll interval (s_sleep units of 64 clocks; profiles/r5/sleep_ab.txt: 3 vs 1, alone -3 %,
+// 5 x G48 +1 %)
 #ifndef DG_SLEEP
-#define DG_SLEEP 1
+#define DG_SLEEP 3
 #endif
 // FSL: phase F's vocab blocks in flight
 // (profiles/r5/fsl_ab.txt: 4 vs 3 slots, alone -1.5 to -2 %; 6 spills)
