@@ -74,7 +74,11 @@ constexpr int KSD = D / 32, KSF = DFF / 32;          // k-steps of K = 768 / 307
 constexpr int QS = KSD / NW, QF = KSF / NW;          // k-steps of one wave's K quarter: 6 / 24
 constexpr int NCB_Q = QKVN / 16, NCB_D = D / 16, NCB_F = DFF / 16;   // 16-column blocks
 constexpr unsigned SPIN_MAX = 1u << 22;
-constexpr int NSH = 8;                               // barrier counter shards, one 128-B line each
+#ifndef DG_NSH
+#define DG_NSH 8
+#endif
+constexpr int NSH = DG_NSH;                          // barrier counter shards, one 128-B line each
+static_assert(NSH <= 16 && 48 % NSH == 0, "shards: <= 16 (WS_SYNC_BYTES), dividing every grid");
 constexpr int ECH = 4;                               // phase E: k-steps per streamed chunk
 
 // Tiles per workgroup of each GEMM phase: CB column blocks x RB row blocks of 16 (workgroup w
