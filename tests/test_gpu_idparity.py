@@ -27,7 +27,10 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 GOLDENS = ["c1_greedy", "c2_margin", "c2_margin_flat", "c2_gpt2init"]
-GOLDENS_BF16 = ["c2_margin_flat", "c2_gpt2init"]       # the goldens whose bf16 gate bites
+# every bf16 golden: the error bound and zero violations hold on all four; the compared-fraction
+# floor applies where the rule compares most tokens (c1_greedy / c2_margin: reference bf16 error
+# ~1 / 0.23 logit at step 0, < 2 % of their tokens compared)
+GOLDENS_BF16 = ["c1_greedy", "c2_margin", "c2_margin_flat", "c2_gpt2init"]
 
 
 @pytest.mark.parametrize("name", GOLDENS)
@@ -61,4 +64,4 @@ def test_bf16_ids_exact_above_margin(cuda, name):
           f"{r['tau']}, compared {r['compared_tokens']} / {r['total_tokens']} tokens "
           f"({r['compared_frac']}), clips required exact {r['clips_exact_required']}")
     assert not r["violations"], f"{name}: {r['violations']}"
-    assert r["compared_frac"] >= idparity.MIN_COMPARED_FRAC[name], r
+    assert r["compared_frac"] >= idparity.MIN_COMPARED_FRAC.get(name, 0.0), r

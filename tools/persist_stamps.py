@@ -58,6 +58,8 @@ def main():
         torch.cuda.synchronize()
     call("zs_decode_persist_set_stamps", None, 0, None)
     t = buf.cpu().numpy().astype(np.float64) / 100.0     # us (100 MHz)
+    if os.environ.get("STAMPS_OUT"):                      # raw stamps for offline analysis
+        np.save(os.environ["STAMPS_OUT"], t)
     start, end = t[:, 127], t[:, 126]
     names = []
     for l in range(12):
@@ -91,6 +93,18 @@ def main():
     summ["step_us"] = round(float(np.median(end - start)), 1)
     print(json.dumps({"grid": G, "background_grids": nbg, "per_phase_kind_mean_us": summ}))
     # phase F per workgroup, and by blockIdx % 8 (the XCD under round-robin dispatch)
+    # does a workgroup that is slow in one phase stay slow in the next?  (rank correlation of
+    # per-workgroup compute times of consecutive phases, and how often the last arrival of a
+    # barrier is also among the slowest quarter of the next phase)
+    cm = np.array(comp[:-1])
+    rk = np.argsort(np.argsort(cm, axis=1), axis=1).astype(np.float64)
+    cors = [float(np.corrcoef(rk[i], rk[i + 1])[0, 1]) for i in range(len(rk) - 1)]
+    last_slow = [int(np.argmax(cm[i]) in set(np.argsort(-cm[i + 1])[:max(1, G // 4)]))
+                 for i in range(len(cm) - 1)]
+    print(json.dumps({"rank_corr_next_phase_mean": round(float(np.mean(cors)), 3),
+                      "slowest_in_next_quarter_frac": round(float(np.mean(last_slow)), 3),
+                      "compute_mean_over_phases": round(float(cm.mean()), 2),
+                      "compute_max_over_phases": round(float(cm.max(axis=1).mean()), 2)}))
     fc = comp[-1]
     print(json.dumps({"F_compute_by_wg": [round(float(x), 1) for x in fc],
                       "F_compute_by_wg_mod8": [round(float(np.mean(fc[k::8])), 1) for k in range(8)],

@@ -16,10 +16,11 @@
 //     16x16x32 chain over its k-steps in increasing order from 0, added as (p0 + p1) + (p2 + p3);
 //     then + bias (and the activation / + residual).  The grid only decides WHICH workgroup owns
 //     an element (tiles of 16 x 16 are independent in the MFMA);
-//   * a LayerNorm row (ln_1 / ln_2 / ln_f) reads bf16(x), sums each wave's quarter in a fixed
-//     in-lane order, across the 4 lanes of a row by swap-adds, across the waves as (w0 + w1) +
-//     (w2 + w3): mean, then the squared deviations the same way (two-pass), rstd = rsqrt(q / 768 +
-//     1e-5);
+//   * a LayerNorm row (ln_1 / ln_2 / ln_f) reads bf16(x), sums x and x^2 over each wave's quarter
+//     in a fixed in-lane order (v_dot2 over the bf16 pairs), across the 4 lanes of a row by
+//     swap-adds, across the waves as (w0 + w1) + (w2 + w3): ONE pass, var = E[x^2] - mean^2,
+//     rstd = rsqrt(var + 1e-5) (the f32 parity kernel below is two-pass; the one-pass error on a
+//     row with a large mean is bounded in tests/test_ln_onepass.py);
 //   * an attention unit (row, head) runs the online softmax over its cached keys in 32-key chunks
 //     (8 lane groups x 4 keys), then folds in the new key;
 //   * the argmax over the vocabulary is exact (ties -> lower id, as torch.argmax).
@@ -78,7 +79,8 @@ constexpr unsigned SPIN_MAX = 1u << 22;
 #define DG_NSH 8
 #endif
 constexpr int NSH = DG_NSH;                          // barrier counter shards, one 128-B line each
-static_assert(NSH <= 16 && 48 % NSH == 0, "shards: <= 16 (WS_SYNC_BYTES), dividing every grid");
+static_assert(NSH <= 16 && 48 % NSH == 0 && (NSH & (NSH - 1)) == 0,
+              "shards: a power of two (bar_arrive takes w & (NSH - 1)) <= 16, dividing every grid");
 constexpr int ECH = 4;                               // phase E: k-steps per streamed chunk
 
 // Tiles per workgroup of each GEMM phase: CB column blocks x RB row blocks of 16 (workgroup w
@@ -147,6 +149,8 @@ typedef __attribute__((address_space(3))) int lds_int_t;
 constexpr int WS_SH = 0;                          // NSH counters, 128 B apart
 constexpr int WS_TMO = NSH * 128;                 // timeout word
 constexpr int WS_KEY = WS_TMO + 128;              // u64 [2][64] LM-head argmax keys (step parity)
+constexpr int WS_CLM = WS_KEY + 2 * RM * 8;       // tile-claim counters, 128 B apart (persistent)
+constexpr int CLM_F = 0;                          // phase F: [step & 1]
 constexpr int WS_SYNC_BYTES = 4096;               // zeroed by the launcher
 constexpr int WS_Q = WS_SYNC_BYTES;               // bf16 [64][768]
 constexpr int WS_ATT = WS_Q + RM * D * 2;         // bf16 [4][24][64][8] (fragment order)
@@ -338,26 +342,79 @@ __device__ __forceinline__ void bar_arrive(Bar& b, int w) {
   stamp(b.sb, 2 * (b.n - b.n0));
   ++b.n;
 }
+// The poll keeps 3 shard reads in flight (each issued DG_SLEEP x 64 clocks after the previous
+// one, consumed oldest first): a serial poll sees the last arrival one read latency plus up to
+// one more poll period late (under 9 other grids that latency is ~1-2 us, and the workgroups
+// detecting a barrier late were the next phase's last arrivers: release spread 2 us,
+// tools/persist_stamps.py); with reads in flight the period shrinks to about a third of it.
+#define DG_STR_(x) #x
+#define DG_STR(x) DG_STR_(x)
+// A workgroup that gives up raises every shard to >= GIVEUP, so every other workgroup's poll sees its
+// barrier "met" with a value >= GIVEUP and gives up too (the timeout word is only for the host,
+// zs_decode_persist_status): no second load in the poll loop, whose reads stay counted.
+constexpr unsigned GIVEUP = 1u << 30;
 __device__ __forceinline__ bool bar_wait(Bar& b, volatile lds_int_t* s_ok) {
   if (threadIdx.x < 64) {
     const int lane = threadIdx.x;
     const unsigned target = b.n * b.per;
     unsigned spins = 0;
     int ok = 1;
-    for (;;) {
-      const unsigned c = lane < NSH
-          ? __hip_atomic_load(b.sh + lane * 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : target;
-      if (__ballot(c < target) == 0) break;
-      ++spins;
+    // (hand-written: compiled from C++, the rotation of the reads in flight through the loop's
+    // registers made the compiler wait for every read at the end of each round.  Every lane
+    // reads shard lane % NSH -- the duplicate lanes share the 8 lines' requests -- and the
+    // loop ends with vmcnt(0): no read of it is left in flight into a register it gave back)
+    const gu32* addr = b.sh + (lane & (NSH - 1)) * 32;
+    unsigned c0, c1, c2, cm;
+    asm volatile(
+        "global_load_dword %[c0], %[ad], off sc1\n\t"
+        "s_sleep " DG_STR(DG_SLEEP) "\n\t"
+        "global_load_dword %[c1], %[ad], off sc1\n\t"
+        "s_sleep " DG_STR(DG_SLEEP) "\n\t"
+        "global_load_dword %[c2], %[ad], off sc1\n\t"
+        "s_mov_b32 %[sp], 0\n"
+        "1:\n\t"
+        "s_waitcnt vmcnt(2)\n\t"
+        "v_cmp_gt_u32 vcc, %[tg], %[c0]\n\t"
+        "s_cbranch_vccz 2f\n\t"
+        "s_sleep " DG_STR(DG_SLEEP) "\n\t"
+        "global_load_dword %[c0], %[ad], off sc1\n\t"
+        "s_waitcnt vmcnt(2)\n\t"
+        "v_cmp_gt_u32 vcc, %[tg], %[c1]\n\t"
+        "s_cbranch_vccz 3f\n\t"
+        "s_sleep " DG_STR(DG_SLEEP) "\n\t"
+        "global_load_dword %[c1], %[ad], off sc1\n\t"
+        "s_waitcnt vmcnt(2)\n\t"
+        "v_cmp_gt_u32 vcc, %[tg], %[c2]\n\t"
+        "s_cbranch_vccz 4f\n\t"
+        "s_sleep " DG_STR(DG_SLEEP) "\n\t"
+        "global_load_dword %[c2], %[ad], off sc1\n\t"
+        "s_add_u32 %[sp], %[sp], 3\n\t"
+        "s_cmp_gt_u32 %[sp], %[sm]\n\t"
+        "s_cbranch_scc0 1b\n\t"
+        "v_mov_b32 %[cm], 0\n\t"
+        "s_branch 5f\n"
+        "2:\n\t"
+        "v_mov_b32 %[cm], %[c0]\n\t"
+        "s_branch 5f\n"
+        "3:\n\t"
+        "v_mov_b32 %[cm], %[c1]\n\t"
+        "s_branch 5f\n"
+        "4:\n\t"
+        "v_mov_b32 %[cm], %[c2]\n"
+        "5:\n\t"
+        "s_waitcnt vmcnt(0)"
+        : [c0] "=&v"(c0), [c1] "=&v"(c1), [c2] "=&v"(c2), [cm] "=&v"(cm), [sp] "=&s"(spins)
+        : [ad] "v"(addr), [tg] "s"(target), [sm] "s"(b.spin_max)
+        : "vcc", "scc", "memory");
+    if (spins > b.spin_max) {
       // bounded: give up (and tell every other workgroup) after spin_max polls, so a grid that
       // is not co-resident drains instead of hanging
-      if (spins > b.spin_max ||
-          ((spins & 255) == 0 && __hip_atomic_load(b.tmo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
-        if (lane == 0) __hip_atomic_store(b.tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        ok = 0;
-        break;
-      }
-      __builtin_amdgcn_s_sleep(DG_SLEEP);
+      // (a max, not an add: several workgroups may give up at once)
+      if (lane < NSH) __hip_atomic_fetch_max(b.sh + lane * 32, GIVEUP, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (lane == 0) __hip_atomic_store(b.tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      ok = 0;
+    } else if (__ballot(cm >= GIVEUP) != 0) {
+      ok = 0;                                    // another workgroup gave up
     }
     if (lane == 0) *s_ok = ok;
   }
@@ -883,33 +940,56 @@ __device__ __forceinline__ void phase_b(const Args& a, const Rs& rs, int l, cons
 // fragment-packed table) into all 64 rows, the 4 partial tiles go through double-buffered slabs,
 // and wave v finalises row block v: 4 logits per lane, a running (logit, id) best per lane.
 // A ring of FSL blocks of weights per wave is in flight.
-template <int G>
-__device__ __forceinline__ void phase_f(const Args& a, const Rs& rs, int w, const Sm& sm, gu64* keys) {
+// DYN (persistent launches): the vocab blocks are split into a static part -- outer iterations
+// u < su of FSL blocks each, block w + G (FSL u + k) -- and a dynamic part of chunks of FSL
+// consecutive blocks from d0 = G FSL su, which the workgroups claim from an agent-scope counter
+// (fctr, zeroed for this step) three outer iterations ahead: a workgroup that runs slow beside
+// other grids claims fewer chunks, so the phase ends with the average workgroup instead of the
+// slowest (a logit's arithmetic does not depend on who computes it; the argmax is an exact
+// max).  Phase launches (DYN false) take every block statically.
+template <int G, bool DYN>
+__device__ __forceinline__ void phase_f(const Args& a, const Rs& rs, int w, const Sm& sm, gu64* keys,
+                                        gu32* fctr) {
   const int tid = otid(), v = tid >> 6, lane = tid & 63;
   u32x4_t xf[4 * QS];
   lda<4, QS>(rs.xb, KSD, 0, QS * v, xf);
   const int nvb = (a.V + 15) >> 4, lmv = 16 * nvb;    // lmb: [2][16 nvb] bias, then cs
-  const int nb = (nvb - w + G - 1) / G;
+  constexpr int NSL = Geo<G>::FSL;
+  int su = (nvb + G * NSL - 1) / (G * NSL);           // static: every block (past nvb: skipped)
+  bool dyn = false;
+  if constexpr (DYN) {
+    // ~5/8 of the blocks static (>= 3 outer iterations: the claims run 3 ahead), the rest claimed
+    const int s2 = max(3, (nvb * 5 / 8) / (G * NSL));
+    if (G * NSL * s2 <= nvb - G && a.exp == 0) { su = s2; dyn = true; }
+  }
+  const int d0 = G * NSL * su, nch = (nvb - d0 + NSL - 1) / NSL;
+  int* const chr = sm.misc + 12;   // LDS ring: the chunk claimed for outer iteration u at [u & 3]
+  // first block and block stride of outer iteration u's items (>= nvb: no items; read once per
+  // iteration into scalars, so the ring refills do not wait on LDS)
+  auto iter_blocks = [&](int u, int& b0, int& st) {
+    if (u < su) { b0 = w + G * NSL * u; st = G; }
+    else if (dyn) { b0 = d0 + NSL * __builtin_amdgcn_readfirstlane(chr[u & 3]); st = 1; }
+    else { b0 = 0x3fffffff; st = 0; }
+  };
   // ring of FSL block slots, each this wave's 6 weight fragments of the block; every refill is
-  // unconditional (block index clamped to the workgroup's last block: a conditional load left the
-  // compiler counting conservatively, vmcnt(0) before every block, one round trip per block).  The
-  // lane's 4 per-token biases and column sums of a block are loaded one block ahead (FSL even: the
-  // pair a block uses is fixed at compile time)
-  static_assert(Geo<G>::FSL % 2 == 0, "F ring: an even number of slots");
+  // unconditional (block index clamped to the last block: a conditional load left the compiler
+  // counting conservatively, vmcnt(0) before every block, one round trip per block).  The lane's 4
+  // per-token biases and column sums of a block are loaded one block ahead (FSL even: the pair a
+  // block uses is fixed at compile time)
+  static_assert(Geo<G>::FSL % 2 == 0 && Geo<G>::FSL >= 2, "F ring: an even number of slots");
   struct Slot {
     u32x4_t w[QS];
   };
-  constexpr int NSL = Geo<G>::FSL;
   Slot R[NSL];
-  auto fill = [&](int i, Slot& r) { ldw<1, QS>(a.wtep, KSD, w + G * min(i, nb - 1), QS * v, r.w); };
+  auto fill = [&](int b, Slot& r) { ldw<1, QS>(a.wtep, KSD, min(b, nvb - 1), QS * v, r.w); };
   float4 bq[2], cq[2];
-  auto fill_b = [&](int i, float4& b, float4& c) {
-    const int blk = w + G * min(i, nb - 1);
-    b = *reinterpret_cast<const float4*>(a.lmb + 16 * blk + 4 * (lane >> 4));
-    c = *reinterpret_cast<const float4*>(a.lmb + lmv + 16 * blk + 4 * (lane >> 4));
+  auto fill_b = [&](int b, float4& bb, float4& c) {
+    const int bc = min(b, nvb - 1);
+    bb = *reinterpret_cast<const float4*>(a.lmb + 16 * bc + 4 * (lane >> 4));
+    c = *reinterpret_cast<const float4*>(a.lmb + lmv + 16 * bc + 4 * (lane >> 4));
   };
-  static_for<NSL>([&](auto k) { fill(decltype(k)::value, R[decltype(k)::value]); });
-  fill_b(0, bq[0], cq[0]);
+  static_for<NSL>([&](auto k) { fill(w + G * decltype(k)::value, R[decltype(k)::value]); });
+  fill_b(w, bq[0], cq[0]);
   __builtin_amdgcn_sched_barrier(0);
   ln_stats<4>(xf, sm, 0);
   float bv = -INFINITY;
@@ -919,7 +999,7 @@ __device__ __forceinline__ void phase_f(const Args& a, const Rs& rs, int w, cons
   lds_sync();     // the previous phase's slab readers are done; the row statistics are in
   float mean, rstd;
   ln_row(sm, 16 * v + (lane & 15), mean, rstd);   // wave v finalises row block v
-  auto consume = [&](int i, const Slot& r, const float4& rb_, const float4& rc_) {
+  auto consume = [&](int b, const Slot& r, const float4& rb_, const float4& rc_) {
     f32x4_t acc[4];
 #pragma unroll
     for (int rb = 0; rb < 4; ++rb) acc[rb] = f32x4_t{0.f, 0.f, 0.f, 0.f};
@@ -933,7 +1013,7 @@ __device__ __forceinline__ void phase_f(const Args& a, const Rs& rs, int w, cons
     lds_sync();
     const f32x4_t sum = (red[v * 64 + lane] + red[(4 + v) * 64 + lane]) +
                         (red[(8 + v) * 64 + lane] + red[(12 + v) * 64 + lane]);
-    const int col0 = 16 * (w + G * i) + 4 * (lane >> 4);
+    const int col0 = 16 * b + 4 * (lane >> 4);
     const float4 lg4 = ln_fold(sum, mean, rstd, rc_, rb_);
     const float lgv[4] = {lg4.x, lg4.y, lg4.z, lg4.w};
 #pragma unroll
@@ -944,16 +1024,38 @@ __device__ __forceinline__ void phase_f(const Args& a, const Rs& rs, int w, cons
     }
     buf ^= 1;
   };
+  // claims (thread 0, dynamic part): at slot 1 of outer iteration u the chunk claimed at u - 1 is
+  // published for u + 2, and the chunk for u + 3 claimed -- before slot 1's ring refill, so the
+  // next iteration's wait for that refill has also waited for the claim (no extra round trip);
+  // the other waves read it after the next consume's workgroup barrier.  Claims only grow, so a
+  // workgroup's chunks end at its first invalid one (later claims are discarded; the counter of
+  // the other step parity is re-zeroed by workgroup 0 during the next step)
+  unsigned pend = 0;
+  int bu, stu;
+  iter_blocks(0, bu, stu);
+  // (an iteration whose first block is past the vocabulary has no items, and neither has any
+  // later one: static blocks grow with u, claimed chunks too)
 #pragma nounroll
-  for (int i = 0; i < nb; i += NSL) {
+  for (int u = 0; bu < nvb && u < su + nch; ++u) {
+    int bn, stn;
+    iter_blocks(u + 1, bn, stn);      // (u + 1's chunk: published at u - 1, slot 1)
     static_for<NSL>([&](auto kk) {
       constexpr int k = decltype(kk)::value;
-      if (k == 0 || i + k < nb) {                       // (wave-uniform)
-        fill_b(i + k + 1, bq[(k + 1) % 2], cq[(k + 1) % 2]);
-        consume(i + k, R[k], bq[k % 2], cq[k % 2]);
+      const int b = bu + k * stu;
+      if (b < nvb) {                                    // (wave-uniform)
+        fill_b(k + 1 < NSL ? b + stu : bn, bq[(k + 1) % 2], cq[(k + 1) % 2]);
+        consume(b, R[k], bq[k % 2], cq[k % 2]);
       }
-      fill(i + k + NSL, R[k]);
+      if constexpr (k == 1) {
+        if (dyn && tid == 0 && u >= su - 3) {
+          if (u >= su - 2) chr[(u + 2) & 3] = (int)pend;
+          pend = __hip_atomic_fetch_add(fctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+      }
+      fill(bn + k * stn, R[k]);
     });
+    bu = bn;
+    stu = stn;
   }
   // the 4 lanes of a row (l % 16 equal): larger logit, then the lower id
 #pragma unroll
@@ -1038,6 +1140,7 @@ __global__ __launch_bounds__(NT, 2) void dg_persist_kernel(Args a) {
   const Rs rs = make_rs(a.ws, a.exp);
   Bar bar{(gu32*)(a.ws + WS_SH), (gu32*)(a.ws + WS_TMO), 0, G / NSH, a.spin_max, nullptr, 0};
   gu64* const keys = (gu64*)(a.ws + WS_KEY);
+  gu32* const clm = (gu32*)(a.ws + WS_CLM);
   volatile lds_int_t* s_ok = (volatile lds_int_t*)(sm.misc + 8);
   unsigned long long* const stamps =
       (dp_stamp_ws == nullptr || dp_stamp_ws == a.ws) ? dp_stamp_buf : nullptr;
@@ -1066,9 +1169,13 @@ __global__ __launch_bounds__(NT, 2) void dg_persist_kernel(Args a) {
       u32x4_t kr[KU][KC], vr[KU][KC];
       attn_load<KU, KC>(a, l, sm, ub, 0, kr, vr);
       if (!bar_wait(bar, s_ok)) return gave_up(a);
-      if (l == 0 && w == 0 && otid() < RM)   // last step's keys: every workgroup has read them
+      if (l == 0 && w == 0 && otid() < RM) {  // last step's keys / F claims: every workgroup is done
         __hip_atomic_store(keys + ((step + 1) & 1) * RM + otid(), 0ull, __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
+        if (otid() == 0)
+          __hip_atomic_store(clm + (CLM_F + ((step + 1) & 1)) * 32, 0u, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+      }
       phase_b<KU, KC>(a, rs, l, sm, ub, kr, vr);
       bar_arrive(bar, w);
       u32x4_t wo[Gm::ECB * QS];
@@ -1094,7 +1201,7 @@ __global__ __launch_bounds__(NT, 2) void dg_persist_kernel(Args a) {
       else for (int i = 0; i < Gm::APF * QS; ++i) wq[i] = u32x4_t{0u, 0u, 0u, 0u};
       if (!bar_wait(bar, s_ok)) return gave_up(a);
     }
-    phase_f<G>(a, rs, w, sm, keys + (step & 1) * RM);
+    phase_f<G, true>(a, rs, w, sm, keys + (step & 1) * RM, clm + (CLM_F + (step & 1)) * 32);
     bar_arrive(bar, w);
     ldw<Gm::APF, QS>(a.wq[0], KSD, acb0, QS * V_, wq);
     if (!bar_wait(bar, s_ok)) return gave_up(a);
@@ -1149,7 +1256,7 @@ __global__ __launch_bounds__(NT, 2) void dg_phase_kernel(Args a) {
     f32x4_t xo{0.f, 0.f, 0.f, 0.f};
     phase_e<G, true>(a, rs, l, w, sm, wm, xo);
   } else {
-    phase_f<G>(a, rs, w, sm, (gu64*)(a.ws + WS_KEY));
+    phase_f<G, false>(a, rs, w, sm, (gu64*)(a.ws + WS_KEY), nullptr);
   }
 }
 // the step's bookkeeping (phase launches): one workgroup of 64 threads; zeroes the keys

@@ -672,6 +672,12 @@ static long nblocks(const GemmArgs& g, int bm, int bn) {
 int g_fast_ns = 2;     // zs_tune_set("fast_ns", n): stages of the 128x128 tile (experiment knob)
 int g_fast_tile = 0;   // zs_tune_set("fast_tile", t): force a tile (see dispatch_fast)
 int g_lean_min128 = 256;  // zs_tune_set("lean_min128", n): 128x128 2-stage tiles from n tiles up
+#ifndef ZS_LEAN128_NS
+#define ZS_LEAN128_NS 3
+#endif
+// zs_tune_set("lean128_ns", 3 | 4): stages of the 8-wave 128x128 tile taken at 128 <= n128 < 256
+// (3: 96 KiB of LDS, fits beside a grid-decode workgroup; 4: 128 KiB, round 4's tile)
+int g_lean128_ns = ZS_LEAN128_NS;
 
 // largest tile that still puts >= 1 block on every CU, else the smallest
 static int dispatch_fast(GemmArgs& g, hipStream_t st) {
@@ -719,7 +725,9 @@ static int dispatch_fast(GemmArgs& g, hipStream_t st) {
     if (lt == 1 || (!lt && n128 >= g_lean_min128)) return launch_lean<128, 128, 2, 64>(g, st);
     // (3 stages, 96 KiB of LDS: the 4-stage ring's 128 KiB does not fit beside a persistent decode
     // workgroup's 35 KiB, and the prefill would wait for a decode grid to end)
-    if (!lt && n128 >= 128) return launch_lean<128, 128, 3, 64, 2, 4>(g, st);
+    if (!lt && n128 >= 128)
+      return g_lean128_ns == 4 ? launch_lean<128, 128, 4, 64, 2, 4>(g, st)
+                               : launch_lean<128, 128, 3, 64, 2, 4>(g, st);
     if (lt == 2 || (!lt && nblocks(g, 128, 64) >= 256))
       return g.M >= g.N ? launch_lean<128, 64, 3, 64>(g, st) : launch_lean<64, 128, 3, 64>(g, st);
     // 64x64 with 128-deep k-steps when a 64x64 grid is still under one tile per CU at >= 512

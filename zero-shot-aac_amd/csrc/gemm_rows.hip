@@ -68,7 +68,10 @@ struct RowsArgs {
 // then fit beside a persistent decode workgroup (4 waves x 256 registers), so a begin's mapper
 // GEMM does not wait for a decode grid to end
 template <int NT, int WAVES, int LNM, int S>
-__global__ __launch_bounds__(64 * WAVES, WAVES == 8 ? 4 : 1) void gemm_rows_kernel(RowsArgs g) {
+#ifndef ZS_ROWS_MINB8
+#define ZS_ROWS_MINB8 4   // (-DZS_ROWS_MINB8=1: round 4's unbounded registers, for the A/B)
+#endif
+__global__ __launch_bounds__(64 * WAVES, WAVES == 8 ? ZS_ROWS_MINB8 : 1) void gemm_rows_kernel(RowsArgs g) {
   constexpr bool LN = LNM != 0, AFF = LNM == 1;
   // S = 32-deep k-steps per wave (K = 32 * WAVES * S), a template parameter so that every load
   // is issued unconditionally and up front (a runtime trip count put each load in its own

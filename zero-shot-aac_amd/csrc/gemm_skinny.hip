@@ -252,6 +252,7 @@ extern int g_logmel_wave;   // frontend.hip
 extern int g_lean96;        // gemm.hip
 extern int g_lean8w;        // gemm.hip
 extern int g_lean_min128;    // gemm.hip
+extern int g_lean128_ns;     // gemm.hip
 extern int g_lm_prio;       // gemm.hip
 extern int g_gemm_rows;     // gemm_rows.hip
 extern int g_rows_nt48;     // gemm_rows.hip
@@ -308,6 +309,7 @@ extern "C" int zs_tune_set(const char* key, int value) {
   if (!strcmp(key, "lean96")) { g_lean96 = value; return 0; }
   if (!strcmp(key, "lean8w")) { g_lean8w = value; return 0; }
   if (!strcmp(key, "lean_min128")) { g_lean_min128 = value; return 0; }
+  if (!strcmp(key, "lean128_ns")) { g_lean128_ns = value; return 0; }
   if (!strcmp(key, "lm_prio")) { g_lm_prio = value; return 0; }
   if (!strcmp(key, "gemm_rows")) { g_gemm_rows = value; return 0; }
   if (!strcmp(key, "rows_nt48")) { g_rows_nt48 = value; return 0; }

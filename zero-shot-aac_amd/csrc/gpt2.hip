@@ -13,7 +13,10 @@ namespace zs {
 // threads per prompt / label-top-k block: 8 waves (2 per SIMD at <= 128 registers) fit beside a
 // persistent decode workgroup (4 waves x 256 registers = half of every SIMD's register file), so a
 // batch's begin is never held back until a decode grid ends (1024 threads = 4 waves per SIMD did not)
-constexpr int PB = 512;
+#ifndef ZS_PROMPT_PB
+#define ZS_PROMPT_PB 512   // (-DZS_PROMPT_PB=1024: round 4's block, for the round-5 regression A/B)
+#endif
+constexpr int PB = ZS_PROMPT_PB;
 // sound_effect_choice (utils.py:131-137 / caption_model.py:15-20): the k labels of highest
 // similarity emb . label (softmax is monotone, so top-k of the raw similarities), best first,
 // ties to the lower label index; one block per row (PB threads: each wave dots one label row at a

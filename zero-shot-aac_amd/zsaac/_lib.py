@@ -12,7 +12,9 @@ import subprocess
 import threading
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libzsaac_hip.so")
+# ZSAAC_LIB: another in-tree build of the same sources (A/B variants, e.g. libzsaac_hip_r4b.so)
+LIB_PATH = (os.path.join(HERE, os.path.basename(os.environ["ZSAAC_LIB"]))
+            if os.environ.get("ZSAAC_LIB") else os.path.join(HERE, "libzsaac_hip.so"))
 CSRC = os.path.join(os.path.dirname(HERE), "csrc")
 
 ZS_F32, ZS_BF16 = 0, 1

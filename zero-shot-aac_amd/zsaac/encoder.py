@@ -179,6 +179,7 @@ class AudioEncoder:
         t = copy.copy(self)
         if max_batch:
             t.B = int(max_batch)
+        t._graphs = {}     # captured graphs read / write the parent's buffers: never shared
         t._alloc()
         return t
 

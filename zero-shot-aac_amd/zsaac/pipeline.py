@@ -539,6 +539,7 @@ class ConcurrentRunner:
                     break
                 p, s = self.pipes[i], self.streams[i]
                 p.decoder.persist_grid = g
+                p.decoder.persist_exclusive = False    # (not a value left over from run())
                 with torch.cuda.stream(s):
                     for ev in gate:          # the first round's launches: after every begin
                         s.wait_event(ev)
