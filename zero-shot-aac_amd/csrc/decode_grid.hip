@@ -962,7 +962,7 @@ __device__ __forceinline__ void phase_f(const Args& a, const Rs& rs, int w, cons
     const int s2 = max(3, (nvb * 5 / 8) / (G * NSL));
     if (G * NSL * s2 <= nvb - G && a.exp == 0) { su = s2; dyn = true; }
   }
-  const int d0 = G * NSL * su, nch = (nvb - d0 + NSL - 1) / NSL;
+  const int d0 = G * NSL * su, nch = dyn ? (nvb - d0 + NSL - 1) / NSL : 0;   // claimable chunks
   int* const chr = sm.misc + 12;   // LDS ring: the chunk claimed for outer iteration u at [u & 3]
   // first block and block stride of outer iteration u's items (>= nvb: no items; read once per
   // iteration into scalars, so the ring refills do not wait on LDS)
@@ -981,10 +981,10 @@ __device__ __forceinline__ void phase_f(const Args& a, const Rs& rs, int w, cons
     u32x4_t w[QS];
   };
   Slot R[NSL];
-  auto fill = [&](int b, Slot& r) { ldw<1, QS>(a.wtep, KSD, min(b, nvb - 1), QS * v, r.w); };
+  auto fill = [&](int b, Slot& r) { ldw<1, QS>(a.wtep, KSD, min(max(b, 0), nvb - 1), QS * v, r.w); };
   float4 bq[2], cq[2];
   auto fill_b = [&](int b, float4& bb, float4& c) {
-    const int bc = min(b, nvb - 1);
+    const int bc = min(max(b, 0), nvb - 1);
     bb = *reinterpret_cast<const float4*>(a.lmb + 16 * bc + 4 * (lane >> 4));
     c = *reinterpret_cast<const float4*>(a.lmb + lmv + 16 * bc + 4 * (lane >> 4));
   };
@@ -1090,7 +1090,10 @@ __device__ __forceinline__ void bookkeep(const A& a, const Sm& sm, gu64* keys, i
   int alive = 0;
   if (tid < RM) {
     const unsigned long long key = __hip_atomic_load(keys + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const int t = (int)~(unsigned)key;
+    // (a key no workgroup raised -- impossible unless the vocabulary pass skipped a row's every
+    // block -- would read as id -1: clamped, so a broken pass shows as wrong ids, never as an
+    // out-of-bounds embedding read next step)
+    const int t = min(max((int)~(unsigned)key, 0), a.V - 1);
     if (tid < a.R) {
       int d = sm.done[tid];
       if (!d) {
