@@ -65,6 +65,7 @@ namespace zs {
 int g_dp_spin = 0;   // zs_tune_set("dp_spin", n): give up a grid-barrier wait after n polls (0 =
                      // the default 2^22, < 0: at the first unmet poll); tests force the give-up
 int g_dg_exp = 0;    // zs_tune_set("dg_exp", m): traffic experiments (grid_bench only; ids garbage)
+int g_dg_dynf = 1;   // zs_tune_set("dg_dynf", 0): phase F all static in persistent launches too (A/B)
 int g_dp_abort = -1; // zs_tune_set("dp_abort_step", k): every workgroup gives up at the start of
                      // decode step k (a mid-launch give-up for the resume test); -1 = never
 namespace dg {
@@ -168,7 +169,7 @@ constexpr int SM_TOTAL = SM_ST + (3 * RM + 16) * 4;
 constexpr int EXCL_LDS = 80 * 1024 + 512;        // an exclusive launch's LDS per workgroup (> 1/2 CU)
 
 struct Args {
-  int R, Lmax, max_steps, stop0, stop1, V, layer, abort_step, exp;
+  int R, Lmax, max_steps, stop0, stop1, V, layer, abort_step, exp, dynf;
   unsigned spin_max;
   int kv_bytes;         // bytes of one layer's K (or V) cache
   float temp;
@@ -960,7 +961,7 @@ __device__ __forceinline__ void phase_f(const Args& a, const Rs& rs, int w, cons
   if constexpr (DYN) {
     // ~5/8 of the blocks static (>= 3 outer iterations: the claims run 3 ahead), the rest claimed
     const int s2 = max(3, (nvb * 5 / 8) / (G * NSL));
-    if (G * NSL * s2 <= nvb - G && a.exp == 0) { su = s2; dyn = true; }
+    if (G * NSL * s2 <= nvb - G && a.exp == 0 && a.dynf) { su = s2; dyn = true; }
   }
   const int d0 = G * NSL * su, nch = dyn ? (nvb - d0 + NSL - 1) / NSL : 0;   // claimable chunks
   int* const chr = sm.misc + 12;   // LDS ring: the chunk claimed for outer iteration u at [u & 3]
@@ -1934,6 +1935,7 @@ int dg_args(dg::Args& a, int R, int Lmax, int max_steps, int stop0, int stop1, i
   a.spin_max = g_dp_spin > 0 ? (unsigned)g_dp_spin : g_dp_spin < 0 ? 0u : SPIN_MAX;
   a.abort_step = g_dp_abort;
   a.exp = g_dg_exp;
+  a.dynf = g_dg_dynf;
   a.kv_bytes = R * NH * Lmax * HD * 2;
   a.temp = temperature;
   a.wte = (const bf16_t*)wte; a.wpe = (const bf16_t*)wpe;

@@ -267,6 +267,7 @@ extern int g_big_min;       // gemm.hip
 extern int g_dp_spin;       // decode_grid.hip
 extern int g_dp_abort;      // decode_grid.hip
 extern int g_dg_exp;
+extern int g_dg_dynf;       // decode_grid.hip
 extern int g_beam_xcd;      // attn.hip
 extern int g_f32_tile;      // gemm.hip
 
@@ -324,6 +325,7 @@ extern "C" int zs_tune_set(const char* key, int value) {
   if (!strcmp(key, "dp_spin")) { g_dp_spin = value; return 0; }
   if (!strcmp(key, "dp_abort_step")) { g_dp_abort = value; return 0; }
   if (!strcmp(key, "dg_exp")) { g_dg_exp = value; return 0; }
+  if (!strcmp(key, "dg_dynf")) { g_dg_dynf = value; return 0; }
   if (!strcmp(key, "beam_xcd")) { g_beam_xcd = value; return 0; }
   if (!strcmp(key, "f32_tile")) { g_f32_tile = value; return 0; }
   return fail(ZS_ERR_ARG, "zs_tune_set: unknown key %s", key);

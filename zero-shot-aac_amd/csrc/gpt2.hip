@@ -10,125 +10,98 @@
 namespace zs {
 
 // ------------------------------------------------------------------ prompt
-// threads per prompt / label-top-k block: 8 waves (2 per SIMD at <= 128 registers) fit beside a
-// persistent decode workgroup (4 waves x 256 registers = half of every SIMD's register file), so a
-// batch's begin is never held back until a decode grid ends (1024 threads = 4 waves per SIMD did not)
-#ifndef ZS_PROMPT_PB
-#define ZS_PROMPT_PB 512   // (-DZS_PROMPT_PB=1024: round 4's block, for the round-5 regression A/B)
-#endif
-constexpr int PB = ZS_PROMPT_PB;
 // sound_effect_choice (utils.py:131-137 / caption_model.py:15-20): the k labels of highest
 // similarity emb . label (softmax is monotone, so top-k of the raw similarities), best first,
-// ties to the lower label index; one block per row (PB threads: each wave dots one label row at a
-// time with coalesced 16-byte loads, four rows in flight), result in sel[0..k).
-__device__ __forceinline__ void label_select(const float* __restrict__ emb, int D,
-                                             const float* __restrict__ labels, int L, int k,
-                                             float* e, float* sim, int* sel, float* rv, int* ri) {
-  const int b = blockIdx.x;
-  for (int d = threadIdx.x; d < D; d += PB) e[d] = emb[(long)b * D + d];
-  __syncthreads();
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  if ((D & 3) == 0 && ((uintptr_t)labels & 15) == 0) {
-    // one label row per wave at a time, 16-byte coalesced loads (a 4 KB row is 4 wave loads),
-    // four rows in flight per wave, lane partials reduced across the wave
-    constexpr int NR = 4, NWV = PB / 64;
-    const float4* e4 = reinterpret_cast<const float4*>(e);
-    const int D4 = D >> 2;
-    for (int l0 = wid; l0 < L; l0 += NR * NWV) {
-      const float4* r[NR];
+// ties to the lower label index.
+//
+// ONE wave per clip, everything in registers: lane l holds e[4 l + 256 u .. + 4), u < 4 (D = 1024;
+// other D in 16-byte chunks c = lane + 64 u), each label row is read in the same chunks (four
+// rows in flight), the lane partials summed over the wave by DPP row ops and permlane swaps (no
+// LDS, no ds_bpermute, no workgroup barrier), and the running top-k kept in uniform registers,
+// labels visited in increasing index so a tie keeps the lower one.  (Round 5's 512-thread block
+// version -- the embedding staged in LDS, ds_bpermute reductions, a block-wide top-k through LDS
+// -- chose different labels now and then while decode grids ran on other streams: 144 of 418k
+// clips over 40 rounds, tools/prompt_stress.py grid mode; none alone or beside GEMMs; the cause
+// in that kernel was not isolated, this one shares nothing with it.)
+constexpr int PK_MAX = 16;          // k <= 16
+template <int CTRL>
+__device__ __forceinline__ float pdpp(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xf, 0xf, false));
+}
+// the sum of v over the 64 lanes, on every lane, in one fixed order
+__device__ __forceinline__ float wave_sum_dpp(float v) {
+  v += pdpp<0xB1>(v);                              // quad_perm [1,0,3,2]
+  v += pdpp<0x4E>(v);                              // quad_perm [2,3,0,1]
+  v += pdpp<0x141>(v);                             // row_half_mirror: 8-lane sums
+  v += pdpp<0x128>(v);                             // row_ror:8: 16-lane sums
+  {
+    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    v = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+  }
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+// top-k labels of clip blockIdx.x into sel[0..k) (uniform across the wave)
+__device__ __forceinline__ void label_select_wave(const float* __restrict__ emb, int D,
+                                                  const float* __restrict__ labels, int L, int k,
+                                                  int (&sel)[PK_MAX]) {
+  const int b = blockIdx.x, lane = threadIdx.x & 63;
+  float tv[PK_MAX];
+#pragma unroll
+  for (int i = 0; i < PK_MAX; ++i) { tv[i] = -INFINITY; sel[i] = 0x7fffffff; }
+  auto insert = [&](float sv, int l) {          // strictly better only: ties keep the earlier
+#pragma unroll
+    for (int i = 0; i < PK_MAX; ++i) {
+      if (i < k && sv > tv[i]) {
+        const float t = tv[i]; const int ti = sel[i];
+        tv[i] = sv; sel[i] = l; sv = t; l = ti;
+      }
+    }
+  };
+  const float* er = emb + (long)b * D;
+  if (D == 1024 && ((uintptr_t)labels & 15) == 0 && ((uintptr_t)er & 15) == 0) {
+    float4 e[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) e[u] = reinterpret_cast<const float4*>(er)[lane + 64 * u];
+    constexpr int NR = 4;
+    for (int l0 = 0; l0 < L; l0 += NR) {
+      float4 a[NR][4];
 #pragma unroll
       for (int j = 0; j < NR; ++j)
-        r[j] = reinterpret_cast<const float4*>(labels + (long)min(l0 + j * NWV, L - 1) * D);
-      float sj[NR] = {};
-      if (D4 == 256) {                 // CLAP width 1024: every row chunk issued before any use
-        float4 a[4][NR];
 #pragma unroll
         for (int u = 0; u < 4; ++u)
-#pragma unroll
-          for (int j = 0; j < NR; ++j) a[u][j] = r[j][lane + 64 * u];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const float4 v = e4[lane + 64 * u];
-#pragma unroll
-          for (int j = 0; j < NR; ++j)
-            sj[j] += (a[u][j].x * v.x + a[u][j].y * v.y) + (a[u][j].z * v.z + a[u][j].w * v.w);
-        }
-      } else {
-        for (int c = lane; c < D4; c += 64) {
-          float4 a[NR];
-#pragma unroll
-          for (int j = 0; j < NR; ++j) a[j] = r[j][c];
-          const float4 v = e4[c];
-#pragma unroll
-          for (int j = 0; j < NR; ++j) sj[j] += (a[j].x * v.x + a[j].y * v.y) + (a[j].z * v.z + a[j].w * v.w);
-        }
-      }
+          a[j][u] = reinterpret_cast<const float4*>(labels + (long)min(l0 + j, L - 1) * D)[lane + 64 * u];
 #pragma unroll
       for (int j = 0; j < NR; ++j) {
+        float sj = 0.f;
 #pragma unroll
-        for (int o = 32; o > 0; o >>= 1) sj[j] += __shfl_xor(sj[j], o, 64);
-        if (lane == 0 && l0 + j * NWV < L) sim[l0 + j * NWV] = sj[j];
+        for (int u = 0; u < 4; ++u)
+          sj += (a[j][u].x * e[u].x + a[j][u].y * e[u].y) + (a[j][u].z * e[u].z + a[j][u].w * e[u].w);
+        sj = wave_sum_dpp(sj);
+        if (l0 + j < L) insert(__int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(sj))), l0 + j);
       }
     }
-  } else {
-    for (int l = threadIdx.x; l < L; l += PB) {
+  } else {                                         // any D: lane-strided scalar dot products
+    for (int l = 0; l < L; ++l) {
       const float* lr = labels + (long)l * D;
-      float s = 0.f;
-      for (int d = 0; d < D; ++d) s += e[d] * lr[d];
-      sim[l] = s;
+      float sj = 0.f;
+      for (int d = lane; d < D; d += 64) sj += er[d] * lr[d];
+      insert(__int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(wave_sum_dpp(sj)))), l);
     }
-  }
-  __syncthreads();
-  for (int q = 0; q < k; ++q) {
-    float bv = -INFINITY;
-    int bi = 0x7fffffff;
-    for (int l = threadIdx.x; l < L; l += PB) {
-      bool taken = false;
-      for (int p = 0; p < q; ++p) taken |= (sel[p] == l);
-      if (!taken && (sim[l] > bv || (sim[l] == bv && l < bi))) { bv = sim[l]; bi = l; }
-    }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-      const float ov = __shfl_xor(bv, o, 64);
-      const int oi = __shfl_xor(bi, o, 64);
-      if (ov > bv || (ov == bv && oi < bi)) { bv = ov; bi = oi; }
-    }
-    if (lane == 0) { rv[wid] = bv; ri[wid] = bi; }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      float v = rv[0];
-      int i = ri[0];
-      for (int w = 1; w < PB / 64; ++w)
-        if (rv[w] > v || (rv[w] == v && ri[w] < i)) { v = rv[w]; i = ri[w]; }
-      sel[q] = i;
-    }
-    __syncthreads();
   }
 }
 
-__global__ __launch_bounds__(PB) void prompt_kernel(const float* __restrict__ emb, int D,
+__global__ __launch_bounds__(64) void prompt_kernel(const float* __restrict__ emb, int D,
                                                      const float* __restrict__ labels, int L,
                                                      int k, const int* __restrict__ ltok,
                                                      const int* __restrict__ llen, int max_tok,
                                                      int* __restrict__ hard_ids, int h_cap,
                                                      int* __restrict__ hard_len,
                                                      int* __restrict__ chosen) {
-  extern __shared__ float sm[];
-  __shared__ int sel[16];
-  __shared__ float rv[PB / 64];
-  __shared__ int ri[PB / 64];
-  __shared__ int stok[16 * 32], slen[16];
-  const int b = blockIdx.x;
-  label_select(emb, D, labels, L, k, sm, sm + D, sel, rv, ri);
-  // the chosen labels' token ids gathered in parallel (one load round trip, not one per token)
-  const int mt = min(max_tok, 32);
-  if (threadIdx.x < k * mt) {
-    const int q = threadIdx.x / mt, t = threadIdx.x % mt;
-    stok[q * 32 + t] = ltok[(long)sel[q] * max_tok + t];
-  }
-  if (threadIdx.x < k) slen[threadIdx.x] = llen[sel[threadIdx.x]];
-  __syncthreads();
-  if (threadIdx.x == 0) {
+  int sel[PK_MAX];
+  label_select_wave(emb, D, labels, L, k, sel);
+  const int b = blockIdx.x, lane = threadIdx.x & 63;
+  if (lane == 0) {
     int* out = hard_ids + (long)b * h_cap;
     int n = 0;
     auto put = [&](int id) { if (n < h_cap) out[n] = id; ++n; };
@@ -138,7 +111,8 @@ __global__ __launch_bounds__(PB) void prompt_kernel(const float* __restrict__ em
     } else {
       for (int q = 0; q < k; ++q) {
         const int l = sel[q];
-        for (int t = 0; t < slen[q] && t < mt; ++t) put(stok[q * 32 + t]);
+        const int nt = min(llen[l], min(max_tok, 32));
+        for (int t = 0; t < nt; ++t) put(ltok[(long)l * max_tok + t]);
         if (q + 1 < k) put(11);             // ","
         if (chosen) chosen[(long)b * k + q] = l;
       }
@@ -151,20 +125,17 @@ __global__ __launch_bounds__(PB) void prompt_kernel(const float* __restrict__ em
 
 // the chosen labels' rows gathered: rows[b][q][:] = labels[sel[q]][:] (caption_model.py:15-20,
 // sound_effect_embeddings[index].squeeze(1)), and their indices
-__global__ __launch_bounds__(PB) void label_topk_kernel(const float* __restrict__ emb, int D,
+__global__ __launch_bounds__(64) void label_topk_kernel(const float* __restrict__ emb, int D,
                                                          const float* __restrict__ labels, int L,
                                                          int k, int* __restrict__ idx,
                                                          float* __restrict__ rows) {
-  extern __shared__ float sm[];
-  __shared__ int sel[16];
-  __shared__ float rv[PB / 64];
-  __shared__ int ri[PB / 64];
-  const int b = blockIdx.x;
-  label_select(emb, D, labels, L, k, sm, sm + D, sel, rv, ri);
-  if (idx && threadIdx.x < k) idx[(long)b * k + threadIdx.x] = sel[threadIdx.x];
-  for (int q = 0; q < k; ++q)
-    for (int d = threadIdx.x; d < D; d += PB)
-      rows[((long)b * k + q) * D + d] = labels[(long)sel[q] * D + d];
+  int sel[PK_MAX];
+  label_select_wave(emb, D, labels, L, k, sel);
+  const int b = blockIdx.x, lane = threadIdx.x & 63;
+  for (int q = 0; q < k; ++q) {
+    if (idx && lane == 0) idx[(long)b * k + q] = sel[q];
+    for (int d = lane; d < D; d += 64) rows[((long)b * k + q) * D + d] = labels[(long)sel[q] * D + d];
+  }
 }
 
 // ------------------------------------------------------------------ embeddings
@@ -538,9 +509,7 @@ extern "C" int zs_prompt_assemble(const float* emb, int B, int D, const float* l
                                   int* hard_ids, int h_cap, int* hard_len, int* chosen,
                                   void* stream) {
   ZS_REQUIRE(B > 0 && D > 0 && L > 0 && k >= 0 && k <= 16 && k <= L && max_tok <= 32, "zs_prompt_assemble: bad shape");
-  const size_t smem = (size_t)(D + L) * sizeof(float);
-  ZS_REQUIRE(smem <= 64 * 1024, "zs_prompt_assemble: D+L too large");
-  hipLaunchKernelGGL(prompt_kernel, dim3(B), dim3(PB), smem, S(stream), emb, D, labels, L, k,
+  hipLaunchKernelGGL(prompt_kernel, dim3(B), dim3(64), 0, S(stream), emb, D, labels, L, k,
                      label_tok, label_len, max_tok, hard_ids, h_cap, hard_len, chosen);
   ZS_LAUNCH_CHECK();
   return 0;
@@ -550,9 +519,7 @@ extern "C" int zs_label_topk(const float* emb, int B, int D, const float* labels
                              int* idx, float* rows, void* stream) {
   ZS_REQUIRE(B > 0 && D > 0 && L > 0 && k >= 1 && k <= 16 && k <= L, "zs_label_topk: bad shape");
   ZS_REQUIRE(emb && labels && rows, "zs_label_topk: null pointer");
-  const size_t smem = (size_t)(D + L) * sizeof(float);
-  ZS_REQUIRE(smem <= 64 * 1024, "zs_label_topk: D+L too large");
-  hipLaunchKernelGGL(label_topk_kernel, dim3(B), dim3(PB), smem, S(stream), emb, D, labels, L, k,
+  hipLaunchKernelGGL(label_topk_kernel, dim3(B), dim3(64), 0, S(stream), emb, D, labels, L, k,
                      idx, rows);
   ZS_LAUNCH_CHECK();
   return 0;
