@@ -343,79 +343,30 @@ __device__ __forceinline__ void bar_arrive(Bar& b, int w) {
   stamp(b.sb, 2 * (b.n - b.n0));
   ++b.n;
 }
-// The poll keeps 3 shard reads in flight (each issued DG_SLEEP x 64 clocks after the previous
-// one, consumed oldest first): a serial poll sees the last arrival one read latency plus up to
-// one more poll period late (under 9 other grids that latency is ~1-2 us, and the workgroups
-// detecting a barrier late were the next phase's last arrivers: release spread 2 us,
-// tools/persist_stamps.py); with reads in flight the period shrinks to about a third of it.
-#define DG_STR_(x) #x
-#define DG_STR(x) DG_STR_(x)
-// A workgroup that gives up raises every shard to >= GIVEUP, so every other workgroup's poll sees its
-// barrier "met" with a value >= GIVEUP and gives up too (the timeout word is only for the host,
-// zs_decode_persist_status): no second load in the poll loop, whose reads stay counted.
-constexpr unsigned GIVEUP = 1u << 30;
+// (round 6 A/B, tools/grid_bench.py + tools/persist_stamps.py: keeping 3 shard reads in flight --
+// a hand-written pipelined poll -- cut no barrier wait under load and took 12 % of ten G48 grids'
+// aggregate rate (10.2k vs 11.6k steps/s; loaded step 747 vs 682 us): the extra reads slow the
+// co-resident workgroups more than the earlier detection gains.  The poll stays serial.)
 __device__ __forceinline__ bool bar_wait(Bar& b, volatile lds_int_t* s_ok) {
   if (threadIdx.x < 64) {
     const int lane = threadIdx.x;
     const unsigned target = b.n * b.per;
     unsigned spins = 0;
     int ok = 1;
-    // (hand-written: compiled from C++, the rotation of the reads in flight through the loop's
-    // registers made the compiler wait for every read at the end of each round.  Every lane
-    // reads shard lane % NSH -- the duplicate lanes share the 8 lines' requests -- and the
-    // loop ends with vmcnt(0): no read of it is left in flight into a register it gave back)
-    const gu32* addr = b.sh + (lane & (NSH - 1)) * 32;
-    unsigned c0, c1, c2, cm;
-    asm volatile(
-        "global_load_dword %[c0], %[ad], off sc1\n\t"
-        "s_sleep " DG_STR(DG_SLEEP) "\n\t"
-        "global_load_dword %[c1], %[ad], off sc1\n\t"
-        "s_sleep " DG_STR(DG_SLEEP) "\n\t"
-        "global_load_dword %[c2], %[ad], off sc1\n\t"
-        "s_mov_b32 %[sp], 0\n"
-        "1:\n\t"
-        "s_waitcnt vmcnt(2)\n\t"
-        "v_cmp_gt_u32 vcc, %[tg], %[c0]\n\t"
-        "s_cbranch_vccz 2f\n\t"
-        "s_sleep " DG_STR(DG_SLEEP) "\n\t"
-        "global_load_dword %[c0], %[ad], off sc1\n\t"
-        "s_waitcnt vmcnt(2)\n\t"
-        "v_cmp_gt_u32 vcc, %[tg], %[c1]\n\t"
-        "s_cbranch_vccz 3f\n\t"
-        "s_sleep " DG_STR(DG_SLEEP) "\n\t"
-        "global_load_dword %[c1], %[ad], off sc1\n\t"
-        "s_waitcnt vmcnt(2)\n\t"
-        "v_cmp_gt_u32 vcc, %[tg], %[c2]\n\t"
-        "s_cbranch_vccz 4f\n\t"
-        "s_sleep " DG_STR(DG_SLEEP) "\n\t"
-        "global_load_dword %[c2], %[ad], off sc1\n\t"
-        "s_add_u32 %[sp], %[sp], 3\n\t"
-        "s_cmp_gt_u32 %[sp], %[sm]\n\t"
-        "s_cbranch_scc0 1b\n\t"
-        "v_mov_b32 %[cm], 0\n\t"
-        "s_branch 5f\n"
-        "2:\n\t"
-        "v_mov_b32 %[cm], %[c0]\n\t"
-        "s_branch 5f\n"
-        "3:\n\t"
-        "v_mov_b32 %[cm], %[c1]\n\t"
-        "s_branch 5f\n"
-        "4:\n\t"
-        "v_mov_b32 %[cm], %[c2]\n"
-        "5:\n\t"
-        "s_waitcnt vmcnt(0)"
-        : [c0] "=&v"(c0), [c1] "=&v"(c1), [c2] "=&v"(c2), [cm] "=&v"(cm), [sp] "=&s"(spins)
-        : [ad] "v"(addr), [tg] "s"(target), [sm] "s"(b.spin_max)
-        : "vcc", "scc", "memory");
-    if (spins > b.spin_max) {
+    for (;;) {
+      const unsigned c = lane < NSH
+          ? __hip_atomic_load(b.sh + lane * 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : target;
+      if (__ballot(c < target) == 0) break;
+      ++spins;
       // bounded: give up (and tell every other workgroup) after spin_max polls, so a grid that
       // is not co-resident drains instead of hanging
-      // (a max, not an add: several workgroups may give up at once)
-      if (lane < NSH) __hip_atomic_fetch_max(b.sh + lane * 32, GIVEUP, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (lane == 0) __hip_atomic_store(b.tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      ok = 0;
-    } else if (__ballot(cm >= GIVEUP) != 0) {
-      ok = 0;                                    // another workgroup gave up
+      if (spins > b.spin_max ||
+          ((spins & 255) == 0 && __hip_atomic_load(b.tmo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
+        if (lane == 0) __hip_atomic_store(b.tmo, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        ok = 0;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(DG_SLEEP);
     }
     if (lane == 0) *s_ok = ok;
   }

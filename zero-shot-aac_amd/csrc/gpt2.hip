@@ -41,17 +41,22 @@ __device__ __forceinline__ float wave_sum_dpp(float v) {
   const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
   return __uint_as_float(r[0]) + __uint_as_float(r[1]);
 }
-// top-k labels of clip blockIdx.x into sel[0..k) (uniform across the wave)
-__device__ __forceinline__ void label_select_wave(const float* __restrict__ emb, int D,
-                                                  const float* __restrict__ labels, int L, int k,
-                                                  int (&sel)[PK_MAX]) {
+// top-k labels of clip blockIdx.x into sel[0..k) (uniform across the wave); K = k (3, the
+// reference's sound_effect_num) or PK_MAX (any k <= 16)
+template <int K>
+__device__ __forceinline__ void label_select_k(const float* __restrict__ emb, int D,
+                                               const float* __restrict__ labels, int L, int k,
+                                               int (&sel)[PK_MAX]) {
   const int b = blockIdx.x, lane = threadIdx.x & 63;
-  float tv[PK_MAX];
+  float tv[K];
 #pragma unroll
-  for (int i = 0; i < PK_MAX; ++i) { tv[i] = -INFINITY; sel[i] = 0x7fffffff; }
+  for (int i = 0; i < K; ++i) tv[i] = -INFINITY;
+#pragma unroll
+  for (int i = 0; i < PK_MAX; ++i) sel[i] = 0x7fffffff;
   auto insert = [&](float sv, int l) {          // strictly better only: ties keep the earlier
+    if (K != PK_MAX && !(sv > tv[K - 1])) return;   // (K == k: below the k-th best)
 #pragma unroll
-    for (int i = 0; i < PK_MAX; ++i) {
+    for (int i = 0; i < K; ++i) {
       if (i < k && sv > tv[i]) {
         const float t = tv[i]; const int ti = sel[i];
         tv[i] = sv; sel[i] = l; sv = t; l = ti;
@@ -63,14 +68,16 @@ __device__ __forceinline__ void label_select_wave(const float* __restrict__ emb,
     float4 e[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) e[u] = reinterpret_cast<const float4*>(er)[lane + 64 * u];
+    // four label rows per group, the next group's loads issued before this group's sums
     constexpr int NR = 4;
-    for (int l0 = 0; l0 < L; l0 += NR) {
-      float4 a[NR][4];
+    auto load = [&](int l0, float4 (&a)[NR][4]) {
 #pragma unroll
       for (int j = 0; j < NR; ++j)
 #pragma unroll
         for (int u = 0; u < 4; ++u)
           a[j][u] = reinterpret_cast<const float4*>(labels + (long)min(l0 + j, L - 1) * D)[lane + 64 * u];
+    };
+    auto consume = [&](int l0, const float4 (&a)[NR][4]) {
 #pragma unroll
       for (int j = 0; j < NR; ++j) {
         float sj = 0.f;
@@ -80,6 +87,14 @@ __device__ __forceinline__ void label_select_wave(const float* __restrict__ emb,
         sj = wave_sum_dpp(sj);
         if (l0 + j < L) insert(__int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(sj))), l0 + j);
       }
+    };
+    float4 a0[NR][4], a1[NR][4];
+    load(0, a0);
+    for (int l0 = 0; l0 < L; l0 += 2 * NR) {
+      load(l0 + NR, a1);
+      consume(l0, a0);
+      load(l0 + 2 * NR, a0);
+      if (l0 + NR < L) consume(l0 + NR, a1);
     }
   } else {                                         // any D: lane-strided scalar dot products
     for (int l = 0; l < L; ++l) {
@@ -89,6 +104,12 @@ __device__ __forceinline__ void label_select_wave(const float* __restrict__ emb,
       insert(__int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(wave_sum_dpp(sj)))), l);
     }
   }
+}
+__device__ __forceinline__ void label_select_wave(const float* __restrict__ emb, int D,
+                                                  const float* __restrict__ labels, int L, int k,
+                                                  int (&sel)[PK_MAX]) {
+  if (k == 3) label_select_k<3>(emb, D, labels, L, k, sel);
+  else label_select_k<PK_MAX>(emb, D, labels, L, k, sel);
 }
 
 __global__ __launch_bounds__(64) void prompt_kernel(const float* __restrict__ emb, int D,
