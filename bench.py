@@ -133,6 +133,9 @@ def parse(argv=None):
                          "encodes consecutive eval batches together on a stream of its own, each "
                          "batch's begin waits for its own pass; 0 = every batch encodes its own "
                          "clips at --batch)")
+    ap.add_argument("--cu-split", type=int, default=0,
+                    help="A/B: CUs reserved (by stream CU masks) for the begins; the decode "
+                         "grids get the rest (0: no split)")
     ap.add_argument("--persist-budget", type=int, default=0,
                     help="workgroup slots (half a CU each) the in-flight persistent decode grids "
                          "may hold together (0: ZSAAC_PERSIST_BUDGET or 1.5 per CU)")
@@ -277,7 +280,7 @@ def run_captions(args, world, rank, device, pipe, n_local, first, counts, inflig
                               streams=run_streams(device, max(1, inflight) + extra),
                               budget=getattr(args, "persist_budget", 0) or None,
                               encode_ahead=ahead, enc_stream=enc_stream(device) if ahead else None,
-                              extra_pipes=extra)
+                              extra_pipes=extra, cu_split=getattr(args, "cu_split", 0))
     for size in sorted({b.shape[0] for b in batches}, reverse=True):   # captures every graph
         runner.warmup(next(b for b in batches if b.shape[0] == size))
         log(f"captured the decode graphs of {size}-clip batches")

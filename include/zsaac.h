@@ -41,6 +41,10 @@ int zs_tune_set(const char* key, int value);  /* tuning knobs, e.g. "skinny_mode
  * streams (two streams sharing a hardware queue serialize).  priority < 0: the device's highest
  * stream priority, > 0: its lowest, 0: the default. */
 int zs_stream_create(void** stream, int priority);
+/* zs_stream_create_masked: the same, restricted to the CUs whose bits are set in cu_mask
+ * (mask_words 32-bit words, bit i = CU i, hipExtStreamCreateWithCUMask): the caption runner's
+ * optional split of the chip between the begins (prompt .. step 0) and the decode grids. */
+int zs_stream_create_masked(void** stream, const unsigned* cu_mask, int mask_words);
 int zs_stream_destroy(void* stream);
 
 /* ------------------------------------------------------------------ audio front end

@@ -65,6 +65,18 @@ extern "C" int zs_stream_create(void** stream, int priority) {
   return 0;
 }
 
+extern "C" int zs_stream_create_masked(void** stream, const unsigned* cu_mask, int mask_words) {
+  if (!stream || !cu_mask || mask_words <= 0 || mask_words > 64) return ZS_ERR_ARG;
+  static int* scratch = nullptr;
+  if (!scratch) ZS_CHECK_HIP(hipMalloc(&scratch, 256));
+  hipStream_t s = nullptr;
+  ZS_CHECK_HIP(hipExtStreamCreateWithCUMask(&s, (uint32_t)mask_words, cu_mask));
+  ZS_CHECK_HIP(hipMemsetAsync(scratch, 0, 4, s));
+  ZS_CHECK_HIP(hipStreamSynchronize(s));
+  *stream = (void*)s;
+  return 0;
+}
+
 extern "C" int zs_stream_destroy(void* stream) {
   if (!stream) return ZS_ERR_ARG;
   ZS_CHECK_HIP(hipStreamDestroy((hipStream_t)stream));

@@ -347,6 +347,36 @@ def dedicated_streams(n: int, device, priority: int = 0) -> list:
     return out
 
 
+def cu_split_masks(cus: int, n_begin: int):
+    """(begin mask, grid mask) as lists of 32-bit words: n_begin of the device's cus CUs for the
+    begins, the rest for the decode grids.  The begin CUs are taken evenly over the bit range in
+    a pattern that lands on every XCD whether the driver deals mask bits to XCDs in blocks of
+    cus / 8 or round-robin: bit i when ((i >> 3) & 3) == (i & 3) (a quarter of the CUs), trimmed
+    or padded in bit order to n_begin."""
+    words = (cus + 31) // 32
+    pick = [i for i in range(cus) if ((i >> 3) & 3) == (i & 3)]
+    rest = [i for i in range(cus) if i not in set(pick)]
+    chosen = set((pick + rest)[:n_begin])
+    b = [0] * words
+    g = [0] * words
+    for i in range(cus):
+        (b if i in chosen else g)[i // 32] |= 1 << (i % 32)
+    return b, g
+
+
+def masked_streams(n: int, device, mask) -> list:
+    """n new HIP streams on the CUs of ``mask`` (zs_stream_create_masked), as torch streams."""
+    import ctypes as C
+    arr = (C.c_uint * len(mask))(*mask)
+    out = []
+    with torch.cuda.device(device):
+        for _ in range(n):
+            h = C.c_void_p()
+            call("zs_stream_create_masked", C.byref(h), arr, len(mask))
+            out.append(torch.cuda.ExternalStream(h.value, device=device))
+    return out
+
+
 def decode_attention_map(qkv, R, rowmap, nphys, D, heads, kc, vc, Lmax, pos, out, cpos=None):
     """decode_attention over compact slots c < R whose physical row is rowmap[c]."""
     call("zs_decode_attention_map", _p(qkv), R, _p(rowmap), nphys, D, heads, _p(kc), _p(vc), Lmax,

@@ -271,6 +271,9 @@ def choose_persist_grid(in_flight: int, to_begin: int, grids: List[int], budget:
     return g_min
 
 
+_SPLIT_STREAMS = {}     # (device, CUs, begin CUs) -> (begin streams, grid streams)
+
+
 class ConcurrentRunner:
     """Keeps several independent bs=`cfg.batch` batches in flight on one GPU: pipeline twins
     (shared weights, private buffers/KV cache/graphs), each on its own HIP stream.  A batch is
@@ -283,7 +286,7 @@ class ConcurrentRunner:
     def __init__(self, pipe: CaptionPipeline, n_inflight: int = 2, streams: Optional[list] = None,
                  grids: Optional[List[int]] = None, budget: Optional[int] = None,
                  encode_ahead: int = 0, encode_first: bool = False, begin_first: bool = False,
-                 extra_pipes: int = 0, enc_stream=None):
+                 extra_pipes: int = 0, enc_stream=None, cu_split: int = 0):
         self.cus = torch.cuda.get_device_properties(pipe.dev).multi_processor_count
         # persistent grids (greedy bf16 at <= 64 rows; beam search never launches one), one size
         # per batch from `grids` (largest first, see choose_persist_grid)
@@ -325,6 +328,21 @@ class ConcurrentRunner:
         # first use and can end up sharing one, which serializes the batches
         # (``streams``: reuse another runner's, at least as many -- tools/headline_ab.py)
         need = len(self.pipes)
+        # cu_split > 0 (persistent decode, A/B option): the chip is split by CU masks -- the
+        # pipelines' begins (prompt .. step 0, and a give-up's phase launches) on cu_split CUs,
+        # the decode grids on the rest (each pipeline launches its grid on a second stream of
+        # its own); the budget then holds the grids to two workgroups per grid CU
+        self.cu_split = int(cu_split) if self.persist else 0
+        self.gstreams = None
+        if self.cu_split:
+            key = (str(pipe.dev), self.cus, self.cu_split)
+            have = _SPLIT_STREAMS.setdefault(key, ([], []))   # reused by later runners
+            bmask, gmask = ops.cu_split_masks(self.cus, self.cu_split)
+            if len(have[0]) < need:
+                have[0].extend(ops.masked_streams(need - len(have[0]), pipe.dev, bmask))
+                have[1].extend(ops.masked_streams(need - len(have[1]), pipe.dev, gmask))
+            streams, self.gstreams = have[0][:need], have[1][:need]
+            self.budget = min(self.budget, 2 * (self.cus - self.cu_split))
         streams = (list(streams[:need]) if streams is not None
                    else ops.dedicated_streams(need, pipe.dev, priority=-1))
         assert len(streams) == need, "ConcurrentRunner: too few streams given"
@@ -445,7 +463,10 @@ class ConcurrentRunner:
                     slots[i] = g
                     excl_slots[i] = g if excl else 0
                     self.grid[bi] = g
-                    with torch.cuda.stream(s):
+                    gs = self.gstreams[i] if self.gstreams else s
+                    if gs is not s:
+                        gs.wait_stream(s)
+                    with torch.cuda.stream(gs):
                         p.decoder.launch_pending()
                         ev, flag = p.decoder.finished_async()
                     active[i] = (bi, 0, ev, flag)
@@ -457,6 +478,8 @@ class ConcurrentRunner:
                 if not ev.query():
                     continue
                 progressed = True
+                if self.gstreams and n == 0:
+                    s.wait_stream(self.gstreams[i])   # (the grid ran on its own stream)
                 if int(flag[1]) < 0:
                     # the persistent launch gave up waiting (its grid was not co-resident): finish
                     # this batch on the per-step path from the state it started from
@@ -488,6 +511,8 @@ class ConcurrentRunner:
             if not progressed:
                 time.sleep(20e-6)
         for s in self.streams:           # results are consumed on the caller's stream
+            caller.wait_stream(s)
+        for s in self.gstreams or []:
             caller.wait_stream(s)
         if ahead is not None:
             caller.wait_stream(self.enc_stream)
