@@ -504,7 +504,7 @@ def persist_launch_bytes(w_step, plen, steps, kv_row=12 * 2 * 768 * 2):
     return n * w_step + kv_row * (keys + len(plen) * n)
 
 
-PMC_PERSIST_FILE = os.path.join(ROOT, "profiles", "r5", "pmc_persist_g48.json")
+PMC_PERSIST_FILE = os.path.join(ROOT, "profiles", "r6", "pmc_persist_g48.json")
 F32_INFLIGHT = 4
 
 
