@@ -52,6 +52,28 @@ def main(d, n=17, bucket=5.0):
             lo, hi = max(a, i * bucket), min(b, (i + 1) * bucket)
             if hi > lo:
                 tgt[i] += (hi - lo) / bucket
+    # per begin: on each pipeline queue, the kernels between two persistent launches (the
+    # begin of the batch whose grid follows): wall (first start -> last end) vs kernel-busy time
+    begins = []
+    by_q = {}
+    for r in rows:
+        if r[1] < t0 or r[0] > t1 or r[3] in enc_q:
+            continue
+        by_q.setdefault(r[3], []).append(r)
+    for q, rs in by_q.items():
+        seg = []
+        for r in rs:
+            if "dg_persist_kernel" in r[2]:
+                if seg:
+                    wall = (max(x[1] for x in seg) - min(x[0] for x in seg)) / 1e6
+                    busy = sum(x[1] - x[0] for x in seg) / 1e6
+                    begins.append({"start": round(ms(seg[0][0]), 2), "wall_ms": round(wall, 2),
+                                   "kernel_ms": round(busy, 2), "kernels": len(seg),
+                                   "grid_start_after_ms": round((r[0] - max(x[1] for x in seg)) / 1e6, 2)})
+                seg = []
+            else:
+                seg.append(r)
+    begins.sort(key=lambda b: b["start"])
     st = sorted(ms(r[0]) for r in timed)
     en = sorted(ms(r[1]) for r in timed)
     out = {"span_ms": round(ms(t1), 2), "first_grid_start": round(st[0], 2),
@@ -62,7 +84,8 @@ def main(d, n=17, bucket=5.0):
            "encoder_density": [round(x, 2) for x in enc],
            "begins_density": [round(x, 2) for x in beg],
            "grids_in_flight": [round(x, 2) for x in dec],
-           "top_kernels_ms": {k: round(v, 2) for k, v in sorted(names.items(), key=lambda kv: -kv[1])[:14]}}
+           "top_kernels_ms": {k: round(v, 2) for k, v in sorted(names.items(), key=lambda kv: -kv[1])[:14]},
+           "begins": begins}
     print(json.dumps(out))
 
 

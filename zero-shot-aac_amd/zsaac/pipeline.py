@@ -137,6 +137,8 @@ class CaptionPipeline:
         self.embed = torch.empty(B * self.Pmax, 768, device=dev)
         self.prefix_ids = torch.zeros(B * self.Pmax, **i32)
         self.emb_buf = torch.empty(B, 1024, device=dev)
+        self.emb_in = torch.empty(B, 1024, device=dev)     # begin_emb_graphed's input
+        self._begin_graphs = {}
 
     def _setup_tables(self, label_table, label_tokens):
         cfg, dev = self.cfg, self.dev
@@ -203,9 +205,45 @@ class CaptionPipeline:
     def begin_emb(self, emb: torch.Tensor):
         """Enqueue prompt assembly, mapper, prefill, get_prefix_tokens and decode step 0 for a
         batch of CLAP embeddings, without any host synchronisation."""
-        cfg, B, Pmax = self.cfg, emb.shape[0], self.Pmax
+        cfg, B = self.cfg, emb.shape[0]
         self._B, self._emb = B, emb
         assert B <= cfg.batch
+        self._begin_device(emb)
+        dec = self.decoder
+        if cfg.beam:
+            dec.beam_begin(B, cfg.beam)
+        else:
+            dec.greedy_begin_host(B)
+
+    def begin_emb_graphed(self, emb: torch.Tensor):
+        """begin_emb with its device work (prompt .. step 0: ~100 kernels) replayed from a hipGraph
+        per batch size, captured on first use on the current (non-default) stream: the embedding
+        is copied into a fixed buffer first, every other operand already lives in this pipeline's
+        buffers.  Greedy decoding only (beam search: begin_emb).  A kernel trace of the headline
+        showed a begin's stream idle between its kernels for 50-75 % of the begin's wall time
+        (tools/tl_phases.py: 14-30 ms wall, 5-13 ms of kernels beside the decode grids)."""
+        cfg, B = self.cfg, emb.shape[0]
+        assert B <= cfg.batch and not cfg.beam
+        self.emb_in[:B].copy_(emb)
+        if not hasattr(self, "_begin_graphs"):
+            self._begin_graphs = {}
+        g = self._begin_graphs.get(B)
+        if g is None:
+            g = torch.cuda.CUDAGraph()
+            g.capture_begin()
+            try:
+                self._begin_device(self.emb_in[:B])
+            finally:
+                g.capture_end()
+            self._begin_graphs[B] = g
+            self.decoder.n_captures += 1
+        g.replay()
+        self._B, self._emb = B, self.emb_in[:B]
+        self.decoder.greedy_begin_host(B)
+
+    def _begin_device(self, emb: torch.Tensor):
+        """The device work of a begin (no host state: capturable)."""
+        cfg, B, Pmax = self.cfg, emb.shape[0], self.Pmax
         ops.prompt_assemble(emb, self.labels, cfg.sound_effect_num, self.label_tok, self.label_len,
                             self.hard_ids[:B], self.hard_len[:B])
         prefix = self.prefix[:B]
@@ -222,10 +260,9 @@ class CaptionPipeline:
             self.prefix_tokens(B, soft)
         if cfg.beam:
             dec.prefill(B, Pmax, row_stride=cfg.beam)
-            dec.beam_begin(B, cfg.beam)
         else:
             dec.prefill(B, Pmax)
-            dec.greedy_begin(B)
+            dec.greedy_begin_device(B)
 
 
 def persist_grids(env: Optional[str] = None) -> List[int]:
@@ -306,6 +343,9 @@ class ConcurrentRunner:
         # the encoder's up-front passes replayed from per-size hipGraphs (Encoder.encode_graphed)
         self.enc_graph = True
         self.spread = False       # A/B: exclusive (one CU per workgroup) grids while CUs allow
+        # greedy begins replayed from per-pipeline hipGraphs (CaptionPipeline.begin_emb_graphed),
+        # captured in warmup
+        self.graph_begins = self.persist and os.environ.get("ZSAAC_GRAPH_BEGINS", "1") != "0"
         if self.persist and not self.begin_first:
             # persistent decode grids must be co-resident: at most budget // (smallest grid)
             n_inflight = max(1, min(n_inflight, self.budget // self.grids[-1]))
@@ -354,11 +394,18 @@ class ConcurrentRunner:
                                else ops.dedicated_streams(1, pipe.dev, priority=1)[0])
 
     def warmup(self, wav: torch.Tensor):
-        """Runs one batch per pipeline synchronously (captures every decode graph)."""
+        """Runs one batch per pipeline synchronously (captures every decode graph, and with
+        graph_begins the begin graph of this batch size)."""
         for p, s in zip(self.pipes, self.streams):
             s.wait_stream(torch.cuda.current_stream(p.dev))
             with torch.cuda.stream(s):
-                p.caption_wav(wav)
+                if self.graph_begins:
+                    p.begin_emb(p.encode(wav))          # (eager first: every lazy buffer exists)
+                    p.decoder.run_to_completion()
+                    p.begin_emb_graphed(p.encode(wav))
+                    p.decoder.run_to_completion()
+                else:
+                    p.caption_wav(wav)
                 p.decoder.capture_buckets()
             s.synchronize()
 
@@ -367,6 +414,9 @@ class ConcurrentRunner:
             s.wait_stream(torch.cuda.current_stream(p.dev))
             with torch.cuda.stream(s):
                 p.caption_emb(emb)
+                if self.graph_begins:
+                    p.begin_emb_graphed(emb)
+                    p.decoder.run_to_completion()
                 p.decoder.capture_buckets()
             s.synchronize()
 
@@ -520,12 +570,15 @@ class ConcurrentRunner:
 
     def _begin(self, i, bi, batches, inputs, ahead):
         p, s = self.pipes[i], self.streams[i]
+        begin = p.begin_emb_graphed if self.graph_begins else p.begin_emb
         with torch.cuda.stream(s):
             if ahead is not None:
                 s.wait_event(ahead.ready(bi))
-                p.begin_emb(ahead.embs[bi])
+                begin(ahead.embs[bi])
+            elif inputs == "wav":
+                begin(p.encode(batches[bi]))
             else:
-                (p.begin_wav if inputs == "wav" else p.begin_emb)(batches[bi])
+                begin(batches[bi])
 
     def _run_staged(self, batches, keep, inputs, caller, ahead):
         """run() with begin_first: begins on every free pipeline first (persistent launches
