@@ -343,9 +343,11 @@ class ConcurrentRunner:
         # the encoder's up-front passes replayed from per-size hipGraphs (Encoder.encode_graphed)
         self.enc_graph = True
         self.spread = False       # A/B: exclusive (one CU per workgroup) grids while CUs allow
-        # greedy begins replayed from per-pipeline hipGraphs (CaptionPipeline.begin_emb_graphed),
-        # captured in warmup
-        self.graph_begins = self.persist and os.environ.get("ZSAAC_GRAPH_BEGINS", "1") != "0"
+        # A/B (ZSAAC_GRAPH_BEGINS=1): greedy begins replayed from per-pipeline hipGraphs
+        # (CaptionPipeline.begin_emb_graphed), captured in warmup -- measured 5.75k vs 5.86k and
+        # 5.09k vs 5.30k clips/s (same box, medians of 5): the idle time between a begin's kernels
+        # beside the grids is waiting for CU resources, not host enqueue
+        self.graph_begins = self.persist and os.environ.get("ZSAAC_GRAPH_BEGINS", "0") != "0"
         if self.persist and not self.begin_first:
             # persistent decode grids must be co-resident: at most budget // (smallest grid)
             n_inflight = max(1, min(n_inflight, self.budget // self.grids[-1]))
