@@ -9,13 +9,17 @@ eval batches of 64 clips exactly as the reference evaluates them: STFT/log-mel +
 audio_proj + L2 -> sound-effect hard prompt -> MLP mapper -> GPT-2 small prefill +
 get_prefix_tokens + greedy generate2 (entry_length 67, stop ids 13 / 764), bf16 operands / f32
 accumulation.  Every decode GEMM of a batch is a 64-row GEMM.  One "step" = one eval batch of
-64 clips (the last batch of the 1045 holds 21).  Independent batches are in flight per GPU (up to
---inflight, within --persist-budget), each on its own HIP stream (pipeline twins sharing the
-weights, zsaac/pipeline.py ConcurrentRunner), each decoding in its own persistent launch of 48
-half-CU workgroups (a larger grid when few batches wait, zsaac.pipeline.choose_persist_grid; the
-grid never changes an id, decode_grid.hip); the timed region runs --reps times (median reported);
-GPU_MAX_HW_QUEUES is raised to --hw-queues (default 16, the runtime allows up to 32) so those
-streams get hardware queues of their own.  With N ranks the
+64 clips (the last batch of the 1045 holds 21).  Independent batches are in flight per GPU, each
+on its own HIP stream (pipeline twins sharing the weights, zsaac/pipeline.py ConcurrentRunner),
+each decoding in its own persistent launch of 48 half-CU workgroups (a larger grid when few
+batches wait, zsaac.pipeline.choose_persist_grid; the grid never changes an id, decode_grid.hip).
+Schedule (--begin-first 1, the default): a pipeline per batch; every batch's begin (prompt,
+mapper, prefill, get_prefix_tokens, step 0) runs as the encoder's passes deliver, before the
+first decode grid launches; the grids then launch in batch order within --persist-budget slots
+(default 2 x CUs less a sixteenth: ten grids of 48); --begin-first 0 is round 5's pipelined
+schedule (at most --inflight batches, begins beside the grids).  The timed region runs --reps
+times (median reported); GPU_MAX_HW_QUEUES is raised to --hw-queues (default 16, the runtime
+allows up to 32; streams beyond it share queues in order).  With N ranks the
 clips are sharded (zsaac/dist.py shard_range) and ONE RCCL all-gather of the generated token ids
 + lengths (zsaac/dist.py collect_captions) is inside the timed region.
 
@@ -136,6 +140,11 @@ def parse(argv=None):
     ap.add_argument("--cu-split", type=int, default=0,
                     help="A/B: CUs reserved (by stream CU masks) for the begins; the decode "
                          "grids get the rest (0: no split)")
+    ap.add_argument("--begin-first", type=int, default=1,
+                    help="1 (default): a pipeline per batch, every begin (prompt .. step 0) "
+                         "enqueued first; the first grid launches wait for --begin-gate begins "
+                         "(0: all of them); 0: round 5's pipelined schedule (begins beside grids)")
+    ap.add_argument("--begin-gate", type=int, default=0)
     ap.add_argument("--persist-budget", type=int, default=0,
                     help="workgroup slots (half a CU each) the in-flight persistent decode grids "
                          "may hold together (0: ZSAAC_PERSIST_BUDGET or 1.5 per CU)")
@@ -264,7 +273,7 @@ def run_captions(args, world, rank, device, pipe, n_local, first, counts, inflig
     """Times the captioning of this rank's n_local clips (clip ids first..) in batches of
     pipe.cfg.batch (split_batches) on `inflight` streams, then the all-gather; returns (seconds
     max over ranks, outs, runner, info)."""
-    from zsaac.pipeline import ConcurrentRunner
+    from zsaac.pipeline import ConcurrentRunner, persist_budget
     from zsaac import decoder as zdec, dist as zd
     B = pipe.cfg.batch
     pool = synthetic_clips(n_local, first, device)
@@ -276,11 +285,24 @@ def run_captions(args, world, rank, device, pipe, n_local, first, counts, inflig
     if getattr(args, "beam", 0) or ahead < B:      # beam runs / larger batches: encoder per batch
         ahead = 0
     extra = getattr(args, "extra_pipes", 0)
+    # (bf16 only: the f32 parity mode's two co-resident G192 grids ran 1.49k vs 1.58k clips/s
+    # staged, profiles/r6/begin_first_ab.txt)
+    bfirst = (bool(getattr(args, "begin_first", 0)) and pipe.decoder.persist and not pipe.cfg.beam
+              and pipe.cfg.batch <= 64 and not getattr(pipe.decoder, "f32_grid", False))
+    budget = getattr(args, "persist_budget", 0) or None
+    if bfirst:                  # a pipeline per batch: every begin runs before / beside few grids
+        inflight = max(inflight, len(batches))
+        budget = budget or persist_budget(torch.cuda.get_device_properties(device).multi_processor_count,
+                                          staged=True)
+    nstreams = max(1, inflight) + extra
+    if bfirst:                  # (as ConcurrentRunner: the grids the budget holds + 2)
+        nstreams = min(nstreams, budget // 48 + 2)
     runner = ConcurrentRunner(pipe, max(1, inflight),
-                              streams=run_streams(device, max(1, inflight) + extra),
-                              budget=getattr(args, "persist_budget", 0) or None,
+                              streams=run_streams(device, nstreams),
+                              budget=budget,
                               encode_ahead=ahead, enc_stream=enc_stream(device) if ahead else None,
-                              extra_pipes=extra, cu_split=getattr(args, "cu_split", 0))
+                              extra_pipes=extra, cu_split=getattr(args, "cu_split", 0),
+                              begin_first=bfirst, begin_gate=getattr(args, "begin_gate", 0))
     for size in sorted({b.shape[0] for b in batches}, reverse=True):   # captures every graph
         runner.warmup(next(b for b in batches if b.shape[0] == size))
         log(f"captured the decode graphs of {size}-clip batches")
@@ -333,6 +355,10 @@ def run_captions(args, world, rank, device, pipe, n_local, first, counts, inflig
             "persist_grids": grid_counts(runner),
             "persist_budget_wg_slots": getattr(runner, "budget", None),
             "batches_in_flight": runner.n_inflight,
+            "schedule": ("begin_first: a pipeline per batch, every begin (prompt .. step 0) "
+                         "before the first grid launches, grids launched as the budget frees"
+                         if getattr(runner, "begin_first", False) and len(batches) > runner.budget // runner.grids[-1]
+                         else "pipelined: begins beside the decode grids"),
             # decode rows stepped per clip in ONE repetition of the timed region
             "decode_rows_stepped_per_clip": round((rows1 - rows0) / max(1, reps) / max(1, n_local), 2),
             "decode_steps_mean": round(sum(runner.decode_steps) / max(1, len(runner.decode_steps)), 2),

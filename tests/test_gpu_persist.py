@@ -216,14 +216,17 @@ def test_concurrent_runner_mixed_grids(cuda):
     assert runner.gave_up == 0
 
 
-def test_concurrent_headline_schedule_ids_equal_single_stream(cuda):
+@pytest.mark.parametrize("staged", [False, True], ids=["pipelined", "begin_first"])
+def test_concurrent_headline_schedule_ids_equal_single_stream(cuda, staged):
     """The headline's schedule at the headline's size on the bench's own weights (c2_gpt2init,
     GPT-2's init scale, small margins): 1045 embeddings in 17 eval batches of <= 64 (the last 21)
-    through ConcurrentRunner with its default grids and budget -- ten batches in flight, grids
-    chosen per batch -- give, batch for batch, the ids of a single-stream run of the same batches
-    (persistent grid 48, one batch at a time), and no launch gave up."""
+    through ConcurrentRunner -- pipelined: its default grids and budget, ten batches in flight,
+    grids chosen per batch; begin_first (the bench's schedule): a pipeline per batch, every begin
+    first, ten grids of 48 at a time within the staged budget -- give, batch for batch, the ids of
+    a single-stream run of the same batches (persistent grid 48, one batch at a time), and no
+    launch gave up."""
     from tools import idparity
-    from zsaac.pipeline import ConcurrentRunner
+    from zsaac.pipeline import ConcurrentRunner, persist_budget
     g = idparity.load("c2_gpt2init")
     base = torch.from_numpy(g["clap_emb"]).to(cuda)
     n = 1045
@@ -233,7 +236,12 @@ def test_concurrent_headline_schedule_ids_equal_single_stream(cuda):
     p = _pipe(g, cuda, True, batch=64)
     p.decoder.persist_grid = 48
     single = [p.caption_emb(b).captions() for b in batches]
-    runner = ConcurrentRunner(p, 10)
+    if staged:
+        cus = torch.cuda.get_device_properties(cuda).multi_processor_count
+        runner = ConcurrentRunner(p, len(batches), begin_first=True,
+                                  budget=persist_budget(cus, staged=True))
+    else:
+        runner = ConcurrentRunner(p, 10)
     runner.warmup_emb(batches[0])
     fails = []
     for rep in range(3):
@@ -249,6 +257,7 @@ def test_concurrent_headline_schedule_ids_equal_single_stream(cuda):
                               "gave_up": runner.gave_up})
     assert not fails, f"concurrent ids differ from the single-stream run: {fails}"
     assert sum(len(c) for c in single) == n
+    assert runner.gave_up == 0
 
 
 def test_prompts_beside_grids_deterministic(cuda):

@@ -285,13 +285,17 @@ def persist_grids(env: Optional[str] = None) -> List[int]:
 DEFAULT_PERSIST_GRIDS = "96,48"
 
 
-def persist_budget(cus: int) -> int:
+def persist_budget(cus: int, staged: bool = False) -> int:
     """Workgroup slots the in-flight persistent grids may hold together: a grid workgroup takes
-    half a CU (4 waves x <= 256 registers), so 2 x CUs is the chip.  The default, 1.5 x CUs (8
-    grids of 48), leaves a quarter of the slots to the begins' kernels: measured in one process
-    (tools/headline_ab.py, 12 reps, encode-ahead 256, grids sized at launch): 5.73k clips/s
-    against 5.33k at 2 x CUs and 4.71k at 1 x CUs.  ZSAAC_PERSIST_BUDGET overrides."""
-    return int(os.environ.get("ZSAAC_PERSIST_BUDGET", str(3 * cus // 2)))
+    half a CU (4 waves x <= 256 registers), so 2 x CUs is the chip.  The pipelined schedule's
+    default, 1.5 x CUs (8 grids of 48), leaves a quarter of the slots to the begins' kernels:
+    measured in one process (tools/headline_ab.py, 12 reps, encode-ahead 256, grids sized at
+    launch): 5.73k clips/s against 5.33k at 2 x CUs and 4.71k at 1 x CUs.  ``staged``
+    (begin_first: the begins have run before the grids) 2 x CUs less a sixteenth, ten grids of 48
+    on 256 CUs (profiles/r6/begin_first_ab.txt: 448 / 480 / 512 slots 7.03k / 7.02k / 7.11k on
+    the 1045-clip set, 480 / 512 6.96k / 6.81k on 1280 clips).  ZSAAC_PERSIST_BUDGET overrides."""
+    dflt = 2 * cus - cus // 8 if staged else 3 * cus // 2
+    return int(os.environ.get("ZSAAC_PERSIST_BUDGET", str(dflt)))
 
 
 def choose_persist_grid(in_flight: int, to_begin: int, grids: List[int], budget: int) -> int:
@@ -309,6 +313,9 @@ def choose_persist_grid(in_flight: int, to_begin: int, grids: List[int], budget:
 
 
 _SPLIT_STREAMS = {}     # (device, CUs, begin CUs) -> (begin streams, grid streams)
+# a staged run that sees no event complete for this long raises (with its state) instead of
+# spinning: a persistent launch that cannot become co-resident gives up after ~2^22 polls (s)
+STALL_S = float(os.environ.get("ZSAAC_RUNNER_STALL_S", "60"))
 
 
 class ConcurrentRunner:
@@ -323,7 +330,8 @@ class ConcurrentRunner:
     def __init__(self, pipe: CaptionPipeline, n_inflight: int = 2, streams: Optional[list] = None,
                  grids: Optional[List[int]] = None, budget: Optional[int] = None,
                  encode_ahead: int = 0, encode_first: bool = False, begin_first: bool = False,
-                 extra_pipes: int = 0, enc_stream=None, cu_split: int = 0):
+                 extra_pipes: int = 0, enc_stream=None, cu_split: int = 0,
+                 begin_gate: int = 0):
         self.cus = torch.cuda.get_device_properties(pipe.dev).multi_processor_count
         # persistent grids (greedy bf16 at <= 64 rows; beam search never launches one), one size
         # per batch from `grids` (largest first, see choose_persist_grid)
@@ -335,6 +343,9 @@ class ConcurrentRunner:
         # at once, and the persistent launches follow as the budget frees, the first ones after
         # every first-round begin -- the begins run on the whole chip instead of beside the grids
         self.begin_first = bool(begin_first) and self.persist
+        # begin_first: the first persistent launches wait for the first `begin_gate` begins (0:
+        # every begin of the first round), so those begins run beside no decode grid
+        self.begin_gate = int(begin_gate)
         self.late_grid = True     # grid size chosen when the begin has finished (False: at begin)
         # one begin per pass over the pipelines: a begin costs milliseconds of host enqueue, so
         # beginning every idle pipeline in one pass delayed the first grids' launches until the
@@ -370,6 +381,13 @@ class ConcurrentRunner:
         # first use and can end up sharing one, which serializes the batches
         # (``streams``: reuse another runner's, at least as many -- tools/headline_ab.py)
         need = len(self.pipes)
+        if self.begin_first:
+            # begin_first keeps a pipeline per batch but only as many streams as grids can run at
+            # once (+2 for the begins): every stream is a hardware queue, and a process holding
+            # more queues than the scheduler maps at once gets its queues time-sliced (a
+            # stream per pipeline, 20 at 1280 clips, slowed every later multi-stream run 5-27 %:
+            # profiles/r6/begin_first_ab.txt)
+            need = min(need, self.budget // self.grids[-1] + 2)
         # cu_split > 0 (persistent decode, A/B option): the chip is split by CU masks -- the
         # pipelines' begins (prompt .. step 0, and a give-up's phase launches) on cu_split CUs,
         # the decode grids on the rest (each pipeline launches its grid on a second stream of
@@ -398,7 +416,8 @@ class ConcurrentRunner:
     def warmup(self, wav: torch.Tensor):
         """Runs one batch per pipeline synchronously (captures every decode graph, and with
         graph_begins the begin graph of this batch size)."""
-        for p, s in zip(self.pipes, self.streams):
+        for i, p in enumerate(self.pipes):
+            s = self.streams[i % len(self.streams)]
             s.wait_stream(torch.cuda.current_stream(p.dev))
             with torch.cuda.stream(s):
                 if self.graph_begins:
@@ -412,7 +431,8 @@ class ConcurrentRunner:
             s.synchronize()
 
     def warmup_emb(self, emb: torch.Tensor):
-        for p, s in zip(self.pipes, self.streams):
+        for i, p in enumerate(self.pipes):
+            s = self.streams[i % len(self.streams)]
             s.wait_stream(torch.cuda.current_stream(p.dev))
             with torch.cuda.stream(s):
                 p.caption_emb(emb)
@@ -438,7 +458,9 @@ class ConcurrentRunner:
             # (a run that fits its pipelines at once begins sooner encoding per batch: measured
             # on a 131-clip shard, 37.5 vs 40 ms)
             ahead = self._encode_ahead(batches, caller)
-        if self.begin_first:
+        if self.begin_first and len(batches) > self.budget // self.grids[-1]:
+            # (more batches than grids the budget holds at once; fewer take the pipelined path
+            # below, whose small-run form gives each batch an exclusive grid)
             return self._run_staged(batches, keep, inputs, caller, ahead)
         # a run that fits its pipelines at once (a small shard) has no later begins to leave room
         # for: its grids may fill the chip, and they take one CU per workgroup (exclusive
@@ -571,7 +593,7 @@ class ConcurrentRunner:
         return results
 
     def _begin(self, i, bi, batches, inputs, ahead):
-        p, s = self.pipes[i], self.streams[i]
+        p, s = self.pipes[i], self.streams[i % len(self.streams)]
         begin = p.begin_emb_graphed if self.graph_begins else p.begin_emb
         with torch.cuda.stream(s):
             if ahead is not None:
@@ -583,60 +605,80 @@ class ConcurrentRunner:
                 begin(batches[bi])
 
     def _run_staged(self, batches, keep, inputs, caller, ahead):
-        """run() with begin_first: begins on every free pipeline first (persistent launches
-        deferred), launches in batch order while the grids in flight fit the budget."""
+        """run() with begin_first: a begin on every free pipeline (persistent launches deferred),
+        one begin per pass over the loop so finished batches and launches are handled between
+        begins; launches in batch order while the grids in flight fit the budget, each on a
+        stream no grid is running on, after its own begin and -- the first ones -- after the
+        first `begin_gate` begins (0: every begin of the first round) have finished on the GPU.
+        With a pipeline per batch every begin runs before (or beside few) decode grids and every
+        later launch finds its batch begun."""
         n = len(batches)
+        S = len(self.streams)
         results: List[Optional[CaptionBatch]] = [None] * n
         self.decode_steps = [0] * n
         self.assign, self.grid, self.gave_up = [], [0] * n, 0
         free = list(range(len(self.pipes)))
+        n_gate = min(n, len(free)) if self.begin_gate <= 0 else min(n, self.begin_gate)
         begun, active, slots = [], {}, {}
-        first_round, gate = True, []
+        gate, bev, sbusy = [], {}, set()
         nxt = 0
+        trace = self.trace = [] if os.environ.get("ZSAAC_RUNNER_TRACE") else None
+        t_run = t_prog = time.perf_counter()
         while nxt < n or begun or active:
             progressed = False
-            while nxt < n and free:
+            if ahead is not None:
+                ahead.pump()
+            if nxt < n and free:
                 i = free.pop(0)
                 self.pipes[i].decoder.defer_launch = True
                 try:
                     self._begin(i, nxt, batches, inputs, ahead)
                 finally:
                     self.pipes[i].decoder.defer_launch = False
-                if first_round:
-                    ev = torch.cuda.Event()
-                    ev.record(self.streams[i])
+                ev = torch.cuda.Event()
+                ev.record(self.streams[i % S])
+                bev[nxt] = ev
+                if len(gate) < n_gate:
                     gate.append(ev)
                 begun.append((nxt, i))
                 self.assign.append((i, nxt))
+                if trace is not None:
+                    trace.append(("begin", nxt, round((time.perf_counter() - t_run) * 1e3, 2)))
                 nxt += 1
                 progressed = True
-            first_round = False
-            while begun:
+            while begun and len(gate) >= n_gate and len(sbusy) < S:
                 bi, i = begun[0]
                 used = sum(slots.values())
                 g = choose_persist_grid(used, len(begun) + n - nxt, self.grids, self.budget)
                 if used + g > self.budget:
                     break
-                p, s = self.pipes[i], self.streams[i]
+                k = next(k for k in range(S) if k not in sbusy)
+                p, s = self.pipes[i], self.streams[k]
                 p.decoder.persist_grid = g
                 p.decoder.persist_exclusive = False    # (not a value left over from run())
                 with torch.cuda.stream(s):
-                    for ev in gate:          # the first round's launches: after every begin
+                    s.wait_event(bev.pop(bi))
+                    for ev in gate:          # the first launches: after the gating begins
                         s.wait_event(ev)
                     p.decoder.launch_pending()
                     ev, flag = p.decoder.finished_async()
                 slots[i] = g
+                sbusy.add(k)
                 self.grid[bi] = g
-                active[i] = (bi, 0, ev, flag)
+                active[i] = (bi, 0, ev, flag, k)
                 begun.pop(0)
+                if trace is not None:
+                    trace.append(("launch", bi, round((time.perf_counter() - t_run) * 1e3, 2)))
                 progressed = True
-            gate = []
+            if len(gate) >= n_gate and active:
+                gate = []                    # (launches after the first ones: no gate)
+                n_gate = 0
             for i in list(active):
-                bi, k, ev, flag = active[i]
+                bi, c, ev, flag, k = active[i]
                 if not ev.query():
                     continue
                 progressed = True
-                p, s = self.pipes[i], self.streams[i]
+                p, s = self.pipes[i], self.streams[k]
                 if int(flag[1]) < 0:          # gave up (not co-resident): finish stepwise
                     self.gave_up += 1
                     with torch.cuda.stream(s):
@@ -644,9 +686,9 @@ class ConcurrentRunner:
                         p.decoder.step_chunk(None)
                         ev, flag = p.decoder.finished_async()
                     slots.pop(i, None)
-                    active[i] = (bi, 1, ev, flag)
+                    active[i] = (bi, 1, ev, flag, k)
                     continue
-                if int(flag[0]) or k >= p.decoder.n_chunks:
+                if int(flag[0]) or c >= p.decoder.n_chunks:
                     p.decoder.note_persist_steps(int(flag[3]))
                     self.decode_steps[bi] = int(flag[3])
                     with torch.cuda.stream(s):
@@ -655,14 +697,22 @@ class ConcurrentRunner:
                             keep(results[bi])
                     del active[i]
                     slots.pop(i, None)
+                    sbusy.discard(k)
                     free.append(i)
                 else:
                     with torch.cuda.stream(s):
                         p.decoder.step_chunk(int(flag[2]))
                         ev, flag = p.decoder.finished_async()
-                    active[i] = (bi, k + 1, ev, flag)
-            if not progressed:
+                    active[i] = (bi, c + 1, ev, flag, k)
+            if progressed:
+                t_prog = time.perf_counter()
+            else:
                 time.sleep(20e-6)
+                if time.perf_counter() - t_prog > STALL_S:
+                    raise RuntimeError(
+                        f"ConcurrentRunner (begin_first): no progress for {STALL_S} s; begun "
+                        f"{begun}, active {[(i, a[0], a[1], a[4]) for i, a in active.items()]}, "
+                        f"grids {slots}, next batch {nxt} of {n}")
         for s in self.streams:
             caller.wait_stream(s)
         if ahead is not None:
