@@ -145,6 +145,9 @@ def parse(argv=None):
                          "enqueued first; the first grid launches wait for --begin-gate begins "
                          "(0: all of them); 0: round 5's pipelined schedule (begins beside grids)")
     ap.add_argument("--begin-gate", type=int, default=0)
+    ap.add_argument("--begin-group", type=int, default=4,
+                    help="with --begin-first: eval batches per begin (one encoder pass, prefill "
+                         "and get_prefix_tokens for all of them; 0 = a begin per batch)")
     ap.add_argument("--persist-budget", type=int, default=0,
                     help="workgroup slots (half a CU each) the in-flight persistent decode grids "
                          "may hold together (0: ZSAAC_PERSIST_BUDGET or 1.5 per CU)")
@@ -263,8 +266,8 @@ def enc_stream(device):
     """The low-priority stream the caption runs' encoder twin runs ahead on (one per process)."""
     from zsaac import ops
     key = "enc:" + str(device)
-    if key not in _STREAMS:
-        _STREAMS[key] = ops.dedicated_streams(1, device, priority=1)[0]
+    if key not in _STREAMS:       # (ZSAAC_ENC_PRIO: A/B of the encoder stream's priority)
+        _STREAMS[key] = ops.dedicated_streams(1, device, priority=int(os.environ.get("ZSAAC_ENC_PRIO", "1")))[0]
     return _STREAMS[key]
 
 
@@ -290,19 +293,22 @@ def run_captions(args, world, rank, device, pipe, n_local, first, counts, inflig
     bfirst = (bool(getattr(args, "begin_first", 0)) and pipe.decoder.persist and not pipe.cfg.beam
               and pipe.cfg.batch <= 64 and not getattr(pipe.decoder, "f32_grid", False))
     budget = getattr(args, "persist_budget", 0) or None
-    if bfirst:                  # a pipeline per batch: every begin runs before / beside few grids
-        inflight = max(inflight, len(batches))
+    bgroup = int(getattr(args, "begin_group", 4)) if bfirst and args.mapper == "mlp" else 0
+    if bfirst:
+        if not bgroup:          # a pipeline per batch: every begin runs before the grids
+            inflight = max(inflight, len(batches))
         budget = budget or persist_budget(torch.cuda.get_device_properties(device).multi_processor_count,
                                           staged=True)
     nstreams = max(1, inflight) + extra
     if bfirst:                  # (as ConcurrentRunner: the grids the budget holds + 2)
-        nstreams = min(nstreams, budget // 48 + 2)
+        nstreams = budget // 48 + 2 if bgroup else min(nstreams, budget // 48 + 2)
     runner = ConcurrentRunner(pipe, max(1, inflight),
                               streams=run_streams(device, nstreams),
                               budget=budget,
                               encode_ahead=ahead, enc_stream=enc_stream(device) if ahead else None,
                               extra_pipes=extra, cu_split=getattr(args, "cu_split", 0),
-                              begin_first=bfirst, begin_gate=getattr(args, "begin_gate", 0))
+                              begin_first=bfirst, begin_gate=getattr(args, "begin_gate", 0),
+                              begin_group=bgroup, n_batches=len(batches))
     for size in sorted({b.shape[0] for b in batches}, reverse=True):   # captures every graph
         runner.warmup(next(b for b in batches if b.shape[0] == size))
         log(f"captured the decode graphs of {size}-clip batches")
@@ -313,8 +319,8 @@ def run_captions(args, world, rank, device, pipe, n_local, first, counts, inflig
     if world > 1:
         torch.distributed.barrier()
     torch.cuda.synchronize()
-    cap0 = sum(p.decoder.n_captures for p in runner.pipes)
-    rows0 = sum(p.decoder.rows_stepped for p in runner.pipes)
+    cap0 = sum(d.n_captures for d in runner.decoders())
+    rows0 = sum(d.rows_stepped for d in runner.decoders())
     times, gave_up = [], 0
     for _ in range(reps):          # every repetition the whole region; the median is reported
         t0 = time.perf_counter()
@@ -332,7 +338,7 @@ def run_captions(args, world, rank, device, pipe, n_local, first, counts, inflig
             dt_r = float(t)
         times.append(dt_r)
         gave_up += getattr(runner, "gave_up", 0)
-    rows1 = sum(p.decoder.rows_stepped for p in runner.pipes)     # (before the log pass)
+    rows1 = sum(d.rows_stepped for d in runner.decoders())     # (before the log pass)
     dt = sorted(times)[len(times) // 2]
     log(f"timed: {n_local} clips in {dt:.3f} s (median of {reps}: {[round(t, 4) for t in times]})")
     if gave_up:
@@ -349,14 +355,18 @@ def run_captions(args, world, rank, device, pipe, n_local, first, counts, inflig
         finally:
             zdec.PERSIST_LOG = None         # no events around launches outside this pass
         ALL_PERSIST_LOGS.extend(runner.timed_log)
-    info = {"graph_captures_timed": sum(p.decoder.n_captures for p in runner.pipes) - cap0,
+    info = {"graph_captures_timed": sum(d.n_captures for d in runner.decoders()) - cap0,
             "timed_reps_s": [round(t, 5) for t in times],
             "persist_gave_up": gave_up,
             "persist_grids": grid_counts(runner),
             "persist_budget_wg_slots": getattr(runner, "budget", None),
             "batches_in_flight": runner.n_inflight,
-            "schedule": ("begin_first: a pipeline per batch, every begin (prompt .. step 0) "
-                         "before the first grid launches, grids launched as the budget frees"
+            "schedule": (("begin_first: " + (f"one begin per {runner.begin_group} eval batches "
+                                             "(encoder pass, prefill, get_prefix_tokens at "
+                                             f"{runner.begin_group * B} clips), a decoder per batch"
+                                             if runner.begin_group else "a pipeline per batch")
+                          + ", every begin before the first grid launches, grids launched as the "
+                            "budget frees")
                          if getattr(runner, "begin_first", False) and len(batches) > runner.budget // runner.grids[-1]
                          else "pipelined: begins beside the decode grids"),
             # decode rows stepped per clip in ONE repetition of the timed region
@@ -555,8 +565,9 @@ def persist_roofline(pipe, runner, outs, dt, log):
     for e0, e1, tag in log:
         by_dec.setdefault(tag, []).append((e0, e1))
     durs, byts = [], []
+    bdec = getattr(runner, "bdec", None)      # (begin groups: batch -> its sub-decoder)
     for i, b in runner.assign:
-        e0, e1 = by_dec[id(runner.pipes[i].decoder)].pop(0)
+        e0, e1 = by_dec[id(bdec[b] if bdec else runner.pipes[i].decoder)].pop(0)
         durs.append(e0.elapsed_time(e1) / 1e3)
         byts.append(persist_launch_bytes(w_step, outs[b].plen.tolist(), runner.decode_steps[b]))
     n = len(durs)

@@ -129,6 +129,9 @@ class _CpuRunner:
     def warmup(self, wav):
         pass
 
+    def decoders(self):
+        return [p.decoder for p in self.pipes]
+
     def run(self, batches, keep=None, inputs="wav"):
         import time
         from types import SimpleNamespace

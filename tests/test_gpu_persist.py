@@ -216,15 +216,17 @@ def test_concurrent_runner_mixed_grids(cuda):
     assert runner.gave_up == 0
 
 
-@pytest.mark.parametrize("staged", [False, True], ids=["pipelined", "begin_first"])
+@pytest.mark.parametrize("staged", [0, 1, 4], ids=["pipelined", "begin_first", "begin_group4"])
 def test_concurrent_headline_schedule_ids_equal_single_stream(cuda, staged):
     """The headline's schedule at the headline's size on the bench's own weights (c2_gpt2init,
     GPT-2's init scale, small margins): 1045 embeddings in 17 eval batches of <= 64 (the last 21)
     through ConcurrentRunner -- pipelined: its default grids and budget, ten batches in flight,
-    grids chosen per batch; begin_first (the bench's schedule): a pipeline per batch, every begin
-    first, ten grids of 48 at a time within the staged budget -- give, batch for batch, the ids of
-    a single-stream run of the same batches (persistent grid 48, one batch at a time), and no
-    launch gave up."""
+    grids chosen per batch; begin_first: a pipeline per batch, every begin first, ten grids of 48
+    at a time within the staged budget; begin_group4 (the bench's schedule): begin_first with one
+    begin (mapper, get_prefix_tokens, prefill at 256 rows) per 4 consecutive batches and a
+    sub-decoder per batch -- give, batch for batch, the ids of a single-stream run of the same
+    batches (each its own begin, persistent grid 48, one batch at a time), and no launch gave
+    up."""
     from tools import idparity
     from zsaac.pipeline import ConcurrentRunner, persist_budget
     g = idparity.load("c2_gpt2init")
@@ -238,8 +240,10 @@ def test_concurrent_headline_schedule_ids_equal_single_stream(cuda, staged):
     single = [p.caption_emb(b).captions() for b in batches]
     if staged:
         cus = torch.cuda.get_device_properties(cuda).multi_processor_count
-        runner = ConcurrentRunner(p, len(batches), begin_first=True,
-                                  budget=persist_budget(cus, staged=True))
+        runner = ConcurrentRunner(p, len(batches) if staged == 1 else 10, begin_first=True,
+                                  budget=persist_budget(cus, staged=True),
+                                  begin_group=0 if staged == 1 else staged, n_batches=len(batches))
+        assert runner.begin_group == (0 if staged == 1 else staged)
     else:
         runner = ConcurrentRunner(p, 10)
     runner.warmup_emb(batches[0])

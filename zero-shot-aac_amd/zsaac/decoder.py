@@ -302,7 +302,9 @@ class Gpt2Decoder:
     def __init__(self, w: Gpt2Weights, max_rows: int, max_prompt: int, max_steps: int = 67,
                  max_prefill_rows: Optional[int] = None, topk: int = 8, chunk: int = 0,
                  use_graph: bool = True, compact: Optional[bool] = None,
-                 persist: Optional[bool] = None):
+                 persist: Optional[bool] = None, alloc_kv: bool = True):
+        """alloc_kv False: no KV cache of its own -- share_rows gives it rows of another
+        decoder's (a group begin's sub-decoder)."""
         if chunk <= 0:   # a divisor of the steps after step 0, near 6 (no wasted tail steps)
             n = max(max_steps - 1, 1)
             cands = [c for c in range(4, 13) if n % c == 0]
@@ -328,8 +330,9 @@ class Gpt2Decoder:
         self.qkv = torch.empty(Mp, 3 * D, device=dev, dtype=dt)
         self.att = torch.empty(Mp, D, device=dev, dtype=dt)
         self.hid = torch.empty(Mp, 4 * D, device=dev, dtype=dt)
-        self.kc = [torch.empty(self.R, NH, self.Lmax, HD, device=dev, dtype=dt) for _ in range(NL)]
-        self.vc = [torch.empty(self.R, NH, self.Lmax, HD, device=dev, dtype=dt) for _ in range(NL)]
+        kv_rows = self.R if alloc_kv else 0
+        self.kc = [torch.empty(kv_rows, NH, self.Lmax, HD, device=dev, dtype=dt) for _ in range(NL)]
+        self.vc = [torch.empty(kv_rows, NH, self.Lmax, HD, device=dev, dtype=dt) for _ in range(NL)]
         self.hf = torch.empty(max(self.R, self.Rp), D, device=dev, dtype=dt)
         self.nblk = ops.lmhead_nblk(w.V)
         R = max(self.R, self.Rp)
@@ -410,6 +413,22 @@ class Gpt2Decoder:
         self.persist_exclusive = False   # the launch takes a CU per workgroup (runner's choice)
         self.ws = ops.skinny_workspace(dev, [(M, N, K) for M in {self.R, self.Rp}
                                              for N, K in ((3 * D, D), (D, D), (4 * D, D), (D, 4 * D))])
+
+    def share_rows(self, src: "Gpt2Decoder", r0: int):
+        """Decode rows r0 .. r0 + R of ``src``'s prefill: this decoder's KV cache, last-position
+        hidden rows (hf, step 0's LM-head input) and prompt lengths become views of src's rows
+        (pipeline.CaptionPipeline.begin_group runs the prefill of several eval batches at once;
+        each batch then takes step 0 and its persistent decode on its own decoder)."""
+        R = self.R
+        assert src.Lmax == self.Lmax and r0 + R <= src.R and src.dtype == self.dtype
+        self.kc = [t[r0:r0 + R] for t in src.kc]
+        self.vc = [t[r0:r0 + R] for t in src.vc]
+        self.hf = src.hf[r0:r0 + R]
+        self.plen = src.plen[r0:r0 + R]
+        if self.grid_decode:
+            import ctypes
+            self._kv_ptrs = (ctypes.c_void_p * (2 * NL))(
+                *[t.data_ptr() for t in self.kc], *[t.data_ptr() for t in self.vc])
 
     # ---------------------------------------------------------------- blocks
     def _layers(self, M, attn_fn):

@@ -12,6 +12,7 @@ batch of clips.  Multi-GPU sharding and the token-id all-gather live in zsaac/di
 from __future__ import annotations
 
 import copy
+import dataclasses
 import os
 import time
 from dataclasses import dataclass
@@ -21,7 +22,7 @@ import numpy as np
 import torch
 
 from . import ops
-from .decoder import Gpt2Decoder, Gpt2Weights, build_mapper
+from .decoder import Gpt2Decoder, Gpt2Weights, MlpMapper, build_mapper
 from .encoder import AudioEncoder
 
 
@@ -120,6 +121,79 @@ class CaptionPipeline:
         t.mapper = self.mapper.twin()
         t._alloc()
         return t
+
+    def group_twin(self, k: int) -> "CaptionPipeline":
+        """A twin sized for k eval batches (k x cfg.batch clips) whose begin (encode, prompt,
+        mapper, get_prefix_tokens, prefill) runs for all of them at once (begin_group); each
+        batch then takes step 0 and its persistent decode on a sub-decoder of its own whose KV
+        cache rows are this twin's (Gpt2Decoder.share_rows).  Greedy bf16 / f32 decoding with
+        the MLP mapper only."""
+        assert not self.cfg.beam and isinstance(self.mapper, MlpMapper)
+        sb = self.cfg.batch
+        t = copy.copy(self)
+        t.cfg = dataclasses.replace(self.cfg, batch=k * sb, encoder_batch=k * sb)
+        t.encoder = self.encoder.twin(max_batch=k * sb) if self.encoder is not None else None
+        t.mapper = self.mapper.twin()        # (called per eval batch: sb rows)
+        t._alloc()
+        t.sub_batch = sb
+        t.soft_buf = torch.empty(k * sb, self.mapper.soft_ld, device=self.dev)
+        t.subs = []
+        for j in range(k):
+            d = Gpt2Decoder(self.gpt, sb, self.Pmax, self.cfg.entry_length, max_prefill_rows=1,
+                            use_graph=self.cfg.use_graph, topk=8, compact=self.cfg.compact_decode,
+                            persist=self.cfg.persist_decode, alloc_kv=False)
+            d.share_rows(t.decoder, j * sb)
+            t.subs.append(d)
+        return t
+
+    def begin_group(self, emb: torch.Tensor):
+        """The begins of the consecutive eval batches of ``emb`` [<= k x sub_batch, 1024] at once
+        (group_twin): prompt assembly, L2 norm, the mapper (one launch pair per eval batch, as a
+        batch's own begin runs it), prefill_embed, get_prefix_tokens and the prefill over every
+        row, then step 0 of each batch on its sub-decoder, persistent launches deferred
+        (sub-decoder.launch_pending).  Every kernel's per-row arithmetic is independent of the
+        rows it runs with (the tiled GEMMs accumulate k in order whatever the tile), so each
+        batch's ids equal its own begin's (tests/test_gpu_persist.py)."""
+        cfg, B, Pmax, sb = self.cfg, emb.shape[0], self.Pmax, self.sub_batch
+        assert B <= cfg.batch
+        self._B, self._emb = B, emb
+        ops.prompt_assemble(emb, self.labels, cfg.sound_effect_num, self.label_tok, self.label_len,
+                            self.hard_ids[:B], self.hard_len[:B])
+        prefix = self.prefix[:B]
+        if cfg.normalize_prefix:
+            ops.l2norm(emb, out=prefix)               # dataset.py:448-449
+        else:
+            prefix.copy_(emb)
+        soft = self.soft_buf[:B]
+        for c0 in range(0, B, sb):
+            c1 = min(B, c0 + sb)
+            soft[c0:c1].copy_(self.mapper(prefix[c0:c1]))
+        dec = self.decoder
+        ops.prefill_embed(self.hard_ids[:B], self.hard_len[:B], soft, self.mapper.soft_ld,
+                          cfg.prefix_length, self.gpt.wte, self.gpt.wpe, B, Pmax,
+                          self.embed[:B * Pmax], dec.x, dec.plen, dec.last_row)
+        if cfg.prefix_tokens:
+            self.prefix_tokens(B, soft)
+        dec.prefill(B, Pmax)
+        for j in range(-(-B // sb)):
+            d, r = self.subs[j], min(sb, B - j * sb)
+            d.greedy_begin_device(r)
+            d.defer_launch = True
+            try:
+                d.greedy_begin_host(r)
+            finally:
+                d.defer_launch = False
+
+    def sub_result(self, j: int) -> CaptionBatch:
+        """Batch j of the last begin_group's outputs (views, valid until the next begin_group)."""
+        sb, Pmax = self.sub_batch, self.Pmax
+        r0 = j * sb
+        r = min(sb, self._B - r0)
+        d = self.subs[j]
+        pid = (self.prefix_ids[r0 * Pmax:(r0 + r) * Pmax].view(r, Pmax)
+               if self.cfg.prefix_tokens else None)
+        return CaptionBatch(d.out_ids[:r], d.out_len[:r], None, self.hard_ids[r0:r0 + r],
+                            self.hard_len[r0:r0 + r], d.plen[:r], pid, self._emb[r0:r0 + r])
 
     def _alloc(self):
         cfg, dev, B = self.cfg, self.dev, self.cfg.batch
@@ -331,7 +405,7 @@ class ConcurrentRunner:
                  grids: Optional[List[int]] = None, budget: Optional[int] = None,
                  encode_ahead: int = 0, encode_first: bool = False, begin_first: bool = False,
                  extra_pipes: int = 0, enc_stream=None, cu_split: int = 0,
-                 begin_gate: int = 0):
+                 begin_gate: int = 0, begin_group: int = 0, n_batches: int = 0):
         self.cus = torch.cuda.get_device_properties(pipe.dev).multi_processor_count
         # persistent grids (greedy bf16 at <= 64 rows; beam search never launches one), one size
         # per batch from `grids` (largest first, see choose_persist_grid)
@@ -346,6 +420,15 @@ class ConcurrentRunner:
         # begin_first: the first persistent launches wait for the first `begin_gate` begins (0:
         # every begin of the first round), so those begins run beside no decode grid
         self.begin_gate = int(begin_gate)
+        # begin_group k > 0 (begin_first, greedy, MLP mapper): the begins of k consecutive eval
+        # batches run as ONE begin of k x batch clips on a group twin (CaptionPipeline.group_twin:
+        # encoder pass, prefill and get_prefix_tokens at k x the rows), each batch then decodes
+        # on a sub-decoder sharing the twin's KV cache rows; n_batches sizes the group twins
+        # warmup() prepares
+        self.begin_group = (int(begin_group) if self.begin_first and not pipe.cfg.beam
+                            and isinstance(pipe.mapper, MlpMapper) else 0)
+        self.n_batches = int(n_batches)
+        self.gpipes: List[CaptionPipeline] = []
         self.late_grid = True     # grid size chosen when the begin has finished (False: at begin)
         # one begin per pass over the pipelines: a begin costs milliseconds of host enqueue, so
         # beginning every idle pipeline in one pass delayed the first grids' launches until the
@@ -359,7 +442,7 @@ class ConcurrentRunner:
         # 5.09k vs 5.30k clips/s (same box, medians of 5): the idle time between a begin's kernels
         # beside the grids is waiting for CU resources, not host enqueue
         self.graph_begins = self.persist and os.environ.get("ZSAAC_GRAPH_BEGINS", "0") != "0"
-        if self.persist and not self.begin_first:
+        if self.persist and (not self.begin_first or self.begin_group):
             # persistent decode grids must be co-resident: at most budget // (smallest grid)
             n_inflight = max(1, min(n_inflight, self.budget // self.grids[-1]))
         self.n_inflight = n_inflight
@@ -387,7 +470,8 @@ class ConcurrentRunner:
             # more queues than the scheduler maps at once gets its queues time-sliced (a
             # stream per pipeline, 20 at 1280 clips, slowed every later multi-stream run 5-27 %:
             # profiles/r6/begin_first_ab.txt)
-            need = min(need, self.budget // self.grids[-1] + 2)
+            cap = self.budget // self.grids[-1] + 2
+            need = cap if self.begin_group else min(need, cap)
         # cu_split > 0 (persistent decode, A/B option): the chip is split by CU masks -- the
         # pipelines' begins (prompt .. step 0, and a give-up's phase launches) on cu_split CUs,
         # the decode grids on the rest (each pipeline launches its grid on a second stream of
@@ -429,6 +513,7 @@ class ConcurrentRunner:
                     p.caption_wav(wav)
                 p.decoder.capture_buckets()
             s.synchronize()
+        self._warm_groups(wav, "wav")
 
     def warmup_emb(self, emb: torch.Tensor):
         for i, p in enumerate(self.pipes):
@@ -441,6 +526,34 @@ class ConcurrentRunner:
                     p.decoder.run_to_completion()
                 p.decoder.capture_buckets()
             s.synchronize()
+        self._warm_groups(emb, "emb")
+
+    def decoders(self) -> List[Gpt2Decoder]:
+        """Every decoder this runner steps: the pipelines' and the group twins' sub-decoders."""
+        return [p.decoder for p in self.pipes] + [d for G in self.gpipes for d in G.subs]
+
+    def _warm_groups(self, x: torch.Tensor, inputs: str):
+        """begin_group: the group twins a run of n_batches needs, each run once (a full group of
+        x's rows repeated) with its sub-decoders' persistent launches, synchronously."""
+        k = self.begin_group
+        if not k or not self.n_batches:
+            return
+        need = -(-self.n_batches // k)
+        while len(self.gpipes) < need:
+            self.gpipes.append(self.pipes[0].group_twin(k))
+        sb = self.pipes[0].cfg.batch
+        xs = x.repeat((-(-k * sb // x.shape[0]),) + (1,) * (x.dim() - 1))[:k * sb].contiguous()
+        s = self.streams[0]
+        s.wait_stream(torch.cuda.current_stream(self.pipes[0].dev))
+        for G in self.gpipes:
+            with torch.cuda.stream(s):
+                G.begin_group(G.encode(xs) if inputs == "wav" else xs)
+                for d in G.subs:
+                    d.persist_grid = self.grids[-1]
+                    d.persist_exclusive = False
+                    d.launch_pending()
+                    d.run_to_completion()
+            s.synchronize()
 
     def run(self, batches: Sequence[torch.Tensor], keep=None, inputs: str = "wav") -> List[CaptionBatch]:
         """Captions every batch (waveforms [B, n] or, with inputs="emb", CLAP embeddings
@@ -449,16 +562,25 @@ class ConcurrentRunner:
         completion order is timing-dependent, so it must not issue collectives (gather after
         run() instead, in input order — see bench.py)."""
         assert inputs in ("wav", "emb")
+        self.bdec = None                 # (_run_grouped: batch -> the sub-decoder that decoded it)
         results: List[Optional[CaptionBatch]] = [None] * len(batches)
         caller = torch.cuda.current_stream(self.pipes[0].dev)
         for s in self.streams:           # inputs were produced on the caller's stream
             s.wait_stream(caller)
+        staged = self.begin_first and len(batches) > self.budget // self.grids[-1]
         ahead = None
-        if inputs == "wav" and self.enc is not None and len(batches) > len(self.pipes):
-            # (a run that fits its pipelines at once begins sooner encoding per batch: measured
-            # on a 131-clip shard, 37.5 vs 40 ms)
+        if inputs == "wav" and self.enc is not None and not (staged and self.begin_group) and (
+                (staged and os.environ.get("ZSAAC_STAGED_AHEAD", "0") != "0")
+                or (not staged and len(batches) > len(self.pipes))):
+            # (a pipelined run that fits its pipelines at once begins sooner encoding per batch:
+            # measured on a 131-clip shard, 37.5 vs 40 ms.  A staged run encodes per batch on its
+            # pipeline's stream too: with the encoder's 256-clip passes on their low-priority
+            # stream (ZSAAC_STAGED_AHEAD=1) every repetition took 2-32 s instead of 0.15 s --
+            # profiles/r6/begin_first_ab.txt, r6i)
             ahead = self._encode_ahead(batches, caller)
-        if self.begin_first and len(batches) > self.budget // self.grids[-1]:
+        if staged and self.begin_group:
+            return self._run_grouped(batches, keep, inputs, caller)
+        if staged:
             # (more batches than grids the budget holds at once; fewer take the pipelined path
             # below, whose small-run form gives each batch an exclusive grid)
             return self._run_staged(batches, keep, inputs, caller, ahead)
@@ -717,6 +839,110 @@ class ConcurrentRunner:
             caller.wait_stream(s)
         if ahead is not None:
             caller.wait_stream(self.enc_stream)
+        return results
+
+    def _run_grouped(self, batches, keep, inputs, caller):
+        """run() with begin_first and begin_group k: one begin per group of k consecutive eval
+        batches (CaptionPipeline.begin_group on a group twin: the encoder pass, prefill and
+        get_prefix_tokens at k x the rows), the groups' begins spread over the streams and all
+        enqueued first; the decode grids then launch in batch order within the budget, each on
+        a stream no grid is running on, after its group's begin -- the first ones after every
+        group's begin has finished on the GPU."""
+        n, k, S = len(batches), self.begin_group, len(self.streams)
+        groups = [list(range(g, min(n, g + k))) for g in range(0, n, k)]
+        while len(self.gpipes) < len(groups):
+            self.gpipes.append(self.pipes[0].group_twin(k))
+        results: List[Optional[CaptionBatch]] = [None] * n
+        self.decode_steps = [0] * n
+        self.assign, self.grid, self.gave_up = [], [0] * n, 0
+        gev = []
+        trace = self.trace = [] if os.environ.get("ZSAAC_RUNNER_TRACE") else None
+        t_run = t_prog = time.perf_counter()
+        for gi, bl in enumerate(groups):
+            G, s = self.gpipes[gi], self.streams[gi % S]
+            with torch.cuda.stream(s):
+                x = _rows_span([batches[b] for b in bl])
+                G.begin_group(G.encode(x) if inputs == "wav" else x)
+                ev = torch.cuda.Event()
+                ev.record(s)
+            gev.append(ev)
+            if trace is not None:
+                trace.append(("begin_group", gi, round((time.perf_counter() - t_run) * 1e3, 2)))
+        pending = [(gi, j, b) for gi, bl in enumerate(groups) for j, b in enumerate(bl)]
+        self.bdec = {b: self.gpipes[gi].subs[j] for gi, j, b in pending}
+        gate = list(gev)
+        active, slots, sbusy = {}, {}, set()
+        while pending or active:
+            progressed = False
+            while pending and len(sbusy) < S:
+                gi, j, b = pending[0]
+                used = sum(slots.values())
+                g = choose_persist_grid(used, len(pending), self.grids, self.budget)
+                if used + g > self.budget:
+                    break
+                kk = next(q for q in range(S) if q not in sbusy)
+                d, s = self.gpipes[gi].subs[j], self.streams[kk]
+                d.persist_grid = g
+                d.persist_exclusive = False
+                with torch.cuda.stream(s):
+                    s.wait_event(gev[gi])
+                    for ev in gate:          # the first launches: after every group's begin
+                        s.wait_event(ev)
+                    d.launch_pending()
+                    ev, flag = d.finished_async()
+                slots[b] = g
+                sbusy.add(kk)
+                self.grid[b] = g
+                self.assign.append((gi, b))
+                active[b] = (gi, j, 0, ev, flag, kk)
+                pending.pop(0)
+                if trace is not None:
+                    trace.append(("launch", b, round((time.perf_counter() - t_run) * 1e3, 2)))
+                progressed = True
+            if active:
+                gate = []
+            for b in list(active):
+                gi, j, c, ev, flag, kk = active[b]
+                if not ev.query():
+                    continue
+                progressed = True
+                G, s = self.gpipes[gi], self.streams[kk]
+                d = G.subs[j]
+                if int(flag[1]) < 0:          # gave up (not co-resident): finish stepwise
+                    self.gave_up += 1
+                    with torch.cuda.stream(s):
+                        d.resume_stepwise()
+                        d.step_chunk(None)
+                        ev, flag = d.finished_async()
+                    slots.pop(b, None)
+                    active[b] = (gi, j, 1, ev, flag, kk)
+                    continue
+                if int(flag[0]) or c >= d.n_chunks:
+                    d.note_persist_steps(int(flag[3]))
+                    self.decode_steps[b] = int(flag[3])
+                    with torch.cuda.stream(s):
+                        results[b] = _copy_batch(G.sub_result(j), caller)
+                        if keep is not None:
+                            keep(results[b])
+                    del active[b]
+                    slots.pop(b, None)
+                    sbusy.discard(kk)
+                else:
+                    with torch.cuda.stream(s):
+                        d.step_chunk(int(flag[2]))
+                        ev, flag = d.finished_async()
+                    active[b] = (gi, j, c + 1, ev, flag, kk)
+            if progressed:
+                t_prog = time.perf_counter()
+            else:
+                time.sleep(20e-6)
+                if time.perf_counter() - t_prog > STALL_S:
+                    raise RuntimeError(
+                        f"ConcurrentRunner (begin_group): no progress for {STALL_S} s; pending "
+                        f"{pending[:4]}.., active {[(b, a[0], a[2], a[5]) for b, a in active.items()]}, "
+                        f"grids {slots}")
+        for s in self.streams:
+            caller.wait_stream(s)
         return results
 
     def _encode_ahead(self, batches, caller):
