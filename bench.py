@@ -301,7 +301,8 @@ def run_captions(args, world, rank, device, pipe, n_local, first, counts, inflig
                                           staged=True)
     nstreams = max(1, inflight) + extra
     if bfirst:                  # (as ConcurrentRunner: the grids the budget holds + 2)
-        nstreams = budget // 48 + 2 if bgroup else min(nstreams, budget // 48 + 2)
+        pool = budget // 48 + int(os.environ.get("ZSAAC_POOL_EXTRA", "0"))
+        nstreams = pool if bgroup else min(nstreams, pool)
     runner = ConcurrentRunner(pipe, max(1, inflight),
                               streams=run_streams(device, nstreams),
                               budget=budget,
@@ -1366,10 +1367,17 @@ def main():
             args, device, pipe, t_full, CLOTHO_EVAL_CLIPS,
             full_src=res["clotho_1045"]["source"] if "clotho_1045" in res else None)
     del runner, outs
-    if rank == 0 and world == 1 and args.extras and args.group == 1 and not args.beam:
-        del pipe
+
+    def release():
+        # (runners hold reference cycles: collect them so their buffers return to the device
+        # before the next configuration allocates its own)
+        import gc
+        gc.collect()
         torch.cuda.synchronize()
         torch.cuda.empty_cache()
+    if rank == 0 and world == 1 and args.extras and args.group == 1 and not args.beam:
+        del pipe
+        release()
         log("f32 parity mode")
         # the f32 grid decode (G = 192): two grids co-resident, so 2 pipelines run (4 asked;
         # tools/f32_profile.py, profiles/r5/f32_sweep.txt)
@@ -1377,13 +1385,16 @@ def main():
                                          CLOTHO_EVAL_CLIPS, 1, reps=3)
         res["f32_parity_mode"]["note"] = ("the headline's 1045 clips at bs=64 in f32: the mode "
                                           "whose greedy ids are bit-exact")
+        release()
         log("throughput mode")
         res["throughput_mode"] = sub_run(args, device, torch.bfloat16, 128, 3, 3 * 8192, 1,
                                          encoder_batch=256)
         res["throughput_mode"]["note"] = ("128 eval batches decoded together (8192-row decode "
                                           "GEMMs), 3 in flight: NOT the metric's bs=64")
+        release()
         log("C3 beam 5")
         res["c3_beam5"] = c3_beam5(args, device)
+        release()
         log("C5 Mistral-7B")
         res["c5_mistral"] = c5_mistral(args, device)
         log("id agreement")

@@ -466,11 +466,11 @@ class ConcurrentRunner:
         need = len(self.pipes)
         if self.begin_first:
             # begin_first keeps a pipeline per batch but only as many streams as grids can run at
-            # once (+2 for the begins): every stream is a hardware queue, and a process holding
-            # more queues than the scheduler maps at once gets its queues time-sliced (a
-            # stream per pipeline, 20 at 1280 clips, slowed every later multi-stream run 5-27 %:
-            # profiles/r6/begin_first_ab.txt)
-            cap = self.budget // self.grids[-1] + 2
+            # once: every stream is a hardware queue, and a process holding more queues than the
+            # scheduler maps at once gets its queues time-sliced (a stream per pipeline, 20 at
+            # 1280 clips, slowed every later multi-stream run 5-27 %; a pool of 12 still cost C3
+            # 9 % and C5's step 2.7 -> 3.8 ms, a pool of 10 nothing: profiles/r6/begin_first_ab.txt)
+            cap = self.budget // self.grids[-1] + int(os.environ.get("ZSAAC_POOL_EXTRA", "0"))
             need = cap if self.begin_group else min(need, cap)
         # cu_split > 0 (persistent decode, A/B option): the chip is split by CU masks -- the
         # pipelines' begins (prompt .. step 0, and a give-up's phase launches) on cu_split CUs,
