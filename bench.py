@@ -1044,7 +1044,7 @@ def c5_mistral(args, device, n=2, warmup=1):
             k, v = kv.split("=")
             dec.run_cfg[k] = tuple(int(t) for t in v.split("x"))
     dec = decs[0]
-    streams = ops.dedicated_streams(3, device) if conc else None
+    streams = run_streams(device, 3) if conc else None   # (the process pool: no new HW queues)
     wav = synthetic_clips(B, 0, device)
 
     def one():

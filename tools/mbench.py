@@ -122,8 +122,9 @@ def bench_gemm_htsat():
     from zsaac import ops
     from zsaac._lib import call
     dev = torch.device("cuda", 0)
+    clips = int(os.environ.get("ZS_CLIPS", 64))
     for C, T in ((96, 4096), (192, 1024), (384, 256), (768, 64)):
-        M = 64 * T
+        M = clips * T
         shapes = [(3 * C, C, "qkv"), (C, C, "proj"), (4 * C, C, "fc1"), (C, 4 * C, "fc2")]
         if C < 768:
             shapes.append((2 * C, 4 * C, "merge"))
@@ -144,8 +145,9 @@ def bench_gemm_htsat():
             call("zs_tune_set", b"gemm_fast", 1)
             res["torch"] = timeit(lambda: torch.nn.functional.linear(a, w, b.bfloat16()), reps=20)
             gbs = (Mr * K + Mr * N + N * K) * 2 / res["auto"] / 1e3
+            tf = 2 * Mr * N * K / 1e6
             print(f"C{C:4d} M{Mr:7d} {name:6s} N{N:5d} K{K:5d} auto {gbs:5.0f} GB/s " +
-                  "  ".join(f"{k}={v:8.2f}us" for k, v in res.items()), flush=True)
+                  "  ".join(f"{k}={v:8.2f}us/{tf / v:5.0f}TF" for k, v in res.items()), flush=True)
 
 
 def bench_gemm_f32():
@@ -154,8 +156,9 @@ def bench_gemm_f32():
     from zsaac import ops
     dev = torch.device("cuda", 0)
     shapes = []
+    clips = int(os.environ.get("ZS_CLIPS", 64))
     for C, T in ((96, 4096), (192, 1024), (384, 256), (768, 64)):
-        M = 64 * T
+        M = clips * T
         shapes += [(M, 3 * C, C, f"C{C} qkv"), (M, C, C, f"C{C} proj"), (M, 4 * C, C, f"C{C} fc1"),
                    (M, C, 4 * C, f"C{C} fc2")]
         if C < 768:
@@ -198,8 +201,9 @@ def bench_gemm_f32_tiles():
     from zsaac._lib import call
     dev = torch.device("cuda", 0)
     shapes = []
+    clips = int(os.environ.get("ZS_CLIPS", 64))
     for C, T in ((96, 4096), (192, 1024), (384, 256), (768, 64)):
-        M = 64 * T
+        M = clips * T
         shapes += [(M, 3 * C, C, f"C{C} qkv", 2), (M, C, C, f"C{C} proj", 2),
                    (M, 4 * C, C, f"C{C} fc1", 2), (M, C, 4 * C, f"C{C} fc2", 2)]
         if C < 768:
