@@ -46,6 +46,13 @@ int zs_stream_create(void** stream, int priority);
  * optional split of the chip between the begins (prompt .. step 0) and the decode grids. */
 int zs_stream_create_masked(void** stream, const unsigned* cu_mask, int mask_words);
 int zs_stream_destroy(void* stream);
+/* zs_stream_spin: enqueue a one-wave kernel that holds `stream` for `us` microseconds (s_memrealtime,
+ * 100 MHz; nothing written): the caption runner releases the first wave of persistent decode grids
+ * one after another, 300 us apart, after a gate they all wait on -- released together, the
+ * dispatcher sometimes left one grid without room for all its workgroups until another grid
+ * ended (a grid ~40 ms late; profiles/r6/begin_first_ab.txt).  0 <= us <= 1e6; us == 0 enqueues
+ * nothing. */
+int zs_stream_spin(int us, void* stream);
 
 /* ------------------------------------------------------------------ audio front end
  * zs_logmel: retrieval/models/feature_extractor.py:34-38 (torchlibrosa Spectrogram +

@@ -1990,6 +1990,24 @@ extern "C" int zs_gpt2_decode_phases(int R, int Lmax, int max_steps, int stop0, 
   return 0;
 }
 
+// one wave that waits `ticks` of the 100 MHz realtime counter (zs_stream_spin)
+__global__ __launch_bounds__(64) void dg_spin_kernel(unsigned long long ticks) {
+  unsigned long long t0, t;
+  asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t0)::"memory");
+  do {
+    __builtin_amdgcn_s_sleep(32);
+    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  } while (t - t0 < ticks);
+}
+
+extern "C" int zs_stream_spin(int us, void* stream) {
+  ZS_REQUIRE(us >= 0 && us <= 1000000, "zs_stream_spin: us %d", us);
+  if (us == 0) return 0;
+  hipLaunchKernelGGL(dg_spin_kernel, dim3(1), dim3(64), 0, S(stream), (unsigned long long)us * 100ull);
+  ZS_LAUNCH_CHECK();
+  return 0;
+}
+
 extern "C" int zs_decode_persist_set_stamps(void* buf, int step, const void* ws) {
   ZS_CHECK_HIP(hipMemcpyToSymbol(HIP_SYMBOL(dg::dp_stamp_buf), &buf, sizeof(buf)));
   ZS_CHECK_HIP(hipMemcpyToSymbol(HIP_SYMBOL(dg::dp_stamp_ws), &ws, sizeof(ws)));

@@ -34,6 +34,7 @@ SIGNATURES = {
     "zs_tune_set": [C.c_char_p, I],
     "zs_stream_create": [P, I],
     "zs_stream_create_masked": [P, P, I],
+    "zs_stream_spin": [I, P],
     "zs_stream_destroy": [P],
     "zs_logmel": [P, I, I, P, P, P, P, P, P, P, P, P, P, P],
     "zs_wav2img": [P, I, I, P, P],

@@ -332,6 +332,11 @@ def label_topk(emb, labels, k, rows, idx=None):
     return rows
 
 
+def stream_spin(us: int, stream=None):
+    """Hold the (current) stream for `us` microseconds on the GPU (zs_stream_spin)."""
+    call("zs_stream_spin", int(us), (stream or torch.cuda.current_stream()).cuda_stream)
+
+
 def dedicated_streams(n: int, device, priority: int = 0) -> list:
     """n new HIP streams bound to distinct hardware queues (zs_stream_create), as torch streams.
     torch's pooled streams get their hardware queue at first use, so concurrent batch streams

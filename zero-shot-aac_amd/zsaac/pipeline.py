@@ -390,6 +390,12 @@ _SPLIT_STREAMS = {}     # (device, CUs, begin CUs) -> (begin streams, grid strea
 # a staged run that sees no event complete for this long raises (with its state) instead of
 # spinning: a persistent launch that cannot become co-resident gives up after ~2^22 polls (s)
 STALL_S = float(os.environ.get("ZSAAC_RUNNER_STALL_S", "60"))
+# the first wave of a staged run's grids, released by one gate, start STAGGER_US apart (each
+# waits k x STAGGER_US after the gate on the GPU, zs_stream_spin): released together, one grid of
+# ten sometimes found no room for all its workgroups until another ended -- a 1280-clip
+# repetition 0.16 or 0.18 s at random; staggered by 300 us every repetition took 0.162-0.164 s
+# (profiles/r6/begin_first_ab.txt, r6u)
+STAGGER_US = int(os.environ.get("ZSAAC_STAGGER_US", "300"))
 
 
 class ConcurrentRunner:
@@ -782,6 +788,8 @@ class ConcurrentRunner:
                     s.wait_event(bev.pop(bi))
                     for ev in gate:          # the first launches: after the gating begins
                         s.wait_event(ev)
+                    if gate and STAGGER_US:      # (released in turn, as _run_grouped)
+                        ops.stream_spin(STAGGER_US * len(sbusy), s)
                     p.decoder.launch_pending()
                     ev, flag = p.decoder.finished_async()
                 slots[i] = g
@@ -857,9 +865,12 @@ class ConcurrentRunner:
         self.assign, self.grid, self.gave_up = [], [0] * n, 0
         gev = []
         trace = self.trace = [] if os.environ.get("ZSAAC_RUNNER_TRACE") else None
+        if trace is not None:
+            self.traces = getattr(self, "traces", []) + [trace]
         t_run = t_prog = time.perf_counter()
+        nbs = max(1, min(S, int(os.environ.get("ZSAAC_BEGIN_STREAMS", str(S)))))
         for gi, bl in enumerate(groups):
-            G, s = self.gpipes[gi], self.streams[gi % S]
+            G, s = self.gpipes[gi], self.streams[gi % nbs]
             with torch.cuda.stream(s):
                 x = _rows_span([batches[b] for b in bl])
                 G.begin_group(G.encode(x) if inputs == "wav" else x)
@@ -888,6 +899,8 @@ class ConcurrentRunner:
                     s.wait_event(gev[gi])
                     for ev in gate:          # the first launches: after every group's begin
                         s.wait_event(ev)
+                    if gate and STAGGER_US:      # the first wave's grids released in turn
+                        ops.stream_spin(STAGGER_US * len(sbusy), s)
                     d.launch_pending()
                     ev, flag = d.finished_async()
                 slots[b] = g
@@ -920,6 +933,8 @@ class ConcurrentRunner:
                 if int(flag[0]) or c >= d.n_chunks:
                     d.note_persist_steps(int(flag[3]))
                     self.decode_steps[b] = int(flag[3])
+                    if trace is not None:
+                        trace.append(("done", b, round((time.perf_counter() - t_run) * 1e3, 2)))
                     with torch.cuda.stream(s):
                         results[b] = _copy_batch(G.sub_result(j), caller)
                         if keep is not None:
