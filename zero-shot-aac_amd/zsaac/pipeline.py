@@ -881,7 +881,8 @@ class ConcurrentRunner:
                 trace.append(("begin_group", gi, round((time.perf_counter() - t_run) * 1e3, 2)))
         pending = [(gi, j, b) for gi, bl in enumerate(groups) for j, b in enumerate(bl)]
         self.bdec = {b: self.gpipes[gi].subs[j] for gi, j, b in pending}
-        gate = list(gev)
+        ng = int(os.environ.get("ZSAAC_GROUP_GATE", "0"))   # (A/B: gate on the first ng groups)
+        gate = list(gev[:ng] if ng > 0 else gev)
         active, slots, sbusy = {}, {}, set()
         while pending or active:
             progressed = False
