@@ -399,11 +399,19 @@ STAGGER_US = int(os.environ.get("ZSAAC_STAGGER_US", "300"))
 
 
 class ConcurrentRunner:
-    """Keeps several independent bs=`cfg.batch` batches in flight on one GPU: pipeline twins
-    (shared weights, private buffers/KV cache/graphs), each on its own HIP stream.  A batch is
-    encode + mapper + prefill enqueued at once, then its decode graph chunks are enqueued one at a
-    time; the host only polls events and a pinned all-done flag (no blocking syncs), so while
-    one batch waits on a latency-bound decode kernel the others' kernels fill the chip.
+    """Keeps several independent bs=`cfg.batch` batches in flight on one GPU; the host only
+    polls events and a pinned all-done flag (no blocking syncs).  Two schedules:
+
+    * pipelined (run's main loop): pipeline twins (shared weights, private buffers / KV cache /
+      graphs), each on its own HIP stream; a batch's begin (encode .. step 0) is enqueued when a
+      pipeline frees, its persistent decode grid when the begin has finished -- begins and grids
+      share the chip.  Also the path of a run with no more batches than grids fit at once.
+    * staged (begin_first, the bench's headline schedule; _run_grouped with begin_group, else
+      _run_staged): every begin runs first -- with begin_group k, one begin per k consecutive
+      batches on a group twin, each batch decoding on a sub-decoder that shares the twin's KV
+      cache rows -- and the decode grids launch once every begin has finished, in batch order as
+      the budget frees, on a pool of budget / 48 streams, the first wave released STAGGER_US
+      apart.  Ids are the same under either schedule (tests/test_gpu_persist.py).
 
     Results are copied out on the pipeline's stream before it takes the next batch."""
 
