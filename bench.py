@@ -301,7 +301,7 @@ def run_captions(args, world, rank, device, pipe, n_local, first, counts, inflig
                                           staged=True)
     nstreams = max(1, inflight) + extra
     if bfirst:                  # (as ConcurrentRunner: the grids the budget holds + 2)
-        pool = budget // 48 + int(os.environ.get("ZSAAC_POOL_EXTRA", "0"))
+        pool = budget // 48
         nstreams = pool if bgroup else min(nstreams, pool)
     runner = ConcurrentRunner(pipe, max(1, inflight),
                               streams=run_streams(device, nstreams),

@@ -484,7 +484,7 @@ class ConcurrentRunner:
             # scheduler maps at once gets its queues time-sliced (a stream per pipeline, 20 at
             # 1280 clips, slowed every later multi-stream run 5-27 %; a pool of 12 still cost C3
             # 9 % and C5's step 2.7 -> 3.8 ms, a pool of 10 nothing: profiles/r6/begin_first_ab.txt)
-            cap = self.budget // self.grids[-1] + int(os.environ.get("ZSAAC_POOL_EXTRA", "0"))
+            cap = self.budget // self.grids[-1]
             need = cap if self.begin_group else min(need, cap)
         # cu_split > 0 (persistent decode, A/B option): the chip is split by CU masks -- the
         # pipelines' begins (prompt .. step 0, and a give-up's phase launches) on cu_split CUs,
@@ -583,14 +583,11 @@ class ConcurrentRunner:
             s.wait_stream(caller)
         staged = self.begin_first and len(batches) > self.budget // self.grids[-1]
         ahead = None
-        if inputs == "wav" and self.enc is not None and not (staged and self.begin_group) and (
-                (staged and os.environ.get("ZSAAC_STAGED_AHEAD", "0") != "0")
-                or (not staged and len(batches) > len(self.pipes))):
+        if inputs == "wav" and self.enc is not None and not staged and len(batches) > len(self.pipes):
             # (a pipelined run that fits its pipelines at once begins sooner encoding per batch:
-            # measured on a 131-clip shard, 37.5 vs 40 ms.  A staged run encodes per batch on its
-            # pipeline's stream too: with the encoder's 256-clip passes on their low-priority
-            # stream (ZSAAC_STAGED_AHEAD=1) every repetition took 2-32 s instead of 0.15 s --
-            # profiles/r6/begin_first_ab.txt, r6i)
+            # measured on a 131-clip shard, 37.5 vs 40 ms.  A staged run encodes on its begins'
+            # streams: with the encoder's passes on their low-priority stream every repetition
+            # took 2-32 s instead of 0.15 s -- profiles/r6/begin_first_ab.txt, r6i)
             ahead = self._encode_ahead(batches, caller)
         if staged and self.begin_group:
             return self._run_grouped(batches, keep, inputs, caller)
@@ -876,9 +873,8 @@ class ConcurrentRunner:
         if trace is not None:
             self.traces = getattr(self, "traces", []) + [trace]
         t_run = t_prog = time.perf_counter()
-        nbs = max(1, min(S, int(os.environ.get("ZSAAC_BEGIN_STREAMS", str(S)))))
-        for gi, bl in enumerate(groups):
-            G, s = self.gpipes[gi], self.streams[gi % nbs]
+        for gi, bl in enumerate(groups):      # (on one stream: 5.3k instead of 7.3k clips/s)
+            G, s = self.gpipes[gi], self.streams[gi % S]
             with torch.cuda.stream(s):
                 x = _rows_span([batches[b] for b in bl])
                 G.begin_group(G.encode(x) if inputs == "wav" else x)
@@ -889,8 +885,7 @@ class ConcurrentRunner:
                 trace.append(("begin_group", gi, round((time.perf_counter() - t_run) * 1e3, 2)))
         pending = [(gi, j, b) for gi, bl in enumerate(groups) for j, b in enumerate(bl)]
         self.bdec = {b: self.gpipes[gi].subs[j] for gi, j, b in pending}
-        ng = int(os.environ.get("ZSAAC_GROUP_GATE", "0"))   # (A/B: gate on the first ng groups)
-        gate = list(gev[:ng] if ng > 0 else gev)
+        gate = list(gev)    # (gating on fewer groups brought the late grid back: r6w)
         active, slots, sbusy = {}, {}, set()
         while pending or active:
             progressed = False
