@@ -264,6 +264,36 @@ def test_concurrent_headline_schedule_ids_equal_single_stream(cuda, staged):
     assert runner.gave_up == 0
 
 
+def test_begin_groups_ragged_batches(cuda):
+    """Begin groups over eval batches of uneven sizes (44 / 64 / 30 / 64 clips, 12 batches: the
+    staged, grouped path): each batch's sub-decoder decodes exactly that batch's clips -- ids and
+    prompt lengths equal a single-stream run of the same batches."""
+    from tools import idparity
+    from zsaac.pipeline import ConcurrentRunner, persist_budget
+    g = idparity.load("c2_gpt2init")
+    base = torch.from_numpy(g["clap_emb"]).to(cuda)
+    sizes = [44, 64, 30, 64] * 3
+    n = sum(sizes)
+    i = torch.arange(n, device=cuda, dtype=torch.float32)[:, None]
+    emb = base[torch.arange(n, device=cuda) % base.shape[0]] * (1.0 + 0.03 * torch.cos(0.29 * i))
+    offs = [sum(sizes[:k]) for k in range(len(sizes))]
+    batches = [emb[o:o + z] for o, z in zip(offs, sizes)]
+    p = _pipe(g, cuda, True, batch=64)
+    p.decoder.persist_grid = 48
+    single = [(p.caption_emb(b).captions(), p.result().plen.tolist()) for b in batches]
+    cus = torch.cuda.get_device_properties(cuda).multi_processor_count
+    runner = ConcurrentRunner(p, 10, begin_first=True, budget=persist_budget(cus, staged=True),
+                              begin_group=4, n_batches=len(batches))
+    runner.warmup_emb(batches[1])
+    outs = runner.run(batches, inputs="emb")
+    assert runner.bdec is not None, "the grouped path did not run"
+    for k, o in enumerate(outs):
+        assert o.ids.shape[0] == sizes[k]
+        assert o.captions() == single[k][0], f"batch {k} ({sizes[k]} clips): ids differ"
+        assert o.plen.tolist() == single[k][1]
+    assert runner.gave_up == 0
+
+
 def test_prompts_beside_grids_deterministic(cuda):
     """The sound-effect prompt (prompt_kernel, gpt2.hip) computed on ten streams while ten
     persistent decode grids run on ten others equals the prompt computed alone, for all 1045

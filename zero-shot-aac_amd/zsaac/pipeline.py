@@ -146,8 +146,10 @@ class CaptionPipeline:
             t.subs.append(d)
         return t
 
-    def begin_group(self, emb: torch.Tensor):
+    def begin_group(self, emb: torch.Tensor, sizes: Optional[Sequence[int]] = None):
         """The begins of the consecutive eval batches of ``emb`` [<= k x sub_batch, 1024] at once
+        (``sizes``: the batches' clip counts, each <= sub_batch; default: sub_batch each, the last
+        ragged)
         (group_twin): prompt assembly, L2 norm, the mapper (one launch pair per eval batch, as a
         batch's own begin runs it), prefill_embed, get_prefix_tokens and the prefill over every
         row, then step 0 of each batch on its sub-decoder, persistent launches deferred
@@ -156,7 +158,12 @@ class CaptionPipeline:
         batch's ids equal its own begin's (tests/test_gpu_persist.py)."""
         cfg, B, Pmax, sb = self.cfg, emb.shape[0], self.Pmax, self.sub_batch
         assert B <= cfg.batch
-        self._B, self._emb = B, emb
+        if sizes is None:
+            sizes = [min(sb, B - r) for r in range(0, B, sb)]
+        sizes = [int(z) for z in sizes]
+        assert sum(sizes) == B and len(sizes) <= len(self.subs) and all(0 < z <= sb for z in sizes)
+        self._B, self._emb, self._sizes = B, emb, sizes
+        self._offs = [sum(sizes[:j]) for j in range(len(sizes))]
         ops.prompt_assemble(emb, self.labels, cfg.sound_effect_num, self.label_tok, self.label_len,
                             self.hard_ids[:B], self.hard_len[:B])
         prefix = self.prefix[:B]
@@ -165,9 +172,8 @@ class CaptionPipeline:
         else:
             prefix.copy_(emb)
         soft = self.soft_buf[:B]
-        for c0 in range(0, B, sb):
-            c1 = min(B, c0 + sb)
-            soft[c0:c1].copy_(self.mapper(prefix[c0:c1]))
+        for c0, z in zip(self._offs, sizes):      # the mapper per eval batch, as its own begin
+            soft[c0:c0 + z].copy_(self.mapper(prefix[c0:c0 + z]))
         dec = self.decoder
         ops.prefill_embed(self.hard_ids[:B], self.hard_len[:B], soft, self.mapper.soft_ld,
                           cfg.prefix_length, self.gpt.wte, self.gpt.wpe, B, Pmax,
@@ -175,8 +181,10 @@ class CaptionPipeline:
         if cfg.prefix_tokens:
             self.prefix_tokens(B, soft)
         dec.prefill(B, Pmax)
-        for j in range(-(-B // sb)):
-            d, r = self.subs[j], min(sb, B - j * sb)
+        for j, (r0, r) in enumerate(zip(self._offs, sizes)):
+            d = self.subs[j]
+            if d.kc[0].data_ptr() != dec.kc[0][r0:].data_ptr():
+                d.share_rows(dec, r0)           # (batch j's rows start at r0 this time)
             d.greedy_begin_device(r)
             d.defer_launch = True
             try:
@@ -186,9 +194,8 @@ class CaptionPipeline:
 
     def sub_result(self, j: int) -> CaptionBatch:
         """Batch j of the last begin_group's outputs (views, valid until the next begin_group)."""
-        sb, Pmax = self.sub_batch, self.Pmax
-        r0 = j * sb
-        r = min(sb, self._B - r0)
+        Pmax = self.Pmax
+        r0, r = self._offs[j], self._sizes[j]
         d = self.subs[j]
         pid = (self.prefix_ids[r0 * Pmax:(r0 + r) * Pmax].view(r, Pmax)
                if self.cfg.prefix_tokens else None)
@@ -862,6 +869,7 @@ class ConcurrentRunner:
         a stream no grid is running on, after its group's begin -- the first ones after every
         group's begin has finished on the GPU."""
         n, k, S = len(batches), self.begin_group, len(self.streams)
+        budget = self.budget
         groups = [list(range(g, min(n, g + k))) for g in range(0, n, k)]
         while len(self.gpipes) < len(groups):
             self.gpipes.append(self.pipes[0].group_twin(k))
@@ -877,7 +885,8 @@ class ConcurrentRunner:
             G, s = self.gpipes[gi], self.streams[gi % S]
             with torch.cuda.stream(s):
                 x = _rows_span([batches[b] for b in bl])
-                G.begin_group(G.encode(x) if inputs == "wav" else x)
+                G.begin_group(G.encode(x) if inputs == "wav" else x,
+                              [int(batches[b].shape[0]) for b in bl])
                 ev = torch.cuda.Event()
                 ev.record(s)
             gev.append(ev)
@@ -892,8 +901,8 @@ class ConcurrentRunner:
             while pending and len(sbusy) < S:
                 gi, j, b = pending[0]
                 used = sum(slots.values())
-                g = choose_persist_grid(used, len(pending), self.grids, self.budget)
-                if used + g > self.budget:
+                g = choose_persist_grid(used, len(pending), self.grids, budget)
+                if used + g > budget:
                     break
                 kk = next(q for q in range(S) if q not in sbusy)
                 d, s = self.gpipes[gi].subs[j], self.streams[kk]
