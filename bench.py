@@ -145,9 +145,11 @@ def parse(argv=None):
                          "enqueued first; the first grid launches wait for --begin-gate begins "
                          "(0: all of them); 0: round 5's pipelined schedule (begins beside grids)")
     ap.add_argument("--begin-gate", type=int, default=0)
-    ap.add_argument("--begin-group", type=int, default=4,
+    ap.add_argument("--begin-group", type=int, default=2,
                     help="with --begin-first: eval batches per begin (one encoder pass, prefill "
-                         "and get_prefix_tokens for all of them; 0 = a begin per batch)")
+                         "and get_prefix_tokens for all of them; 0 = a begin per batch; 2 / 3 / 4 "
+                         "/ 5 measured 7.93k / 7.98k / 7.83k / 7.95k clips/s at 1280 clips and "
+                         "7.31k / 7.20k / 7.25k at 1045, profiles/r6/begin_first_ab.txt r6dd)")
     ap.add_argument("--persist-budget", type=int, default=0,
                     help="workgroup slots (half a CU each) the in-flight persistent decode grids "
                          "may hold together (0: ZSAAC_PERSIST_BUDGET or 1.5 per CU)")
@@ -293,7 +295,7 @@ def run_captions(args, world, rank, device, pipe, n_local, first, counts, inflig
     bfirst = (bool(getattr(args, "begin_first", 0)) and pipe.decoder.persist and not pipe.cfg.beam
               and pipe.cfg.batch <= 64 and not getattr(pipe.decoder, "f32_grid", False))
     budget = getattr(args, "persist_budget", 0) or None
-    bgroup = int(getattr(args, "begin_group", 4)) if bfirst and args.mapper == "mlp" else 0
+    bgroup = int(getattr(args, "begin_group", 2)) if bfirst and args.mapper == "mlp" else 0
     if bfirst:
         if not bgroup:          # a pipeline per batch: every begin runs before the grids
             inflight = max(inflight, len(batches))
