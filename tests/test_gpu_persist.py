@@ -216,7 +216,7 @@ def test_concurrent_runner_mixed_grids(cuda):
     assert runner.gave_up == 0
 
 
-@pytest.mark.parametrize("staged", [0, 1, 4], ids=["pipelined", "begin_first", "begin_group4"])
+@pytest.mark.parametrize("staged", [0, 1, 2, 4], ids=["pipelined", "begin_first", "begin_group2", "begin_group4"])
 def test_concurrent_headline_schedule_ids_equal_single_stream(cuda, staged):
     """The headline's schedule at the headline's size on the bench's own weights (c2_gpt2init,
     GPT-2's init scale, small margins): 1045 embeddings in 17 eval batches of <= 64 (the last 21)
