@@ -48,7 +48,7 @@ int zs_stream_create_masked(void** stream, const unsigned* cu_mask, int mask_wor
 int zs_stream_destroy(void* stream);
 /* zs_stream_spin: enqueue a one-wave kernel that holds `stream` for `us` microseconds (s_memrealtime,
  * 100 MHz; nothing written): the caption runner releases the first wave of persistent decode grids
- * one after another, 300 us apart, after a gate they all wait on -- released together, the
+ * one after another, 200 us apart, after a gate they all wait on -- released together, the
  * dispatcher sometimes left one grid without room for all its workgroups until another grid
  * ended (a grid ~40 ms late; profiles/r6/begin_first_ab.txt).  0 <= us <= 1e6; us == 0 enqueues
  * nothing. */

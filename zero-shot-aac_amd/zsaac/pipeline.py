@@ -401,8 +401,9 @@ STALL_S = float(os.environ.get("ZSAAC_RUNNER_STALL_S", "60"))
 # waits k x STAGGER_US after the gate on the GPU, zs_stream_spin): released together, one grid of
 # ten sometimes found no room for all its workgroups until another ended -- a 1280-clip
 # repetition 0.16 or 0.18 s at random; staggered by 300 us every repetition took 0.162-0.164 s
-# (profiles/r6/begin_first_ab.txt, r6u)
-STAGGER_US = int(os.environ.get("ZSAAC_STAGGER_US", "300"))
+# (profiles/r6/begin_first_ab.txt, r6u; 100 us: 2 late grids in 8 repetitions; with begin groups
+# of 2, 150 / 200 / 300 us: none in 8 each, 8.01k / 7.99k / 7.97k clips/s, r6ee)
+STAGGER_US = int(os.environ.get("ZSAAC_STAGGER_US", "200"))
 
 
 class ConcurrentRunner:
